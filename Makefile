@@ -1,0 +1,38 @@
+# Build libs2c.so (HIP kernels for gfx950 + host parser/planner/generator) in-tree.
+# Used by __graft_entry__.build(); also `make -j8` by hand.
+HIPCC   ?= /opt/rocm/bin/hipcc
+CXX     ?= g++
+ARCH    ?= gfx950
+SRC      = sam2consensus_amd/csrc
+OUT      = sam2consensus_amd/libs2c.so
+BUILD    = build
+CXXFLAGS = -O3 -std=c++17 -fPIC -Wall -Wextra -Iinclude
+HIPFLAGS = -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -Iinclude \
+           -Wno-unused-result
+
+all: $(OUT)
+
+$(BUILD)/s2c_host.o: $(SRC)/s2c_host.cpp include/s2c.h | $(BUILD)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(BUILD)/s2c_synth.o: $(SRC)/s2c_synth.cpp include/s2c.h | $(BUILD)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(BUILD)/s2c_kernels.o: $(SRC)/s2c_kernels.hip include/s2c.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OUT): $(BUILD)/s2c_host.o $(BUILD)/s2c_synth.o $(BUILD)/s2c_kernels.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ -lz -o $@
+
+$(BUILD):
+	mkdir -p $(BUILD)
+
+# kernel resource usage (VGPR/SGPR/LDS/occupancy) and ISA for inspection
+isa: | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $(SRC)/s2c_kernels.hip -o $(BUILD)/isa.o -save-temps=obj \
+	    -Rpass-analysis=kernel-resource-usage 2> $(BUILD)/resource_usage.txt
+
+clean:
+	rm -rf $(BUILD) $(OUT)
+
+.PHONY: all clean isa

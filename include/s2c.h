@@ -1,0 +1,219 @@
+/*
+ * s2c.h — C-ABI of libs2c.so, the MI355X (gfx950) pileup-and-vote engine behind
+ * the sam2consensus.py drop-in CLI.
+ *
+ * The reference (zoujiayun/sam2consensus v2.1) is ONE Python-2 script; its hot path
+ * is inline in main().  Each entry point below names the reference region it
+ * replaces (sam2consensus.py:LINE).  A Python host binds these with ctypes
+ * (sam2consensus_amd/_lib.py); INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - every function returns int: S2C_OK (0) or a negative S2C_ERR_* code;
+ *     s2c_last_error() gives the message (thread-local).
+ *   - error codes S2C_ERR_KEY..S2C_ERR_OVERFLOW are the Python exception classes the
+ *     reference dies with on the same input (SURVEY.md §5 "Failure detection");
+ *     the host raises that class, exits non-zero and writes no FASTA.
+ *   - no torch / HIP C++ types in signatures: device buffers are plain pointers
+ *     owned by the caller (torch tensors in the Python host); the stream is a
+ *     hipStream_t passed as void*.
+ */
+#ifndef S2C_H
+#define S2C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define S2C_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------------------- */
+#define S2C_OK            0
+#define S2C_ERR_KEY      -1   /* KeyError:   unknown RNAME (:212,:221), base not in -ACGNT (:212,:287), vote key (:367,:381) */
+#define S2C_ERR_INDEX    -2   /* IndexError: <6 / <10 fields (:195,:206), empty RNAME (:200), pos out of range (:212), insertion key (:294) */
+#define S2C_ERR_VALUE    -3   /* ValueError: non-int POS (:201) or LN (:164); int(nan*100) (:394) */
+#define S2C_ERR_ZERODIV  -4   /* ZeroDivisionError: zero-length record (:395, e.g. -f "") */
+#define S2C_ERR_OVERFLOW -5   /* OverflowError: int(inf*100) (:394) */
+#define S2C_ERR_IO      -10   /* file / gzip I/O */
+#define S2C_ERR_HIP     -11   /* HIP runtime failure */
+#define S2C_ERR_ARG     -12   /* bad argument / shape check failed before a launch */
+#define S2C_ERR_LIMIT   -13   /* input beyond this build's limits (e.g. > 2^32 positions) */
+
+const char *s2c_last_error(void);
+int s2c_abi_version(void);
+/* ABI self-check for FFI mirrors: fills out[0..n) with sizeof/offsetof values of the
+ * structs below (order documented in sam2consensus_amd/_lib.py); returns the count. */
+int s2c_layout(int64_t *out, int n);
+
+/* ---- constants shared with the kernels -------------------------------------------- */
+#define S2C_NSYM          6    /* symbols '-','A','C','G','N','T' — sorted() order (:367) */
+#define S2C_POS_ALIGN    64    /* each reference starts at a multiple of this global coordinate */
+#define S2C_VOTE_BLOCK 1024    /* positions per consensus/assembly block (never straddles a ref) */
+#define S2C_ITEM_WORDS    8    /* u32 words per pileup work item */
+#define S2C_BLOCK_WORDS   4    /* u32 words per consensus block */
+#define S2C_CODE_FILL     0    /* codes[] value for a fill position */
+#define S2C_CODE_ERR   0xFF    /* codes[] value where the vote hit a missing amb key (:367) */
+
+/* ======================================================================================
+ * Host side: SAM/SAM.gz parser → packed read batch          (replaces :147-228, :256-294)
+ * ======================================================================================
+ * The parser reproduces the reference's record handling exactly (header pass :149-172,
+ * record filter :195, RNAME/POS :200-201, parsecigar :46-82, maxdel rule :210, error
+ * classes in file order) and emits the packed batch of north_star subsystem (1):
+ * reads bucket-sorted by global start, effective CIGAR op words, 4-bit bases,
+ * insertion events, and the pileup / consensus work plan.
+ */
+typedef struct s2c_parser s2c_parser;
+typedef struct s2c_batch  s2c_batch;
+
+/* maxdel_active = 0 reproduces Python 2's `int <= str` when -d is given (:102,:210). */
+int  s2c_parser_new(int maxdel_active, int64_t maxdel, s2c_parser **out);
+/* Feed raw SAM text (any chunking; lines may straddle calls). */
+int  s2c_parser_feed(s2c_parser *p, const char *buf, size_t len);
+/* Parse a whole file; ".gz" suffix → zlib (:111-114). */
+int  s2c_parser_feed_file(s2c_parser *p, const char *path);
+/* End of input: reformat-phase checks (:284-294), global layout and work plan. */
+int  s2c_parser_finish(s2c_parser *p, s2c_batch **out);
+void s2c_parser_free(s2c_parser *p);
+
+typedef struct {
+    int64_t n_refs;            /* @SQ references (:160-169) */
+    int64_t total_len;         /* Σ LN over refs (real positions) */
+    int64_t padded_len;        /* global coordinate extent (refs aligned to S2C_POS_ALIGN) */
+    int64_t header_lines;      /* :158 */
+    int64_t lines_total;       /* all lines seen (:194 counts from -header_lines) */
+    int64_t reads_mapped;      /* records passing :195 */
+    int64_t aligned_bases;     /* A = Σ len(seqout) over mapped reads (the metric's unit) */
+    int64_t query_bases;       /* Q = M/=/X + I bases packed (B_alg 0.5·Q) */
+    int64_t n_reads;           /* pileup read records (after wrap splitting) */
+    int64_t n_long;            /* of which "long" reads handled through per-tile extras */
+    int64_t n_ops;             /* effective op words (B_alg 4·K) */
+    int64_t n_base_words;      /* u32 words of packed bases */
+    int64_t n_ins;             /* insertion events kept (key in [0, LN), non-empty motif) */
+    int64_t n_ins_bases;       /* Σ motif lengths */
+    int64_t n_ins_words;       /* u32 words of packed motif bases */
+    int64_t n_items;           /* pileup work items */
+    int64_t n_extras;          /* extra (long-read) references over all items */
+    int64_t n_blocks;          /* consensus blocks */
+    int64_t tile_max;          /* max positions of any pileup tile (LDS sizing) */
+} s2c_batch_info;
+
+typedef struct {               /* host pointers into the batch (valid until s2c_batch_free) */
+    const int64_t  *ref_len;   /* [n_refs] */
+    const int64_t  *ref_off;   /* [n_refs] global coordinate of position 0 */
+    const int64_t  *ref_cov_reads; /* [n_refs] pileup records per ref (0 ⇒ Σcov may be 0) */
+    const uint32_t *rd_pos;    /* [n_reads]   global coordinate of seqout char 0 */
+    const uint32_t *rd_op;     /* [n_reads+1] op offset; bit31 of entry i = drop dashes (:210) */
+    const uint32_t *rd_base;   /* [n_reads]   word offset of the read's 4-bit bases */
+    const uint32_t *ops;       /* [n_ops]     (len << 1) | cls, cls 0 = M/=/X, 1 = D/N/P */
+    const uint32_t *bases;     /* [n_base_words] 8 codes per word, low nibble first */
+    const uint32_t *ins_key;   /* [n_ins]     global coordinate of the insertion key (:74) */
+    const uint32_t *ins_off;   /* [n_ins+1]   nibble offset of each motif in ins_bases */
+    const uint32_t *ins_bases; /* [n_ins_words] */
+    const uint32_t *items;     /* [n_items][S2C_ITEM_WORDS] pileup work items */
+    const uint32_t *extras;    /* [n_extras] read indices */
+    const uint32_t *blocks;    /* [n_blocks][S2C_BLOCK_WORDS] {g_begin, g_end, ref, first_block_of_ref} */
+} s2c_batch_arrays;
+
+int  s2c_batch_info_get(const s2c_batch *b, s2c_batch_info *out);
+int  s2c_batch_arrays_get(const s2c_batch *b, s2c_batch_arrays *out);
+/* Reference name i (NUL-terminated, owned by the batch). */
+const char *s2c_batch_ref_name(const s2c_batch *b, int64_t i);
+void s2c_batch_free(s2c_batch *b);
+
+/* parsecigar(cigarstring, seq, pos_ref) (:46-82) for one read, same semantics.
+ * seqout: caller buffer of capacity cap (gets NUL); *seqout_len = chars written.
+ * Insertions: up to max_ins (ref_pos, seq offset, len) triples into ins[3*k]. */
+int  s2c_parsecigar(const char *cigar, size_t cigar_len, const char *seq, size_t seq_len,
+                    int64_t pos_ref, char *seqout, size_t cap, size_t *seqout_len,
+                    int64_t *ins, size_t max_ins, size_t *n_ins);
+
+/* ======================================================================================
+ * Synthetic workloads (BASELINE.json configs C1..C5) — deterministic (splitmix64)
+ * ====================================================================================== */
+typedef struct {
+    int32_t  n_refs;
+    int64_t  ref_len;
+    double   depth;            /* reads per ref = floor(depth·ref_len / read_len) */
+    int32_t  read_len;
+    double   ins_frac;         /* fraction of reads with one I of 1..ins_max bases */
+    int32_t  ins_max;
+    double   del_frac;         /* fraction of reads with one D of 1..del_max bases */
+    int32_t  del_max;
+    double   long_del_frac;    /* of the D reads, fraction with a D of read_len+1 .. 2·read_len */
+    double   sub_rate;         /* substitution rate */
+    double   n_rate;           /* N-call rate */
+    int32_t  amplicons;        /* >0: starts drawn from this many tiled amplicon starts */
+    int32_t  shuffle;          /* 1: record order shuffled (else coordinate-sorted) */
+    uint64_t seed;
+    const char *ref_prefix;    /* reference names ref_prefix + index (NULL → "gene") */
+} s2c_synth_spec;
+
+/* Stream the SAM text of `spec` into parser p (no file), or write it to `path`
+ * (gzip if it ends with ".gz").  *n_reads_out gets the record count. */
+int s2c_synth_feed(const s2c_synth_spec *spec, s2c_parser *p, int64_t *n_reads_out);
+int s2c_synth_write(const s2c_synth_spec *spec, const char *path, int64_t *n_reads_out);
+
+/* ======================================================================================
+ * Device side (HIP, gfx950).  All pointers are device pointers; stream = hipStream_t.
+ * ====================================================================================== */
+typedef struct {
+    /* ---- packed batch (device copies of s2c_batch_arrays) ---- */
+    const uint32_t *rd_pos, *rd_op, *rd_base, *ops, *bases;
+    const uint32_t *items, *extras, *blocks;
+    const uint32_t *ins_key, *ins_off, *ins_bases;
+    int64_t n_reads, n_items, n_blocks, n_ins, n_ins_bases, padded_len;
+    int32_t tile_max, n_refs;
+
+    /* ---- options (:117-138) ---- */
+    const double *thresholds;  /* [T] device copy of -c values, CLI order */
+    int32_t  n_thr;
+    int32_t  min_depth;        /* -m */
+    int32_t  fill_len;         /* len(-f) */
+    int32_t  fill_nondash;     /* count of chars != '-' in -f */
+    const uint8_t *fill;       /* [fill_len] device copy of -f bytes */
+
+    /* ---- workspace (caller allocates; sizes from s2c_workspace_sizes) ---- */
+    uint32_t *counts;          /* [6][padded_len] pileup counts (SoA by symbol) */
+    uint32_t *ins_table;       /* [ins_cap][4] {key, maxlen, colbase, pad}; ins_cap pow2 */
+    int64_t   ins_cap;
+    uint32_t *ins_cols;        /* [n_ins_bases][6] insertion column counts */
+    uint32_t *ins_cnt;         /* [T][ins_cap] emitted insertion chars per key */
+    uint8_t  *ins_chr;         /* [T][n_ins_bases] emitted insertion chars, column order */
+    uint32_t *ins_bits;        /* [padded_len/32] positions that carry an insertion key */
+    uint32_t *scalars;         /* [16] col allocator, error flags */
+    uint8_t  *codes;           /* [T][padded_len] per-position consensus char (0 = fill) */
+    uint64_t *blk_len;         /* [T*n_blocks + 1] output bytes per block → exclusive scan */
+
+    /* ---- outputs ---- */
+    uint64_t *stats;           /* [n_refs][T][4] {sumcov, len, nondash, vote_errors} (:352-397) */
+    uint8_t  *out;             /* assembled consensus bytes, [t][block] order; size = blk_len[T*n_blocks] */
+    int64_t   out_cap;
+} s2c_dev;
+
+/* Sizes (bytes) of every workspace / output buffer for a batch and T thresholds. */
+typedef struct {
+    int64_t counts, ins_table, ins_cap, ins_cols, ins_cnt, ins_chr, ins_bits, scalars,
+            codes, blk_len, stats;
+} s2c_ws_sizes;
+int s2c_workspace_sizes(const s2c_batch_info *info, int32_t n_thr, s2c_ws_sizes *out);
+
+/* (2) CIGAR expansion + pileup: items → counts[6][L]                    (:206-218) */
+int s2c_pileup(const s2c_dev *d, void *stream);
+/* (3) insertion hash table, column counts and insertion vote            (:221,:256-311,:370-385) */
+int s2c_insertions(const s2c_dev *d, void *stream);
+/* (4) per-position threshold vote, min-depth/fill, IUPAC, per-(ref,t) stats (:232-253,:344-397) */
+int s2c_consensus(const s2c_dev *d, void *stream);
+/* device FASTA body assembly: block scan + byte scatter               (:350-389 string build) */
+int s2c_assemble(const s2c_dev *d, void *stream);
+/* all four, in order, on one stream (graph-capturable: no allocation, no sync) */
+int s2c_run(const s2c_dev *d, void *stream);
+/* error flags raised by the device vote (S2C_OK or S2C_ERR_KEY); call after stream sync */
+int s2c_device_error(const s2c_dev *d, void *stream, int *err_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* S2C_H */

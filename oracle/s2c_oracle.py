@@ -23,6 +23,7 @@ import re
 
 CODES = "-ACGNT"                      # sorted() order of the 6 symbols (:167, :367)
 CODE = {c: i for i, c in enumerate(CODES)}
+_VALID = frozenset(CODES)
 
 # ------------------------------------------------------------------ IUPAC LUT
 _IUPAC = {"A": "A", "C": "C", "G": "G", "T": "T", "AC": "M", "AG": "R", "AT": "W",
@@ -246,6 +247,12 @@ def pileup(lines, refs, opt):
         cref = counts[rname]
         L = len(cref)
         drop = opt.maxdel_active and seqout.count("-") > opt.maxdel   # :210
+        if not drop and 0 <= pos and pos + len(seqout) <= L and _VALID.issuperset(seqout):
+            for ch in seqout:                                # :211-213, nothing can raise
+                cref[pos][CODE[ch]] += 1
+                pos += 1
+            inserts[rname] += ins
+            continue
         for ch in seqout:                                    # :211-218
             if not (drop and ch == "-"):
                 if not (-L <= pos < L):

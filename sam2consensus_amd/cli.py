@@ -1,0 +1,153 @@
+"""Drop-in ``sam2consensus.py`` command line (reference sam2consensus.py:86-430).
+
+Same flags, same outputs (``outfolder/REF__PREFIX.fasta``), same stdout text and the
+same failure behaviour: the reference's exception class propagates (traceback, exit
+status 1) and no FASTA file is written.  The pileup-and-vote work runs on the GPU
+through libs2c.so; host SAM parsing runs in libs2c.so's C++ parser.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+__version__ = "2.1"
+DESCRIPTION = """
++------------------------------------------------------------------+
+| sam2consensus.py: extract the consensus sequence from a SAM file |
++------------------------------------------------------------------+
+
+Consensus sequences (Geneious threshold rule, IUPAC ambiguity codes) from reads mapped
+to one or more references (.sam or .sam.gz), one FASTA file per reference with one
+record per consensus threshold.  MI355X implementation: pileup, insertion and vote run
+as HIP kernels (libs2c.so); output is byte-identical to sam2consensus.py v2.1.
+"""
+
+
+def build_parser():
+    p = argparse.ArgumentParser(description=DESCRIPTION, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("-i", "--input", action="store", dest="filename", required=True,
+                   help="Name of the SAM file, SAM does not need to be sorted and can be compressed with gzip")
+    p.add_argument("-c", "--consensus-thresholds", action="store", dest="thresholds", type=str, default="0.25",
+                   help="List of consensus thresold(s) separated by commas, no spaces, example: -c 0.25,0.75,0.50, default=0.25")
+    p.add_argument("-n", action="store", dest="n", type=int, default=0,
+                   help="Split FASTA output sequences every n nucleotides, default=do not split sequence")
+    p.add_argument("-o", "--outfolder", action="store", dest="outfolder", default="./",
+                   help="Name of output folder, default=same folder as input")
+    p.add_argument("-p", "--prefix", action="store", dest="prefix", default="",
+                   help="Prefix for output file name, default=input filename without .sam extension")
+    p.add_argument("-m", "--min-depth", action="store", dest="min_depth", type=int, default=1,
+                   help="Minimum read depth at each site to report the nucleotide in the consensus, default=1")
+    p.add_argument("-f", "--fill", action="store", dest="fill", default="-",
+                   help="Character for padding regions not covered in the reference, default= - (gap)")
+    # no type= on purpose (:102): a given -d stays a string, which Python 2 compares
+    # as greater than every int, so the maxdel filter (:210) is then never applied.
+    p.add_argument("-d", "--maxdel", action="store", dest="maxdel", default=150,
+                   help="Ignore deletions longer than this value, default=150")
+    return p
+
+
+class RunResult:
+    def __init__(self, files, timings, info):
+        self.files = files          # {filename: bytes}
+        self.timings = timings      # phase → seconds
+        self.info = info            # s2c_batch_info
+
+
+def consensus_batch(hb, thresholds, prefix, min_depth=1, fill=b"-", nchar=0, device=None, timings=None):
+    """Device pipeline on a parsed HostBatch → {``REF__PREFIX.fasta``: bytes}."""
+    import torch
+
+    from .engine import DeviceBatch, Workspace
+    from .records import build_records, render
+
+    t = timings if timings is not None else {}
+    t0 = time.perf_counter()
+    db = DeviceBatch(hb, device)
+    ws = Workspace(db, thresholds, min_depth, fill)
+    torch.cuda.synchronize(db.device)
+    t["h2d"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    ws.run()
+    stats, offs, out = ws.fetch()
+    t["device"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    fastas = build_records(hb, thresholds, prefix, stats, offs, out)
+    pre = prefix.encode("latin-1") if isinstance(prefix, str) else prefix
+    files = {}
+    for name, recs in fastas.items():
+        files[name.encode("latin-1") + b"__" + pre + b".fasta"] = render(recs, nchar)
+    t["format"] = time.perf_counter() - t0
+    return files
+
+
+def consensus_files(filename, thresholds, prefix, min_depth=1, fill=b"-", nchar=0, maxdel_active=True,
+                    device=None, log=None):
+    """Run the whole pipeline on one SAM/SAM.gz file; returns a RunResult whose
+    ``files`` maps ``REF__PREFIX.fasta`` → content bytes (nothing written)."""
+    from .batch import parse_file
+
+    t = {}
+    t0 = time.perf_counter()
+    hb = parse_file(filename, maxdel_active, 150)
+    t["parse"] = time.perf_counter() - t0
+    if log:
+        log("SAM header processed, " + str(hb.info.n_refs) + " references found.\n")
+        reads_total = hb.info.lines_total - hb.info.header_lines
+        log("A total of " + str(reads_total) + " reads were processed, out of which, " +
+            str(hb.info.reads_mapped) + " reads were mapped.\n")
+    files = consensus_batch(hb, thresholds, prefix, min_depth, fill, nchar, device, t)
+    return RunResult(files, t, hb.info)
+
+
+def run_text(sam_text, argv, device=None):
+    """Library entry for tests: SAM text + CLI args (without -i) → (status, {fname: str}).
+    status is "ok" or the reference's exception class name; nothing touches the disk."""
+    from .batch import parse_text
+
+    args = build_parser().parse_args(["-i", "in.sam"] + list(argv))
+    try:
+        thresholds = [float(i) for i in args.thresholds.split(",")]
+        prefix = args.prefix or "in"
+        hb = parse_text(sam_text, not isinstance(args.maxdel, str), 150)
+        files = consensus_batch(hb, thresholds, os.fsencode(prefix), args.min_depth,
+                                os.fsencode(args.fill), args.n, device)
+    except (KeyError, IndexError, ValueError, ZeroDivisionError, OverflowError) as e:
+        return type(e).__name__, {}
+    return "ok", {k.decode("latin-1"): v.decode("latin-1") for k, v in files.items()}
+
+
+def main(argv=None):
+    args = build_parser().parse_args(argv)
+    filename = args.filename
+    thresholds = [float(i) for i in args.thresholds.split(",")]                # :117-118
+    if args.prefix == "":
+        prefix = "".join(args.filename.split("/")[-1]).split(".")[0]            # :121-122
+    else:
+        prefix = args.prefix
+    outfolder = args.outfolder.rstrip("/")                                       # :127-130
+    if not os.path.exists(outfolder):
+        os.makedirs(outfolder)
+    outfolder += "/"
+    maxdel_active = not isinstance(args.maxdel, str)
+    print("\nProcessing file " + filename + ":\n")
+    res = consensus_files(filename, thresholds, os.fsencode(prefix), args.min_depth, os.fsencode(args.fill),
+                          args.n, maxdel_active, log=lambda s: print(s))
+    for fname, body in res.files.items():                                         # :411-424
+        path = os.fsencode(outfolder) + fname
+        with open(path, "wb") as fh:
+            fh.write(body)
+        shown = os.fsdecode(path)
+        if len(thresholds) == 1:
+            print("Consensus sequence at " + str(int(thresholds[0] * 100)) + "% saved for " +
+                  os.fsdecode(fname[: fname.rfind(b"__")]) + " in: " + shown)
+        else:
+            print("Consensus sequences at " + ",".join([str(int(i * 100)) + "%" for i in thresholds]) +
+                  " saved for " + os.fsdecode(fname[: fname.rfind(b"__")]) + " in: " + shown)
+    print("Done.\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,799 @@
+// s2c_host.cpp — host side of libs2c.so: SAM/SAM.gz parser → packed read batch → work plan.
+//
+// Reproduces the reference's record handling (zoujiayun/sam2consensus v2.1,
+// sam2consensus.py) exactly, including its Python-2 quirks:
+//   header pass            :149-172   (leading '@' lines, @SQ SN:/LN: parse)
+//   record filter          :195       (line[0] != '@' and field[5] != "*"; FLAG ignored)
+//   RNAME / POS            :200-201   (str.split()[0], int() - 1)
+//   parsecigar             :46-82     (regex tokens, SEQ truncation, I/S/H/P/N semantics)
+//   maxdel rule            :210-218   (total '-' in seqout > maxdel ⇒ '-' not counted)
+//   Python negative index  :212       (pos -1 → last base)
+//   error classes          :195,:200,:201,:206,:212,:217,:221,:287,:294 in file order
+// and emits north_star subsystem (1): the packed batch the HIP kernels consume.
+#include "../../include/s2c.h"
+
+#include <zlib.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+// ------------------------------------------------------------------ errors
+static thread_local std::string g_err;
+int s2c_set_error(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+extern "C" const char *s2c_last_error(void) { return g_err.c_str(); }
+extern "C" int s2c_abi_version(void) { return S2C_ABI_VERSION; }
+
+// ------------------------------------------------------------------ tables
+namespace {
+constexpr uint8_t BAD = 0xFF;
+struct CodeLut {
+    uint8_t v[256];
+    CodeLut() {
+        memset(v, BAD, sizeof(v));
+        v[(uint8_t)'-'] = 0; v[(uint8_t)'A'] = 1; v[(uint8_t)'C'] = 2;
+        v[(uint8_t)'G'] = 3; v[(uint8_t)'N'] = 4; v[(uint8_t)'T'] = 5;
+    }
+};
+const CodeLut LUT;
+
+inline bool py2_ws(char c) {  // Python 2 str.split()/int() whitespace (C locale isspace)
+    return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\x0b' || c == '\x0c';
+}
+
+// Python 2 int(str): whitespace, sign, decimal digits, whitespace.  Saturates at ±2^62
+// (positions that large are out of range anyway and raise IndexError downstream).
+bool py2_int(const char *s, size_t n, int64_t *out) {
+    size_t i = 0;
+    while (i < n && py2_ws(s[i])) i++;
+    bool neg = false;
+    if (i < n && (s[i] == '+' || s[i] == '-')) { neg = s[i] == '-'; i++; }
+    size_t d0 = i;
+    int64_t v = 0;
+    const int64_t CAP = (int64_t)1 << 62;
+    while (i < n && s[i] >= '0' && s[i] <= '9') {
+        if (v < CAP) v = v * 10 + (s[i] - '0');
+        if (v > CAP) v = CAP;
+        i++;
+    }
+    if (i == d0) return false;
+    while (i < n && py2_ws(s[i])) i++;
+    if (i != n) return false;
+    *out = neg ? -v : v;
+    return true;
+}
+
+// first whitespace-delimited token (Python 2 str.split()[0])
+bool py2_first_token(const char *s, size_t n, const char **tb, size_t *tl) {
+    size_t i = 0;
+    while (i < n && py2_ws(s[i])) i++;
+    if (i == n) return false;
+    size_t j = i;
+    while (j < n && !py2_ws(s[j])) j++;
+    *tb = s + i;
+    *tl = j - i;
+    return true;
+}
+
+// str.replace(pat, "") — Python's single left-to-right non-overlapping pass.
+std::string py_remove(const char *s, size_t n, const char *pat) {
+    size_t m = strlen(pat);
+    std::string out;
+    out.reserve(n);
+    size_t i = 0;
+    while (i < n) {
+        if (i + m <= n && memcmp(s + i, pat, m) == 0) { i += m; continue; }
+        out.push_back(s[i++]);
+    }
+    return out;
+}
+
+struct Tok { char op; int64_t len; };
+
+// re.findall(r"(\d+)([MIDNSHPX=]{1})", cigar) (:58): a match is a maximal digit run
+// immediately followed by an op letter; everything else is skipped.
+int tokenize_cigar(const char *s, size_t n, std::vector<Tok> &out) {
+    out.clear();
+    size_t i = 0;
+    while (i < n) {
+        if (s[i] < '0' || s[i] > '9') { i++; continue; }
+        size_t j = i;
+        int64_t v = 0;
+        bool big = false;
+        while (j < n && s[j] >= '0' && s[j] <= '9') {
+            v = v * 10 + (s[j] - '0');
+            if (v >= ((int64_t)1 << 31)) { big = true; v = (int64_t)1 << 31; }
+            j++;
+        }
+        if (j < n) {
+            char c = s[j];
+            if (c == 'M' || c == 'I' || c == 'D' || c == 'N' || c == 'S' || c == 'H' || c == 'P' ||
+                c == 'X' || c == '=') {
+                if (big) return s2c_set_error(S2C_ERR_LIMIT, "CIGAR op length >= 2^31 not supported");
+                out.push_back({c, v});
+                i = j + 1;
+                continue;
+            }
+        }
+        i = j;
+    }
+    return S2C_OK;
+}
+}  // namespace
+
+// ------------------------------------------------------------------ parser state
+struct EffOp { uint8_t cls; int64_t len; };   // cls 0 = M (bases), 1 = D (dashes)
+
+struct s2c_parser {
+    bool maxdel_active = true;
+    int64_t maxdel = 150;
+    bool in_header = true;
+    int64_t header_lines = 0, lines_total = 0, reads_mapped = 0, aligned = 0, qbases = 0;
+    std::vector<std::string> ref_names;
+    std::vector<int64_t> ref_len;
+    std::unordered_map<std::string, uint32_t> ref_idx;
+    // pileup pieces (file order): every position of a piece lies in [0, LN) of its ref
+    std::vector<uint32_t> p_ref;
+    std::vector<int64_t> p_pos;
+    std::vector<uint32_t> p_span;
+    std::vector<uint8_t> p_drop;
+    std::vector<uint64_t> p_op;     // CSR into ops (size n+1)
+    std::vector<uint32_t> ops;      // (len<<1)|cls
+    std::vector<uint64_t> p_base;   // CSR (word offsets) into words (size n+1)
+    std::vector<uint32_t> words;    // 4-bit codes, 8 per word
+    // insertion events (file order), raw motif bytes (validated at finish, :287)
+    std::vector<uint32_t> i_ref;
+    std::vector<int64_t> i_key;
+    std::vector<uint64_t> i_off;
+    std::vector<uint32_t> i_len;
+    std::string i_raw;
+    // streaming
+    std::string carry;
+    int err = S2C_OK;
+    std::string errmsg;
+    // scratch
+    std::vector<Tok> toks;
+    std::vector<EffOp> eff;
+    std::vector<uint8_t> codes;
+    std::string last_name;
+    int64_t last_ref = -1;
+
+    s2c_parser() { p_op.push_back(0); p_base.push_back(0); }
+};
+
+struct s2c_batch {
+    s2c_batch_info info{};
+    std::vector<std::string> names;
+    std::vector<int64_t> ref_len, ref_off, ref_reads;
+    std::vector<uint32_t> rd_pos, rd_op, rd_base, ops, bases;
+    std::vector<uint32_t> ins_key, ins_off, ins_bases;
+    std::vector<uint32_t> items, extras, blocks;
+};
+
+static int perr(s2c_parser *p, int code, const std::string &msg) {
+    p->err = code;
+    p->errmsg = msg;
+    return s2c_set_error(code, msg);
+}
+
+// @SQ line (:160-169): refname = f[1].replace("SN:","").split()[0]; LN = int(f[2].replace("LN:",""))
+static int parse_sq(s2c_parser *p, const char *s, size_t n) {
+    const char *f[3];
+    size_t fl[3];
+    int nf = 0;
+    const char *cur = s, *end = s + n;
+    while (nf < 3) {
+        const char *t = (const char *)memchr(cur, '\t', end - cur);
+        f[nf] = cur;
+        if (!t) { fl[nf++] = end - cur; break; }
+        fl[nf++] = t - cur;
+        cur = t + 1;
+    }
+    if (nf < 2) return perr(p, S2C_ERR_INDEX, "IndexError: @SQ line has no field 1 (:163)");
+    std::string f1 = py_remove(f[1], fl[1], "SN:");
+    const char *tb;
+    size_t tl;
+    if (!py2_first_token(f1.data(), f1.size(), &tb, &tl))
+        return perr(p, S2C_ERR_INDEX, "IndexError: empty @SQ SN (:163)");
+    std::string name(tb, tl);
+    if (nf < 3) return perr(p, S2C_ERR_INDEX, "IndexError: @SQ line has no field 2 (:164)");
+    std::string f2 = py_remove(f[2], fl[2], "LN:");
+    int64_t ln;
+    if (!py2_int(f2.data(), f2.size(), &ln))
+        return perr(p, S2C_ERR_VALUE, "ValueError: invalid @SQ LN '" + f2 + "' (:164)");
+    if (ln < 0) ln = 0;  // range(negative) → empty list (:167)
+    auto it = p->ref_idx.find(name);
+    if (it == p->ref_idx.end()) {
+        p->ref_idx.emplace(name, (uint32_t)p->ref_names.size());
+        p->ref_names.push_back(name);
+        p->ref_len.push_back(ln);
+    } else {
+        p->ref_len[it->second] = ln;  // duplicate @SQ re-initialises (:167-169)
+    }
+    return S2C_OK;
+}
+
+// Append piece = seqout[ka, kb) of the current read (eff ops + codes) at ref position pos.
+static void emit_piece(s2c_parser *p, uint32_t ref, int64_t pos, bool drop, int64_t ka, int64_t kb) {
+    int64_t k = 0;
+    size_t ci = 0;  // index into p->codes (M bases in seqout order)
+    uint32_t nops = 0;
+    std::vector<uint8_t> &codes = p->codes;
+    size_t w0 = p->words.size();
+    uint32_t acc = 0;
+    int nib = 0;
+    for (const EffOp &o : p->eff) {
+        int64_t a = std::max(k, ka), b = std::min(k + o.len, kb);
+        if (b > a) {
+            uint32_t w = (uint32_t)(((uint64_t)(b - a) << 1) | o.cls);
+            if (nops && (p->ops.back() & 1) == o.cls) {
+                p->ops.back() += (uint32_t)((b - a) << 1);   // merge same-class neighbours
+            } else {
+                p->ops.push_back(w);
+                nops++;
+            }
+            if (o.cls == 0) {
+                for (int64_t j = a - k; j < b - k; j++) {
+                    acc |= (uint32_t)codes[ci + j] << (4 * nib);
+                    if (++nib == 8) { p->words.push_back(acc); acc = 0; nib = 0; }
+                }
+            }
+        }
+        if (o.cls == 0) ci += (size_t)o.len;
+        k += o.len;
+    }
+    if (nib) p->words.push_back(acc);
+    p->p_ref.push_back(ref);
+    p->p_pos.push_back(pos);
+    p->p_span.push_back((uint32_t)(kb - ka));
+    p->p_drop.push_back(drop ? 1 : 0);
+    p->p_op.push_back(p->ops.size());
+    p->p_base.push_back(p->words.size());
+    (void)w0;
+}
+
+// One SAM line, n includes the trailing '\n' when present (Python 2 line semantics).
+static int process_line(s2c_parser *p, const char *s, size_t n) {
+    p->lines_total++;
+    if (p->in_header) {
+        if (s[0] == '@') {
+            p->header_lines++;
+            if (n >= 3 && s[1] == 'S' && s[2] == 'Q') return parse_sq(p, s, n);
+            return S2C_OK;
+        }
+        p->in_header = false;
+    }
+    if (s[0] == '@') return S2C_OK;                                   // :195
+    const char *f[10];
+    size_t fl[10];
+    int nf = 0;
+    const char *cur = s, *end = s + n;
+    while (nf < 10) {
+        const char *t = (const char *)memchr(cur, '\t', end - cur);
+        f[nf] = cur;
+        if (!t) { fl[nf++] = end - cur; break; }
+        fl[nf++] = t - cur;
+        cur = t + 1;
+    }
+    if (nf < 6) return perr(p, S2C_ERR_INDEX, "IndexError: record with < 6 fields (:195)");
+    if (fl[5] == 1 && f[5][0] == '*') return S2C_OK;                  // unmapped (:195)
+    p->reads_mapped++;
+    const char *nb;
+    size_t nl;
+    if (!py2_first_token(f[2], fl[2], &nb, &nl))
+        return perr(p, S2C_ERR_INDEX, "IndexError: empty RNAME (:200)");
+    int64_t pos1;
+    if (!py2_int(f[3], fl[3], &pos1))
+        return perr(p, S2C_ERR_VALUE, "ValueError: invalid POS '" + std::string(f[3], fl[3]) + "' (:201)");
+    int64_t pos0 = pos1 - 1;
+    if (nf < 10) return perr(p, S2C_ERR_INDEX, "IndexError: record with < 10 fields (:206)");
+
+    // ---- parsecigar (:46-82) ----
+    int rc = tokenize_cigar(f[5], fl[5], p->toks);
+    if (rc) return perr(p, rc, s2c_last_error());
+    const char *seq = f[9];
+    const int64_t slen = (int64_t)fl[9];
+    int64_t start = 0, start_ref = pos0, klen = 0;
+    p->eff.clear();
+    p->codes.clear();
+    size_t ins_first = p->i_ref.size();
+    for (const Tok &t : p->toks) {
+        int64_t l = t.len;
+        switch (t.op) {
+            case 'M': case '=': case 'X': {
+                int64_t take = start < slen ? std::min(l, slen - start) : 0;
+                if (take > 0) {
+                    if (!p->eff.empty() && p->eff.back().cls == 0) p->eff.back().len += take;
+                    else p->eff.push_back({0, take});
+                    for (int64_t j = 0; j < take; j++) p->codes.push_back(LUT.v[(uint8_t)seq[start + j]]);
+                    klen += take;
+                }
+                start += l;
+                start_ref += l;
+                break;
+            }
+            case 'D': case 'N': case 'P':
+                if (l > 0) {
+                    if (!p->eff.empty() && p->eff.back().cls == 1) p->eff.back().len += l;
+                    else p->eff.push_back({1, l});
+                    klen += l;
+                }
+                start_ref += l;
+                break;
+            case 'I': {
+                int64_t take = start < slen ? std::min(l, slen - start) : 0;
+                if (take > 0) {    // an empty motif never reaches a column (:280-287)
+                    p->i_ref.push_back(0);  // fixed below once the ref is known
+                    p->i_key.push_back(start_ref);
+                    p->i_off.push_back(p->i_raw.size());
+                    p->i_len.push_back((uint32_t)take);
+                    p->i_raw.append(seq + start, (size_t)take);
+                }
+                start += l;
+                break;
+            }
+            case 'S':
+                start += l;
+                break;
+            default:  // 'H' (:78-79)
+                break;
+        }
+    }
+    if (klen >= ((int64_t)1 << 31)) return perr(p, S2C_ERR_LIMIT, "seqout longer than 2^31");
+    p->aligned += klen;
+
+    // ---- reference lookup: sequences[refname] / insertions[refname] (:212,:217,:221) ----
+    int64_t ref;
+    if (p->last_ref >= 0 && p->last_name.size() == nl && memcmp(p->last_name.data(), nb, nl) == 0) {
+        ref = p->last_ref;
+    } else {
+        std::string name(nb, nl);
+        auto it = p->ref_idx.find(name);
+        if (it == p->ref_idx.end()) return perr(p, S2C_ERR_KEY, "KeyError: '" + name + "' (:212/:221)");
+        ref = it->second;
+        p->last_ref = ref;
+        p->last_name = name;
+    }
+    for (size_t i = ins_first; i < p->i_ref.size(); i++) {
+        p->i_ref[i] = (uint32_t)ref;
+        p->qbases += p->i_len[i];
+    }
+    const int64_t L = p->ref_len[ref];
+
+    // ---- maxdel rule (:210): '-' count of the whole seqout ----
+    int64_t dashes = 0, mbases = 0;
+    for (const EffOp &o : p->eff) if (o.cls == 1) dashes += o.len; else mbases += o.len;
+    bool any_bad = false;
+    for (uint8_t c : p->codes) { dashes += (c == 0); any_bad |= (c == BAD); }
+    p->qbases += mbases;
+    const bool drop = p->maxdel_active && dashes > p->maxdel;
+
+    // ---- validation in seqout order (:211-218): index check, then symbol check ----
+    const bool in_range = pos0 >= 0 && pos0 + klen <= L;
+    int64_t kc0 = -1, kc1 = -1;  // first / last counted seqout index
+    if (!in_range || any_bad || drop) {
+        int64_t k = 0;
+        size_t ci = 0;
+        for (const EffOp &o : p->eff) {
+            for (int64_t j = 0; j < o.len; j++, k++) {
+                uint8_t c = o.cls ? 0 : p->codes[ci + j];
+                if (drop && c == 0) continue;               // '-' skipped (:216)
+                int64_t pp = pos0 + k;
+                if (pp < -L || pp >= L)
+                    return perr(p, S2C_ERR_INDEX, "IndexError: list index out of range (:212)");
+                if (c == BAD) return perr(p, S2C_ERR_KEY, "KeyError: base not in -ACGNT (:212)");
+                if (kc0 < 0) kc0 = k;
+                kc1 = k + 1;
+            }
+            if (o.cls == 0) ci += (size_t)o.len;
+        }
+    } else if (klen > 0) {
+        kc0 = 0;
+        kc1 = klen;
+    }
+    if (kc0 < 0) return S2C_OK;   // nothing counted (empty seqout, or all '-' dropped)
+
+    // ---- pieces: Python negative indices wrap (pos -1 → LN-1, :212) ----
+    int64_t pa = pos0 + kc0;
+    if (pa < 0) {
+        int64_t kb = std::min(kc1, -pos0);
+        emit_piece(p, (uint32_t)ref, L + pa, drop, kc0, kb);
+        if (kc1 > -pos0) emit_piece(p, (uint32_t)ref, 0, drop, -pos0, kc1);
+    } else {
+        emit_piece(p, (uint32_t)ref, pa, drop, kc0, kc1);
+    }
+    return S2C_OK;
+}
+
+extern "C" int s2c_parser_new(int maxdel_active, int64_t maxdel, s2c_parser **out) {
+    if (!out) return s2c_set_error(S2C_ERR_ARG, "out is NULL");
+    s2c_parser *p = new s2c_parser();
+    p->maxdel_active = maxdel_active != 0;
+    p->maxdel = maxdel;
+    *out = p;
+    return S2C_OK;
+}
+
+extern "C" void s2c_parser_free(s2c_parser *p) { delete p; }
+
+extern "C" int s2c_parser_feed(s2c_parser *p, const char *buf, size_t len) {
+    if (!p) return s2c_set_error(S2C_ERR_ARG, "parser is NULL");
+    if (p->err) return s2c_set_error(p->err, p->errmsg);
+    const char *s = buf, *end = buf + len;
+    if (!p->carry.empty()) {
+        const char *nl = (const char *)memchr(s, '\n', end - s);
+        if (!nl) { p->carry.append(s, len); return S2C_OK; }
+        p->carry.append(s, nl + 1 - s);
+        int rc = process_line(p, p->carry.data(), p->carry.size());
+        p->carry.clear();
+        if (rc) return rc;
+        s = nl + 1;
+    }
+    while (s < end) {
+        const char *nl = (const char *)memchr(s, '\n', end - s);
+        if (!nl) { p->carry.assign(s, end - s); break; }
+        int rc = process_line(p, s, nl + 1 - s);
+        if (rc) return rc;
+        s = nl + 1;
+    }
+    return S2C_OK;
+}
+
+static int feed_flush(s2c_parser *p) {
+    if (p->err) return s2c_set_error(p->err, p->errmsg);
+    if (!p->carry.empty()) {   // last line without '\n'
+        std::string last;
+        last.swap(p->carry);
+        int rc = process_line(p, last.data(), last.size());
+        if (rc) return rc;
+    }
+    return S2C_OK;
+}
+
+extern "C" int s2c_parser_feed_file(s2c_parser *p, const char *path) {
+    if (!p || !path) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
+    size_t n = strlen(path);
+    bool gz = n >= 3 && strcmp(path + n - 3, ".gz") == 0;   // :111
+    std::vector<char> buf(1 << 22);
+    if (gz) {
+        gzFile g = gzopen(path, "rb");
+        if (!g) return s2c_set_error(S2C_ERR_IO, std::string("cannot open ") + path);
+        gzbuffer(g, 1 << 20);
+        for (;;) {
+            int r = gzread(g, buf.data(), (unsigned)buf.size());
+            if (r < 0) { gzclose(g); return s2c_set_error(S2C_ERR_IO, "gzip read error"); }
+            if (r == 0) break;
+            int rc = s2c_parser_feed(p, buf.data(), (size_t)r);
+            if (rc) { gzclose(g); return rc; }
+        }
+        gzclose(g);
+    } else {
+        FILE *f = fopen(path, "rb");
+        if (!f) return s2c_set_error(S2C_ERR_IO, std::string("cannot open ") + path);
+        for (;;) {
+            size_t r = fread(buf.data(), 1, buf.size(), f);
+            if (r == 0) break;
+            int rc = s2c_parser_feed(p, buf.data(), r);
+            if (rc) { fclose(f); return rc; }
+        }
+        fclose(f);
+    }
+    return feed_flush(p);
+}
+
+// ------------------------------------------------------------------ finish: plan
+namespace {
+constexpr int64_t TP_MIN = 256, TP_MAX = 2048;      // pileup tile bounds (positions)
+constexpr double E_TARGET = 131072.0;                // aligned bases per pileup work item
+constexpr int64_t LONG_SPAN = 1024;                  // longer pieces go through per-tile extras
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline int64_t align_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }
+}  // namespace
+
+extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
+    if (!p || !out) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
+    int rc = feed_flush(p);
+    if (rc) return rc;
+    const int64_t R = (int64_t)p->ref_names.size();
+
+    // ---- reformat-phase checks (:284-294), refs in header order: motif symbols (KeyError,
+    //      :287) are checked for every key before any key's coverage lookup (IndexError, :294)
+    {
+        std::vector<uint8_t> bad_sym(R, 0), bad_key(R, 0);
+        for (size_t i = 0; i < p->i_ref.size(); i++) {
+            uint32_t r = p->i_ref[i];
+            const int64_t L = p->ref_len[r];
+            for (uint32_t j = 0; j < p->i_len[i]; j++)
+                if (LUT.v[(uint8_t)p->i_raw[p->i_off[i] + j]] == BAD) { bad_sym[r] = 1; break; }
+            if (p->i_key[i] < -L || p->i_key[i] >= L) bad_key[r] = 1;
+        }
+        for (int64_t r = 0; r < R; r++) {
+            if (bad_sym[r]) return s2c_set_error(S2C_ERR_KEY, "KeyError: insertion base not in -ACGNT (:287)");
+            if (bad_key[r]) return s2c_set_error(S2C_ERR_INDEX, "IndexError: insertion key out of range (:294)");
+        }
+    }
+
+    s2c_batch *b = new s2c_batch();
+    s2c_batch_info &I = b->info;
+    b->names = p->ref_names;
+    b->ref_len = p->ref_len;
+    b->ref_off.resize(R);
+    b->ref_reads.assign(R, 0);
+    int64_t g = 0;
+    for (int64_t r = 0; r < R; r++) {
+        b->ref_off[r] = g;
+        g = align_up(g + p->ref_len[r], S2C_POS_ALIGN);
+    }
+    const int64_t Lpad = std::max<int64_t>(g, S2C_POS_ALIGN);
+    if (Lpad >= ((int64_t)1 << 32) - 4096) {
+        delete b;
+        return s2c_set_error(S2C_ERR_LIMIT, "more than 2^32 reference positions");
+    }
+    I.n_refs = R;
+    I.padded_len = Lpad;
+    for (int64_t r = 0; r < R; r++) I.total_len += p->ref_len[r];
+    I.header_lines = p->header_lines;
+    I.lines_total = p->lines_total;
+    I.reads_mapped = p->reads_mapped;
+    I.aligned_bases = p->aligned;
+    I.query_bases = p->qbases;
+
+    // ---- pieces → global coordinates; bucket sort by start (64-position buckets) ----
+    const int64_t NP = (int64_t)p->p_ref.size();
+    std::vector<uint64_t> gstart(NP);
+    std::vector<uint8_t> is_long(NP);
+    const int64_t NB = Lpad / S2C_POS_ALIGN + 1;
+    std::vector<int64_t> bucket(NB + 1, 0);
+    int64_t n_long = 0;
+    for (int64_t i = 0; i < NP; i++) {
+        gstart[i] = (uint64_t)(b->ref_off[p->p_ref[i]] + p->p_pos[i]);
+        b->ref_reads[p->p_ref[i]]++;
+        is_long[i] = p->p_span[i] > LONG_SPAN;
+        if (is_long[i]) n_long++;
+        else bucket[gstart[i] / S2C_POS_ALIGN + 1]++;
+    }
+    for (int64_t k = 0; k < NB; k++) bucket[k + 1] += bucket[k];
+    const int64_t NS = NP - n_long;
+    std::vector<int64_t> order(NP);
+    {
+        std::vector<int64_t> fill(bucket.begin(), bucket.end() - 1);
+        int64_t li = NS;
+        for (int64_t i = 0; i < NP; i++) {
+            if (is_long[i]) order[li++] = i;
+            else order[fill[gstart[i] / S2C_POS_ALIGN]++] = i;
+        }
+    }
+    I.n_reads = NP;
+    I.n_long = n_long;
+    b->rd_pos.resize(NP);
+    b->rd_op.resize(NP + 1);
+    b->rd_base.resize(NP);
+    uint64_t nops = 0, nwords = 0;
+    for (int64_t i = 0; i < NP; i++) {
+        nops += p->p_op[i + 1] - p->p_op[i];
+        nwords += p->p_base[i + 1] - p->p_base[i];
+    }
+    if (nops >= (1ull << 31) || nwords >= (1ull << 32)) {
+        delete b;
+        return s2c_set_error(S2C_ERR_LIMIT, "batch exceeds 2^31 ops or 2^32 base words");
+    }
+    b->ops.resize(nops);
+    b->bases.resize(nwords);
+    std::vector<uint64_t> gend(NS);
+    {
+        uint64_t oo = 0, ww = 0;
+        for (int64_t j = 0; j < NP; j++) {
+            int64_t i = order[j];
+            b->rd_pos[j] = (uint32_t)gstart[i];
+            b->rd_op[j] = (uint32_t)oo | (p->p_drop[i] ? 0x80000000u : 0u);
+            b->rd_base[j] = (uint32_t)ww;
+            uint64_t no = p->p_op[i + 1] - p->p_op[i], nw = p->p_base[i + 1] - p->p_base[i];
+            memcpy(&b->ops[oo], &p->ops[p->p_op[i]], no * 4);
+            memcpy(&b->bases[ww], &p->words[p->p_base[i]], nw * 4);
+            oo += no;
+            ww += nw;
+            if (j < NS) gend[j] = gstart[i] + p->p_span[i];
+        }
+        b->rd_op[NP] = (uint32_t)oo;
+    }
+    I.n_ops = (int64_t)nops;
+    I.n_base_words = (int64_t)nwords;
+    // prefix max of piece ends (short pieces, sorted order) → first overlapping read per tile
+    std::vector<uint64_t> pmax(NS);
+    {
+        uint64_t m = 0;
+        for (int64_t j = 0; j < NS; j++) { m = std::max(m, gend[j]); pmax[j] = m; }
+    }
+    // long pieces: per tile lists, built after tiles are known
+    // ---- pileup work items ----
+    std::vector<int64_t> ref_events(R, 0);
+    for (int64_t i = 0; i < NP; i++) ref_events[p->p_ref[i]] += p->p_span[i];
+    struct Tile { int64_t a, b, lo, hi; double ev; };
+    std::vector<Tile> tiles;
+    int64_t tile_max = S2C_POS_ALIGN;
+    for (int64_t r = 0; r < R; r++) {
+        const int64_t L = p->ref_len[r], off = b->ref_off[r];
+        if (L == 0) continue;
+        double depth = (double)ref_events[r] / (double)L;
+        int64_t tp = depth > 0 ? align_up((int64_t)std::ceil(E_TARGET / depth), S2C_POS_ALIGN) : TP_MAX;
+        tp = std::min(std::max(tp, TP_MIN), TP_MAX);
+        // spread the ref evenly over ceil(L/tp) tiles, each a multiple of 64
+        int64_t nt = ceil_div(L, tp);
+        int64_t step = align_up(ceil_div(L, nt), S2C_POS_ALIGN);
+        for (int64_t a = off; a < off + L; a += step) {
+            int64_t e = std::min(a + step, off + L);
+            int64_t hi = bucket[std::min<int64_t>(align_up(e, S2C_POS_ALIGN) / S2C_POS_ALIGN, NB)];
+            int64_t lo = std::upper_bound(pmax.begin(), pmax.begin() + hi, (uint64_t)a) - pmax.begin();
+            tiles.push_back({a, e, lo, hi, depth * (double)(e - a)});
+            tile_max = std::max(tile_max, e - a);
+        }
+    }
+    I.tile_max = tile_max;
+    // long pieces → tiles they overlap (tiles are sorted by a)
+    std::vector<std::vector<uint32_t>> tile_x(tiles.size());
+    for (int64_t j = NS; j < NP; j++) {
+        uint64_t s = b->rd_pos[j];
+        uint64_t e = s + p->p_span[order[j]];
+        size_t t0 = std::upper_bound(tiles.begin(), tiles.end(), (int64_t)s,
+                                     [](int64_t v, const Tile &t) { return v < t.a; }) - tiles.begin();
+        if (t0 > 0) t0--;
+        for (size_t t = t0; t < tiles.size() && (uint64_t)tiles[t].a < e; t++)
+            if ((uint64_t)tiles[t].b > s) tile_x[t].push_back((uint32_t)j);
+    }
+    for (size_t t = 0; t < tiles.size(); t++) {
+        const Tile &T = tiles[t];
+        int64_t nch = std::max<int64_t>(1, (int64_t)std::ceil(T.ev / (2.0 * E_TARGET)));
+        int64_t nr = T.hi - T.lo;
+        if (nr < nch) nch = std::max<int64_t>(1, nr);
+        uint32_t x_lo = (uint32_t)b->extras.size();
+        for (uint32_t x : tile_x[t]) b->extras.push_back(x);
+        uint32_t x_hi = (uint32_t)b->extras.size();
+        for (int64_t c = 0; c < nch; c++) {
+            int64_t r0 = T.lo + nr * c / nch, r1 = T.lo + nr * (c + 1) / nch;
+            uint32_t it[S2C_ITEM_WORDS] = {(uint32_t)T.a, (uint32_t)T.b, (uint32_t)r0, (uint32_t)r1,
+                                           c == 0 ? x_lo : x_hi, x_hi,
+                                           (uint32_t)((nch > 1 ? 1u : 0u) | (c == 0 ? 2u : 0u)), 0};
+            b->items.insert(b->items.end(), it, it + S2C_ITEM_WORDS);
+        }
+    }
+    I.n_items = (int64_t)(b->items.size() / S2C_ITEM_WORDS);
+    I.n_extras = (int64_t)b->extras.size();
+
+    // ---- consensus blocks (never straddle a ref) ----
+    for (int64_t r = 0; r < R; r++) {
+        const int64_t L = p->ref_len[r], off = b->ref_off[r];
+        uint32_t first = (uint32_t)(b->blocks.size() / S2C_BLOCK_WORDS);
+        for (int64_t a = off; a < off + L; a += S2C_VOTE_BLOCK) {
+            uint32_t blk[S2C_BLOCK_WORDS] = {(uint32_t)a, (uint32_t)std::min(a + S2C_VOTE_BLOCK, off + L),
+                                             (uint32_t)r, first};
+            b->blocks.insert(b->blocks.end(), blk, blk + S2C_BLOCK_WORDS);
+        }
+    }
+    I.n_blocks = (int64_t)(b->blocks.size() / S2C_BLOCK_WORDS);
+
+    // ---- insertion events: keys in [0, LN) (negative keys are never emitted, :371) ----
+    {
+        uint64_t nb = 0;
+        for (size_t i = 0; i < p->i_ref.size(); i++) {
+            int64_t key = p->i_key[i];
+            if (key < 0) continue;
+            b->ins_key.push_back((uint32_t)(b->ref_off[p->i_ref[i]] + key));
+            b->ins_off.push_back((uint32_t)nb);
+            nb += p->i_len[i];
+        }
+        if (nb >= (1ull << 32)) { delete b; return s2c_set_error(S2C_ERR_LIMIT, "insertion bases >= 2^32"); }
+        b->ins_off.push_back((uint32_t)nb);
+        b->ins_bases.assign((nb + 7) / 8, 0);
+        uint64_t q = 0;
+        for (size_t i = 0; i < p->i_ref.size(); i++) {
+            if (p->i_key[i] < 0) continue;
+            for (uint32_t j = 0; j < p->i_len[i]; j++, q++)
+                b->ins_bases[q >> 3] |= (uint32_t)LUT.v[(uint8_t)p->i_raw[p->i_off[i] + j]] << (4 * (q & 7));
+        }
+        I.n_ins = (int64_t)b->ins_key.size();
+        I.n_ins_bases = (int64_t)nb;
+        I.n_ins_words = (int64_t)b->ins_bases.size();
+    }
+    *out = b;
+    return S2C_OK;
+}
+
+extern "C" int s2c_batch_info_get(const s2c_batch *b, s2c_batch_info *out) {
+    if (!b || !out) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
+    *out = b->info;
+    return S2C_OK;
+}
+
+extern "C" int s2c_batch_arrays_get(const s2c_batch *b, s2c_batch_arrays *o) {
+    if (!b || !o) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
+    o->ref_len = b->ref_len.data();
+    o->ref_off = b->ref_off.data();
+    o->ref_cov_reads = b->ref_reads.data();
+    o->rd_pos = b->rd_pos.data();
+    o->rd_op = b->rd_op.data();
+    o->rd_base = b->rd_base.data();
+    o->ops = b->ops.data();
+    o->bases = b->bases.data();
+    o->ins_key = b->ins_key.data();
+    o->ins_off = b->ins_off.data();
+    o->ins_bases = b->ins_bases.data();
+    o->items = b->items.data();
+    o->extras = b->extras.data();
+    o->blocks = b->blocks.data();
+    return S2C_OK;
+}
+
+extern "C" const char *s2c_batch_ref_name(const s2c_batch *b, int64_t i) {
+    if (!b || i < 0 || i >= (int64_t)b->names.size()) return nullptr;
+    return b->names[i].c_str();
+}
+
+extern "C" void s2c_batch_free(s2c_batch *b) { delete b; }
+
+// ------------------------------------------------------------------ parsecigar (:46-82)
+extern "C" int s2c_parsecigar(const char *cigar, size_t cigar_len, const char *seq, size_t seq_len,
+                              int64_t pos_ref, char *seqout, size_t cap, size_t *seqout_len,
+                              int64_t *ins, size_t max_ins, size_t *n_ins) {
+    std::vector<Tok> toks;
+    int rc = tokenize_cigar(cigar, cigar_len, toks);
+    if (rc) return rc;
+    int64_t start = 0, start_ref = pos_ref;
+    const int64_t slen = (int64_t)seq_len;
+    size_t o = 0, ni = 0;
+    auto put = [&](char c) -> bool {
+        if (o + 1 >= cap) return false;
+        seqout[o++] = c;
+        return true;
+    };
+    for (const Tok &t : toks) {
+        int64_t l = t.len;
+        if (t.op == 'M' || t.op == '=' || t.op == 'X') {
+            int64_t take = start < slen ? std::min(l, slen - start) : 0;
+            for (int64_t j = 0; j < take; j++)
+                if (!put(seq[start + j])) return s2c_set_error(S2C_ERR_ARG, "seqout buffer too small");
+            start += l;
+            start_ref += l;
+        } else if (t.op == 'D' || t.op == 'N' || t.op == 'P') {
+            for (int64_t j = 0; j < l; j++)
+                if (!put('-')) return s2c_set_error(S2C_ERR_ARG, "seqout buffer too small");
+            start_ref += l;
+        } else if (t.op == 'I') {
+            int64_t take = start < slen ? std::min(l, slen - start) : 0;
+            if (ni < max_ins) {
+                ins[3 * ni] = start_ref;
+                ins[3 * ni + 1] = std::min(start, slen);
+                ins[3 * ni + 2] = take;
+            }
+            ni++;
+            start += l;
+        } else if (t.op == 'S') {
+            start += l;
+        }
+    }
+    if (cap) seqout[o] = 0;
+    *seqout_len = o;
+    *n_ins = ni;
+    return ni > max_ins ? s2c_set_error(S2C_ERR_ARG, "insertion buffer too small") : S2C_OK;
+}
+
+// ------------------------------------------------------------------ ABI layout self-check
+// Lets the ctypes mirror (sam2consensus_amd/_lib.py) verify struct sizes/offsets at load.
+#include <cstddef>
+extern "C" int s2c_layout(int64_t *out, int n) {
+    const int64_t v[] = {
+        (int64_t)sizeof(s2c_dev), (int64_t)offsetof(s2c_dev, tile_max), (int64_t)offsetof(s2c_dev, thresholds),
+        (int64_t)offsetof(s2c_dev, fill), (int64_t)offsetof(s2c_dev, counts), (int64_t)offsetof(s2c_dev, ins_cap),
+        (int64_t)offsetof(s2c_dev, stats), (int64_t)offsetof(s2c_dev, out_cap),
+        (int64_t)sizeof(s2c_synth_spec), (int64_t)offsetof(s2c_synth_spec, seed),
+        (int64_t)sizeof(s2c_batch_info), (int64_t)sizeof(s2c_batch_arrays), (int64_t)sizeof(s2c_ws_sizes)};
+    const int m = (int)(sizeof(v) / sizeof(v[0]));
+    for (int i = 0; i < n && i < m; i++) out[i] = v[i];
+    return m;
+}

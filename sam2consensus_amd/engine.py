@@ -1,0 +1,147 @@
+"""Device side: packed batch → HBM, workspace, the four HIP stages, results → host.
+
+PyTorch is used only as the device allocator / stream provider; all compute is
+libs2c.so's hand-written HIP kernels (s2c_kernels.hip).  There is no CPU
+fallback: without a visible GPU ``DeviceBatch`` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from ._lib import lib
+
+
+def _dev(device):
+    if device is None:
+        device = "cuda:%d" % int(os.environ.get("LOCAL_RANK", "0"))
+    d = torch.device(device)
+    if d.type != "cuda" or not torch.cuda.is_available():
+        raise RuntimeError("sam2consensus_amd needs a ROCm GPU (torch.cuda unavailable); no CPU fallback")
+    return d
+
+
+def _up(arr, device):
+    """numpy u32/i64 array → device tensor (bit-preserving, ≥1 element)."""
+    a = np.ascontiguousarray(arr)
+    if a.dtype == np.uint32:
+        a = a.view(np.int32)
+    elif a.dtype == np.uint64:
+        a = a.view(np.int64)
+    if a.size == 0:
+        a = np.zeros(4, dtype=a.dtype if a.dtype != np.uint8 else np.uint8)
+    return torch.from_numpy(a).to(device, non_blocking=False)
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p()
+
+
+class DeviceBatch:
+    """The packed batch resident in HBM (inputs of every launch)."""
+
+    def __init__(self, hb, device=None):
+        self.device = _dev(device)
+        self.hb = hb
+        i = hb.info
+        self.info = i
+        up = lambda a: _up(a, self.device)  # noqa: E731
+        self.rd_pos, self.rd_op, self.rd_base = up(hb.rd_pos), up(hb.rd_op), up(hb.rd_base)
+        self.ops, self.bases = up(hb.ops), up(hb.bases)
+        self.items, self.extras, self.blocks = up(hb.items.reshape(-1)), up(hb.extras), up(hb.blocks.reshape(-1))
+        self.ins_key, self.ins_off, self.ins_bases = up(hb.ins_key), up(hb.ins_off), up(hb.ins_bases)
+
+    def nbytes(self):
+        return sum(t.numel() * t.element_size() for t in (
+            self.rd_pos, self.rd_op, self.rd_base, self.ops, self.bases, self.items, self.extras, self.blocks,
+            self.ins_key, self.ins_off, self.ins_bases))
+
+
+class Workspace:
+    """All scratch + output buffers for one (batch, thresholds, fill) configuration."""
+
+    def __init__(self, db: DeviceBatch, thresholds, min_depth=1, fill=b"-"):
+        dev = db.device
+        i = db.info
+        self.db = db
+        self.T = len(thresholds)
+        sz = L.WsSizes()
+        L.check(lib.s2c_workspace_sizes(C.byref(i), self.T, C.byref(sz)))
+        self.sizes = sz
+        u8 = lambda n: torch.empty(max(int(n), 16), dtype=torch.uint8, device=dev)  # noqa: E731
+        self.thr = torch.tensor([float(t) for t in thresholds], dtype=torch.float64, device=dev)
+        fill = bytes(fill)
+        self.fill_bytes = fill
+        self.fill = torch.tensor(list(fill) or [0], dtype=torch.uint8, device=dev)
+        self.counts = u8(sz.counts)
+        self.ins_table = u8(sz.ins_table)
+        self.ins_cols = u8(sz.ins_cols)
+        self.ins_cnt = u8(sz.ins_cnt)
+        self.ins_chr = u8(sz.ins_chr)
+        self.ins_bits = u8(sz.ins_bits)
+        self.scalars = u8(sz.scalars)
+        self.codes = u8(sz.codes)
+        self.blk_len = u8(sz.blk_len)
+        self.stats = u8(sz.stats)
+        # output upper bound: every position fill or char + every insertion base, per threshold
+        cap = self.T * (i.total_len * max(1, len(fill)) + i.n_ins_bases) + 16
+        self.out = u8(cap)
+        d = L.Dev()
+        d.rd_pos, d.rd_op, d.rd_base = _ptr(db.rd_pos), _ptr(db.rd_op), _ptr(db.rd_base)
+        d.ops, d.bases = _ptr(db.ops), _ptr(db.bases)
+        d.items, d.extras, d.blocks = _ptr(db.items), _ptr(db.extras), _ptr(db.blocks)
+        d.ins_key, d.ins_off, d.ins_bases = _ptr(db.ins_key), _ptr(db.ins_off), _ptr(db.ins_bases)
+        d.n_reads, d.n_items, d.n_blocks = i.n_reads, i.n_items, i.n_blocks
+        d.n_ins, d.n_ins_bases, d.padded_len = i.n_ins, i.n_ins_bases, i.padded_len
+        d.tile_max, d.n_refs = i.tile_max, i.n_refs
+        d.thresholds, d.n_thr = _ptr(self.thr), self.T
+        d.min_depth = int(max(min(min_depth, 2**31 - 1), -2**31))
+        d.fill_len, d.fill_nondash = len(fill), sum(1 for c in fill if c != ord("-"))
+        d.fill = _ptr(self.fill)
+        d.counts, d.ins_table, d.ins_cap = _ptr(self.counts), _ptr(self.ins_table), sz.ins_cap
+        d.ins_cols, d.ins_cnt, d.ins_chr = _ptr(self.ins_cols), _ptr(self.ins_cnt), _ptr(self.ins_chr)
+        d.ins_bits, d.scalars = _ptr(self.ins_bits), _ptr(self.scalars)
+        d.codes, d.blk_len = _ptr(self.codes), _ptr(self.blk_len)
+        d.stats, d.out, d.out_cap = _ptr(self.stats), _ptr(self.out), cap
+        self.dev = d
+
+    def stream_handle(self):
+        return C.c_void_p(torch.cuda.current_stream(self.db.device).cuda_stream)
+
+    # ---- the four stages (each one C-ABI call; all asynchronous on the current stream)
+    def pileup(self):
+        L.check(lib.s2c_pileup(C.byref(self.dev), self.stream_handle()))
+
+    def insertions(self):
+        L.check(lib.s2c_insertions(C.byref(self.dev), self.stream_handle()))
+
+    def consensus(self):
+        L.check(lib.s2c_consensus(C.byref(self.dev), self.stream_handle()))
+
+    def assemble(self):
+        L.check(lib.s2c_assemble(C.byref(self.dev), self.stream_handle()))
+
+    def run(self):
+        """pileup → insertions → consensus → assembly (no host sync)."""
+        L.check(lib.s2c_run(C.byref(self.dev), self.stream_handle()))
+
+    # ---- results
+    def counts_host(self):
+        """counts[6][padded_len] as numpy u32 (for parity tests)."""
+        Lp = self.db.info.padded_len
+        return self.counts[: 6 * Lp * 4].view(torch.int32).cpu().numpy().view(np.uint32).reshape(6, Lp)
+
+    def fetch(self):
+        """Synchronise and copy results: (stats[R,T,4] u64, blk_off[T*nb+1] u64, out bytes)."""
+        torch.cuda.synchronize(self.db.device)
+        i = self.db.info
+        R, T, nb = i.n_refs, self.T, i.n_blocks
+        stats = self.stats[: R * T * 32].view(torch.int64).cpu().numpy().view(np.uint64).reshape(R, T, 4)
+        offs = self.blk_len[: (T * nb + 1) * 8].view(torch.int64).cpu().numpy().view(np.uint64)
+        total = int(offs[-1])
+        out = self.out[:total].cpu().numpy().tobytes()
+        return stats, offs, out

@@ -1,0 +1,146 @@
+"""CPU tier: libs2c.so loads and exports the C-ABI; the host parser + packed batch + work
+plan, run through a kernel-shaped CPU model (tests/batch_model.py), reproduce the
+reference's golden outputs; parsecigar mirror; generator determinism."""
+import hashlib
+import os
+import random
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+import batch_model as bm
+import golden_io
+import s2c_oracle as o
+from sam2consensus_amd import _lib, batch, configs, records
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CASES = golden_io.cases()
+
+
+def test_library_exports_every_declared_symbol():
+    header = open(os.path.join(ROOT, "include", "s2c.h")).read()
+    import re
+    declared = set(re.findall(r"\b(s2c_[a-z_0-9]+)\s*\(", header))
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert declared <= exported, declared - exported
+    assert declared == set(_lib.EXPORTS)
+    assert _lib.lib.s2c_abi_version() == 1
+
+
+def _model_case(sam, args):
+    opt = o.parse_argv(["-i", "in.sam"] + list(args))
+    try:
+        hb = batch.parse_text(sam, opt.maxdel_active, 150)
+        bm.check_plan(hb)
+        stats, offs, out = bm.model_pipeline(hb, opt.thresholds, opt.min_depth, opt.fill.encode("latin-1"))
+        fastas = records.build_records(hb, opt.thresholds, opt.prefix, stats, offs, out)
+        return "ok", {n + "__" + opt.prefix + ".fasta": records.render(r, opt.n).decode("latin-1")
+                      for n, r in fastas.items()}
+    except (KeyError, IndexError, ValueError, ZeroDivisionError, OverflowError) as e:
+        return type(e).__name__, {}
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_packed_batch_model_matches_reference(case):
+    status, files = _model_case(case["sam"], case["args"])
+    assert status == case["status"]
+    assert files == case["files"]
+
+
+def test_parsecigar_mirror_matches_oracle():
+    rng = random.Random(3)
+    for _ in range(3000):
+        cig = "".join("%d%s" % (rng.randint(0, 7), rng.choice("MIDNSHPX=?")) for _ in range(rng.randint(0, 5)))
+        seq = "".join(rng.choice("ACGTN-") for _ in range(rng.randint(0, 20)))
+        pos = rng.randint(-3, 30)
+        assert batch.parsecigar(cig, seq, pos) == o.parsecigar(cig, seq, pos), (cig, seq, pos)
+
+
+def test_plan_covers_every_position_c2_scaled():
+    hb = configs.synth_batch("c2", scale=0.05)
+    bm.check_plan(hb)
+    assert hb.info.n_ins > 0
+    # the batch reproduces the oracle's counts exactly (kernel-shaped walk of items)
+    counts = bm.model_counts(hb)
+    sp = configs.spec("c2", scale=0.05)
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "c2s.sam")
+        import ctypes as C
+        n = C.c_int64()
+        _lib.check(_lib.lib.s2c_synth_write(C.byref(sp), p.encode(), C.byref(n)))
+        text = open(p, "rb").read().decode("latin-1")
+    lines = o._lines(text)
+    refs = o.read_header(lines)
+    ocounts, _ = o.pileup(lines, refs, o.parse_argv(["-i", "x"] + configs.cli_args("c2")))
+    for r, name in enumerate(hb.names):
+        off, L = int(hb.ref_off[r]), int(hb.ref_len[r])
+        want = np.array(ocounts[name], dtype=np.int64).T
+        assert (counts[:, off:off + L] == want).all()
+    assert int(counts.sum()) == hb.info.aligned_bases  # no maxdel drops in c2
+
+
+def test_long_reads_and_wrap_pieces():
+    # spans > LONG_SPAN use per-tile extras; POS=0 wraps (:212)
+    sam = "@SQ\tSN:g\tLN:5000\n"
+    sam += "r\t0\tg\t1\t60\t10M3000N10M\t*\t0\t0\t%s\t*\n" % ("A" * 20)
+    sam += "r\t0\tg\t0\t60\t5M\t*\t0\t0\tCCCCC\t*\n"
+    for s in range(1, 4900, 7):
+        sam += "r\t0\tg\t%d\t60\t100M\t*\t0\t0\t%s\t*\n" % (s, "G" * 100)
+    hb = batch.parse_text(sam, True, 150)
+    assert hb.info.n_long == 1 and hb.info.n_extras >= 2
+    bm.check_plan(hb)
+    opt = o.parse_argv(["-i", "in.sam", "-d", "1"])
+    hb2 = batch.parse_text(sam, False, 150)
+    stats, offs, out = bm.model_pipeline(hb2, opt.thresholds, 1, b"-")
+    fastas = records.build_records(hb2, opt.thresholds, "in", stats, offs, out)
+    got = {n + "__in.fasta": records.render(r, 0).decode() for n, r in fastas.items()}
+    assert got == o.run_case(sam, ["-d", "1"])["files"]
+
+
+def test_text_and_file_and_gzip_parse_agree():
+    sam = golden_io.load("kat")[0]["sam"]
+    with tempfile.TemporaryDirectory() as td:
+        import gzip
+        p1, p2 = os.path.join(td, "a.sam"), os.path.join(td, "a.sam.gz")
+        open(p1, "w").write(sam)
+        with gzip.open(p2, "wt") as fh:
+            fh.write(sam)
+        hbs = [batch.parse_text(sam), batch.parse_file(p1), batch.parse_file(p2)]
+    for h in hbs[1:]:
+        assert (h.rd_pos == hbs[0].rd_pos).all() and (h.bases == hbs[0].bases).all()
+        assert (h.ins_key == hbs[0].ins_key).all()
+
+
+def test_streaming_chunks_equal_whole():
+    sam = "".join(c["sam"] for c in golden_io.load("kat")[:1])
+    p = batch.Parser()
+    for i in range(0, len(sam), 7):
+        p.feed(sam[i:i + 7].encode())
+    a = p.finish()
+    b = batch.parse_text(sam)
+    assert (a.bases == b.bases).all() and (a.rd_op == b.rd_op).all()
+
+
+def test_generator_c2_is_pinned():
+    g = golden_io.load("configs")["c2"]
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "c2.sam")
+        n = configs.synth_write("c2", p)
+        h = hashlib.sha256()
+        with open(p, "rb") as fh:
+            for chunk in iter(lambda: fh.read(1 << 22), b""):
+                h.update(chunk)
+    assert n == g["n_reads"] == 1176549
+    assert h.hexdigest() == g["sam_sha256"]
+
+
+def test_c2_batch_stats():
+    hb = configs.synth_batch("c2")
+    i = hb.info
+    assert i.reads_mapped == 1176549 and i.n_refs == 353
+    assert 176_000_000 < i.aligned_bases < 177_000_000
+    assert i.n_items >= 1024 and i.tile_max <= 2048
+    bm.check_plan(hb)

@@ -1,0 +1,60 @@
+"""The oracle (oracle/s2c_oracle.py) is pinned to the reference's own outputs."""
+import random
+
+import pytest
+
+import golden_io
+import s2c_oracle as o
+
+CASES = golden_io.cases()
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_oracle_matches_reference(case):
+    r = o.run_case(case["sam"], case["args"])
+    assert r["status"] == case["status"]
+    assert r["files"] == case["files"]
+
+
+def test_amb_table_matches_reference_dict():
+    amb = golden_io.load("amb")                      # sam2consensus.py:317-329 as data
+    assert len(amb) == 62
+    for m in range(64):
+        key = o.mask_key(m)
+        assert o.AMB_TABLE[m] == amb.get(key), key
+    assert "ACGNT" not in amb and o.AMB_TABLE[0b111110] is None
+
+
+def test_closed_form_vote_equals_group_sort():
+    rng = random.Random(7)
+    for _ in range(60000):
+        c = [rng.choice([0, 0, 1, 2, 3, 5, 8, rng.randint(0, 60)]) for _ in range(6)]
+        if rng.random() < 0.3:
+            c[0] = rng.randint(-40, 3)          # insertion columns: '-' may be <= 0 (:294)
+        cov = sum(c) + (rng.randint(0, 30) if rng.random() < 0.4 else 0)
+        t = rng.choice([0.1, 0.25, 0.29, 0.5, 0.66, 0.75, 0.9, 1.0, 1.5, 0.0, -0.2])
+        assert o.vote_groups(c, cov, t) == o.vote_closed(c, cov, t)
+
+
+def test_py2_round_and_str():
+    assert o.py2_str_float(o.py2_round(9 / 8.0)) == "1.13"      # Py3 round gives 1.12
+    assert o.py2_str_float(o.py2_round(1.0)) == "1.0"
+    assert o.py2_str_float(o.py2_round(100000.0)) == "100000.0"
+    assert o.py2_str_float(o.py2_round(2 / 3.0)) == "0.67"
+    assert o.py2_str_float(o.py2_round(-9 / 8.0)) == "-1.13"
+
+
+def test_configs_c1_oracle_matches_reference_content():
+    """The oracle reproduces the reference's C1 FASTA files byte for byte."""
+    import hashlib
+    from sam2consensus_amd import configs
+    import tempfile, os
+    g = golden_io.load("configs")["c1"]
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "c1.sam")
+        configs.synth_write("c1", p)
+        assert hashlib.sha256(open(p, "rb").read()).hexdigest() == g["sam_sha256"]
+        text = open(p, "rb").read().decode("latin-1")
+    r = o.run_case(text, g["args"], name="c1.sam")
+    assert r["status"] == "ok"
+    assert {k: v for k, v in r["files"].items()} == g["content"]
