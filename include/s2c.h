@@ -202,7 +202,9 @@ int s2c_workspace_sizes(const s2c_batch_info *info, int32_t n_thr, s2c_ws_sizes 
 
 /* (2) CIGAR expansion + pileup: items → counts[6][L]                    (:206-218) */
 int s2c_pileup(const s2c_dev *d, void *stream);
-/* (3) insertion hash table, column counts and insertion vote            (:221,:256-311,:370-385) */
+/* (3) insertion hash table, column counts and insertion vote            (:221,:256-311,:370-385)
+ *     Also zeroes stats/scalars/ins_bits for this run: call it after s2c_pileup and
+ *     before s2c_consensus (s2c_run does all four in order). */
 int s2c_insertions(const s2c_dev *d, void *stream);
 /* (4) per-position threshold vote, min-depth/fill, IUPAC, per-(ref,t) stats (:232-253,:344-397) */
 int s2c_consensus(const s2c_dev *d, void *stream);

@@ -107,6 +107,11 @@ EXPORTS = [
 
 
 def _load():
+    # One HIP runtime per process: torch (the device allocator) brings its own
+    # libamdhip64.so.7; loading it first makes libs2c.so's DT_NEEDED libamdhip64.so.7 bind
+    # to that same copy instead of mapping /opt/rocm's as a second runtime (which then
+    # reports hipErrorNoDevice for our launches).
+    import torch  # noqa: F401
     if not os.path.exists(LIB_PATH):
         raise ImportError("libs2c.so not built (%s): run `make` or __graft_entry__.build()" % LIB_PATH)
     lib = C.CDLL(LIB_PATH)

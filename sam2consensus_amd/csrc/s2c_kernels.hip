@@ -518,6 +518,9 @@ extern "C" int s2c_insertions(const s2c_dev *d, void *stream) {
     rc = hip_check(hipMemsetAsync(d->scalars, 0, 64, s), "memset scalars");
     if (rc) return rc;
     rc = hip_check(hipMemsetAsync(d->ins_bits, 0, (size_t)(d->padded_len / 32 + 2) * 4, s), "memset ins_bits");
+    if (rc) return rc;
+    // stats are accumulated by the insertion vote (errors) and then by the consensus
+    rc = hip_check(hipMemsetAsync(d->stats, 0, (size_t)d->n_refs * d->n_thr * 32, s), "memset stats");
     if (rc || d->n_ins == 0) return rc;
     rc = hip_check(hipMemsetAsync(d->ins_table, 0, (size_t)d->ins_cap * 16, s), "memset ins_table");
     if (rc) return rc;
@@ -534,8 +537,7 @@ extern "C" int s2c_consensus(const s2c_dev *d, void *stream) {
     int rc = check_dev(d);
     if (rc) return rc;
     hipStream_t s = (hipStream_t)stream;
-    rc = hip_check(hipMemsetAsync(d->stats, 0, (size_t)d->n_refs * d->n_thr * 32, s), "memset stats");
-    if (rc || d->n_blocks == 0) return rc;
+    if (d->n_blocks == 0) return S2C_OK;
     k_consensus<<<(unsigned)d->n_blocks, WG, 0, s>>>(*d);
     return hip_check(hipGetLastError(), "k_consensus");
 }
