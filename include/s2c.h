@@ -105,8 +105,9 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
     const int64_t  *ref_off;   /* [n_refs] global coordinate of position 0 */
     const int64_t  *ref_cov_reads; /* [n_refs] pileup records per ref (0 ⇒ Σcov may be 0) */
     const uint32_t *rd_pos;    /* [n_reads]   global coordinate of seqout char 0 */
-    const uint32_t *rd_op;     /* [n_reads+1] op offset; bit31 of entry i = drop dashes (:210) */
-    const uint32_t *rd_base;   /* [n_reads]   word offset of the read's 4-bit bases */
+    const uint32_t *rd_op;     /* [n_reads+1] op offset (CSR) */
+    const uint32_t *rd_base;   /* [n_reads+1] word offset of the read's 4-bit bases (+ end sentinel) */
+    const uint32_t *rd_span;   /* [n_reads]   seqout length; bit31 = '-' not counted (maxdel rule :210) */
     const uint32_t *ops;       /* [n_ops]     (len << 1) | cls, cls 0 = M/=/X, 1 = D/N/P */
     const uint32_t *bases;     /* [n_base_words] 8 codes per word, low nibble first */
     const uint32_t *ins_key;   /* [n_ins]     global coordinate of the insertion key (:74) */
@@ -161,7 +162,7 @@ int s2c_synth_write(const s2c_synth_spec *spec, const char *path, int64_t *n_rea
  * ====================================================================================== */
 typedef struct {
     /* ---- packed batch (device copies of s2c_batch_arrays) ---- */
-    const uint32_t *rd_pos, *rd_op, *rd_base, *ops, *bases;
+    const uint32_t *rd_pos, *rd_op, *rd_base, *rd_span, *ops, *bases;
     const uint32_t *items, *extras, *blocks;
     const uint32_t *ins_key, *ins_off, *ins_bases;
     int64_t n_reads, n_items, n_blocks, n_ins, n_ins_bases, padded_len;

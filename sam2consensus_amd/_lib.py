@@ -56,7 +56,8 @@ _P32 = C.POINTER(C.c_uint32)
 
 class BatchArrays(C.Structure):
     _fields_ = [("ref_len", _P64), ("ref_off", _P64), ("ref_cov_reads", _P64),
-                ("rd_pos", _P32), ("rd_op", _P32), ("rd_base", _P32), ("ops", _P32), ("bases", _P32),
+                ("rd_pos", _P32), ("rd_op", _P32), ("rd_base", _P32), ("rd_span", _P32), ("ops", _P32),
+                ("bases", _P32),
                 ("ins_key", _P32), ("ins_off", _P32), ("ins_bases", _P32),
                 ("items", _P32), ("extras", _P32), ("blocks", _P32)]
 
@@ -75,7 +76,7 @@ _VP = C.c_void_p
 class Dev(C.Structure):
     """Mirror of ``s2c_dev`` (include/s2c.h)."""
     _fields_ = [
-        ("rd_pos", _VP), ("rd_op", _VP), ("rd_base", _VP), ("ops", _VP), ("bases", _VP),
+        ("rd_pos", _VP), ("rd_op", _VP), ("rd_base", _VP), ("rd_span", _VP), ("ops", _VP), ("bases", _VP),
         ("items", _VP), ("extras", _VP), ("blocks", _VP),
         ("ins_key", _VP), ("ins_off", _VP), ("ins_bases", _VP),
         ("n_reads", C.c_int64), ("n_items", C.c_int64), ("n_blocks", C.c_int64), ("n_ins", C.c_int64),

@@ -69,7 +69,8 @@ class HostBatch:
         self.ref_reads = _view(a.ref_cov_reads, i.n_refs, np.int64)
         self.rd_pos = _view(a.rd_pos, i.n_reads, np.uint32)
         self.rd_op = _view(a.rd_op, i.n_reads + 1, np.uint32)
-        self.rd_base = _view(a.rd_base, i.n_reads, np.uint32)
+        self.rd_base = _view(a.rd_base, i.n_reads + 1, np.uint32)
+        self.rd_span = _view(a.rd_span, i.n_reads, np.uint32)
         self.ops = _view(a.ops, i.n_ops, np.uint32)
         self.bases = _view(a.bases, i.n_base_words, np.uint32)
         self.ins_key = _view(a.ins_key, i.n_ins, np.uint32)

@@ -172,7 +172,7 @@ struct s2c_batch {
     s2c_batch_info info{};
     std::vector<std::string> names;
     std::vector<int64_t> ref_len, ref_off, ref_reads;
-    std::vector<uint32_t> rd_pos, rd_op, rd_base, ops, bases;
+    std::vector<uint32_t> rd_pos, rd_op, rd_base, rd_span, ops, bases;
     std::vector<uint32_t> ins_key, ins_off, ins_bases;
     std::vector<uint32_t> items, extras, blocks;
 };
@@ -493,6 +493,7 @@ namespace {
 constexpr int64_t TP_MIN = 256, TP_MAX = 2048;      // pileup tile bounds (positions)
 constexpr double E_TARGET = 131072.0;                // aligned bases per pileup work item
 constexpr int64_t LONG_SPAN = 1024;                  // longer pieces go through per-tile extras
+constexpr uint64_t MAX_SHORT_OPS = 64;               // … and so do pieces with more op words
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline int64_t align_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }
 }  // namespace
@@ -555,7 +556,7 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
     for (int64_t i = 0; i < NP; i++) {
         gstart[i] = (uint64_t)(b->ref_off[p->p_ref[i]] + p->p_pos[i]);
         b->ref_reads[p->p_ref[i]]++;
-        is_long[i] = p->p_span[i] > LONG_SPAN;
+        is_long[i] = p->p_span[i] > LONG_SPAN || p->p_op[i + 1] - p->p_op[i] > MAX_SHORT_OPS;
         if (is_long[i]) n_long++;
         else bucket[gstart[i] / S2C_POS_ALIGN + 1]++;
     }
@@ -574,7 +575,8 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
     I.n_long = n_long;
     b->rd_pos.resize(NP);
     b->rd_op.resize(NP + 1);
-    b->rd_base.resize(NP);
+    b->rd_span.resize(NP);
+    b->rd_base.resize(NP + 1);
     uint64_t nops = 0, nwords = 0;
     for (int64_t i = 0; i < NP; i++) {
         nops += p->p_op[i + 1] - p->p_op[i];
@@ -592,7 +594,8 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
         for (int64_t j = 0; j < NP; j++) {
             int64_t i = order[j];
             b->rd_pos[j] = (uint32_t)gstart[i];
-            b->rd_op[j] = (uint32_t)oo | (p->p_drop[i] ? 0x80000000u : 0u);
+            b->rd_op[j] = (uint32_t)oo;
+            b->rd_span[j] = p->p_span[i] | (p->p_drop[i] ? 0x80000000u : 0u);
             b->rd_base[j] = (uint32_t)ww;
             uint64_t no = p->p_op[i + 1] - p->p_op[i], nw = p->p_base[i + 1] - p->p_base[i];
             memcpy(&b->ops[oo], &p->ops[p->p_op[i]], no * 4);
@@ -602,6 +605,7 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
             if (j < NS) gend[j] = gstart[i] + p->p_span[i];
         }
         b->rd_op[NP] = (uint32_t)oo;
+        b->rd_base[NP] = (uint32_t)ww;    // sentinel: words of read j = [rd_base[j], rd_base[j+1])
     }
     I.n_ops = (int64_t)nops;
     I.n_base_words = (int64_t)nwords;
@@ -719,6 +723,7 @@ extern "C" int s2c_batch_arrays_get(const s2c_batch *b, s2c_batch_arrays *o) {
     o->rd_pos = b->rd_pos.data();
     o->rd_op = b->rd_op.data();
     o->rd_base = b->rd_base.data();
+    o->rd_span = b->rd_span.data();
     o->ops = b->ops.data();
     o->bases = b->bases.data();
     o->ins_key = b->ins_key.data();

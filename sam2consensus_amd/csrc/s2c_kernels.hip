@@ -128,60 +128,189 @@ __global__ void k_zero_tiles(const s2c_dev d) {
         for (uint32_t i = threadIdx.x; i < n; i += WG) d.counts[(size_t)c * d.padded_len + a + i] = 0;
 }
 
-__device__ __forceinline__ void pileup_read(const s2c_dev &d, uint32_t *lds, uint32_t tp, uint32_t a,
-                                            uint32_t b, uint32_t r, uint32_t lane) {
-    const uint32_t s = uni(d.rd_pos[r]);
-    const uint32_t w0 = uni(d.rd_op[r]);
-    const uint32_t o1 = uni(d.rd_op[r + 1]) & 0x7FFFFFFFu;
-    const bool drop = (w0 >> 31) != 0;
-    const uint32_t wb = uni(d.rd_base[r]);
-    if (s >= b) return;
-    const uint32_t kwin0 = a > s ? a - s : 0;  // seqout window inside the tile
-    const uint32_t kwin1 = b - s;
-    const uint32_t *__restrict__ bw = d.bases + wb;
-    uint32_t k = 0, q = 0;
-    for (uint32_t o = w0 & 0x7FFFFFFFu; o < o1 && k < kwin1; o++) {
-        const uint32_t w = uni(d.ops[o]);
-        const uint32_t len = w >> 1, cls = w & 1u;
-        const uint32_t ka = k > kwin0 ? k : kwin0;
-        const uint32_t kb = (k + len) < kwin1 ? (k + len) : kwin1;
-        if (cls == 0) {
-            for (uint32_t j = ka + lane; j < kb; j += 64) {
-                const uint32_t qi = q + (j - k);
-                const uint32_t code = (bw[qi >> 3] >> ((qi & 7) * 4)) & 15u;
-                if (!(drop && code == 0)) atomicAdd(&lds[code * tp + (s + j - a)], 1u);
+// Staged-chunk limits.  The host classifies a piece as "long" (per-tile extras, read
+// straight from HBM) when its span > 1024 or it has > 64 op words, so every short read
+// fits a chunk (≤ 129 base words, ≤ 64 ops).
+constexpr int CH_READS = WG;      // reads per chunk (< 1023: a 10-bit field never overflows)
+constexpr int CH_WORDS = 4096;    // 16 KiB of packed bases per chunk
+constexpr int CH_OPS = 1024;      // op words per chunk
+constexpr int MAX_WIN = 32;       // 64-position windows per tile (tile ≤ 2048 positions)
+
+struct __attribute__((aligned(16))) ChunkLds {
+    uint4 meta[CH_READS];         // x: start - a (signed), y: span | drop<<31,
+                                  // z: op offset | nops<<16 | single-M<<31, w: base word offset
+    uint32_t ops[CH_OPS];
+    uint32_t bases[CH_WORDS];
+    uint32_t win_lo[MAX_WIN], win_hi[MAX_WIN];
+    uint32_t tot_words, tot_ops;
+};
+
+// code of seqout index j (lane-varying) of a read whose ops/bases sit at (ops, bases)
+__device__ __forceinline__ uint32_t seqout_code(const uint32_t *ops, uint32_t nops, const uint32_t *bases, int j,
+                                                bool mine) {
+    uint32_t code = 15;
+    int k = 0, q = 0;
+    for (uint32_t o = 0; o < nops; o++) {
+        const uint32_t w = uni(ops[o]);
+        const int len = (int)(w >> 1);
+        const bool m = (w & 1u) == 0;
+        if (mine && (unsigned)(j - k) < (unsigned)len) {
+            if (m) {
+                const uint32_t qi = (uint32_t)(q + j - k);
+                code = (bases[qi >> 3] >> ((qi & 7) * 4)) & 15u;
+            } else {
+                code = 0;
             }
-            q += len;
-        } else if (!drop) {
-            for (uint32_t j = ka + lane; j < kb; j += 64) atomicAdd(&lds[s + j - a], 1u);
         }
         k += len;
+        q += m ? len : 0;
     }
+    return code;
 }
 
+// One workgroup per work item = (tile [a,b) of one reference, read range [lo,hi) + long-read
+// extras).  Position-major: lane ℓ of a wave owns tile position 64·w + ℓ of each of its
+// windows and keeps its six counts in registers — a u64 of 10-bit fields per window
+// (+1 << 10·code per covering read, no atomics), folded into u32 counts after every chunk.
+// Reads are staged through LDS in chunks of ≤256 (coalesced global loads of their
+// metadata, op words and packed bases), so a read costs no HBM round trip when its
+// windows are visited.  Only windows inside the tile are visited: a read straddling a
+// tile edge costs one extra window visit, never an extra count.  Tiles holding the whole
+// depth store counts with plain coalesced stores; chunked (ultra-deep) tiles add them.
+template <int WPW>
 __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    __shared__ ChunkLds S;
     const uint32_t *it = d.items + (size_t)blockIdx.x * S2C_ITEM_WORDS;
     const uint32_t a = uni(it[0]), b = uni(it[1]), lo = uni(it[2]), hi = uni(it[3]);
     const uint32_t xlo = uni(it[4]), xhi = uni(it[5]), flags = uni(it[6]);
-    const uint32_t tp = (uint32_t)d.tile_max;
-    const uint32_t n = b - a;
-    for (uint32_t c = 0; c < NSYM; c++)
-        for (uint32_t i = threadIdx.x; i < n; i += WG) lds[c * tp + i] = 0;
-    __syncthreads();
-    const uint32_t wave = uni(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    for (uint32_t r = lo + wave; r < hi; r += WG / 64) pileup_read(d, lds, tp, a, b, r, lane);
-    for (uint32_t x = xlo + wave; x < xhi; x += WG / 64) pileup_read(d, lds, tp, a, b, uni(d.extras[x]), lane);
-    __syncthreads();
-    if (flags & 1u) {
-        for (uint32_t c = 0; c < NSYM; c++)
-            for (uint32_t i = threadIdx.x; i < n; i += WG) {
-                const uint32_t v = lds[c * tp + i];
-                if (v) atomicAdd(&d.counts[(size_t)c * d.padded_len + a + i], v);
+    const int n = (int)(b - a), nw = (n + 63) >> 6;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const int wbase = (int)uni(tid >> 6) * WPW;
+    uint64_t acc[WPW];
+    uint32_t cnt[WPW][NSYM];
+#pragma unroll
+    for (int wi = 0; wi < WPW; wi++) {
+        acc[wi] = 0;
+#pragma unroll
+        for (uint32_t c = 0; c < NSYM; c++) cnt[wi][c] = 0;
+    }
+    auto fold = [&]() {
+#pragma unroll
+        for (int wi = 0; wi < WPW; wi++) {
+#pragma unroll
+            for (uint32_t c = 0; c < NSYM; c++) cnt[wi][c] += (uint32_t)(acc[wi] >> (10 * c)) & 1023u;
+            acc[wi] = 0;
+        }
+    };
+    for (uint32_t r0 = lo; r0 < hi;) {
+        // ---- stage one chunk: metadata, per-window read ranges, ops, bases ----
+        if (tid < MAX_WIN) { S.win_lo[tid] = 0xFFFFFFFFu; S.win_hi[tid] = 0; }
+        const uint32_t bw0 = uni(d.rd_base[r0]), op0 = uni(d.rd_op[r0]);
+        const uint32_t rr = r0 + tid;
+        const bool in = rr < hi;
+        uint32_t bend = 0, oend = 0;
+        if (in) { bend = d.rd_base[rr + 1]; oend = d.rd_op[rr + 1]; }
+        const bool ok = in && bend - bw0 <= (uint32_t)CH_WORDS && oend - op0 <= (uint32_t)CH_OPS;
+        const uint32_t nr = (uint32_t)__syncthreads_count(ok);
+        if (tid < nr) {
+            const uint32_t sp = d.rd_span[rr], o = d.rd_op[rr], bb = d.rd_base[rr];
+            const int s_rel = (int)(d.rd_pos[rr] - a);
+            const uint32_t nops = oend - o;
+            const bool single = nops == 1 && (d.ops[o] & 1u) == 0;
+            S.meta[tid] = make_uint4((uint32_t)s_rel, sp, (o - op0) | (nops << 16) | (single ? 0x80000000u : 0u),
+                                     bb - bw0);
+            const int e = s_rel + (int)(sp & 0x7FFFFFFFu);
+            if (e > 0 && s_rel < n) {
+                const int wf = (s_rel > 0 ? s_rel : 0) >> 6, wl = ((e < n ? e : n) - 1) >> 6;
+                for (int i = wf; i <= wl; i++) { atomicMin(&S.win_lo[i], tid); atomicMax(&S.win_hi[i], tid + 1); }
             }
-    } else {
-        for (uint32_t c = 0; c < NSYM; c++)
-            for (uint32_t i = threadIdx.x; i < n; i += WG) d.counts[(size_t)c * d.padded_len + a + i] = lds[c * tp + i];
+            if (tid == nr - 1) { S.tot_words = bend - bw0; S.tot_ops = oend - op0; }
+        }
+        __syncthreads();
+        const uint32_t nwd = S.tot_words, nop = S.tot_ops;
+        for (uint32_t i = tid; i < nop; i += WG) S.ops[i] = d.ops[op0 + i];
+        {
+            const uint32_t *src = d.bases + bw0;
+            uint32_t i = tid;
+            for (; i + 3 * WG < nwd; i += 4 * WG) {
+                const uint32_t v0 = src[i], v1 = src[i + WG], v2 = src[i + 2 * WG], v3 = src[i + 3 * WG];
+                S.bases[i] = v0; S.bases[i + WG] = v1; S.bases[i + 2 * WG] = v2; S.bases[i + 3 * WG] = v3;
+            }
+            for (; i < nwd; i += WG) S.bases[i] = src[i];
+        }
+        __syncthreads();
+        // ---- count: every read overlapping one of this wave's windows ----
+        if (wbase < nw) {
+            uint32_t rlo = 0xFFFFFFFFu, rhi = 0;
+#pragma unroll
+            for (int wi = 0; wi < WPW; wi++)
+                if (wbase + wi < nw) {
+                    rlo = min(rlo, S.win_lo[wbase + wi]);
+                    rhi = max(rhi, S.win_hi[wbase + wi]);
+                }
+            rlo = uni(rlo);
+            rhi = uni(rhi);
+            for (uint32_t t = rlo; t < rhi; t++) {
+                const uint4 m = S.meta[t];
+                const int s_rel = (int)uni(m.x);
+                const uint32_t sp = uni(m.y), oo = uni(m.z), bo = uni(m.w);
+                const int span = (int)(sp & 0x7FFFFFFFu);
+                const bool drop = (sp >> 31) != 0;
+#pragma unroll
+                for (int wi = 0; wi < WPW; wi++) {
+                    const int w0 = (wbase + wi) * 64;
+                    if (wbase + wi >= nw || s_rel >= w0 + 64 || s_rel + span <= w0) continue;
+                    const int j = w0 + (int)lane - s_rel;
+                    const bool mine = (unsigned)j < (unsigned)span && w0 + (int)lane < n;
+                    uint32_t code = 15;
+                    if (oo >> 31) {   // single M op: seqout index = query index
+                        if (mine) code = (S.bases[bo + ((uint32_t)j >> 3)] >> ((j & 7) * 4)) & 15u;
+                    } else {
+                        code = seqout_code(S.ops + (oo & 0xFFFFu), (oo >> 16) & 0x7FFFu, S.bases + bo, j, mine);
+                    }
+                    if (mine && !(drop && code == 0)) acc[wi] += 1ull << (10 * code);
+                }
+            }
+        }
+        fold();
+        __syncthreads();
+        r0 += nr;
+    }
+    // ---- long reads overlapping this tile (rare): metadata/ops/bases straight from HBM ----
+    for (uint32_t x = xlo; x < xhi; x++) {
+        const uint32_t r = uni(d.extras[x]);
+        const int s_rel = (int)(uni(d.rd_pos[r]) - a);
+        const uint32_t sp = uni(d.rd_span[r]);
+        const int span = (int)(sp & 0x7FFFFFFFu);
+        const bool drop = (sp >> 31) != 0;
+        const uint32_t o = uni(d.rd_op[r]), nops = uni(d.rd_op[r + 1]) - o;
+        const uint32_t *bw = d.bases + uni(d.rd_base[r]);
+#pragma unroll
+        for (int wi = 0; wi < WPW; wi++) {
+            const int w0 = (wbase + wi) * 64;
+            if (wbase + wi >= nw || s_rel >= w0 + 64 || s_rel + span <= w0) continue;
+            const int j = w0 + (int)lane - s_rel;
+            const bool mine = (unsigned)j < (unsigned)span && w0 + (int)lane < n;
+            const uint32_t code = seqout_code(d.ops + o, nops, bw, j, mine);
+            if (mine && !(drop && code == 0)) acc[wi] += 1ull << (10 * code);
+        }
+        if (((x - xlo) & 255u) == 255u) fold();
+    }
+    fold();
+    // ---- tile counts → HBM (symbol-major, coalesced) ----
+#pragma unroll
+    for (int wi = 0; wi < WPW; wi++) {
+        const int pl = (wbase + wi) * 64 + (int)lane;
+        if (wbase + wi >= nw || pl >= n) continue;
+#pragma unroll
+        for (uint32_t c = 0; c < NSYM; c++) {
+            uint32_t *dst = d.counts + (size_t)c * d.padded_len + a + pl;
+            if (flags & 1u) {
+                if (cnt[wi][c]) atomicAdd(dst, cnt[wi][c]);
+            } else {
+                *dst = cnt[wi][c];
+            }
+        }
     }
 }
 
@@ -491,7 +620,7 @@ extern "C" int s2c_workspace_sizes(const s2c_batch_info *info, int32_t n_thr, s2
 static int check_dev(const s2c_dev *d) {
     if (!d) return s2c_set_error(S2C_ERR_ARG, "s2c_dev is NULL");
     if (d->n_thr <= 0) return s2c_set_error(S2C_ERR_ARG, "no thresholds");
-    if (d->tile_max <= 0 || d->tile_max > 4096) return s2c_set_error(S2C_ERR_ARG, "tile_max out of range");
+    if (d->tile_max <= 0 || d->tile_max > 64 * MAX_WIN) return s2c_set_error(S2C_ERR_ARG, "tile_max out of range");
     if (d->padded_len <= 0 || d->padded_len >= ((int64_t)1 << 32)) return s2c_set_error(S2C_ERR_ARG, "bad padded_len");
     if (d->ins_cap <= 0 || (d->ins_cap & (d->ins_cap - 1))) return s2c_set_error(S2C_ERR_ARG, "ins_cap not pow2");
     if (d->n_items > 0 && (!d->items || !d->counts)) return s2c_set_error(S2C_ERR_ARG, "missing pileup buffers");
@@ -506,8 +635,11 @@ extern "C" int s2c_pileup(const s2c_dev *d, void *stream) {
     if (d->n_items == 0) return S2C_OK;
     hipStream_t s = (hipStream_t)stream;
     k_zero_tiles<<<(unsigned)d->n_items, WG, 0, s>>>(*d);
-    const size_t lds = (size_t)NSYM * d->tile_max * 4;
-    k_pileup<<<(unsigned)d->n_items, WG, lds, s>>>(*d);
+    const unsigned g = (unsigned)d->n_items;
+    if (d->tile_max <= 256) k_pileup<1><<<g, WG, 0, s>>>(*d);
+    else if (d->tile_max <= 512) k_pileup<2><<<g, WG, 0, s>>>(*d);
+    else if (d->tile_max <= 1024) k_pileup<4><<<g, WG, 0, s>>>(*d);
+    else k_pileup<8><<<g, WG, 0, s>>>(*d);
     return hip_check(hipGetLastError(), "k_pileup");
 }
 

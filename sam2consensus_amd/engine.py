@@ -51,13 +51,14 @@ class DeviceBatch:
         self.info = i
         up = lambda a: _up(a, self.device)  # noqa: E731
         self.rd_pos, self.rd_op, self.rd_base = up(hb.rd_pos), up(hb.rd_op), up(hb.rd_base)
+        self.rd_span = up(hb.rd_span)
         self.ops, self.bases = up(hb.ops), up(hb.bases)
         self.items, self.extras, self.blocks = up(hb.items.reshape(-1)), up(hb.extras), up(hb.blocks.reshape(-1))
         self.ins_key, self.ins_off, self.ins_bases = up(hb.ins_key), up(hb.ins_off), up(hb.ins_bases)
 
     def nbytes(self):
         return sum(t.numel() * t.element_size() for t in (
-            self.rd_pos, self.rd_op, self.rd_base, self.ops, self.bases, self.items, self.extras, self.blocks,
+            self.rd_pos, self.rd_op, self.rd_base, self.rd_span, self.ops, self.bases, self.items, self.extras, self.blocks,
             self.ins_key, self.ins_off, self.ins_bases))
 
 
@@ -92,6 +93,7 @@ class Workspace:
         self.out = u8(cap)
         d = L.Dev()
         d.rd_pos, d.rd_op, d.rd_base = _ptr(db.rd_pos), _ptr(db.rd_op), _ptr(db.rd_base)
+        d.rd_span = _ptr(db.rd_span)
         d.ops, d.bases = _ptr(db.ops), _ptr(db.bases)
         d.items, d.extras, d.blocks = _ptr(db.items), _ptr(db.extras), _ptr(db.blocks)
         d.ins_key, d.ins_off, d.ins_bases = _ptr(db.ins_key), _ptr(db.ins_off), _ptr(db.ins_bases)

@@ -27,9 +27,10 @@ def _amb():
 
 def read_codes(hb, r):
     """Expand read r: (start, drop, list of (cls, len), codes of M bases)."""
-    o0 = int(hb.rd_op[r]) & 0x7FFFFFFF
-    o1 = int(hb.rd_op[r + 1]) & 0x7FFFFFFF
-    drop = bool(int(hb.rd_op[r]) >> 31)
+    o0 = int(hb.rd_op[r])
+    o1 = int(hb.rd_op[r + 1])
+    drop = bool(int(hb.rd_span[r]) >> 31)
+    assert sum(int(w) >> 1 for w in hb.ops[o0:o1]) == int(hb.rd_span[r]) & 0x7FFFFFFF
     ops = [(int(w) & 1, int(w) >> 1) for w in hb.ops[o0:o1]]
     nm = sum(l for c, l in ops if c == 0)
     w0 = int(hb.rd_base[r])
