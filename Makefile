@@ -28,9 +28,11 @@ $(BUILD):
 	mkdir -p $(BUILD)
 
 # kernel resource usage (VGPR/SGPR/LDS/occupancy) and ISA for inspection
-isa: | $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -c $(SRC)/s2c_kernels.hip -o $(BUILD)/isa.o -save-temps=obj \
-	    -Rpass-analysis=kernel-resource-usage 2> $(BUILD)/resource_usage.txt
+ISA_DIR ?= /tmp/s2c_isa
+isa:
+	mkdir -p $(ISA_DIR)
+	$(HIPCC) $(HIPFLAGS) -c $(SRC)/s2c_kernels.hip -o $(ISA_DIR)/isa.o -save-temps=obj \
+	    -Rpass-analysis=kernel-resource-usage 2> $(ISA_DIR)/resource_usage.txt
 
 clean:
 	rm -rf $(BUILD) $(OUT)

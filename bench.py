@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """bench.py — BASELINE.json metric: aligned bases/s into consensus on MI355X.
 
-A step = one pass of the device hot path (pileup → insertions → consensus vote →
-FASTA-body assembly) over one synthetic batch already resident in
+A step = one pass of the device hot path (insertion table → pileup + fused vote →
+deep-tile vote → FASTA-body assembly) over one synthetic batch resident in
 HBM (host SAM parse and H2D excluded; parse time reported separately).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2]
@@ -36,12 +36,18 @@ WORKLOADS = {
 
 
 def b_alg(info, T):
-    """SURVEY.md §8(d) algorithmic bytes of one step and of the pileup kernel alone."""
+    """Algorithmic bytes of one step, and of the fused k_pileup launch.
+
+    step   = 0.5·Q + 16·N + 4·K + (48+T)·L + Σ_ins(8 + 0.5·len)   (SURVEY's formula, which
+             prices the count tensor as written once + read once)
+    k_pileup = 0.5·Q_M + 16·N + 4·K + T·L: packed bases, read records and op words in,
+             per-threshold consensus codes out.  The fused kernel keeps counts in registers,
+             so no count bytes are charged to it (deep tiles, none in c2, would add 24·L)."""
     Q, N, K, L = info.query_bases, info.reads_mapped, info.n_ops, info.total_len
     ins = 8 * info.n_ins + 0.5 * info.n_ins_bases
     step = 0.5 * Q + 16 * N + 4 * K + (48 + T) * L + ins
     q_m = Q - info.n_ins_bases
-    pileup = 0.5 * q_m + 16 * N + 4 * K + 24 * L     # bases+ops+read records in, counts out once
+    pileup = 0.5 * q_m + 16 * N + 4 * K + T * L
     return step, pileup
 
 
@@ -122,10 +128,10 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(K):
+        ws.insertions()
         ev[k][0].record()
         ws.pileup()
         ev[k][1].record()
-        ws.insertions()
         ws.consensus()
         ws.assemble()
     torch.cuda.synchronize(dev)
@@ -172,7 +178,7 @@ def main():
                        "parallelism": "one batch per GPU, sharded by reference (no collective on the data path)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic_from_profile(wl),
-                         "kernel": "k_pileup (+k_zero_tiles)", "kernel_ms": pileup_ms,
+                         "kernel": "k_pileup (counting + fused vote epilogue)", "kernel_ms": pileup_ms,
                          "alg_bytes_per_launch": pileup_bytes},
             "step_alg_bytes": step_bytes,
             "step_achieved_gbps": step_bytes / (ms * 1e-3) / 1e9,

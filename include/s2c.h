@@ -50,8 +50,7 @@ int s2c_layout(int64_t *out, int n);
 /* ---- constants shared with the kernels -------------------------------------------- */
 #define S2C_NSYM          6    /* symbols '-','A','C','G','N','T' — sorted() order (:367) */
 #define S2C_POS_ALIGN    64    /* each reference starts at a multiple of this global coordinate */
-#define S2C_VOTE_BLOCK 1024    /* positions per consensus/assembly block (never straddles a ref) */
-#define S2C_ITEM_WORDS    8    /* u32 words per pileup work item */
+#define S2C_ITEM_WORDS    8    /* u32 words per pileup work item {a, b, lo, hi, xlo, xhi, flags, tile} */
 #define S2C_BLOCK_WORDS   4    /* u32 words per consensus block */
 #define S2C_CODE_FILL     0    /* codes[] value for a fill position */
 #define S2C_CODE_ERR   0xFF    /* codes[] value where the vote hit a missing amb key (:367) */
@@ -96,8 +95,9 @@ typedef struct {
     int64_t n_ins_words;       /* u32 words of packed motif bases */
     int64_t n_items;           /* pileup work items */
     int64_t n_extras;          /* extra (long-read) references over all items */
-    int64_t n_blocks;          /* consensus blocks */
-    int64_t tile_max;          /* max positions of any pileup tile (LDS sizing) */
+    int64_t n_blocks;          /* tiles = consensus/assembly blocks (never straddle a ref) */
+    int64_t tile_max;          /* max positions of any tile (≤ 2048) */
+    int64_t n_deep;            /* tiles split over several work items (voted by k_consensus) */
 } s2c_batch_info;
 
 typedef struct {               /* host pointers into the batch (valid until s2c_batch_free) */
@@ -107,7 +107,8 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
     const uint32_t *rd_pos;    /* [n_reads]   global coordinate of seqout char 0 */
     const uint32_t *rd_op;     /* [n_reads+1] op offset (CSR) */
     const uint32_t *rd_base;   /* [n_reads+1] word offset of the read's 4-bit bases (+ end sentinel) */
-    const uint32_t *rd_span;   /* [n_reads]   seqout length; bit31 = '-' not counted (maxdel rule :210) */
+    const uint32_t *rd_span;   /* [n_reads]   seqout length (bits 0-29); bit30 = a single M op;
+                                  bit31 = '-' not counted (maxdel rule :210) */
     const uint32_t *ops;       /* [n_ops]     (len << 1) | cls, cls 0 = M/=/X, 1 = D/N/P */
     const uint32_t *bases;     /* [n_base_words] 8 codes per word, low nibble first */
     const uint32_t *ins_key;   /* [n_ins]     global coordinate of the insertion key (:74) */
@@ -115,7 +116,8 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
     const uint32_t *ins_bases; /* [n_ins_words] */
     const uint32_t *items;     /* [n_items][S2C_ITEM_WORDS] pileup work items */
     const uint32_t *extras;    /* [n_extras] read indices */
-    const uint32_t *blocks;    /* [n_blocks][S2C_BLOCK_WORDS] {g_begin, g_end, ref, first_block_of_ref} */
+    const uint32_t *blocks;    /* [n_blocks][S2C_BLOCK_WORDS] tiles {g_begin, g_end, ref, deep} */
+    const uint32_t *deep;      /* [n_deep] indices of deep tiles */
 } s2c_batch_arrays;
 
 int  s2c_batch_info_get(const s2c_batch *b, s2c_batch_info *out);
@@ -163,9 +165,9 @@ int s2c_synth_write(const s2c_synth_spec *spec, const char *path, int64_t *n_rea
 typedef struct {
     /* ---- packed batch (device copies of s2c_batch_arrays) ---- */
     const uint32_t *rd_pos, *rd_op, *rd_base, *rd_span, *ops, *bases;
-    const uint32_t *items, *extras, *blocks;
+    const uint32_t *items, *extras, *blocks, *deep;
     const uint32_t *ins_key, *ins_off, *ins_bases;
-    int64_t n_reads, n_items, n_blocks, n_ins, n_ins_bases, padded_len;
+    int64_t n_reads, n_items, n_blocks, n_deep, n_ins, n_ins_bases, padded_len;
     int32_t tile_max, n_refs;
 
     /* ---- options (:117-138) ---- */
@@ -177,7 +179,7 @@ typedef struct {
     const uint8_t *fill;       /* [fill_len] device copy of -f bytes */
 
     /* ---- workspace (caller allocates; sizes from s2c_workspace_sizes) ---- */
-    uint32_t *counts;          /* [6][padded_len] pileup counts (SoA by symbol) */
+    uint32_t *counts;          /* [6][padded_len] pileup counts of deep tiles (SoA by symbol) */
     uint32_t *ins_table;       /* [ins_cap][4] {key, maxlen, colbase, pad}; ins_cap pow2 */
     int64_t   ins_cap;
     uint32_t *ins_cols;        /* [n_ins_bases][6] insertion column counts */
@@ -192,6 +194,12 @@ typedef struct {
     uint64_t *stats;           /* [n_refs][T][4] {sumcov, len, nondash, vote_errors} (:352-397) */
     uint8_t  *out;             /* assembled consensus bytes, [t][block] order; size = blk_len[T*n_blocks] */
     int64_t   out_cap;
+
+    /* ---- diagnostics, 0 in the product: bit 1 skips counting, bit 2 skips base staging
+     *      (timing ablations, results wrong: scripts/ablate.py); bit 4 makes every tile
+     *      store its counts to `counts` instead of voting (counts parity tests) ---- */
+    int32_t   ablate;
+    int32_t   reserved;
 } s2c_dev;
 
 /* Sizes (bytes) of every workspace / output buffer for a batch and T thresholds. */
@@ -201,15 +209,17 @@ typedef struct {
 } s2c_ws_sizes;
 int s2c_workspace_sizes(const s2c_batch_info *info, int32_t n_thr, s2c_ws_sizes *out);
 
-/* (2) CIGAR expansion + pileup: items → counts[6][L]                    (:206-218) */
-int s2c_pileup(const s2c_dev *d, void *stream);
-/* (3) insertion hash table, column counts and insertion vote            (:221,:256-311,:370-385)
- *     Also zeroes stats/scalars/ins_bits for this run: call it after s2c_pileup and
- *     before s2c_consensus (s2c_run does all four in order). */
+/* Stage order (s2c_run): s2c_insertions → s2c_pileup → s2c_consensus → s2c_assemble.
+ * (3) zero per-run state; insertion hash table, longest motifs, column counts
+ *                                                                      (:221,:256-294) */
 int s2c_insertions(const s2c_dev *d, void *stream);
-/* (4) per-position threshold vote, min-depth/fill, IUPAC, per-(ref,t) stats (:232-253,:344-397) */
+/* (2) CIGAR expansion + pileup per tile; for tiles holding their whole depth also
+ * (4) the vote (all thresholds, IUPAC, min-depth/fill, insertion columns, stats)
+ *                                                (:206-218, :232-253, :290-311, :344-397) */
+int s2c_pileup(const s2c_dev *d, void *stream);
+/* (4) the vote for deep tiles (reads split over several work items)   (:232-253,:344-397) */
 int s2c_consensus(const s2c_dev *d, void *stream);
-/* device FASTA body assembly: block scan + byte scatter               (:350-389 string build) */
+/* device FASTA body assembly: tile scan + byte scatter                 (:350-389 string build) */
 int s2c_assemble(const s2c_dev *d, void *stream);
 /* all four, in order, on one stream (graph-capturable: no allocation, no sync) */
 int s2c_run(const s2c_dev *d, void *stream);

@@ -25,7 +25,6 @@ S2C_ERR_LIMIT = -13
 
 S2C_NSYM = 6
 S2C_POS_ALIGN = 64
-S2C_VOTE_BLOCK = 1024
 S2C_ITEM_WORDS = 8
 S2C_BLOCK_WORDS = 4
 S2C_CODE_FILL = 0
@@ -47,7 +46,7 @@ class BatchInfo(C.Structure):
     _fields_ = [(n, C.c_int64) for n in (
         "n_refs", "total_len", "padded_len", "header_lines", "lines_total", "reads_mapped",
         "aligned_bases", "query_bases", "n_reads", "n_long", "n_ops", "n_base_words", "n_ins",
-        "n_ins_bases", "n_ins_words", "n_items", "n_extras", "n_blocks", "tile_max")]
+        "n_ins_bases", "n_ins_words", "n_items", "n_extras", "n_blocks", "tile_max", "n_deep")]
 
 
 _P64 = C.POINTER(C.c_int64)
@@ -59,7 +58,7 @@ class BatchArrays(C.Structure):
                 ("rd_pos", _P32), ("rd_op", _P32), ("rd_base", _P32), ("rd_span", _P32), ("ops", _P32),
                 ("bases", _P32),
                 ("ins_key", _P32), ("ins_off", _P32), ("ins_bases", _P32),
-                ("items", _P32), ("extras", _P32), ("blocks", _P32)]
+                ("items", _P32), ("extras", _P32), ("blocks", _P32), ("deep", _P32)]
 
 
 class SynthSpec(C.Structure):
@@ -77,9 +76,10 @@ class Dev(C.Structure):
     """Mirror of ``s2c_dev`` (include/s2c.h)."""
     _fields_ = [
         ("rd_pos", _VP), ("rd_op", _VP), ("rd_base", _VP), ("rd_span", _VP), ("ops", _VP), ("bases", _VP),
-        ("items", _VP), ("extras", _VP), ("blocks", _VP),
+        ("items", _VP), ("extras", _VP), ("blocks", _VP), ("deep", _VP),
         ("ins_key", _VP), ("ins_off", _VP), ("ins_bases", _VP),
-        ("n_reads", C.c_int64), ("n_items", C.c_int64), ("n_blocks", C.c_int64), ("n_ins", C.c_int64),
+        ("n_reads", C.c_int64), ("n_items", C.c_int64), ("n_blocks", C.c_int64), ("n_deep", C.c_int64),
+        ("n_ins", C.c_int64),
         ("n_ins_bases", C.c_int64), ("padded_len", C.c_int64),
         ("tile_max", C.c_int32), ("n_refs", C.c_int32),
         ("thresholds", _VP), ("n_thr", C.c_int32), ("min_depth", C.c_int32),
@@ -87,7 +87,8 @@ class Dev(C.Structure):
         ("counts", _VP), ("ins_table", _VP), ("ins_cap", C.c_int64), ("ins_cols", _VP),
         ("ins_cnt", _VP), ("ins_chr", _VP), ("ins_bits", _VP), ("scalars", _VP),
         ("codes", _VP), ("blk_len", _VP),
-        ("stats", _VP), ("out", _VP), ("out_cap", C.c_int64)]
+        ("stats", _VP), ("out", _VP), ("out_cap", C.c_int64),
+        ("ablate", C.c_int32), ("reserved", C.c_int32)]
 
 
 class WsSizes(C.Structure):

@@ -79,6 +79,7 @@ class HostBatch:
         self.items = _view(a.items, i.n_items * L.S2C_ITEM_WORDS, np.uint32).reshape(-1, L.S2C_ITEM_WORDS)
         self.extras = _view(a.extras, i.n_extras, np.uint32)
         self.blocks = _view(a.blocks, i.n_blocks * L.S2C_BLOCK_WORDS, np.uint32).reshape(-1, L.S2C_BLOCK_WORDS)
+        self.deep = _view(a.deep, i.n_deep, np.uint32)
         self.names = [lib.s2c_batch_ref_name(self._b, k).decode("latin-1") for k in range(i.n_refs)]
         # per-ref block ranges (blocks are emitted ref by ref, in header order)
         nb = np.bincount(self.blocks[:, 2].astype(np.int64), minlength=i.n_refs) if i.n_blocks else \

@@ -174,7 +174,7 @@ struct s2c_batch {
     std::vector<int64_t> ref_len, ref_off, ref_reads;
     std::vector<uint32_t> rd_pos, rd_op, rd_base, rd_span, ops, bases;
     std::vector<uint32_t> ins_key, ins_off, ins_bases;
-    std::vector<uint32_t> items, extras, blocks;
+    std::vector<uint32_t> items, extras, blocks, deep;
 };
 
 static int perr(s2c_parser *p, int code, const std::string &msg) {
@@ -594,10 +594,12 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
         for (int64_t j = 0; j < NP; j++) {
             int64_t i = order[j];
             b->rd_pos[j] = (uint32_t)gstart[i];
+            const uint64_t no = p->p_op[i + 1] - p->p_op[i], nw = p->p_base[i + 1] - p->p_base[i];
             b->rd_op[j] = (uint32_t)oo;
-            b->rd_span[j] = p->p_span[i] | (p->p_drop[i] ? 0x80000000u : 0u);
+            // bit31: '-' not counted (maxdel); bit30: one M op, counted as is (fast path)
+            const bool simple = !p->p_drop[i] && no == 1 && (p->ops[p->p_op[i]] & 1u) == 0;
+            b->rd_span[j] = p->p_span[i] | (p->p_drop[i] ? 0x80000000u : 0u) | (simple ? 0x40000000u : 0u);
             b->rd_base[j] = (uint32_t)ww;
-            uint64_t no = p->p_op[i + 1] - p->p_op[i], nw = p->p_base[i + 1] - p->p_base[i];
             memcpy(&b->ops[oo], &p->ops[p->p_op[i]], no * 4);
             memcpy(&b->bases[ww], &p->words[p->p_base[i]], nw * 4);
             oo += no;
@@ -619,7 +621,7 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
     // ---- pileup work items ----
     std::vector<int64_t> ref_events(R, 0);
     for (int64_t i = 0; i < NP; i++) ref_events[p->p_ref[i]] += p->p_span[i];
-    struct Tile { int64_t a, b, lo, hi; double ev; };
+    struct Tile { int64_t a, b, lo, hi; double ev; int64_t ref; };
     std::vector<Tile> tiles;
     int64_t tile_max = S2C_POS_ALIGN;
     for (int64_t r = 0; r < R; r++) {
@@ -635,7 +637,7 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
             int64_t e = std::min(a + step, off + L);
             int64_t hi = bucket[std::min<int64_t>(align_up(e, S2C_POS_ALIGN) / S2C_POS_ALIGN, NB)];
             int64_t lo = std::upper_bound(pmax.begin(), pmax.begin() + hi, (uint64_t)a) - pmax.begin();
-            tiles.push_back({a, e, lo, hi, depth * (double)(e - a)});
+            tiles.push_back({a, e, lo, hi, depth * (double)(e - a), r});
             tile_max = std::max(tile_max, e - a);
         }
     }
@@ -651,6 +653,9 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
         for (size_t t = t0; t < tiles.size() && (uint64_t)tiles[t].a < e; t++)
             if ((uint64_t)tiles[t].b > s) tile_x[t].push_back((uint32_t)j);
     }
+    // Each tile is also the consensus/assembly block: a tile whose reads fit one work item
+    // is voted in the pileup kernel's epilogue (counts never reach HBM); a chunked
+    // ("deep") tile accumulates counts in HBM and is voted by k_consensus.
     for (size_t t = 0; t < tiles.size(); t++) {
         const Tile &T = tiles[t];
         int64_t nch = std::max<int64_t>(1, (int64_t)std::ceil(T.ev / (2.0 * E_TARGET)));
@@ -663,24 +668,17 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
             int64_t r0 = T.lo + nr * c / nch, r1 = T.lo + nr * (c + 1) / nch;
             uint32_t it[S2C_ITEM_WORDS] = {(uint32_t)T.a, (uint32_t)T.b, (uint32_t)r0, (uint32_t)r1,
                                            c == 0 ? x_lo : x_hi, x_hi,
-                                           (uint32_t)((nch > 1 ? 1u : 0u) | (c == 0 ? 2u : 0u)), 0};
+                                           (uint32_t)((nch > 1 ? 1u : 0u) | (c == 0 ? 2u : 0u)), (uint32_t)t};
             b->items.insert(b->items.end(), it, it + S2C_ITEM_WORDS);
         }
+        uint32_t blk[S2C_BLOCK_WORDS] = {(uint32_t)T.a, (uint32_t)T.b, (uint32_t)T.ref, nch > 1 ? 1u : 0u};
+        b->blocks.insert(b->blocks.end(), blk, blk + S2C_BLOCK_WORDS);
+        if (nch > 1) b->deep.push_back((uint32_t)t);
     }
     I.n_items = (int64_t)(b->items.size() / S2C_ITEM_WORDS);
     I.n_extras = (int64_t)b->extras.size();
-
-    // ---- consensus blocks (never straddle a ref) ----
-    for (int64_t r = 0; r < R; r++) {
-        const int64_t L = p->ref_len[r], off = b->ref_off[r];
-        uint32_t first = (uint32_t)(b->blocks.size() / S2C_BLOCK_WORDS);
-        for (int64_t a = off; a < off + L; a += S2C_VOTE_BLOCK) {
-            uint32_t blk[S2C_BLOCK_WORDS] = {(uint32_t)a, (uint32_t)std::min(a + S2C_VOTE_BLOCK, off + L),
-                                             (uint32_t)r, first};
-            b->blocks.insert(b->blocks.end(), blk, blk + S2C_BLOCK_WORDS);
-        }
-    }
     I.n_blocks = (int64_t)(b->blocks.size() / S2C_BLOCK_WORDS);
+    I.n_deep = (int64_t)b->deep.size();
 
     // ---- insertion events: keys in [0, LN) (negative keys are never emitted, :371) ----
     {
@@ -732,6 +730,7 @@ extern "C" int s2c_batch_arrays_get(const s2c_batch *b, s2c_batch_arrays *o) {
     o->items = b->items.data();
     o->extras = b->extras.data();
     o->blocks = b->blocks.data();
+    o->deep = b->deep.data();
     return S2C_OK;
 }
 

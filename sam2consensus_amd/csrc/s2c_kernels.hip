@@ -2,14 +2,19 @@
 //
 // The reference's hot path (sam2consensus.py) is a per-base Python dict increment
 // (:210-218), an insertion motif aggregation (:256-311) and a per-position threshold
-// vote (:232-253, :344-389).  Here it is four stream-ordered stages over the packed
-// batch built by s2c_host.cpp:
+// vote (:232-253, :344-389).  Here it is a stream-ordered chain over the packed batch
+// built by s2c_host.cpp, whose unit is the TILE (≤2048 positions of one reference):
 //
-//   k_zero_tiles / k_pileup   (2) CIGAR expansion + per-tile LDS histograms → counts[6][L]
-//   k_ins_*                   (3) insertion hash table, column counts, insertion vote
-//   k_consensus               (4) one pass per position for all thresholds: closed-form
-//                                 Geneious vote, IUPAC LUT, min-depth / fill, stats
-//   k_scan / k_assemble       device FASTA body assembly (block scan + byte scatter)
+//   k_prep                 zero per-run state (replaces memsets: one launch)
+//   k_ins_build/alloc/     (3) insertion hash table: key → slot, longest motif, column
+//   k_ins_scatter              base, per-column symbol counts (:262-287)
+//   k_pileup               (2) CIGAR expansion + position-major counting per tile, and
+//                          (4) for tiles holding their whole depth, the vote epilogue:
+//                          all thresholds, IUPAC, min-depth/fill, insertion columns,
+//                          per-(ref,t) stats — counts never reach HBM
+//   k_consensus            (4) the same epilogue for "deep" tiles whose reads were split
+//                          over several work items (counts summed in HBM)
+//   k_scan / k_assemble    device FASTA body assembly (tile scan + byte scatter)
 //
 // Everything is integer counting; the single floating-point operation is the
 // reference's `cov_nucs < t*coverage` (:362, :376), evaluated as
@@ -67,6 +72,20 @@ __device__ __forceinline__ uint32_t nibble(const uint32_t *__restrict__ w, uint6
     return (w[idx >> 3] >> ((idx & 7) * 4)) & 15u;
 }
 
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T *sh) {   // 256-thread workgroup sum, all threads get it
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const uint32_t w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[w] = v;
+    __syncthreads();
+    T r = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) r += sh[i];
+    return r;
+}
+
 // Closed form of the group-sort vote (proven equal to :241-251 +
 // :359-366 in tests/test_oracle.py): symbol i is taken iff c_i != 0 and the sum of the
 // counts strictly greater than c_i is < t·cov (fp64 product, exact integer compare).
@@ -104,54 +123,207 @@ __device__ __forceinline__ uint32_t ins_find(const uint32_t *__restrict__ tab, u
     return 0xFFFFFFFFu;
 }
 
-template <typename T>
-__device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
 
-// ======================================================================= (2) pileup
-// One workgroup per work item = (tile [a,b) of one reference, read range [lo,hi) +
-// long-read extras).  Counts for the tile accumulate in LDS as [6][tile] u32 (symbol-
-// major: consecutive lanes hit consecutive banks), each wave expanding one read's CIGAR
-// at a time — lane j handles seqout char j (+64…).  Only the seqout window inside the
-// tile is visited, so reads straddling tile edges cost no extra counting.  Tiles that
-// hold the whole depth write their histogram with plain coalesced stores (no HBM
-// atomics); tiles split into read chunks (ultra-deep, C4) add theirs atomically into a
-// range zeroed by k_zero_tiles.
-__global__ void k_zero_tiles(const s2c_dev d) {
-    const uint32_t *it = d.items + (size_t)blockIdx.x * S2C_ITEM_WORDS;
-    if ((it[6] & 3u) != 3u) return;  // atomic tile, first chunk
-    const uint32_t a = it[0], n = it[1] - it[0];
+// ======================================================================= per-run state
+// One launch zeroes everything a run accumulates into: per-(ref,t) stats, flags, the
+// insertion bitmap / hash table / column counts, and the count ranges of deep tiles.
+constexpr int PREP_BLOCKS = 512;
+__global__ __launch_bounds__(WG) void k_prep(const s2c_dev d) {
+    if (blockIdx.x < PREP_BLOCKS) {
+        const size_t i0 = (size_t)blockIdx.x * WG + threadIdx.x, step = (size_t)PREP_BLOCKS * WG;
+        const size_t n_stats = (size_t)d.n_refs * d.n_thr * 4, n_bits = (size_t)(d.padded_len / 32 + 2);
+        const size_t n_tab = d.n_ins ? (size_t)d.ins_cap * 4 : 0, n_cols = (size_t)d.n_ins_bases * NSYM;
+        for (size_t i = i0; i < n_stats; i += step) d.stats[i] = 0;
+        for (size_t i = i0; i < 16; i += step) d.scalars[i] = 0;
+        for (size_t i = i0; i < n_bits; i += step) d.ins_bits[i] = 0;
+        for (size_t i = i0; i < n_tab; i += step) d.ins_table[i] = 0;
+        for (size_t i = i0; i < n_cols; i += step) d.ins_cols[i] = 0;
+        return;
+    }
+    const uint32_t t = d.deep[blockIdx.x - PREP_BLOCKS];
+    const uint32_t a = d.blocks[(size_t)t * S2C_BLOCK_WORDS], n = d.blocks[(size_t)t * S2C_BLOCK_WORDS + 1] - a;
     for (uint32_t c = 0; c < NSYM; c++)
         for (uint32_t i = threadIdx.x; i < n; i += WG) d.counts[(size_t)c * d.padded_len + a + i] = 0;
 }
 
+// ======================================================================= (3) insertions
+// (:264-271) motif multiplicities and (:284-287) per-column sums are additive, so the
+// column counts are accumulated straight from the events: column c of key k gets +1 at
+// motif[c] for every event at k with len > c.  The hash table maps key → slot with the
+// longest motif (:278-281) and a column base; the columns are voted (with '-' =
+// cov[key] − Σ column, :294) in the tile epilogue that owns the key's position.
+__global__ void k_ins_build(const s2c_dev d) {
+    const uint32_t e = blockIdx.x * WG + threadIdx.x;
+    if (e >= d.n_ins) return;
+    const uint32_t key = d.ins_key[e];
+    const uint32_t len = d.ins_off[e + 1] - d.ins_off[e];
+    const uint32_t cap = (uint32_t)d.ins_cap;
+    uint32_t h = hash32(key) & (cap - 1);
+    for (uint32_t probe = 0; probe < cap; probe++) {
+        const uint32_t prev = atomicCAS(&d.ins_table[4 * h], 0u, key + 1);
+        if (prev == 0u || prev == key + 1) {
+            atomicMax(&d.ins_table[4 * h + 1], len);
+            break;
+        }
+        h = (h + 1) & (cap - 1);
+    }
+    atomicOr(&d.ins_bits[key >> 5], 1u << (key & 31));
+}
+
+// column bases: workgroup scan of the slots' longest motifs, one atomic per workgroup
+constexpr int ALLOC_WG = 1024;
+__global__ __launch_bounds__(ALLOC_WG) void k_ins_alloc(const s2c_dev d) {
+    __shared__ uint32_t wsum[ALLOC_WG / 64];
+    __shared__ uint32_t base;
+    const uint32_t s = blockIdx.x * ALLOC_WG + threadIdx.x;
+    const uint32_t need = (s < (uint32_t)d.ins_cap && d.ins_table[4 * s] != 0u) ? d.ins_table[4 * s + 1] : 0u;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = need;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int i = 0; i < ALLOC_WG / 64; i++) { const uint32_t v = wsum[i]; wsum[i] = tot; tot += v; }
+        base = tot ? atomicAdd(&d.scalars[0], tot) : 0u;
+    }
+    __syncthreads();
+    if (need) d.ins_table[4 * s + 2] = base + wsum[w] + x - need;
+}
+
+__global__ void k_ins_scatter(const s2c_dev d) {
+    const uint32_t e = blockIdx.x * WG + threadIdx.x;
+    if (e >= d.n_ins) return;
+    const uint32_t key = d.ins_key[e];
+    const uint32_t o0 = d.ins_off[e], o1 = d.ins_off[e + 1];
+    const uint32_t slot = ins_find(d.ins_table, (uint32_t)d.ins_cap, key);
+    if (slot == 0xFFFFFFFFu) return;
+    const uint32_t cb = d.ins_table[4 * slot + 2];
+    for (uint32_t c = 0; o0 + c < o1; c++)
+        atomicAdd(&d.ins_cols[(size_t)(cb + c) * NSYM + nibble(d.ins_bases, o0 + c)], 1u);
+}
+
+// ======================================================================= (4) vote epilogue
+// Per position: the closed-form vote for every threshold, the IUPAC char (or fill when
+// cov == 0 or cov < min_depth, :356-389), and — at a called position carrying an
+// insertion key — the insertion columns' votes with '-' = cov − Σ column (:290-311,
+// :370-385), emitted chars compacted per threshold.  Per tile and threshold: output
+// bytes (→ blk_len for the assembly scan) and the record stats sumcov / len / non-'-' /
+// vote errors (:357, :385, :395-396), added into stats[ref][t].
+template <int NP>
+__device__ __forceinline__ void vote_epilogue(const s2c_dev &d, uint32_t tile, uint32_t ref, uint32_t a,
+                                              const int (&pl)[NP], const uint32_t (&cnt)[NP][NSYM],
+                                              uint64_t *sh) {
+    const int T = d.n_thr;
+    uint64_t cov[NP];
+    int64_t gs[NP][NSYM];
+    bool called[NP];
+    uint32_t slot[NP];
+#pragma unroll
+    for (int k = 0; k < NP; k++) {
+        cov[k] = 0;
+#pragma unroll
+        for (uint32_t c = 0; c < NSYM; c++) cov[k] += cnt[k][c];
+        called[k] = pl[k] >= 0 && cov[k] > 0 && (int64_t)cov[k] >= (int64_t)d.min_depth;
+        greater_sums(cnt[k], gs[k]);
+        slot[k] = 0xFFFFFFFFu;
+        if (called[k]) {
+            const uint32_t p = a + (uint32_t)pl[k];
+            if (d.ins_bits[p >> 5] >> (p & 31) & 1u) slot[k] = ins_find(d.ins_table, (uint32_t)d.ins_cap, p);
+        }
+    }
+    for (int t = 0; t < T; t++) {
+        const double thr = d.thresholds[t];
+        uint64_t len = 0, nondash = 0, sumcov = 0, nerr = 0;
+#pragma unroll
+        for (int k = 0; k < NP; k++) {
+            if (pl[k] < 0) continue;
+            const uint32_t p = a + (uint32_t)pl[k];
+            uint8_t code = S2C_CODE_FILL;
+            if (called[k]) {
+                const double tc = thr * (double)cov[k];
+                const uint8_t ch = c_amb[vote_mask(cnt[k], gs[k], tc)];
+                nerr += ch == 0xFF;
+                code = ch;
+                uint32_t emitted = 0;
+                if (slot[k] != 0xFFFFFFFFu) {   // insertion columns after the base (:370-385)
+                    const uint32_t ml = d.ins_table[4 * slot[k] + 1], cb = d.ins_table[4 * slot[k] + 2];
+                    for (uint32_t c = 0; c < ml; c++) {
+                        const uint32_t *col = d.ins_cols + (size_t)(cb + c) * NSYM;
+                        int64_t v[NSYM];
+                        int64_t tot = 0;
+#pragma unroll
+                        for (uint32_t j = 0; j < NSYM; j++) { v[j] = col[j]; tot += v[j]; }
+                        v[0] = (int64_t)cov[k] - tot;   // :294 (the column's own '-' count is in the sum)
+                        int64_t g2[NSYM];
+                        greater_sums(v, g2);
+                        const uint8_t ic = c_amb[vote_mask(v, g2, tc)];
+                        if (ic == 0xFF) { nerr++; continue; }
+                        if (ic != '-') d.ins_chr[(size_t)t * d.n_ins_bases + cb + emitted++] = ic;
+                    }
+                    d.ins_cnt[(size_t)t * d.ins_cap + slot[k]] = emitted;
+                }
+                len += 1 + emitted;
+                nondash += (ch != '-') + emitted;
+                sumcov += cov[k] * (1 + emitted);
+            } else {
+                len += (uint32_t)d.fill_len;
+                nondash += (uint32_t)d.fill_nondash;
+                sumcov += cov[k];
+            }
+            d.codes[(size_t)t * d.padded_len + p] = code;
+        }
+        len = block_sum(len, sh);
+        nondash = block_sum(nondash, sh);
+        sumcov = block_sum(sumcov, sh);
+        nerr = block_sum(nerr, sh);
+        if (threadIdx.x == 0) {
+            uint64_t *st = d.stats + ((size_t)ref * T + t) * 4;
+            atomicAdd((unsigned long long *)&st[0], (unsigned long long)sumcov);
+            atomicAdd((unsigned long long *)&st[1], (unsigned long long)len);
+            atomicAdd((unsigned long long *)&st[2], (unsigned long long)nondash);
+            if (nerr) {
+                atomicAdd((unsigned long long *)&st[3], (unsigned long long)nerr);
+                atomicOr(&d.scalars[1], 1u);
+            }
+            d.blk_len[(size_t)t * d.n_blocks + tile] = len;
+        }
+    }
+}
+
+// ======================================================================= (2) pileup
 // Staged-chunk limits.  The host classifies a piece as "long" (per-tile extras, read
-// straight from HBM) when its span > 1024 or it has > 64 op words, so every short read
-// fits a chunk (≤ 129 base words, ≤ 64 ops).
-constexpr int CH_READS = WG;      // reads per chunk (< 1023: a 10-bit field never overflows)
-constexpr int CH_WORDS = 4096;    // 16 KiB of packed bases per chunk
-constexpr int CH_OPS = 1024;      // op words per chunk
+// straight from HBM) when its span > 1024 or it has > 64 op words, so a short read
+// needs ≤ 129 base words and ≤ 64 ops.  A chunk is ≤ CH reads; if its words or ops do not
+// fit the LDS buffers the chunk takes the HBM path for everything (never seen on the
+// BASELINE configs: 128 reads of 150 bp use ~2.4k words).
+constexpr int CH = 128;           // reads per chunk (< 1023: a 10-bit field never overflows)
+constexpr int CH_WORDS = 4096;    // 16 KiB of packed bases
+constexpr int CH_OPS = 512;       // op words
 constexpr int MAX_WIN = 32;       // 64-position windows per tile (tile ≤ 2048 positions)
+constexpr uint32_t SPAN_MASK = 0x3FFFFFFFu, SIMPLE = 0x40000000u, DROP = 0x80000000u;
 
 struct __attribute__((aligned(16))) ChunkLds {
-    uint4 meta[CH_READS];         // x: start - a (signed), y: span | drop<<31,
-                                  // z: op offset | nops<<16 | single-M<<31, w: base word offset
+    uint2 meta[CH];               // x: start - a (signed); y: nibble offset (16b) | span << 16 (11b) | !simple << 31
+    uint2 slow[CH];               // x: chunk read index, y: op offset (16b) | nops << 16; reads off the fast path
     uint32_t ops[CH_OPS];
     uint32_t bases[CH_WORDS];
     uint32_t win_lo[MAX_WIN], win_hi[MAX_WIN];
-    uint32_t tot_words, tot_ops;
+    uint32_t n_slow, tot_words, tot_ops, fits;
 };
 
-// code of seqout index j (lane-varying) of a read whose ops/bases sit at (ops, bases)
+// code of seqout index j (lane-varying) of a read whose ops/bases sit at (ops, bases);
+// 6 (a field nobody reads) where the lane has nothing to count.
 __device__ __forceinline__ uint32_t seqout_code(const uint32_t *ops, uint32_t nops, const uint32_t *bases, int j,
-                                                bool mine) {
-    uint32_t code = 15;
+                                                bool mine, bool drop) {
+    uint32_t code = 6;
     int k = 0, q = 0;
     for (uint32_t o = 0; o < nops; o++) {
-        const uint32_t w = uni(ops[o]);
+        const uint32_t w = ops[o];
         const int len = (int)(w >> 1);
         const bool m = (w & 1u) == 0;
         if (mine && (unsigned)(j - k) < (unsigned)len) {
@@ -165,18 +337,21 @@ __device__ __forceinline__ uint32_t seqout_code(const uint32_t *ops, uint32_t no
         k += len;
         q += m ? len : 0;
     }
-    return code;
+    return (drop && code == 0) ? 6u : code;
 }
 
 // One workgroup per work item = (tile [a,b) of one reference, read range [lo,hi) + long-read
 // extras).  Position-major: lane ℓ of a wave owns tile position 64·w + ℓ of each of its
-// windows and keeps its six counts in registers — a u64 of 10-bit fields per window
-// (+1 << 10·code per covering read, no atomics), folded into u32 counts after every chunk.
-// Reads are staged through LDS in chunks of ≤256 (coalesced global loads of their
-// metadata, op words and packed bases), so a read costs no HBM round trip when its
-// windows are visited.  Only windows inside the tile are visited: a read straddling a
-// tile edge costs one extra window visit, never an extra count.  Tiles holding the whole
-// depth store counts with plain coalesced stores; chunked (ultra-deep) tiles add them.
+// windows w and keeps its six counts in registers — a u64 of 10-bit fields per window,
+// += 1 << 10·code per covering read (no atomics), folded into u32 counts after every chunk.
+// Reads are staged through LDS in chunks of ≤128: metadata, op words and packed bases
+// arrive by coalesced loads, then each window sweeps the chunk's reads that overlap it.
+// Single-M-op reads (all but D/N/P reads and maxdel-dropped ones) take a branch-free
+// path: per (read, window) ~13 VALU + 2 LDS reads, 4 reads in flight per iteration;
+// the others take the op-walk path from a compacted list.  Only windows inside the tile
+// are visited, so a read straddling a tile edge costs a visit, never a count.  A tile
+// holding its whole depth runs the vote epilogue on its register counts; a deep tile
+// (reads split over items) adds its counts into HBM for k_consensus.
 template <int WPW>
 __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
     __shared__ ChunkLds S;
@@ -202,35 +377,34 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
             acc[wi] = 0;
         }
     };
-    for (uint32_t r0 = lo; r0 < hi;) {
-        // ---- stage one chunk: metadata, per-window read ranges, ops, bases ----
+    for (uint32_t r0 = lo; r0 < hi; r0 += CH) {
+        const uint32_t r1 = min(hi, r0 + CH);
+        // ---- stage: per-read metadata (one coalesced load per array), then ops/bases ----
         if (tid < MAX_WIN) { S.win_lo[tid] = 0xFFFFFFFFu; S.win_hi[tid] = 0; }
+        if (tid == 0) S.n_slow = 0;
         const uint32_t bw0 = uni(d.rd_base[r0]), op0 = uni(d.rd_op[r0]);
+        const uint32_t bw1 = uni(d.rd_base[r1]), op1 = uni(d.rd_op[r1]);
+        const bool fits = bw1 - bw0 <= (uint32_t)CH_WORDS && op1 - op0 <= (uint32_t)CH_OPS;
+        __syncthreads();
         const uint32_t rr = r0 + tid;
-        const bool in = rr < hi;
-        uint32_t bend = 0, oend = 0;
-        if (in) { bend = d.rd_base[rr + 1]; oend = d.rd_op[rr + 1]; }
-        const bool ok = in && bend - bw0 <= (uint32_t)CH_WORDS && oend - op0 <= (uint32_t)CH_OPS;
-        const uint32_t nr = (uint32_t)__syncthreads_count(ok);
-        if (tid < nr) {
-            const uint32_t sp = d.rd_span[rr], o = d.rd_op[rr], bb = d.rd_base[rr];
+        if (rr < r1) {
+            const uint32_t sp = d.rd_span[rr], o = d.rd_op[rr], o1 = d.rd_op[rr + 1], bb = d.rd_base[rr];
             const int s_rel = (int)(d.rd_pos[rr] - a);
-            const uint32_t nops = oend - o;
-            const bool single = nops == 1 && (d.ops[o] & 1u) == 0;
-            S.meta[tid] = make_uint4((uint32_t)s_rel, sp, (o - op0) | (nops << 16) | (single ? 0x80000000u : 0u),
-                                     bb - bw0);
-            const int e = s_rel + (int)(sp & 0x7FFFFFFFu);
+            const int span = (int)(sp & SPAN_MASK);
+            const bool fast = fits && (sp & SIMPLE);
+            S.meta[tid] = make_uint2((uint32_t)s_rel, ((bb - bw0) * 8u & 0xFFFFu) | ((uint32_t)span << 16) |
+                                                          (fast ? 0u : 0x80000000u));
+            const int e = s_rel + span;
             if (e > 0 && s_rel < n) {
                 const int wf = (s_rel > 0 ? s_rel : 0) >> 6, wl = ((e < n ? e : n) - 1) >> 6;
                 for (int i = wf; i <= wl; i++) { atomicMin(&S.win_lo[i], tid); atomicMax(&S.win_hi[i], tid + 1); }
+                if (!fast) S.slow[atomicAdd(&S.n_slow, 1u)] = make_uint2(tid, (o - op0) | ((o1 - o) << 16));
             }
-            if (tid == nr - 1) { S.tot_words = bend - bw0; S.tot_ops = oend - op0; }
         }
-        __syncthreads();
-        const uint32_t nwd = S.tot_words, nop = S.tot_ops;
-        for (uint32_t i = tid; i < nop; i += WG) S.ops[i] = d.ops[op0 + i];
-        {
+        if (fits) {
+            for (uint32_t i = tid; i < op1 - op0; i += WG) S.ops[i] = d.ops[op0 + i];
             const uint32_t *src = d.bases + bw0;
+            const uint32_t nwd = bw1 - bw0;
             uint32_t i = tid;
             for (; i + 3 * WG < nwd; i += 4 * WG) {
                 const uint32_t v0 = src[i], v1 = src[i + WG], v2 = src[i + 2 * WG], v3 = src[i + 3 * WG];
@@ -239,50 +413,62 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
             for (; i < nwd; i += WG) S.bases[i] = src[i];
         }
         __syncthreads();
-        // ---- count: every read overlapping one of this wave's windows ----
-        if (wbase < nw) {
-            uint32_t rlo = 0xFFFFFFFFu, rhi = 0;
+        if (d.ablate & 1) goto chunk_done;
+        // ---- fast path: single-M reads, branch-free, 4 in flight ----
 #pragma unroll
-            for (int wi = 0; wi < WPW; wi++)
-                if (wbase + wi < nw) {
-                    rlo = min(rlo, S.win_lo[wbase + wi]);
-                    rhi = max(rhi, S.win_hi[wbase + wi]);
-                }
-            rlo = uni(rlo);
-            rhi = uni(rhi);
-            for (uint32_t t = rlo; t < rhi; t++) {
-                const uint4 m = S.meta[t];
-                const int s_rel = (int)uni(m.x);
-                const uint32_t sp = uni(m.y), oo = uni(m.z), bo = uni(m.w);
-                const int span = (int)(sp & 0x7FFFFFFFu);
-                const bool drop = (sp >> 31) != 0;
+        for (int wi = 0; wi < WPW; wi++) {
+            if (wbase + wi >= nw) break;
+            const int pl = (wbase + wi) * 64 + (int)lane;
+            const uint32_t tlo = S.win_lo[wbase + wi], thi = S.win_hi[wbase + wi];
+            uint32_t t = tlo;
+            auto one = [&](uint2 m) -> uint32_t {
+                const uint32_t j = (uint32_t)(pl - (int)m.x);
+                const uint32_t span = (m.y >> 16) & 0x7FFFu;
+                const uint32_t nib = (m.y & 0xFFFFu) + j;
+                const uint32_t word = S.bases[(nib >> 3) & (CH_WORDS - 1)];
+                const uint32_t code = (word >> ((nib & 7u) * 4u)) & 15u;
+                return (j < span && !(m.y >> 31)) ? code * 10u : 60u;   // 60: spill field
+            };
+            for (; t + 4 <= thi; t += 4) {
+                const uint2 m0 = S.meta[t], m1 = S.meta[t + 1], m2 = S.meta[t + 2], m3 = S.meta[t + 3];
+                const uint32_t s0 = one(m0), s1 = one(m1), s2 = one(m2), s3 = one(m3);
+                acc[wi] += (1ull << s0) + (1ull << s1) + (1ull << s2) + (1ull << s3);
+            }
+            for (; t < thi; t++) acc[wi] += 1ull << one(S.meta[t]);
+            if (pl >= n) acc[wi] = 0;
+        }
+        // ---- slow path: multi-op / maxdel-dropped reads (op walk), compacted list ----
+        {
+            const uint32_t ns = S.n_slow;
+            for (uint32_t u = 0; u < ns; u++) {
+                const uint2 sl = S.slow[u];
+                const uint2 m = S.meta[sl.x];
+                const int s_rel = (int)m.x;
+                const uint32_t sp = d.rd_span[r0 + sl.x];
+                const int span = (int)(sp & SPAN_MASK);
+                const bool drop = (sp & DROP) != 0;
+                const uint32_t *ops = fits ? S.ops + (sl.y & 0xFFFFu) : d.ops + op0 + (sl.y & 0xFFFFu);
+                const uint32_t *bw = fits ? S.bases + (m.y & 0xFFFFu) / 8u : d.bases + d.rd_base[r0 + sl.x];
 #pragma unroll
                 for (int wi = 0; wi < WPW; wi++) {
                     const int w0 = (wbase + wi) * 64;
                     if (wbase + wi >= nw || s_rel >= w0 + 64 || s_rel + span <= w0) continue;
                     const int j = w0 + (int)lane - s_rel;
                     const bool mine = (unsigned)j < (unsigned)span && w0 + (int)lane < n;
-                    uint32_t code = 15;
-                    if (oo >> 31) {   // single M op: seqout index = query index
-                        if (mine) code = (S.bases[bo + ((uint32_t)j >> 3)] >> ((j & 7) * 4)) & 15u;
-                    } else {
-                        code = seqout_code(S.ops + (oo & 0xFFFFu), (oo >> 16) & 0x7FFFu, S.bases + bo, j, mine);
-                    }
-                    if (mine && !(drop && code == 0)) acc[wi] += 1ull << (10 * code);
+                    acc[wi] += 1ull << (10u * seqout_code(ops, sl.y >> 16, bw, j, mine, drop));
                 }
             }
         }
+    chunk_done:
         fold();
         __syncthreads();
-        r0 += nr;
     }
     // ---- long reads overlapping this tile (rare): metadata/ops/bases straight from HBM ----
     for (uint32_t x = xlo; x < xhi; x++) {
         const uint32_t r = uni(d.extras[x]);
         const int s_rel = (int)(uni(d.rd_pos[r]) - a);
         const uint32_t sp = uni(d.rd_span[r]);
-        const int span = (int)(sp & 0x7FFFFFFFu);
-        const bool drop = (sp >> 31) != 0;
+        const int span = (int)(sp & SPAN_MASK);
         const uint32_t o = uni(d.rd_op[r]), nops = uni(d.rd_op[r + 1]) - o;
         const uint32_t *bw = d.bases + uni(d.rd_base[r]);
 #pragma unroll
@@ -291,13 +477,25 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
             if (wbase + wi >= nw || s_rel >= w0 + 64 || s_rel + span <= w0) continue;
             const int j = w0 + (int)lane - s_rel;
             const bool mine = (unsigned)j < (unsigned)span && w0 + (int)lane < n;
-            const uint32_t code = seqout_code(d.ops + o, nops, bw, j, mine);
-            if (mine && !(drop && code == 0)) acc[wi] += 1ull << (10 * code);
+            acc[wi] += 1ull << (10u * seqout_code(d.ops + o, nops, bw, j, mine, (sp & DROP) != 0));
         }
         if (((x - xlo) & 255u) == 255u) fold();
     }
     fold();
-    // ---- tile counts → HBM (symbol-major, coalesced) ----
+    if (!(flags & 1u) && !(d.ablate & 4)) {   // the tile's whole depth is here: vote it now
+        __shared__ uint64_t sh[4];
+        int pls[WPW];
+#pragma unroll
+        for (int wi = 0; wi < WPW; wi++) {
+            const int pl = (wbase + wi) * 64 + (int)lane;
+            pls[wi] = (wbase + wi < nw && pl < n) ? pl : -1;
+        }
+        const uint32_t tile = uni(it[7]);
+        vote_epilogue<WPW>(d, tile, uni(d.blocks[(size_t)tile * S2C_BLOCK_WORDS + 2]), a, pls, cnt, sh);
+        return;
+    }
+    // ---- deep tile: this chunk's counts → HBM (symbol-major, coalesced atomics); with the
+    //      diagnostic flag 4 every tile stores its counts instead of voting (parity tests) ----
 #pragma unroll
     for (int wi = 0; wi < WPW; wi++) {
         const int pl = (wbase + wi) * 64 + (int)lane;
@@ -314,195 +512,23 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
     }
 }
 
-// ======================================================================= (3) insertions
-// (:264-271) motif multiplicities and (:284-287) per-column sums are additive, so the
-// column counts are accumulated straight from the events: column c of key k gets +1 at
-// motif[c] for every event at k with len > c.  The hash table maps key → slot with the
-// longest motif (:278-281) and a column base from a wave-aggregated bump allocator.
-__global__ void k_ins_insert(const s2c_dev d) {
-    const uint32_t e = blockIdx.x * WG + threadIdx.x;
-    if (e >= d.n_ins) return;
-    const uint32_t key = d.ins_key[e];
-    const uint32_t len = d.ins_off[e + 1] - d.ins_off[e];
-    const uint32_t cap = (uint32_t)d.ins_cap;
-    uint32_t h = hash32(key) & (cap - 1);
-    for (uint32_t probe = 0; probe < cap; probe++) {
-        const uint32_t prev = atomicCAS(&d.ins_table[4 * h], 0u, key + 1);
-        if (prev == 0u || prev == key + 1) {
-            atomicMax(&d.ins_table[4 * h + 1], len);
-            break;
-        }
-        h = (h + 1) & (cap - 1);
-    }
-    atomicOr(&d.ins_bits[key >> 5], 1u << (key & 31));
-}
-
-__global__ void k_ins_alloc(const s2c_dev d) {
-    const uint32_t s = blockIdx.x * WG + threadIdx.x;
-    const uint32_t cap = (uint32_t)d.ins_cap;
-    const uint32_t need = (s < cap && d.ins_table[4 * s] != 0u) ? d.ins_table[4 * s + 1] : 0u;
-    // wave-inclusive scan of `need`, one atomic per wave
-    uint32_t x = need;
-    const uint32_t lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= (uint32_t)o) x += y;
-    }
-    const uint32_t total = __shfl(x, 63, 64);
-    uint32_t base = 0;
-    if (lane == 63 && total) base = atomicAdd(&d.scalars[0], total);
-    base = __shfl(base, 63, 64);
-    if (need) d.ins_table[4 * s + 2] = base + x - need;
-}
-
-__global__ void k_ins_scatter(const s2c_dev d) {
-    const uint32_t e = blockIdx.x * WG + threadIdx.x;
-    if (e >= d.n_ins) return;
-    const uint32_t key = d.ins_key[e];
-    const uint32_t o0 = d.ins_off[e], o1 = d.ins_off[e + 1];
-    const uint32_t slot = ins_find(d.ins_table, (uint32_t)d.ins_cap, key);
-    if (slot == 0xFFFFFFFFu) return;
-    const uint32_t cb = d.ins_table[4 * slot + 2];
-    for (uint32_t c = 0; o0 + c < o1; c++)
-        atomicAdd(&d.ins_cols[(size_t)(cb + c) * NSYM + nibble(d.ins_bases, o0 + c)], 1u);
-}
-
-// (:290-309, :370-385) per key: '-' = cov[key] − Σ column (may be ≤ 0), vote each column
-// for every threshold; emitted chars (vote != "-") are compacted per threshold.
-__global__ void k_ins_vote(const s2c_dev d) {
-    const uint32_t s = blockIdx.x * WG + threadIdx.x;
-    const uint32_t cap = (uint32_t)d.ins_cap;
-    if (s >= cap) return;
-    const uint32_t k1 = d.ins_table[4 * s];
-    const int T = d.n_thr;
-    if (k1 == 0u) return;
-    const uint32_t p = k1 - 1;
-    uint64_t cov = 0;
-    for (uint32_t c = 0; c < NSYM; c++) cov += d.counts[(size_t)c * d.padded_len + p];
-    const bool called = cov > 0 && (int64_t)cov >= (int64_t)d.min_depth;
-    const uint32_t ml = d.ins_table[4 * s + 1], cb = d.ins_table[4 * s + 2];
-    // the key's reference: the consensus block containing p (blocks sorted by g_begin)
-    int64_t lo = 0, hi = d.n_blocks - 1;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi + 1) >> 1;
-        if (d.blocks[mid * S2C_BLOCK_WORDS] <= p) lo = mid; else hi = mid - 1;
-    }
-    const uint32_t ref = d.blocks[lo * S2C_BLOCK_WORDS + 2];
-    for (int t = 0; t < T; t++) {
-        uint32_t emitted = 0;
-        if (called) {
-            const double tc = d.thresholds[t] * (double)cov;
-            for (uint32_t c = 0; c < ml; c++) {
-                const uint32_t *col = d.ins_cols + (size_t)(cb + c) * NSYM;
-                int64_t v[NSYM];
-                int64_t tot = 0;
-#pragma unroll
-                for (uint32_t j = 0; j < NSYM; j++) { v[j] = col[j]; tot += v[j]; }
-                v[0] = (int64_t)cov - tot;   // :294 (the column's own '-' count is in the sum)
-                int64_t gs[NSYM];
-                greater_sums(v, gs);
-                const uint8_t ch = c_amb[vote_mask(v, gs, tc)];
-                if (ch == 0xFF) {
-                    atomicOr(&d.scalars[1], 1u);
-                    atomicAdd((unsigned long long *)&d.stats[((size_t)ref * T + t) * 4 + 3], 1ull);
-                    continue;
-                }
-                if (ch != '-') d.ins_chr[(size_t)t * d.n_ins_bases + cb + emitted++] = ch;
-            }
-        }
-        d.ins_cnt[(size_t)t * cap + s] = emitted;
-    }
-}
-
-__device__ __forceinline__ uint32_t ins_emitted(const s2c_dev &d, uint32_t p, int t, uint32_t *slot_out) {
-    if (!(d.ins_bits[p >> 5] >> (p & 31) & 1u)) return 0;
-    const uint32_t s = ins_find(d.ins_table, (uint32_t)d.ins_cap, p);
-    if (s == 0xFFFFFFFFu) return 0;
-    *slot_out = s;
-    return d.ins_cnt[(size_t)t * d.ins_cap + s];
-}
-
-// ======================================================================= (4) consensus
-// One workgroup per block (≤1024 positions of one ref); 4 positions per thread.
-// Per position, the 6 counts are read once and voted for every threshold.
-// Per (ref, t): sumcov (:357,:385), len and non-'-' chars of the record (:395-396).
-template <typename T>
-__device__ __forceinline__ T block_sum(T v, T *sh) {
-    v = wave_sum(v);
-    const uint32_t w = threadIdx.x >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) sh[w] = v;
-    __syncthreads();
-    T r = 0;
-#pragma unroll
-    for (int i = 0; i < WG / 64; i++) r += sh[i];
-    return r;
-}
-
+// Deep tiles: counts summed in HBM by their work items → the same vote epilogue.
 __global__ __launch_bounds__(WG) void k_consensus(const s2c_dev d) {
-    __shared__ uint64_t sh[WG / 64];
-    const uint32_t *blk = d.blocks + (size_t)blockIdx.x * S2C_BLOCK_WORDS;
-    const uint32_t g0 = uni(blk[0]), g1 = uni(blk[1]), ref = uni(blk[2]);
-    const int T = d.n_thr;
-    // positions handled by this thread
-    uint32_t cnt[4][NSYM];
-    uint64_t cov[4];
-    int64_t gs[4][NSYM];
-    bool valid[4], called[4];
+    __shared__ uint64_t sh[4];
+    const uint32_t tile = d.deep[blockIdx.x];
+    const uint32_t *blk = d.blocks + (size_t)tile * S2C_BLOCK_WORDS;
+    const uint32_t a = uni(blk[0]), n = uni(blk[1]) - a, ref = uni(blk[2]);
+    constexpr int NP = 2048 / WG;
+    int pl[NP];
+    uint32_t cnt[NP][NSYM];
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const uint32_t p = g0 + threadIdx.x + j * WG;
-        valid[j] = p < g1;
-        cov[j] = 0;
+    for (int k = 0; k < NP; k++) {
+        const uint32_t q = (uint32_t)k * WG + threadIdx.x;
+        pl[k] = q < n ? (int)q : -1;
 #pragma unroll
-        for (uint32_t c = 0; c < NSYM; c++) {
-            cnt[j][c] = valid[j] ? d.counts[(size_t)c * d.padded_len + p] : 0u;
-            cov[j] += cnt[j][c];
-        }
-        called[j] = cov[j] > 0 && (int64_t)cov[j] >= (int64_t)d.min_depth;
-        greater_sums(cnt[j], gs[j]);
+        for (uint32_t c = 0; c < NSYM; c++) cnt[k][c] = q < n ? d.counts[(size_t)c * d.padded_len + a + q] : 0u;
     }
-    for (int t = 0; t < T; t++) {
-        const double thr = d.thresholds[t];
-        uint64_t len = 0, nondash = 0, sumcov = 0, nerr = 0;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            if (!valid[j]) continue;
-            const uint32_t p = g0 + threadIdx.x + j * WG;
-            uint8_t code = S2C_CODE_FILL;
-            if (called[j]) {
-                const uint8_t ch = c_amb[vote_mask(cnt[j], gs[j], thr * (double)cov[j])];
-                uint32_t slot;
-                const uint32_t ne = ins_emitted(d, p, t, &slot);
-                nerr += ch == 0xFF;
-                code = ch;
-                len += 1 + ne;
-                nondash += (ch != '-') + ne;
-                sumcov += cov[j] * (1 + ne);
-            } else {
-                len += (uint32_t)d.fill_len;
-                nondash += (uint32_t)d.fill_nondash;
-                sumcov += cov[j];
-            }
-            d.codes[(size_t)t * d.padded_len + p] = code;
-        }
-        len = block_sum(len, sh);
-        nondash = block_sum(nondash, sh);
-        sumcov = block_sum(sumcov, sh);
-        nerr = block_sum(nerr, sh);
-        if (threadIdx.x == 0) {
-            uint64_t *st = d.stats + ((size_t)ref * T + t) * 4;
-            atomicAdd((unsigned long long *)&st[0], (unsigned long long)sumcov);
-            atomicAdd((unsigned long long *)&st[1], (unsigned long long)len);
-            atomicAdd((unsigned long long *)&st[2], (unsigned long long)nondash);
-            if (nerr) {
-                atomicAdd((unsigned long long *)&st[3], (unsigned long long)nerr);
-                atomicOr(&d.scalars[1], 1u);
-            }
-            d.blk_len[(size_t)t * d.n_blocks + blockIdx.x] = len;
-        }
-    }
+    vote_epilogue<NP>(d, tile, ref, a, pl, cnt, sh);
 }
 
 // ======================================================================= assembly
@@ -532,29 +558,37 @@ __global__ __launch_bounds__(1024) void k_scan(uint64_t *v, int64_t n) {
 
 // grid = n_blocks × T.  Record body of (ref, t) = concatenation over its positions of
 // fill (uncalled) or the vote char followed by the emitted insertion chars (:367-389).
+constexpr int ASM_PER = 2048 / WG;   // consecutive positions per thread
 __global__ __launch_bounds__(WG) void k_assemble(const s2c_dev d) {
-    __shared__ uint64_t sh[WG];
+    __shared__ uint64_t sh[WG / 64];
     const uint32_t bi = blockIdx.x;
     const int t = (int)blockIdx.y;
     const uint32_t *blk = d.blocks + (size_t)bi * S2C_BLOCK_WORDS;
     const uint32_t g0 = uni(blk[0]), g1 = uni(blk[1]);
     const uint64_t base = d.blk_len[(size_t)t * d.n_blocks + bi];
     const uint8_t *codes = d.codes + (size_t)t * d.padded_len;
-    const uint32_t p0 = g0 + 4 * threadIdx.x;
-    uint32_t lens[4], slots[4];
+    const uint32_t p0 = g0 + ASM_PER * threadIdx.x;
+    uint32_t lens[ASM_PER], slots[ASM_PER];
     uint64_t my = 0;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
+    for (int j = 0; j < ASM_PER; j++) {
         const uint32_t p = p0 + j;
         lens[j] = 0;
         slots[j] = 0xFFFFFFFFu;
         if (p < g1) {
             const uint8_t c = codes[p];
-            lens[j] = c == S2C_CODE_FILL ? (uint32_t)d.fill_len : 1u + ins_emitted(d, p, t, &slots[j]);
+            if (c == S2C_CODE_FILL) {
+                lens[j] = (uint32_t)d.fill_len;
+            } else {
+                lens[j] = 1;
+                if (d.ins_bits[p >> 5] >> (p & 31) & 1u) {
+                    slots[j] = ins_find(d.ins_table, (uint32_t)d.ins_cap, p);
+                    lens[j] += d.ins_cnt[(size_t)t * d.ins_cap + slots[j]];
+                }
+            }
         }
         my += lens[j];
     }
-    // block exclusive scan of `my`
     uint64_t x = my;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
@@ -568,7 +602,7 @@ __global__ __launch_bounds__(WG) void k_assemble(const s2c_dev d) {
     for (uint32_t i = 0; i < w; i++) wofs += sh[i];
     uint64_t off = base + wofs + x - my;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
+    for (int j = 0; j < ASM_PER; j++) {
         const uint32_t p = p0 + j;
         if (p >= g1) break;
         const uint8_t c = codes[p];
@@ -592,7 +626,7 @@ inline int hip_check(hipError_t e, const char *what) {
     return s2c_set_error(S2C_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-inline unsigned grid_for(int64_t n) { return (unsigned)((n + WG - 1) / WG); }
+inline unsigned grid_for(int64_t n, int wg = WG) { return (unsigned)((n + wg - 1) / wg); }
 
 }  // namespace
 
@@ -603,7 +637,7 @@ extern "C" int s2c_workspace_sizes(const s2c_batch_info *info, int32_t n_thr, s2
     int64_t cap = 64;
     while (cap < 2 * info->n_ins) cap <<= 1;
     const int64_t nib = info->n_ins_bases > 0 ? info->n_ins_bases : 1;
-    o->counts = NSYM * L * 4;
+    o->counts = info->n_deep ? NSYM * L * 4 : 64;   // only deep tiles keep counts in HBM
     o->ins_cap = cap;
     o->ins_table = cap * 16;
     o->ins_cols = nib * NSYM * 4;
@@ -623,10 +657,25 @@ static int check_dev(const s2c_dev *d) {
     if (d->tile_max <= 0 || d->tile_max > 64 * MAX_WIN) return s2c_set_error(S2C_ERR_ARG, "tile_max out of range");
     if (d->padded_len <= 0 || d->padded_len >= ((int64_t)1 << 32)) return s2c_set_error(S2C_ERR_ARG, "bad padded_len");
     if (d->ins_cap <= 0 || (d->ins_cap & (d->ins_cap - 1))) return s2c_set_error(S2C_ERR_ARG, "ins_cap not pow2");
-    if (d->n_items > 0 && (!d->items || !d->counts)) return s2c_set_error(S2C_ERR_ARG, "missing pileup buffers");
+    if (d->n_items > 0 && !d->items) return s2c_set_error(S2C_ERR_ARG, "missing pileup buffers");
+    if (d->n_deep > 0 && (!d->deep || !d->counts)) return s2c_set_error(S2C_ERR_ARG, "missing deep-tile buffers");
     if (d->n_ins > 0 && (!d->ins_key || !d->ins_off || !d->ins_bases || !d->ins_table || !d->ins_cols))
         return s2c_set_error(S2C_ERR_ARG, "missing insertion buffers");
     return S2C_OK;
+}
+
+// zero per-run state, then the insertion table (must precede the pileup's vote epilogue)
+extern "C" int s2c_insertions(const s2c_dev *d, void *stream) {
+    int rc = check_dev(d);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    k_prep<<<(unsigned)(PREP_BLOCKS + d->n_deep), WG, 0, s>>>(*d);
+    if (d->n_ins) {
+        k_ins_build<<<grid_for(d->n_ins), WG, 0, s>>>(*d);
+        k_ins_alloc<<<grid_for(d->ins_cap, ALLOC_WG), ALLOC_WG, 0, s>>>(*d);
+        k_ins_scatter<<<grid_for(d->n_ins), WG, 0, s>>>(*d);
+    }
+    return hip_check(hipGetLastError(), "k_prep/k_ins_*");
 }
 
 extern "C" int s2c_pileup(const s2c_dev *d, void *stream) {
@@ -634,7 +683,6 @@ extern "C" int s2c_pileup(const s2c_dev *d, void *stream) {
     if (rc) return rc;
     if (d->n_items == 0) return S2C_OK;
     hipStream_t s = (hipStream_t)stream;
-    k_zero_tiles<<<(unsigned)d->n_items, WG, 0, s>>>(*d);
     const unsigned g = (unsigned)d->n_items;
     if (d->tile_max <= 256) k_pileup<1><<<g, WG, 0, s>>>(*d);
     else if (d->tile_max <= 512) k_pileup<2><<<g, WG, 0, s>>>(*d);
@@ -643,34 +691,11 @@ extern "C" int s2c_pileup(const s2c_dev *d, void *stream) {
     return hip_check(hipGetLastError(), "k_pileup");
 }
 
-extern "C" int s2c_insertions(const s2c_dev *d, void *stream) {
-    int rc = check_dev(d);
-    if (rc) return rc;
-    hipStream_t s = (hipStream_t)stream;
-    rc = hip_check(hipMemsetAsync(d->scalars, 0, 64, s), "memset scalars");
-    if (rc) return rc;
-    rc = hip_check(hipMemsetAsync(d->ins_bits, 0, (size_t)(d->padded_len / 32 + 2) * 4, s), "memset ins_bits");
-    if (rc) return rc;
-    // stats are accumulated by the insertion vote (errors) and then by the consensus
-    rc = hip_check(hipMemsetAsync(d->stats, 0, (size_t)d->n_refs * d->n_thr * 32, s), "memset stats");
-    if (rc || d->n_ins == 0) return rc;
-    rc = hip_check(hipMemsetAsync(d->ins_table, 0, (size_t)d->ins_cap * 16, s), "memset ins_table");
-    if (rc) return rc;
-    rc = hip_check(hipMemsetAsync(d->ins_cols, 0, (size_t)d->n_ins_bases * NSYM * 4, s), "memset ins_cols");
-    if (rc) return rc;
-    k_ins_insert<<<grid_for(d->n_ins), WG, 0, s>>>(*d);
-    k_ins_alloc<<<grid_for(d->ins_cap), WG, 0, s>>>(*d);
-    k_ins_scatter<<<grid_for(d->n_ins), WG, 0, s>>>(*d);
-    k_ins_vote<<<grid_for(d->ins_cap), WG, 0, s>>>(*d);
-    return hip_check(hipGetLastError(), "k_ins_*");
-}
-
 extern "C" int s2c_consensus(const s2c_dev *d, void *stream) {
     int rc = check_dev(d);
     if (rc) return rc;
-    hipStream_t s = (hipStream_t)stream;
-    if (d->n_blocks == 0) return S2C_OK;
-    k_consensus<<<(unsigned)d->n_blocks, WG, 0, s>>>(*d);
+    if (d->n_deep == 0) return S2C_OK;
+    k_consensus<<<(unsigned)d->n_deep, WG, 0, (hipStream_t)stream>>>(*d);
     return hip_check(hipGetLastError(), "k_consensus");
 }
 
@@ -686,8 +711,8 @@ extern "C" int s2c_assemble(const s2c_dev *d, void *stream) {
 
 extern "C" int s2c_run(const s2c_dev *d, void *stream) {
     int rc;
-    if ((rc = s2c_pileup(d, stream))) return rc;
     if ((rc = s2c_insertions(d, stream))) return rc;
+    if ((rc = s2c_pileup(d, stream))) return rc;
     if ((rc = s2c_consensus(d, stream))) return rc;
     return s2c_assemble(d, stream);
 }

@@ -54,6 +54,7 @@ class DeviceBatch:
         self.rd_span = up(hb.rd_span)
         self.ops, self.bases = up(hb.ops), up(hb.bases)
         self.items, self.extras, self.blocks = up(hb.items.reshape(-1)), up(hb.extras), up(hb.blocks.reshape(-1))
+        self.deep = up(hb.deep)
         self.ins_key, self.ins_off, self.ins_bases = up(hb.ins_key), up(hb.ins_off), up(hb.ins_bases)
 
     def nbytes(self):
@@ -65,7 +66,7 @@ class DeviceBatch:
 class Workspace:
     """All scratch + output buffers for one (batch, thresholds, fill) configuration."""
 
-    def __init__(self, db: DeviceBatch, thresholds, min_depth=1, fill=b"-"):
+    def __init__(self, db: DeviceBatch, thresholds, min_depth=1, fill=b"-", keep_counts=False):
         dev = db.device
         i = db.info
         self.db = db
@@ -78,7 +79,8 @@ class Workspace:
         fill = bytes(fill)
         self.fill_bytes = fill
         self.fill = torch.tensor(list(fill) or [0], dtype=torch.uint8, device=dev)
-        self.counts = u8(sz.counts)
+        # counts live in HBM only for deep tiles (unless a test asks for all of them)
+        self.counts = u8(6 * i.padded_len * 4 if keep_counts else sz.counts)
         self.ins_table = u8(sz.ins_table)
         self.ins_cols = u8(sz.ins_cols)
         self.ins_cnt = u8(sz.ins_cnt)
@@ -95,9 +97,9 @@ class Workspace:
         d.rd_pos, d.rd_op, d.rd_base = _ptr(db.rd_pos), _ptr(db.rd_op), _ptr(db.rd_base)
         d.rd_span = _ptr(db.rd_span)
         d.ops, d.bases = _ptr(db.ops), _ptr(db.bases)
-        d.items, d.extras, d.blocks = _ptr(db.items), _ptr(db.extras), _ptr(db.blocks)
+        d.items, d.extras, d.blocks, d.deep = _ptr(db.items), _ptr(db.extras), _ptr(db.blocks), _ptr(db.deep)
         d.ins_key, d.ins_off, d.ins_bases = _ptr(db.ins_key), _ptr(db.ins_off), _ptr(db.ins_bases)
-        d.n_reads, d.n_items, d.n_blocks = i.n_reads, i.n_items, i.n_blocks
+        d.n_reads, d.n_items, d.n_blocks, d.n_deep = i.n_reads, i.n_items, i.n_blocks, i.n_deep
         d.n_ins, d.n_ins_bases, d.padded_len = i.n_ins, i.n_ins_bases, i.padded_len
         d.tile_max, d.n_refs = i.tile_max, i.n_refs
         d.thresholds, d.n_thr = _ptr(self.thr), self.T
@@ -114,12 +116,12 @@ class Workspace:
     def stream_handle(self):
         return C.c_void_p(torch.cuda.current_stream(self.db.device).cuda_stream)
 
-    # ---- the four stages (each one C-ABI call; all asynchronous on the current stream)
-    def pileup(self):
-        L.check(lib.s2c_pileup(C.byref(self.dev), self.stream_handle()))
-
+    # ---- the four stages in run order (each one C-ABI call; asynchronous on the current stream)
     def insertions(self):
         L.check(lib.s2c_insertions(C.byref(self.dev), self.stream_handle()))
+
+    def pileup(self):
+        L.check(lib.s2c_pileup(C.byref(self.dev), self.stream_handle()))
 
     def consensus(self):
         L.check(lib.s2c_consensus(C.byref(self.dev), self.stream_handle()))
@@ -128,10 +130,21 @@ class Workspace:
         L.check(lib.s2c_assemble(C.byref(self.dev), self.stream_handle()))
 
     def run(self):
-        """pileup → insertions → consensus → assembly (no host sync)."""
+        """insertions → pileup(+vote) → deep-tile consensus → assembly (no host sync)."""
         L.check(lib.s2c_run(C.byref(self.dev), self.stream_handle()))
 
     # ---- results
+    def pileup_counts(self):
+        """Diagnostic: run prep + pileup with every tile storing its counts (needs
+        keep_counts=True); returns counts[6][padded_len] as numpy u32."""
+        self.insertions()
+        self.dev.ablate = 4
+        try:
+            self.pileup()
+        finally:
+            self.dev.ablate = 0
+        return self.counts_host()
+
     def counts_host(self):
         """counts[6][padded_len] as numpy u32 (for parity tests)."""
         Lp = self.db.info.padded_len

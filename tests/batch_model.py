@@ -30,7 +30,8 @@ def read_codes(hb, r):
     o0 = int(hb.rd_op[r])
     o1 = int(hb.rd_op[r + 1])
     drop = bool(int(hb.rd_span[r]) >> 31)
-    assert sum(int(w) >> 1 for w in hb.ops[o0:o1]) == int(hb.rd_span[r]) & 0x7FFFFFFF
+    assert sum(int(w) >> 1 for w in hb.ops[o0:o1]) == int(hb.rd_span[r]) & 0x3FFFFFFF
+    assert bool(int(hb.rd_span[r]) >> 30 & 1) == (not drop and o1 - o0 == 1 and (int(hb.ops[o0]) & 1) == 0)
     ops = [(int(w) & 1, int(w) >> 1) for w in hb.ops[o0:o1]]
     nm = sum(l for c, l in ops if c == 0)
     w0 = int(hb.rd_base[r])

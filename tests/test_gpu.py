@@ -35,10 +35,10 @@ def test_hip_path_matches_reference(case):
     assert files == case["files"]
 
 
-def _ws(hb, thresholds, min_depth=1, fill=b"-"):
+def _ws(hb, thresholds, min_depth=1, fill=b"-", keep_counts=False):
     from sam2consensus_amd.engine import DeviceBatch, Workspace
     db = DeviceBatch(hb)
-    return Workspace(db, thresholds, min_depth, fill)
+    return Workspace(db, thresholds, min_depth, fill, keep_counts)
 
 
 @pytest.mark.parametrize("name,over", [("c1", {}), ("c2", {"n_refs": 18}), ("c5", {"ref_len": 400_000}),
@@ -47,9 +47,8 @@ def _ws(hb, thresholds, min_depth=1, fill=b"-"):
 def test_pileup_counts_equal_batch_model(name, over):
     from sam2consensus_amd import configs
     hb = configs.synth_batch(name, **over)
-    ws = _ws(hb, [0.25])
-    ws.pileup()
-    got = ws.counts_host().astype(np.int64)
+    ws = _ws(hb, [0.25], keep_counts=True)
+    got = ws.pileup_counts().astype(np.int64)
     want = bm.model_counts(hb)
     for r in range(hb.info.n_refs):
         a, L = int(hb.ref_off[r]), int(hb.ref_len[r])
@@ -80,15 +79,12 @@ def test_config_fasta_byte_identical_to_reference(name):
     assert got == want
     # size-independent property: Σ counts == counted aligned bases (no maxdel drops here)
     if name in ("c1", "c2", "c5"):
-        ws = _ws(hb, opt.thresholds)
-        ws.pileup()
-        import torch
-        Lp = hb.info.padded_len
+        ws = _ws(hb, opt.thresholds, keep_counts=True)
+        cnt = ws.pileup_counts()
         tot = 0
-        cnt = ws.counts[: 6 * Lp * 4].view(torch.int32)
         for r in range(hb.info.n_refs):
             a, L = int(hb.ref_off[r]), int(hb.ref_len[r])
-            tot += int(cnt.view(6, Lp)[:, a:a + L].to(torch.int64).sum())
+            tot += int(cnt[:, a:a + L].astype(np.int64).sum())
         assert tot == hb.info.aligned_bases
 
 
