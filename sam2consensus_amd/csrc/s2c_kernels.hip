@@ -21,6 +21,7 @@
 // (double)S < t * (double)cov — built with -ffp-contract=off.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <string>
 
@@ -355,7 +356,16 @@ __device__ __forceinline__ uint32_t seqout_code(const uint32_t *ops, uint32_t no
 template <int WPW>
 __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
     __shared__ ChunkLds S;
-    const uint32_t *it = d.items + (size_t)blockIdx.x * S2C_ITEM_WORDS;
+    __shared__ uint32_t ticket;
+    __shared__ uint64_t sh[4];
+    // persistent: each workgroup pulls work items from an atomic ticket (zeroed by k_prep)
+    for (;;) {
+    if (threadIdx.x == 0) ticket = atomicAdd(&d.scalars[2], 1u);
+    __syncthreads();
+    const uint32_t item = ticket;
+    __syncthreads();
+    if (item >= (uint32_t)d.n_items) return;
+    const uint32_t *it = d.items + (size_t)item * S2C_ITEM_WORDS;
     const uint32_t a = uni(it[0]), b = uni(it[1]), lo = uni(it[2]), hi = uni(it[3]);
     const uint32_t xlo = uni(it[4]), xhi = uni(it[5]), flags = uni(it[6]);
     const int n = (int)(b - a), nw = (n + 63) >> 6;
@@ -483,7 +493,6 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
     }
     fold();
     if (!(flags & 1u) && !(d.ablate & 4)) {   // the tile's whole depth is here: vote it now
-        __shared__ uint64_t sh[4];
         int pls[WPW];
 #pragma unroll
         for (int wi = 0; wi < WPW; wi++) {
@@ -492,7 +501,7 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
         }
         const uint32_t tile = uni(it[7]);
         vote_epilogue<WPW>(d, tile, uni(d.blocks[(size_t)tile * S2C_BLOCK_WORDS + 2]), a, pls, cnt, sh);
-        return;
+        continue;
     }
     // ---- deep tile: this chunk's counts → HBM (symbol-major, coalesced atomics); with the
     //      diagnostic flag 4 every tile stores its counts instead of voting (parity tests) ----
@@ -510,6 +519,7 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
             }
         }
     }
+    }   // for (;;) items
 }
 
 // Deep tiles: counts summed in HBM by their work items → the same vote epilogue.
@@ -558,7 +568,7 @@ __global__ __launch_bounds__(1024) void k_scan(uint64_t *v, int64_t n) {
 
 // grid = n_blocks × T.  Record body of (ref, t) = concatenation over its positions of
 // fill (uncalled) or the vote char followed by the emitted insertion chars (:367-389).
-constexpr int ASM_PER = 2048 / WG;   // consecutive positions per thread
+template <int ASM_PER>   // consecutive positions per thread (tile_max / 256)
 __global__ __launch_bounds__(WG) void k_assemble(const s2c_dev d) {
     __shared__ uint64_t sh[WG / 64];
     const uint32_t bi = blockIdx.x;
@@ -664,6 +674,24 @@ static int check_dev(const s2c_dev *d) {
     return S2C_OK;
 }
 
+// Persistent grid: as many workgroups as fit at once (occupancy query, cached per kernel),
+// never more than the items; each pulls items from the ticket.
+template <typename K>
+static int launch_persistent(K kern, const s2c_dev *d, hipStream_t s) {
+    static int per_cu = 0, n_cu = 0;
+    if (!per_cu) {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess)
+            return s2c_set_error(S2C_ERR_HIP, "device query failed");
+        n_cu = prop.multiProcessorCount;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, WG, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    }
+    const int64_t g = std::min<int64_t>(d->n_items, (int64_t)per_cu * n_cu);
+    kern<<<(unsigned)g, WG, 0, s>>>(*d);
+    return hip_check(hipGetLastError(), "k_pileup");
+}
+
 // zero per-run state, then the insertion table (must precede the pileup's vote epilogue)
 extern "C" int s2c_insertions(const s2c_dev *d, void *stream) {
     int rc = check_dev(d);
@@ -683,12 +711,10 @@ extern "C" int s2c_pileup(const s2c_dev *d, void *stream) {
     if (rc) return rc;
     if (d->n_items == 0) return S2C_OK;
     hipStream_t s = (hipStream_t)stream;
-    const unsigned g = (unsigned)d->n_items;
-    if (d->tile_max <= 256) k_pileup<1><<<g, WG, 0, s>>>(*d);
-    else if (d->tile_max <= 512) k_pileup<2><<<g, WG, 0, s>>>(*d);
-    else if (d->tile_max <= 1024) k_pileup<4><<<g, WG, 0, s>>>(*d);
-    else k_pileup<8><<<g, WG, 0, s>>>(*d);
-    return hip_check(hipGetLastError(), "k_pileup");
+    if (d->tile_max <= 256) return launch_persistent(k_pileup<1>, d, s);
+    if (d->tile_max <= 512) return launch_persistent(k_pileup<2>, d, s);
+    if (d->tile_max <= 1024) return launch_persistent(k_pileup<4>, d, s);
+    return launch_persistent(k_pileup<8>, d, s);
 }
 
 extern "C" int s2c_consensus(const s2c_dev *d, void *stream) {
@@ -705,7 +731,13 @@ extern "C" int s2c_assemble(const s2c_dev *d, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     const int64_t n = (int64_t)d->n_thr * d->n_blocks;
     k_scan<<<1, 1024, 0, s>>>(d->blk_len, n);
-    if (d->n_blocks) k_assemble<<<dim3((unsigned)d->n_blocks, (unsigned)d->n_thr), WG, 0, s>>>(*d);
+    if (d->n_blocks) {
+        const dim3 g((unsigned)d->n_blocks, (unsigned)d->n_thr);
+        if (d->tile_max <= 256) k_assemble<1><<<g, WG, 0, s>>>(*d);
+        else if (d->tile_max <= 512) k_assemble<2><<<g, WG, 0, s>>>(*d);
+        else if (d->tile_max <= 1024) k_assemble<4><<<g, WG, 0, s>>>(*d);
+        else k_assemble<8><<<g, WG, 0, s>>>(*d);
+    }
     return hip_check(hipGetLastError(), "k_assemble");
 }
 
