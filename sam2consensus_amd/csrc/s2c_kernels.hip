@@ -303,18 +303,18 @@ __device__ __forceinline__ void vote_epilogue(const s2c_dev &d, uint32_t tile, u
 // fit the LDS buffers the chunk takes the HBM path for everything (never seen on the
 // BASELINE configs: 128 reads of 150 bp use ~2.4k words).
 constexpr int CH = 128;           // reads per chunk (< 1023: a 10-bit field never overflows)
-constexpr int CH_WORDS = 4096;    // 16 KiB of packed bases
-constexpr int CH_OPS = 512;       // op words
+constexpr int CH_WORDS = 3072;    // 12 KiB of packed bases per buffer
+constexpr int CH_OPS = 384;       // op words per buffer
 constexpr int MAX_WIN = 32;       // 64-position windows per tile (tile ≤ 2048 positions)
 constexpr uint32_t SPAN_MASK = 0x3FFFFFFFu, SIMPLE = 0x40000000u, DROP = 0x80000000u;
 
-struct __attribute__((aligned(16))) ChunkLds {
-    uint2 meta[CH];               // x: start - a (signed); y: nibble offset (16b) | span << 16 (11b) | !simple << 31
-    uint2 slow[CH];               // x: chunk read index, y: op offset (16b) | nops << 16; reads off the fast path
-    uint32_t ops[CH_OPS];
-    uint32_t bases[CH_WORDS];
-    uint32_t win_lo[MAX_WIN], win_hi[MAX_WIN];
-    uint32_t n_slow, tot_words, tot_ops, fits;
+struct __attribute__((aligned(16))) ChunkLds {    // double-buffered: chunk k in [k & 1]
+    uint32_t bases[2][CH_WORDS];
+    uint32_t ops[2][CH_OPS];
+    uint2 meta[2][CH];            // x: start - a (signed); y: nibble offset (16b) | span << 16 (15b) | !fast << 31
+    uint2 slow[2][CH];            // x: chunk read index, y: op offset (16b) | nops << 16; reads off the fast path
+    uint32_t win_lo[2][MAX_WIN], win_hi[2][MAX_WIN];
+    uint32_t n_slow[2];
 };
 
 // code of seqout index j (lane-varying) of a read whose ops/bases sit at (ops, bases);
@@ -341,23 +341,31 @@ __device__ __forceinline__ uint32_t seqout_code(const uint32_t *ops, uint32_t no
     return (drop && code == 0) ? 6u : code;
 }
 
+__device__ __forceinline__ void lds_dma_dword(const uint32_t *g, uint32_t *l) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
+                                     (__attribute__((address_space(3))) void *)l, 4, 0, 0);
+}
+
 // One workgroup per work item = (tile [a,b) of one reference, read range [lo,hi) + long-read
-// extras).  Position-major: lane ℓ of a wave owns tile position 64·w + ℓ of each of its
-// windows w and keeps its six counts in registers — a u64 of 10-bit fields per window,
-// += 1 << 10·code per covering read (no atomics), folded into u32 counts after every chunk.
-// Reads are staged through LDS in chunks of ≤128: metadata, op words and packed bases
-// arrive by coalesced loads, then each window sweeps the chunk's reads that overlap it.
-// Single-M-op reads (all but D/N/P reads and maxdel-dropped ones) take a branch-free
-// path: per (read, window) ~13 VALU + 2 LDS reads, 4 reads in flight per iteration;
-// the others take the op-walk path from a compacted list.  Only windows inside the tile
-// are visited, so a read straddling a tile edge costs a visit, never a count.  A tile
-// holding its whole depth runs the vote epilogue on its register counts; a deep tile
-// (reads split over items) adds its counts into HBM for k_consensus.
+// extras), pulled from an atomic ticket (persistent grid).  Position-major: lane ℓ of a wave
+// owns tile position 64·w + ℓ of each of its windows w and keeps its six counts in
+// registers — a u64 of 10-bit fields per window, += 1 << 10·code per covering read (no
+// atomics), folded into u32 counts after every chunk.  Reads are staged through LDS in
+// chunks of ≤128, double-buffered: while chunk k is counted, chunk k+1's packed bases and
+// op words stream in by LDS-DMA (global_load_lds) and its per-read metadata by plain
+// loads, so a chunk costs one barrier and no exposed HBM round trip.  Single-M-op reads
+// (all but D/N/P reads and maxdel-dropped ones) take a branch-free path: per (read,
+// window) ~13 VALU + 2 LDS reads, 4 reads in flight; the others take the op-walk path
+// from a compacted list.  Only windows inside the tile are visited, so a read straddling
+// a tile edge costs a visit, never a count.  A tile holding its whole depth runs the vote
+// epilogue on its register counts; a deep tile (reads split over items) adds its counts
+// into HBM for k_consensus.
 template <int WPW>
 __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
     __shared__ ChunkLds S;
     __shared__ uint32_t ticket;
     __shared__ uint64_t sh[4];
+    const uint32_t total_words = uni(d.rd_base[d.n_reads]), total_ops = uni(d.rd_op[d.n_reads]);
     // persistent: each workgroup pulls work items from an atomic ticket (zeroed by k_prep)
     for (;;) {
     if (threadIdx.x == 0) ticket = atomicAdd(&d.scalars[2], 1u);
@@ -387,78 +395,103 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
             acc[wi] = 0;
         }
     };
-    for (uint32_t r0 = lo; r0 < hi; r0 += CH) {
-        const uint32_t r1 = min(hi, r0 + CH);
-        // ---- stage: per-read metadata (one coalesced load per array), then ops/bases ----
-        if (tid < MAX_WIN) { S.win_lo[tid] = 0xFFFFFFFFu; S.win_hi[tid] = 0; }
-        if (tid == 0) S.n_slow = 0;
-        const uint32_t bw0 = uni(d.rd_base[r0]), op0 = uni(d.rd_op[r0]);
-        const uint32_t bw1 = uni(d.rd_base[r1]), op1 = uni(d.rd_op[r1]);
-        const bool fits = bw1 - bw0 <= (uint32_t)CH_WORDS && op1 - op0 <= (uint32_t)CH_OPS;
-        __syncthreads();
-        const uint32_t rr = r0 + tid;
-        if (rr < r1) {
-            const uint32_t sp = d.rd_span[rr], o = d.rd_op[rr], o1 = d.rd_op[rr + 1], bb = d.rd_base[rr];
-            const int s_rel = (int)(d.rd_pos[rr] - a);
-            const int span = (int)(sp & SPAN_MASK);
-            const bool fast = fits && (sp & SIMPLE);
-            S.meta[tid] = make_uint2((uint32_t)s_rel, ((bb - bw0) * 8u & 0xFFFFu) | ((uint32_t)span << 16) |
-                                                          (fast ? 0u : 0x80000000u));
+    const uint32_t nchunks = (hi - lo + CH - 1) / CH;
+    auto rb = [&](uint32_t j) { return min(hi, lo + j * CH); };   // first read of chunk j
+    // LDS-DMA of chunk j's words [B0,B1) and ops [O0,O1) into buffer `buf` (if they fit)
+    auto dma = [&](int buf, uint32_t B0, uint32_t B1, uint32_t O0, uint32_t O1) {
+        if (B1 - B0 > (uint32_t)CH_WORDS || O1 - O0 > (uint32_t)CH_OPS) return;
+        const uint32_t w = tid >> 6;
+        for (uint32_t i = w * 64; i < B1 - B0; i += WG)
+            lds_dma_dword(d.bases + min(B0 + i + lane, total_words - 1), &S.bases[buf][i]);
+        for (uint32_t i = w * 64; i < O1 - O0; i += WG)
+            lds_dma_dword(d.ops + min(O0 + i + lane, total_ops - 1), &S.ops[buf][i]);
+    };
+    // chunk-0 prologue: boundaries, DMA, metadata registers
+    uint32_t B0 = uni(d.rd_base[rb(0)]), O0 = uni(d.rd_op[rb(0)]);
+    uint32_t B1 = uni(d.rd_base[rb(1)]), O1 = uni(d.rd_op[rb(1)]);
+    uint32_t m_pos = 0, m_span = 0, m_o = 0, m_o1 = 0, m_bb = 0;
+    auto load_meta = [&](uint32_t j) {
+        const uint32_t rr = rb(j) + tid;
+        if (rr < rb(j + 1)) {
+            m_pos = d.rd_pos[rr]; m_span = d.rd_span[rr]; m_o = d.rd_op[rr]; m_o1 = d.rd_op[rr + 1];
+            m_bb = d.rd_base[rr];
+        }
+    };
+    if (nchunks) {
+        dma(0, B0, B1, O0, O1);
+        load_meta(0);
+    }
+    if (tid < MAX_WIN) { S.win_lo[0][tid] = 0xFFFFFFFFu; S.win_hi[0][tid] = 0; }
+    if (tid == 0) S.n_slow[0] = 0;
+    __syncthreads();
+    for (uint32_t k = 0; k < nchunks; k++) {
+        const int cur = (int)(k & 1);
+        const uint32_t r0 = rb(k), r1 = rb(k + 1);
+        const bool fits = B1 - B0 <= (uint32_t)CH_WORDS && O1 - O0 <= (uint32_t)CH_OPS;
+        const uint32_t B2 = uni(d.rd_base[rb(k + 2)]), O2 = uni(d.rd_op[rb(k + 2)]);
+        // ---- publish chunk k's metadata (registers → LDS), window ranges, slow list ----
+        if (r0 + tid < r1) {
+            const int s_rel = (int)(m_pos - a);
+            const int span = (int)(m_span & SPAN_MASK);
+            const bool fast = fits && (m_span & SIMPLE);
+            S.meta[cur][tid] = make_uint2((uint32_t)s_rel, ((m_bb - B0) * 8u & 0xFFFFu) | ((uint32_t)span << 16) |
+                                                               (fast ? 0u : 0x80000000u));
             const int e = s_rel + span;
             if (e > 0 && s_rel < n) {
                 const int wf = (s_rel > 0 ? s_rel : 0) >> 6, wl = ((e < n ? e : n) - 1) >> 6;
-                for (int i = wf; i <= wl; i++) { atomicMin(&S.win_lo[i], tid); atomicMax(&S.win_hi[i], tid + 1); }
-                if (!fast) S.slow[atomicAdd(&S.n_slow, 1u)] = make_uint2(tid, (o - op0) | ((o1 - o) << 16));
+                for (int i = wf; i <= wl; i++) {
+                    atomicMin(&S.win_lo[cur][i], tid);
+                    atomicMax(&S.win_hi[cur][i], tid + 1);
+                }
+                if (!fast) S.slow[cur][atomicAdd(&S.n_slow[cur], 1u)] = make_uint2(tid, (m_o - O0) | ((m_o1 - m_o) << 16));
             }
         }
-        if (fits) {
-            for (uint32_t i = tid; i < op1 - op0; i += WG) S.ops[i] = d.ops[op0 + i];
-            const uint32_t *src = d.bases + bw0;
-            const uint32_t nwd = bw1 - bw0;
-            uint32_t i = tid;
-            for (; i + 3 * WG < nwd; i += 4 * WG) {
-                const uint32_t v0 = src[i], v1 = src[i + WG], v2 = src[i + 2 * WG], v3 = src[i + 3 * WG];
-                S.bases[i] = v0; S.bases[i + WG] = v1; S.bases[i + 2 * WG] = v2; S.bases[i + 3 * WG] = v3;
-            }
-            for (; i < nwd; i += WG) S.bases[i] = src[i];
-        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // chunk k's LDS-DMA has landed
         __syncthreads();
-        if (d.ablate & 1) goto chunk_done;
-        // ---- fast path: single-M reads, branch-free, 4 in flight ----
-#pragma unroll
-        for (int wi = 0; wi < WPW; wi++) {
-            if (wbase + wi >= nw) break;
-            const int pl = (wbase + wi) * 64 + (int)lane;
-            const uint32_t tlo = S.win_lo[wbase + wi], thi = S.win_hi[wbase + wi];
-            uint32_t t = tlo;
-            auto one = [&](uint2 m) -> uint32_t {
-                const uint32_t j = (uint32_t)(pl - (int)m.x);
-                const uint32_t span = (m.y >> 16) & 0x7FFFu;
-                const uint32_t nib = (m.y & 0xFFFFu) + j;
-                const uint32_t word = S.bases[(nib >> 3) & (CH_WORDS - 1)];
-                const uint32_t code = (word >> ((nib & 7u) * 4u)) & 15u;
-                return (j < span && !(m.y >> 31)) ? code * 10u : 60u;   // 60: spill field
-            };
-            for (; t + 4 <= thi; t += 4) {
-                const uint2 m0 = S.meta[t], m1 = S.meta[t + 1], m2 = S.meta[t + 2], m3 = S.meta[t + 3];
-                const uint32_t s0 = one(m0), s1 = one(m1), s2 = one(m2), s3 = one(m3);
-                acc[wi] += (1ull << s0) + (1ull << s1) + (1ull << s2) + (1ull << s3);
-            }
-            for (; t < thi; t++) acc[wi] += 1ull << one(S.meta[t]);
-            if (pl >= n) acc[wi] = 0;
+        // ---- prefetch chunk k+1 (its buffer was last read by chunk k-1, before the barrier) ----
+        if (tid < MAX_WIN) { S.win_lo[cur ^ 1][tid] = 0xFFFFFFFFu; S.win_hi[cur ^ 1][tid] = 0; }
+        if (tid == 0) S.n_slow[cur ^ 1] = 0;
+        if (k + 1 < nchunks) {
+            dma(cur ^ 1, B1, B2, O1, O2);
+            load_meta(k + 1);
         }
-        // ---- slow path: multi-op / maxdel-dropped reads (op walk), compacted list ----
-        {
-            const uint32_t ns = S.n_slow;
+        if (!(d.ablate & 1)) {
+            // ---- fast path: single-M reads, branch-free, 4 in flight ----
+            const uint32_t *bases = S.bases[cur];
+            const uint2 *meta = S.meta[cur];
+#pragma unroll
+            for (int wi = 0; wi < WPW; wi++) {
+                if (wbase + wi >= nw) break;
+                const int pl = (wbase + wi) * 64 + (int)lane;
+                const uint32_t tlo = S.win_lo[cur][wbase + wi], thi = S.win_hi[cur][wbase + wi];
+                uint32_t t = tlo;
+                auto one = [&](uint2 m) -> uint32_t {
+                    const uint32_t j = (uint32_t)(pl - (int)m.x);
+                    const uint32_t span = (m.y >> 16) & 0x7FFFu;
+                    const uint32_t nib = (m.y & 0xFFFFu) + j;
+                    const uint32_t word = bases[(nib >> 3) % (uint32_t)CH_WORDS];
+                    const uint32_t code = (word >> ((nib & 7u) * 4u)) & 15u;
+                    return (j < span && !(m.y >> 31)) ? code * 10u : 60u;   // 60: spill field
+                };
+                for (; t + 4 <= thi; t += 4) {
+                    const uint2 m0 = meta[t], m1 = meta[t + 1], m2 = meta[t + 2], m3 = meta[t + 3];
+                    const uint32_t s0 = one(m0), s1 = one(m1), s2 = one(m2), s3 = one(m3);
+                    acc[wi] += (1ull << s0) + (1ull << s1) + (1ull << s2) + (1ull << s3);
+                }
+                for (; t < thi; t++) acc[wi] += 1ull << one(meta[t]);
+                if (pl >= n) acc[wi] = 0;
+            }
+            // ---- slow path: multi-op / maxdel-dropped reads (op walk), compacted list ----
+            const uint32_t ns = S.n_slow[cur];
             for (uint32_t u = 0; u < ns; u++) {
-                const uint2 sl = S.slow[u];
-                const uint2 m = S.meta[sl.x];
+                const uint2 sl = S.slow[cur][u];
+                const uint2 m = meta[sl.x];
                 const int s_rel = (int)m.x;
                 const uint32_t sp = d.rd_span[r0 + sl.x];
                 const int span = (int)(sp & SPAN_MASK);
                 const bool drop = (sp & DROP) != 0;
-                const uint32_t *ops = fits ? S.ops + (sl.y & 0xFFFFu) : d.ops + op0 + (sl.y & 0xFFFFu);
-                const uint32_t *bw = fits ? S.bases + (m.y & 0xFFFFu) / 8u : d.bases + d.rd_base[r0 + sl.x];
+                const uint32_t *ops = fits ? S.ops[cur] + (sl.y & 0xFFFFu) : d.ops + O0 + (sl.y & 0xFFFFu);
+                const uint32_t *bw = fits ? bases + (m.y & 0xFFFFu) / 8u : d.bases + d.rd_base[r0 + sl.x];
 #pragma unroll
                 for (int wi = 0; wi < WPW; wi++) {
                     const int w0 = (wbase + wi) * 64;
@@ -469,10 +502,10 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
                 }
             }
         }
-    chunk_done:
         fold();
-        __syncthreads();
+        B0 = B1; B1 = B2; O0 = O1; O1 = O2;
     }
+    __syncthreads();
     // ---- long reads overlapping this tile (rare): metadata/ops/bases straight from HBM ----
     for (uint32_t x = xlo; x < xhi; x++) {
         const uint32_t r = uni(d.extras[x]);
