@@ -118,6 +118,46 @@ def run_text(sam_text, argv, device=None):
     return "ok", {k.decode("latin-1"): v.decode("latin-1") for k, v in files.items()}
 
 
+def _dist_env():
+    return int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")), \
+        int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def consensus_files_sharded(filename, thresholds, prefix, min_depth, fill, nchar, maxdel_active, log=None):
+    """One process per GPU (torchrun): every rank parses, runs its position-range shard
+    (sam2consensus_amd.shard), stats are all-reduced over RCCL and the FASTA bodies
+    gathered; rank 0 returns the files, other ranks None."""
+    import torch
+    import torch.distributed as dist
+
+    from .batch import parse_file
+    from .engine import DeviceBatch, Workspace
+    from .records import build_records, render
+    from .shard import run_sharded
+
+    world, rank, local = _dist_env()
+    torch.cuda.set_device(local)
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    hb = parse_file(filename, maxdel_active, 150)
+    if log and rank == 0:
+        log("SAM header processed, " + str(hb.info.n_refs) + " references found.\n")
+        log("A total of " + str(hb.info.lines_total - hb.info.header_lines) + " reads were processed, out of "
+            "which, " + str(hb.info.reads_mapped) + " reads were mapped.\n")
+
+    def runner(sub):
+        ws = Workspace(DeviceBatch(sub, "cuda:%d" % local), thresholds, min_depth, fill)
+        ws.run()
+        return ws.fetch()
+
+    res = run_sharded(hb, rank, world, thresholds, runner)
+    if rank != 0:
+        return None
+    fastas = build_records(hb, thresholds, prefix, *res)
+    pre = prefix.encode("latin-1") if isinstance(prefix, str) else prefix
+    return {n.encode("latin-1") + b"__" + pre + b".fasta": render(r, nchar) for n, r in fastas.items()}
+
+
 def main(argv=None):
     args = build_parser().parse_args(argv)
     filename = args.filename
@@ -131,10 +171,18 @@ def main(argv=None):
         os.makedirs(outfolder)
     outfolder += "/"
     maxdel_active = not isinstance(args.maxdel, str)
-    print("\nProcessing file " + filename + ":\n")
-    res = consensus_files(filename, thresholds, os.fsencode(prefix), args.min_depth, os.fsencode(args.fill),
-                          args.n, maxdel_active, log=lambda s: print(s))
-    for fname, body in res.files.items():                                         # :411-424
+    world, rank, _ = _dist_env()
+    if rank == 0:
+        print("\nProcessing file " + filename + ":\n")
+    if world > 1:
+        files = consensus_files_sharded(filename, thresholds, os.fsencode(prefix), args.min_depth,
+                                        os.fsencode(args.fill), args.n, maxdel_active, log=print)
+        if files is None:
+            return 0
+    else:
+        files = consensus_files(filename, thresholds, os.fsencode(prefix), args.min_depth, os.fsencode(args.fill),
+                                args.n, maxdel_active, log=lambda s: print(s)).files
+    for fname, body in files.items():                                             # :411-424
         path = os.fsencode(outfolder) + fname
         with open(path, "wb") as fh:
             fh.write(body)

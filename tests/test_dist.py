@@ -1,0 +1,114 @@
+"""Multi-rank sharding (sam2consensus_amd/shard.py) on CPU: tile split, sub-batch slicing,
+stats all-reduce and output gather must reproduce the single-shard result byte for byte.
+The per-rank runner is the kernel-shaped CPU model (tests/batch_model.py); on GPU the
+same sub-batches run through libs2c.so (tests/test_gpu.py::test_sharded_on_device)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import batch_model as bm
+import golden_io
+import s2c_oracle as o
+from sam2consensus_amd import batch, configs, records, shard
+
+
+def _files(hb, opt, stats, offs, out):
+    fastas = records.build_records(hb, opt.thresholds, opt.prefix, stats, offs, out)
+    return {n + "__" + opt.prefix + ".fasta": records.render(r, opt.n).decode("latin-1") for n, r in fastas.items()}
+
+
+def _virtual(hb, opt, world):
+    parts, stats = [], None
+    for rank, (t0, t1) in enumerate(shard.split_tiles(hb, world)):
+        sub = shard.SubBatch(hb, t0, t1)
+        st, offs, out = bm.model_pipeline(sub, opt.thresholds, opt.min_depth, opt.fill.encode("latin-1"))
+        stats = st if stats is None else stats + st
+        parts.append((t0, t1, offs, out))
+    offs, out = shard.merge_outputs(parts, len(opt.thresholds))
+    return _files(hb, opt, stats, offs, out)
+
+
+MULTI = golden_io.load("kat")
+
+
+def _big_case():
+    """Several refs with insertions, deletions, long (N) reads and POS=0 wrap."""
+    sam = "@SQ\tSN:a\tLN:900\n@SQ\tSN:b\tLN:3000\n@SQ\tSN:c\tLN:40\n"
+    rows = []
+    for s in range(1, 760, 3):
+        rows.append(("a", s, "60M2I50M", "ACGT" * 28))
+    for s in range(1, 2800, 5):
+        rows.append(("b", s, "40M3D60M", "TTGCA" * 20))
+    rows.append(("b", 10, "10M2000N10M", "G" * 20))
+    rows.append(("c", 0, "5M", "CCCCC"))
+    for r in rows:
+        sam += "r\t0\t%s\t%d\t60\t%s\t*\t0\t0\t%s\t*\n" % r
+    return sam
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
+def test_virtual_ranks_reproduce_reference(world):
+    for case in [c for c in MULTI if c["status"] == "ok"][:12]:
+        opt = o.parse_argv(["-i", "in.sam"] + case["args"])
+        hb = batch.parse_text(case["sam"], opt.maxdel_active, 150)
+        assert _virtual(hb, opt, world) == case["files"], case["name"]
+    sam = _big_case()
+    for args in ([], ["-c", "0.25,0.75"], ["-d", "9"]):
+        opt = o.parse_argv(["-i", "in.sam"] + args)
+        hb = batch.parse_text(sam, opt.maxdel_active, 150)
+        assert _virtual(hb, opt, world) == o.run_case(sam, args)["files"]
+
+
+def test_split_is_balanced_and_contiguous():
+    hb = configs.synth_batch("c2", n_refs=40)
+    for world in (2, 4, 8):
+        rng = shard.split_tiles(hb, world)
+        assert rng[0][0] == 0 and rng[-1][1] == hb.info.n_blocks
+        assert all(rng[k][1] == rng[k + 1][0] for k in range(world - 1))
+        w = shard.tile_weights(hb)
+        loads = [w[a:b].sum() for a, b in rng]
+        assert max(loads) < 1.3 * (sum(loads) / world)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, sam, args, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        opt = o.parse_argv(["-i", "in.sam"] + args)
+        hb = batch.parse_text(sam, opt.maxdel_active, 150)
+        res = shard.run_sharded(hb, rank, world, opt.thresholds,
+                                lambda sub: bm.model_pipeline(sub, opt.thresholds, opt.min_depth,
+                                                              opt.fill.encode("latin-1")))
+        if rank == 0:
+            q.put(_files(hb, opt, *res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_two_ranks_match_reference():
+    import torch.multiprocessing as mp
+    sam = _big_case()
+    args = ["-c", "0.25,0.5"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, sam, args, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert got == o.run_case(sam, args)["files"]

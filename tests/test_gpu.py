@@ -121,3 +121,31 @@ def test_repeated_runs_identical():
         ws.run()
         b = ws.fetch()
         assert (a[0] == b[0]).all() and (a[1] == b[1]).all() and a[2] == b[2]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_on_device(world):
+    """Position-range shards run through libs2c.so and merged == the unsharded run."""
+    from sam2consensus_amd import configs, shard
+    from sam2consensus_amd.engine import DeviceBatch, Workspace
+    from sam2consensus_amd.records import build_records, render
+    thr = [0.25, 0.5, 0.75]
+    hb = configs.synth_batch("c2", n_refs=24)
+
+    def files(stats, offs, out):
+        recs = build_records(hb, thr, "x", stats, offs, out)
+        return {n: render(r, 0) for n, r in recs.items()}
+
+    ws = Workspace(DeviceBatch(hb), thr)
+    ws.run()
+    want = files(*ws.fetch())
+    parts, stats = [], None
+    for t0, t1 in shard.split_tiles(hb, world):
+        sub = shard.SubBatch(hb, t0, t1)
+        w2 = Workspace(DeviceBatch(sub), thr)
+        w2.run()
+        st, offs, out = w2.fetch()
+        stats = st if stats is None else stats + st
+        parts.append((t0, t1, offs, out))
+    offs, out = shard.merge_outputs(parts, len(thr))
+    assert files(stats, offs, out) == want
