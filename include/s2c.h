@@ -54,6 +54,7 @@ int s2c_layout(int64_t *out, int n);
 #define S2C_BLOCK_WORDS   4    /* u32 words per consensus block */
 #define S2C_CODE_FILL     0    /* codes[] value for a fill position */
 #define S2C_CODE_ERR   0xFF    /* codes[] value where the vote hit a missing amb key (:367) */
+#define S2C_TILE_MAX   2048    /* positions per tile */
 
 /* ======================================================================================
  * Host side: SAM/SAM.gz parser → packed read batch          (replaces :147-228, :256-294)
@@ -109,8 +110,12 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
     const uint32_t *rd_base;   /* [n_reads+1] word offset of the read's 4-bit bases (+ end sentinel) */
     const uint32_t *rd_span;   /* [n_reads]   seqout length (bits 0-29); bit30 = a single M op;
                                   bit31 = '-' not counted (maxdel rule :210) */
+    const uint32_t *rd_meta;   /* [n_reads+1][4] kernel read record {start, span|flags, base word, op offset} */
+    const uint32_t *word_lo;   /* [padded_len/32] first short read that may overlap 32-position word W */
+    const uint32_t *word_hi;   /* [padded_len/32] first short read starting after word W */
     const uint32_t *ops;       /* [n_ops]     (len << 1) | cls, cls 0 = M/=/X, 1 = D/N/P */
-    const uint32_t *bases;     /* [n_base_words] 8 codes per word, low nibble first */
+    const uint32_t *bases;     /* [n_base_words] per read: 3 bit-planes of the M bases' codes,
+                                  word-interleaved {p0,p1,p2}[i] + one zero triple */
     const uint32_t *ins_key;   /* [n_ins]     global coordinate of the insertion key (:74) */
     const uint32_t *ins_off;   /* [n_ins+1]   nibble offset of each motif in ins_bases */
     const uint32_t *ins_bases; /* [n_ins_words] */
@@ -165,6 +170,7 @@ int s2c_synth_write(const s2c_synth_spec *spec, const char *path, int64_t *n_rea
 typedef struct {
     /* ---- packed batch (device copies of s2c_batch_arrays) ---- */
     const uint32_t *rd_pos, *rd_op, *rd_base, *rd_span, *ops, *bases;
+    const uint32_t *rd_meta, *word_lo, *word_hi;
     const uint32_t *items, *extras, *blocks, *deep;
     const uint32_t *ins_key, *ins_off, *ins_bases;
     int64_t n_reads, n_items, n_blocks, n_deep, n_ins, n_ins_bases, padded_len;

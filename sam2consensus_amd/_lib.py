@@ -55,7 +55,8 @@ _P32 = C.POINTER(C.c_uint32)
 
 class BatchArrays(C.Structure):
     _fields_ = [("ref_len", _P64), ("ref_off", _P64), ("ref_cov_reads", _P64),
-                ("rd_pos", _P32), ("rd_op", _P32), ("rd_base", _P32), ("rd_span", _P32), ("ops", _P32),
+                ("rd_pos", _P32), ("rd_op", _P32), ("rd_base", _P32), ("rd_span", _P32),
+                ("rd_meta", _P32), ("word_lo", _P32), ("word_hi", _P32), ("ops", _P32),
                 ("bases", _P32),
                 ("ins_key", _P32), ("ins_off", _P32), ("ins_bases", _P32),
                 ("items", _P32), ("extras", _P32), ("blocks", _P32), ("deep", _P32)]
@@ -76,6 +77,7 @@ class Dev(C.Structure):
     """Mirror of ``s2c_dev`` (include/s2c.h)."""
     _fields_ = [
         ("rd_pos", _VP), ("rd_op", _VP), ("rd_base", _VP), ("rd_span", _VP), ("ops", _VP), ("bases", _VP),
+        ("rd_meta", _VP), ("word_lo", _VP), ("word_hi", _VP),
         ("items", _VP), ("extras", _VP), ("blocks", _VP), ("deep", _VP),
         ("ins_key", _VP), ("ins_off", _VP), ("ins_bases", _VP),
         ("n_reads", C.c_int64), ("n_items", C.c_int64), ("n_blocks", C.c_int64), ("n_deep", C.c_int64),

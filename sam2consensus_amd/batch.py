@@ -71,6 +71,9 @@ class HostBatch:
         self.rd_op = _view(a.rd_op, i.n_reads + 1, np.uint32)
         self.rd_base = _view(a.rd_base, i.n_reads + 1, np.uint32)
         self.rd_span = _view(a.rd_span, i.n_reads, np.uint32)
+        self.rd_meta = _view(a.rd_meta, 4 * (i.n_reads + 1), np.uint32).reshape(-1, 4)
+        self.word_lo = _view(a.word_lo, i.padded_len // 32, np.uint32)
+        self.word_hi = _view(a.word_hi, i.padded_len // 32, np.uint32)
         self.ops = _view(a.ops, i.n_ops, np.uint32)
         self.bases = _view(a.bases, i.n_base_words, np.uint32)
         self.ins_key = _view(a.ins_key, i.n_ins, np.uint32)

@@ -147,7 +147,7 @@ struct s2c_parser {
     std::vector<uint64_t> p_op;     // CSR into ops (size n+1)
     std::vector<uint32_t> ops;      // (len<<1)|cls
     std::vector<uint64_t> p_base;   // CSR (word offsets) into words (size n+1)
-    std::vector<uint32_t> words;    // 4-bit codes, 8 per word
+    std::vector<uint32_t> words;    // 3 bit-planes per read, word-interleaved
     // insertion events (file order), raw motif bytes (validated at finish, :287)
     std::vector<uint32_t> i_ref;
     std::vector<int64_t> i_key;
@@ -161,7 +161,7 @@ struct s2c_parser {
     // scratch
     std::vector<Tok> toks;
     std::vector<EffOp> eff;
-    std::vector<uint8_t> codes;
+    std::vector<uint8_t> codes, qcodes;
     std::string last_name;
     int64_t last_ref = -1;
 
@@ -172,7 +172,8 @@ struct s2c_batch {
     s2c_batch_info info{};
     std::vector<std::string> names;
     std::vector<int64_t> ref_len, ref_off, ref_reads;
-    std::vector<uint32_t> rd_pos, rd_op, rd_base, rd_span, ops, bases;
+    std::vector<uint32_t> rd_pos, rd_op, rd_base, rd_span, rd_meta, ops, bases;
+    std::vector<uint32_t> word_lo, word_hi;
     std::vector<uint32_t> ins_key, ins_off, ins_bases;
     std::vector<uint32_t> items, extras, blocks, deep;
 };
@@ -221,14 +222,17 @@ static int parse_sq(s2c_parser *p, const char *s, size_t n) {
 }
 
 // Append piece = seqout[ka, kb) of the current read (eff ops + codes) at ref position pos.
+// Append piece = seqout[ka, kb) of the current read (eff ops + codes) at ref position pos.
+// Bases are packed as 3 bit-planes (bit k of each symbol code), word-interleaved:
+// for query word i (32 bases): {plane0[i], plane1[i], plane2[i]}, plus one zero word
+// triple at the end so a 32-bit window at any offset is a funnel shift of two words.
 static void emit_piece(s2c_parser *p, uint32_t ref, int64_t pos, bool drop, int64_t ka, int64_t kb) {
     int64_t k = 0;
     size_t ci = 0;  // index into p->codes (M bases in seqout order)
     uint32_t nops = 0;
     std::vector<uint8_t> &codes = p->codes;
-    size_t w0 = p->words.size();
-    uint32_t acc = 0;
-    int nib = 0;
+    std::vector<uint8_t> &q = p->qcodes;
+    q.clear();
     for (const EffOp &o : p->eff) {
         int64_t a = std::max(k, ka), b = std::min(k + o.len, kb);
         if (b > a) {
@@ -239,24 +243,28 @@ static void emit_piece(s2c_parser *p, uint32_t ref, int64_t pos, bool drop, int6
                 p->ops.push_back(w);
                 nops++;
             }
-            if (o.cls == 0) {
-                for (int64_t j = a - k; j < b - k; j++) {
-                    acc |= (uint32_t)codes[ci + j] << (4 * nib);
-                    if (++nib == 8) { p->words.push_back(acc); acc = 0; nib = 0; }
-                }
-            }
+            if (o.cls == 0)
+                for (int64_t j = a - k; j < b - k; j++) q.push_back(codes[ci + j]);
         }
         if (o.cls == 0) ci += (size_t)o.len;
         k += o.len;
     }
-    if (nib) p->words.push_back(acc);
+    const size_t nwq = (q.size() + 31) / 32 + 1;
+    const size_t w0 = p->words.size();
+    p->words.resize(w0 + 3 * nwq, 0u);
+    for (size_t j = 0; j < q.size(); j++) {
+        const uint32_t c = q[j], bit = 1u << (j & 31);
+        uint32_t *w = &p->words[w0 + 3 * (j >> 5)];
+        if (c & 1) w[0] |= bit;
+        if (c & 2) w[1] |= bit;
+        if (c & 4) w[2] |= bit;
+    }
     p->p_ref.push_back(ref);
     p->p_pos.push_back(pos);
     p->p_span.push_back((uint32_t)(kb - ka));
     p->p_drop.push_back(drop ? 1 : 0);
     p->p_op.push_back(p->ops.size());
     p->p_base.push_back(p->words.size());
-    (void)w0;
 }
 
 // One SAM line, n includes the trailing '\n' when present (Python 2 line semantics).
@@ -491,7 +499,7 @@ extern "C" int s2c_parser_feed_file(s2c_parser *p, const char *path) {
 // ------------------------------------------------------------------ finish: plan
 namespace {
 constexpr int64_t TP_MIN = 256, TP_MAX = 2048;      // pileup tile bounds (positions)
-constexpr double E_TARGET = 131072.0;                // aligned bases per pileup work item
+constexpr double E_TARGET = 131072.0;                // aligned bases per tile (tile width from depth)
 constexpr int64_t LONG_SPAN = 1024;                  // longer pieces go through per-tile extras
 constexpr uint64_t MAX_SHORT_OPS = 64;               // … and so do pieces with more op words
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
@@ -571,6 +579,12 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
             else order[fill[gstart[i] / S2C_POS_ALIGN]++] = i;
         }
     }
+    // exact start order inside each 64-position bucket (per-word read ranges need it)
+    for (int64_t k = 0; k < NB; k++)
+        if (bucket[k + 1] - bucket[k] > 1)
+            std::sort(order.begin() + bucket[k], order.begin() + bucket[k + 1], [&](int64_t x, int64_t y) {
+                return gstart[x] != gstart[y] ? gstart[x] < gstart[y] : x < y;
+            });
     I.n_reads = NP;
     I.n_long = n_long;
     b->rd_pos.resize(NP);
@@ -611,11 +625,32 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
     }
     I.n_ops = (int64_t)nops;
     I.n_base_words = (int64_t)nwords;
+    // kernel-side read record: {start, span|flags, base word, op offset} (+ sentinel)
+    b->rd_meta.resize(4 * (size_t)(NP + 1));
+    for (int64_t j = 0; j <= NP; j++) {
+        b->rd_meta[4 * j + 0] = j < NP ? b->rd_pos[j] : 0u;
+        b->rd_meta[4 * j + 1] = j < NP ? b->rd_span[j] : 0u;
+        b->rd_meta[4 * j + 2] = b->rd_base[j];
+        b->rd_meta[4 * j + 3] = b->rd_op[j];
+    }
     // prefix max of piece ends (short pieces, sorted order) → first overlapping read per tile
     std::vector<uint64_t> pmax(NS);
     {
         uint64_t m = 0;
         for (int64_t j = 0; j < NS; j++) { m = std::max(m, gend[j]); pmax[j] = m; }
+    }
+    // per 32-position word W: short reads [word_lo[W], word_hi[W]) may overlap it
+    {
+        const int64_t NW = Lpad / 32;
+        b->word_lo.resize(NW);
+        b->word_hi.resize(NW);
+        int64_t jl = 0, jh = 0;
+        for (int64_t W = 0; W < NW; W++) {
+            while (jl < NS && pmax[jl] <= (uint64_t)(32 * W)) jl++;
+            while (jh < NS && b->rd_pos[jh] < (uint64_t)(32 * (W + 1))) jh++;
+            b->word_lo[W] = (uint32_t)jl;
+            b->word_hi[W] = (uint32_t)std::max(jl, jh);
+        }
     }
     // long pieces: per tile lists, built after tiles are known
     // ---- pileup work items ----
@@ -656,11 +691,16 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
     // Each tile is also the consensus/assembly block: a tile whose reads fit one work item
     // is voted in the pileup kernel's epilogue (counts never reach HBM); a chunked
     // ("deep") tile accumulates counts in HBM and is voted by k_consensus.
+    // Per-lane counter capacity (k_pileup's 8-bit vertical counters): a workgroup splits its
+    // 256 lanes into G = 256 / words-per-tile groups that share each word's reads, so a work
+    // item may hold at most 255·G reads; deeper tiles are split into several items.
+    int64_t nwp = 8;
+    while (nwp * 32 < tile_max) nwp *= 2;
+    const int64_t cap_reads = 255 * (256 / nwp);
     for (size_t t = 0; t < tiles.size(); t++) {
         const Tile &T = tiles[t];
-        int64_t nch = std::max<int64_t>(1, (int64_t)std::ceil(T.ev / (2.0 * E_TARGET)));
         int64_t nr = T.hi - T.lo;
-        if (nr < nch) nch = std::max<int64_t>(1, nr);
+        int64_t nch = std::max<int64_t>(1, ceil_div(nr, cap_reads));
         uint32_t x_lo = (uint32_t)b->extras.size();
         for (uint32_t x : tile_x[t]) b->extras.push_back(x);
         uint32_t x_hi = (uint32_t)b->extras.size();
@@ -722,6 +762,9 @@ extern "C" int s2c_batch_arrays_get(const s2c_batch *b, s2c_batch_arrays *o) {
     o->rd_op = b->rd_op.data();
     o->rd_base = b->rd_base.data();
     o->rd_span = b->rd_span.data();
+    o->rd_meta = b->rd_meta.data();
+    o->word_lo = b->word_lo.data();
+    o->word_hi = b->word_hi.data();
     o->ops = b->ops.data();
     o->bases = b->bases.data();
     o->ins_key = b->ins_key.data();

@@ -215,66 +215,54 @@ __global__ void k_ins_scatter(const s2c_dev d) {
 // :370-385), emitted chars compacted per threshold.  Per tile and threshold: output
 // bytes (→ blk_len for the assembly scan) and the record stats sumcov / len / non-'-' /
 // vote errors (:357, :385, :395-396), added into stats[ref][t].
-template <int NP>
-__device__ __forceinline__ void vote_epilogue(const s2c_dev &d, uint32_t tile, uint32_t ref, uint32_t a,
-                                              const int (&pl)[NP], const uint32_t (&cnt)[NP][NSYM],
-                                              uint64_t *sh) {
+template <class Fetch>
+__device__ __forceinline__ void vote_tile(const s2c_dev &d, uint32_t tile, uint32_t ref, uint32_t a, uint32_t n,
+                                          Fetch fetch, uint64_t *sh) {
     const int T = d.n_thr;
-    uint64_t cov[NP];
-    int64_t gs[NP][NSYM];
-    bool called[NP];
-    uint32_t slot[NP];
-#pragma unroll
-    for (int k = 0; k < NP; k++) {
-        cov[k] = 0;
-#pragma unroll
-        for (uint32_t c = 0; c < NSYM; c++) cov[k] += cnt[k][c];
-        called[k] = pl[k] >= 0 && cov[k] > 0 && (int64_t)cov[k] >= (int64_t)d.min_depth;
-        greater_sums(cnt[k], gs[k]);
-        slot[k] = 0xFFFFFFFFu;
-        if (called[k]) {
-            const uint32_t p = a + (uint32_t)pl[k];
-            if (d.ins_bits[p >> 5] >> (p & 31) & 1u) slot[k] = ins_find(d.ins_table, (uint32_t)d.ins_cap, p);
-        }
-    }
     for (int t = 0; t < T; t++) {
         const double thr = d.thresholds[t];
         uint64_t len = 0, nondash = 0, sumcov = 0, nerr = 0;
+#pragma unroll 1
+        for (uint32_t q = threadIdx.x; q < n; q += WG) {
+            const uint32_t p = a + q;
+            uint32_t cnt[NSYM];
+            uint64_t cov = 0;
 #pragma unroll
-        for (int k = 0; k < NP; k++) {
-            if (pl[k] < 0) continue;
-            const uint32_t p = a + (uint32_t)pl[k];
+            for (uint32_t c = 0; c < NSYM; c++) { cnt[c] = fetch(q, c); cov += cnt[c]; }
             uint8_t code = S2C_CODE_FILL;
-            if (called[k]) {
-                const double tc = thr * (double)cov[k];
-                const uint8_t ch = c_amb[vote_mask(cnt[k], gs[k], tc)];
+            if (cov > 0 && (int64_t)cov >= (int64_t)d.min_depth) {   // :359 coverage test
+                int64_t gs[NSYM];
+                greater_sums(cnt, gs);
+                const double tc = thr * (double)cov;
+                const uint8_t ch = c_amb[vote_mask(cnt, gs, tc)];
                 nerr += ch == 0xFF;
                 code = ch;
                 uint32_t emitted = 0;
-                if (slot[k] != 0xFFFFFFFFu) {   // insertion columns after the base (:370-385)
-                    const uint32_t ml = d.ins_table[4 * slot[k] + 1], cb = d.ins_table[4 * slot[k] + 2];
+                if (d.ins_bits[p >> 5] >> (p & 31) & 1u) {   // insertion columns after the base (:370-385)
+                    const uint32_t slot = ins_find(d.ins_table, (uint32_t)d.ins_cap, p);
+                    const uint32_t ml = d.ins_table[4 * slot + 1], cb = d.ins_table[4 * slot + 2];
                     for (uint32_t c = 0; c < ml; c++) {
                         const uint32_t *col = d.ins_cols + (size_t)(cb + c) * NSYM;
                         int64_t v[NSYM];
                         int64_t tot = 0;
 #pragma unroll
                         for (uint32_t j = 0; j < NSYM; j++) { v[j] = col[j]; tot += v[j]; }
-                        v[0] = (int64_t)cov[k] - tot;   // :294 (the column's own '-' count is in the sum)
+                        v[0] = (int64_t)cov - tot;   // :294 (the column's own '-' count is in the sum)
                         int64_t g2[NSYM];
                         greater_sums(v, g2);
                         const uint8_t ic = c_amb[vote_mask(v, g2, tc)];
                         if (ic == 0xFF) { nerr++; continue; }
                         if (ic != '-') d.ins_chr[(size_t)t * d.n_ins_bases + cb + emitted++] = ic;
                     }
-                    d.ins_cnt[(size_t)t * d.ins_cap + slot[k]] = emitted;
+                    d.ins_cnt[(size_t)t * d.ins_cap + slot] = emitted;
                 }
                 len += 1 + emitted;
                 nondash += (ch != '-') + emitted;
-                sumcov += cov[k] * (1 + emitted);
+                sumcov += cov * (1 + emitted);
             } else {
                 len += (uint32_t)d.fill_len;
                 nondash += (uint32_t)d.fill_nondash;
-                sumcov += cov[k];
+                sumcov += cov;
             }
             d.codes[(size_t)t * d.padded_len + p] = code;
         }
@@ -297,261 +285,223 @@ __device__ __forceinline__ void vote_epilogue(const s2c_dev &d, uint32_t tile, u
 }
 
 // ======================================================================= (2) pileup
-// Staged-chunk limits.  The host classifies a piece as "long" (per-tile extras, read
-// straight from HBM) when its span > 1024 or it has > 64 op words, so a short read
-// needs ≤ 129 base words and ≤ 64 ops.  A chunk is ≤ CH reads; if its words or ops do not
-// fit the LDS buffers the chunk takes the HBM path for everything (never seen on the
-// BASELINE configs: 128 reads of 150 bp use ~2.4k words).
-constexpr int CH = 128;           // reads per chunk (< 1023: a 10-bit field never overflows)
-constexpr int CH_WORDS = 3072;    // 12 KiB of packed bases per buffer
-constexpr int CH_OPS = 384;       // op words per buffer
-constexpr int MAX_WIN = 32;       // 64-position windows per tile (tile ≤ 2048 positions)
 constexpr uint32_t SPAN_MASK = 0x3FFFFFFFu, SIMPLE = 0x40000000u, DROP = 0x80000000u;
+constexpr int TILE_MAX = S2C_TILE_MAX;   // positions per tile (≤ 64 words of 32)
 
-struct __attribute__((aligned(16))) ChunkLds {    // double-buffered: chunk k in [k & 1]
-    uint32_t bases[2][CH_WORDS];
-    uint32_t ops[2][CH_OPS];
-    uint2 meta[2][CH];            // x: start - a (signed); y: nibble offset (16b) | span << 16 (15b) | !fast << 31
-    uint2 slow[2][CH];            // x: chunk read index, y: op offset (16b) | nops << 16; reads off the fast path
-    uint32_t win_lo[2][MAX_WIN], win_hi[2][MAX_WIN];
-    uint32_t n_slow[2];
-};
+// 32 query bases starting at query index qs: one 32-bit window per bit-plane, a funnel
+// shift of two consecutive word triples (the packer appends a zero triple per read).
+__device__ __forceinline__ void planes_at(const uint32_t *__restrict__ bw, uint32_t qs, uint32_t (&W)[3]) {
+    const uint32_t *w = bw + 3 * (qs >> 5);
+    const uint32_t sh = qs & 31u;
+    const uint32_t l0 = w[0], l1 = w[1], l2 = w[2], h0 = w[3], h1 = w[4], h2 = w[5];
+    W[0] = __builtin_amdgcn_alignbit(h0, l0, sh);
+    W[1] = __builtin_amdgcn_alignbit(h1, l1, sh);
+    W[2] = __builtin_amdgcn_alignbit(h2, l2, sh);
+}
 
-// code of seqout index j (lane-varying) of a read whose ops/bases sit at (ops, bases);
-// 6 (a field nobody reads) where the lane has nothing to count.
-__device__ __forceinline__ uint32_t seqout_code(const uint32_t *ops, uint32_t nops, const uint32_t *bases, int j,
-                                                bool mine, bool drop) {
-    uint32_t code = 6;
+// CIGAR expansion for one (read, 32-position word) pair: the read's seqout positions
+// [o, o+32) as symbol bit-planes P0..P2 (code = P2·4 + P1·2 + P0) and a mask of the
+// positions it counts.  M/=/X ops copy query bases (:67), D/N/P ops are '-' = code 0
+// (:71), a maxdel-dropped read counts no '-' (:214-218); I/S/H never reach here.
+__device__ __forceinline__ void expand_word(const s2c_dev &d, uint4 m, int o, uint32_t (&P)[3], uint32_t &valid,
+                                            uint32_t next_op) {
+    const uint32_t span = m.y & SPAN_MASK;
+    const uint32_t *bw = d.bases + m.z;
+    P[0] = P[1] = P[2] = 0;
+    valid = 0;
+    const bool simple = (m.y & SIMPLE) != 0, drop = (m.y & DROP) != 0;
+    const uint32_t nops = simple ? 1u : next_op - m.w;
     int k = 0, q = 0;
-    for (uint32_t o = 0; o < nops; o++) {
-        const uint32_t w = ops[o];
+    for (uint32_t op = 0; op < nops; op++) {
+        const uint32_t w = simple ? (span << 1) : d.ops[m.w + op];
         const int len = (int)(w >> 1);
-        const bool m = (w & 1u) == 0;
-        if (mine && (unsigned)(j - k) < (unsigned)len) {
-            if (m) {
-                const uint32_t qi = (uint32_t)(q + j - k);
-                code = (bases[qi >> 3] >> ((qi & 7) * 4)) & 15u;
-            } else {
-                code = 0;
+        const bool isM = (w & 1u) == 0;
+        const int x0 = max(k, o), x1 = min(k + len, o + 32);
+        if (x0 < x1) {
+            const uint32_t bl = (uint32_t)(x0 - o), cnt = (uint32_t)(x1 - x0);
+            const uint32_t mask = (cnt == 32u ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << bl;
+            if (isM) {
+                uint32_t W[3];
+                planes_at(bw, (uint32_t)(q + x0 - k), W);
+                P[0] |= (W[0] << bl) & mask;
+                P[1] |= (W[1] << bl) & mask;
+                P[2] |= (W[2] << bl) & mask;
+                valid |= mask;
+            } else if (!drop) {
+                valid |= mask;
             }
         }
         k += len;
-        q += m ? len : 0;
+        q += isM ? len : 0;
+        if (k >= o + 32) break;
     }
-    return (drop && code == 0) ? 6u : code;
+    if (drop) valid &= P[0] | P[1] | P[2];
 }
 
-__device__ __forceinline__ void lds_dma_dword(const uint32_t *g, uint32_t *l) {
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
-                                     (__attribute__((address_space(3))) void *)l, 4, 0, 0);
+// Six one-hot masks (codes 0..5 = '-',A,C,G,N,T) added into 8-bit vertical counters:
+// V[c][b] bit i = bit b of position i's count of code c.  32 positions per VALU op.
+__device__ __forceinline__ void count_word(uint32_t (&V)[NSYM][8], const uint32_t (&P)[3], uint32_t valid) {
+    const uint32_t x = valid & ~P[2], z = valid & P[2] & ~P[1];
+    const uint32_t y0 = x & ~P[1], y1 = x & P[1];
+    const uint32_t m[NSYM] = {y0 & ~P[0], y0 & P[0], y1 & ~P[0], y1 & P[0], z & ~P[0], z & P[0]};
+#pragma unroll
+    for (uint32_t c = 0; c < NSYM; c++) {
+        uint32_t carry = m[c];
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            const uint32_t t = V[c][b] & carry;
+            V[c][b] ^= carry;
+            carry = t;
+        }
+    }
 }
 
-// One workgroup per work item = (tile [a,b) of one reference, read range [lo,hi) + long-read
-// extras), pulled from an atomic ticket (persistent grid).  Position-major: lane ℓ of a wave
-// owns tile position 64·w + ℓ of each of its windows w and keeps its six counts in
-// registers — a u64 of 10-bit fields per window, += 1 << 10·code per covering read (no
-// atomics), folded into u32 counts after every chunk.  Reads are staged through LDS in
-// chunks of ≤128, double-buffered: while chunk k is counted, chunk k+1's packed bases and
-// op words stream in by LDS-DMA (global_load_lds) and its per-read metadata by plain
-// loads, so a chunk costs one barrier and no exposed HBM round trip.  Single-M-op reads
-// (all but D/N/P reads and maxdel-dropped ones) take a branch-free path: per (read,
-// window) ~13 VALU + 2 LDS reads, 4 reads in flight; the others take the op-walk path
-// from a compacted list.  Only windows inside the tile are visited, so a read straddling
-// a tile edge costs a visit, never a count.  A tile holding its whole depth runs the vote
-// epilogue on its register counts; a deep tile (reads split over items) adds its counts
-// into HBM for k_consensus.
-template <int WPW>
+// One workgroup per work item = (tile [a,b) of ≤2048 positions, read-index window [lo,hi)
+// + long-read extras).  Bit-sliced counting: lane L owns 32-position word w = L mod NWP of
+// the tile and read group g = L / NWP (G = 256/NWP groups); it walks the reads that may
+// cover its word (host-built per-word ranges [word_lo, word_hi), index ≡ g mod G) straight
+// from L2 — one 16-B read record + two 12-B plane windows per read, 4 reads in flight —
+// expands the read's CIGAR over its 32 positions (expand_word) and adds six one-hot masks
+// into 8-bit vertical counters (count_word).  ≤255 reads per lane between flushes (the
+// host sizes items to 255·G reads); a flush transposes each code's 8 planes (8×8 bit
+// transposes on 4 byte lanes at once) and adds the 32 counts into an LDS histogram
+// [6][tile].  A tile holding its whole depth is then voted from LDS (fused epilogue); a
+// deep tile (reads split over items) adds its histogram into HBM for k_consensus.
+template <int NWP>
 __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
-    __shared__ ChunkLds S;
+    constexpr int G = WG / NWP;
+    __shared__ uint32_t hist[NSYM][TILE_MAX];
     __shared__ uint32_t ticket;
     __shared__ uint64_t sh[4];
-    const uint32_t total_words = uni(d.rd_base[d.n_reads]), total_ops = uni(d.rd_op[d.n_reads]);
-    // persistent: each workgroup pulls work items from an atomic ticket (zeroed by k_prep)
+    const uint32_t tid = threadIdx.x;
+    const uint32_t w = tid % NWP, g = tid / NWP;
     for (;;) {
-    if (threadIdx.x == 0) ticket = atomicAdd(&d.scalars[2], 1u);
+    if (tid == 0) ticket = atomicAdd(&d.scalars[2], 1u);
     __syncthreads();
     const uint32_t item = ticket;
-    __syncthreads();
     if (item >= (uint32_t)d.n_items) return;
     const uint32_t *it = d.items + (size_t)item * S2C_ITEM_WORDS;
     const uint32_t a = uni(it[0]), b = uni(it[1]), lo = uni(it[2]), hi = uni(it[3]);
     const uint32_t xlo = uni(it[4]), xhi = uni(it[5]), flags = uni(it[6]);
-    const int n = (int)(b - a), nw = (n + 63) >> 6;
-    const uint32_t tid = threadIdx.x, lane = tid & 63;
-    const int wbase = (int)uni(tid >> 6) * WPW;
-    uint64_t acc[WPW];
-    uint32_t cnt[WPW][NSYM];
-#pragma unroll
-    for (int wi = 0; wi < WPW; wi++) {
-        acc[wi] = 0;
-#pragma unroll
-        for (uint32_t c = 0; c < NSYM; c++) cnt[wi][c] = 0;
-    }
-    auto fold = [&]() {
-#pragma unroll
-        for (int wi = 0; wi < WPW; wi++) {
-#pragma unroll
-            for (uint32_t c = 0; c < NSYM; c++) cnt[wi][c] += (uint32_t)(acc[wi] >> (10 * c)) & 1023u;
-            acc[wi] = 0;
-        }
-    };
-    const uint32_t nchunks = (hi - lo + CH - 1) / CH;
-    auto rb = [&](uint32_t j) { return min(hi, lo + j * CH); };   // first read of chunk j
-    // LDS-DMA of chunk j's words [B0,B1) and ops [O0,O1) into buffer `buf` (if they fit)
-    auto dma = [&](int buf, uint32_t B0, uint32_t B1, uint32_t O0, uint32_t O1) {
-        if (B1 - B0 > (uint32_t)CH_WORDS || O1 - O0 > (uint32_t)CH_OPS) return;
-        const uint32_t w = tid >> 6;
-        for (uint32_t i = w * 64; i < B1 - B0; i += WG)
-            lds_dma_dword(d.bases + min(B0 + i + lane, total_words - 1), &S.bases[buf][i]);
-        for (uint32_t i = w * 64; i < O1 - O0; i += WG)
-            lds_dma_dword(d.ops + min(O0 + i + lane, total_ops - 1), &S.ops[buf][i]);
-    };
-    // chunk-0 prologue: boundaries, DMA, metadata registers
-    uint32_t B0 = uni(d.rd_base[rb(0)]), O0 = uni(d.rd_op[rb(0)]);
-    uint32_t B1 = uni(d.rd_base[rb(1)]), O1 = uni(d.rd_op[rb(1)]);
-    uint32_t m_pos = 0, m_span = 0, m_o = 0, m_o1 = 0, m_bb = 0;
-    auto load_meta = [&](uint32_t j) {
-        const uint32_t rr = rb(j) + tid;
-        if (rr < rb(j + 1)) {
-            m_pos = d.rd_pos[rr]; m_span = d.rd_span[rr]; m_o = d.rd_op[rr]; m_o1 = d.rd_op[rr + 1];
-            m_bb = d.rd_base[rr];
-        }
-    };
-    if (nchunks) {
-        dma(0, B0, B1, O0, O1);
-        load_meta(0);
-    }
-    if (tid < MAX_WIN) { S.win_lo[0][tid] = 0xFFFFFFFFu; S.win_hi[0][tid] = 0; }
-    if (tid == 0) S.n_slow[0] = 0;
+    const uint32_t n = b - a;
+    for (uint32_t i = tid; i < NSYM * (uint32_t)TILE_MAX; i += WG) (&hist[0][0])[i] = 0;
     __syncthreads();
-    for (uint32_t k = 0; k < nchunks; k++) {
-        const int cur = (int)(k & 1);
-        const uint32_t r0 = rb(k), r1 = rb(k + 1);
-        const bool fits = B1 - B0 <= (uint32_t)CH_WORDS && O1 - O0 <= (uint32_t)CH_OPS;
-        const uint32_t B2 = uni(d.rd_base[rb(k + 2)]), O2 = uni(d.rd_op[rb(k + 2)]);
-        // ---- publish chunk k's metadata (registers → LDS), window ranges, slow list ----
-        if (r0 + tid < r1) {
-            const int s_rel = (int)(m_pos - a);
-            const int span = (int)(m_span & SPAN_MASK);
-            const bool fast = fits && (m_span & SIMPLE);
-            S.meta[cur][tid] = make_uint2((uint32_t)s_rel, ((m_bb - B0) * 8u & 0xFFFFu) | ((uint32_t)span << 16) |
-                                                               (fast ? 0u : 0x80000000u));
-            const int e = s_rel + span;
-            if (e > 0 && s_rel < n) {
-                const int wf = (s_rel > 0 ? s_rel : 0) >> 6, wl = ((e < n ? e : n) - 1) >> 6;
-                for (int i = wf; i <= wl; i++) {
-                    atomicMin(&S.win_lo[cur][i], tid);
-                    atomicMax(&S.win_hi[cur][i], tid + 1);
-                }
-                if (!fast) S.slow[cur][atomicAdd(&S.n_slow[cur], 1u)] = make_uint2(tid, (m_o - O0) | ((m_o1 - m_o) << 16));
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // chunk k's LDS-DMA has landed
-        __syncthreads();
-        // ---- prefetch chunk k+1 (its buffer was last read by chunk k-1, before the barrier) ----
-        if (tid < MAX_WIN) { S.win_lo[cur ^ 1][tid] = 0xFFFFFFFFu; S.win_hi[cur ^ 1][tid] = 0; }
-        if (tid == 0) S.n_slow[cur ^ 1] = 0;
-        if (k + 1 < nchunks) {
-            dma(cur ^ 1, B1, B2, O1, O2);
-            load_meta(k + 1);
-        }
-        if (!(d.ablate & 1)) {
-            // ---- fast path: single-M reads, branch-free, 4 in flight ----
-            const uint32_t *bases = S.bases[cur];
-            const uint2 *meta = S.meta[cur];
+    const uint32_t ws = 32u * w;                  // word start, tile-relative
+    const bool active = ws < n;
+    uint32_t V[NSYM][8];
+    auto zeroV = [&]() {
 #pragma unroll
-            for (int wi = 0; wi < WPW; wi++) {
-                if (wbase + wi >= nw) break;
-                const int pl = (wbase + wi) * 64 + (int)lane;
-                const uint32_t tlo = S.win_lo[cur][wbase + wi], thi = S.win_hi[cur][wbase + wi];
-                uint32_t t = tlo;
-                auto one = [&](uint2 m) -> uint32_t {
-                    const uint32_t j = (uint32_t)(pl - (int)m.x);
-                    const uint32_t span = (m.y >> 16) & 0x7FFFu;
-                    const uint32_t nib = (m.y & 0xFFFFu) + j;
-                    const uint32_t word = bases[(nib >> 3) % (uint32_t)CH_WORDS];
-                    const uint32_t code = (word >> ((nib & 7u) * 4u)) & 15u;
-                    return (j < span && !(m.y >> 31)) ? code * 10u : 60u;   // 60: spill field
-                };
-                for (; t + 4 <= thi; t += 4) {
-                    const uint2 m0 = meta[t], m1 = meta[t + 1], m2 = meta[t + 2], m3 = meta[t + 3];
-                    const uint32_t s0 = one(m0), s1 = one(m1), s2 = one(m2), s3 = one(m3);
-                    acc[wi] += (1ull << s0) + (1ull << s1) + (1ull << s2) + (1ull << s3);
-                }
-                for (; t < thi; t++) acc[wi] += 1ull << one(meta[t]);
-                if (pl >= n) acc[wi] = 0;
-            }
-            // ---- slow path: multi-op / maxdel-dropped reads (op walk), compacted list ----
-            const uint32_t ns = S.n_slow[cur];
-            for (uint32_t u = 0; u < ns; u++) {
-                const uint2 sl = S.slow[cur][u];
-                const uint2 m = meta[sl.x];
-                const int s_rel = (int)m.x;
-                const uint32_t sp = d.rd_span[r0 + sl.x];
-                const int span = (int)(sp & SPAN_MASK);
-                const bool drop = (sp & DROP) != 0;
-                const uint32_t *ops = fits ? S.ops[cur] + (sl.y & 0xFFFFu) : d.ops + O0 + (sl.y & 0xFFFFu);
-                const uint32_t *bw = fits ? bases + (m.y & 0xFFFFu) / 8u : d.bases + d.rd_base[r0 + sl.x];
+        for (uint32_t c = 0; c < NSYM; c++)
 #pragma unroll
-                for (int wi = 0; wi < WPW; wi++) {
-                    const int w0 = (wbase + wi) * 64;
-                    if (wbase + wi >= nw || s_rel >= w0 + 64 || s_rel + span <= w0) continue;
-                    const int j = w0 + (int)lane - s_rel;
-                    const bool mine = (unsigned)j < (unsigned)span && w0 + (int)lane < n;
-                    acc[wi] += 1ull << (10u * seqout_code(ops, sl.y >> 16, bw, j, mine, drop));
+            for (int bb = 0; bb < 8; bb++) V[c][bb] = 0;
+    };
+    // counts of this lane's 32 positions → LDS histogram (8×8 bit transposes per byte lane)
+    auto flush = [&]() {
+        if (active) {
+#pragma unroll
+            for (uint32_t c = 0; c < NSYM; c++) {
+                uint32_t R[8];
+#pragma unroll
+                for (int r = 0; r < 8; r++) R[r] = V[c][r];
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const uint32_t t = ((R[r] >> 4) ^ R[r + 4]) & 0x0F0F0F0Fu;
+                    R[r + 4] ^= t;
+                    R[r] ^= t << 4;
                 }
+#pragma unroll
+                for (int r = 0; r < 8; r++) {
+                    if (r & 2) continue;
+                    const uint32_t t = ((R[r] >> 2) ^ R[r + 2]) & 0x33333333u;
+                    R[r + 2] ^= t;
+                    R[r] ^= t << 2;
+                }
+#pragma unroll
+                for (int r = 0; r < 8; r += 2) {
+                    const uint32_t t = ((R[r] >> 1) ^ R[r + 1]) & 0x55555555u;
+                    R[r + 1] ^= t;
+                    R[r] ^= t << 1;
+                }
+                // R[r] byte j = count of position 8j + r
+#pragma unroll
+                for (int r = 0; r < 8; r++)
+#pragma unroll
+                    for (int jb = 0; jb < 4; jb++) {
+                        const uint32_t v = (R[r] >> (8 * jb)) & 0xFFu;
+                        const uint32_t pp = ws + 8u * jb + (uint32_t)r;
+                        if (v && pp < n) atomicAdd(&hist[c][pp], v);
+                    }
             }
         }
-        fold();
-        B0 = B1; B1 = B2; O0 = O1; O1 = O2;
+        zeroV();
+    };
+    zeroV();
+    if (active && !(d.ablate & 1)) {
+        const uint32_t gw = (a >> 5) + w;
+        const uint32_t lw = max(lo, d.word_lo[gw]), hw = min(hi, d.word_hi[gw]);
+        const int wst = (int)(a + ws);
+        // reads with index ≡ g (mod G), in blocks of ≤255 per lane between flushes
+        for (uint32_t tb = lo; tb < hi; tb += 255u * G) {
+            const uint32_t te = min(hw, tb + 255u * G);
+            uint32_t t = max(lw, tb);
+            t += (g + G - t % G) % G;
+            for (; t < te; t += 4 * G) {
+                uint4 m[4];
+                bool ok[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t tt = t + u * G;
+                    ok[u] = tt < te;
+                    m[u] = ok[u] ? *reinterpret_cast<const uint4 *>(d.rd_meta + 4 * (size_t)tt) : make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int o = wst - (int)m[u].x;
+                    if (!ok[u] || o >= (int)(m[u].y & SPAN_MASK) || o <= -32) continue;
+                    const uint32_t nx = (m[u].y & SIMPLE) ? 0u : d.rd_meta[4 * (size_t)(t + u * G + 1) + 3];
+                    uint32_t P[3], valid;
+                    expand_word(d, m[u], o, P, valid, nx);
+                    count_word(V, P, valid);
+                }
+            }
+            if (tb + 255u * G < hi) flush();
+        }
+        // long reads overlapping this tile (rare): same path, groups stride the list
+        for (uint32_t xb = xlo; xb < xhi; xb += 255u * G) {
+            flush();
+            for (uint32_t x = xb + g; x < min(xhi, xb + 255u * G); x += G) {
+                const uint32_t r = d.extras[x];
+                const uint4 m = *reinterpret_cast<const uint4 *>(d.rd_meta + 4 * (size_t)r);
+                const int o = wst - (int)m.x;
+                if (o >= (int)(m.y & SPAN_MASK) || o <= -32) continue;
+                const uint32_t nx = (m.y & SIMPLE) ? 0u : d.rd_meta[4 * (size_t)(r + 1) + 3];
+                uint32_t P[3], valid;
+                expand_word(d, m, o, P, valid, nx);
+                count_word(V, P, valid);
+            }
+        }
     }
+    flush();
     __syncthreads();
-    // ---- long reads overlapping this tile (rare): metadata/ops/bases straight from HBM ----
-    for (uint32_t x = xlo; x < xhi; x++) {
-        const uint32_t r = uni(d.extras[x]);
-        const int s_rel = (int)(uni(d.rd_pos[r]) - a);
-        const uint32_t sp = uni(d.rd_span[r]);
-        const int span = (int)(sp & SPAN_MASK);
-        const uint32_t o = uni(d.rd_op[r]), nops = uni(d.rd_op[r + 1]) - o;
-        const uint32_t *bw = d.bases + uni(d.rd_base[r]);
-#pragma unroll
-        for (int wi = 0; wi < WPW; wi++) {
-            const int w0 = (wbase + wi) * 64;
-            if (wbase + wi >= nw || s_rel >= w0 + 64 || s_rel + span <= w0) continue;
-            const int j = w0 + (int)lane - s_rel;
-            const bool mine = (unsigned)j < (unsigned)span && w0 + (int)lane < n;
-            acc[wi] += 1ull << (10u * seqout_code(d.ops + o, nops, bw, j, mine, (sp & DROP) != 0));
-        }
-        if (((x - xlo) & 255u) == 255u) fold();
-    }
-    fold();
     if (!(flags & 1u) && !(d.ablate & 4)) {   // the tile's whole depth is here: vote it now
-        int pls[WPW];
-#pragma unroll
-        for (int wi = 0; wi < WPW; wi++) {
-            const int pl = (wbase + wi) * 64 + (int)lane;
-            pls[wi] = (wbase + wi < nw && pl < n) ? pl : -1;
-        }
         const uint32_t tile = uni(it[7]);
-        vote_epilogue<WPW>(d, tile, uni(d.blocks[(size_t)tile * S2C_BLOCK_WORDS + 2]), a, pls, cnt, sh);
-        continue;
-    }
-    // ---- deep tile: this chunk's counts → HBM (symbol-major, coalesced atomics); with the
-    //      diagnostic flag 4 every tile stores its counts instead of voting (parity tests) ----
+        vote_tile(d, tile, uni(d.blocks[(size_t)tile * S2C_BLOCK_WORDS + 2]), a, n,
+                  [&](uint32_t q, uint32_t c) { return hist[c][q]; }, sh);
+    } else {
+        // deep tile: this item's counts → HBM (symbol-major, coalesced atomics); with the
+        // diagnostic flag 4 every tile stores its counts instead of voting (parity tests)
+        for (uint32_t q = tid; q < n; q += WG)
 #pragma unroll
-    for (int wi = 0; wi < WPW; wi++) {
-        const int pl = (wbase + wi) * 64 + (int)lane;
-        if (wbase + wi >= nw || pl >= n) continue;
-#pragma unroll
-        for (uint32_t c = 0; c < NSYM; c++) {
-            uint32_t *dst = d.counts + (size_t)c * d.padded_len + a + pl;
-            if (flags & 1u) {
-                if (cnt[wi][c]) atomicAdd(dst, cnt[wi][c]);
-            } else {
-                *dst = cnt[wi][c];
+            for (uint32_t c = 0; c < NSYM; c++) {
+                uint32_t *dst = d.counts + (size_t)c * d.padded_len + a + q;
+                if (flags & 1u) {
+                    if (hist[c][q]) atomicAdd(dst, hist[c][q]);
+                } else {
+                    *dst = hist[c][q];
+                }
             }
-        }
     }
+    __syncthreads();
     }   // for (;;) items
 }
 
@@ -561,17 +511,9 @@ __global__ __launch_bounds__(WG) void k_consensus(const s2c_dev d) {
     const uint32_t tile = d.deep[blockIdx.x];
     const uint32_t *blk = d.blocks + (size_t)tile * S2C_BLOCK_WORDS;
     const uint32_t a = uni(blk[0]), n = uni(blk[1]) - a, ref = uni(blk[2]);
-    constexpr int NP = 2048 / WG;
-    int pl[NP];
-    uint32_t cnt[NP][NSYM];
-#pragma unroll
-    for (int k = 0; k < NP; k++) {
-        const uint32_t q = (uint32_t)k * WG + threadIdx.x;
-        pl[k] = q < n ? (int)q : -1;
-#pragma unroll
-        for (uint32_t c = 0; c < NSYM; c++) cnt[k][c] = q < n ? d.counts[(size_t)c * d.padded_len + a + q] : 0u;
-    }
-    vote_epilogue<NP>(d, tile, ref, a, pl, cnt, sh);
+    const uint32_t *cts = d.counts + a;
+    const size_t L = d.padded_len;
+    vote_tile(d, tile, ref, a, n, [&](uint32_t q, uint32_t c) { return cts[(size_t)c * L + q]; }, sh);
 }
 
 // ======================================================================= assembly
@@ -697,10 +639,11 @@ extern "C" int s2c_workspace_sizes(const s2c_batch_info *info, int32_t n_thr, s2
 static int check_dev(const s2c_dev *d) {
     if (!d) return s2c_set_error(S2C_ERR_ARG, "s2c_dev is NULL");
     if (d->n_thr <= 0) return s2c_set_error(S2C_ERR_ARG, "no thresholds");
-    if (d->tile_max <= 0 || d->tile_max > 64 * MAX_WIN) return s2c_set_error(S2C_ERR_ARG, "tile_max out of range");
+    if (d->tile_max <= 0 || d->tile_max > TILE_MAX) return s2c_set_error(S2C_ERR_ARG, "tile_max out of range");
     if (d->padded_len <= 0 || d->padded_len >= ((int64_t)1 << 32)) return s2c_set_error(S2C_ERR_ARG, "bad padded_len");
     if (d->ins_cap <= 0 || (d->ins_cap & (d->ins_cap - 1))) return s2c_set_error(S2C_ERR_ARG, "ins_cap not pow2");
-    if (d->n_items > 0 && !d->items) return s2c_set_error(S2C_ERR_ARG, "missing pileup buffers");
+    if (d->n_items > 0 && (!d->items || !d->rd_meta || !d->word_lo || !d->word_hi))
+        return s2c_set_error(S2C_ERR_ARG, "missing pileup buffers");
     if (d->n_deep > 0 && (!d->deep || !d->counts)) return s2c_set_error(S2C_ERR_ARG, "missing deep-tile buffers");
     if (d->n_ins > 0 && (!d->ins_key || !d->ins_off || !d->ins_bases || !d->ins_table || !d->ins_cols))
         return s2c_set_error(S2C_ERR_ARG, "missing insertion buffers");
@@ -744,10 +687,10 @@ extern "C" int s2c_pileup(const s2c_dev *d, void *stream) {
     if (rc) return rc;
     if (d->n_items == 0) return S2C_OK;
     hipStream_t s = (hipStream_t)stream;
-    if (d->tile_max <= 256) return launch_persistent(k_pileup<1>, d, s);
-    if (d->tile_max <= 512) return launch_persistent(k_pileup<2>, d, s);
-    if (d->tile_max <= 1024) return launch_persistent(k_pileup<4>, d, s);
-    return launch_persistent(k_pileup<8>, d, s);
+    if (d->tile_max <= 256) return launch_persistent(k_pileup<8>, d, s);
+    if (d->tile_max <= 512) return launch_persistent(k_pileup<16>, d, s);
+    if (d->tile_max <= 1024) return launch_persistent(k_pileup<32>, d, s);
+    return launch_persistent(k_pileup<64>, d, s);
 }
 
 extern "C" int s2c_consensus(const s2c_dev *d, void *stream) {

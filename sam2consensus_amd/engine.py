@@ -52,6 +52,7 @@ class DeviceBatch:
         up = lambda a: _up(a, self.device)  # noqa: E731
         self.rd_pos, self.rd_op, self.rd_base = up(hb.rd_pos), up(hb.rd_op), up(hb.rd_base)
         self.rd_span = up(hb.rd_span)
+        self.rd_meta, self.word_lo, self.word_hi = up(hb.rd_meta.reshape(-1)), up(hb.word_lo), up(hb.word_hi)
         self.ops, self.bases = up(hb.ops), up(hb.bases)
         self.items, self.extras, self.blocks = up(hb.items.reshape(-1)), up(hb.extras), up(hb.blocks.reshape(-1))
         self.deep = up(hb.deep)
@@ -96,6 +97,7 @@ class Workspace:
         d = L.Dev()
         d.rd_pos, d.rd_op, d.rd_base = _ptr(db.rd_pos), _ptr(db.rd_op), _ptr(db.rd_base)
         d.rd_span = _ptr(db.rd_span)
+        d.rd_meta, d.word_lo, d.word_hi = _ptr(db.rd_meta), _ptr(db.word_lo), _ptr(db.word_hi)
         d.ops, d.bases = _ptr(db.ops), _ptr(db.bases)
         d.items, d.extras, d.blocks, d.deep = _ptr(db.items), _ptr(db.extras), _ptr(db.blocks), _ptr(db.deep)
         d.ins_key, d.ins_off, d.ins_bases = _ptr(db.ins_key), _ptr(db.ins_off), _ptr(db.ins_bases)

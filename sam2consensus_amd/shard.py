@@ -62,6 +62,17 @@ class SubBatch:
         self.ops = np.concatenate([hb.ops[a:b] for a, b in zip(op_lo, op_hi)]) if len(reads) else np.zeros(0, np.uint32)
         self.bases = (np.concatenate([hb.bases[a:b] for a, b in zip(b_lo, b_hi)]) if len(reads)
                       else np.zeros(0, np.uint32))
+        # kernel read records {start, span|flags, base word, op offset} + sentinel
+        self.rd_meta = np.zeros((len(reads) + 1, 4), np.uint32)
+        self.rd_meta[:-1, 0] = self.rd_pos
+        self.rd_meta[:-1, 1] = self.rd_span
+        self.rd_meta[:, 2] = self.rd_base
+        self.rd_meta[:, 3] = self.rd_op
+        # per-word short-read ranges, re-indexed to this shard's read window
+        n_sub = r_hi - r_lo
+        self.word_lo = np.clip(hb.word_lo.astype(np.int64) - r_lo, 0, n_sub).astype(np.uint32)
+        self.word_hi = np.maximum(np.clip(hb.word_hi.astype(np.int64) - r_lo, 0, n_sub),
+                                  self.word_lo).astype(np.uint32)
         # items / extras re-indexed
         extras = []
         for row in it:

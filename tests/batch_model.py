@@ -35,8 +35,9 @@ def read_codes(hb, r):
     ops = [(int(w) & 1, int(w) >> 1) for w in hb.ops[o0:o1]]
     nm = sum(l for c, l in ops if c == 0)
     w0 = int(hb.rd_base[r])
-    words = hb.bases[w0:w0 + (nm + 7) // 8].astype(np.uint64)
-    codes = [(int(words[q >> 3]) >> (4 * (q & 7))) & 15 for q in range(nm)]
+    assert int(hb.rd_base[r + 1]) - w0 == 3 * ((nm + 31) // 32 + 1)
+    words = hb.bases[w0:w0 + 3 * ((nm + 31) // 32)].astype(np.int64)
+    codes = [sum(((int(words[3 * (q >> 5) + k]) >> (q & 31)) & 1) << k for k in range(3)) for q in range(nm)]
     return int(hb.rd_pos[r]), drop, ops, codes
 
 
