@@ -169,8 +169,9 @@ int s2c_synth_write(const s2c_synth_spec *spec, const char *path, int64_t *n_rea
  * ====================================================================================== */
 typedef struct {
     /* ---- packed batch (device copies of s2c_batch_arrays) ---- */
-    const uint32_t *rd_pos, *rd_op, *rd_base, *rd_span, *ops, *bases;
-    const uint32_t *rd_meta, *word_lo, *word_hi;
+    const uint32_t *rd_meta;   /* [n_reads+1][4] {start, span|flags, base word, op offset} */
+    const uint32_t *bases;     /* planar seqout words (s2c_batch_arrays.bases) */
+    const uint32_t *word_lo, *word_hi;   /* [padded_len/32] per-word short-read ranges */
     const uint32_t *items, *extras, *blocks, *deep;
     const uint32_t *ins_key, *ins_off, *ins_bases;
     int64_t n_reads, n_items, n_blocks, n_deep, n_ins, n_ins_bases, padded_len;
@@ -186,7 +187,7 @@ typedef struct {
 
     /* ---- workspace (caller allocates; sizes from s2c_workspace_sizes) ---- */
     uint32_t *counts;          /* [6][padded_len] pileup counts of deep tiles (SoA by symbol) */
-    uint32_t *ins_table;       /* [ins_cap][4] {key, maxlen, colbase, pad}; ins_cap pow2 */
+    uint32_t *ins_table;       /* [ins_cap][4] {key+1, maxlen, colbase, cov if called}; ins_cap pow2 */
     int64_t   ins_cap;
     uint32_t *ins_cols;        /* [n_ins_bases][6] insertion column counts */
     uint32_t *ins_cnt;         /* [T][ins_cap] emitted insertion chars per key */
@@ -201,9 +202,10 @@ typedef struct {
     uint8_t  *out;             /* assembled consensus bytes, [t][block] order; size = blk_len[T*n_blocks] */
     int64_t   out_cap;
 
-    /* ---- diagnostics, 0 in the product: bit 1 skips counting, bit 2 skips base staging
-     *      (timing ablations, results wrong: scripts/ablate.py); bit 4 makes every tile
-     *      store its counts to `counts` instead of voting (counts parity tests) ---- */
+    /* ---- diagnostics, 0 in the product: bit 1 skips counting, bit 2 loads without
+     *      counting, bit 8 skips the histogram flush (timing ablations, results wrong:
+     *      scripts/ablate.py); bit 4 makes every tile store its counts to `counts`
+     *      (sized 6*padded_len*4) instead of voting (counts parity tests) ---- */
     int32_t   ablate;
     int32_t   reserved;
 } s2c_dev;

@@ -76,8 +76,7 @@ _VP = C.c_void_p
 class Dev(C.Structure):
     """Mirror of ``s2c_dev`` (include/s2c.h)."""
     _fields_ = [
-        ("rd_pos", _VP), ("rd_op", _VP), ("rd_base", _VP), ("rd_span", _VP), ("ops", _VP), ("bases", _VP),
-        ("rd_meta", _VP), ("word_lo", _VP), ("word_hi", _VP),
+        ("rd_meta", _VP), ("bases", _VP), ("word_lo", _VP), ("word_hi", _VP),
         ("items", _VP), ("extras", _VP), ("blocks", _VP), ("deep", _VP),
         ("ins_key", _VP), ("ins_off", _VP), ("ins_bases", _VP),
         ("n_reads", C.c_int64), ("n_items", C.c_int64), ("n_blocks", C.c_int64), ("n_deep", C.c_int64),

@@ -222,10 +222,12 @@ static int parse_sq(s2c_parser *p, const char *s, size_t n) {
 }
 
 // Append piece = seqout[ka, kb) of the current read (eff ops + codes) at ref position pos.
-// Append piece = seqout[ka, kb) of the current read (eff ops + codes) at ref position pos.
-// Bases are packed as 3 bit-planes (bit k of each symbol code), word-interleaved:
-// for query word i (32 bases): {plane0[i], plane1[i], plane2[i]}, plus one zero word
-// triple at the end so a 32-bit window at any offset is a funnel shift of two words.
+// The piece's seqout (:64-81: M/=/X bases, D/N/P as '-' = code 0) is packed as 3
+// bit-planes (bit k of each symbol code), word-interleaved: for seqout word i (32
+// positions) {plane0[i], plane1[i], plane2[i]}, plus one zero triple at the end so a
+// 32-bit window at any offset is a funnel shift of two triples.  The device never walks
+// the CIGAR: a read's 32 positions under a word are one window load.  The effective ops
+// are kept on the host (planner, CPU model); SIMPLE marks single-M-op pieces.
 static void emit_piece(s2c_parser *p, uint32_t ref, int64_t pos, bool drop, int64_t ka, int64_t kb) {
     int64_t k = 0;
     size_t ci = 0;  // index into p->codes (M bases in seqout order)
@@ -245,6 +247,8 @@ static void emit_piece(s2c_parser *p, uint32_t ref, int64_t pos, bool drop, int6
             }
             if (o.cls == 0)
                 for (int64_t j = a - k; j < b - k; j++) q.push_back(codes[ci + j]);
+            else
+                q.insert(q.end(), (size_t)(b - a), (uint8_t)0);   // D/N/P: '-' (code 0) in seqout (:71)
         }
         if (o.cls == 0) ci += (size_t)o.len;
         k += o.len;
@@ -596,9 +600,10 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
         nops += p->p_op[i + 1] - p->p_op[i];
         nwords += p->p_base[i + 1] - p->p_base[i];
     }
-    if (nops >= (1ull << 31) || nwords >= (1ull << 32)) {
+    // the pileup kernel addresses read records and seqout words with 32-bit byte offsets
+    if (nops >= (1ull << 31) || nwords >= (1ull << 30) || NP >= ((int64_t)1 << 28) - 1) {
         delete b;
-        return s2c_set_error(S2C_ERR_LIMIT, "batch exceeds 2^31 ops or 2^32 base words");
+        return s2c_set_error(S2C_ERR_LIMIT, "batch exceeds 2^31 ops, 2^30 seqout words or 2^28 read pieces (split the input)");
     }
     b->ops.resize(nops);
     b->bases.resize(nwords);
@@ -659,12 +664,18 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
     struct Tile { int64_t a, b, lo, hi; double ev; int64_t ref; };
     std::vector<Tile> tiles;
     int64_t tile_max = S2C_POS_ALIGN;
+    // diagnostic override of the tile width (S2C_TILE_POS, a multiple of 64 in [64, 2048])
+    int64_t tile_force = 0;
+    if (const char *e = getenv("S2C_TILE_POS")) {
+        tile_force = align_up(std::min<int64_t>(std::max<int64_t>(atoll(e), 64), TP_MAX), S2C_POS_ALIGN);
+    }
     for (int64_t r = 0; r < R; r++) {
         const int64_t L = p->ref_len[r], off = b->ref_off[r];
         if (L == 0) continue;
         double depth = (double)ref_events[r] / (double)L;
         int64_t tp = depth > 0 ? align_up((int64_t)std::ceil(E_TARGET / depth), S2C_POS_ALIGN) : TP_MAX;
         tp = std::min(std::max(tp, TP_MIN), TP_MAX);
+        if (tile_force > 0) tp = tile_force;
         // spread the ref evenly over ceil(L/tp) tiles, each a multiple of 64
         int64_t nt = ceil_div(L, tp);
         int64_t step = align_up(ceil_div(L, nt), S2C_POS_ALIGN);

@@ -112,7 +112,7 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
     x ^= x >> 16; x *= 0x85ebca6bu; x ^= x >> 13; x *= 0xc2b2ae35u; x ^= x >> 16;
     return x;
 }
-// table entry: {key+1 (0 = empty), maxlen, colbase, unused}
+// table entry: {key+1 (0 = empty), maxlen, colbase, cov of the key if called (else 0)}
 __device__ __forceinline__ uint32_t ins_find(const uint32_t *__restrict__ tab, uint32_t cap, uint32_t key) {
     uint32_t h = hash32(key) & (cap - 1);
     for (uint32_t probe = 0; probe < cap; probe++) {
@@ -151,8 +151,8 @@ __global__ __launch_bounds__(WG) void k_prep(const s2c_dev d) {
 // (:264-271) motif multiplicities and (:284-287) per-column sums are additive, so the
 // column counts are accumulated straight from the events: column c of key k gets +1 at
 // motif[c] for every event at k with len > c.  The hash table maps key → slot with the
-// longest motif (:278-281) and a column base; the columns are voted (with '-' =
-// cov[key] − Σ column, :294) in the tile epilogue that owns the key's position.
+// longest motif (:278-281), a column base and (set by the vote) the key's coverage; the
+// columns are voted (with '-' = cov[key] − Σ column, :294) by k_ins_vote.
 __global__ void k_ins_build(const s2c_dev d) {
     const uint32_t e = blockIdx.x * WG + threadIdx.x;
     if (e >= d.n_ins) return;
@@ -209,78 +209,138 @@ __global__ void k_ins_scatter(const s2c_dev d) {
 }
 
 // ======================================================================= (4) vote epilogue
-// Per position: the closed-form vote for every threshold, the IUPAC char (or fill when
-// cov == 0 or cov < min_depth, :356-389), and — at a called position carrying an
-// insertion key — the insertion columns' votes with '-' = cov − Σ column (:290-311,
-// :370-385), emitted chars compacted per threshold.  Per tile and threshold: output
-// bytes (→ blk_len for the assembly scan) and the record stats sumcov / len / non-'-' /
-// vote errors (:357, :385, :395-396), added into stats[ref][t].
+// Per position: the closed-form vote for every threshold and the IUPAC char (or fill when
+// cov == 0 or cov < min_depth, :356-389).  Per tile: len and sumcov do not depend on the
+// threshold (1 per called position or len(fill); cov, :357/:385), the per-threshold
+// non-'-' and vote-error counts are wave ballots.  At a called position carrying an
+// insertion key the key's coverage is stored into its hash slot; k_ins_vote then votes
+// the insertion columns (:290-311, :370-385) and adds their chars to the same stats.
+constexpr int VT_TMAX = 16;   // thresholds per pass over the tile's positions
+constexpr int VT_ACC = 2 + 2 * VT_TMAX;   // LDS u64: sumcov, len, {nondash, nerr}[VT_TMAX]
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// acc: LDS [VT_ACC] u64; amb: LDS copy of c_amb.
 template <class Fetch>
 __device__ __forceinline__ void vote_tile(const s2c_dev &d, uint32_t tile, uint32_t ref, uint32_t a, uint32_t n,
-                                          Fetch fetch, uint64_t *sh) {
+                                          Fetch fetch, unsigned long long *acc, const uint8_t *amb) {
     const int T = d.n_thr;
-    for (int t = 0; t < T; t++) {
-        const double thr = d.thresholds[t];
-        uint64_t len = 0, nondash = 0, sumcov = 0, nerr = 0;
-#pragma unroll 1
-        for (uint32_t q = threadIdx.x; q < n; q += WG) {
-            const uint32_t p = a + q;
+    const uint32_t lane = threadIdx.x & 63;
+    for (int t0 = 0; t0 < T; t0 += VT_TMAX) {
+        const int t1 = min(T, t0 + VT_TMAX);
+        if (threadIdx.x < (uint32_t)VT_ACC && (t0 == 0 || threadIdx.x >= 2)) acc[threadIdx.x] = 0;
+        __syncthreads();
+        uint64_t sumcov = 0, len = 0;
+        for (uint32_t q0 = 0; q0 < n; q0 += WG) {   // uniform trip count: every lane votes in the ballots
+            const uint32_t q = q0 + threadIdx.x, p = a + q;
+            const bool in = q < n;
             uint32_t cnt[NSYM];
             uint64_t cov = 0;
 #pragma unroll
-            for (uint32_t c = 0; c < NSYM; c++) { cnt[c] = fetch(q, c); cov += cnt[c]; }
-            uint8_t code = S2C_CODE_FILL;
-            if (cov > 0 && (int64_t)cov >= (int64_t)d.min_depth) {   // :359 coverage test
-                int64_t gs[NSYM];
-                greater_sums(cnt, gs);
-                const double tc = thr * (double)cov;
-                const uint8_t ch = c_amb[vote_mask(cnt, gs, tc)];
-                nerr += ch == 0xFF;
-                code = ch;
-                uint32_t emitted = 0;
-                if (d.ins_bits[p >> 5] >> (p & 31) & 1u) {   // insertion columns after the base (:370-385)
-                    const uint32_t slot = ins_find(d.ins_table, (uint32_t)d.ins_cap, p);
-                    const uint32_t ml = d.ins_table[4 * slot + 1], cb = d.ins_table[4 * slot + 2];
-                    for (uint32_t c = 0; c < ml; c++) {
-                        const uint32_t *col = d.ins_cols + (size_t)(cb + c) * NSYM;
-                        int64_t v[NSYM];
-                        int64_t tot = 0;
-#pragma unroll
-                        for (uint32_t j = 0; j < NSYM; j++) { v[j] = col[j]; tot += v[j]; }
-                        v[0] = (int64_t)cov - tot;   // :294 (the column's own '-' count is in the sum)
-                        int64_t g2[NSYM];
-                        greater_sums(v, g2);
-                        const uint8_t ic = c_amb[vote_mask(v, g2, tc)];
-                        if (ic == 0xFF) { nerr++; continue; }
-                        if (ic != '-') d.ins_chr[(size_t)t * d.n_ins_bases + cb + emitted++] = ic;
-                    }
-                    d.ins_cnt[(size_t)t * d.ins_cap + slot] = emitted;
-                }
-                len += 1 + emitted;
-                nondash += (ch != '-') + emitted;
-                sumcov += cov * (1 + emitted);
-            } else {
-                len += (uint32_t)d.fill_len;
-                nondash += (uint32_t)d.fill_nondash;
+            for (uint32_t c = 0; c < NSYM; c++) { cnt[c] = in ? fetch(q, c) : 0u; cov += cnt[c]; }
+            const bool called = in && cov > 0 && (int64_t)cov >= (int64_t)d.min_depth;   // :359
+            if (t0 == 0) {
                 sumcov += cov;
+                len += called ? 1u : (in ? (uint32_t)d.fill_len : 0u);
+                if (called && (d.ins_bits[p >> 5] >> (p & 31) & 1u))   // key coverage for k_ins_vote
+                    d.ins_table[4 * ins_find(d.ins_table, (uint32_t)d.ins_cap, p) + 3] = (uint32_t)cov;
             }
-            d.codes[(size_t)t * d.padded_len + p] = code;
+            int64_t gs[NSYM];
+            greater_sums(cnt, gs);
+            const uint32_t n_unc = (uint32_t)__popcll(__ballot(in && !called));
+            for (int t = t0; t < t1; t++) {
+                const double tc = d.thresholds[t] * (double)cov;
+                const uint8_t code = called ? amb[vote_mask(cnt, gs, tc)] : (uint8_t)S2C_CODE_FILL;
+                if (in) d.codes[(size_t)t * d.padded_len + p] = code;
+                const uint32_t nd = (uint32_t)__popcll(__ballot(called && code != '-'));
+                const uint32_t ne = (uint32_t)__popcll(__ballot(called && code == 0xFF));
+                if (lane == 0) {
+                    atomicAdd(&acc[2 + 2 * (t - t0)], (unsigned long long)(nd + (uint64_t)d.fill_nondash * n_unc));
+                    if (ne) atomicAdd(&acc[3 + 2 * (t - t0)], (unsigned long long)ne);
+                }
+            }
         }
-        len = block_sum(len, sh);
-        nondash = block_sum(nondash, sh);
-        sumcov = block_sum(sumcov, sh);
-        nerr = block_sum(nerr, sh);
-        if (threadIdx.x == 0) {
+        if (t0 == 0) {
+            sumcov = wave_sum(sumcov);
+            len = wave_sum(len);
+            if (lane == 0) {
+                atomicAdd(&acc[0], (unsigned long long)sumcov);
+                atomicAdd(&acc[1], (unsigned long long)len);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < 4 * (uint32_t)(t1 - t0)) {   // tile totals → stats[ref][t], blk_len
+            const uint32_t t = t0 + threadIdx.x / 4, k = threadIdx.x % 4;
+            const unsigned long long v = k < 2 ? acc[k] : acc[2 + 2 * (t - t0) + (k - 2)];
             uint64_t *st = d.stats + ((size_t)ref * T + t) * 4;
-            atomicAdd((unsigned long long *)&st[0], (unsigned long long)sumcov);
-            atomicAdd((unsigned long long *)&st[1], (unsigned long long)len);
-            atomicAdd((unsigned long long *)&st[2], (unsigned long long)nondash);
-            if (nerr) {
-                atomicAdd((unsigned long long *)&st[3], (unsigned long long)nerr);
-                atomicOr(&d.scalars[1], 1u);
-            }
-            d.blk_len[(size_t)t * d.n_blocks + tile] = len;
+            if (v) atomicAdd((unsigned long long *)&st[k], v);
+            if (k == 3 && v) atomicOr(&d.scalars[1], 1u);
+            if (k == 1) d.blk_len[(size_t)t * d.n_blocks + tile] = v;
         }
+        __syncthreads();
+    }
+}
+
+// Insertion columns of the called keys of one tile (grid = tiles; dynamic LDS [T][4] u64):
+// per column and threshold the same vote with '-' = cov[key] − Σ column (:294, signed);
+// '-' results are skipped, others emitted after the key's base (:370-385) and added to
+// the tile's len / non-'-' / sumcov (cov per emitted char, :385) and block length.
+__global__ __launch_bounds__(WG) void k_ins_vote(const s2c_dev d) {
+    extern __shared__ unsigned long long iacc[];
+    const uint32_t tile = blockIdx.x;
+    const uint32_t *blk = d.blocks + (size_t)tile * S2C_BLOCK_WORDS;
+    const uint32_t a = uni(blk[0]), n = uni(blk[1]) - a, ref = uni(blk[2]);
+    const int T = d.n_thr;
+    bool any = false;
+    for (uint32_t w = (a >> 5) + threadIdx.x; w < ((a + n + 31) >> 5); w += WG) any |= d.ins_bits[w] != 0u;
+    if (!__syncthreads_or(any)) return;
+    for (uint32_t i = threadIdx.x; i < 4u * (uint32_t)T; i += WG) iacc[i] = 0;
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < n; q += WG) {
+        const uint32_t p = a + q;
+        if (!(d.ins_bits[p >> 5] >> (p & 31) & 1u)) continue;
+        const uint32_t slot = ins_find(d.ins_table, (uint32_t)d.ins_cap, p);
+        const uint32_t cov = d.ins_table[4 * slot + 3];
+        if (cov == 0) continue;   // position not called: no insertion chars (:356-358)
+        const uint32_t ml = d.ins_table[4 * slot + 1], cb = d.ins_table[4 * slot + 2];
+        for (int t = 0; t < T; t++) {
+            const double tc = d.thresholds[t] * (double)cov;
+            uint32_t emitted = 0, nerr = 0;
+            for (uint32_t c = 0; c < ml; c++) {
+                const uint32_t *col = d.ins_cols + (size_t)(cb + c) * NSYM;
+                int64_t v[NSYM];
+                int64_t tot = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < NSYM; j++) { v[j] = col[j]; tot += v[j]; }
+                v[0] = (int64_t)cov - tot;   // :294 (the column's own '-' count is in the sum)
+                int64_t g2[NSYM];
+                greater_sums(v, g2);
+                const uint8_t ic = c_amb[vote_mask(v, g2, tc)];
+                if (ic == 0xFF) { nerr++; continue; }
+                if (ic != '-') d.ins_chr[(size_t)t * d.n_ins_bases + cb + emitted++] = ic;
+            }
+            d.ins_cnt[(size_t)t * d.ins_cap + slot] = emitted;
+            if (emitted) {
+                atomicAdd(&iacc[4 * t + 0], (unsigned long long)cov * emitted);
+                atomicAdd(&iacc[4 * t + 1], (unsigned long long)emitted);
+                atomicAdd(&iacc[4 * t + 2], (unsigned long long)emitted);
+            }
+            if (nerr) atomicAdd(&iacc[4 * t + 3], (unsigned long long)nerr);
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < 4u * (uint32_t)T; i += WG) {
+        const unsigned long long v = iacc[i];
+        if (!v) continue;
+        const uint32_t t = i / 4, k = i % 4;
+        atomicAdd((unsigned long long *)&d.stats[((size_t)ref * T + t) * 4 + k], v);
+        if (k == 3) atomicOr(&d.scalars[1], 1u);
+        if (k == 1) atomicAdd((unsigned long long *)&d.blk_len[(size_t)t * d.n_blocks + tile], v);
     }
 }
 
@@ -288,54 +348,22 @@ __device__ __forceinline__ void vote_tile(const s2c_dev &d, uint32_t tile, uint3
 constexpr uint32_t SPAN_MASK = 0x3FFFFFFFu, SIMPLE = 0x40000000u, DROP = 0x80000000u;
 constexpr int TILE_MAX = S2C_TILE_MAX;   // positions per tile (≤ 64 words of 32)
 
-// 32 query bases starting at query index qs: one 32-bit window per bit-plane, a funnel
-// shift of two consecutive word triples (the packer appends a zero triple per read).
-__device__ __forceinline__ void planes_at(const uint32_t *__restrict__ bw, uint32_t qs, uint32_t (&W)[3]) {
-    const uint32_t *w = bw + 3 * (qs >> 5);
-    const uint32_t sh = qs & 31u;
-    const uint32_t l0 = w[0], l1 = w[1], l2 = w[2], h0 = w[3], h1 = w[4], h2 = w[5];
-    W[0] = __builtin_amdgcn_alignbit(h0, l0, sh);
-    W[1] = __builtin_amdgcn_alignbit(h1, l1, sh);
-    W[2] = __builtin_amdgcn_alignbit(h2, l2, sh);
-}
-
-// CIGAR expansion for one (read, 32-position word) pair: the read's seqout positions
-// [o, o+32) as symbol bit-planes P0..P2 (code = P2·4 + P1·2 + P0) and a mask of the
-// positions it counts.  M/=/X ops copy query bases (:67), D/N/P ops are '-' = code 0
-// (:71), a maxdel-dropped read counts no '-' (:214-218); I/S/H never reach here.
-__device__ __forceinline__ void expand_word(const s2c_dev &d, uint4 m, int o, uint32_t (&P)[3], uint32_t &valid,
-                                            uint32_t next_op) {
-    const uint32_t span = m.y & SPAN_MASK;
-    const uint32_t *bw = d.bases + m.z;
-    P[0] = P[1] = P[2] = 0;
-    valid = 0;
-    const bool simple = (m.y & SIMPLE) != 0, drop = (m.y & DROP) != 0;
-    const uint32_t nops = simple ? 1u : next_op - m.w;
-    int k = 0, q = 0;
-    for (uint32_t op = 0; op < nops; op++) {
-        const uint32_t w = simple ? (span << 1) : d.ops[m.w + op];
-        const int len = (int)(w >> 1);
-        const bool isM = (w & 1u) == 0;
-        const int x0 = max(k, o), x1 = min(k + len, o + 32);
-        if (x0 < x1) {
-            const uint32_t bl = (uint32_t)(x0 - o), cnt = (uint32_t)(x1 - x0);
-            const uint32_t mask = (cnt == 32u ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << bl;
-            if (isM) {
-                uint32_t W[3];
-                planes_at(bw, (uint32_t)(q + x0 - k), W);
-                P[0] |= (W[0] << bl) & mask;
-                P[1] |= (W[1] << bl) & mask;
-                P[2] |= (W[2] << bl) & mask;
-                valid |= mask;
-            } else if (!drop) {
-                valid |= mask;
-            }
-        }
-        k += len;
-        q += isM ? len : 0;
-        if (k >= o + 32) break;
-    }
-    if (drop) valid &= P[0] | P[1] | P[2];
+// A read's 32 seqout positions under a word (o = word start − read start, −32 < o < span)
+// from its planar seqout: a funnel shift of the two triples at seqout index max(o, 0),
+// shifted up by max(−o, 0).  L = the six loaded words {lo triple, hi triple}.  The
+// positions counted: [0, span) of the read; a maxdel-dropped read (:214-218) counts no
+// '-' (code 0).  No CIGAR walk: D/N/P are '-' in the packed seqout.
+__device__ __forceinline__ void window(const uint32_t (&L)[6], int o, uint32_t span_flags, bool hit,
+                                       uint32_t (&P)[3], uint32_t &valid) {
+    const uint32_t span = span_flags & SPAN_MASK;
+    const uint32_t qs = (uint32_t)max(o, 0), sh = qs & 31u, bl = (uint32_t)max(-o, 0);
+    P[0] = __builtin_amdgcn_alignbit(L[3], L[0], sh) << bl;
+    P[1] = __builtin_amdgcn_alignbit(L[4], L[1], sh) << bl;
+    P[2] = __builtin_amdgcn_alignbit(L[5], L[2], sh) << bl;
+    const uint32_t nv = min(span - qs, 32u - bl);   // ≥ 1 when hit
+    const uint32_t mask = (nv >= 32u ? 0xFFFFFFFFu : ((1u << nv) - 1u)) << bl;
+    valid = hit ? mask : 0u;
+    if (span_flags & DROP) valid &= P[0] | P[1] | P[2];
 }
 
 // Six one-hot masks (codes 0..5 = '-',A,C,G,N,T) added into 8-bit vertical counters:
@@ -356,25 +384,35 @@ __device__ __forceinline__ void count_word(uint32_t (&V)[NSYM][8], const uint32_
     }
 }
 
-// One workgroup per work item = (tile [a,b) of ≤2048 positions, read-index window [lo,hi)
-// + long-read extras).  Bit-sliced counting: lane L owns 32-position word w = L mod NWP of
-// the tile and read group g = L / NWP (G = 256/NWP groups); it walks the reads that may
-// cover its word (host-built per-word ranges [word_lo, word_hi), index ≡ g mod G) straight
-// from L2 — one 16-B read record + two 12-B plane windows per read, 4 reads in flight —
-// expands the read's CIGAR over its 32 positions (expand_word) and adds six one-hot masks
-// into 8-bit vertical counters (count_word).  ≤255 reads per lane between flushes (the
-// host sizes items to 255·G reads); a flush transposes each code's 8 planes (8×8 bit
-// transposes on 4 byte lanes at once) and adds the 32 counts into an LDS histogram
-// [6][tile].  A tile holding its whole depth is then voted from LDS (fused epilogue); a
-// deep tile (reads split over items) adds its histogram into HBM for k_consensus.
+// One workgroup per work item = (tile [a,b) of ≤ TW = 32·NWP positions, read-index window
+// [lo,hi) + long-read extras).  Bit-sliced counting: lane L owns 32-position word
+// w = L mod NWP of the tile and read group g = L / NWP (G = 256/NWP groups); it walks the
+// reads that may cover its word (host-built per-word ranges [word_lo, word_hi), index ≡ g
+// mod G) straight from L2/HBM, U reads per step with all their loads in flight (one 16-B
+// read record, then one 24-B seqout window each; out-of-range reads load their own first
+// window and are masked), and adds six one-hot masks into 8-bit vertical counters
+// (count_word: 32 positions per VALU op).  ≤255 reads per lane between flushes (the host
+// sizes items to 255·G reads; the kernel also flushes every 255·G indices).  A flush
+// transposes each code's 8 planes (8×8 bit transposes on 4 byte lanes at once) and adds
+// the 32 counts into the LDS histogram [6][TW] (padded 1 word per 32 against bank
+// conflicts).  A tile holding its whole depth is voted from LDS (vote_tile); a deep tile
+// adds its histogram into HBM for k_consensus.
 template <int NWP>
 __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
-    constexpr int G = WG / NWP;
-    __shared__ uint32_t hist[NSYM][TILE_MAX];
+    constexpr int G = WG / NWP, TW = NWP * 32, TWP = TW + TW / 32, U = 4;
+    __shared__ uint32_t hist[NSYM][TWP];
     __shared__ uint32_t ticket;
-    __shared__ uint64_t sh[4];
+    __shared__ unsigned long long acc[VT_ACC];
+    __shared__ uint8_t amb[64];
     const uint32_t tid = threadIdx.x;
     const uint32_t w = tid % NWP, g = tid / NWP;
+    if (tid < 64) amb[tid] = c_amb[tid];   // published by the item loop's first barrier
+    // 32-bit byte offsets from scalar bases (global_load v_off, s[base]); the host caps a
+    // batch at 2^28 read pieces and 2^30 seqout words
+    const char *__restrict__ meta_b = reinterpret_cast<const char *>(d.rd_meta);
+    const char *__restrict__ bases_b = reinterpret_cast<const char *>(d.bases);
+    auto meta = [&](uint32_t r) { return *reinterpret_cast<const uint4 *>(meta_b + r * 16u); };
+    auto words = [&](uint32_t wi) { return reinterpret_cast<const uint32_t *>(bases_b + wi * 4u); };
     for (;;) {
     if (tid == 0) ticket = atomicAdd(&d.scalars[2], 1u);
     __syncthreads();
@@ -384,7 +422,7 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
     const uint32_t a = uni(it[0]), b = uni(it[1]), lo = uni(it[2]), hi = uni(it[3]);
     const uint32_t xlo = uni(it[4]), xhi = uni(it[5]), flags = uni(it[6]);
     const uint32_t n = b - a;
-    for (uint32_t i = tid; i < NSYM * (uint32_t)TILE_MAX; i += WG) (&hist[0][0])[i] = 0;
+    for (uint32_t i = tid; i < NSYM * (uint32_t)TWP; i += WG) (&hist[0][0])[i] = 0;
     __syncthreads();
     const uint32_t ws = 32u * w;                  // word start, tile-relative
     const bool active = ws < n;
@@ -397,7 +435,7 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
     };
     // counts of this lane's 32 positions → LDS histogram (8×8 bit transposes per byte lane)
     auto flush = [&]() {
-        if (active) {
+        if (active && !(d.ablate & 8)) {
 #pragma unroll
             for (uint32_t c = 0; c < NSYM; c++) {
                 uint32_t R[8];
@@ -422,71 +460,76 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
                     R[r + 1] ^= t;
                     R[r] ^= t << 1;
                 }
-                // R[r] byte j = count of position 8j + r
+                // R[r] byte j = count of position 8j + r of the word.  Entries at positions
+                // ≥ n (next tile) are added too but never read.  +w: one pad word per 32.
+                uint32_t *hw0 = &hist[c][ws + w];
 #pragma unroll
                 for (int r = 0; r < 8; r++)
 #pragma unroll
-                    for (int jb = 0; jb < 4; jb++) {
-                        const uint32_t v = (R[r] >> (8 * jb)) & 0xFFu;
-                        const uint32_t pp = ws + 8u * jb + (uint32_t)r;
-                        if (v && pp < n) atomicAdd(&hist[c][pp], v);
-                    }
+                    for (int jb = 0; jb < 4; jb++) atomicAdd(hw0 + 8 * jb + r, (R[r] >> (8 * jb)) & 0xFFu);
             }
         }
         zeroV();
     };
     zeroV();
-    if (active && !(d.ablate & 1)) {
-        const uint32_t gw = (a >> 5) + w;
-        const uint32_t lw = max(lo, d.word_lo[gw]), hw = min(hi, d.word_hi[gw]);
-        const int wst = (int)(a + ws);
-        // reads with index ≡ g (mod G), in blocks of ≤255 per lane between flushes
-        for (uint32_t tb = lo; tb < hi; tb += 255u * G) {
-            const uint32_t te = min(hw, tb + 255u * G);
-            uint32_t t = max(lw, tb);
-            t += (g + G - t % G) % G;
-            for (; t < te; t += 4 * G) {
-                uint4 m[4];
-                bool ok[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const uint32_t tt = t + u * G;
-                    ok[u] = tt < te;
-                    m[u] = ok[u] ? *reinterpret_cast<const uint4 *>(d.rd_meta + 4 * (size_t)tt) : make_uint4(0, 0, 0, 0);
-                }
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int o = wst - (int)m[u].x;
-                    if (!ok[u] || o >= (int)(m[u].y & SPAN_MASK) || o <= -32) continue;
-                    const uint32_t nx = (m[u].y & SIMPLE) ? 0u : d.rd_meta[4 * (size_t)(t + u * G + 1) + 3];
-                    uint32_t P[3], valid;
-                    expand_word(d, m[u], o, P, valid, nx);
-                    count_word(V, P, valid);
-                }
-            }
-            if (tb + 255u * G < hi) flush();
+    // Blocks of ≤255·G read indices (≤255 per lane): the item's short reads [lo, hi)
+    // (restricted per lane to its word's range), then its long-read extras.  One flush per
+    // block, at one site.
+    const uint32_t CAP = 255u * G;
+    const uint32_t nbm = hi > lo ? (hi - lo + CAP - 1) / CAP : 0u;
+    const uint32_t nbx = xhi > xlo ? (xhi - xlo + CAP - 1) / CAP : 0u;
+    const uint32_t nblk = (d.ablate & 1) ? 0u : nbm + nbx;
+    const uint32_t gw = (a >> 5) + w;
+    const uint32_t lw = active ? max(lo, d.word_lo[gw]) : 0u, hw = active ? min(hi, d.word_hi[gw]) : 0u;
+    const uint32_t wst = a + ws;
+    for (uint32_t blk = 0; blk < nblk; blk++) {
+        const bool xmode = blk >= nbm;   // uniform
+        uint32_t s0, e0;
+        if (!xmode) {
+            const uint32_t tb = lo + blk * CAP;
+            s0 = max(lw, tb);
+            e0 = min(hw, tb + CAP);
+        } else {
+            s0 = xlo + (blk - nbm) * CAP;
+            e0 = active ? min(xhi, s0 + CAP) : 0u;
         }
-        // long reads overlapping this tile (rare): same path, groups stride the list
-        for (uint32_t xb = xlo; xb < xhi; xb += 255u * G) {
-            flush();
-            for (uint32_t x = xb + g; x < min(xhi, xb + 255u * G); x += G) {
-                const uint32_t r = d.extras[x];
-                const uint4 m = *reinterpret_cast<const uint4 *>(d.rd_meta + 4 * (size_t)r);
-                const int o = wst - (int)m.x;
-                if (o >= (int)(m.y & SPAN_MASK) || o <= -32) continue;
-                const uint32_t nx = (m.y & SIMPLE) ? 0u : d.rd_meta[4 * (size_t)(r + 1) + 3];
+        uint32_t t = s0 + (g + G - s0 % G) % G;
+        for (; t < e0; t += U * G) {
+            uint4 m[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                uint32_t r = min(t + u * G, e0 - 1);
+                if (xmode) r = d.extras[r];
+                m[u] = meta(r);
+            }
+            uint32_t L[U][6];
+            int o[U];
+            bool hit[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                o[u] = (int)(wst - m[u].x);
+                hit[u] = t + u * G < e0 && o[u] < (int)(m[u].y & SPAN_MASK) && o[u] > -32;
+                const uint32_t qs = hit[u] ? (uint32_t)max(o[u], 0) : 0u;
+                const uint32_t *src = words(m[u].z + 3 * (qs >> 5));
+#pragma unroll
+                for (int k = 0; k < 6; k++) L[u][k] = src[k];
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
                 uint32_t P[3], valid;
-                expand_word(d, m, o, P, valid, nx);
+                window(L[u], o[u], m[u].y, hit[u], P, valid);
+                if (d.ablate & 2) valid = 0;   // diagnostic: loads only
                 count_word(V, P, valid);
             }
         }
+        flush();
     }
-    flush();
     __syncthreads();
+    auto hidx = [](uint32_t q) { return q + (q >> 5); };
     if (!(flags & 1u) && !(d.ablate & 4)) {   // the tile's whole depth is here: vote it now
         const uint32_t tile = uni(it[7]);
         vote_tile(d, tile, uni(d.blocks[(size_t)tile * S2C_BLOCK_WORDS + 2]), a, n,
-                  [&](uint32_t q, uint32_t c) { return hist[c][q]; }, sh);
+                  [&](uint32_t q, uint32_t c) { return hist[c][hidx(q)]; }, acc, amb);
     } else {
         // deep tile: this item's counts → HBM (symbol-major, coalesced atomics); with the
         // diagnostic flag 4 every tile stores its counts instead of voting (parity tests)
@@ -494,10 +537,11 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
 #pragma unroll
             for (uint32_t c = 0; c < NSYM; c++) {
                 uint32_t *dst = d.counts + (size_t)c * d.padded_len + a + q;
+                const uint32_t v = hist[c][hidx(q)];
                 if (flags & 1u) {
-                    if (hist[c][q]) atomicAdd(dst, hist[c][q]);
+                    if (v) atomicAdd(dst, v);
                 } else {
-                    *dst = hist[c][q];
+                    *dst = v;
                 }
             }
     }
@@ -507,13 +551,15 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
 
 // Deep tiles: counts summed in HBM by their work items → the same vote epilogue.
 __global__ __launch_bounds__(WG) void k_consensus(const s2c_dev d) {
-    __shared__ uint64_t sh[4];
+    __shared__ unsigned long long acc[VT_ACC];
+    __shared__ uint8_t amb[64];
+    if (threadIdx.x < 64) amb[threadIdx.x] = c_amb[threadIdx.x];   // published by vote_tile's first barrier
     const uint32_t tile = d.deep[blockIdx.x];
     const uint32_t *blk = d.blocks + (size_t)tile * S2C_BLOCK_WORDS;
     const uint32_t a = uni(blk[0]), n = uni(blk[1]) - a, ref = uni(blk[2]);
     const uint32_t *cts = d.counts + a;
     const size_t L = d.padded_len;
-    vote_tile(d, tile, ref, a, n, [&](uint32_t q, uint32_t c) { return cts[(size_t)c * L + q]; }, sh);
+    vote_tile(d, tile, ref, a, n, [&](uint32_t q, uint32_t c) { return cts[(size_t)c * L + q]; }, acc, amb);
 }
 
 // ======================================================================= assembly
@@ -639,12 +685,14 @@ extern "C" int s2c_workspace_sizes(const s2c_batch_info *info, int32_t n_thr, s2
 static int check_dev(const s2c_dev *d) {
     if (!d) return s2c_set_error(S2C_ERR_ARG, "s2c_dev is NULL");
     if (d->n_thr <= 0) return s2c_set_error(S2C_ERR_ARG, "no thresholds");
+    if (d->n_thr > 1024) return s2c_set_error(S2C_ERR_LIMIT, "more than 1024 thresholds");
     if (d->tile_max <= 0 || d->tile_max > TILE_MAX) return s2c_set_error(S2C_ERR_ARG, "tile_max out of range");
     if (d->padded_len <= 0 || d->padded_len >= ((int64_t)1 << 32)) return s2c_set_error(S2C_ERR_ARG, "bad padded_len");
     if (d->ins_cap <= 0 || (d->ins_cap & (d->ins_cap - 1))) return s2c_set_error(S2C_ERR_ARG, "ins_cap not pow2");
     if (d->n_items > 0 && (!d->items || !d->rd_meta || !d->word_lo || !d->word_hi))
         return s2c_set_error(S2C_ERR_ARG, "missing pileup buffers");
     if (d->n_deep > 0 && (!d->deep || !d->counts)) return s2c_set_error(S2C_ERR_ARG, "missing deep-tile buffers");
+    if ((d->ablate & 4) && !d->counts) return s2c_set_error(S2C_ERR_ARG, "ablate&4 stores all counts: counts buffer required");
     if (d->n_ins > 0 && (!d->ins_key || !d->ins_off || !d->ins_bases || !d->ins_table || !d->ins_cols))
         return s2c_set_error(S2C_ERR_ARG, "missing insertion buffers");
     return S2C_OK;
@@ -696,9 +744,16 @@ extern "C" int s2c_pileup(const s2c_dev *d, void *stream) {
 extern "C" int s2c_consensus(const s2c_dev *d, void *stream) {
     int rc = check_dev(d);
     if (rc) return rc;
-    if (d->n_deep == 0) return S2C_OK;
-    k_consensus<<<(unsigned)d->n_deep, WG, 0, (hipStream_t)stream>>>(*d);
-    return hip_check(hipGetLastError(), "k_consensus");
+    hipStream_t s = (hipStream_t)stream;
+    if (d->n_deep > 0) {
+        k_consensus<<<(unsigned)d->n_deep, WG, 0, s>>>(*d);
+        if ((rc = hip_check(hipGetLastError(), "k_consensus"))) return rc;
+    }
+    if (d->n_ins > 0 && d->n_blocks > 0) {
+        k_ins_vote<<<(unsigned)d->n_blocks, WG, (size_t)32 * d->n_thr, s>>>(*d);
+        if ((rc = hip_check(hipGetLastError(), "k_ins_vote"))) return rc;
+    }
+    return S2C_OK;
 }
 
 extern "C" int s2c_assemble(const s2c_dev *d, void *stream) {

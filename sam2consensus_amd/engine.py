@@ -50,17 +50,16 @@ class DeviceBatch:
         i = hb.info
         self.info = i
         up = lambda a: _up(a, self.device)  # noqa: E731
-        self.rd_pos, self.rd_op, self.rd_base = up(hb.rd_pos), up(hb.rd_op), up(hb.rd_base)
-        self.rd_span = up(hb.rd_span)
+        # read records + planar seqout + per-word read ranges (the CIGAR ops stay on the host)
         self.rd_meta, self.word_lo, self.word_hi = up(hb.rd_meta.reshape(-1)), up(hb.word_lo), up(hb.word_hi)
-        self.ops, self.bases = up(hb.ops), up(hb.bases)
+        self.bases = up(hb.bases)
         self.items, self.extras, self.blocks = up(hb.items.reshape(-1)), up(hb.extras), up(hb.blocks.reshape(-1))
         self.deep = up(hb.deep)
         self.ins_key, self.ins_off, self.ins_bases = up(hb.ins_key), up(hb.ins_off), up(hb.ins_bases)
 
     def nbytes(self):
         return sum(t.numel() * t.element_size() for t in (
-            self.rd_pos, self.rd_op, self.rd_base, self.rd_span, self.ops, self.bases, self.items, self.extras, self.blocks,
+            self.rd_meta, self.word_lo, self.word_hi, self.bases, self.items, self.extras, self.blocks,
             self.ins_key, self.ins_off, self.ins_bases))
 
 
@@ -95,10 +94,8 @@ class Workspace:
         cap = self.T * (i.total_len * max(1, len(fill)) + i.n_ins_bases) + 16
         self.out = u8(cap)
         d = L.Dev()
-        d.rd_pos, d.rd_op, d.rd_base = _ptr(db.rd_pos), _ptr(db.rd_op), _ptr(db.rd_base)
-        d.rd_span = _ptr(db.rd_span)
         d.rd_meta, d.word_lo, d.word_hi = _ptr(db.rd_meta), _ptr(db.word_lo), _ptr(db.word_hi)
-        d.ops, d.bases = _ptr(db.ops), _ptr(db.bases)
+        d.bases = _ptr(db.bases)
         d.items, d.extras, d.blocks, d.deep = _ptr(db.items), _ptr(db.extras), _ptr(db.blocks), _ptr(db.deep)
         d.ins_key, d.ins_off, d.ins_bases = _ptr(db.ins_key), _ptr(db.ins_off), _ptr(db.ins_bases)
         d.n_reads, d.n_items, d.n_blocks, d.n_deep = i.n_reads, i.n_items, i.n_blocks, i.n_deep

@@ -12,14 +12,15 @@ import torch  # noqa: E402
 from sam2consensus_amd import configs  # noqa: E402
 from sam2consensus_amd.engine import DeviceBatch, Workspace  # noqa: E402
 
-MODES = {0: "full", 1: "staging only (skip counting loop)", 2: "skip base-word staging", 3: "1|2"}
+MODES = {0: "full", 1: "skip counting loop", 2: "loads only (no counting)",
+         4: "store counts, no vote", 5: "1|4 (zero+store only)", 6: "2|4", 12: "4|8 (no flush, no vote)"}
 
 
 def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else "c2"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     hb = configs.synth_batch(wl)
-    ws = Workspace(DeviceBatch(hb), [0.25, 0.5, 0.75])
+    ws = Workspace(DeviceBatch(hb), [0.25, 0.5, 0.75], keep_counts=True)   # mode 4 stores all counts
     times = {m: [] for m in MODES}
     for _ in range(reps):
         for m in MODES:

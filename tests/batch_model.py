@@ -26,43 +26,41 @@ def _amb():
 
 
 def read_codes(hb, r):
-    """Expand read r: (start, drop, list of (cls, len), codes of M bases)."""
+    """Read piece r: (start, drop, effective ops [(cls, len)], seqout codes).  The packed
+    planes hold the piece's seqout — M bases and '-' (code 0) for D/N/P — checked here
+    against the effective ops."""
     o0 = int(hb.rd_op[r])
     o1 = int(hb.rd_op[r + 1])
     drop = bool(int(hb.rd_span[r]) >> 31)
-    assert sum(int(w) >> 1 for w in hb.ops[o0:o1]) == int(hb.rd_span[r]) & 0x3FFFFFFF
+    span = int(hb.rd_span[r]) & 0x3FFFFFFF
+    assert sum(int(w) >> 1 for w in hb.ops[o0:o1]) == span
     assert bool(int(hb.rd_span[r]) >> 30 & 1) == (not drop and o1 - o0 == 1 and (int(hb.ops[o0]) & 1) == 0)
     ops = [(int(w) & 1, int(w) >> 1) for w in hb.ops[o0:o1]]
-    nm = sum(l for c, l in ops if c == 0)
     w0 = int(hb.rd_base[r])
-    assert int(hb.rd_base[r + 1]) - w0 == 3 * ((nm + 31) // 32 + 1)
-    words = hb.bases[w0:w0 + 3 * ((nm + 31) // 32)].astype(np.int64)
-    codes = [sum(((int(words[3 * (q >> 5) + k]) >> (q & 31)) & 1) << k for k in range(3)) for q in range(nm)]
+    assert int(hb.rd_base[r + 1]) - w0 == 3 * ((span + 31) // 32 + 1)
+    assert not hb.bases[w0 + 3 * ((span + 31) // 32):w0 + 3 * ((span + 31) // 32 + 1)].any()
+    words = hb.bases[w0:w0 + 3 * ((span + 31) // 32)].astype(np.int64).reshape(-1, 3)
+    q = np.arange(span)
+    bits = (words[q >> 5] >> (q & 31)[:, None]) & 1
+    codes = (bits * np.array([1, 2, 4])).sum(axis=1)
+    k = 0
+    for cls, ln in ops:
+        if cls == 1:
+            assert not codes[k:k + ln].any()
+        k += ln
     return int(hb.rd_pos[r]), drop, ops, codes
 
 
 def read_arrays(hb, r):
-    """Read r as (positions, symbol codes) of the entries the pileup counts."""
+    """Read r as (positions, symbol codes) of the entries the pileup counts: every seqout
+    position, except '-' when the read is maxdel-dropped (:214-218)."""
     s, drop, ops, codes = read_codes(hb, r)
-    pos, sym = [], []
-    k = q = 0
-    for cls, ln in ops:
-        if cls == 0:
-            c = np.asarray(codes[q:q + ln], dtype=np.int64)
-            p = np.arange(s + k, s + k + ln, dtype=np.int64)
-            if drop:
-                keep = c != 0
-                c, p = c[keep], p[keep]
-            pos.append(p)
-            sym.append(c)
-            q += ln
-        elif not drop:
-            pos.append(np.arange(s + k, s + k + ln, dtype=np.int64))
-            sym.append(np.zeros(ln, dtype=np.int64))
-        k += ln
-    if not pos:
-        return np.zeros(0, np.int64), np.zeros(0, np.int64)
-    return np.concatenate(pos), np.concatenate(sym)
+    pos = np.arange(s, s + len(codes), dtype=np.int64)
+    c = np.asarray(codes, dtype=np.int64)
+    if drop:
+        keep = c != 0
+        pos, c = pos[keep], c[keep]
+    return pos, c
 
 
 def model_counts(hb):
