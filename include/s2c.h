@@ -50,7 +50,7 @@ int s2c_layout(int64_t *out, int n);
 /* ---- constants shared with the kernels -------------------------------------------- */
 #define S2C_NSYM          6    /* symbols '-','A','C','G','N','T' — sorted() order (:367) */
 #define S2C_POS_ALIGN    64    /* each reference starts at a multiple of this global coordinate */
-#define S2C_ITEM_WORDS    8    /* u32 words per pileup work item {a, b, lo, hi, xlo, xhi, flags, tile} */
+#define S2C_ITEM_WORDS    4    /* u32 words per pileup work item {a, b, chunk, tile} */
 #define S2C_BLOCK_WORDS   4    /* u32 words per consensus block */
 #define S2C_CODE_FILL     0    /* codes[] value for a fill position */
 #define S2C_CODE_ERR   0xFF    /* codes[] value where the vote hit a missing amb key (:367) */
@@ -61,9 +61,9 @@ int s2c_layout(int64_t *out, int n);
  * ======================================================================================
  * The parser reproduces the reference's record handling exactly (header pass :149-172,
  * record filter :195, RNAME/POS :200-201, parsecigar :46-82, maxdel rule :210, error
- * classes in file order) and emits the packed batch of north_star subsystem (1):
- * reads bucket-sorted by global start, effective CIGAR op words, 4-bit bases,
- * insertion events, and the pileup / consensus work plan.
+ * classes in file order) and emits the packed batch: every read's seqout (:64-81) cut
+ * at the global 32-position grid into word-major records of 3 bit-planes, insertion
+ * events, the pileup / consensus work plan, and a host-side read-piece table.
  */
 typedef struct s2c_parser s2c_parser;
 typedef struct s2c_batch  s2c_batch;
@@ -87,15 +87,14 @@ typedef struct {
     int64_t reads_mapped;      /* records passing :195 */
     int64_t aligned_bases;     /* A = Σ len(seqout) over mapped reads (the metric's unit) */
     int64_t query_bases;       /* Q = M/=/X + I bases packed (B_alg 0.5·Q) */
-    int64_t n_reads;           /* pileup read records (after wrap splitting) */
-    int64_t n_long;            /* of which "long" reads handled through per-tile extras */
+    int64_t n_reads;           /* read pieces (after POS=0 wrap splitting, :212) */
     int64_t n_ops;             /* effective op words (B_alg 4·K) */
-    int64_t n_base_words;      /* u32 words of packed bases */
+    int64_t n_recs;            /* (piece, 32-position word) seqout records */
+    int64_t chunk_recs;        /* records per word per work item (deep tiles take several) */
     int64_t n_ins;             /* insertion events kept (key in [0, LN), non-empty motif) */
     int64_t n_ins_bases;       /* Σ motif lengths */
     int64_t n_ins_words;       /* u32 words of packed motif bases */
     int64_t n_items;           /* pileup work items */
-    int64_t n_extras;          /* extra (long-read) references over all items */
     int64_t n_blocks;          /* tiles = consensus/assembly blocks (never straddle a ref) */
     int64_t tile_max;          /* max positions of any tile (≤ 2048) */
     int64_t n_deep;            /* tiles split over several work items (voted by k_consensus) */
@@ -105,22 +104,17 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
     const int64_t  *ref_len;   /* [n_refs] */
     const int64_t  *ref_off;   /* [n_refs] global coordinate of position 0 */
     const int64_t  *ref_cov_reads; /* [n_refs] pileup records per ref (0 ⇒ Σcov may be 0) */
-    const uint32_t *rd_pos;    /* [n_reads]   global coordinate of seqout char 0 */
+    const uint32_t *rd_pos;    /* [n_reads]   global coordinate of seqout char 0 (file order) */
     const uint32_t *rd_op;     /* [n_reads+1] op offset (CSR) */
-    const uint32_t *rd_base;   /* [n_reads+1] word offset of the read's 4-bit bases (+ end sentinel) */
-    const uint32_t *rd_span;   /* [n_reads]   seqout length (bits 0-29); bit30 = a single M op;
-                                  bit31 = '-' not counted (maxdel rule :210) */
-    const uint32_t *rd_meta;   /* [n_reads+1][4] kernel read record {start, span|flags, base word, op offset} */
-    const uint32_t *word_lo;   /* [padded_len/32] first short read that may overlap 32-position word W */
-    const uint32_t *word_hi;   /* [padded_len/32] first short read starting after word W */
+    const uint32_t *rd_span;   /* [n_reads]   seqout length (bits 0-30); bit31 = '-' not counted (maxdel :210) */
     const uint32_t *ops;       /* [n_ops]     (len << 1) | cls, cls 0 = M/=/X, 1 = D/N/P */
-    const uint32_t *bases;     /* [n_base_words] per read: 3 bit-planes of the M bases' codes,
-                                  word-interleaved {p0,p1,p2}[i] + one zero triple */
+    const uint32_t *wrec;      /* [padded_len/32 + 1] CSR: records of global word W = [wrec[W], wrec[W+1]) */
+    const uint32_t *recs;      /* [n_recs][3] bit-planes {p0,p1,p2} of the 32 positions' codes
+                                  (p2·4+p1·2+p0: 0 '-' 1 A 2 C 3 G 4 N 5 T, 7 = no entry) */
     const uint32_t *ins_key;   /* [n_ins]     global coordinate of the insertion key (:74) */
     const uint32_t *ins_off;   /* [n_ins+1]   nibble offset of each motif in ins_bases */
     const uint32_t *ins_bases; /* [n_ins_words] */
     const uint32_t *items;     /* [n_items][S2C_ITEM_WORDS] pileup work items */
-    const uint32_t *extras;    /* [n_extras] read indices */
     const uint32_t *blocks;    /* [n_blocks][S2C_BLOCK_WORDS] tiles {g_begin, g_end, ref, deep} */
     const uint32_t *deep;      /* [n_deep] indices of deep tiles */
 } s2c_batch_arrays;
@@ -169,12 +163,10 @@ int s2c_synth_write(const s2c_synth_spec *spec, const char *path, int64_t *n_rea
  * ====================================================================================== */
 typedef struct {
     /* ---- packed batch (device copies of s2c_batch_arrays) ---- */
-    const uint32_t *rd_meta;   /* [n_reads+1][4] {start, span|flags, base word, op offset} */
-    const uint32_t *bases;     /* planar seqout words (s2c_batch_arrays.bases) */
-    const uint32_t *word_lo, *word_hi;   /* [padded_len/32] per-word short-read ranges */
-    const uint32_t *items, *extras, *blocks, *deep;
+    const uint32_t *wrec, *recs;   /* word-major seqout records (s2c_batch_arrays) */
+    const uint32_t *items, *blocks, *deep;
     const uint32_t *ins_key, *ins_off, *ins_bases;
-    int64_t n_reads, n_items, n_blocks, n_deep, n_ins, n_ins_bases, padded_len;
+    int64_t n_recs, chunk_recs, n_items, n_blocks, n_deep, n_ins, n_ins_bases, padded_len;
     int32_t tile_max, n_refs;
 
     /* ---- options (:117-138) ---- */

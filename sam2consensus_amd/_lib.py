@@ -25,7 +25,7 @@ S2C_ERR_LIMIT = -13
 
 S2C_NSYM = 6
 S2C_POS_ALIGN = 64
-S2C_ITEM_WORDS = 8
+S2C_ITEM_WORDS = 4
 S2C_BLOCK_WORDS = 4
 S2C_CODE_FILL = 0
 
@@ -45,8 +45,8 @@ class S2CError(RuntimeError):
 class BatchInfo(C.Structure):
     _fields_ = [(n, C.c_int64) for n in (
         "n_refs", "total_len", "padded_len", "header_lines", "lines_total", "reads_mapped",
-        "aligned_bases", "query_bases", "n_reads", "n_long", "n_ops", "n_base_words", "n_ins",
-        "n_ins_bases", "n_ins_words", "n_items", "n_extras", "n_blocks", "tile_max", "n_deep")]
+        "aligned_bases", "query_bases", "n_reads", "n_ops", "n_recs", "chunk_recs", "n_ins",
+        "n_ins_bases", "n_ins_words", "n_items", "n_blocks", "tile_max", "n_deep")]
 
 
 _P64 = C.POINTER(C.c_int64)
@@ -55,11 +55,10 @@ _P32 = C.POINTER(C.c_uint32)
 
 class BatchArrays(C.Structure):
     _fields_ = [("ref_len", _P64), ("ref_off", _P64), ("ref_cov_reads", _P64),
-                ("rd_pos", _P32), ("rd_op", _P32), ("rd_base", _P32), ("rd_span", _P32),
-                ("rd_meta", _P32), ("word_lo", _P32), ("word_hi", _P32), ("ops", _P32),
-                ("bases", _P32),
+                ("rd_pos", _P32), ("rd_op", _P32), ("rd_span", _P32), ("ops", _P32),
+                ("wrec", _P32), ("recs", _P32),
                 ("ins_key", _P32), ("ins_off", _P32), ("ins_bases", _P32),
-                ("items", _P32), ("extras", _P32), ("blocks", _P32), ("deep", _P32)]
+                ("items", _P32), ("blocks", _P32), ("deep", _P32)]
 
 
 class SynthSpec(C.Structure):
@@ -76,10 +75,11 @@ _VP = C.c_void_p
 class Dev(C.Structure):
     """Mirror of ``s2c_dev`` (include/s2c.h)."""
     _fields_ = [
-        ("rd_meta", _VP), ("bases", _VP), ("word_lo", _VP), ("word_hi", _VP),
-        ("items", _VP), ("extras", _VP), ("blocks", _VP), ("deep", _VP),
+        ("wrec", _VP), ("recs", _VP),
+        ("items", _VP), ("blocks", _VP), ("deep", _VP),
         ("ins_key", _VP), ("ins_off", _VP), ("ins_bases", _VP),
-        ("n_reads", C.c_int64), ("n_items", C.c_int64), ("n_blocks", C.c_int64), ("n_deep", C.c_int64),
+        ("n_recs", C.c_int64), ("chunk_recs", C.c_int64),
+        ("n_items", C.c_int64), ("n_blocks", C.c_int64), ("n_deep", C.c_int64),
         ("n_ins", C.c_int64),
         ("n_ins_bases", C.c_int64), ("padded_len", C.c_int64),
         ("tile_max", C.c_int32), ("n_refs", C.c_int32),

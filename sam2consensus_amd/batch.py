@@ -67,20 +67,18 @@ class HostBatch:
         self.ref_len = _view(a.ref_len, i.n_refs, np.int64)
         self.ref_off = _view(a.ref_off, i.n_refs, np.int64)
         self.ref_reads = _view(a.ref_cov_reads, i.n_refs, np.int64)
+        # host-side read-piece table (file order)
         self.rd_pos = _view(a.rd_pos, i.n_reads, np.uint32)
         self.rd_op = _view(a.rd_op, i.n_reads + 1, np.uint32)
-        self.rd_base = _view(a.rd_base, i.n_reads + 1, np.uint32)
         self.rd_span = _view(a.rd_span, i.n_reads, np.uint32)
-        self.rd_meta = _view(a.rd_meta, 4 * (i.n_reads + 1), np.uint32).reshape(-1, 4)
-        self.word_lo = _view(a.word_lo, i.padded_len // 32, np.uint32)
-        self.word_hi = _view(a.word_hi, i.padded_len // 32, np.uint32)
         self.ops = _view(a.ops, i.n_ops, np.uint32)
-        self.bases = _view(a.bases, i.n_base_words, np.uint32)
+        # word-major seqout records (what the pileup kernel reads)
+        self.wrec = _view(a.wrec, i.padded_len // 32 + 1, np.uint32)
+        self.recs = _view(a.recs, 3 * i.n_recs, np.uint32).reshape(-1, 3)
         self.ins_key = _view(a.ins_key, i.n_ins, np.uint32)
         self.ins_off = _view(a.ins_off, i.n_ins + 1, np.uint32)
         self.ins_bases = _view(a.ins_bases, i.n_ins_words, np.uint32)
         self.items = _view(a.items, i.n_items * L.S2C_ITEM_WORDS, np.uint32).reshape(-1, L.S2C_ITEM_WORDS)
-        self.extras = _view(a.extras, i.n_extras, np.uint32)
         self.blocks = _view(a.blocks, i.n_blocks * L.S2C_BLOCK_WORDS, np.uint32).reshape(-1, L.S2C_BLOCK_WORDS)
         self.deep = _view(a.deep, i.n_deep, np.uint32)
         self.names = [lib.s2c_batch_ref_name(self._b, k).decode("latin-1") for k in range(i.n_refs)]

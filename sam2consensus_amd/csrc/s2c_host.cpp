@@ -172,10 +172,10 @@ struct s2c_batch {
     s2c_batch_info info{};
     std::vector<std::string> names;
     std::vector<int64_t> ref_len, ref_off, ref_reads;
-    std::vector<uint32_t> rd_pos, rd_op, rd_base, rd_span, rd_meta, ops, bases;
-    std::vector<uint32_t> word_lo, word_hi;
+    std::vector<uint32_t> rd_pos, rd_op, rd_span, ops;   // host-side read-piece table
+    std::vector<uint32_t> wrec, recs;                     // word-major seqout windows
     std::vector<uint32_t> ins_key, ins_off, ins_bases;
-    std::vector<uint32_t> items, extras, blocks, deep;
+    std::vector<uint32_t> items, blocks, deep;
 };
 
 static int perr(s2c_parser *p, int code, const std::string &msg) {
@@ -503,9 +503,7 @@ extern "C" int s2c_parser_feed_file(s2c_parser *p, const char *path) {
 // ------------------------------------------------------------------ finish: plan
 namespace {
 constexpr int64_t TP_MIN = 256, TP_MAX = 2048;      // pileup tile bounds (positions)
-constexpr double E_TARGET = 131072.0;                // aligned bases per tile (tile width from depth)
-constexpr int64_t LONG_SPAN = 1024;                  // longer pieces go through per-tile extras
-constexpr uint64_t MAX_SHORT_OPS = 64;               // … and so do pieces with more op words
+constexpr double E_TARGET = 262144.0;                // aligned bases per tile (tile width from depth)
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline int64_t align_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }
 }  // namespace
@@ -558,110 +556,90 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
     I.aligned_bases = p->aligned;
     I.query_bases = p->qbases;
 
-    // ---- pieces → global coordinates; bucket sort by start (64-position buckets) ----
+    // ---- read pieces → global coordinates (host-side read table, file order) ----
     const int64_t NP = (int64_t)p->p_ref.size();
     std::vector<uint64_t> gstart(NP);
-    std::vector<uint8_t> is_long(NP);
-    const int64_t NB = Lpad / S2C_POS_ALIGN + 1;
-    std::vector<int64_t> bucket(NB + 1, 0);
-    int64_t n_long = 0;
+    uint64_t nops = 0;
     for (int64_t i = 0; i < NP; i++) {
         gstart[i] = (uint64_t)(b->ref_off[p->p_ref[i]] + p->p_pos[i]);
         b->ref_reads[p->p_ref[i]]++;
-        is_long[i] = p->p_span[i] > LONG_SPAN || p->p_op[i + 1] - p->p_op[i] > MAX_SHORT_OPS;
-        if (is_long[i]) n_long++;
-        else bucket[gstart[i] / S2C_POS_ALIGN + 1]++;
-    }
-    for (int64_t k = 0; k < NB; k++) bucket[k + 1] += bucket[k];
-    const int64_t NS = NP - n_long;
-    std::vector<int64_t> order(NP);
-    {
-        std::vector<int64_t> fill(bucket.begin(), bucket.end() - 1);
-        int64_t li = NS;
-        for (int64_t i = 0; i < NP; i++) {
-            if (is_long[i]) order[li++] = i;
-            else order[fill[gstart[i] / S2C_POS_ALIGN]++] = i;
-        }
-    }
-    // exact start order inside each 64-position bucket (per-word read ranges need it)
-    for (int64_t k = 0; k < NB; k++)
-        if (bucket[k + 1] - bucket[k] > 1)
-            std::sort(order.begin() + bucket[k], order.begin() + bucket[k + 1], [&](int64_t x, int64_t y) {
-                return gstart[x] != gstart[y] ? gstart[x] < gstart[y] : x < y;
-            });
-    I.n_reads = NP;
-    I.n_long = n_long;
-    b->rd_pos.resize(NP);
-    b->rd_op.resize(NP + 1);
-    b->rd_span.resize(NP);
-    b->rd_base.resize(NP + 1);
-    uint64_t nops = 0, nwords = 0;
-    for (int64_t i = 0; i < NP; i++) {
         nops += p->p_op[i + 1] - p->p_op[i];
-        nwords += p->p_base[i + 1] - p->p_base[i];
     }
-    // the pileup kernel addresses read records and seqout words with 32-bit byte offsets
-    if (nops >= (1ull << 31) || nwords >= (1ull << 30) || NP >= ((int64_t)1 << 28) - 1) {
+    if (nops >= (1ull << 32) || NP >= ((int64_t)1 << 32) - 1) {
         delete b;
-        return s2c_set_error(S2C_ERR_LIMIT, "batch exceeds 2^31 ops, 2^30 seqout words or 2^28 read pieces (split the input)");
+        return s2c_set_error(S2C_ERR_LIMIT, "batch exceeds 2^32 ops or read pieces (split the input)");
     }
+    I.n_reads = NP;
+    I.n_ops = (int64_t)nops;
+    b->rd_pos.resize(NP);
+    b->rd_span.resize(NP);
+    b->rd_op.resize(NP + 1);
     b->ops.resize(nops);
-    b->bases.resize(nwords);
-    std::vector<uint64_t> gend(NS);
     {
-        uint64_t oo = 0, ww = 0;
-        for (int64_t j = 0; j < NP; j++) {
-            int64_t i = order[j];
-            b->rd_pos[j] = (uint32_t)gstart[i];
-            const uint64_t no = p->p_op[i + 1] - p->p_op[i], nw = p->p_base[i + 1] - p->p_base[i];
-            b->rd_op[j] = (uint32_t)oo;
-            // bit31: '-' not counted (maxdel); bit30: one M op, counted as is (fast path)
-            const bool simple = !p->p_drop[i] && no == 1 && (p->ops[p->p_op[i]] & 1u) == 0;
-            b->rd_span[j] = p->p_span[i] | (p->p_drop[i] ? 0x80000000u : 0u) | (simple ? 0x40000000u : 0u);
-            b->rd_base[j] = (uint32_t)ww;
+        uint64_t oo = 0;
+        for (int64_t i = 0; i < NP; i++) {
+            const uint64_t no = p->p_op[i + 1] - p->p_op[i];
+            b->rd_pos[i] = (uint32_t)gstart[i];
+            b->rd_span[i] = p->p_span[i] | (p->p_drop[i] ? 0x80000000u : 0u);   // bit31: maxdel drop (:210)
+            b->rd_op[i] = (uint32_t)oo;
             memcpy(&b->ops[oo], &p->ops[p->p_op[i]], no * 4);
-            memcpy(&b->bases[ww], &p->words[p->p_base[i]], nw * 4);
             oo += no;
-            ww += nw;
-            if (j < NS) gend[j] = gstart[i] + p->p_span[i];
         }
         b->rd_op[NP] = (uint32_t)oo;
-        b->rd_base[NP] = (uint32_t)ww;    // sentinel: words of read j = [rd_base[j], rd_base[j+1])
     }
-    I.n_ops = (int64_t)nops;
-    I.n_base_words = (int64_t)nwords;
-    // kernel-side read record: {start, span|flags, base word, op offset} (+ sentinel)
-    b->rd_meta.resize(4 * (size_t)(NP + 1));
-    for (int64_t j = 0; j <= NP; j++) {
-        b->rd_meta[4 * j + 0] = j < NP ? b->rd_pos[j] : 0u;
-        b->rd_meta[4 * j + 1] = j < NP ? b->rd_span[j] : 0u;
-        b->rd_meta[4 * j + 2] = b->rd_base[j];
-        b->rd_meta[4 * j + 3] = b->rd_op[j];
+
+    // ---- word-major seqout windows: one record per (piece, global 32-position word) ----
+    // record = 3 bit-planes of the codes of the word's 32 positions (code = p2·4+p1·2+p0:
+    // 0 '-', 1 A, 2 C, 3 G, 4 N, 5 T; 7 = no entry: outside the piece, or a '-' of a
+    // maxdel-dropped read, :214-218).  Grouped by word (CSR wrec), piece order inside.
+    const int64_t NW = Lpad / 32;
+    b->wrec.assign(NW + 1, 0);
+    uint64_t nrec = 0;
+    for (int64_t i = 0; i < NP; i++) {
+        const uint64_t span = p->p_span[i];
+        if (!span) continue;
+        const uint64_t W0 = gstart[i] >> 5, W1 = (gstart[i] + span - 1) >> 5;
+        for (uint64_t W = W0; W <= W1; W++) b->wrec[W + 1]++;
+        nrec += W1 - W0 + 1;
     }
-    // prefix max of piece ends (short pieces, sorted order) → first overlapping read per tile
-    std::vector<uint64_t> pmax(NS);
+    if (nrec >= (1ull << 32) - 1) {
+        delete b;
+        return s2c_set_error(S2C_ERR_LIMIT, "more than 2^32 seqout word records (split the input)");
+    }
+    for (int64_t W = 0; W < NW; W++) b->wrec[W + 1] += b->wrec[W];
+    I.n_recs = (int64_t)nrec;
+    b->recs.resize(3 * nrec);
     {
-        uint64_t m = 0;
-        for (int64_t j = 0; j < NS; j++) { m = std::max(m, gend[j]); pmax[j] = m; }
-    }
-    // per 32-position word W: short reads [word_lo[W], word_hi[W]) may overlap it
-    {
-        const int64_t NW = Lpad / 32;
-        b->word_lo.resize(NW);
-        b->word_hi.resize(NW);
-        int64_t jl = 0, jh = 0;
-        for (int64_t W = 0; W < NW; W++) {
-            while (jl < NS && pmax[jl] <= (uint64_t)(32 * W)) jl++;
-            while (jh < NS && b->rd_pos[jh] < (uint64_t)(32 * (W + 1))) jh++;
-            b->word_lo[W] = (uint32_t)jl;
-            b->word_hi[W] = (uint32_t)std::max(jl, jh);
+        std::vector<uint32_t> cur(b->wrec.begin(), b->wrec.end() - 1);
+        for (int64_t i = 0; i < NP; i++) {
+            const int64_t span = p->p_span[i];
+            if (!span) continue;
+            const uint32_t *pw = &p->words[p->p_base[i]];   // piece planes + zero pad triple
+            const bool drop = p->p_drop[i] != 0;
+            const int64_t s0 = (int64_t)gstart[i];
+            for (int64_t W = s0 >> 5; W <= (s0 + span - 1) >> 5; W++) {
+                const int64_t o = 32 * W - s0;                    // seqout index of the word's first position
+                const int64_t qs = std::max<int64_t>(o, 0), bl = std::max<int64_t>(-o, 0);
+                const uint32_t *lo = pw + 3 * (qs >> 5), *hi = lo + 3;
+                const uint32_t sh = (uint32_t)(qs & 31);
+                uint32_t P[3];
+                for (int k = 0; k < 3; k++) {
+                    const uint64_t v = ((uint64_t)hi[k] << 32 | lo[k]) >> sh;
+                    P[k] = (uint32_t)v << bl;
+                }
+                const int64_t nv = std::min<int64_t>(span - qs, 32 - bl);
+                uint32_t valid = (nv >= 32 ? 0xFFFFFFFFu : ((1u << nv) - 1u)) << bl;
+                if (drop) valid &= P[0] | P[1] | P[2];
+                uint32_t *r = &b->recs[3 * (size_t)cur[W]++];
+                for (int k = 0; k < 3; k++) r[k] = (P[k] & valid) | ~valid;
+            }
         }
     }
-    // long pieces: per tile lists, built after tiles are known
-    // ---- pileup work items ----
+
+    // ---- tiles (consensus/assembly blocks) and pileup work items ----
     std::vector<int64_t> ref_events(R, 0);
     for (int64_t i = 0; i < NP; i++) ref_events[p->p_ref[i]] += p->p_span[i];
-    struct Tile { int64_t a, b, lo, hi; double ev; int64_t ref; };
+    struct Tile { int64_t a, b, ref; };
     std::vector<Tile> tiles;
     int64_t tile_max = S2C_POS_ALIGN;
     // diagnostic override of the tile width (S2C_TILE_POS, a multiple of 64 in [64, 2048])
@@ -680,46 +658,29 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
         int64_t nt = ceil_div(L, tp);
         int64_t step = align_up(ceil_div(L, nt), S2C_POS_ALIGN);
         for (int64_t a = off; a < off + L; a += step) {
-            int64_t e = std::min(a + step, off + L);
-            int64_t hi = bucket[std::min<int64_t>(align_up(e, S2C_POS_ALIGN) / S2C_POS_ALIGN, NB)];
-            int64_t lo = std::upper_bound(pmax.begin(), pmax.begin() + hi, (uint64_t)a) - pmax.begin();
-            tiles.push_back({a, e, lo, hi, depth * (double)(e - a), r});
-            tile_max = std::max(tile_max, e - a);
+            tiles.push_back({a, std::min(a + step, off + L), r});
+            tile_max = std::max(tile_max, tiles.back().b - a);
         }
     }
     I.tile_max = tile_max;
-    // long pieces → tiles they overlap (tiles are sorted by a)
-    std::vector<std::vector<uint32_t>> tile_x(tiles.size());
-    for (int64_t j = NS; j < NP; j++) {
-        uint64_t s = b->rd_pos[j];
-        uint64_t e = s + p->p_span[order[j]];
-        size_t t0 = std::upper_bound(tiles.begin(), tiles.end(), (int64_t)s,
-                                     [](int64_t v, const Tile &t) { return v < t.a; }) - tiles.begin();
-        if (t0 > 0) t0--;
-        for (size_t t = t0; t < tiles.size() && (uint64_t)tiles[t].a < e; t++)
-            if ((uint64_t)tiles[t].b > s) tile_x[t].push_back((uint32_t)j);
-    }
-    // Each tile is also the consensus/assembly block: a tile whose reads fit one work item
-    // is voted in the pileup kernel's epilogue (counts never reach HBM); a chunked
-    // ("deep") tile accumulates counts in HBM and is voted by k_consensus.
-    // Per-lane counter capacity (k_pileup's 8-bit vertical counters): a workgroup splits its
-    // 256 lanes into G = 256 / words-per-tile groups that share each word's reads, so a work
-    // item may hold at most 255·G reads; deeper tiles are split into several items.
+    // Each tile is also the consensus/assembly block.  k_pileup gives a tile 256 lanes:
+    // one 32-position word per lane × G = 256 / words-per-tile lanes per word, each with
+    // 8-bit counters (≤255 records between flushes).  A work item takes chunk k of every
+    // word's records, [k·chunk, (k+1)·chunk) with chunk = 255·G; a tile whose deepest word
+    // needs one chunk is voted in the kernel's epilogue (counts never reach HBM), a deeper
+    // ("deep") tile adds its chunks' counts into HBM and is voted by k_consensus.
     int64_t nwp = 8;
     while (nwp * 32 < tile_max) nwp *= 2;
-    const int64_t cap_reads = 255 * (256 / nwp);
+    const int64_t chunk = 255 * (256 / nwp);
+    I.chunk_recs = chunk;
     for (size_t t = 0; t < tiles.size(); t++) {
         const Tile &T = tiles[t];
-        int64_t nr = T.hi - T.lo;
-        int64_t nch = std::max<int64_t>(1, ceil_div(nr, cap_reads));
-        uint32_t x_lo = (uint32_t)b->extras.size();
-        for (uint32_t x : tile_x[t]) b->extras.push_back(x);
-        uint32_t x_hi = (uint32_t)b->extras.size();
+        int64_t maxw = 0;
+        for (int64_t W = T.a >> 5; W < (T.b + 31) >> 5; W++)
+            maxw = std::max<int64_t>(maxw, (int64_t)(b->wrec[W + 1] - b->wrec[W]));
+        const int64_t nch = std::max<int64_t>(1, ceil_div(maxw, chunk));
         for (int64_t c = 0; c < nch; c++) {
-            int64_t r0 = T.lo + nr * c / nch, r1 = T.lo + nr * (c + 1) / nch;
-            uint32_t it[S2C_ITEM_WORDS] = {(uint32_t)T.a, (uint32_t)T.b, (uint32_t)r0, (uint32_t)r1,
-                                           c == 0 ? x_lo : x_hi, x_hi,
-                                           (uint32_t)((nch > 1 ? 1u : 0u) | (c == 0 ? 2u : 0u)), (uint32_t)t};
+            uint32_t it[S2C_ITEM_WORDS] = {(uint32_t)T.a, (uint32_t)T.b, (uint32_t)c, (uint32_t)t};
             b->items.insert(b->items.end(), it, it + S2C_ITEM_WORDS);
         }
         uint32_t blk[S2C_BLOCK_WORDS] = {(uint32_t)T.a, (uint32_t)T.b, (uint32_t)T.ref, nch > 1 ? 1u : 0u};
@@ -727,7 +688,6 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
         if (nch > 1) b->deep.push_back((uint32_t)t);
     }
     I.n_items = (int64_t)(b->items.size() / S2C_ITEM_WORDS);
-    I.n_extras = (int64_t)b->extras.size();
     I.n_blocks = (int64_t)(b->blocks.size() / S2C_BLOCK_WORDS);
     I.n_deep = (int64_t)b->deep.size();
 
@@ -771,18 +731,14 @@ extern "C" int s2c_batch_arrays_get(const s2c_batch *b, s2c_batch_arrays *o) {
     o->ref_cov_reads = b->ref_reads.data();
     o->rd_pos = b->rd_pos.data();
     o->rd_op = b->rd_op.data();
-    o->rd_base = b->rd_base.data();
     o->rd_span = b->rd_span.data();
-    o->rd_meta = b->rd_meta.data();
-    o->word_lo = b->word_lo.data();
-    o->word_hi = b->word_hi.data();
     o->ops = b->ops.data();
-    o->bases = b->bases.data();
+    o->wrec = b->wrec.data();
+    o->recs = b->recs.data();
     o->ins_key = b->ins_key.data();
     o->ins_off = b->ins_off.data();
     o->ins_bases = b->ins_bases.data();
     o->items = b->items.data();
-    o->extras = b->extras.data();
     o->blocks = b->blocks.data();
     o->deep = b->deep.data();
     return S2C_OK;

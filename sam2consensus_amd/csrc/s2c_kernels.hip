@@ -8,12 +8,13 @@
 //   k_prep                 zero per-run state (replaces memsets: one launch)
 //   k_ins_build/alloc/     (3) insertion hash table: key → slot, longest motif, column
 //   k_ins_scatter              base, per-column symbol counts (:262-287)
-//   k_pileup               (2) CIGAR expansion + position-major counting per tile, and
-//                          (4) for tiles holding their whole depth, the vote epilogue:
-//                          all thresholds, IUPAC, min-depth/fill, insertion columns,
-//                          per-(ref,t) stats — counts never reach HBM
-//   k_consensus            (4) the same epilogue for "deep" tiles whose reads were split
+//   k_pileup               (2) bit-sliced counting of the word-major seqout records per
+//                          tile (32 positions per VALU op), and (4) for tiles voted in one
+//                          work item the vote epilogue: all thresholds, IUPAC, min-depth/
+//                          fill, per-(ref,t) stats — counts never reach HBM
+//   k_consensus            (4) the same vote for "deep" tiles whose records were split
 //                          over several work items (counts summed in HBM)
+//   k_ins_vote             (4) insertion columns of called keys (:290-311, :370-385)
 //   k_scan / k_assemble    device FASTA body assembly (tile scan + byte scatter)
 //
 // Everything is integer counting; the single floating-point operation is the
@@ -291,50 +292,69 @@ __device__ __forceinline__ void vote_tile(const s2c_dev &d, uint32_t tile, uint3
 // '-' results are skipped, others emitted after the key's base (:370-385) and added to
 // the tile's len / non-'-' / sumcov (cov per emitted char, :385) and block length.
 __global__ __launch_bounds__(WG) void k_ins_vote(const s2c_dev d) {
-    extern __shared__ unsigned long long iacc[];
+    extern __shared__ unsigned long long iacc[];   // [T][4]
+    __shared__ uint32_t em[VT_TMAX][WG];           // emitted chars per (threshold, thread)
+    __shared__ uint8_t amb[64];
+    const uint32_t tid = threadIdx.x;
     const uint32_t tile = blockIdx.x;
     const uint32_t *blk = d.blocks + (size_t)tile * S2C_BLOCK_WORDS;
     const uint32_t a = uni(blk[0]), n = uni(blk[1]) - a, ref = uni(blk[2]);
     const int T = d.n_thr;
     bool any = false;
-    for (uint32_t w = (a >> 5) + threadIdx.x; w < ((a + n + 31) >> 5); w += WG) any |= d.ins_bits[w] != 0u;
+    for (uint32_t w = (a >> 5) + tid; w < ((a + n + 31) >> 5); w += WG) any |= d.ins_bits[w] != 0u;
     if (!__syncthreads_or(any)) return;
-    for (uint32_t i = threadIdx.x; i < 4u * (uint32_t)T; i += WG) iacc[i] = 0;
+    for (uint32_t i = tid; i < 4u * (uint32_t)T; i += WG) iacc[i] = 0;
+    if (tid < 64) amb[tid] = c_amb[tid];
     __syncthreads();
-    for (uint32_t q = threadIdx.x; q < n; q += WG) {
+    const uint32_t *__restrict__ cols = d.ins_cols;
+    uint8_t *__restrict__ chr = d.ins_chr;
+    for (uint32_t q = tid; q < n; q += WG) {
         const uint32_t p = a + q;
         if (!(d.ins_bits[p >> 5] >> (p & 31) & 1u)) continue;
         const uint32_t slot = ins_find(d.ins_table, (uint32_t)d.ins_cap, p);
-        const uint32_t cov = d.ins_table[4 * slot + 3];
+        const uint4 e = *reinterpret_cast<const uint4 *>(d.ins_table + 4 * (size_t)slot);
+        const uint32_t ml = e.y, cb = e.z, cov = e.w;
         if (cov == 0) continue;   // position not called: no insertion chars (:356-358)
-        const uint32_t ml = d.ins_table[4 * slot + 1], cb = d.ins_table[4 * slot + 2];
-        for (int t = 0; t < T; t++) {
-            const double tc = d.thresholds[t] * (double)cov;
-            uint32_t emitted = 0, nerr = 0;
-            for (uint32_t c = 0; c < ml; c++) {
-                const uint32_t *col = d.ins_cols + (size_t)(cb + c) * NSYM;
-                int64_t v[NSYM];
-                int64_t tot = 0;
+        for (int t0 = 0; t0 < T; t0 += VT_TMAX) {
+            const int t1 = min(T, t0 + VT_TMAX);
+            for (int t = t0; t < t1; t++) em[t - t0][tid] = 0;
+            for (uint32_t c0 = 0; c0 < ml; c0 += 4) {   // 4 columns' loads in flight
+                uint32_t cv[4][NSYM];
 #pragma unroll
-                for (uint32_t j = 0; j < NSYM; j++) { v[j] = col[j]; tot += v[j]; }
-                v[0] = (int64_t)cov - tot;   // :294 (the column's own '-' count is in the sum)
-                int64_t g2[NSYM];
-                greater_sums(v, g2);
-                const uint8_t ic = c_amb[vote_mask(v, g2, tc)];
-                if (ic == 0xFF) { nerr++; continue; }
-                if (ic != '-') d.ins_chr[(size_t)t * d.n_ins_bases + cb + emitted++] = ic;
+                for (int u = 0; u < 4; u++)
+#pragma unroll
+                    for (uint32_t j = 0; j < NSYM; j++)
+                        cv[u][j] = c0 + u < ml ? cols[(size_t)(cb + c0 + u) * NSYM + j] : 0u;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (c0 + u >= ml) break;
+                    int64_t v[NSYM];
+                    int64_t tot = 0;
+#pragma unroll
+                    for (uint32_t j = 0; j < NSYM; j++) { v[j] = cv[u][j]; tot += v[j]; }
+                    v[0] = (int64_t)cov - tot;   // :294 (the column's own '-' count is in the sum)
+                    int64_t g2[NSYM];
+                    greater_sums(v, g2);
+                    for (int t = t0; t < t1; t++) {
+                        const uint8_t ic = amb[vote_mask(v, g2, d.thresholds[t] * (double)cov)];
+                        if (ic == 0xFF) { atomicAdd(&iacc[4 * t + 3], 1ull); continue; }
+                        if (ic != '-') chr[(size_t)t * d.n_ins_bases + cb + em[t - t0][tid]++] = ic;
+                    }
+                }
             }
-            d.ins_cnt[(size_t)t * d.ins_cap + slot] = emitted;
-            if (emitted) {
-                atomicAdd(&iacc[4 * t + 0], (unsigned long long)cov * emitted);
-                atomicAdd(&iacc[4 * t + 1], (unsigned long long)emitted);
-                atomicAdd(&iacc[4 * t + 2], (unsigned long long)emitted);
+            for (int t = t0; t < t1; t++) {
+                const uint32_t emitted = em[t - t0][tid];
+                d.ins_cnt[(size_t)t * d.ins_cap + slot] = emitted;
+                if (emitted) {
+                    atomicAdd(&iacc[4 * t + 0], (unsigned long long)cov * emitted);
+                    atomicAdd(&iacc[4 * t + 1], (unsigned long long)emitted);
+                    atomicAdd(&iacc[4 * t + 2], (unsigned long long)emitted);
+                }
             }
-            if (nerr) atomicAdd(&iacc[4 * t + 3], (unsigned long long)nerr);
         }
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < 4u * (uint32_t)T; i += WG) {
+    for (uint32_t i = tid; i < 4u * (uint32_t)T; i += WG) {
         const unsigned long long v = iacc[i];
         if (!v) continue;
         const uint32_t t = i / 4, k = i % 4;
@@ -345,33 +365,15 @@ __global__ __launch_bounds__(WG) void k_ins_vote(const s2c_dev d) {
 }
 
 // ======================================================================= (2) pileup
-constexpr uint32_t SPAN_MASK = 0x3FFFFFFFu, SIMPLE = 0x40000000u, DROP = 0x80000000u;
 constexpr int TILE_MAX = S2C_TILE_MAX;   // positions per tile (≤ 64 words of 32)
 
-// A read's 32 seqout positions under a word (o = word start − read start, −32 < o < span)
-// from its planar seqout: a funnel shift of the two triples at seqout index max(o, 0),
-// shifted up by max(−o, 0).  L = the six loaded words {lo triple, hi triple}.  The
-// positions counted: [0, span) of the read; a maxdel-dropped read (:214-218) counts no
-// '-' (code 0).  No CIGAR walk: D/N/P are '-' in the packed seqout.
-__device__ __forceinline__ void window(const uint32_t (&L)[6], int o, uint32_t span_flags, bool hit,
-                                       uint32_t (&P)[3], uint32_t &valid) {
-    const uint32_t span = span_flags & SPAN_MASK;
-    const uint32_t qs = (uint32_t)max(o, 0), sh = qs & 31u, bl = (uint32_t)max(-o, 0);
-    P[0] = __builtin_amdgcn_alignbit(L[3], L[0], sh) << bl;
-    P[1] = __builtin_amdgcn_alignbit(L[4], L[1], sh) << bl;
-    P[2] = __builtin_amdgcn_alignbit(L[5], L[2], sh) << bl;
-    const uint32_t nv = min(span - qs, 32u - bl);   // ≥ 1 when hit
-    const uint32_t mask = (nv >= 32u ? 0xFFFFFFFFu : ((1u << nv) - 1u)) << bl;
-    valid = hit ? mask : 0u;
-    if (span_flags & DROP) valid &= P[0] | P[1] | P[2];
-}
-
-// Six one-hot masks (codes 0..5 = '-',A,C,G,N,T) added into 8-bit vertical counters:
-// V[c][b] bit i = bit b of position i's count of code c.  32 positions per VALU op.
-__device__ __forceinline__ void count_word(uint32_t (&V)[NSYM][8], const uint32_t (&P)[3], uint32_t valid) {
-    const uint32_t x = valid & ~P[2], z = valid & P[2] & ~P[1];
-    const uint32_t y0 = x & ~P[1], y1 = x & P[1];
-    const uint32_t m[NSYM] = {y0 & ~P[0], y0 & P[0], y1 & ~P[0], y1 & P[0], z & ~P[0], z & P[0]};
+// One record's six one-hot masks (codes 0..5 = '-',A,C,G,N,T; code 7 = no entry matches
+// none) added into 8-bit vertical counters: V[c][b] bit i = bit b of position i's count of
+// code c.  32 positions per VALU op.
+__device__ __forceinline__ void count_record(uint32_t (&V)[NSYM][8], uint32_t p0, uint32_t p1, uint32_t p2) {
+    const uint32_t x = ~p2, z = p2 & ~p1;
+    const uint32_t y0 = x & ~p1, y1 = x & p1;
+    const uint32_t m[NSYM] = {y0 & ~p0, y0 & p0, y1 & ~p0, y1 & p0, z & ~p0, z & p0};
 #pragma unroll
     for (uint32_t c = 0; c < NSYM; c++) {
         uint32_t carry = m[c];
@@ -384,43 +386,34 @@ __device__ __forceinline__ void count_word(uint32_t (&V)[NSYM][8], const uint32_
     }
 }
 
-// One workgroup per work item = (tile [a,b) of ≤ TW = 32·NWP positions, read-index window
-// [lo,hi) + long-read extras).  Bit-sliced counting: lane L owns 32-position word
-// w = L mod NWP of the tile and read group g = L / NWP (G = 256/NWP groups); it walks the
-// reads that may cover its word (host-built per-word ranges [word_lo, word_hi), index ≡ g
-// mod G) straight from L2/HBM, U reads per step with all their loads in flight (one 16-B
-// read record, then one 24-B seqout window each; out-of-range reads load their own first
-// window and are masked), and adds six one-hot masks into 8-bit vertical counters
-// (count_word: 32 positions per VALU op).  ≤255 reads per lane between flushes (the host
-// sizes items to 255·G reads; the kernel also flushes every 255·G indices).  A flush
-// transposes each code's 8 planes (8×8 bit transposes on 4 byte lanes at once) and adds
-// the 32 counts into the LDS histogram [6][TW] (padded 1 word per 32 against bank
-// conflicts).  A tile holding its whole depth is voted from LDS (vote_tile); a deep tile
-// adds its histogram into HBM for k_consensus.
+// One workgroup per work item = (tile [a,b) of ≤ TW = 32·NWP positions, chunk k).  Lane
+// L owns 32-position word w = L mod NWP of the tile and lane group g = L / NWP (G = 256/NWP
+// lanes per word).  The word's seqout records [wrec[W], wrec[W+1]) are cut into chunks of
+// chunk_recs; the item streams chunk k, lane g taking records ≡ g (mod G), U independent
+// 12-B loads in flight (a group's lanes read consecutive records: coalesced), and adds each
+// record's six one-hot masks into 8-bit vertical counters (count_record).  Every 255·G
+// records (≤255 per lane) a flush transposes each code's 8 planes (8×8 bit transposes on
+// 4 byte lanes at once) and adds the 32 counts into the LDS histogram [6][TW] (padded one
+// word per 32).  A tile voted in one item (not deep) is voted from LDS (vote_tile); a deep
+// tile's chunks add their histograms into HBM for k_consensus.
 template <int NWP>
 __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
-    constexpr int G = WG / NWP, TW = NWP * 32, TWP = TW + TW / 32, U = 4;
+    constexpr int G = WG / NWP, TW = NWP * 32, TWP = TW + TW / 32, U = 8;
+    constexpr uint32_t FB = 255u * G;   // records per word between flushes
     __shared__ uint32_t hist[NSYM][TWP];
-    __shared__ uint32_t ticket;
     __shared__ unsigned long long acc[VT_ACC];
     __shared__ uint8_t amb[64];
     const uint32_t tid = threadIdx.x;
     const uint32_t w = tid % NWP, g = tid / NWP;
-    if (tid < 64) amb[tid] = c_amb[tid];   // published by the item loop's first barrier
-    // 32-bit byte offsets from scalar bases (global_load v_off, s[base]); the host caps a
-    // batch at 2^28 read pieces and 2^30 seqout words
-    const char *__restrict__ meta_b = reinterpret_cast<const char *>(d.rd_meta);
-    const char *__restrict__ bases_b = reinterpret_cast<const char *>(d.bases);
-    auto meta = [&](uint32_t r) { return *reinterpret_cast<const uint4 *>(meta_b + r * 16u); };
-    auto words = [&](uint32_t wi) { return reinterpret_cast<const uint32_t *>(bases_b + wi * 4u); };
-    for (;;) {
-    if (tid == 0) ticket = atomicAdd(&d.scalars[2], 1u);
-    __syncthreads();
-    const uint32_t item = ticket;
-    if (item >= (uint32_t)d.n_items) return;
+    if (tid < 64) amb[tid] = c_amb[tid];   // published by the barrier after the histogram zeroing
+    const uint32_t *__restrict__ recs = d.recs;
+    const uint32_t CH = (uint32_t)d.chunk_recs;
+    const uint32_t nfb = (CH + FB - 1) / FB;
+    const uint32_t item = blockIdx.x;   // grid = work items
     const uint32_t *it = d.items + (size_t)item * S2C_ITEM_WORDS;
-    const uint32_t a = uni(it[0]), b = uni(it[1]), lo = uni(it[2]), hi = uni(it[3]);
-    const uint32_t xlo = uni(it[4]), xhi = uni(it[5]), flags = uni(it[6]);
+    const uint32_t a = uni(it[0]), b = uni(it[1]), chunk = uni(it[2]), tile = uni(it[3]);
+    const uint32_t *blk = d.blocks + (size_t)tile * S2C_BLOCK_WORDS;
+    const uint32_t ref = uni(blk[2]), deep = uni(blk[3]);
     const uint32_t n = b - a;
     for (uint32_t i = tid; i < NSYM * (uint32_t)TWP; i += WG) (&hist[0][0])[i] = 0;
     __syncthreads();
@@ -461,7 +454,8 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
                     R[r] ^= t << 1;
                 }
                 // R[r] byte j = count of position 8j + r of the word.  Entries at positions
-                // ≥ n (next tile) are added too but never read.  +w: one pad word per 32.
+                // ≥ n (padding after a ref's end) stay zero or are never read.  +w: one pad
+                // word per 32.
                 uint32_t *hw0 = &hist[c][ws + w];
 #pragma unroll
                 for (int r = 0; r < 8; r++)
@@ -472,81 +466,51 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
         zeroV();
     };
     zeroV();
-    // Blocks of ≤255·G read indices (≤255 per lane): the item's short reads [lo, hi)
-    // (restricted per lane to its word's range), then its long-read extras.  One flush per
-    // block, at one site.
-    const uint32_t CAP = 255u * G;
-    const uint32_t nbm = hi > lo ? (hi - lo + CAP - 1) / CAP : 0u;
-    const uint32_t nbx = xhi > xlo ? (xhi - xlo + CAP - 1) / CAP : 0u;
-    const uint32_t nblk = (d.ablate & 1) ? 0u : nbm + nbx;
-    const uint32_t gw = (a >> 5) + w;
-    const uint32_t lw = active ? max(lo, d.word_lo[gw]) : 0u, hw = active ? min(hi, d.word_hi[gw]) : 0u;
-    const uint32_t wst = a + ws;
-    for (uint32_t blk = 0; blk < nblk; blk++) {
-        const bool xmode = blk >= nbm;   // uniform
-        uint32_t s0, e0;
-        if (!xmode) {
-            const uint32_t tb = lo + blk * CAP;
-            s0 = max(lw, tb);
-            e0 = min(hw, tb + CAP);
-        } else {
-            s0 = xlo + (blk - nbm) * CAP;
-            e0 = active ? min(xhi, s0 + CAP) : 0u;
-        }
-        uint32_t t = s0 + (g + G - s0 % G) % G;
-        for (; t < e0; t += U * G) {
-            uint4 m[U];
+    uint32_t r0 = 0, r1 = 0;   // this word's records in chunk `chunk`
+    if (active) {
+        const uint32_t W = (a >> 5) + w;
+        const uint32_t wb = d.wrec[W], we = d.wrec[W + 1];
+        r0 = (uint32_t)min((uint64_t)we, (uint64_t)wb + (uint64_t)chunk * CH);
+        r1 = (uint32_t)min((uint64_t)we, (uint64_t)r0 + CH);
+    }
+    for (uint32_t fb = 0; fb < ((d.ablate & 1) ? 0u : nfb); fb++) {   // uniform
+        const uint32_t s0 = r0 + fb * FB, e0 = min(r1, s0 + FB);
+        for (uint32_t t = s0 + g; t < e0; t += U * G) {
+            uint32_t P[U][3];
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                uint32_t r = min(t + u * G, e0 - 1);
-                if (xmode) r = d.extras[r];
-                m[u] = meta(r);
-            }
-            uint32_t L[U][6];
-            int o[U];
-            bool hit[U];
+            for (int u = 0; u < U; u++) {   // clamped loads, all in flight; tail → code 7
+                const uint32_t i = min(t + u * G, e0 - 1);
+                const uint32_t *src = recs + 3 * (size_t)i;
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                o[u] = (int)(wst - m[u].x);
-                hit[u] = t + u * G < e0 && o[u] < (int)(m[u].y & SPAN_MASK) && o[u] > -32;
-                const uint32_t qs = hit[u] ? (uint32_t)max(o[u], 0) : 0u;
-                const uint32_t *src = words(m[u].z + 3 * (qs >> 5));
-#pragma unroll
-                for (int k = 0; k < 6; k++) L[u][k] = src[k];
+                for (int k = 0; k < 3; k++) P[u][k] = src[k];
             }
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                uint32_t P[3], valid;
-                window(L[u], o[u], m[u].y, hit[u], P, valid);
-                if (d.ablate & 2) valid = 0;   // diagnostic: loads only
-                count_word(V, P, valid);
+                const uint32_t none = (t + u * G < e0 && !(d.ablate & 2)) ? 0u : 0xFFFFFFFFu;
+                count_record(V, P[u][0] | none, P[u][1] | none, P[u][2] | none);
             }
         }
         flush();
     }
     __syncthreads();
     auto hidx = [](uint32_t q) { return q + (q >> 5); };
-    if (!(flags & 1u) && !(d.ablate & 4)) {   // the tile's whole depth is here: vote it now
-        const uint32_t tile = uni(it[7]);
-        vote_tile(d, tile, uni(d.blocks[(size_t)tile * S2C_BLOCK_WORDS + 2]), a, n,
-                  [&](uint32_t q, uint32_t c) { return hist[c][hidx(q)]; }, acc, amb);
+    if (!deep && !(d.ablate & 4)) {   // the tile's whole depth is here: vote it now
+        vote_tile(d, tile, ref, a, n, [&](uint32_t q, uint32_t c) { return hist[c][hidx(q)]; }, acc, amb);
     } else {
-        // deep tile: this item's counts → HBM (symbol-major, coalesced atomics); with the
+        // deep tile: this chunk's counts → HBM (symbol-major, coalesced atomics); with the
         // diagnostic flag 4 every tile stores its counts instead of voting (parity tests)
         for (uint32_t q = tid; q < n; q += WG)
 #pragma unroll
             for (uint32_t c = 0; c < NSYM; c++) {
                 uint32_t *dst = d.counts + (size_t)c * d.padded_len + a + q;
                 const uint32_t v = hist[c][hidx(q)];
-                if (flags & 1u) {
+                if (deep) {
                     if (v) atomicAdd(dst, v);
                 } else {
                     *dst = v;
                 }
             }
     }
-    __syncthreads();
-    }   // for (;;) items
 }
 
 // Deep tiles: counts summed in HBM by their work items → the same vote epilogue.
@@ -689,7 +653,7 @@ static int check_dev(const s2c_dev *d) {
     if (d->tile_max <= 0 || d->tile_max > TILE_MAX) return s2c_set_error(S2C_ERR_ARG, "tile_max out of range");
     if (d->padded_len <= 0 || d->padded_len >= ((int64_t)1 << 32)) return s2c_set_error(S2C_ERR_ARG, "bad padded_len");
     if (d->ins_cap <= 0 || (d->ins_cap & (d->ins_cap - 1))) return s2c_set_error(S2C_ERR_ARG, "ins_cap not pow2");
-    if (d->n_items > 0 && (!d->items || !d->rd_meta || !d->word_lo || !d->word_hi))
+    if (d->n_items > 0 && (!d->items || !d->wrec || (d->n_recs > 0 && !d->recs) || d->chunk_recs <= 0))
         return s2c_set_error(S2C_ERR_ARG, "missing pileup buffers");
     if (d->n_deep > 0 && (!d->deep || !d->counts)) return s2c_set_error(S2C_ERR_ARG, "missing deep-tile buffers");
     if ((d->ablate & 4) && !d->counts) return s2c_set_error(S2C_ERR_ARG, "ablate&4 stores all counts: counts buffer required");
@@ -700,19 +664,9 @@ static int check_dev(const s2c_dev *d) {
 
 // Persistent grid: as many workgroups as fit at once (occupancy query, cached per kernel),
 // never more than the items; each pulls items from the ticket.
-template <typename K>
-static int launch_persistent(K kern, const s2c_dev *d, hipStream_t s) {
-    static int per_cu = 0, n_cu = 0;
-    if (!per_cu) {
-        int dev = 0;
-        hipDeviceProp_t prop;
-        if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess)
-            return s2c_set_error(S2C_ERR_HIP, "device query failed");
-        n_cu = prop.multiProcessorCount;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, WG, 0) != hipSuccess || per_cu < 1) per_cu = 1;
-    }
-    const int64_t g = std::min<int64_t>(d->n_items, (int64_t)per_cu * n_cu);
-    kern<<<(unsigned)g, WG, 0, s>>>(*d);
+template <int NWP>
+static int launch_pileup(const s2c_dev *d, hipStream_t s) {
+    k_pileup<NWP><<<(unsigned)d->n_items, WG, 0, s>>>(*d);
     return hip_check(hipGetLastError(), "k_pileup");
 }
 
@@ -735,10 +689,11 @@ extern "C" int s2c_pileup(const s2c_dev *d, void *stream) {
     if (rc) return rc;
     if (d->n_items == 0) return S2C_OK;
     hipStream_t s = (hipStream_t)stream;
-    if (d->tile_max <= 256) return launch_persistent(k_pileup<8>, d, s);
-    if (d->tile_max <= 512) return launch_persistent(k_pileup<16>, d, s);
-    if (d->tile_max <= 1024) return launch_persistent(k_pileup<32>, d, s);
-    return launch_persistent(k_pileup<64>, d, s);
+    if (d->n_items >= ((int64_t)1 << 31)) return s2c_set_error(S2C_ERR_LIMIT, "more than 2^31 work items");
+    if (d->tile_max <= 256) return launch_pileup<8>(d, s);
+    if (d->tile_max <= 512) return launch_pileup<16>(d, s);
+    if (d->tile_max <= 1024) return launch_pileup<32>(d, s);
+    return launch_pileup<64>(d, s);
 }
 
 extern "C" int s2c_consensus(const s2c_dev *d, void *stream) {

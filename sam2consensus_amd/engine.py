@@ -50,16 +50,15 @@ class DeviceBatch:
         i = hb.info
         self.info = i
         up = lambda a: _up(a, self.device)  # noqa: E731
-        # read records + planar seqout + per-word read ranges (the CIGAR ops stay on the host)
-        self.rd_meta, self.word_lo, self.word_hi = up(hb.rd_meta.reshape(-1)), up(hb.word_lo), up(hb.word_hi)
-        self.bases = up(hb.bases)
-        self.items, self.extras, self.blocks = up(hb.items.reshape(-1)), up(hb.extras), up(hb.blocks.reshape(-1))
+        # word-major seqout records + work plan (the read-piece table stays on the host)
+        self.wrec, self.recs = up(hb.wrec), up(hb.recs.reshape(-1))
+        self.items, self.blocks = up(hb.items.reshape(-1)), up(hb.blocks.reshape(-1))
         self.deep = up(hb.deep)
         self.ins_key, self.ins_off, self.ins_bases = up(hb.ins_key), up(hb.ins_off), up(hb.ins_bases)
 
     def nbytes(self):
         return sum(t.numel() * t.element_size() for t in (
-            self.rd_meta, self.word_lo, self.word_hi, self.bases, self.items, self.extras, self.blocks,
+            self.wrec, self.recs, self.items, self.blocks, self.deep,
             self.ins_key, self.ins_off, self.ins_bases))
 
 
@@ -80,6 +79,7 @@ class Workspace:
         self.fill_bytes = fill
         self.fill = torch.tensor(list(fill) or [0], dtype=torch.uint8, device=dev)
         # counts live in HBM only for deep tiles (unless a test asks for all of them)
+        self.keep_counts = keep_counts
         self.counts = u8(6 * i.padded_len * 4 if keep_counts else sz.counts)
         self.ins_table = u8(sz.ins_table)
         self.ins_cols = u8(sz.ins_cols)
@@ -94,11 +94,11 @@ class Workspace:
         cap = self.T * (i.total_len * max(1, len(fill)) + i.n_ins_bases) + 16
         self.out = u8(cap)
         d = L.Dev()
-        d.rd_meta, d.word_lo, d.word_hi = _ptr(db.rd_meta), _ptr(db.word_lo), _ptr(db.word_hi)
-        d.bases = _ptr(db.bases)
-        d.items, d.extras, d.blocks, d.deep = _ptr(db.items), _ptr(db.extras), _ptr(db.blocks), _ptr(db.deep)
+        d.wrec, d.recs = _ptr(db.wrec), _ptr(db.recs)
+        d.items, d.blocks, d.deep = _ptr(db.items), _ptr(db.blocks), _ptr(db.deep)
         d.ins_key, d.ins_off, d.ins_bases = _ptr(db.ins_key), _ptr(db.ins_off), _ptr(db.ins_bases)
-        d.n_reads, d.n_items, d.n_blocks, d.n_deep = i.n_reads, i.n_items, i.n_blocks, i.n_deep
+        d.n_recs, d.chunk_recs = i.n_recs, i.chunk_recs
+        d.n_items, d.n_blocks, d.n_deep = i.n_items, i.n_blocks, i.n_deep
         d.n_ins, d.n_ins_bases, d.padded_len = i.n_ins, i.n_ins_bases, i.padded_len
         d.tile_max, d.n_refs = i.tile_max, i.n_refs
         d.thresholds, d.n_thr = _ptr(self.thr), self.T
@@ -120,6 +120,8 @@ class Workspace:
         L.check(lib.s2c_insertions(C.byref(self.dev), self.stream_handle()))
 
     def pileup(self):
+        if (self.dev.ablate & 4) and not self.keep_counts:
+            raise ValueError("diagnostic ablate&4 stores every count: build the Workspace with keep_counts=True")
         L.check(lib.s2c_pileup(C.byref(self.dev), self.stream_handle()))
 
     def consensus(self):
@@ -136,6 +138,8 @@ class Workspace:
     def pileup_counts(self):
         """Diagnostic: run prep + pileup with every tile storing its counts (needs
         keep_counts=True); returns counts[6][padded_len] as numpy u32."""
+        if not self.keep_counts:
+            raise ValueError("pileup_counts needs Workspace(keep_counts=True)")
         self.insertions()
         self.dev.ablate = 4
         try:

@@ -1,17 +1,16 @@
 """Position-range sharding of a packed batch across GPUs (one process per GPU).
 
 North_star partitioning: the global coordinate (references concatenated in header
-order) is cut into contiguous tile ranges of roughly equal aligned bases; each rank gets
-its tiles, the reads that overlap them (a contiguous range of the position-sorted reads
-plus any long reads they list), and the insertion events keyed inside them.  Tiles pull
-every read that covers them, so straddling reads are simply read by both neighbours —
-no count exchange is needed.  The one real exchange step is the per-(reference,
+order) is cut into contiguous tile ranges of roughly equal work; each rank gets its
+tiles, the word-major seqout records of their words (one contiguous slice: a read that
+straddles a shard boundary already has one record per word, so each side holds its own
+part — no count exchange is needed), and the insertion events keyed inside them.  The one real exchange step is the per-(reference,
 threshold) record statistics (:352-397) of references cut by a shard boundary: an
 all-reduce of a [R, T, 4] u64 tensor.  FASTA body bytes are gathered to rank 0, which
 formats and writes the files.
 
 Positions keep their global coordinates on every rank (position-indexed buffers are
-sized to the whole batch; read/op/base/insertion arrays are sliced and re-indexed).
+sized to the whole batch; record and insertion arrays are sliced and re-indexed).
 """
 from __future__ import annotations
 
@@ -30,65 +29,25 @@ class SubBatch:
         info = L.BatchInfo()
         for name, _ in L.BatchInfo._fields_:
             setattr(info, name, getattr(i, name))
-        items = hb.items
-        sel = (items[:, 7] >= t0) & (items[:, 7] < t1)
-        it = items[sel].copy()
-        n_short = int(i.n_reads - i.n_long)
-        if len(it):
-            r_lo = int(it[:, 2].min())
-            r_hi = int(it[:, 3].max())
-        else:
-            r_lo = r_hi = 0
-        r_hi = max(r_hi, r_lo)
-        # long reads referenced by these items' extras
-        xs = []
-        for row in it:
-            xs.extend(int(x) for x in hb.extras[int(row[4]):int(row[5])])
-        longs = sorted(set(xs))
-        reads = np.concatenate([np.arange(r_lo, r_hi, dtype=np.int64), np.asarray(longs, dtype=np.int64)])
-        remap = {r: k for k, r in enumerate(longs, start=r_hi - r_lo)}
-        # reads: positions global; ops / bases sliced
-        self.rd_pos = hb.rd_pos[reads].copy() if len(reads) else np.zeros(0, np.uint32)
-        self.rd_span = hb.rd_span[reads].copy() if len(reads) else np.zeros(0, np.uint32)
-        op_lo = hb.rd_op[reads].astype(np.int64)
-        op_hi = hb.rd_op[reads + 1].astype(np.int64)
-        b_lo = hb.rd_base[reads].astype(np.int64)
-        b_hi = hb.rd_base[reads + 1].astype(np.int64)
-        op_len, b_len = op_hi - op_lo, b_hi - b_lo
-        self.rd_op = np.zeros(len(reads) + 1, np.uint32)
-        self.rd_op[1:] = np.cumsum(op_len)
-        self.rd_base = np.zeros(len(reads) + 1, np.uint32)
-        self.rd_base[1:] = np.cumsum(b_len)
-        self.ops = np.concatenate([hb.ops[a:b] for a, b in zip(op_lo, op_hi)]) if len(reads) else np.zeros(0, np.uint32)
-        self.bases = (np.concatenate([hb.bases[a:b] for a, b in zip(b_lo, b_hi)]) if len(reads)
-                      else np.zeros(0, np.uint32))
-        # kernel read records {start, span|flags, base word, op offset} + sentinel
-        self.rd_meta = np.zeros((len(reads) + 1, 4), np.uint32)
-        self.rd_meta[:-1, 0] = self.rd_pos
-        self.rd_meta[:-1, 1] = self.rd_span
-        self.rd_meta[:, 2] = self.rd_base
-        self.rd_meta[:, 3] = self.rd_op
-        # per-word short-read ranges, re-indexed to this shard's read window
-        n_sub = r_hi - r_lo
-        self.word_lo = np.clip(hb.word_lo.astype(np.int64) - r_lo, 0, n_sub).astype(np.uint32)
-        self.word_hi = np.maximum(np.clip(hb.word_hi.astype(np.int64) - r_lo, 0, n_sub),
-                                  self.word_lo).astype(np.uint32)
-        # items / extras re-indexed
-        extras = []
-        for row in it:
-            xl = len(extras)
-            extras.extend(remap[int(x)] for x in hb.extras[int(row[4]):int(row[5])])
-            row[4], row[5] = xl, len(extras)
-            row[2] -= r_lo
-            row[3] -= r_lo
-            row[7] -= t0
-        self.items = it.astype(np.uint32)
-        self.extras = np.asarray(extras, dtype=np.uint32)
         self.blocks = hb.blocks[t0:t1].copy()
+        sel = (hb.items[:, 3] >= t0) & (hb.items[:, 3] < t1)
+        it = hb.items[sel].copy()
+        it[:, 3] -= t0
+        self.items = it.astype(np.uint32)
         self.deep = (hb.deep[(hb.deep >= t0) & (hb.deep < t1)] - t0).astype(np.uint32)
-        # insertion events keyed inside [A, B)
         A = int(self.blocks[0, 0]) if len(self.blocks) else 0
         B = int(self.blocks[-1, 1]) if len(self.blocks) else 0
+        # the records of the shard's words are contiguous: slice them, rebase the CSR
+        # (positions stay global; words outside the shard get empty ranges)
+        wrec = hb.wrec.astype(np.int64)
+        r0, r1 = int(wrec[A >> 5]), int(wrec[(B + 31) >> 5])
+        self.recs = hb.recs[r0:r1].copy()
+        self.wrec = np.clip(wrec - r0, 0, r1 - r0).astype(np.uint32)
+        # the read-piece table stays with the parent (host-side only)
+        self.rd_pos = self.rd_span = np.zeros(0, np.uint32)
+        self.rd_op = np.zeros(1, np.uint32)
+        self.ops = np.zeros(0, np.uint32)
+        # insertion events keyed inside [A, B)
         keep = np.nonzero((hb.ins_key >= A) & (hb.ins_key < B))[0]
         self.ins_key = hb.ins_key[keep].copy()
         lens = (hb.ins_off[keep + 1].astype(np.int64) - hb.ins_off[keep].astype(np.int64))
@@ -98,21 +57,17 @@ class SubBatch:
         nibs = (np.concatenate([nib_all[int(hb.ins_off[e]):int(hb.ins_off[e + 1])] for e in keep])
                 if len(keep) else np.zeros(0, np.uint8))
         self.ins_bases = _pack_nibbles(nibs)
-        # info
-        info.n_reads = len(reads)
-        info.n_long = len(longs)
-        info.n_ops = len(self.ops)
-        info.n_base_words = len(self.bases)
+        info.n_reads = 0
+        info.n_ops = 0
+        info.n_recs = len(self.recs)
         info.n_items = len(self.items)
-        info.n_extras = len(self.extras)
         info.n_blocks = len(self.blocks)
         info.n_deep = len(self.deep)
         info.n_ins = len(keep)
         info.n_ins_bases = int(self.ins_off[-1])
         info.n_ins_words = len(self.ins_bases)
         info.tile_max = int((self.blocks[:, 1] - self.blocks[:, 0]).max()) if len(self.blocks) else 64
-        # aligned bases counted by this shard (the metric's units): seqout chars in its tiles
-        self.info = info
+        self.info = info   # chunk_recs is the parent's: the items' chunk indices refer to it
         self.names = hb.names
         self.ref_len, self.ref_off = hb.ref_len, hb.ref_off
         self.ref_reads = hb.ref_reads
@@ -141,15 +96,14 @@ def _pack_nibbles(nibs):
 
 
 def tile_weights(hb):
-    """Aligned-base estimate per tile: Σ over its items of reads × mean span."""
-    nt = hb.info.n_blocks
-    w = np.zeros(nt, np.float64)
-    if hb.info.n_items:
-        span = np.maximum(1, (hb.rd_span & 0x3FFFFFFF).mean() if hb.info.n_reads else 1)
-        np.add.at(w, hb.items[:, 7].astype(np.int64),
-                  (hb.items[:, 3].astype(np.float64) - hb.items[:, 2]) * float(span))
-    w += (hb.blocks[:, 1].astype(np.float64) - hb.blocks[:, 0]) * 1.0   # vote cost per position
-    return w
+    """Work estimate per tile: the seqout records of its words (one 12-B load + one
+    count each) plus a vote term per 32 positions."""
+    if not hb.info.n_blocks:
+        return np.zeros(0, np.float64)
+    wrec = hb.wrec.astype(np.float64)
+    a = hb.blocks[:, 0].astype(np.int64)
+    b = hb.blocks[:, 1].astype(np.int64)
+    return wrec[(b + 31) >> 5] - wrec[a >> 5] + (b - a) / 32.0
 
 
 def split_tiles(hb, world):

@@ -1,0 +1,55 @@
+"""Per-launch HBM traffic of the bench kernels from the PMC passes of scripts/pmc.sh.
+
+    python scripts/traffic.py [workload] [round-tag]
+Reads gpurun_out/pmc_<wl>/p3 (FETCH_SIZE) and p4 (WRITE_SIZE), averages every dispatch
+of each kernel, applies the gfx950 correction of MI355X_MICROARCH.md §HBM (FETCH_SIZE
+reports half the bytes of a 16-B/lane streaming read: ×2) and writes
+profiles/traffic_<wl>.json, which bench.py reports as roofline.traffic.  Units: the
+rocprofv3 FETCH_SIZE / WRITE_SIZE values are KiB."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_kernel(path_glob, counter):
+    acc = defaultdict(list)
+    for f in glob.glob(path_glob, recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row["Counter_Name"] == counter:
+                    name = row["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+                    acc[name].append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main():
+    wl = sys.argv[1] if len(sys.argv) > 1 else "c2"
+    tag = sys.argv[2] if len(sys.argv) > 2 else ""
+    base = os.path.join(ROOT, "gpurun_out", "pmc_%s" % wl)
+    fetch = per_kernel(os.path.join(base, "p3", "**", "*counter_collection.csv"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(base, "p4", "**", "*counter_collection.csv"), "WRITE_SIZE")
+    kernels = {}
+    for k in sorted(set(fetch) | set(write)):
+        f_raw, w_raw = fetch.get(k, 0.0), write.get(k, 0.0)
+        kernels[k] = {"fetch_kib_raw": f_raw, "write_kib_raw": w_raw,
+                      "hbm_bytes_per_launch": (2.0 * f_raw + w_raw) * 1024.0}
+    pile = [v for k, v in kernels.items() if k.startswith("k_pileup")]
+    out = {"workload": wl, "round": tag, "kernels": kernels,
+           "k_pileup_hbm_bytes_per_launch": pile[0]["hbm_bytes_per_launch"] if pile else None,
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (scripts/pmc.sh); "
+                     "bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 per dispatch, averaged; the x2 is the gfx950 "
+                     "read correction of MI355X_MICROARCH.md; WRITE_SIZE is uncalibrated for byte stores/atomics. "
+                     "The C2 batch (~90 MB) fits the 256 MiB Infinity Cache, whose hits these counters include."}
+    dst = os.path.join(ROOT, "profiles", "traffic_%s.json" % wl)
+    with open(dst, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps({k: round(v["hbm_bytes_per_launch"] / 1e6, 3) for k, v in kernels.items()}))
+
+
+if __name__ == "__main__":
+    main()

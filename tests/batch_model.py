@@ -25,72 +25,48 @@ def _amb():
     return AMB
 
 
-def read_codes(hb, r):
-    """Read piece r: (start, drop, effective ops [(cls, len)], seqout codes).  The packed
-    planes hold the piece's seqout — M bases and '-' (code 0) for D/N/P — checked here
-    against the effective ops."""
-    o0 = int(hb.rd_op[r])
-    o1 = int(hb.rd_op[r + 1])
-    drop = bool(int(hb.rd_span[r]) >> 31)
-    span = int(hb.rd_span[r]) & 0x3FFFFFFF
-    assert sum(int(w) >> 1 for w in hb.ops[o0:o1]) == span
-    assert bool(int(hb.rd_span[r]) >> 30 & 1) == (not drop and o1 - o0 == 1 and (int(hb.ops[o0]) & 1) == 0)
-    ops = [(int(w) & 1, int(w) >> 1) for w in hb.ops[o0:o1]]
-    w0 = int(hb.rd_base[r])
-    assert int(hb.rd_base[r + 1]) - w0 == 3 * ((span + 31) // 32 + 1)
-    assert not hb.bases[w0 + 3 * ((span + 31) // 32):w0 + 3 * ((span + 31) // 32 + 1)].any()
-    words = hb.bases[w0:w0 + 3 * ((span + 31) // 32)].astype(np.int64).reshape(-1, 3)
-    q = np.arange(span)
-    bits = (words[q >> 5] >> (q & 31)[:, None]) & 1
-    codes = (bits * np.array([1, 2, 4])).sum(axis=1)
-    k = 0
-    for cls, ln in ops:
-        if cls == 1:
-            assert not codes[k:k + ln].any()
-        k += ln
-    return int(hb.rd_pos[r]), drop, ops, codes
+def record_codes(recs):
+    """Records [n][3] bit-planes → codes [n][32] (7 = no entry)."""
+    q = np.arange(32, dtype=np.int64)
+    r = np.asarray(recs, dtype=np.int64)
+    return ((r[:, 0, None] >> q) & 1) + 2 * ((r[:, 1, None] >> q) & 1) + 4 * ((r[:, 2, None] >> q) & 1)
 
 
-def read_arrays(hb, r):
-    """Read r as (positions, symbol codes) of the entries the pileup counts: every seqout
-    position, except '-' when the read is maxdel-dropped (:214-218)."""
-    s, drop, ops, codes = read_codes(hb, r)
-    pos = np.arange(s, s + len(codes), dtype=np.int64)
-    c = np.asarray(codes, dtype=np.int64)
-    if drop:
-        keep = c != 0
-        pos, c = pos[keep], c[keep]
-    return pos, c
-
-
-def model_counts(hb):
-    """counts[6][padded_len] following k_pileup's item/tile/extras walk."""
+def model_counts(hb, block=1 << 18):
+    """counts[6][padded_len] from the word-major seqout records, as k_pileup adds them."""
     Lp = hb.info.padded_len
-    counts = np.zeros((NSYM, Lp), dtype=np.int64)
-    cache = {}
-    for it in hb.items:
-        a, b, lo, hi, xlo, xhi = (int(v) for v in it[:6])
-        reads = list(range(lo, hi)) + [int(x) for x in hb.extras[xlo:xhi]]
-        for r in reads:
-            if r not in cache:
-                cache[r] = read_arrays(hb, r)
-            p, c = cache[r]
-            m = (p >= a) & (p < b)
-            np.add.at(counts, (c[m], p[m]), 1)
-    return counts
+    wrec = hb.wrec.astype(np.int64)
+    assert wrec[0] == 0 and wrec[-1] == hb.info.n_recs and (np.diff(wrec) >= 0).all()
+    word_of = np.repeat(np.arange(Lp // 32, dtype=np.int64), np.diff(wrec))
+    flat = np.zeros(NSYM * Lp, dtype=np.int64)
+    for k in range(0, len(word_of), block):
+        codes = record_codes(hb.recs[k:k + block])
+        assert not (codes == 6).any(), "code 6 is never packed"
+        pos = word_of[k:k + block, None] * 32 + np.arange(32)
+        keep = codes < NSYM
+        flat += np.bincount((codes[keep] * Lp + pos[keep]), minlength=NSYM * Lp)
+    return flat.reshape(NSYM, Lp)
 
 
 def check_plan(hb):
-    """Every real position is owned by exactly one tile; chunks of one tile share [a,b)."""
+    """Every real position is owned by exactly one tile; a tile's items are chunks
+    0..nch-1 whose record ranges cover every word of the tile; deep = nch > 1."""
     Lp = hb.info.padded_len
     own = np.zeros(Lp, dtype=np.int64)
-    seen = set()
-    for it in hb.items:
-        a, b, flags = int(it[0]), int(it[1]), int(it[6])
-        if (a, b) in seen:
-            assert flags & 1, "multi-item tile must be atomic"
-            continue
-        seen.add((a, b))
+    wrec = hb.wrec.astype(np.int64)
+    ch = int(hb.info.chunk_recs)
+    assert ch > 0
+    chunks = {}
+    for a, b, c, t in hb.items.astype(np.int64):
+        chunks.setdefault(int(t), []).append(int(c))
+        assert (int(hb.blocks[t, 0]), int(hb.blocks[t, 1])) == (a, b)
+    for t, (a, b, ref, deep) in enumerate(hb.blocks.astype(np.int64)):
+        cs = sorted(chunks[t])
+        assert cs == list(range(len(cs))), "tile %d chunks %r" % (t, cs)
+        assert bool(deep) == (len(cs) > 1)
+        assert a % 32 == 0
+        words = np.arange(a // 32, (b + 31) // 32)
+        assert (wrec[words + 1] - wrec[words]).max(initial=0) <= len(cs) * ch
         own[a:b] += 1
     for r in range(hb.info.n_refs):
         o, L = int(hb.ref_off[r]), int(hb.ref_len[r])

@@ -63,7 +63,7 @@ def test_plan_covers_every_position_c2_scaled():
     hb = configs.synth_batch("c2", scale=0.05)
     bm.check_plan(hb)
     assert hb.info.n_ins > 0
-    # the batch reproduces the oracle's counts exactly (kernel-shaped walk of items)
+    # the word-major records reproduce the oracle's counts exactly
     counts = bm.model_counts(hb)
     sp = configs.spec("c2", scale=0.05)
     with tempfile.TemporaryDirectory() as td:
@@ -83,17 +83,25 @@ def test_plan_covers_every_position_c2_scaled():
 
 
 def test_long_reads_and_wrap_pieces():
-    # spans > LONG_SPAN use per-tile extras; POS=0 wraps (:212)
+    # a 3020-position read spans 95+ words (one record each); POS=0 wraps (:212) into
+    # two pieces at the reference's end and start
     sam = "@SQ\tSN:g\tLN:5000\n"
     sam += "r\t0\tg\t1\t60\t10M3000N10M\t*\t0\t0\t%s\t*\n" % ("A" * 20)
     sam += "r\t0\tg\t0\t60\t5M\t*\t0\t0\tCCCCC\t*\n"
     for s in range(1, 4900, 7):
         sam += "r\t0\tg\t%d\t60\t100M\t*\t0\t0\t%s\t*\n" % (s, "G" * 100)
     hb = batch.parse_text(sam, True, 150)
-    assert hb.info.n_long == 1 and hb.info.n_extras >= 2
+    assert hb.info.n_reads == 1 + 2 + len(range(1, 4900, 7))
+    long_w = np.arange(0, 3020 // 32 + 1)
+    assert (np.diff(hb.wrec.astype(np.int64))[long_w] >= 1).all()
     bm.check_plan(hb)
+    counts = bm.model_counts(hb)
+    assert counts[1, 0:10].tolist() == [1] * 10 and counts[1, 3010:3020].tolist() == [1] * 10
+    assert counts[0, 10:3010].max() == 0               # 3000 '-' > maxdel 150: not counted (:214-218)
+    assert counts[2, 4999] == 1 and counts[2, 0:4].tolist() == [1] * 4   # wrap: C at 4999, 0-3
     opt = o.parse_argv(["-i", "in.sam", "-d", "1"])
     hb2 = batch.parse_text(sam, False, 150)
+    assert (bm.model_counts(hb2)[0, 10:3010] == 1).all()   # -d given: the filter is never applied
     stats, offs, out = bm.model_pipeline(hb2, opt.thresholds, 1, b"-")
     fastas = records.build_records(hb2, opt.thresholds, "in", stats, offs, out)
     got = {n + "__in.fasta": records.render(r, 0).decode() for n, r in fastas.items()}
@@ -110,7 +118,8 @@ def test_text_and_file_and_gzip_parse_agree():
             fh.write(sam)
         hbs = [batch.parse_text(sam), batch.parse_file(p1), batch.parse_file(p2)]
     for h in hbs[1:]:
-        assert (h.rd_pos == hbs[0].rd_pos).all() and (h.bases == hbs[0].bases).all()
+        assert (h.rd_pos == hbs[0].rd_pos).all() and (h.recs == hbs[0].recs).all()
+        assert (h.wrec == hbs[0].wrec).all()
         assert (h.ins_key == hbs[0].ins_key).all()
 
 
@@ -121,7 +130,7 @@ def test_streaming_chunks_equal_whole():
         p.feed(sam[i:i + 7].encode())
     a = p.finish()
     b = batch.parse_text(sam)
-    assert (a.bases == b.bases).all() and (a.rd_op == b.rd_op).all()
+    assert (a.recs == b.recs).all() and (a.wrec == b.wrec).all() and (a.rd_op == b.rd_op).all()
 
 
 def test_generator_c2_is_pinned():
@@ -142,5 +151,5 @@ def test_c2_batch_stats():
     i = hb.info
     assert i.reads_mapped == 1176549 and i.n_refs == 353
     assert 176_000_000 < i.aligned_bases < 177_000_000
-    assert i.n_items >= 1024 and i.tile_max <= 2048
+    assert i.n_items >= 512 and i.tile_max <= 2048   # enough work items to fill 256 CUs
     bm.check_plan(hb)
