@@ -55,6 +55,7 @@ int s2c_layout(int64_t *out, int n);
 #define S2C_CODE_FILL     0    /* codes[] value for a fill position */
 #define S2C_CODE_ERR   0xFF    /* codes[] value where the vote hit a missing amb key (:367) */
 #define S2C_TILE_MAX   2048    /* positions per tile */
+#define S2C_INS_UNIT    256    /* insertion events per count unit (a key with more is split) */
 
 /* ======================================================================================
  * Host side: SAM/SAM.gz parser → packed read batch          (replaces :147-228, :256-294)
@@ -94,6 +95,9 @@ typedef struct {
     int64_t n_ins;             /* insertion events kept (key in [0, LN), non-empty motif) */
     int64_t n_ins_bases;       /* Σ motif lengths */
     int64_t n_ins_words;       /* u32 words of packed motif bases */
+    int64_t n_keys;            /* distinct insertion keys (:262-271 dict keys) */
+    int64_t n_cols;            /* insertion columns = Σ over keys of the longest motif (:278-281) */
+    int64_t n_units;           /* insertion count units (≤ S2C_INS_UNIT events of one key) */
     int64_t n_items;           /* pileup work items */
     int64_t n_blocks;          /* tiles = consensus/assembly blocks (never straddle a ref) */
     int64_t tile_max;          /* max positions of any tile (≤ 2048) */
@@ -111,9 +115,14 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
     const uint32_t *wrec;      /* [padded_len/32 + 1] CSR: records of global word W = [wrec[W], wrec[W+1]) */
     const uint32_t *recs;      /* [n_recs][3] bit-planes {p0,p1,p2} of the 32 positions' codes
                                   (p2·4+p1·2+p0: 0 '-' 1 A 2 C 3 G 4 N 5 T, 7 = no entry) */
-    const uint32_t *ins_key;   /* [n_ins]     global coordinate of the insertion key (:74) */
-    const uint32_t *ins_off;   /* [n_ins+1]   nibble offset of each motif in ins_bases */
-    const uint32_t *ins_bases; /* [n_ins_words] */
+    const uint32_t *ins_key;   /* [n_keys]    global coordinate of each key (:74), ascending */
+    const uint32_t *ins_koff;  /* [n_keys+1]  events of key k = [koff[k], koff[k+1]) (file order) */
+    const uint32_t *ins_kcol;  /* [n_keys+1]  columns of key k = [kcol[k], kcol[k+1]) */
+    const uint32_t *ins_off;   /* [n_ins+1]   nibble offset of each event's motif in ins_bases */
+    const uint32_t *ins_bases; /* [n_ins_words] motif symbol codes, 8 nibbles per word */
+    const uint32_t *ins_units; /* [n_units][2] {key, first event} count units */
+    const uint32_t *ins_bits;  /* [padded_len/32] bit p: position p is a key */
+    const uint32_t *ins_rank;  /* [padded_len/32+1] keys before 32-position word W */
     const uint32_t *items;     /* [n_items][S2C_ITEM_WORDS] pileup work items */
     const uint32_t *blocks;    /* [n_blocks][S2C_BLOCK_WORDS] tiles {g_begin, g_end, ref, deep} */
     const uint32_t *deep;      /* [n_deep] indices of deep tiles */
@@ -165,8 +174,8 @@ typedef struct {
     /* ---- packed batch (device copies of s2c_batch_arrays) ---- */
     const uint32_t *wrec, *recs;   /* word-major seqout records (s2c_batch_arrays) */
     const uint32_t *items, *blocks, *deep;
-    const uint32_t *ins_key, *ins_off, *ins_bases;
-    int64_t n_recs, chunk_recs, n_items, n_blocks, n_deep, n_ins, n_ins_bases, padded_len;
+    const uint32_t *ins_koff, *ins_kcol, *ins_off, *ins_bases, *ins_units, *ins_bits, *ins_rank;
+    int64_t n_recs, chunk_recs, n_items, n_blocks, n_deep, n_keys, n_cols, n_units, padded_len;
     int32_t tile_max, n_refs;
 
     /* ---- options (:117-138) ---- */
@@ -179,12 +188,10 @@ typedef struct {
 
     /* ---- workspace (caller allocates; sizes from s2c_workspace_sizes) ---- */
     uint32_t *counts;          /* [6][padded_len] pileup counts of deep tiles (SoA by symbol) */
-    uint32_t *ins_table;       /* [ins_cap][4] {key+1, maxlen, colbase, cov if called}; ins_cap pow2 */
-    int64_t   ins_cap;
-    uint32_t *ins_cols;        /* [n_ins_bases][6] insertion column counts */
-    uint32_t *ins_cnt;         /* [T][ins_cap] emitted insertion chars per key */
-    uint8_t  *ins_chr;         /* [T][n_ins_bases] emitted insertion chars, column order */
-    uint32_t *ins_bits;        /* [padded_len/32] positions that carry an insertion key */
+    uint32_t *key_cov;         /* [n_keys] coverage of a called key's position, else 0 (vote → k_ins_vote) */
+    uint32_t *ins_cols;        /* [n_cols][6] insertion column symbol counts */
+    uint32_t *ins_cnt;         /* [T][n_keys] insertion chars emitted per key */
+    uint8_t  *ins_chr;         /* [T][n_cols] emitted insertion chars, column order */
     uint32_t *scalars;         /* [16] col allocator, error flags */
     uint8_t  *codes;           /* [T][padded_len] per-position consensus char (0 = fill) */
     uint64_t *blk_len;         /* [T*n_blocks + 1] output bytes per block → exclusive scan */
@@ -204,20 +211,19 @@ typedef struct {
 
 /* Sizes (bytes) of every workspace / output buffer for a batch and T thresholds. */
 typedef struct {
-    int64_t counts, ins_table, ins_cap, ins_cols, ins_cnt, ins_chr, ins_bits, scalars,
-            codes, blk_len, stats;
+    int64_t counts, key_cov, ins_cols, ins_cnt, ins_chr, scalars, codes, blk_len, stats;
 } s2c_ws_sizes;
 int s2c_workspace_sizes(const s2c_batch_info *info, int32_t n_thr, s2c_ws_sizes *out);
 
 /* Stage order (s2c_run): s2c_insertions → s2c_pileup → s2c_consensus → s2c_assemble.
- * (3) zero per-run state; insertion hash table, longest motifs, column counts
- *                                                                      (:221,:256-294) */
+ * (3) zero per-run state; insertion column counts per key           (:221, :256-294) */
 int s2c_insertions(const s2c_dev *d, void *stream);
 /* (2) CIGAR expansion + pileup per tile; for tiles holding their whole depth also
  * (4) the vote (all thresholds, IUPAC, min-depth/fill, insertion columns, stats)
  *                                                (:206-218, :232-253, :290-311, :344-397) */
 int s2c_pileup(const s2c_dev *d, void *stream);
-/* (4) the vote for deep tiles (reads split over several work items)   (:232-253,:344-397) */
+/* (4) the vote for deep tiles (records split over several work items), then the
+ * insertion columns of every called key                    (:232-253, :290-311, :344-397) */
 int s2c_consensus(const s2c_dev *d, void *stream);
 /* device FASTA body assembly: tile scan + byte scatter                 (:350-389 string build) */
 int s2c_assemble(const s2c_dev *d, void *stream);

@@ -46,7 +46,8 @@ class BatchInfo(C.Structure):
     _fields_ = [(n, C.c_int64) for n in (
         "n_refs", "total_len", "padded_len", "header_lines", "lines_total", "reads_mapped",
         "aligned_bases", "query_bases", "n_reads", "n_ops", "n_recs", "chunk_recs", "n_ins",
-        "n_ins_bases", "n_ins_words", "n_items", "n_blocks", "tile_max", "n_deep")]
+        "n_ins_bases", "n_ins_words", "n_keys", "n_cols", "n_units", "n_items", "n_blocks", "tile_max",
+        "n_deep")]
 
 
 _P64 = C.POINTER(C.c_int64)
@@ -57,7 +58,8 @@ class BatchArrays(C.Structure):
     _fields_ = [("ref_len", _P64), ("ref_off", _P64), ("ref_cov_reads", _P64),
                 ("rd_pos", _P32), ("rd_op", _P32), ("rd_span", _P32), ("ops", _P32),
                 ("wrec", _P32), ("recs", _P32),
-                ("ins_key", _P32), ("ins_off", _P32), ("ins_bases", _P32),
+                ("ins_key", _P32), ("ins_koff", _P32), ("ins_kcol", _P32), ("ins_off", _P32),
+                ("ins_bases", _P32), ("ins_units", _P32), ("ins_bits", _P32), ("ins_rank", _P32),
                 ("items", _P32), ("blocks", _P32), ("deep", _P32)]
 
 
@@ -77,16 +79,16 @@ class Dev(C.Structure):
     _fields_ = [
         ("wrec", _VP), ("recs", _VP),
         ("items", _VP), ("blocks", _VP), ("deep", _VP),
-        ("ins_key", _VP), ("ins_off", _VP), ("ins_bases", _VP),
+        ("ins_koff", _VP), ("ins_kcol", _VP), ("ins_off", _VP), ("ins_bases", _VP), ("ins_units", _VP),
+        ("ins_bits", _VP), ("ins_rank", _VP),
         ("n_recs", C.c_int64), ("chunk_recs", C.c_int64),
         ("n_items", C.c_int64), ("n_blocks", C.c_int64), ("n_deep", C.c_int64),
-        ("n_ins", C.c_int64),
-        ("n_ins_bases", C.c_int64), ("padded_len", C.c_int64),
+        ("n_keys", C.c_int64), ("n_cols", C.c_int64), ("n_units", C.c_int64), ("padded_len", C.c_int64),
         ("tile_max", C.c_int32), ("n_refs", C.c_int32),
         ("thresholds", _VP), ("n_thr", C.c_int32), ("min_depth", C.c_int32),
         ("fill_len", C.c_int32), ("fill_nondash", C.c_int32), ("fill", _VP),
-        ("counts", _VP), ("ins_table", _VP), ("ins_cap", C.c_int64), ("ins_cols", _VP),
-        ("ins_cnt", _VP), ("ins_chr", _VP), ("ins_bits", _VP), ("scalars", _VP),
+        ("counts", _VP), ("key_cov", _VP), ("ins_cols", _VP), ("ins_cnt", _VP), ("ins_chr", _VP),
+        ("scalars", _VP),
         ("codes", _VP), ("blk_len", _VP),
         ("stats", _VP), ("out", _VP), ("out_cap", C.c_int64),
         ("ablate", C.c_int32), ("reserved", C.c_int32)]
@@ -94,8 +96,7 @@ class Dev(C.Structure):
 
 class WsSizes(C.Structure):
     _fields_ = [(n, C.c_int64) for n in (
-        "counts", "ins_table", "ins_cap", "ins_cols", "ins_cnt", "ins_chr", "ins_bits", "scalars",
-        "codes", "blk_len", "stats")]
+        "counts", "key_cov", "ins_cols", "ins_cnt", "ins_chr", "scalars", "codes", "blk_len", "stats")]
 
 
 # every symbol include/s2c.h declares (tests/test_lib.py checks the export table)
@@ -160,7 +161,7 @@ def _layout_check():
     buf = (C.c_int64 * 16)()
     n = lib.s2c_layout(buf, 16)
     want = [C.sizeof(Dev), Dev.tile_max.offset, Dev.thresholds.offset, Dev.fill.offset,
-            Dev.counts.offset, Dev.ins_cap.offset, Dev.stats.offset, Dev.out_cap.offset,
+            Dev.counts.offset, Dev.ins_chr.offset, Dev.stats.offset, Dev.out_cap.offset,
             C.sizeof(SynthSpec), SynthSpec.seed.offset, C.sizeof(BatchInfo), C.sizeof(BatchArrays),
             C.sizeof(WsSizes)]
     got = list(buf[:n])

@@ -75,9 +75,16 @@ class HostBatch:
         # word-major seqout records (what the pileup kernel reads)
         self.wrec = _view(a.wrec, i.padded_len // 32 + 1, np.uint32)
         self.recs = _view(a.recs, 3 * i.n_recs, np.uint32).reshape(-1, 3)
-        self.ins_key = _view(a.ins_key, i.n_ins, np.uint32)
+        # insertion events grouped by key (keys ascending)
+        nw = i.padded_len // 32
+        self.ins_key = _view(a.ins_key, i.n_keys, np.uint32)
+        self.ins_koff = _view(a.ins_koff, i.n_keys + 1, np.uint32)
+        self.ins_kcol = _view(a.ins_kcol, i.n_keys + 1, np.uint32)
         self.ins_off = _view(a.ins_off, i.n_ins + 1, np.uint32)
         self.ins_bases = _view(a.ins_bases, i.n_ins_words, np.uint32)
+        self.ins_units = _view(a.ins_units, 2 * i.n_units, np.uint32).reshape(-1, 2)
+        self.ins_bits = _view(a.ins_bits, nw, np.uint32)
+        self.ins_rank = _view(a.ins_rank, nw + 1, np.uint32)
         self.items = _view(a.items, i.n_items * L.S2C_ITEM_WORDS, np.uint32).reshape(-1, L.S2C_ITEM_WORDS)
         self.blocks = _view(a.blocks, i.n_blocks * L.S2C_BLOCK_WORDS, np.uint32).reshape(-1, L.S2C_BLOCK_WORDS)
         self.deep = _view(a.deep, i.n_deep, np.uint32)

@@ -174,7 +174,7 @@ struct s2c_batch {
     std::vector<int64_t> ref_len, ref_off, ref_reads;
     std::vector<uint32_t> rd_pos, rd_op, rd_span, ops;   // host-side read-piece table
     std::vector<uint32_t> wrec, recs;                     // word-major seqout windows
-    std::vector<uint32_t> ins_key, ins_off, ins_bases;
+    std::vector<uint32_t> ins_key, ins_koff, ins_kcol, ins_off, ins_bases, ins_units, ins_bits, ins_rank;
     std::vector<uint32_t> items, blocks, deep;
 };
 
@@ -691,28 +691,70 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
     I.n_blocks = (int64_t)(b->blocks.size() / S2C_BLOCK_WORDS);
     I.n_deep = (int64_t)b->deep.size();
 
-    // ---- insertion events: keys in [0, LN) (negative keys are never emitted, :371) ----
+    // ---- insertion events grouped by key (:256-294), keys sorted by position ----
+    // Keys in [0, LN) only (negative keys are never emitted, :371).  Per key: its events
+    // (file order), a column base (Σ of the keys' longest motif lengths, :278-281), and
+    // count units of ≤ S2C_INS_UNIT events.  Positions → key index: a bitmap and the
+    // number of keys before each 32-position word (rank).
     {
+        std::vector<uint32_t> ev;
+        ev.reserve(p->i_ref.size());
+        for (size_t i = 0; i < p->i_ref.size(); i++)
+            if (p->i_key[i] >= 0) ev.push_back((uint32_t)i);
+        auto gkey = [&](uint32_t i) { return (uint64_t)(b->ref_off[p->i_ref[i]] + p->i_key[i]); };
+        std::stable_sort(ev.begin(), ev.end(), [&](uint32_t x, uint32_t y) { return gkey(x) < gkey(y); });
         uint64_t nb = 0;
-        for (size_t i = 0; i < p->i_ref.size(); i++) {
-            int64_t key = p->i_key[i];
-            if (key < 0) continue;
-            b->ins_key.push_back((uint32_t)(b->ref_off[p->i_ref[i]] + key));
-            b->ins_off.push_back((uint32_t)nb);
-            nb += p->i_len[i];
+        for (uint32_t i : ev) nb += p->i_len[i];
+        if (nb >= (1ull << 32) || ev.size() >= (1ull << 31)) {
+            delete b;
+            return s2c_set_error(S2C_ERR_LIMIT, "insertion events or bases >= 2^31 / 2^32");
         }
-        if (nb >= (1ull << 32)) { delete b; return s2c_set_error(S2C_ERR_LIMIT, "insertion bases >= 2^32"); }
-        b->ins_off.push_back((uint32_t)nb);
+        b->ins_off.reserve(ev.size() + 1);
         b->ins_bases.assign((nb + 7) / 8, 0);
-        uint64_t q = 0;
-        for (size_t i = 0; i < p->i_ref.size(); i++) {
-            if (p->i_key[i] < 0) continue;
-            for (uint32_t j = 0; j < p->i_len[i]; j++, q++)
-                b->ins_bases[q >> 3] |= (uint32_t)LUT.v[(uint8_t)p->i_raw[p->i_off[i] + j]] << (4 * (q & 7));
+        b->ins_bits.assign(NW, 0);
+        b->ins_rank.assign(NW + 1, 0);
+        b->ins_koff.push_back(0);
+        b->ins_kcol.push_back(0);
+        uint64_t q = 0, ncol = 0;
+        uint32_t maxlen = 0;
+        for (size_t j = 0; j < ev.size(); j++) {
+            const uint32_t i = ev[j];
+            const uint64_t key = gkey(i);
+            if (j == 0 || key != b->ins_key.back()) {
+                if (j) {                                   // close the previous key
+                    ncol += maxlen;
+                    b->ins_koff.push_back((uint32_t)j);
+                    b->ins_kcol.push_back((uint32_t)ncol);
+                }
+                b->ins_key.push_back((uint32_t)key);
+                b->ins_bits[key >> 5] |= 1u << (key & 31);
+                b->ins_rank[(key >> 5) + 1]++;
+                maxlen = 0;
+            }
+            maxlen = std::max(maxlen, p->i_len[i]);
+            b->ins_off.push_back((uint32_t)q);
+            for (uint32_t c = 0; c < p->i_len[i]; c++, q++)
+                b->ins_bases[q >> 3] |= (uint32_t)LUT.v[(uint8_t)p->i_raw[p->i_off[i] + c]] << (4 * (q & 7));
         }
-        I.n_ins = (int64_t)b->ins_key.size();
+        if (!ev.empty()) {
+            ncol += maxlen;
+            b->ins_koff.push_back((uint32_t)ev.size());
+            b->ins_kcol.push_back((uint32_t)ncol);
+        }
+        b->ins_off.push_back((uint32_t)q);
+        for (int64_t W = 0; W < NW; W++) b->ins_rank[W + 1] += b->ins_rank[W];
+        const size_t nk = b->ins_key.size();
+        for (size_t k = 0; k < nk; k++)
+            for (uint32_t e = b->ins_koff[k]; e < b->ins_koff[k + 1]; e += S2C_INS_UNIT) {
+                b->ins_units.push_back((uint32_t)k);
+                b->ins_units.push_back(e);
+            }
+        I.n_ins = (int64_t)ev.size();
         I.n_ins_bases = (int64_t)nb;
         I.n_ins_words = (int64_t)b->ins_bases.size();
+        I.n_keys = (int64_t)nk;
+        I.n_cols = (int64_t)ncol;
+        I.n_units = (int64_t)(b->ins_units.size() / 2);
     }
     *out = b;
     return S2C_OK;
@@ -736,8 +778,13 @@ extern "C" int s2c_batch_arrays_get(const s2c_batch *b, s2c_batch_arrays *o) {
     o->wrec = b->wrec.data();
     o->recs = b->recs.data();
     o->ins_key = b->ins_key.data();
+    o->ins_koff = b->ins_koff.data();
+    o->ins_kcol = b->ins_kcol.data();
     o->ins_off = b->ins_off.data();
     o->ins_bases = b->ins_bases.data();
+    o->ins_units = b->ins_units.data();
+    o->ins_bits = b->ins_bits.data();
+    o->ins_rank = b->ins_rank.data();
     o->items = b->items.data();
     o->blocks = b->blocks.data();
     o->deep = b->deep.data();
@@ -803,7 +850,7 @@ extern "C" int s2c_parsecigar(const char *cigar, size_t cigar_len, const char *s
 extern "C" int s2c_layout(int64_t *out, int n) {
     const int64_t v[] = {
         (int64_t)sizeof(s2c_dev), (int64_t)offsetof(s2c_dev, tile_max), (int64_t)offsetof(s2c_dev, thresholds),
-        (int64_t)offsetof(s2c_dev, fill), (int64_t)offsetof(s2c_dev, counts), (int64_t)offsetof(s2c_dev, ins_cap),
+        (int64_t)offsetof(s2c_dev, fill), (int64_t)offsetof(s2c_dev, counts), (int64_t)offsetof(s2c_dev, ins_chr),
         (int64_t)offsetof(s2c_dev, stats), (int64_t)offsetof(s2c_dev, out_cap),
         (int64_t)sizeof(s2c_synth_spec), (int64_t)offsetof(s2c_synth_spec, seed),
         (int64_t)sizeof(s2c_batch_info), (int64_t)sizeof(s2c_batch_arrays), (int64_t)sizeof(s2c_ws_sizes)};

@@ -6,8 +6,7 @@
 // built by s2c_host.cpp, whose unit is the TILE (≤2048 positions of one reference):
 //
 //   k_prep                 zero per-run state (replaces memsets: one launch)
-//   k_ins_build/alloc/     (3) insertion hash table: key → slot, longest motif, column
-//   k_ins_scatter              base, per-column symbol counts (:262-287)
+//   k_ins_count            (3) insertion column symbol counts per key (:262-287)
 //   k_pileup               (2) bit-sliced counting of the word-major seqout records per
 //                          tile (32 positions per VALU op), and (4) for tiles voted in one
 //                          work item the vote epilogue: all thresholds, IUPAC, min-depth/
@@ -109,22 +108,11 @@ __device__ __forceinline__ uint32_t vote_mask(const T (&c)[NSYM], const int64_t 
     return m;
 }
 
-__device__ __forceinline__ uint32_t hash32(uint32_t x) {
-    x ^= x >> 16; x *= 0x85ebca6bu; x ^= x >> 13; x *= 0xc2b2ae35u; x ^= x >> 16;
-    return x;
+// index of the insertion key at position p (p must carry a key): keys before p's word + the
+// key bits below p in it
+__device__ __forceinline__ uint32_t key_index(const s2c_dev &d, uint32_t p, uint32_t bits) {
+    return d.ins_rank[p >> 5] + (uint32_t)__popc(bits & ((1u << (p & 31)) - 1u));
 }
-// table entry: {key+1 (0 = empty), maxlen, colbase, cov of the key if called (else 0)}
-__device__ __forceinline__ uint32_t ins_find(const uint32_t *__restrict__ tab, uint32_t cap, uint32_t key) {
-    uint32_t h = hash32(key) & (cap - 1);
-    for (uint32_t probe = 0; probe < cap; probe++) {
-        uint32_t k = tab[4 * h];
-        if (k == key + 1) return h;
-        if (k == 0) return 0xFFFFFFFFu;
-        h = (h + 1) & (cap - 1);
-    }
-    return 0xFFFFFFFFu;
-}
-
 
 // ======================================================================= per-run state
 // One launch zeroes everything a run accumulates into: per-(ref,t) stats, flags, the
@@ -133,12 +121,9 @@ constexpr int PREP_BLOCKS = 512;
 __global__ __launch_bounds__(WG) void k_prep(const s2c_dev d) {
     if (blockIdx.x < PREP_BLOCKS) {
         const size_t i0 = (size_t)blockIdx.x * WG + threadIdx.x, step = (size_t)PREP_BLOCKS * WG;
-        const size_t n_stats = (size_t)d.n_refs * d.n_thr * 4, n_bits = (size_t)(d.padded_len / 32 + 2);
-        const size_t n_tab = d.n_ins ? (size_t)d.ins_cap * 4 : 0, n_cols = (size_t)d.n_ins_bases * NSYM;
+        const size_t n_stats = (size_t)d.n_refs * d.n_thr * 4, n_cols = (size_t)d.n_cols * NSYM;
         for (size_t i = i0; i < n_stats; i += step) d.stats[i] = 0;
         for (size_t i = i0; i < 16; i += step) d.scalars[i] = 0;
-        for (size_t i = i0; i < n_bits; i += step) d.ins_bits[i] = 0;
-        for (size_t i = i0; i < n_tab; i += step) d.ins_table[i] = 0;
         for (size_t i = i0; i < n_cols; i += step) d.ins_cols[i] = 0;
         return;
     }
@@ -149,73 +134,42 @@ __global__ __launch_bounds__(WG) void k_prep(const s2c_dev d) {
 }
 
 // ======================================================================= (3) insertions
-// (:264-271) motif multiplicities and (:284-287) per-column sums are additive, so the
-// column counts are accumulated straight from the events: column c of key k gets +1 at
-// motif[c] for every event at k with len > c.  The hash table maps key → slot with the
-// longest motif (:278-281), a column base and (set by the vote) the key's coverage; the
-// columns are voted (with '-' = cov[key] − Σ column, :294) by k_ins_vote.
-__global__ void k_ins_build(const s2c_dev d) {
-    const uint32_t e = blockIdx.x * WG + threadIdx.x;
-    if (e >= d.n_ins) return;
-    const uint32_t key = d.ins_key[e];
-    const uint32_t len = d.ins_off[e + 1] - d.ins_off[e];
-    const uint32_t cap = (uint32_t)d.ins_cap;
-    uint32_t h = hash32(key) & (cap - 1);
-    for (uint32_t probe = 0; probe < cap; probe++) {
-        const uint32_t prev = atomicCAS(&d.ins_table[4 * h], 0u, key + 1);
-        if (prev == 0u || prev == key + 1) {
-            atomicMax(&d.ins_table[4 * h + 1], len);
-            break;
+// (:264-271) motif multiplicities and (:284-287) per-column sums are additive: column c of
+// key k counts motif[c] over the key's events with len > c.  The host groups events by
+// key (sorted) and cuts them into units of ≤ S2C_INS_UNIT events; one thread per unit
+// counts every column of its key (columns outer, its events inner) and stores the six
+// counts, or adds them when the key is split over several units.  The columns are voted
+// (with '-' = cov[key] − Σ column, :294) by k_ins_vote.
+__global__ __launch_bounds__(WG) void k_ins_count(const s2c_dev d) {
+    const uint32_t u = blockIdx.x * WG + threadIdx.x;
+    if (u >= (uint32_t)d.n_units) return;
+    const uint32_t k = d.ins_units[2 * u], e0 = d.ins_units[2 * u + 1];
+    const uint32_t ke0 = d.ins_koff[k], ke1 = d.ins_koff[k + 1];
+    const uint32_t e1 = min(ke1, e0 + (uint32_t)S2C_INS_UNIT);
+    const bool whole = e0 == ke0 && e1 == ke1;
+    const uint32_t cb = d.ins_kcol[k], ml = d.ins_kcol[k + 1] - cb;
+    for (uint32_t c = 0; c < ml; c++) {
+        uint32_t cnt[NSYM] = {0, 0, 0, 0, 0, 0};
+        for (uint32_t e = e0; e < e1; e++) {
+            const uint32_t o0 = d.ins_off[e];
+            if (c < d.ins_off[e + 1] - o0) cnt[nibble(d.ins_bases, (uint64_t)o0 + c)]++;
         }
-        h = (h + 1) & (cap - 1);
-    }
-    atomicOr(&d.ins_bits[key >> 5], 1u << (key & 31));
-}
-
-// column bases: workgroup scan of the slots' longest motifs, one atomic per workgroup
-constexpr int ALLOC_WG = 1024;
-__global__ __launch_bounds__(ALLOC_WG) void k_ins_alloc(const s2c_dev d) {
-    __shared__ uint32_t wsum[ALLOC_WG / 64];
-    __shared__ uint32_t base;
-    const uint32_t s = blockIdx.x * ALLOC_WG + threadIdx.x;
-    const uint32_t need = (s < (uint32_t)d.ins_cap && d.ins_table[4 * s] != 0u) ? d.ins_table[4 * s + 1] : 0u;
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t x = need;
+        uint32_t *col = d.ins_cols + (size_t)(cb + c) * NSYM;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= (uint32_t)o) x += y;
+        for (uint32_t j = 0; j < NSYM; j++) {
+            if (whole) col[j] = cnt[j];
+            else if (cnt[j]) atomicAdd(&col[j], cnt[j]);
+        }
     }
-    if (lane == 63) wsum[w] = x;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t tot = 0;
-        for (int i = 0; i < ALLOC_WG / 64; i++) { const uint32_t v = wsum[i]; wsum[i] = tot; tot += v; }
-        base = tot ? atomicAdd(&d.scalars[0], tot) : 0u;
-    }
-    __syncthreads();
-    if (need) d.ins_table[4 * s + 2] = base + wsum[w] + x - need;
-}
-
-__global__ void k_ins_scatter(const s2c_dev d) {
-    const uint32_t e = blockIdx.x * WG + threadIdx.x;
-    if (e >= d.n_ins) return;
-    const uint32_t key = d.ins_key[e];
-    const uint32_t o0 = d.ins_off[e], o1 = d.ins_off[e + 1];
-    const uint32_t slot = ins_find(d.ins_table, (uint32_t)d.ins_cap, key);
-    if (slot == 0xFFFFFFFFu) return;
-    const uint32_t cb = d.ins_table[4 * slot + 2];
-    for (uint32_t c = 0; o0 + c < o1; c++)
-        atomicAdd(&d.ins_cols[(size_t)(cb + c) * NSYM + nibble(d.ins_bases, o0 + c)], 1u);
 }
 
 // ======================================================================= (4) vote epilogue
 // Per position: the closed-form vote for every threshold and the IUPAC char (or fill when
 // cov == 0 or cov < min_depth, :356-389).  Per tile: len and sumcov do not depend on the
 // threshold (1 per called position or len(fill); cov, :357/:385), the per-threshold
-// non-'-' and vote-error counts are wave ballots.  At a called position carrying an
-// insertion key the key's coverage is stored into its hash slot; k_ins_vote then votes
-// the insertion columns (:290-311, :370-385) and adds their chars to the same stats.
+// non-'-' and vote-error counts are wave ballots.  At a position carrying an insertion key
+// the key's coverage (0 when not called) is stored for k_ins_vote, which votes the
+// insertion columns (:290-311, :370-385) and adds their chars to the same stats.
 constexpr int VT_TMAX = 16;   // thresholds per pass over the tile's positions
 constexpr int VT_ACC = 2 + 2 * VT_TMAX;   // LDS u64: sumcov, len, {nondash, nerr}[VT_TMAX]
 
@@ -248,8 +202,8 @@ __device__ __forceinline__ void vote_tile(const s2c_dev &d, uint32_t tile, uint3
             if (t0 == 0) {
                 sumcov += cov;
                 len += called ? 1u : (in ? (uint32_t)d.fill_len : 0u);
-                if (called && (d.ins_bits[p >> 5] >> (p & 31) & 1u))   // key coverage for k_ins_vote
-                    d.ins_table[4 * ins_find(d.ins_table, (uint32_t)d.ins_cap, p) + 3] = (uint32_t)cov;
+                const uint32_t bits = in ? d.ins_bits[p >> 5] : 0u;
+                if (bits >> (p & 31) & 1u) d.key_cov[key_index(d, p, bits)] = called ? (uint32_t)cov : 0u;
             }
             int64_t gs[NSYM];
             greater_sums(cnt, gs);
@@ -287,10 +241,11 @@ __device__ __forceinline__ void vote_tile(const s2c_dev &d, uint32_t tile, uint3
     }
 }
 
-// Insertion columns of the called keys of one tile (grid = tiles; dynamic LDS [T][4] u64):
-// per column and threshold the same vote with '-' = cov[key] − Σ column (:294, signed);
-// '-' results are skipped, others emitted after the key's base (:370-385) and added to
-// the tile's len / non-'-' / sumcov (cov per emitted char, :385) and block length.
+// Insertion columns of the called keys of one tile (grid = tiles; the tile's keys are the
+// contiguous range [rank(a), rank(b)); dynamic LDS [T][4] u64): per column and threshold
+// the same vote with '-' = cov[key] − Σ column (:294, signed); '-' results are skipped,
+// others emitted after the key's base (:370-385) and added to the tile's len / non-'-' /
+// sumcov (cov per emitted char, :385) and block length.
 __global__ __launch_bounds__(WG) void k_ins_vote(const s2c_dev d) {
     extern __shared__ unsigned long long iacc[];   // [T][4]
     __shared__ uint32_t em[VT_TMAX][WG];           // emitted chars per (threshold, thread)
@@ -298,23 +253,19 @@ __global__ __launch_bounds__(WG) void k_ins_vote(const s2c_dev d) {
     const uint32_t tid = threadIdx.x;
     const uint32_t tile = blockIdx.x;
     const uint32_t *blk = d.blocks + (size_t)tile * S2C_BLOCK_WORDS;
-    const uint32_t a = uni(blk[0]), n = uni(blk[1]) - a, ref = uni(blk[2]);
+    const uint32_t a = uni(blk[0]), b = uni(blk[1]), ref = uni(blk[2]);
+    const uint32_t klo = uni(d.ins_rank[a >> 5]), khi = uni(d.ins_rank[(b + 31) >> 5]);
+    if (klo == khi) return;
     const int T = d.n_thr;
-    bool any = false;
-    for (uint32_t w = (a >> 5) + tid; w < ((a + n + 31) >> 5); w += WG) any |= d.ins_bits[w] != 0u;
-    if (!__syncthreads_or(any)) return;
     for (uint32_t i = tid; i < 4u * (uint32_t)T; i += WG) iacc[i] = 0;
     if (tid < 64) amb[tid] = c_amb[tid];
     __syncthreads();
     const uint32_t *__restrict__ cols = d.ins_cols;
     uint8_t *__restrict__ chr = d.ins_chr;
-    for (uint32_t q = tid; q < n; q += WG) {
-        const uint32_t p = a + q;
-        if (!(d.ins_bits[p >> 5] >> (p & 31) & 1u)) continue;
-        const uint32_t slot = ins_find(d.ins_table, (uint32_t)d.ins_cap, p);
-        const uint4 e = *reinterpret_cast<const uint4 *>(d.ins_table + 4 * (size_t)slot);
-        const uint32_t ml = e.y, cb = e.z, cov = e.w;
+    for (uint32_t k = klo + tid; k < khi; k += WG) {
+        const uint32_t cov = d.key_cov[k];
         if (cov == 0) continue;   // position not called: no insertion chars (:356-358)
+        const uint32_t cb = d.ins_kcol[k], ml = d.ins_kcol[k + 1] - cb;
         for (int t0 = 0; t0 < T; t0 += VT_TMAX) {
             const int t1 = min(T, t0 + VT_TMAX);
             for (int t = t0; t < t1; t++) em[t - t0][tid] = 0;
@@ -338,13 +289,13 @@ __global__ __launch_bounds__(WG) void k_ins_vote(const s2c_dev d) {
                     for (int t = t0; t < t1; t++) {
                         const uint8_t ic = amb[vote_mask(v, g2, d.thresholds[t] * (double)cov)];
                         if (ic == 0xFF) { atomicAdd(&iacc[4 * t + 3], 1ull); continue; }
-                        if (ic != '-') chr[(size_t)t * d.n_ins_bases + cb + em[t - t0][tid]++] = ic;
+                        if (ic != '-') chr[(size_t)t * d.n_cols + cb + em[t - t0][tid]++] = ic;
                     }
                 }
             }
             for (int t = t0; t < t1; t++) {
                 const uint32_t emitted = em[t - t0][tid];
-                d.ins_cnt[(size_t)t * d.ins_cap + slot] = emitted;
+                d.ins_cnt[(size_t)t * d.n_keys + k] = emitted;
                 if (emitted) {
                     atomicAdd(&iacc[4 * t + 0], (unsigned long long)cov * emitted);
                     atomicAdd(&iacc[4 * t + 1], (unsigned long long)emitted);
@@ -576,9 +527,10 @@ __global__ __launch_bounds__(WG) void k_assemble(const s2c_dev d) {
                 lens[j] = (uint32_t)d.fill_len;
             } else {
                 lens[j] = 1;
-                if (d.ins_bits[p >> 5] >> (p & 31) & 1u) {
-                    slots[j] = ins_find(d.ins_table, (uint32_t)d.ins_cap, p);
-                    lens[j] += d.ins_cnt[(size_t)t * d.ins_cap + slots[j]];
+                const uint32_t bits = d.ins_bits[p >> 5];
+                if (bits >> (p & 31) & 1u) {
+                    slots[j] = key_index(d, p, bits);
+                    lens[j] += d.ins_cnt[(size_t)t * d.n_keys + slots[j]];
                 }
             }
         }
@@ -608,8 +560,7 @@ __global__ __launch_bounds__(WG) void k_assemble(const s2c_dev d) {
             d.out[off++] = c;
             const uint32_t ne = lens[j] - 1;
             if (ne) {
-                const uint32_t cb = d.ins_table[4 * slots[j] + 2];
-                const uint8_t *src = d.ins_chr + (size_t)t * d.n_ins_bases + cb;
+                const uint8_t *src = d.ins_chr + (size_t)t * d.n_cols + d.ins_kcol[slots[j]];
                 for (uint32_t i = 0; i < ne; i++) d.out[off++] = src[i];
             }
         }
@@ -629,16 +580,12 @@ inline unsigned grid_for(int64_t n, int wg = WG) { return (unsigned)((n + wg - 1
 extern "C" int s2c_workspace_sizes(const s2c_batch_info *info, int32_t n_thr, s2c_ws_sizes *o) {
     if (!info || !o || n_thr <= 0) return s2c_set_error(S2C_ERR_ARG, "bad workspace query");
     const int64_t L = info->padded_len, T = n_thr;
-    int64_t cap = 64;
-    while (cap < 2 * info->n_ins) cap <<= 1;
-    const int64_t nib = info->n_ins_bases > 0 ? info->n_ins_bases : 1;
+    const int64_t nk = std::max<int64_t>(info->n_keys, 1), nc = std::max<int64_t>(info->n_cols, 1);
     o->counts = info->n_deep ? NSYM * L * 4 : 64;   // only deep tiles keep counts in HBM
-    o->ins_cap = cap;
-    o->ins_table = cap * 16;
-    o->ins_cols = nib * NSYM * 4;
-    o->ins_cnt = T * cap * 4;
-    o->ins_chr = T * nib;
-    o->ins_bits = (L / 32 + 2) * 4;
+    o->key_cov = nk * 4;
+    o->ins_cols = nc * NSYM * 4;
+    o->ins_cnt = T * nk * 4;
+    o->ins_chr = T * nc;
     o->scalars = 64;
     o->codes = T * L;
     o->blk_len = (T * info->n_blocks + 1) * 8;
@@ -652,12 +599,13 @@ static int check_dev(const s2c_dev *d) {
     if (d->n_thr > 1024) return s2c_set_error(S2C_ERR_LIMIT, "more than 1024 thresholds");
     if (d->tile_max <= 0 || d->tile_max > TILE_MAX) return s2c_set_error(S2C_ERR_ARG, "tile_max out of range");
     if (d->padded_len <= 0 || d->padded_len >= ((int64_t)1 << 32)) return s2c_set_error(S2C_ERR_ARG, "bad padded_len");
-    if (d->ins_cap <= 0 || (d->ins_cap & (d->ins_cap - 1))) return s2c_set_error(S2C_ERR_ARG, "ins_cap not pow2");
     if (d->n_items > 0 && (!d->items || !d->wrec || (d->n_recs > 0 && !d->recs) || d->chunk_recs <= 0))
         return s2c_set_error(S2C_ERR_ARG, "missing pileup buffers");
     if (d->n_deep > 0 && (!d->deep || !d->counts)) return s2c_set_error(S2C_ERR_ARG, "missing deep-tile buffers");
     if ((d->ablate & 4) && !d->counts) return s2c_set_error(S2C_ERR_ARG, "ablate&4 stores all counts: counts buffer required");
-    if (d->n_ins > 0 && (!d->ins_key || !d->ins_off || !d->ins_bases || !d->ins_table || !d->ins_cols))
+    if (!d->ins_bits || !d->ins_rank) return s2c_set_error(S2C_ERR_ARG, "missing key bitmap/rank");
+    if (d->n_keys > 0 && (!d->ins_koff || !d->ins_kcol || !d->ins_off || !d->ins_bases || !d->ins_units ||
+                          !d->key_cov || !d->ins_cols || !d->ins_cnt || !d->ins_chr))
         return s2c_set_error(S2C_ERR_ARG, "missing insertion buffers");
     return S2C_OK;
 }
@@ -676,12 +624,8 @@ extern "C" int s2c_insertions(const s2c_dev *d, void *stream) {
     if (rc) return rc;
     hipStream_t s = (hipStream_t)stream;
     k_prep<<<(unsigned)(PREP_BLOCKS + d->n_deep), WG, 0, s>>>(*d);
-    if (d->n_ins) {
-        k_ins_build<<<grid_for(d->n_ins), WG, 0, s>>>(*d);
-        k_ins_alloc<<<grid_for(d->ins_cap, ALLOC_WG), ALLOC_WG, 0, s>>>(*d);
-        k_ins_scatter<<<grid_for(d->n_ins), WG, 0, s>>>(*d);
-    }
-    return hip_check(hipGetLastError(), "k_prep/k_ins_*");
+    if (d->n_units) k_ins_count<<<grid_for(d->n_units), WG, 0, s>>>(*d);
+    return hip_check(hipGetLastError(), "k_prep/k_ins_count");
 }
 
 extern "C" int s2c_pileup(const s2c_dev *d, void *stream) {
@@ -704,7 +648,7 @@ extern "C" int s2c_consensus(const s2c_dev *d, void *stream) {
         k_consensus<<<(unsigned)d->n_deep, WG, 0, s>>>(*d);
         if ((rc = hip_check(hipGetLastError(), "k_consensus"))) return rc;
     }
-    if (d->n_ins > 0 && d->n_blocks > 0) {
+    if (d->n_keys > 0 && d->n_blocks > 0) {
         k_ins_vote<<<(unsigned)d->n_blocks, WG, (size_t)32 * d->n_thr, s>>>(*d);
         if ((rc = hip_check(hipGetLastError(), "k_ins_vote"))) return rc;
     }

@@ -54,12 +54,15 @@ class DeviceBatch:
         self.wrec, self.recs = up(hb.wrec), up(hb.recs.reshape(-1))
         self.items, self.blocks = up(hb.items.reshape(-1)), up(hb.blocks.reshape(-1))
         self.deep = up(hb.deep)
-        self.ins_key, self.ins_off, self.ins_bases = up(hb.ins_key), up(hb.ins_off), up(hb.ins_bases)
+        self.ins_koff, self.ins_kcol, self.ins_off = up(hb.ins_koff), up(hb.ins_kcol), up(hb.ins_off)
+        self.ins_bases, self.ins_units = up(hb.ins_bases), up(hb.ins_units.reshape(-1))
+        self.ins_bits, self.ins_rank = up(hb.ins_bits), up(hb.ins_rank)
 
     def nbytes(self):
         return sum(t.numel() * t.element_size() for t in (
             self.wrec, self.recs, self.items, self.blocks, self.deep,
-            self.ins_key, self.ins_off, self.ins_bases))
+            self.ins_koff, self.ins_kcol, self.ins_off, self.ins_bases, self.ins_units, self.ins_bits,
+            self.ins_rank))
 
 
 class Workspace:
@@ -81,33 +84,34 @@ class Workspace:
         # counts live in HBM only for deep tiles (unless a test asks for all of them)
         self.keep_counts = keep_counts
         self.counts = u8(6 * i.padded_len * 4 if keep_counts else sz.counts)
-        self.ins_table = u8(sz.ins_table)
+        self.key_cov = u8(sz.key_cov)
         self.ins_cols = u8(sz.ins_cols)
         self.ins_cnt = u8(sz.ins_cnt)
         self.ins_chr = u8(sz.ins_chr)
-        self.ins_bits = u8(sz.ins_bits)
         self.scalars = u8(sz.scalars)
         self.codes = u8(sz.codes)
         self.blk_len = u8(sz.blk_len)
         self.stats = u8(sz.stats)
         # output upper bound: every position fill or char + every insertion base, per threshold
-        cap = self.T * (i.total_len * max(1, len(fill)) + i.n_ins_bases) + 16
+        cap = self.T * (i.total_len * max(1, len(fill)) + i.n_cols) + 16
         self.out = u8(cap)
         d = L.Dev()
         d.wrec, d.recs = _ptr(db.wrec), _ptr(db.recs)
         d.items, d.blocks, d.deep = _ptr(db.items), _ptr(db.blocks), _ptr(db.deep)
-        d.ins_key, d.ins_off, d.ins_bases = _ptr(db.ins_key), _ptr(db.ins_off), _ptr(db.ins_bases)
+        d.ins_koff, d.ins_kcol, d.ins_off = _ptr(db.ins_koff), _ptr(db.ins_kcol), _ptr(db.ins_off)
+        d.ins_bases, d.ins_units = _ptr(db.ins_bases), _ptr(db.ins_units)
+        d.ins_bits, d.ins_rank = _ptr(db.ins_bits), _ptr(db.ins_rank)
         d.n_recs, d.chunk_recs = i.n_recs, i.chunk_recs
         d.n_items, d.n_blocks, d.n_deep = i.n_items, i.n_blocks, i.n_deep
-        d.n_ins, d.n_ins_bases, d.padded_len = i.n_ins, i.n_ins_bases, i.padded_len
+        d.n_keys, d.n_cols, d.n_units, d.padded_len = i.n_keys, i.n_cols, i.n_units, i.padded_len
         d.tile_max, d.n_refs = i.tile_max, i.n_refs
         d.thresholds, d.n_thr = _ptr(self.thr), self.T
         d.min_depth = int(max(min(min_depth, 2**31 - 1), -2**31))
         d.fill_len, d.fill_nondash = len(fill), sum(1 for c in fill if c != ord("-"))
         d.fill = _ptr(self.fill)
-        d.counts, d.ins_table, d.ins_cap = _ptr(self.counts), _ptr(self.ins_table), sz.ins_cap
+        d.counts, d.key_cov = _ptr(self.counts), _ptr(self.key_cov)
         d.ins_cols, d.ins_cnt, d.ins_chr = _ptr(self.ins_cols), _ptr(self.ins_cnt), _ptr(self.ins_chr)
-        d.ins_bits, d.scalars = _ptr(self.ins_bits), _ptr(self.scalars)
+        d.scalars = _ptr(self.scalars)
         d.codes, d.blk_len = _ptr(self.codes), _ptr(self.blk_len)
         d.stats, d.out, d.out_cap = _ptr(self.stats), _ptr(self.out), cap
         self.dev = d

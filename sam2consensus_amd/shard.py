@@ -47,25 +47,38 @@ class SubBatch:
         self.rd_pos = self.rd_span = np.zeros(0, np.uint32)
         self.rd_op = np.zeros(1, np.uint32)
         self.ops = np.zeros(0, np.uint32)
-        # insertion events keyed inside [A, B)
-        keep = np.nonzero((hb.ins_key >= A) & (hb.ins_key < B))[0]
-        self.ins_key = hb.ins_key[keep].copy()
-        lens = (hb.ins_off[keep + 1].astype(np.int64) - hb.ins_off[keep].astype(np.int64))
-        self.ins_off = np.zeros(len(keep) + 1, np.uint32)
-        self.ins_off[1:] = np.cumsum(lens)
-        nib_all = _unpack_nibbles(hb.ins_bases, int(hb.ins_off[-1]) if len(hb.ins_off) else 0)
-        nibs = (np.concatenate([nib_all[int(hb.ins_off[e]):int(hb.ins_off[e + 1])] for e in keep])
-                if len(keep) else np.zeros(0, np.uint8))
-        self.ins_bases = _pack_nibbles(nibs)
+        # insertion keys inside [A, B): a contiguous key range (keys ascending), hence
+        # contiguous events and columns; re-based, the bitmap cleared outside the shard
+        k0, k1 = (int(x) for x in np.searchsorted(hb.ins_key, [A, B]))
+        koff, kcol = hb.ins_koff.astype(np.int64), hb.ins_kcol.astype(np.int64)
+        e0, e1 = int(koff[k0]), int(koff[k1])
+        self.ins_key = hb.ins_key[k0:k1].copy()
+        self.ins_koff = (koff[k0:k1 + 1] - e0).astype(np.uint32)
+        self.ins_kcol = (kcol[k0:k1 + 1] - kcol[k0]).astype(np.uint32)
+        off = hb.ins_off.astype(np.int64)
+        self.ins_off = (off[e0:e1 + 1] - off[e0]).astype(np.uint32)
+        nib_all = _unpack_nibbles(hb.ins_bases, int(off[-1]))
+        self.ins_bases = _pack_nibbles(nib_all[int(off[e0]):int(off[e1])])
+        u = hb.ins_units.astype(np.int64)
+        u = u[(u[:, 0] >= k0) & (u[:, 0] < k1)] - np.array([k0, e0])
+        self.ins_units = u.astype(np.uint32).reshape(-1, 2)
+        bits = np.zeros_like(hb.ins_bits)
+        wa, wb = A >> 5, (B + 31) >> 5
+        bits[wa:wb] = hb.ins_bits[wa:wb]
+        self.ins_bits = bits
+        self.ins_rank = np.clip(hb.ins_rank.astype(np.int64) - k0, 0, k1 - k0).astype(np.uint32)
         info.n_reads = 0
         info.n_ops = 0
         info.n_recs = len(self.recs)
         info.n_items = len(self.items)
         info.n_blocks = len(self.blocks)
         info.n_deep = len(self.deep)
-        info.n_ins = len(keep)
+        info.n_ins = e1 - e0
         info.n_ins_bases = int(self.ins_off[-1])
         info.n_ins_words = len(self.ins_bases)
+        info.n_keys = k1 - k0
+        info.n_cols = int(self.ins_kcol[-1])
+        info.n_units = len(self.ins_units)
         info.tile_max = int((self.blocks[:, 1] - self.blocks[:, 0]).max()) if len(self.blocks) else 64
         self.info = info   # chunk_recs is the parent's: the items' chunk indices refer to it
         self.names = hb.names

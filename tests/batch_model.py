@@ -71,6 +71,29 @@ def check_plan(hb):
     for r in range(hb.info.n_refs):
         o, L = int(hb.ref_off[r]), int(hb.ref_len[r])
         assert (own[o:o + L] == 1).all(), "ref %d positions not tiled exactly once" % r
+    check_ins_layout(hb)
+
+
+def check_ins_layout(hb):
+    """Keys ascending and unique; bitmap/rank give each key's index; count units cover
+    every event of their key exactly once, ≤ S2C_INS_UNIT events each."""
+    nk = hb.info.n_keys
+    key = hb.ins_key.astype(np.int64)
+    assert (np.diff(key) > 0).all()
+    bits = hb.ins_bits.astype(np.int64)
+    pos = np.nonzero(((bits[:, None] >> np.arange(32)) & 1).reshape(-1))[0]
+    assert (pos == key).all()
+    rank = hb.ins_rank.astype(np.int64)
+    assert rank[-1] == nk and (rank[key >> 5] + [int(bin(int(bits[k >> 5]) & ((1 << (k & 31)) - 1)).count("1"))
+                                                 for k in key] == np.arange(nk)).all()
+    koff = hb.ins_koff.astype(np.int64)
+    assert koff[0] == 0 and koff[-1] == hb.info.n_ins and (np.diff(koff) > 0).all()
+    cover = np.zeros(hb.info.n_ins, np.int64)
+    for k, e in hb.ins_units.astype(np.int64):
+        e1 = min(koff[k + 1], e + 256)
+        assert koff[k] <= e < koff[k + 1]
+        cover[e:e1] += 1
+    assert (cover == 1).all()
 
 
 def _vote(c, cov, t):
@@ -91,16 +114,18 @@ def model_pipeline(hb, thresholds, min_depth=1, fill=b"-"):
     cov = counts.sum(axis=0)
     # insertion columns per key (:264-294)
     cols = {}
-    for e in range(hb.info.n_ins):
-        key = int(hb.ins_key[e])
-        o0, o1 = int(hb.ins_off[e]), int(hb.ins_off[e + 1])
+    for k in range(hb.info.n_keys):
+        key = int(hb.ins_key[k])
         cl = cols.setdefault(key, [])
-        for c in range(o1 - o0):
-            q = o0 + c
-            code = (int(hb.ins_bases[q >> 3]) >> (4 * (q & 7))) & 15
-            while len(cl) <= c:
-                cl.append([0] * NSYM)
-            cl[c][code] += 1
+        for e in range(int(hb.ins_koff[k]), int(hb.ins_koff[k + 1])):
+            o0, o1 = int(hb.ins_off[e]), int(hb.ins_off[e + 1])
+            for c in range(o1 - o0):
+                q = o0 + c
+                code = (int(hb.ins_bases[q >> 3]) >> (4 * (q & 7))) & 15
+                while len(cl) <= c:
+                    cl.append([0] * NSYM)
+                cl[c][code] += 1
+        assert len(cl) == int(hb.ins_kcol[k + 1]) - int(hb.ins_kcol[k])
     nb = hb.info.n_blocks
     R = hb.info.n_refs
     stats = np.zeros((R, T, 4), dtype=np.uint64)
