@@ -172,7 +172,8 @@ int s2c_synth_write(const s2c_synth_spec *spec, const char *path, int64_t *n_rea
  * ====================================================================================== */
 typedef struct {
     /* ---- packed batch (device copies of s2c_batch_arrays) ---- */
-    const uint32_t *wrec, *recs;   /* word-major seqout records (s2c_batch_arrays) */
+    const uint32_t *wrec, *recs;   /* word-major seqout records (s2c_batch_arrays); recs holds
+                                      n_recs + 1 records, the last all zero (sentinel) */
     const uint32_t *items, *blocks, *deep;
     const uint32_t *ins_koff, *ins_kcol, *ins_off, *ins_bases, *ins_units, *ins_bits, *ins_rank;
     int64_t n_recs, chunk_recs, n_items, n_blocks, n_deep, n_keys, n_cols, n_units, padded_len;

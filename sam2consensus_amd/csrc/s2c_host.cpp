@@ -665,13 +665,13 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
     I.tile_max = tile_max;
     // Each tile is also the consensus/assembly block.  k_pileup gives a tile 256 lanes:
     // one 32-position word per lane × G = 256 / words-per-tile lanes per word, each with
-    // 8-bit counters (≤255 records between flushes).  A work item takes chunk k of every
-    // word's records, [k·chunk, (k+1)·chunk) with chunk = 255·G; a tile whose deepest word
+    // 8-bit counters (≤248 records per lane between flushes).  A work item takes chunk k of
+    // every word's records, [k·chunk, (k+1)·chunk) with chunk = 248·G; a tile whose deepest word
     // needs one chunk is voted in the kernel's epilogue (counts never reach HBM), a deeper
     // ("deep") tile adds its chunks' counts into HBM and is voted by k_consensus.
     int64_t nwp = 8;
     while (nwp * 32 < tile_max) nwp *= 2;
-    const int64_t chunk = 255 * (256 / nwp);
+    const int64_t chunk = 248 * (256 / nwp);
     I.chunk_recs = chunk;
     for (size_t t = 0; t < tiles.size(); t++) {
         const Tile &T = tiles[t];

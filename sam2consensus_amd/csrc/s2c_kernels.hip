@@ -317,41 +317,119 @@ __global__ __launch_bounds__(WG) void k_ins_vote(const s2c_dev d) {
 
 // ======================================================================= (2) pileup
 constexpr int TILE_MAX = S2C_TILE_MAX;   // positions per tile (≤ 64 words of 32)
+constexpr uint32_t FLUSH_RECS = 248;     // records per lane between flushes: 31 groups of 8 (≤ 255)
 
-// One record's six one-hot masks (codes 0..5 = '-',A,C,G,N,T; code 7 = no entry matches
-// none) added into 8-bit vertical counters: V[c][b] bit i = bit b of position i's count of
-// code c.  32 positions per VALU op.
-__device__ __forceinline__ void count_record(uint32_t (&V)[NSYM][8], uint32_t p0, uint32_t p1, uint32_t p2) {
-    const uint32_t x = ~p2, z = p2 & ~p1;
-    const uint32_t y0 = x & ~p1, y1 = x & p1;
-    const uint32_t m[NSYM] = {y0 & ~p0, y0 & p0, y1 & ~p0, y1 & p0, z & ~p0, z & p0};
+// Bit-sliced counting.  A record holds 3 planes of its 32 positions' codes (p2·4+p1·2+p0:
+// 0 '-', 1 A, 2 C, 3 G, 4 N, 5 T, 7 = no entry).  Six masks are counted per record, each
+// one VALU op from the planes: O = p1|p2 (C,G,N,T,none), A = p0&~O, Y = p1&~p2 (C,G),
+// G = Y&p0, Z = p2&~p1 (N,T), T = Z&p0; at the flush '-' = n − O − A, C = Y − G,
+// N = Z − T, n = records the lane counted.  A slot past the chunk's end loads the all-zero
+// sentinel record recs[n_recs] (no mask set) and is not counted in n.
+// Each counter is 8 bit-planes (bit b of the per-position count): ones, twos, fours, eights
+// from a Harley–Seal carry-save tree over 16 records (15 CSAs of 2 v_bitop3 each), bits
+// 4..7 a ripple counter of the sixteens.  32 positions per VALU op, ≈20 VALU per record.
+constexpr int NCTR = 6;
+// carry-save adder a + b + c = 2h + l: two v_bitop3_b32 (truth tables 0x96 = xor3, 0xE8 =
+// majority; both symmetric, so operand order is free).  Written as asm because the
+// compiler shares a^b between the two and spends three ops.
+__device__ __forceinline__ void csa(uint32_t &h, uint32_t &l, uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t lo, hi;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(lo) : "v"(a), "v"(b), "v"(c));
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe8" : "=v"(hi) : "v"(a), "v"(b), "v"(c));
+    l = lo;
+    h = hi;
+}
+// 8 masks into planes C[0..2]; returns the carry of weight 8
+__device__ __forceinline__ uint32_t tree8(uint32_t (&C)[8], const uint32_t (&m)[8]) {
+    uint32_t t2a, t2b, t4a, t4b, t8;
+    csa(t2a, C[0], C[0], m[0], m[1]);
+    csa(t2b, C[0], C[0], m[2], m[3]);
+    csa(t4a, C[1], C[1], t2a, t2b);
+    csa(t2a, C[0], C[0], m[4], m[5]);
+    csa(t2b, C[0], C[0], m[6], m[7]);
+    csa(t4b, C[1], C[1], t2a, t2b);
+    csa(t8, C[2], C[2], t4a, t4b);
+    return t8;
+}
+// two weight-8 carries into plane C[3], the weight-16 carry rippled into C[4..7]
+__device__ __forceinline__ void close16(uint32_t (&C)[8], uint32_t t8a, uint32_t t8b) {
+    uint32_t t16;
+    csa(t16, C[3], C[3], t8a, t8b);
 #pragma unroll
-    for (uint32_t c = 0; c < NSYM; c++) {
-        uint32_t carry = m[c];
-#pragma unroll
-        for (int b = 0; b < 8; b++) {
-            const uint32_t t = V[c][b] & carry;
-            V[c][b] ^= carry;
-            carry = t;
-        }
+    for (int b = 4; b < 8; b++) {
+        const uint32_t t = C[b] & t16;
+        C[b] ^= t16;
+        t16 = t;
     }
+}
+// one group of 8 records → the six counters' weight-8 carries
+__device__ __forceinline__ void count8(uint32_t (&V)[NCTR][8], const uint32_t (&P)[8][3], uint32_t (&t8)[NCTR]) {
+    uint32_t m[8], y[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) m[u] = P[u][1] | P[u][2];
+    t8[0] = tree8(V[0], m);   // O
+#pragma unroll
+    for (int u = 0; u < 8; u++) m[u] = P[u][0] & ~(P[u][1] | P[u][2]);
+    t8[1] = tree8(V[1], m);   // A
+#pragma unroll
+    for (int u = 0; u < 8; u++) y[u] = P[u][1] & ~P[u][2];
+    t8[2] = tree8(V[2], y);   // Y = C|G
+#pragma unroll
+    for (int u = 0; u < 8; u++) m[u] = y[u] & P[u][0];
+    t8[3] = tree8(V[3], m);   // G
+#pragma unroll
+    for (int u = 0; u < 8; u++) y[u] = P[u][2] & ~P[u][1];
+    t8[4] = tree8(V[4], y);   // Z = N|T
+#pragma unroll
+    for (int u = 0; u < 8; u++) m[u] = y[u] & P[u][0];
+    t8[5] = tree8(V[5], m);   // T
+}
+
+// 8 bit-planes of one counter → R[r] byte j = count of position 8j + r (8×8 bit transposes
+// on 4 byte lanes at once).
+__device__ __forceinline__ void transpose8(uint32_t (&R)[8]) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const uint32_t t = ((R[r] >> 4) ^ R[r + 4]) & 0x0F0F0F0Fu;
+        R[r + 4] ^= t;
+        R[r] ^= t << 4;
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        if (r & 2) continue;
+        const uint32_t t = ((R[r] >> 2) ^ R[r + 2]) & 0x33333333u;
+        R[r + 2] ^= t;
+        R[r] ^= t << 2;
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r += 2) {
+        const uint32_t t = ((R[r] >> 1) ^ R[r + 1]) & 0x55555555u;
+        R[r + 1] ^= t;
+        R[r] ^= t << 1;
+    }
+}
+
+// LDS histogram of a tile: u16 counts in pairs, word s = 16·(word of 32) + i holds
+// positions i (low half) and i + 16 (high half) of that word; one pad word per 16.
+__device__ __forceinline__ uint32_t hslot(uint32_t s) { return s + (s >> 4); }
+__device__ __forceinline__ uint32_t hist_get(const uint32_t *h, uint32_t q) {
+    return (h[hslot(((q >> 5) << 4) | (q & 15))] >> ((q & 16) ? 16 : 0)) & 0xFFFFu;
 }
 
 // One workgroup per work item = (tile [a,b) of ≤ TW = 32·NWP positions, chunk k).  Lane
 // L owns 32-position word w = L mod NWP of the tile and lane group g = L / NWP (G = 256/NWP
 // lanes per word).  The word's seqout records [wrec[W], wrec[W+1]) are cut into chunks of
-// chunk_recs; the item streams chunk k, lane g taking records ≡ g (mod G), U independent
-// 12-B loads in flight (a group's lanes read consecutive records: coalesced), and adds each
-// record's six one-hot masks into 8-bit vertical counters (count_record).  Every 255·G
-// records (≤255 per lane) a flush transposes each code's 8 planes (8×8 bit transposes on
-// 4 byte lanes at once) and adds the 32 counts into the LDS histogram [6][TW] (padded one
-// word per 32).  A tile voted in one item (not deep) is voted from LDS (vote_tile); a deep
-// tile's chunks add their histograms into HBM for k_consensus.
+// chunk_recs (= 248·G, one flush per lane); the item streams chunk k, lane g taking records
+// ≡ g (mod G), 8 at a time with the next 8 in flight (a group's lanes read consecutive
+// records: coalesced), counted by count8.  The flush transposes the counters, derives the
+// six symbol counts and adds them, two u16 per LDS atomic, into the tile's histogram.  A
+// tile voted in one item (not deep) is voted from LDS (vote_tile); a deep tile's chunks add
+// their histograms into HBM for k_consensus.
 template <int NWP>
 __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
-    constexpr int G = WG / NWP, TW = NWP * 32, TWP = TW + TW / 32, U = 8;
-    constexpr uint32_t FB = 255u * G;   // records per word between flushes
-    __shared__ uint32_t hist[NSYM][TWP];
+    constexpr int G = WG / NWP, TW = NWP * 32, HP = TW / 2 + TW / 32;
+    constexpr uint32_t FB = FLUSH_RECS * G;   // records per word between flushes
+    __shared__ uint32_t hist[NSYM][HP];
     __shared__ unsigned long long acc[VT_ACC];
     __shared__ uint8_t amb[64];
     const uint32_t tid = threadIdx.x;
@@ -366,57 +444,9 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
     const uint32_t *blk = d.blocks + (size_t)tile * S2C_BLOCK_WORDS;
     const uint32_t ref = uni(blk[2]), deep = uni(blk[3]);
     const uint32_t n = b - a;
-    for (uint32_t i = tid; i < NSYM * (uint32_t)TWP; i += WG) (&hist[0][0])[i] = 0;
-    __syncthreads();
+    for (uint32_t i = tid; i < NSYM * (uint32_t)HP; i += WG) (&hist[0][0])[i] = 0;
     const uint32_t ws = 32u * w;                  // word start, tile-relative
     const bool active = ws < n;
-    uint32_t V[NSYM][8];
-    auto zeroV = [&]() {
-#pragma unroll
-        for (uint32_t c = 0; c < NSYM; c++)
-#pragma unroll
-            for (int bb = 0; bb < 8; bb++) V[c][bb] = 0;
-    };
-    // counts of this lane's 32 positions → LDS histogram (8×8 bit transposes per byte lane)
-    auto flush = [&]() {
-        if (active && !(d.ablate & 8)) {
-#pragma unroll
-            for (uint32_t c = 0; c < NSYM; c++) {
-                uint32_t R[8];
-#pragma unroll
-                for (int r = 0; r < 8; r++) R[r] = V[c][r];
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const uint32_t t = ((R[r] >> 4) ^ R[r + 4]) & 0x0F0F0F0Fu;
-                    R[r + 4] ^= t;
-                    R[r] ^= t << 4;
-                }
-#pragma unroll
-                for (int r = 0; r < 8; r++) {
-                    if (r & 2) continue;
-                    const uint32_t t = ((R[r] >> 2) ^ R[r + 2]) & 0x33333333u;
-                    R[r + 2] ^= t;
-                    R[r] ^= t << 2;
-                }
-#pragma unroll
-                for (int r = 0; r < 8; r += 2) {
-                    const uint32_t t = ((R[r] >> 1) ^ R[r + 1]) & 0x55555555u;
-                    R[r + 1] ^= t;
-                    R[r] ^= t << 1;
-                }
-                // R[r] byte j = count of position 8j + r of the word.  Entries at positions
-                // ≥ n (padding after a ref's end) stay zero or are never read.  +w: one pad
-                // word per 32.
-                uint32_t *hw0 = &hist[c][ws + w];
-#pragma unroll
-                for (int r = 0; r < 8; r++)
-#pragma unroll
-                    for (int jb = 0; jb < 4; jb++) atomicAdd(hw0 + 8 * jb + r, (R[r] >> (8 * jb)) & 0xFFu);
-            }
-        }
-        zeroV();
-    };
-    zeroV();
     uint32_t r0 = 0, r1 = 0;   // this word's records in chunk `chunk`
     if (active) {
         const uint32_t W = (a >> 5) + w;
@@ -424,29 +454,95 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
         r0 = (uint32_t)min((uint64_t)we, (uint64_t)wb + (uint64_t)chunk * CH);
         r1 = (uint32_t)min((uint64_t)we, (uint64_t)r0 + CH);
     }
-    for (uint32_t fb = 0; fb < ((d.ablate & 1) ? 0u : nfb); fb++) {   // uniform
-        const uint32_t s0 = r0 + fb * FB, e0 = min(r1, s0 + FB);
-        for (uint32_t t = s0 + g; t < e0; t += U * G) {
-            uint32_t P[U][3];
+    __syncthreads();
+    uint32_t V[NCTR][8];
+    auto zeroV = [&]() {
 #pragma unroll
-            for (int u = 0; u < U; u++) {   // clamped loads, all in flight; tail → code 7
-                const uint32_t i = min(t + u * G, e0 - 1);
-                const uint32_t *src = recs + 3 * (size_t)i;
+        for (int c = 0; c < NCTR; c++)
 #pragma unroll
-                for (int k = 0; k < 3; k++) P[u][k] = src[k];
-            }
+            for (int bb = 0; bb < 8; bb++) V[c][bb] = 0;
+    };
+    const uint32_t sentinel = (uint32_t)d.n_recs;   // all-zero record
+    auto load8 = [&](uint32_t (&P)[8][3], uint32_t t, uint32_t e0) {
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                const uint32_t none = (t + u * G < e0 && !(d.ablate & 2)) ? 0u : 0xFFFFFFFFu;
-                count_record(V, P[u][0] | none, P[u][1] | none, P[u][2] | none);
+        for (int u = 0; u < 8; u++) {
+            const uint32_t i = t + u * G < e0 ? t + u * G : sentinel;
+            const uint32_t *src = recs + 3 * (size_t)i;
+#pragma unroll
+            for (int k = 0; k < 3; k++) P[u][k] = src[k];
+        }
+    };
+    uint32_t sink = 0;   // diagnostic ablate&2: loads consumed without counting
+    auto sink8 = [&](const uint32_t (&P)[8][3]) {
+#pragma unroll
+        for (int u = 0; u < 8; u++) sink ^= P[u][0] ^ P[u][1] ^ P[u][2];
+    };
+    // valid records of the group starting at t
+    auto nvalid = [&](uint32_t t, uint32_t e0) -> uint32_t {
+        return t < e0 ? min(8u, (e0 - t + G - 1) / G) : 0u;
+    };
+    // counters of this lane's 32 positions → six symbol counts → LDS histogram
+    auto flush = [&](uint32_t nrec) {
+        if (active && !(d.ablate & 8)) {
+            uint32_t *h0 = &hist[0][0] + 17 * w;
+            auto add = [&](uint32_t sym, const uint32_t (&R)[8]) {
+                uint32_t *hw = h0 + sym * HP;
+#pragma unroll
+                for (int r = 0; r < 8; r++) {
+                    const uint32_t lo = R[r] & 0x00FF00FFu, hi = (R[r] >> 8) & 0x00FF00FFu;
+                    if (lo) atomicAdd(hw + r, lo);
+                    if (hi) atomicAdd(hw + 8 + r, hi);
+                }
+            };
+            const uint32_t nb = nrec * 0x01010101u;
+#pragma unroll
+            for (int pr = 0; pr < 3; pr++) {   // (O,A) → '-',A; (Y,G) → C,G; (Z,T) → N,T
+                uint32_t X[8], Y[8];
+#pragma unroll
+                for (int r = 0; r < 8; r++) { X[r] = V[2 * pr][r]; Y[r] = V[2 * pr + 1][r]; }
+                transpose8(X);
+                transpose8(Y);
+#pragma unroll
+                for (int r = 0; r < 8; r++) X[r] = pr == 0 ? nb - X[r] - Y[r] : X[r] - Y[r];   // no byte borrows
+                add(pr == 0 ? 0 : (pr == 1 ? 2 : 4), X);
+                add(pr == 0 ? 1 : (pr == 1 ? 3 : 5), Y);
             }
         }
-        flush();
+        zeroV();
+    };
+    zeroV();
+    for (uint32_t fb = 0; fb < ((d.ablate & 1) ? 0u : nfb); fb++) {   // uniform
+        const uint32_t s0 = r0 + fb * FB, e0 = min(r1, s0 + FB);
+        uint32_t t = s0 + g, nrec = 0;
+        if (t < e0) {
+            // two groups of 8 per trip (one 16-record carry-save step), the next group
+            // always in flight while one is counted.  sched_barrier keeps each group's loads
+            // issued ahead of the other group's count (the scheduler otherwise sinks them
+            // next to their use to save registers).
+            uint32_t P[8][3], Q[8][3], ta[NCTR], tb[NCTR];
+            load8(P, t, e0);
+            for (; t < e0; t += 16 * G) {
+                load8(Q, t + 8 * G, e0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (d.ablate & 2) sink8(P); else count8(V, P, ta);
+                load8(P, t + 16 * G, e0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (d.ablate & 2) {
+                    sink8(Q);
+                    continue;
+                }
+                count8(V, Q, tb);
+#pragma unroll
+                for (int c = 0; c < NCTR; c++) close16(V[c], ta[c], tb[c]);
+                nrec += nvalid(t, e0) + nvalid(t + 8 * G, e0);
+            }
+        }
+        flush(nrec);
     }
+    if (sink == 0x9E3779B9u) hist[0][0] = 1;   // keeps the ablation's loads alive
     __syncthreads();
-    auto hidx = [](uint32_t q) { return q + (q >> 5); };
     if (!deep && !(d.ablate & 4)) {   // the tile's whole depth is here: vote it now
-        vote_tile(d, tile, ref, a, n, [&](uint32_t q, uint32_t c) { return hist[c][hidx(q)]; }, acc, amb);
+        vote_tile(d, tile, ref, a, n, [&](uint32_t q, uint32_t c) { return hist_get(hist[c], q); }, acc, amb);
     } else {
         // deep tile: this chunk's counts → HBM (symbol-major, coalesced atomics); with the
         // diagnostic flag 4 every tile stores its counts instead of voting (parity tests)
@@ -454,7 +550,7 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
 #pragma unroll
             for (uint32_t c = 0; c < NSYM; c++) {
                 uint32_t *dst = d.counts + (size_t)c * d.padded_len + a + q;
-                const uint32_t v = hist[c][hidx(q)];
+                const uint32_t v = hist_get(hist[c], q);
                 if (deep) {
                     if (v) atomicAdd(dst, v);
                 } else {
@@ -601,6 +697,12 @@ static int check_dev(const s2c_dev *d) {
     if (d->padded_len <= 0 || d->padded_len >= ((int64_t)1 << 32)) return s2c_set_error(S2C_ERR_ARG, "bad padded_len");
     if (d->n_items > 0 && (!d->items || !d->wrec || (d->n_recs > 0 && !d->recs) || d->chunk_recs <= 0))
         return s2c_set_error(S2C_ERR_ARG, "missing pileup buffers");
+    {   // one flush per item: the LDS histogram's u16 halves hold ≤ 248·G per position
+        int64_t nwp = 8;
+        while (nwp * 32 < d->tile_max) nwp *= 2;
+        if (d->chunk_recs > (int64_t)FLUSH_RECS * (WG / nwp))
+            return s2c_set_error(S2C_ERR_ARG, "chunk_recs exceeds one flush per work item");
+    }
     if (d->n_deep > 0 && (!d->deep || !d->counts)) return s2c_set_error(S2C_ERR_ARG, "missing deep-tile buffers");
     if ((d->ablate & 4) && !d->counts) return s2c_set_error(S2C_ERR_ARG, "ablate&4 stores all counts: counts buffer required");
     if (!d->ins_bits || !d->ins_rank) return s2c_set_error(S2C_ERR_ARG, "missing key bitmap/rank");

@@ -51,7 +51,12 @@ class DeviceBatch:
         self.info = i
         up = lambda a: _up(a, self.device)  # noqa: E731
         # word-major seqout records + work plan (the read-piece table stays on the host)
-        self.wrec, self.recs = up(hb.wrec), up(hb.recs.reshape(-1))
+        self.wrec = up(hb.wrec)
+        # records + one all-zero sentinel record at index n_recs (k_pileup's past-the-end slots)
+        n = int(i.n_recs)
+        self.recs = torch.zeros(3 * (n + 1), dtype=torch.int32, device=self.device)
+        if n:
+            self.recs[: 3 * n].copy_(torch.from_numpy(np.ascontiguousarray(hb.recs.reshape(-1)).view(np.int32)))
         self.items, self.blocks = up(hb.items.reshape(-1)), up(hb.blocks.reshape(-1))
         self.deep = up(hb.deep)
         self.ins_koff, self.ins_kcol, self.ins_off = up(hb.ins_koff), up(hb.ins_kcol), up(hb.ins_off)
