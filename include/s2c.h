@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define S2C_ABI_VERSION 1
+#define S2C_ABI_VERSION 2
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define S2C_OK            0
@@ -51,11 +51,10 @@ int s2c_layout(int64_t *out, int n);
 #define S2C_NSYM          6    /* symbols '-','A','C','G','N','T' — sorted() order (:367) */
 #define S2C_POS_ALIGN    64    /* each reference starts at a multiple of this global coordinate */
 #define S2C_ITEM_WORDS    4    /* u32 words per pileup work item {a, b, chunk, tile} */
-#define S2C_BLOCK_WORDS   4    /* u32 words per consensus block */
+#define S2C_BLOCK_WORDS  12    /* u32 words per tile {a, b, ref, deep, klo, khi, e0, e1, cb0, cb1, 0, 0} */
 #define S2C_CODE_FILL     0    /* codes[] value for a fill position */
 #define S2C_CODE_ERR   0xFF    /* codes[] value where the vote hit a missing amb key (:367) */
 #define S2C_TILE_MAX   2048    /* positions per tile */
-#define S2C_INS_UNIT    256    /* insertion events per count unit (a key with more is split) */
 
 /* ======================================================================================
  * Host side: SAM/SAM.gz parser → packed read batch          (replaces :147-228, :256-294)
@@ -97,7 +96,6 @@ typedef struct {
     int64_t n_ins_words;       /* u32 words of packed motif bases */
     int64_t n_keys;            /* distinct insertion keys (:262-271 dict keys) */
     int64_t n_cols;            /* insertion columns = Σ over keys of the longest motif (:278-281) */
-    int64_t n_units;           /* insertion count units (≤ S2C_INS_UNIT events of one key) */
     int64_t n_items;           /* pileup work items */
     int64_t n_blocks;          /* tiles = consensus/assembly blocks (never straddle a ref) */
     int64_t tile_max;          /* max positions of any tile (≤ 2048) */
@@ -120,11 +118,15 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
     const uint32_t *ins_kcol;  /* [n_keys+1]  columns of key k = [kcol[k], kcol[k+1]) */
     const uint32_t *ins_off;   /* [n_ins+1]   nibble offset of each event's motif in ins_bases */
     const uint32_t *ins_bases; /* [n_ins_words] motif symbol codes, 8 nibbles per word */
-    const uint32_t *ins_units; /* [n_units][2] {key, first event} count units */
+    const uint32_t *ins_ekey;  /* [n_ins]     key index of each event */
+    const uint32_t *ins_ev;    /* [n_ins][4]  {column offset in the key's tile, motif length,
+                                                nibble offset, first 8 motif nibbles} */
+    const uint32_t *ins_kinfo; /* [n_keys][4] {position, first column, columns, 0} */
     const uint32_t *ins_bits;  /* [padded_len/32] bit p: position p is a key */
     const uint32_t *ins_rank;  /* [padded_len/32+1] keys before 32-position word W */
     const uint32_t *items;     /* [n_items][S2C_ITEM_WORDS] pileup work items */
-    const uint32_t *blocks;    /* [n_blocks][S2C_BLOCK_WORDS] tiles {g_begin, g_end, ref, deep} */
+    const uint32_t *blocks;    /* [n_blocks][S2C_BLOCK_WORDS] tiles {g_begin, g_end, ref, deep, then the
+                                  tile's keys [klo,khi), events [e0,e1), columns [cb0,cb1)} */
     const uint32_t *deep;      /* [n_deep] indices of deep tiles */
 } s2c_batch_arrays;
 
@@ -175,8 +177,8 @@ typedef struct {
     const uint32_t *wrec, *recs;   /* word-major seqout records (s2c_batch_arrays); recs holds
                                       n_recs + 1 records, the last all zero (sentinel) */
     const uint32_t *items, *blocks, *deep;
-    const uint32_t *ins_koff, *ins_kcol, *ins_off, *ins_bases, *ins_units, *ins_bits, *ins_rank;
-    int64_t n_recs, chunk_recs, n_items, n_blocks, n_deep, n_keys, n_cols, n_units, padded_len;
+    const uint32_t *ins_ev, *ins_kinfo, *ins_bases, *ins_bits, *ins_rank;   /* (s2c_batch_arrays) */
+    int64_t n_recs, chunk_recs, n_items, n_blocks, n_deep, n_keys, n_cols, padded_len;
     int32_t tile_max, n_refs;
 
     /* ---- options (:117-138) ---- */
@@ -189,17 +191,18 @@ typedef struct {
 
     /* ---- workspace (caller allocates; sizes from s2c_workspace_sizes) ---- */
     uint32_t *counts;          /* [6][padded_len] pileup counts of deep tiles (SoA by symbol) */
-    uint32_t *key_cov;         /* [n_keys] coverage of a called key's position, else 0 (vote → k_ins_vote) */
-    uint32_t *ins_cols;        /* [n_cols][6] insertion column symbol counts */
-    uint32_t *ins_cnt;         /* [T][n_keys] insertion chars emitted per key */
-    uint8_t  *ins_chr;         /* [T][n_cols] emitted insertion chars, column order */
-    uint32_t *scalars;         /* [16] col allocator, error flags */
+    uint32_t *ins_cols;        /* [n_cols][6] column counts of tiles with > 1024 columns (else in LDS) */
+    uint32_t *ins_cnt;         /* [T][n_keys][4] {insertion chars emitted, first column, columns, 0} */
+    uint8_t  *ins_chr;         /* [T][n_cols] vote char of every insertion column of a called key
+                                  ('-' and 0xFF included; the emitted chars are the others) */
     uint8_t  *codes;           /* [T][padded_len] per-position consensus char (0 = fill) */
-    uint64_t *blk_len;         /* [T*n_blocks + 1] output bytes per block → exclusive scan */
+    uint64_t *blk_len;         /* [T*n_blocks] output bytes of block (t, tile) */
 
     /* ---- outputs ---- */
-    uint64_t *stats;           /* [n_refs][T][4] {sumcov, len, nondash, vote_errors} (:352-397) */
-    uint8_t  *out;             /* assembled consensus bytes, [t][block] order; size = blk_len[T*n_blocks] */
+    uint64_t *tile_stats;      /* [T][n_blocks][4] {sumcov, len, nondash, vote_errors} per tile
+                                  (:352-397; summed per reference by the host) */
+    uint64_t *blk_off;         /* [T*n_blocks + 1] byte offset of block (t, tile) in out; last = total */
+    uint8_t  *out;             /* assembled consensus bytes, [t][block] order */
     int64_t   out_cap;
 
     /* ---- diagnostics, 0 in the product: bit 1 skips counting, bit 2 loads without
@@ -212,26 +215,22 @@ typedef struct {
 
 /* Sizes (bytes) of every workspace / output buffer for a batch and T thresholds. */
 typedef struct {
-    int64_t counts, key_cov, ins_cols, ins_cnt, ins_chr, scalars, codes, blk_len, stats;
+    int64_t counts, ins_cols, ins_cnt, ins_chr, codes, blk_len, blk_off, tile_stats;
 } s2c_ws_sizes;
 int s2c_workspace_sizes(const s2c_batch_info *info, int32_t n_thr, s2c_ws_sizes *out);
 
-/* Stage order (s2c_run): s2c_insertions → s2c_pileup → s2c_consensus → s2c_assemble.
- * (3) zero per-run state; insertion column counts per key           (:221, :256-294) */
-int s2c_insertions(const s2c_dev *d, void *stream);
-/* (2) CIGAR expansion + pileup per tile; for tiles holding their whole depth also
- * (4) the vote (all thresholds, IUPAC, min-depth/fill, insertion columns, stats)
- *                                                (:206-218, :232-253, :290-311, :344-397) */
+/* Stage order (s2c_run): s2c_pileup → s2c_consensus → s2c_assemble.
+ * (2) pileup per tile; for tiles holding their whole depth in one work item also (3) the
+ * insertion columns and (4) the vote (all thresholds, IUPAC, min-depth/fill, insertion
+ * chars, tile statistics)                       (:206-221, :232-253, :256-311, :344-397) */
 int s2c_pileup(const s2c_dev *d, void *stream);
-/* (4) the vote for deep tiles (records split over several work items), then the
- * insertion columns of every called key                    (:232-253, :290-311, :344-397) */
+/* (3)+(4) for deep tiles (records split over several work items, counts summed in HBM)
+ *                                                         (:232-253, :256-311, :344-397) */
 int s2c_consensus(const s2c_dev *d, void *stream);
-/* device FASTA body assembly: tile scan + byte scatter                 (:350-389 string build) */
+/* device FASTA body assembly: block offsets (scan) + byte scatter       (:350-389 string build) */
 int s2c_assemble(const s2c_dev *d, void *stream);
-/* all four, in order, on one stream (graph-capturable: no allocation, no sync) */
+/* all three, in order, on one stream (graph-capturable: no allocation, no sync) */
 int s2c_run(const s2c_dev *d, void *stream);
-/* error flags raised by the device vote (S2C_OK or S2C_ERR_KEY); call after stream sync */
-int s2c_device_error(const s2c_dev *d, void *stream, int *err_out);
 
 #ifdef __cplusplus
 }

@@ -26,7 +26,7 @@ S2C_ERR_LIMIT = -13
 S2C_NSYM = 6
 S2C_POS_ALIGN = 64
 S2C_ITEM_WORDS = 4
-S2C_BLOCK_WORDS = 4
+S2C_BLOCK_WORDS = 12
 S2C_CODE_FILL = 0
 
 # reference exception classes (SURVEY.md §5 "Failure detection")
@@ -46,7 +46,7 @@ class BatchInfo(C.Structure):
     _fields_ = [(n, C.c_int64) for n in (
         "n_refs", "total_len", "padded_len", "header_lines", "lines_total", "reads_mapped",
         "aligned_bases", "query_bases", "n_reads", "n_ops", "n_recs", "chunk_recs", "n_ins",
-        "n_ins_bases", "n_ins_words", "n_keys", "n_cols", "n_units", "n_items", "n_blocks", "tile_max",
+        "n_ins_bases", "n_ins_words", "n_keys", "n_cols", "n_items", "n_blocks", "tile_max",
         "n_deep")]
 
 
@@ -59,7 +59,8 @@ class BatchArrays(C.Structure):
                 ("rd_pos", _P32), ("rd_op", _P32), ("rd_span", _P32), ("ops", _P32),
                 ("wrec", _P32), ("recs", _P32),
                 ("ins_key", _P32), ("ins_koff", _P32), ("ins_kcol", _P32), ("ins_off", _P32),
-                ("ins_bases", _P32), ("ins_units", _P32), ("ins_bits", _P32), ("ins_rank", _P32),
+                ("ins_bases", _P32), ("ins_ekey", _P32), ("ins_ev", _P32), ("ins_kinfo", _P32),
+                ("ins_bits", _P32), ("ins_rank", _P32),
                 ("items", _P32), ("blocks", _P32), ("deep", _P32)]
 
 
@@ -79,24 +80,22 @@ class Dev(C.Structure):
     _fields_ = [
         ("wrec", _VP), ("recs", _VP),
         ("items", _VP), ("blocks", _VP), ("deep", _VP),
-        ("ins_koff", _VP), ("ins_kcol", _VP), ("ins_off", _VP), ("ins_bases", _VP), ("ins_units", _VP),
-        ("ins_bits", _VP), ("ins_rank", _VP),
+        ("ins_ev", _VP), ("ins_kinfo", _VP), ("ins_bases", _VP), ("ins_bits", _VP), ("ins_rank", _VP),
         ("n_recs", C.c_int64), ("chunk_recs", C.c_int64),
         ("n_items", C.c_int64), ("n_blocks", C.c_int64), ("n_deep", C.c_int64),
-        ("n_keys", C.c_int64), ("n_cols", C.c_int64), ("n_units", C.c_int64), ("padded_len", C.c_int64),
+        ("n_keys", C.c_int64), ("n_cols", C.c_int64), ("padded_len", C.c_int64),
         ("tile_max", C.c_int32), ("n_refs", C.c_int32),
         ("thresholds", _VP), ("n_thr", C.c_int32), ("min_depth", C.c_int32),
         ("fill_len", C.c_int32), ("fill_nondash", C.c_int32), ("fill", _VP),
-        ("counts", _VP), ("key_cov", _VP), ("ins_cols", _VP), ("ins_cnt", _VP), ("ins_chr", _VP),
-        ("scalars", _VP),
+        ("counts", _VP), ("ins_cols", _VP), ("ins_cnt", _VP), ("ins_chr", _VP),
         ("codes", _VP), ("blk_len", _VP),
-        ("stats", _VP), ("out", _VP), ("out_cap", C.c_int64),
+        ("tile_stats", _VP), ("blk_off", _VP), ("out", _VP), ("out_cap", C.c_int64),
         ("ablate", C.c_int32), ("reserved", C.c_int32)]
 
 
 class WsSizes(C.Structure):
     _fields_ = [(n, C.c_int64) for n in (
-        "counts", "key_cov", "ins_cols", "ins_cnt", "ins_chr", "scalars", "codes", "blk_len", "stats")]
+        "counts", "ins_cols", "ins_cnt", "ins_chr", "codes", "blk_len", "blk_off", "tile_stats")]
 
 
 # every symbol include/s2c.h declares (tests/test_lib.py checks the export table)
@@ -105,8 +104,7 @@ EXPORTS = [
     "s2c_parser_new", "s2c_parser_feed", "s2c_parser_feed_file", "s2c_parser_finish", "s2c_parser_free",
     "s2c_batch_info_get", "s2c_batch_arrays_get", "s2c_batch_ref_name", "s2c_batch_free",
     "s2c_parsecigar", "s2c_synth_feed", "s2c_synth_write",
-    "s2c_workspace_sizes", "s2c_pileup", "s2c_insertions", "s2c_consensus", "s2c_assemble",
-    "s2c_run", "s2c_device_error",
+    "s2c_workspace_sizes", "s2c_pileup", "s2c_consensus", "s2c_assemble", "s2c_run",
 ]
 
 
@@ -140,11 +138,9 @@ def _load():
         "s2c_synth_write": (C.c_int, [C.POINTER(SynthSpec), C.c_char_p, C.POINTER(C.c_int64)]),
         "s2c_workspace_sizes": (C.c_int, [C.POINTER(BatchInfo), C.c_int32, C.POINTER(WsSizes)]),
         "s2c_pileup": (C.c_int, [C.POINTER(Dev), _VP]),
-        "s2c_insertions": (C.c_int, [C.POINTER(Dev), _VP]),
         "s2c_consensus": (C.c_int, [C.POINTER(Dev), _VP]),
         "s2c_assemble": (C.c_int, [C.POINTER(Dev), _VP]),
         "s2c_run": (C.c_int, [C.POINTER(Dev), _VP]),
-        "s2c_device_error": (C.c_int, [C.POINTER(Dev), _VP, C.POINTER(C.c_int)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -161,7 +157,7 @@ def _layout_check():
     buf = (C.c_int64 * 16)()
     n = lib.s2c_layout(buf, 16)
     want = [C.sizeof(Dev), Dev.tile_max.offset, Dev.thresholds.offset, Dev.fill.offset,
-            Dev.counts.offset, Dev.ins_chr.offset, Dev.stats.offset, Dev.out_cap.offset,
+            Dev.counts.offset, Dev.ins_chr.offset, Dev.tile_stats.offset, Dev.out_cap.offset,
             C.sizeof(SynthSpec), SynthSpec.seed.offset, C.sizeof(BatchInfo), C.sizeof(BatchArrays),
             C.sizeof(WsSizes)]
     got = list(buf[:n])

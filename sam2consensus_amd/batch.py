@@ -82,7 +82,9 @@ class HostBatch:
         self.ins_kcol = _view(a.ins_kcol, i.n_keys + 1, np.uint32)
         self.ins_off = _view(a.ins_off, i.n_ins + 1, np.uint32)
         self.ins_bases = _view(a.ins_bases, i.n_ins_words, np.uint32)
-        self.ins_units = _view(a.ins_units, 2 * i.n_units, np.uint32).reshape(-1, 2)
+        self.ins_ekey = _view(a.ins_ekey, i.n_ins, np.uint32)
+        self.ins_ev = _view(a.ins_ev, 4 * i.n_ins, np.uint32).reshape(-1, 4)
+        self.ins_kinfo = _view(a.ins_kinfo, 4 * i.n_keys, np.uint32).reshape(-1, 4)
         self.ins_bits = _view(a.ins_bits, nw, np.uint32)
         self.ins_rank = _view(a.ins_rank, nw + 1, np.uint32)
         self.items = _view(a.items, i.n_items * L.S2C_ITEM_WORDS, np.uint32).reshape(-1, L.S2C_ITEM_WORDS)

@@ -174,7 +174,8 @@ struct s2c_batch {
     std::vector<int64_t> ref_len, ref_off, ref_reads;
     std::vector<uint32_t> rd_pos, rd_op, rd_span, ops;   // host-side read-piece table
     std::vector<uint32_t> wrec, recs;                     // word-major seqout windows
-    std::vector<uint32_t> ins_key, ins_koff, ins_kcol, ins_off, ins_bases, ins_units, ins_bits, ins_rank;
+    std::vector<uint32_t> ins_key, ins_koff, ins_kcol, ins_off, ins_bases, ins_ekey, ins_bits, ins_rank;
+    std::vector<uint32_t> ins_ev, ins_kinfo;             // device-side event / key records
     std::vector<uint32_t> items, blocks, deep;
 };
 
@@ -683,7 +684,7 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
             uint32_t it[S2C_ITEM_WORDS] = {(uint32_t)T.a, (uint32_t)T.b, (uint32_t)c, (uint32_t)t};
             b->items.insert(b->items.end(), it, it + S2C_ITEM_WORDS);
         }
-        uint32_t blk[S2C_BLOCK_WORDS] = {(uint32_t)T.a, (uint32_t)T.b, (uint32_t)T.ref, nch > 1 ? 1u : 0u};
+        uint32_t blk[S2C_BLOCK_WORDS] = {(uint32_t)T.a, (uint32_t)T.b, (uint32_t)T.ref, nch > 1 ? 1u : 0u};   // words 4-9 below
         b->blocks.insert(b->blocks.end(), blk, blk + S2C_BLOCK_WORDS);
         if (nch > 1) b->deep.push_back((uint32_t)t);
     }
@@ -694,7 +695,7 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
     // ---- insertion events grouped by key (:256-294), keys sorted by position ----
     // Keys in [0, LN) only (negative keys are never emitted, :371).  Per key: its events
     // (file order), a column base (Σ of the keys' longest motif lengths, :278-281), and
-    // count units of ≤ S2C_INS_UNIT events.  Positions → key index: a bitmap and the
+    // the key index of each event.  Positions → key index: a bitmap and the
     // number of keys before each 32-position word (rank).
     {
         std::vector<uint32_t> ev;
@@ -744,17 +745,45 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
         b->ins_off.push_back((uint32_t)q);
         for (int64_t W = 0; W < NW; W++) b->ins_rank[W + 1] += b->ins_rank[W];
         const size_t nk = b->ins_key.size();
+        b->ins_ekey.resize(ev.size());
         for (size_t k = 0; k < nk; k++)
-            for (uint32_t e = b->ins_koff[k]; e < b->ins_koff[k + 1]; e += S2C_INS_UNIT) {
-                b->ins_units.push_back((uint32_t)k);
-                b->ins_units.push_back(e);
+            for (uint32_t e = b->ins_koff[k]; e < b->ins_koff[k + 1]; e++) b->ins_ekey[e] = (uint32_t)k;
+        // per tile: its keys [klo, khi), events [e0, e1), columns [cb0, cb1) (block words
+        // 4-9); per event {column offset in its tile, motif length, nibble offset, first 8
+        // nibbles}; per key {position, first column, columns}: one 16-B load each on the device
+        b->ins_ev.assign(4 * ev.size(), 0);
+        b->ins_kinfo.assign(4 * nk, 0);
+        for (size_t k = 0; k < nk; k++) {
+            b->ins_kinfo[4 * k] = b->ins_key[k];
+            b->ins_kinfo[4 * k + 1] = b->ins_kcol[k];
+            b->ins_kinfo[4 * k + 2] = b->ins_kcol[k + 1] - b->ins_kcol[k];
+        }
+        const size_t ntile = b->blocks.size() / S2C_BLOCK_WORDS;
+        for (size_t t = 0; t < ntile; t++) {
+            uint32_t *blk = &b->blocks[t * S2C_BLOCK_WORDS];
+            const uint32_t klo = nk ? b->ins_rank[blk[0] >> 5] : 0, khi = nk ? b->ins_rank[(blk[1] + 31) >> 5] : 0;
+            blk[4] = klo;
+            blk[5] = khi;
+            blk[6] = nk ? b->ins_koff[klo] : 0;
+            blk[7] = nk ? b->ins_koff[khi] : 0;
+            blk[8] = nk ? b->ins_kcol[klo] : 0;
+            blk[9] = nk ? b->ins_kcol[khi] : 0;
+            for (uint32_t e = blk[6]; e < blk[7]; e++) {
+                const uint32_t o = b->ins_off[e], len = b->ins_off[e + 1] - o;
+                uint32_t w0 = 0;
+                for (uint32_t c = 0; c < len && c < 8; c++) w0 |= ((b->ins_bases[(o + c) >> 3] >> (4 * ((o + c) & 7))) & 15u) << (4 * c);
+                uint32_t *r = &b->ins_ev[4 * (size_t)e];
+                r[0] = b->ins_kcol[b->ins_ekey[e]] - blk[8];
+                r[1] = len;
+                r[2] = o;
+                r[3] = w0;
             }
+        }
         I.n_ins = (int64_t)ev.size();
         I.n_ins_bases = (int64_t)nb;
         I.n_ins_words = (int64_t)b->ins_bases.size();
         I.n_keys = (int64_t)nk;
         I.n_cols = (int64_t)ncol;
-        I.n_units = (int64_t)(b->ins_units.size() / 2);
     }
     *out = b;
     return S2C_OK;
@@ -782,7 +811,9 @@ extern "C" int s2c_batch_arrays_get(const s2c_batch *b, s2c_batch_arrays *o) {
     o->ins_kcol = b->ins_kcol.data();
     o->ins_off = b->ins_off.data();
     o->ins_bases = b->ins_bases.data();
-    o->ins_units = b->ins_units.data();
+    o->ins_ekey = b->ins_ekey.data();
+    o->ins_ev = b->ins_ev.data();
+    o->ins_kinfo = b->ins_kinfo.data();
     o->ins_bits = b->ins_bits.data();
     o->ins_rank = b->ins_rank.data();
     o->items = b->items.data();
@@ -851,7 +882,7 @@ extern "C" int s2c_layout(int64_t *out, int n) {
     const int64_t v[] = {
         (int64_t)sizeof(s2c_dev), (int64_t)offsetof(s2c_dev, tile_max), (int64_t)offsetof(s2c_dev, thresholds),
         (int64_t)offsetof(s2c_dev, fill), (int64_t)offsetof(s2c_dev, counts), (int64_t)offsetof(s2c_dev, ins_chr),
-        (int64_t)offsetof(s2c_dev, stats), (int64_t)offsetof(s2c_dev, out_cap),
+        (int64_t)offsetof(s2c_dev, tile_stats), (int64_t)offsetof(s2c_dev, out_cap),
         (int64_t)sizeof(s2c_synth_spec), (int64_t)offsetof(s2c_synth_spec, seed),
         (int64_t)sizeof(s2c_batch_info), (int64_t)sizeof(s2c_batch_arrays), (int64_t)sizeof(s2c_ws_sizes)};
     const int m = (int)(sizeof(v) / sizeof(v[0]));

@@ -5,16 +5,16 @@
 // vote (:232-253, :344-389).  Here it is a stream-ordered chain over the packed batch
 // built by s2c_host.cpp, whose unit is the TILE (≤2048 positions of one reference):
 //
-//   k_prep                 zero per-run state (replaces memsets: one launch)
-//   k_ins_count            (3) insertion column symbol counts per key (:262-287)
 //   k_pileup               (2) bit-sliced counting of the word-major seqout records per
-//                          tile (32 positions per VALU op), and (4) for tiles voted in one
-//                          work item the vote epilogue: all thresholds, IUPAC, min-depth/
-//                          fill, per-(ref,t) stats — counts never reach HBM
-//   k_consensus            (4) the same vote for "deep" tiles whose records were split
-//                          over several work items (counts summed in HBM)
-//   k_ins_vote             (4) insertion columns of called keys (:290-311, :370-385)
-//   k_scan / k_assemble    device FASTA body assembly (tile scan + byte scatter)
+//                          tile (32 positions per VALU op), then for a tile whose whole
+//                          depth is in one work item the tile epilogue: (3) its insertion
+//                          columns (:256-294) and (4) the vote for all thresholds, IUPAC,
+//                          min-depth/fill, insertion chars, tile statistics — counts never
+//                          reach HBM
+//   k_prep / k_consensus   "deep" tiles (records split over several work items): zero their
+//                          HBM count range, the items add into it, then the same epilogue
+//   k_assemble             device FASTA body assembly: decoupled look-back scan of the
+//                          block lengths + byte scatter
 //
 // Everything is integer counting; the single floating-point operation is the
 // reference's `cov_nucs < t*coverage` (:362, :376), evaluated as
@@ -69,42 +69,50 @@ __constant__ uint8_t c_amb[64] = {
 
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
-__device__ __forceinline__ uint32_t nibble(const uint32_t *__restrict__ w, uint64_t idx) {
-    return (w[idx >> 3] >> ((idx & 7) * 4)) & 15u;
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for
+// its global stores (__syncthreads also drains vmcnt, i.e. waits for every outstanding
+// store of the wave — microseconds under load).  Global data shared inside a workgroup
+// waits explicitly (s_waitcnt vmcnt(0)) before it.
+__device__ __forceinline__ void lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-template <typename T>
-__device__ __forceinline__ T block_sum(T v, T *sh) {   // 256-thread workgroup sum, all threads get it
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    const uint32_t w = threadIdx.x >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) sh[w] = v;
-    __syncthreads();
-    T r = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) r += sh[i];
-    return r;
+__device__ __forceinline__ uint32_t nibble(const uint32_t *__restrict__ w, uint64_t idx) {
+    return (w[idx >> 3] >> ((idx & 7) * 4)) & 15u;
 }
 
 // Closed form of the group-sort vote (proven equal to :241-251 +
 // :359-366 in tests/test_oracle.py): symbol i is taken iff c_i != 0 and the sum of the
 // counts strictly greater than c_i is < t·cov (fp64 product, exact integer compare).
-template <typename T>
-__device__ __forceinline__ void greater_sums(const T (&c)[NSYM], int64_t (&s)[NSYM]) {
+template <typename T, typename S>
+__device__ __forceinline__ void greater_sums(const T (&c)[NSYM], S (&s)[NSYM]) {
 #pragma unroll
     for (int i = 0; i < (int)NSYM; i++) {
-        int64_t a = 0;
+        S a = 0;
 #pragma unroll
-        for (int j = 0; j < (int)NSYM; j++) a += (c[j] > c[i]) ? (int64_t)c[j] : 0;
+        for (int j = 0; j < (int)NSYM; j++) a += (c[j] > c[i]) ? (S)c[j] : (S)0;
         s[i] = a;
     }
 }
-template <typename T>
-__device__ __forceinline__ uint32_t vote_mask(const T (&c)[NSYM], const int64_t (&s)[NSYM], double tc) {
+template <typename T, typename S>
+__device__ __forceinline__ uint32_t vote_mask(const T (&c)[NSYM], const S (&s)[NSYM], double tc) {
     uint32_t m = 0;
 #pragma unroll
     for (int i = 0; i < (int)NSYM; i++) m |= ((c[i] != 0) && ((double)s[i] < tc)) ? (1u << i) : 0u;
+    return m;
+}
+
+// The same mask for non-negative integer sums with one fp64 product x = t·cov per call:
+// for an integer S, S < x ⟺ S ≤ lim with lim = ⌈x⌉ − 1 (x > 0; no S ≥ 0 is < x ≤ 0 or
+// NaN), so the six tests are u32 compares.  Exact: x is the reference's own product.
+__device__ __forceinline__ uint32_t vote_mask_u32(const uint32_t (&c)[NSYM], const uint32_t (&s)[NSYM], double x) {
+    if (!(x > 0.0)) return 0u;
+    const uint32_t lim = x > 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)(ceil(x) - 1.0);
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < (int)NSYM; i++) m |= ((c[i] != 0) && (s[i] <= lim)) ? (1u << i) : 0u;
     return m;
 }
 
@@ -114,205 +122,381 @@ __device__ __forceinline__ uint32_t key_index(const s2c_dev &d, uint32_t p, uint
     return d.ins_rank[p >> 5] + (uint32_t)__popc(bits & ((1u << (p & 31)) - 1u));
 }
 
+// Diagnostic phase stamps (ablate bit 0x100, k_pileup only): thread 0 of work item i writes
+// s_memrealtime (100 MHz) for phase k to ((u64*)counts)[16i + k] (scripts/phases.py).
+#define S2C_STAMP(dd, k)                                                                          \
+    do {                                                                                          \
+        if (((dd).ablate & 0x100) && (dd).n_deep == 0 && threadIdx.x == 0)                       \
+            ((uint64_t *)(dd).counts)[(size_t)blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+
 // ======================================================================= per-run state
-// One launch zeroes everything a run accumulates into: per-(ref,t) stats, flags, the
-// insertion bitmap / hash table / column counts, and the count ranges of deep tiles.
-constexpr int PREP_BLOCKS = 512;
+// Deep tiles add their work items' counts into HBM: their count ranges are zeroed first.
+// (Nothing else accumulates across workgroups: tile statistics and lengths are plain
+// stores, insertion columns are counted per tile, and the completion counter of the
+// epilogues wraps back to zero by itself.)
 __global__ __launch_bounds__(WG) void k_prep(const s2c_dev d) {
-    if (blockIdx.x < PREP_BLOCKS) {
-        const size_t i0 = (size_t)blockIdx.x * WG + threadIdx.x, step = (size_t)PREP_BLOCKS * WG;
-        const size_t n_stats = (size_t)d.n_refs * d.n_thr * 4, n_cols = (size_t)d.n_cols * NSYM;
-        for (size_t i = i0; i < n_stats; i += step) d.stats[i] = 0;
-        for (size_t i = i0; i < 16; i += step) d.scalars[i] = 0;
-        for (size_t i = i0; i < n_cols; i += step) d.ins_cols[i] = 0;
-        return;
-    }
-    const uint32_t t = d.deep[blockIdx.x - PREP_BLOCKS];
+    const uint32_t t = d.deep[blockIdx.x];
     const uint32_t a = d.blocks[(size_t)t * S2C_BLOCK_WORDS], n = d.blocks[(size_t)t * S2C_BLOCK_WORDS + 1] - a;
     for (uint32_t c = 0; c < NSYM; c++)
         for (uint32_t i = threadIdx.x; i < n; i += WG) d.counts[(size_t)c * d.padded_len + a + i] = 0;
 }
 
-// ======================================================================= (3) insertions
-// (:264-271) motif multiplicities and (:284-287) per-column sums are additive: column c of
-// key k counts motif[c] over the key's events with len > c.  The host groups events by
-// key (sorted) and cuts them into units of ≤ S2C_INS_UNIT events; one thread per unit
-// counts every column of its key (columns outer, its events inner) and stores the six
-// counts, or adds them when the key is split over several units.  The columns are voted
-// (with '-' = cov[key] − Σ column, :294) by k_ins_vote.
-__global__ __launch_bounds__(WG) void k_ins_count(const s2c_dev d) {
-    const uint32_t u = blockIdx.x * WG + threadIdx.x;
-    if (u >= (uint32_t)d.n_units) return;
-    const uint32_t k = d.ins_units[2 * u], e0 = d.ins_units[2 * u + 1];
-    const uint32_t ke0 = d.ins_koff[k], ke1 = d.ins_koff[k + 1];
-    const uint32_t e1 = min(ke1, e0 + (uint32_t)S2C_INS_UNIT);
-    const bool whole = e0 == ke0 && e1 == ke1;
-    const uint32_t cb = d.ins_kcol[k], ml = d.ins_kcol[k + 1] - cb;
-    for (uint32_t c = 0; c < ml; c++) {
-        uint32_t cnt[NSYM] = {0, 0, 0, 0, 0, 0};
-        for (uint32_t e = e0; e < e1; e++) {
-            const uint32_t o0 = d.ins_off[e];
-            if (c < d.ins_off[e + 1] - o0) cnt[nibble(d.ins_bases, (uint64_t)o0 + c)]++;
-        }
-        uint32_t *col = d.ins_cols + (size_t)(cb + c) * NSYM;
-#pragma unroll
-        for (uint32_t j = 0; j < NSYM; j++) {
-            if (whole) col[j] = cnt[j];
-            else if (cnt[j]) atomicAdd(&col[j], cnt[j]);
-        }
-    }
-}
+// ======================================================================= (3)+(4) tile epilogue
+// Runs once per tile, in the workgroup that holds the tile's whole depth (k_pileup for a
+// tile voted in one work item, k_consensus for a deep tile), after its counts are complete.
+//
+// (3) Insertion columns (:256-294).  Motif multiplicities (:264-271) and column sums
+// (:284-287) are additive: column c of key k counts motif[c] over the key's events with
+// len > c.  The tile's keys, events and columns are contiguous ranges (block words 4-9);
+// one thread per event adds its motif's symbols into the tile's column counts [ncol][6] —
+// in LDS when ncol ≤ the LDS capacity, else in the tile's own slice of HBM ins_cols.  The
+// first 256 event and key records were prefetched into LDS while the counts streamed.
+//
+// (4) The vote (:344-389).  Per position: the closed-form vote for every threshold and the
+// IUPAC char (or fill when cov == 0 or cov < min_depth, :356-359); len and sumcov do not
+// depend on the threshold (1 per called position or len(fill); cov, :357/:385), the
+// per-threshold non-'-' and vote-error counts are wave ballots.  Then the insertion
+// columns of each called key (:290-311, :370-385), thread per key: '-' = cov[key] − Σ
+// column (:294, signed), '-' results skipped, others emitted (ins_chr, ins_cnt) and added
+// to len / non-'-' / sumcov (cov per emitted char, :385).  The tile's statistics per
+// threshold go to tile_stats and its body lengths to blk_len — plain stores.
 
-// ======================================================================= (4) vote epilogue
-// Per position: the closed-form vote for every threshold and the IUPAC char (or fill when
-// cov == 0 or cov < min_depth, :356-389).  Per tile: len and sumcov do not depend on the
-// threshold (1 per called position or len(fill); cov, :357/:385), the per-threshold
-// non-'-' and vote-error counts are wave ballots.  At a position carrying an insertion key
-// the key's coverage (0 when not called) is stored for k_ins_vote, which votes the
-// insertion columns (:290-311, :370-385) and adds their chars to the same stats.
-constexpr int VT_TMAX = 16;   // thresholds per pass over the tile's positions
-constexpr int VT_ACC = 2 + 2 * VT_TMAX;   // LDS u64: sumcov, len, {nondash, nerr}[VT_TMAX]
+constexpr int VT_TMAX = 16;                   // thresholds per pass over the tile's positions
+constexpr int VT_ACC = 2 + 4 * VT_TMAX;       // LDS u64: sumcov, len, {nondash, nerr, ins sumcov, ins len}[VT_TMAX]
+constexpr uint32_t PF = WG;                   // event / key records prefetched into LDS per tile
+constexpr int THR_MAX = WG;                   // thresholds (-c values) supported: all staged in LDS
 
+// s_waitcnt vmcnt(0) as a real S_WAITCNT (the compiler's wait tracking sees it): ends the
+// rare HBM-reading branches of the epilogue so that no load is "maybe pending" after them —
+// a maybe-pending load makes the compiler wait on every later register reuse, and vmcnt is
+// in order, i.e. it waits for all the vote bytes stored meanwhile.
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+extern "C" __device__ __attribute__((const)) unsigned long long __ockl_wfred_add_u64(unsigned long long);
+
+// Sum over the wave's active lanes, every lane gets it: the device library's DPP reduction
+// (row shifts / broadcasts in the VALU) — a butterfly of __shfl_xor is a dependent chain
+// of ds_bpermute round trips through the LDS pipe, ~5x slower.
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    if constexpr (sizeof(T) == 8) return (T)__ockl_wfred_add_u64((unsigned long long)v);
+    else return (T)__ockl_wfred_add_u32((unsigned int)v);
 }
 
-// acc: LDS [VT_ACC] u64; amb: LDS copy of c_amb.
-template <class Fetch>
-__device__ __forceinline__ void vote_tile(const s2c_dev &d, uint32_t tile, uint32_t ref, uint32_t a, uint32_t n,
-                                          Fetch fetch, unsigned long long *acc, const uint8_t *amb) {
+template <bool LDSC>
+__device__ __forceinline__ uint32_t col_load(const uint32_t *p) {
+    if constexpr (LDSC) return *p;
+    else return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // the L2 copy
+}
+
+// Vote of one insertion column (:290-311) for up to 4 thresholds th[0..tn): counts v[6] of
+// the column's motif symbols, the '-' count replaced by cov − Σ v (:294, signed: the
+// column's own '-' count is in the sum); returns the 4 masks packed in bytes.  The group
+// sums are computed once; exact in int32 while every count is < 2^28 (always, in
+// practice), int64 beyond.
+template <typename S, class V>
+__device__ __forceinline__ uint32_t column_masks_t(const V &col, uint32_t cov, const double *th, int tn) {
+    S v[NSYM], g[NSYM];
+    S tot = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < NSYM; j++) { v[j] = (S)col[j]; tot += v[j]; }
+    v[0] = (S)cov - tot;
+    greater_sums(v, g);
+    uint32_t m = 0;
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+        if (u < tn) m |= vote_mask(v, g, th[u] * (double)cov) << (8 * u);
+    return m;
+}
+template <class V>
+__device__ __forceinline__ uint32_t column_masks(const V &col, uint32_t cov, const double *th, int tn) {
+    uint32_t mx = cov;
+#pragma unroll
+    for (uint32_t j = 0; j < NSYM; j++) mx = max(mx, (uint32_t)col[j]);
+    if (mx < (1u << 28)) return column_masks_t<int32_t>(col, cov, th, tn);   // |Σ| < 6·2^28 < 2^31
+    return column_masks_t<int64_t>(col, cov, th, tn);
+}
+
+// The tile's insertion ranges (block words 4-9) and the LDS of its epilogue.
+struct TileIns {
+    uint32_t klo, khi, e0, e1, cb0, cb1;
+};
+__device__ __forceinline__ TileIns tile_ins(const uint32_t *blk) {
+    const uint4 v1 = *(const uint4 *)(blk + 4);
+    const uint2 v2 = *(const uint2 *)(blk + 8);
+    return {uni(v1.x), uni(v1.y), uni(v1.z), uni(v1.w), uni(v2.x), uni(v2.y)};
+}
+// Everything the epilogue reads lives in LDS (see vm_drain).
+template <uint32_t ICOL>   // LDS insertion columns of the kernel variant
+struct EpiLds {
+    uint4 ev[PF];                      // event records ins_ev[e0 .. e0+PF)
+    uint4 key[PF];                     // key records ins_kinfo[klo .. klo+PF)
+    double thr[THR_MAX];               // -c thresholds, CLI order
+    unsigned long long acc[VT_ACC];
+    uint32_t kcov[PF];                 // coverage of each key's position if called, else 0
+    uint16_t colkey[ICOL];             // key slot of each tile column
+    uint32_t vchr[ICOL];               // vote chars of each tile column, 4 thresholds per word
+    uint8_t amb[64];
+};
+// issue the prefetch loads (registers; stored into LDS by prefetch_store)
+struct Prefetch {
+    uint4 ev, key;
+    double thr;
+};
+__device__ __forceinline__ void prefetch_load(const s2c_dev &d, const TileIns &ti, Prefetch &pf) {
+    const uint32_t tid = threadIdx.x;
+    pf.ev = make_uint4(0, 0, 0, 0);
+    pf.key = make_uint4(0, 0, 0, 0);
+    pf.thr = 0.0;
+    if (ti.e0 + tid < ti.e1) pf.ev = ((const uint4 *)d.ins_ev)[ti.e0 + tid];
+    if (ti.klo + tid < ti.khi) pf.key = ((const uint4 *)d.ins_kinfo)[ti.klo + tid];
+    if (tid < (uint32_t)d.n_thr) pf.thr = d.thresholds[tid];
+}
+template <class EL>
+__device__ __forceinline__ void prefetch_store(const s2c_dev &d, EL &L, const Prefetch &pf) {
+    L.ev[threadIdx.x] = pf.ev;
+    L.key[threadIdx.x] = pf.key;
+    if (threadIdx.x < (uint32_t)d.n_thr) L.thr[threadIdx.x] = pf.thr;
+}
+
+// cols: LDS [ICOL][6] (LDSC) or the tile's HBM slice.  fetch(q, c) = count of symbol c at
+// tile position q.  Every thread calls (barriers inside).  Order: insertion columns counted,
+// then per threshold pass the insertion vote and the position vote (whose byte stores come
+// last, so nothing waits on them), then the tile totals.
+template <bool LDSC, class Fetch, class EL>
+__device__ __forceinline__ void tile_epilogue(const s2c_dev &d, uint32_t tile, uint32_t a, uint32_t n,
+                                              const TileIns &ti, Fetch fetch, uint32_t *cols, EL &L) {
     const int T = d.n_thr;
-    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const bool no_ins = (d.ablate & 0x200) != 0;   // diagnostic: skip (3)/(4) insertions
+    if (ti.khi > ti.klo && !no_ins) {   // (3) count the tile's insertion columns (uniform branch)
+        const uint32_t ncol = ti.cb1 - ti.cb0;
+        for (uint32_t i = tid; i < ncol * NSYM; i += WG) cols[i] = 0;
+        if constexpr (!LDSC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // zeros in L2 before any atomic
+        lds_sync();   // also publishes the prefetched records
+        auto add_event = [&](const uint4 r) {
+            uint32_t *cc = cols + (size_t)r.x * NSYM;
+            for (uint32_t c = 0; c < r.y; c++) {
+                uint32_t sym;
+                if (c < 8) {
+                    sym = (r.w >> (4 * c)) & 15u;
+                } else {
+                    sym = nibble(d.ins_bases, (uint64_t)r.z + c);   // motifs > 8 bases (rare)
+                    vm_drain();
+                }
+                atomicAdd(&cc[c * NSYM + sym], 1u);
+            }
+        };
+        // the prefetched records from LDS, the rest (tiles with > PF events) from HBM: two
+        // loops, so the compiler cannot merge the two sources into one flat load
+        if (ti.e0 + tid < ti.e1) add_event(L.ev[tid]);
+        for (uint32_t e = ti.e0 + PF + tid; e < ti.e1; e += WG) {
+            const uint4 r = ((const uint4 *)d.ins_ev)[e];
+            vm_drain();
+            add_event(r);
+        }
+        if constexpr (!LDSC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // atomics done before the reads
+        // published by the barrier after the accumulator zeroing below
+    }
+    S2C_STAMP(d, 3);
     for (int t0 = 0; t0 < T; t0 += VT_TMAX) {
         const int t1 = min(T, t0 + VT_TMAX);
-        if (threadIdx.x < (uint32_t)VT_ACC && (t0 == 0 || threadIdx.x >= 2)) acc[threadIdx.x] = 0;
-        __syncthreads();
-        uint64_t sumcov = 0, len = 0;
-        for (uint32_t q0 = 0; q0 < n; q0 += WG) {   // uniform trip count: every lane votes in the ballots
-            const uint32_t q = q0 + threadIdx.x, p = a + q;
-            const bool in = q < n;
-            uint32_t cnt[NSYM];
-            uint64_t cov = 0;
+        for (uint32_t i = tid; i < (uint32_t)VT_ACC; i += WG) L.acc[i] = 0;
+        lds_sync();
+        // (4) insertion columns of called keys (:290-311, :370-385).  Every column's vote
+        // char goes to ins_chr[t][column] ('-' and vote errors included); k_assemble emits
+        // the key's chars that are neither; ins_cnt[t][k] = {emitted, first column, columns}.
+        uint4 *cnt_out = (uint4 *)d.ins_cnt;
+        const uint32_t nkeys = ti.khi - ti.klo, ncol = ti.cb1 - ti.cb0;
+        if (no_ins) {
+        } else if (LDSC && nkeys <= PF) {
+            // column-parallel: key coverage + column→key map, then one thread per column
+            if (tid < nkeys) {
+                const uint4 kr = L.key[tid];
+                uint32_t cov = 0;
 #pragma unroll
-            for (uint32_t c = 0; c < NSYM; c++) { cnt[c] = in ? fetch(q, c) : 0u; cov += cnt[c]; }
-            const bool called = in && cov > 0 && (int64_t)cov >= (int64_t)d.min_depth;   // :359
-            if (t0 == 0) {
-                sumcov += cov;
-                len += called ? 1u : (in ? (uint32_t)d.fill_len : 0u);
-                const uint32_t bits = in ? d.ins_bits[p >> 5] : 0u;
-                if (bits >> (p & 31) & 1u) d.key_cov[key_index(d, p, bits)] = called ? (uint32_t)cov : 0u;
+                for (uint32_t c = 0; c < NSYM; c++) cov += fetch(kr.x - a, c);
+                L.kcov[tid] = (cov > 0 && (int64_t)cov >= (int64_t)d.min_depth) ? cov : 0u;   // :356-358
+                for (uint32_t c = 0; c < kr.z; c++) L.colkey[kr.y - ti.cb0 + c] = (uint16_t)tid;
             }
-            int64_t gs[NSYM];
-            greater_sums(cnt, gs);
-            const uint32_t n_unc = (uint32_t)__popcll(__ballot(in && !called));
-            for (int t = t0; t < t1; t++) {
-                const double tc = d.thresholds[t] * (double)cov;
-                const uint8_t code = called ? amb[vote_mask(cnt, gs, tc)] : (uint8_t)S2C_CODE_FILL;
-                if (in) d.codes[(size_t)t * d.padded_len + p] = code;
-                const uint32_t nd = (uint32_t)__popcll(__ballot(called && code != '-'));
-                const uint32_t ne = (uint32_t)__popcll(__ballot(called && code == 0xFF));
-                if (lane == 0) {
-                    atomicAdd(&acc[2 + 2 * (t - t0)], (unsigned long long)(nd + (uint64_t)d.fill_nondash * n_unc));
-                    if (ne) atomicAdd(&acc[3 + 2 * (t - t0)], (unsigned long long)ne);
-                }
-            }
-        }
-        if (t0 == 0) {
-            sumcov = wave_sum(sumcov);
-            len = wave_sum(len);
-            if (lane == 0) {
-                atomicAdd(&acc[0], (unsigned long long)sumcov);
-                atomicAdd(&acc[1], (unsigned long long)len);
-            }
-        }
-        __syncthreads();
-        if (threadIdx.x < 4 * (uint32_t)(t1 - t0)) {   // tile totals → stats[ref][t], blk_len
-            const uint32_t t = t0 + threadIdx.x / 4, k = threadIdx.x % 4;
-            const unsigned long long v = k < 2 ? acc[k] : acc[2 + 2 * (t - t0) + (k - 2)];
-            uint64_t *st = d.stats + ((size_t)ref * T + t) * 4;
-            if (v) atomicAdd((unsigned long long *)&st[k], v);
-            if (k == 3 && v) atomicOr(&d.scalars[1], 1u);
-            if (k == 1) d.blk_len[(size_t)t * d.n_blocks + tile] = v;
-        }
-        __syncthreads();
-    }
-}
-
-// Insertion columns of the called keys of one tile (grid = tiles; the tile's keys are the
-// contiguous range [rank(a), rank(b)); dynamic LDS [T][4] u64): per column and threshold
-// the same vote with '-' = cov[key] − Σ column (:294, signed); '-' results are skipped,
-// others emitted after the key's base (:370-385) and added to the tile's len / non-'-' /
-// sumcov (cov per emitted char, :385) and block length.
-__global__ __launch_bounds__(WG) void k_ins_vote(const s2c_dev d) {
-    extern __shared__ unsigned long long iacc[];   // [T][4]
-    __shared__ uint32_t em[VT_TMAX][WG];           // emitted chars per (threshold, thread)
-    __shared__ uint8_t amb[64];
-    const uint32_t tid = threadIdx.x;
-    const uint32_t tile = blockIdx.x;
-    const uint32_t *blk = d.blocks + (size_t)tile * S2C_BLOCK_WORDS;
-    const uint32_t a = uni(blk[0]), b = uni(blk[1]), ref = uni(blk[2]);
-    const uint32_t klo = uni(d.ins_rank[a >> 5]), khi = uni(d.ins_rank[(b + 31) >> 5]);
-    if (klo == khi) return;
-    const int T = d.n_thr;
-    for (uint32_t i = tid; i < 4u * (uint32_t)T; i += WG) iacc[i] = 0;
-    if (tid < 64) amb[tid] = c_amb[tid];
-    __syncthreads();
-    const uint32_t *__restrict__ cols = d.ins_cols;
-    uint8_t *__restrict__ chr = d.ins_chr;
-    for (uint32_t k = klo + tid; k < khi; k += WG) {
-        const uint32_t cov = d.key_cov[k];
-        if (cov == 0) continue;   // position not called: no insertion chars (:356-358)
-        const uint32_t cb = d.ins_kcol[k], ml = d.ins_kcol[k + 1] - cb;
-        for (int t0 = 0; t0 < T; t0 += VT_TMAX) {
-            const int t1 = min(T, t0 + VT_TMAX);
-            for (int t = t0; t < t1; t++) em[t - t0][tid] = 0;
-            for (uint32_t c0 = 0; c0 < ml; c0 += 4) {   // 4 columns' loads in flight
-                uint32_t cv[4][NSYM];
+            for (int tg = t0; tg < t1; tg += 4) {   // 4 thresholds per column pass
+                const int tn = min(4, t1 - tg);
+                lds_sync();
+                S2C_STAMP(d, 8);
+                // column votes; the tile totals of the emitted chars come from here (Σ over a
+                // key's columns = the key's chars): ballot counts, one u64 sum per threshold
+                uint64_t cs[4] = {0, 0, 0, 0};   // Σ cov over emitted chars (:385)
+                uint32_t ec[4] = {0, 0, 0, 0}, nc[4] = {0, 0, 0, 0};   // emitted / error chars (wave)
+                for (uint32_t jb = 0; jb < ncol; jb += WG) {   // uniform trip count (ballots)
+                    const uint32_t j = jb + tid;
+                    const uint32_t cov = j < ncol ? L.kcov[L.colkey[j]] : 0u;
+                    uint32_t word = 0x2D2D2D2Du;   // '-' (not called: never emitted)
+                    if (cov) {
+                        const uint32_t m = column_masks(cols + (size_t)j * NSYM, cov, &L.thr[tg], tn);
+                        word = 0;
 #pragma unroll
-                for (int u = 0; u < 4; u++)
+                        for (int u = 0; u < 4; u++) word |= (uint32_t)L.amb[(m >> (8 * u)) & 63u] << (8 * u);
+                    }
+                    if (j < ncol) {
+                        L.vchr[j] = word;
+                        for (int u = 0; u < tn; u++)
+                            d.ins_chr[(size_t)(tg + u) * d.n_cols + ti.cb0 + j] = (uint8_t)(word >> (8 * u));
+                    }
 #pragma unroll
-                    for (uint32_t j = 0; j < NSYM; j++)
-                        cv[u][j] = c0 + u < ml ? cols[(size_t)(cb + c0 + u) * NSYM + j] : 0u;
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    if (c0 + u >= ml) break;
-                    int64_t v[NSYM];
-                    int64_t tot = 0;
-#pragma unroll
-                    for (uint32_t j = 0; j < NSYM; j++) { v[j] = cv[u][j]; tot += v[j]; }
-                    v[0] = (int64_t)cov - tot;   // :294 (the column's own '-' count is in the sum)
-                    int64_t g2[NSYM];
-                    greater_sums(v, g2);
-                    for (int t = t0; t < t1; t++) {
-                        const uint8_t ic = amb[vote_mask(v, g2, d.thresholds[t] * (double)cov)];
-                        if (ic == 0xFF) { atomicAdd(&iacc[4 * t + 3], 1ull); continue; }
-                        if (ic != '-') chr[(size_t)t * d.n_cols + cb + em[t - t0][tid]++] = ic;
+                    for (int u = 0; u < 4; u++) {
+                        const uint8_t ic = (uint8_t)(word >> (8 * u));
+                        const bool em = cov && ic != '-' && ic != 0xFF;
+                        ec[u] += (uint32_t)__popcll(__ballot(em));
+                        nc[u] += (uint32_t)__popcll(__ballot(cov && ic == 0xFF));
+                        cs[u] += em ? cov : 0u;
                     }
                 }
+                if (tid < ((ncol + 63) & ~63u)) {   // waves that held columns
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        if (u >= tn) break;
+                        const uint64_t scs = wave_sum(cs[u]);
+                        if (lane == 0) {
+                            unsigned long long *at = L.acc + 2 + 4 * (tg + u - t0);
+                            if (nc[u]) atomicAdd(&at[1], (unsigned long long)nc[u]);
+                            if (ec[u]) {
+                                atomicAdd(&at[2], (unsigned long long)scs);
+                                atomicAdd(&at[3], (unsigned long long)ec[u]);
+                            }
+                        }
+                    }
+                }
+                S2C_STAMP(d, 9);
+                lds_sync();
+                S2C_STAMP(d, 10);
+                if (tid < nkeys && L.kcov[tid]) {   // per key: chars emitted per threshold
+                    const uint4 kr = L.key[tid];
+                    uint32_t em[4] = {0, 0, 0, 0};
+                    for (uint32_t c = 0; c < kr.z; c++) {
+                        const uint32_t wv = L.vchr[kr.y - ti.cb0 + c];
+#pragma unroll
+                        for (int u = 0; u < 4; u++) {
+                            const uint8_t ic = (uint8_t)(wv >> (8 * u));
+                            em[u] += (ic != '-' && ic != 0xFF) ? 1u : 0u;
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        if (u < tn) cnt_out[(size_t)(tg + u) * d.n_keys + ti.klo + tid] = make_uint4(em[u], kr.y, kr.z, 0);
+                }
             }
+        } else {
+            // general: one thread per key, its columns in turn (> PF keys or HBM columns)
+            auto vote_key = [&](const uint32_t k, const uint4 kr) {
+                uint32_t cov = 0;
+#pragma unroll
+                for (uint32_t c = 0; c < NSYM; c++) cov += fetch(kr.x - a, c);
+                if (cov == 0 || (int64_t)cov < (int64_t)d.min_depth) return;   // not called: no chars
+                const uint32_t *kcols = cols + (size_t)(kr.y - ti.cb0) * NSYM;
+                for (int t = t0; t < t1; t++) {
+                    uint32_t em = 0, ne = 0;
+                    for (uint32_t c = 0; c < kr.z; c++) {
+                        uint32_t v[NSYM];
+#pragma unroll
+                        for (uint32_t j = 0; j < NSYM; j++) v[j] = col_load<LDSC>(kcols + c * NSYM + j);
+                        const uint8_t ic = L.amb[column_masks(v, cov, &L.thr[t], 1) & 63u];
+                        em += (ic != '-' && ic != 0xFF) ? 1u : 0u;
+                        ne += ic == 0xFF ? 1u : 0u;
+                        d.ins_chr[(size_t)t * d.n_cols + kr.y + c] = ic;
+                    }
+                    cnt_out[(size_t)t * d.n_keys + k] = make_uint4(em, kr.y, kr.z, 0);
+                    unsigned long long *at = L.acc + 2 + 4 * (t - t0);
+                    if (ne) atomicAdd(&at[1], (unsigned long long)ne);
+                    if (em) {
+                        atomicAdd(&at[2], (unsigned long long)cov * em);
+                        atomicAdd(&at[3], (unsigned long long)em);
+                    }
+                }
+            };
+            if (tid < nkeys && tid < PF) vote_key(ti.klo + tid, L.key[tid]);
+            for (uint32_t k = ti.klo + PF + tid; k < ti.khi; k += WG) {
+                const uint4 kr = ((const uint4 *)d.ins_kinfo)[k];
+                vm_drain();
+                vote_key(k, kr);
+            }
+            if (!LDSC) vm_drain();   // the sc1 column loads
+        }
+        S2C_STAMP(d, 4);
+        // positions: 2 consecutive per thread, each threshold's two codes in one 2-byte store
+        uint64_t sumcov = 0, len = 0;
+        for (uint32_t qb = 0; qb < n; qb += 2 * WG) {   // uniform trip count (ballots inside)
+            const uint32_t q0 = qb + 2 * tid;
+            // per-position coverage < 2^32 (the batch holds < 2^32 read pieces): u32 sums exact
+            uint32_t cnt[2][NSYM], gs[2][NSYM], cov[2];
+            bool in[2], called[2];
+            uint32_t n_unc = 0;
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                in[u] = q0 + u < n;
+                cov[u] = 0;
+#pragma unroll
+                for (uint32_t c = 0; c < NSYM; c++) { cnt[u][c] = in[u] ? fetch(q0 + u, c) : 0u; cov[u] += cnt[u][c]; }
+                called[u] = in[u] && cov[u] > 0 && (int64_t)cov[u] >= (int64_t)d.min_depth;   // :356-359
+                sumcov += cov[u];
+                len += called[u] ? 1u : (in[u] ? (uint32_t)d.fill_len : 0u);
+                n_unc += (uint32_t)__popcll(__ballot(in[u] && !called[u]));
+                greater_sums(cnt[u], gs[u]);
+            }
+            uint8_t *crow = d.codes + (size_t)a + q0;
             for (int t = t0; t < t1; t++) {
-                const uint32_t emitted = em[t - t0][tid];
-                d.ins_cnt[(size_t)t * d.n_keys + k] = emitted;
-                if (emitted) {
-                    atomicAdd(&iacc[4 * t + 0], (unsigned long long)cov * emitted);
-                    atomicAdd(&iacc[4 * t + 1], (unsigned long long)emitted);
-                    atomicAdd(&iacc[4 * t + 2], (unsigned long long)emitted);
+                const double th = L.thr[t];
+                uint32_t nd = 0, ne = 0, word = 0;
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const uint8_t code = called[u] ? L.amb[vote_mask_u32(cnt[u], gs[u], th * (double)cov[u])]
+                                                   : (uint8_t)S2C_CODE_FILL;
+                    word |= (uint32_t)code << (8 * u);
+                    nd += (uint32_t)__popcll(__ballot(called[u] && code != '-'));
+                    ne += (uint32_t)__popcll(__ballot(called[u] && code == 0xFF));
+                }
+                uint8_t *dst = crow + (size_t)t * d.padded_len;
+                if (d.ablate & 0x400) {   // diagnostic: no code stores
+                    if (word == 0x12345u) dst[0] = 1;
+                } else if (in[1]) *(uint16_t *)dst = (uint16_t)word;
+                else if (in[0]) dst[0] = (uint8_t)word;
+                if (lane == 0) {   // non-'-' chars: called non-'-' codes + fill chars of uncalled positions
+                    unsigned long long *at = L.acc + 2 + 4 * (t - t0);
+                    atomicAdd(&at[0], (unsigned long long)(nd + (uint64_t)d.fill_nondash * n_unc));
+                    if (ne) atomicAdd(&at[1], (unsigned long long)ne);
                 }
             }
         }
+        sumcov = wave_sum(sumcov);
+        len = wave_sum(len);
+        if (lane == 0) {
+            atomicAdd(&L.acc[0], (unsigned long long)sumcov);
+            atomicAdd(&L.acc[1], (unsigned long long)len);
+        }
+        lds_sync();
+        S2C_STAMP(d, 5);
+        for (uint32_t i = tid; i < (uint32_t)(t1 - t0); i += WG) {   // tile totals per threshold
+            const unsigned long long *at = L.acc + 2 + 4 * i;
+            const size_t j = (size_t)(t0 + i) * d.n_blocks + tile;
+            uint64_t *st = d.tile_stats + j * 4;
+            st[0] = L.acc[0] + at[2];   // sumcov
+            st[1] = L.acc[1] + at[3];   // len
+            st[2] = at[0] + at[3];      // non-'-' chars (insertion chars are never '-')
+            st[3] = at[1];              // vote errors (KeyError, :367/:381)
+            d.blk_len[j] = L.acc[1] + at[3];
+        }
+        lds_sync();   // acc is rezeroed by the next threshold pass
     }
-    __syncthreads();
-    for (uint32_t i = tid; i < 4u * (uint32_t)T; i += WG) {
-        const unsigned long long v = iacc[i];
-        if (!v) continue;
-        const uint32_t t = i / 4, k = i % 4;
-        atomicAdd((unsigned long long *)&d.stats[((size_t)ref * T + t) * 4 + k], v);
-        if (k == 3) atomicOr(&d.scalars[1], 1u);
-        if (k == 1) atomicAdd((unsigned long long *)&d.blk_len[(size_t)t * d.n_blocks + tile], v);
-    }
+    S2C_STAMP(d, 6);
+    S2C_STAMP(d, 7);
+}
+
+// the epilogue with the column buffer chosen by the tile's column count (uniform)
+template <uint32_t ICOL, class Fetch>
+__device__ __forceinline__ void tile_finish(const s2c_dev &d, uint32_t tile, uint32_t a, uint32_t n, const TileIns &ti,
+                                            Fetch fetch, uint32_t *lds_cols, EpiLds<ICOL> &L) {
+    if (ti.cb1 - ti.cb0 <= ICOL) tile_epilogue<true>(d, tile, a, n, ti, fetch, lds_cols, L);
+    else tile_epilogue<false>(d, tile, a, n, ti, fetch, d.ins_cols + (size_t)ti.cb0 * NSYM, L);
 }
 
 // ======================================================================= (2) pileup
@@ -419,32 +603,34 @@ __device__ __forceinline__ uint32_t hist_get(const uint32_t *h, uint32_t q) {
 // One workgroup per work item = (tile [a,b) of ≤ TW = 32·NWP positions, chunk k).  Lane
 // L owns 32-position word w = L mod NWP of the tile and lane group g = L / NWP (G = 256/NWP
 // lanes per word).  The word's seqout records [wrec[W], wrec[W+1]) are cut into chunks of
-// chunk_recs (= 248·G, one flush per lane); the item streams chunk k, lane g taking records
+// chunk_recs (≤ 248·G: one flush per lane); the item streams chunk k, lane g taking records
 // ≡ g (mod G), 8 at a time with the next 8 in flight (a group's lanes read consecutive
 // records: coalesced), counted by count8.  The flush transposes the counters, derives the
 // six symbol counts and adds them, two u16 per LDS atomic, into the tile's histogram.  A
-// tile voted in one item (not deep) is voted from LDS (vote_tile); a deep tile's chunks add
-// their histograms into HBM for k_consensus.
+// tile voted in one item (not deep) is finished from LDS by the tile epilogue (insertion
+// columns, vote, statistics), its event/key records prefetched under the count stream; a
+// deep tile's chunks add their histograms into HBM for k_consensus.
 template <int NWP>
 __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
     constexpr int G = WG / NWP, TW = NWP * 32, HP = TW / 2 + TW / 32;
-    constexpr uint32_t FB = FLUSH_RECS * G;   // records per word between flushes
+    // LDS insertion columns: ≤ 40 KB of LDS in all (4 workgroups per CU) at 512 positions
+    constexpr uint32_t ICOL = NWP <= 16 ? 736 : (NWP == 32 ? 512 : 256);
     __shared__ uint32_t hist[NSYM][HP];
-    __shared__ unsigned long long acc[VT_ACC];
-    __shared__ uint8_t amb[64];
+    __shared__ uint32_t cols[ICOL * NSYM];
+    __shared__ EpiLds<ICOL> L;
     const uint32_t tid = threadIdx.x;
     const uint32_t w = tid % NWP, g = tid / NWP;
-    if (tid < 64) amb[tid] = c_amb[tid];   // published by the barrier after the histogram zeroing
+    S2C_STAMP(d, 0);
+    if (tid < 64) L.amb[tid] = c_amb[tid];   // published by the barrier after the histogram zeroing
     const uint32_t *__restrict__ recs = d.recs;
     const uint32_t CH = (uint32_t)d.chunk_recs;
-    const uint32_t nfb = (CH + FB - 1) / FB;
     const uint32_t item = blockIdx.x;   // grid = work items
-    const uint32_t *it = d.items + (size_t)item * S2C_ITEM_WORDS;
-    const uint32_t a = uni(it[0]), b = uni(it[1]), chunk = uni(it[2]), tile = uni(it[3]);
+    const uint4 itv = ((const uint4 *)d.items)[item];
+    const uint32_t a = uni(itv.x), b = uni(itv.y), chunk = uni(itv.z), tile = uni(itv.w);
     const uint32_t *blk = d.blocks + (size_t)tile * S2C_BLOCK_WORDS;
-    const uint32_t ref = uni(blk[2]), deep = uni(blk[3]);
+    const uint32_t deep = uni(blk[3]);
+    const TileIns ti = tile_ins(blk);
     const uint32_t n = b - a;
-    for (uint32_t i = tid; i < NSYM * (uint32_t)HP; i += WG) (&hist[0][0])[i] = 0;
     const uint32_t ws = 32u * w;                  // word start, tile-relative
     const bool active = ws < n;
     uint32_t r0 = 0, r1 = 0;   // this word's records in chunk `chunk`
@@ -454,7 +640,12 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
         r0 = (uint32_t)min((uint64_t)we, (uint64_t)wb + (uint64_t)chunk * CH);
         r1 = (uint32_t)min((uint64_t)we, (uint64_t)r0 + CH);
     }
-    __syncthreads();
+    const bool finish = !deep && !(d.ablate & 4);
+    Prefetch pf;   // epilogue records, in flight under the count stream
+    if (finish) prefetch_load(d, ti, pf);
+    for (uint32_t i = tid; i < NSYM * (uint32_t)HP; i += WG) (&hist[0][0])[i] = 0;
+    lds_sync();
+    S2C_STAMP(d, 1);
     uint32_t V[NCTR][8];
     auto zeroV = [&]() {
 #pragma unroll
@@ -481,68 +672,70 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
     auto nvalid = [&](uint32_t t, uint32_t e0) -> uint32_t {
         return t < e0 ? min(8u, (e0 - t + G - 1) / G) : 0u;
     };
-    // counters of this lane's 32 positions → six symbol counts → LDS histogram
-    auto flush = [&](uint32_t nrec) {
-        if (active && !(d.ablate & 8)) {
-            uint32_t *h0 = &hist[0][0] + 17 * w;
-            auto add = [&](uint32_t sym, const uint32_t (&R)[8]) {
-                uint32_t *hw = h0 + sym * HP;
-#pragma unroll
-                for (int r = 0; r < 8; r++) {
-                    const uint32_t lo = R[r] & 0x00FF00FFu, hi = (R[r] >> 8) & 0x00FF00FFu;
-                    if (lo) atomicAdd(hw + r, lo);
-                    if (hi) atomicAdd(hw + 8 + r, hi);
-                }
-            };
-            const uint32_t nb = nrec * 0x01010101u;
-#pragma unroll
-            for (int pr = 0; pr < 3; pr++) {   // (O,A) → '-',A; (Y,G) → C,G; (Z,T) → N,T
-                uint32_t X[8], Y[8];
-#pragma unroll
-                for (int r = 0; r < 8; r++) { X[r] = V[2 * pr][r]; Y[r] = V[2 * pr + 1][r]; }
-                transpose8(X);
-                transpose8(Y);
-#pragma unroll
-                for (int r = 0; r < 8; r++) X[r] = pr == 0 ? nb - X[r] - Y[r] : X[r] - Y[r];   // no byte borrows
-                add(pr == 0 ? 0 : (pr == 1 ? 2 : 4), X);
-                add(pr == 0 ? 1 : (pr == 1 ? 3 : 5), Y);
-            }
-        }
-        zeroV();
-    };
     zeroV();
-    for (uint32_t fb = 0; fb < ((d.ablate & 1) ? 0u : nfb); fb++) {   // uniform
-        const uint32_t s0 = r0 + fb * FB, e0 = min(r1, s0 + FB);
-        uint32_t t = s0 + g, nrec = 0;
-        if (t < e0) {
-            // two groups of 8 per trip (one 16-record carry-save step), the next group
-            // always in flight while one is counted.  sched_barrier keeps each group's loads
-            // issued ahead of the other group's count (the scheduler otherwise sinks them
-            // next to their use to save registers).
-            uint32_t P[8][3], Q[8][3], ta[NCTR], tb[NCTR];
-            load8(P, t, e0);
-            for (; t < e0; t += 16 * G) {
-                load8(Q, t + 8 * G, e0);
-                __builtin_amdgcn_sched_barrier(0);
-                if (d.ablate & 2) sink8(P); else count8(V, P, ta);
-                load8(P, t + 16 * G, e0);
-                __builtin_amdgcn_sched_barrier(0);
-                if (d.ablate & 2) {
-                    sink8(Q);
-                    continue;
-                }
-                count8(V, Q, tb);
-#pragma unroll
-                for (int c = 0; c < NCTR; c++) close16(V[c], ta[c], tb[c]);
-                nrec += nvalid(t, e0) + nvalid(t + 8 * G, e0);
+    // ---- count this word's records of the chunk (one flush: chunk ≤ 248·G, check_dev) ----
+    const uint32_t e0 = (d.ablate & 1) ? r0 : r1;
+    uint32_t t = r0 + g, nrec = 0;
+    uint32_t P[8][3], Q[8][3];
+    if (t < e0) load8(P, t, e0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (finish) prefetch_store(d, L, pf);   // their loads were issued before P's
+    if (t < e0) {
+        // two groups of 8 per trip (one 16-record carry-save step), the next group always
+        // in flight while one is counted.  sched_barrier keeps each group's loads issued
+        // ahead of the other group's count (the scheduler otherwise sinks them next to
+        // their use to save registers).
+        uint32_t ta[NCTR], tb[NCTR];
+        for (; t < e0; t += 16 * G) {
+            load8(Q, t + 8 * G, e0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (d.ablate & 2) sink8(P); else count8(V, P, ta);
+            load8(P, t + 16 * G, e0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (d.ablate & 2) {
+                sink8(Q);
+                continue;
             }
+            count8(V, Q, tb);
+#pragma unroll
+            for (int c = 0; c < NCTR; c++) close16(V[c], ta[c], tb[c]);
+            nrec += nvalid(t, e0) + nvalid(t + 8 * G, e0);
         }
-        flush(nrec);
+    }
+    // ---- flush: counters → six symbol counts → LDS histogram ----
+    if (active && !(d.ablate & 8)) {
+        uint32_t *h0 = &hist[0][0] + 17 * w;
+        auto add = [&](uint32_t sym, const uint32_t (&R)[8]) {
+            uint32_t *hw = h0 + sym * HP;
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                const uint32_t lo = R[r] & 0x00FF00FFu, hi = (R[r] >> 8) & 0x00FF00FFu;
+                if (lo) atomicAdd(hw + r, lo);
+                if (hi) atomicAdd(hw + 8 + r, hi);
+            }
+        };
+        const uint32_t nb = nrec * 0x01010101u;
+#pragma unroll
+        for (int pr = 0; pr < 3; pr++) {   // (O,A) → '-',A; (Y,G) → C,G; (Z,T) → N,T
+            uint32_t X[8], Y[8];
+#pragma unroll
+            for (int r = 0; r < 8; r++) { X[r] = V[2 * pr][r]; Y[r] = V[2 * pr + 1][r]; }
+            transpose8(X);
+            transpose8(Y);
+#pragma unroll
+            for (int r = 0; r < 8; r++) X[r] = pr == 0 ? nb - X[r] - Y[r] : X[r] - Y[r];   // no byte borrows
+            add(pr == 0 ? 0 : (pr == 1 ? 2 : 4), X);
+            add(pr == 0 ? 1 : (pr == 1 ? 3 : 5), Y);
+        }
     }
     if (sink == 0x9E3779B9u) hist[0][0] = 1;   // keeps the ablation's loads alive
-    __syncthreads();
-    if (!deep && !(d.ablate & 4)) {   // the tile's whole depth is here: vote it now
-        vote_tile(d, tile, ref, a, n, [&](uint32_t q, uint32_t c) { return hist_get(hist[c], q); }, acc, amb);
+    // the count loop's last prefetch group is never consumed: drain it here (long landed),
+    // or every later reuse of its registers would wait behind the epilogue's stores
+    vm_drain();
+    lds_sync();
+    S2C_STAMP(d, 2);
+    if (finish) {   // the tile's whole depth is here: finish it now
+        tile_finish<ICOL>(d, tile, a, n, ti, [&](uint32_t q, uint32_t c) { return hist_get(hist[c], q); }, cols, L);
     } else {
         // deep tile: this chunk's counts → HBM (symbol-major, coalesced atomics); with the
         // diagnostic flag 4 every tile stores its counts instead of voting (parity tests)
@@ -560,107 +753,190 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
     }
 }
 
-// Deep tiles: counts summed in HBM by their work items → the same vote epilogue.
+// Deep tiles: counts summed in HBM by their work items → the same epilogue.
 __global__ __launch_bounds__(WG) void k_consensus(const s2c_dev d) {
-    __shared__ unsigned long long acc[VT_ACC];
-    __shared__ uint8_t amb[64];
-    if (threadIdx.x < 64) amb[threadIdx.x] = c_amb[threadIdx.x];   // published by vote_tile's first barrier
+    constexpr uint32_t ICOL = 1024;
+    __shared__ uint32_t cols[ICOL * NSYM];
+    __shared__ EpiLds<ICOL> L;
+    if (threadIdx.x < 64) L.amb[threadIdx.x] = c_amb[threadIdx.x];   // published by the epilogue's first barrier
     const uint32_t tile = d.deep[blockIdx.x];
     const uint32_t *blk = d.blocks + (size_t)tile * S2C_BLOCK_WORDS;
-    const uint32_t a = uni(blk[0]), n = uni(blk[1]) - a, ref = uni(blk[2]);
+    const uint32_t a = uni(blk[0]), n = uni(blk[1]) - a;
+    const TileIns ti = tile_ins(blk);
+    Prefetch pf;
+    prefetch_load(d, ti, pf);
+    prefetch_store(d, L, pf);
     const uint32_t *cts = d.counts + a;
-    const size_t L = d.padded_len;
-    vote_tile(d, tile, ref, a, n, [&](uint32_t q, uint32_t c) { return cts[(size_t)c * L + q]; }, acc, amb);
+    const size_t Lp = d.padded_len;
+    tile_finish<ICOL>(d, tile, a, n, ti, [&](uint32_t q, uint32_t c) { return cts[(size_t)c * Lp + q]; }, cols, L);
 }
 
 // ======================================================================= assembly
-// Exclusive scan of blk_len[T*n_blocks] (one workgroup, 1024 threads, chunked).
-__global__ __launch_bounds__(1024) void k_scan(uint64_t *v, int64_t n) {
-    __shared__ uint64_t sh[1024];
-    const int64_t per = (n + 1023) / 1024;
-    const int64_t b = threadIdx.x * per, e = (b + per < n) ? b + per : n;
-    uint64_t s = 0;
-    for (int64_t i = b; i < e; i++) s += v[i];
-    sh[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-        const uint64_t y = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0;
-        __syncthreads();
-        sh[threadIdx.x] += y;
-        __syncthreads();
-    }
-    uint64_t run = sh[threadIdx.x] - s;
-    for (int64_t i = b; i < e; i++) {
-        const uint64_t x = v[i];
-        v[i] = run;
-        run += x;
-    }
-    if (threadIdx.x == 1023) v[n] = sh[1023];
-}
+// Record body of (ref, t) = concatenation over its positions of fill (uncalled) or the
+// vote char followed by the emitted insertion chars (:367-389).  grid = n_blocks × T;
+// block j = t·n_blocks + tile writes at the exclusive prefix of blk_len ([t][tile] byte
+// order).  Up to ASM_DIRECT blocks each workgroup sums its own prefix (≤ 32 independent
+// loads per thread, L2-resident); beyond, k_scan writes blk_off first.
+constexpr uint64_t ASM_DIRECT = 32 * WG;
 
-// grid = n_blocks × T.  Record body of (ref, t) = concatenation over its positions of
-// fill (uncalled) or the vote char followed by the emitted insertion chars (:367-389).
-template <int ASM_PER>   // consecutive positions per thread (tile_max / 256)
-__global__ __launch_bounds__(WG) void k_assemble(const s2c_dev d) {
-    __shared__ uint64_t sh[WG / 64];
-    const uint32_t bi = blockIdx.x;
-    const int t = (int)blockIdx.y;
-    const uint32_t *blk = d.blocks + (size_t)bi * S2C_BLOCK_WORDS;
-    const uint32_t g0 = uni(blk[0]), g1 = uni(blk[1]);
-    const uint64_t base = d.blk_len[(size_t)t * d.n_blocks + bi];
-    const uint8_t *codes = d.codes + (size_t)t * d.padded_len;
-    const uint32_t p0 = g0 + ASM_PER * threadIdx.x;
-    uint32_t lens[ASM_PER], slots[ASM_PER];
-    uint64_t my = 0;
+__global__ __launch_bounds__(1024) void k_scan(const s2c_dev d) {   // one workgroup
+    __shared__ uint64_t sh[1024 / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint64_t NB = (uint64_t)d.n_thr * (uint64_t)d.n_blocks;
+    const uint64_t per = (NB + 1023) / 1024, b0 = min(NB, tid * per), b1 = min(NB, b0 + per);
+    uint64_t s = 0;
+    for (uint64_t g = b0; g < b1; g += 16) {   // 16 independent loads in flight per thread
+        uint64_t v[16];
 #pragma unroll
-    for (int j = 0; j < ASM_PER; j++) {
-        const uint32_t p = p0 + j;
-        lens[j] = 0;
-        slots[j] = 0xFFFFFFFFu;
-        if (p < g1) {
-            const uint8_t c = codes[p];
-            if (c == S2C_CODE_FILL) {
-                lens[j] = (uint32_t)d.fill_len;
-            } else {
-                lens[j] = 1;
-                const uint32_t bits = d.ins_bits[p >> 5];
-                if (bits >> (p & 31) & 1u) {
-                    slots[j] = key_index(d, p, bits);
-                    lens[j] += d.ins_cnt[(size_t)t * d.n_keys + slots[j]];
-                }
-            }
-        }
-        my += lens[j];
+        for (int u = 0; u < 16; u++) v[u] = g + u < b1 ? d.blk_len[g + u] : 0ull;
+#pragma unroll
+        for (int u = 0; u < 16; u++) s += v[u];
     }
-    uint64_t x = my;
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t x = s;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint64_t y = __shfl_up(x, o, 64);
         if (lane >= (uint32_t)o) x += y;
     }
-    if (lane == 63) sh[w] = x;
-    __syncthreads();
-    uint64_t wofs = 0;
-    for (uint32_t i = 0; i < w; i++) wofs += sh[i];
-    uint64_t off = base + wofs + x - my;
+    if (lane == 63) sh[wv] = x;
+    lds_sync();
+    uint64_t run = x - s;
+    for (uint32_t i = 0; i < wv; i++) run += sh[i];
+    for (uint64_t g = b0; g < b1; g += 16) {
+        uint64_t v[16];
 #pragma unroll
-    for (int j = 0; j < ASM_PER; j++) {
-        const uint32_t p = p0 + j;
-        if (p >= g1) break;
-        const uint8_t c = codes[p];
-        if (c == S2C_CODE_FILL) {
-            for (int f = 0; f < d.fill_len; f++) d.out[off + f] = d.fill[f];
-            off += (uint32_t)d.fill_len;
-        } else {
-            d.out[off++] = c;
-            const uint32_t ne = lens[j] - 1;
-            if (ne) {
-                const uint8_t *src = d.ins_chr + (size_t)t * d.n_cols + d.ins_kcol[slots[j]];
-                for (uint32_t i = 0; i < ne; i++) d.out[off++] = src[i];
+        for (int u = 0; u < 16; u++) v[u] = g + u < b1 ? d.blk_len[g + u] : 0ull;
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+            if (g + u < b1) {
+                d.blk_off[g + u] = run;
+                run += v[u];
+            }
+    }
+    if (tid == 1023) d.blk_off[NB] = run;
+}
+
+extern "C" __device__ unsigned long long __ockl_wfscan_add_u64(unsigned long long, bool);   // (x, inclusive)
+
+// Two rounds of loads: the tile record and the prefix, then everything the tile's bytes
+// need at once — its codes, key bitmap/rank, the insertion summaries of its keys and the
+// vote chars of its columns (staged in LDS) — then one byte scatter.
+constexpr uint32_t ASM_KEYS = WG, ASM_COLS = 2048;
+template <int ASM_PER, bool DIRECT>   // consecutive positions per thread (tile_max / 256)
+__global__ __launch_bounds__(WG) void k_assemble(const s2c_dev d) {
+    __shared__ uint64_t sh[WG / 64];
+    __shared__ uint64_t sbase[WG / 64];
+    __shared__ uint4 kc[ASM_KEYS];           // ins_cnt of the tile's keys (this threshold)
+    __shared__ uint8_t kchr[ASM_COLS];       // ins_chr of the tile's columns (this threshold)
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t bi = blockIdx.x;
+    const int t = (int)blockIdx.y;
+    const uint64_t nb = (uint64_t)d.n_blocks, NB = (uint64_t)d.n_thr * nb;
+    const uint64_t j = (uint64_t)t * nb + bi;
+    // ---- round 1: the tile record, the prefix
+    uint64_t pre = 0;   // this thread's share of the prefix
+    if constexpr (DIRECT) {
+        uint64_t v[ASM_DIRECT / WG];
+#pragma unroll
+        for (uint32_t u = 0; u < ASM_DIRECT / WG; u++) {
+            const uint64_t i = tid + (uint64_t)u * WG;
+            v[u] = i < j ? d.blk_len[i] : 0ull;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < ASM_DIRECT / WG; u++) pre += v[u];
+    } else {
+        if (tid == 0) pre = d.blk_off[j];
+    }
+    const uint32_t *blk = d.blocks + (size_t)bi * S2C_BLOCK_WORDS;
+    const uint32_t g0 = uni(blk[0]), g1 = uni(blk[1]);
+    const TileIns ti = tile_ins(blk);
+    // ---- round 2: codes, key bitmap/rank, the tile's key summaries and column chars
+    const uint8_t *codes = d.codes + (size_t)t * d.padded_len;
+    const uint4 *cnt_in = (const uint4 *)d.ins_cnt + (size_t)t * d.n_keys;
+    const uint8_t *chr_in = d.ins_chr + (size_t)t * d.n_cols;
+    const uint32_t nkeys = ti.khi - ti.klo, ncol = ti.cb1 - ti.cb0;
+    const bool stage = nkeys <= ASM_KEYS && ncol <= ASM_COLS;   // uniform
+    if (stage) {
+        if (tid < nkeys) kc[tid] = cnt_in[ti.klo + tid];
+        for (uint32_t i = tid; i < ncol; i += WG) kchr[i] = chr_in[ti.cb0 + i];
+    }
+    const uint32_t p0 = g0 + ASM_PER * tid;
+    uint8_t cc[ASM_PER];
+    uint32_t bits[ASM_PER], rank[ASM_PER];
+#pragma unroll
+    for (int jj = 0; jj < ASM_PER; jj++) {
+        const uint32_t p = p0 + jj;
+        const bool in = p < g1;
+        cc[jj] = in ? codes[p] : (uint8_t)0;
+        bits[jj] = in ? d.ins_bits[p >> 5] : 0u;
+        rank[jj] = in ? d.ins_rank[p >> 5] : 0u;
+    }
+    lds_sync();   // staged summaries / chars
+    // the rest, with the summaries / chars read from LDS (staged) or HBM (tiles beyond the
+    // staging capacity): two instantiations, so no load becomes a flat (generic) load
+    auto body = [&](auto get_cnt, auto get_chr) {
+        uint32_t lens[ASM_PER], col0[ASM_PER], ncl[ASM_PER];
+        uint64_t my = 0;
+#pragma unroll
+        for (int jj = 0; jj < ASM_PER; jj++) {
+            const uint32_t p = p0 + jj;
+            lens[jj] = 0;
+            col0[jj] = 0;
+            ncl[jj] = 0;
+            if (p < g1) {
+                if (cc[jj] == S2C_CODE_FILL) {
+                    lens[jj] = (uint32_t)d.fill_len;
+                } else {
+                    lens[jj] = 1;
+                    if (bits[jj] >> (p & 31) & 1u) {
+                        const uint32_t k = rank[jj] + (uint32_t)__popc(bits[jj] & ((1u << (p & 31)) - 1u));
+                        const uint4 ic = get_cnt(k);   // {chars, first column, columns}
+                        lens[jj] += ic.x;
+                        col0[jj] = ic.y;
+                        ncl[jj] = ic.z;
+                    }
+                }
+            }
+            my += lens[jj];
+        }
+        pre = wave_sum(pre);
+        const uint64_t x = __ockl_wfscan_add_u64(my, true);   // inclusive (DPP)
+        if (lane == 63) sh[w] = x;
+        if (lane == 0) sbase[w] = pre;
+        lds_sync();
+        uint64_t wofs = 0, base = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < WG / 64; i++) {
+            wofs += i < w ? sh[i] : 0;
+            base += sbase[i];
+        }
+        if (DIRECT && tid == 0) {   // offsets for the host
+            d.blk_off[j] = base;
+            if (j == NB - 1) d.blk_off[NB] = base + sh[0] + sh[1] + sh[2] + sh[3];
+        }
+        uint64_t off = base + wofs + x - my;
+#pragma unroll
+        for (int jj = 0; jj < ASM_PER; jj++) {
+            const uint32_t p = p0 + jj;
+            if (p >= g1) break;
+            if (cc[jj] == S2C_CODE_FILL) {
+                for (int f = 0; f < d.fill_len; f++) d.out[off + f] = d.fill[f];
+                off += (uint32_t)d.fill_len;
+            } else {
+                d.out[off++] = cc[jj];
+                if (lens[jj] > 1) {   // the key's column votes that are neither '-' nor an error
+                    for (uint32_t i = 0; i < ncl[jj]; i++) {
+                        const uint8_t ic = get_chr(col0[jj] + i);
+                        if (ic != '-' && ic != 0xFF) d.out[off++] = ic;
+                    }
+                }
             }
         }
-    }
+    };
+    if (stage)
+        body([&](uint32_t k) { return kc[k - ti.klo]; }, [&](uint32_t c) { return kchr[c - ti.cb0]; });
+    else
+        body([&](uint32_t k) { return cnt_in[k]; }, [&](uint32_t c) { return chr_in[c]; });
 }
 
 inline int hip_check(hipError_t e, const char *what) {
@@ -668,34 +944,33 @@ inline int hip_check(hipError_t e, const char *what) {
     return s2c_set_error(S2C_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-inline unsigned grid_for(int64_t n, int wg = WG) { return (unsigned)((n + wg - 1) / wg); }
-
 }  // namespace
 
 // ======================================================================= C-ABI
 extern "C" int s2c_workspace_sizes(const s2c_batch_info *info, int32_t n_thr, s2c_ws_sizes *o) {
     if (!info || !o || n_thr <= 0) return s2c_set_error(S2C_ERR_ARG, "bad workspace query");
-    const int64_t L = info->padded_len, T = n_thr;
+    const int64_t L = info->padded_len, T = n_thr, NB = T * info->n_blocks;
     const int64_t nk = std::max<int64_t>(info->n_keys, 1), nc = std::max<int64_t>(info->n_cols, 1);
     o->counts = info->n_deep ? NSYM * L * 4 : 64;   // only deep tiles keep counts in HBM
-    o->key_cov = nk * 4;
     o->ins_cols = nc * NSYM * 4;
-    o->ins_cnt = T * nk * 4;
+    o->ins_cnt = T * nk * 16;
     o->ins_chr = T * nc;
-    o->scalars = 64;
     o->codes = T * L;
-    o->blk_len = (T * info->n_blocks + 1) * 8;
-    o->stats = info->n_refs * T * 32;
+    o->blk_len = std::max<int64_t>(NB, 1) * 8;
+    o->blk_off = (NB + 1) * 8;
+    o->tile_stats = std::max<int64_t>(NB, 1) * 32;
     return S2C_OK;
 }
 
 static int check_dev(const s2c_dev *d) {
     if (!d) return s2c_set_error(S2C_ERR_ARG, "s2c_dev is NULL");
     if (d->n_thr <= 0) return s2c_set_error(S2C_ERR_ARG, "no thresholds");
-    if (d->n_thr > 1024) return s2c_set_error(S2C_ERR_LIMIT, "more than 1024 thresholds");
+    if (d->n_thr > THR_MAX) return s2c_set_error(S2C_ERR_LIMIT, "more than 256 thresholds (-c values)");
     if (d->tile_max <= 0 || d->tile_max > TILE_MAX) return s2c_set_error(S2C_ERR_ARG, "tile_max out of range");
     if (d->padded_len <= 0 || d->padded_len >= ((int64_t)1 << 32)) return s2c_set_error(S2C_ERR_ARG, "bad padded_len");
-    if (d->n_items > 0 && (!d->items || !d->wrec || (d->n_recs > 0 && !d->recs) || d->chunk_recs <= 0))
+    if (d->n_blocks >= ((int64_t)1 << 31) || (int64_t)d->n_thr * d->n_blocks >= ((int64_t)1 << 40))
+        return s2c_set_error(S2C_ERR_LIMIT, "too many (threshold, tile) blocks");
+    if (d->n_items > 0 && (!d->items || !d->wrec || !d->recs || d->chunk_recs <= 0))
         return s2c_set_error(S2C_ERR_ARG, "missing pileup buffers");
     {   // one flush per item: the LDS histogram's u16 halves hold ≤ 248·G per position
         int64_t nwp = 8;
@@ -704,37 +979,31 @@ static int check_dev(const s2c_dev *d) {
             return s2c_set_error(S2C_ERR_ARG, "chunk_recs exceeds one flush per work item");
     }
     if (d->n_deep > 0 && (!d->deep || !d->counts)) return s2c_set_error(S2C_ERR_ARG, "missing deep-tile buffers");
-    if ((d->ablate & 4) && !d->counts) return s2c_set_error(S2C_ERR_ARG, "ablate&4 stores all counts: counts buffer required");
+    if ((d->ablate & 0x104) && !d->counts) return s2c_set_error(S2C_ERR_ARG, "ablate&0x104 writes `counts`: counts buffer required");
     if (!d->ins_bits || !d->ins_rank) return s2c_set_error(S2C_ERR_ARG, "missing key bitmap/rank");
-    if (d->n_keys > 0 && (!d->ins_koff || !d->ins_kcol || !d->ins_off || !d->ins_bases || !d->ins_units ||
-                          !d->key_cov || !d->ins_cols || !d->ins_cnt || !d->ins_chr))
+    if (d->n_keys > 0 && (!d->ins_ev || !d->ins_kinfo || !d->ins_bases || !d->ins_cols || !d->ins_cnt || !d->ins_chr))
         return s2c_set_error(S2C_ERR_ARG, "missing insertion buffers");
+    if (d->n_blocks > 0 && (!d->blocks || !d->codes || !d->blk_len || !d->blk_off || !d->tile_stats ||
+                            !d->out))
+        return s2c_set_error(S2C_ERR_ARG, "missing vote/assembly buffers");
     return S2C_OK;
 }
 
-// Persistent grid: as many workgroups as fit at once (occupancy query, cached per kernel),
-// never more than the items; each pulls items from the ticket.
 template <int NWP>
 static int launch_pileup(const s2c_dev *d, hipStream_t s) {
     k_pileup<NWP><<<(unsigned)d->n_items, WG, 0, s>>>(*d);
     return hip_check(hipGetLastError(), "k_pileup");
 }
 
-// zero per-run state, then the insertion table (must precede the pileup's vote epilogue)
-extern "C" int s2c_insertions(const s2c_dev *d, void *stream) {
-    int rc = check_dev(d);
-    if (rc) return rc;
-    hipStream_t s = (hipStream_t)stream;
-    k_prep<<<(unsigned)(PREP_BLOCKS + d->n_deep), WG, 0, s>>>(*d);
-    if (d->n_units) k_ins_count<<<grid_for(d->n_units), WG, 0, s>>>(*d);
-    return hip_check(hipGetLastError(), "k_prep/k_ins_count");
-}
-
 extern "C" int s2c_pileup(const s2c_dev *d, void *stream) {
     int rc = check_dev(d);
     if (rc) return rc;
-    if (d->n_items == 0) return S2C_OK;
     hipStream_t s = (hipStream_t)stream;
+    if (d->n_deep > 0) {
+        k_prep<<<(unsigned)d->n_deep, WG, 0, s>>>(*d);
+        if ((rc = hip_check(hipGetLastError(), "k_prep"))) return rc;
+    }
+    if (d->n_items == 0) return S2C_OK;
     if (d->n_items >= ((int64_t)1 << 31)) return s2c_set_error(S2C_ERR_LIMIT, "more than 2^31 work items");
     if (d->tile_max <= 256) return launch_pileup<8>(d, s);
     if (d->tile_max <= 512) return launch_pileup<16>(d, s);
@@ -745,49 +1014,39 @@ extern "C" int s2c_pileup(const s2c_dev *d, void *stream) {
 extern "C" int s2c_consensus(const s2c_dev *d, void *stream) {
     int rc = check_dev(d);
     if (rc) return rc;
-    hipStream_t s = (hipStream_t)stream;
     if (d->n_deep > 0) {
-        k_consensus<<<(unsigned)d->n_deep, WG, 0, s>>>(*d);
-        if ((rc = hip_check(hipGetLastError(), "k_consensus"))) return rc;
-    }
-    if (d->n_keys > 0 && d->n_blocks > 0) {
-        k_ins_vote<<<(unsigned)d->n_blocks, WG, (size_t)32 * d->n_thr, s>>>(*d);
-        if ((rc = hip_check(hipGetLastError(), "k_ins_vote"))) return rc;
+        k_consensus<<<(unsigned)d->n_deep, WG, 0, (hipStream_t)stream>>>(*d);
+        return hip_check(hipGetLastError(), "k_consensus");
     }
     return S2C_OK;
+}
+
+template <bool DIRECT>
+static void launch_assemble(const s2c_dev *d, hipStream_t s) {
+    const dim3 g((unsigned)d->n_blocks, (unsigned)d->n_thr);
+    if (d->tile_max <= 256) k_assemble<1, DIRECT><<<g, WG, 0, s>>>(*d);
+    else if (d->tile_max <= 512) k_assemble<2, DIRECT><<<g, WG, 0, s>>>(*d);
+    else if (d->tile_max <= 1024) k_assemble<4, DIRECT><<<g, WG, 0, s>>>(*d);
+    else k_assemble<8, DIRECT><<<g, WG, 0, s>>>(*d);
 }
 
 extern "C" int s2c_assemble(const s2c_dev *d, void *stream) {
     int rc = check_dev(d);
     if (rc) return rc;
     hipStream_t s = (hipStream_t)stream;
-    const int64_t n = (int64_t)d->n_thr * d->n_blocks;
-    k_scan<<<1, 1024, 0, s>>>(d->blk_len, n);
-    if (d->n_blocks) {
-        const dim3 g((unsigned)d->n_blocks, (unsigned)d->n_thr);
-        if (d->tile_max <= 256) k_assemble<1><<<g, WG, 0, s>>>(*d);
-        else if (d->tile_max <= 512) k_assemble<2><<<g, WG, 0, s>>>(*d);
-        else if (d->tile_max <= 1024) k_assemble<4><<<g, WG, 0, s>>>(*d);
-        else k_assemble<8><<<g, WG, 0, s>>>(*d);
+    if (d->n_blocks == 0) return S2C_OK;
+    if ((uint64_t)d->n_thr * (uint64_t)d->n_blocks <= ASM_DIRECT) {
+        launch_assemble<true>(d, s);
+    } else {
+        k_scan<<<1, 1024, 0, s>>>(*d);
+        launch_assemble<false>(d, s);
     }
     return hip_check(hipGetLastError(), "k_assemble");
 }
 
 extern "C" int s2c_run(const s2c_dev *d, void *stream) {
     int rc;
-    if ((rc = s2c_insertions(d, stream))) return rc;
     if ((rc = s2c_pileup(d, stream))) return rc;
     if ((rc = s2c_consensus(d, stream))) return rc;
     return s2c_assemble(d, stream);
-}
-
-extern "C" int s2c_device_error(const s2c_dev *d, void *stream, int *err_out) {
-    if (!d || !err_out) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
-    uint32_t v = 0;
-    int rc = hip_check(hipMemcpyAsync(&v, d->scalars + 1, 4, hipMemcpyDeviceToHost, (hipStream_t)stream), "copy flags");
-    if (rc) return rc;
-    rc = hip_check(hipStreamSynchronize((hipStream_t)stream), "sync");
-    if (rc) return rc;
-    *err_out = v ? S2C_ERR_KEY : S2C_OK;
-    return S2C_OK;
 }

@@ -59,15 +59,14 @@ class DeviceBatch:
             self.recs[: 3 * n].copy_(torch.from_numpy(np.ascontiguousarray(hb.recs.reshape(-1)).view(np.int32)))
         self.items, self.blocks = up(hb.items.reshape(-1)), up(hb.blocks.reshape(-1))
         self.deep = up(hb.deep)
-        self.ins_koff, self.ins_kcol, self.ins_off = up(hb.ins_koff), up(hb.ins_kcol), up(hb.ins_off)
-        self.ins_bases, self.ins_units = up(hb.ins_bases), up(hb.ins_units.reshape(-1))
+        self.ins_ev, self.ins_kinfo = up(hb.ins_ev.reshape(-1)), up(hb.ins_kinfo.reshape(-1))
+        self.ins_bases = up(hb.ins_bases)
         self.ins_bits, self.ins_rank = up(hb.ins_bits), up(hb.ins_rank)
 
     def nbytes(self):
         return sum(t.numel() * t.element_size() for t in (
             self.wrec, self.recs, self.items, self.blocks, self.deep,
-            self.ins_koff, self.ins_kcol, self.ins_off, self.ins_bases, self.ins_units, self.ins_bits,
-            self.ins_rank))
+            self.ins_ev, self.ins_kinfo, self.ins_bases, self.ins_bits, self.ins_rank))
 
 
 class Workspace:
@@ -89,45 +88,41 @@ class Workspace:
         # counts live in HBM only for deep tiles (unless a test asks for all of them)
         self.keep_counts = keep_counts
         self.counts = u8(6 * i.padded_len * 4 if keep_counts else sz.counts)
-        self.key_cov = u8(sz.key_cov)
         self.ins_cols = u8(sz.ins_cols)
         self.ins_cnt = u8(sz.ins_cnt)
         self.ins_chr = u8(sz.ins_chr)
-        self.scalars = u8(sz.scalars)
         self.codes = u8(sz.codes)
         self.blk_len = u8(sz.blk_len)
-        self.stats = u8(sz.stats)
+        self.blk_off = u8(sz.blk_off)
+        self.tile_stats = u8(sz.tile_stats)
         # output upper bound: every position fill or char + every insertion base, per threshold
         cap = self.T * (i.total_len * max(1, len(fill)) + i.n_cols) + 16
         self.out = u8(cap)
         d = L.Dev()
         d.wrec, d.recs = _ptr(db.wrec), _ptr(db.recs)
         d.items, d.blocks, d.deep = _ptr(db.items), _ptr(db.blocks), _ptr(db.deep)
-        d.ins_koff, d.ins_kcol, d.ins_off = _ptr(db.ins_koff), _ptr(db.ins_kcol), _ptr(db.ins_off)
-        d.ins_bases, d.ins_units = _ptr(db.ins_bases), _ptr(db.ins_units)
+        d.ins_ev, d.ins_kinfo, d.ins_bases = _ptr(db.ins_ev), _ptr(db.ins_kinfo), _ptr(db.ins_bases)
         d.ins_bits, d.ins_rank = _ptr(db.ins_bits), _ptr(db.ins_rank)
         d.n_recs, d.chunk_recs = i.n_recs, i.chunk_recs
         d.n_items, d.n_blocks, d.n_deep = i.n_items, i.n_blocks, i.n_deep
-        d.n_keys, d.n_cols, d.n_units, d.padded_len = i.n_keys, i.n_cols, i.n_units, i.padded_len
+        d.n_keys, d.n_cols, d.padded_len = i.n_keys, i.n_cols, i.padded_len
         d.tile_max, d.n_refs = i.tile_max, i.n_refs
         d.thresholds, d.n_thr = _ptr(self.thr), self.T
         d.min_depth = int(max(min(min_depth, 2**31 - 1), -2**31))
         d.fill_len, d.fill_nondash = len(fill), sum(1 for c in fill if c != ord("-"))
         d.fill = _ptr(self.fill)
-        d.counts, d.key_cov = _ptr(self.counts), _ptr(self.key_cov)
+        d.counts = _ptr(self.counts)
         d.ins_cols, d.ins_cnt, d.ins_chr = _ptr(self.ins_cols), _ptr(self.ins_cnt), _ptr(self.ins_chr)
-        d.scalars = _ptr(self.scalars)
-        d.codes, d.blk_len = _ptr(self.codes), _ptr(self.blk_len)
-        d.stats, d.out, d.out_cap = _ptr(self.stats), _ptr(self.out), cap
+        d.codes = _ptr(self.codes)
+        d.blk_len = _ptr(self.blk_len)
+        d.tile_stats, d.blk_off = _ptr(self.tile_stats), _ptr(self.blk_off)
+        d.out, d.out_cap = _ptr(self.out), cap
         self.dev = d
 
     def stream_handle(self):
         return C.c_void_p(torch.cuda.current_stream(self.db.device).cuda_stream)
 
-    # ---- the four stages in run order (each one C-ABI call; asynchronous on the current stream)
-    def insertions(self):
-        L.check(lib.s2c_insertions(C.byref(self.dev), self.stream_handle()))
-
+    # ---- the three stages in run order (each one C-ABI call; asynchronous on the current stream)
     def pileup(self):
         if (self.dev.ablate & 4) and not self.keep_counts:
             raise ValueError("diagnostic ablate&4 stores every count: build the Workspace with keep_counts=True")
@@ -140,16 +135,34 @@ class Workspace:
         L.check(lib.s2c_assemble(C.byref(self.dev), self.stream_handle()))
 
     def run(self):
-        """insertions → pileup(+vote) → deep-tile consensus → assembly (no host sync)."""
+        """pileup(+insertions, vote) → deep-tile consensus → assembly (no host sync)."""
         L.check(lib.s2c_run(C.byref(self.dev), self.stream_handle()))
+
+    # ---- HIP graph of one run (the stage launches replayed without host launch overhead)
+    def capture(self):
+        """Capture one ``run()`` into a HIP graph (torch.cuda.CUDAGraph is hipGraph on ROCm);
+        the kernel arguments (this workspace's buffers) are baked in."""
+        dev = self.db.device
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            self.run()                      # warm-up launch outside the capture
+        torch.cuda.current_stream(dev).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.run()
+        self.graph = g
+        return g
+
+    def replay(self):
+        self.graph.replay()
 
     # ---- results
     def pileup_counts(self):
-        """Diagnostic: run prep + pileup with every tile storing its counts (needs
+        """Diagnostic: run the pileup with every tile storing its counts (needs
         keep_counts=True); returns counts[6][padded_len] as numpy u32."""
         if not self.keep_counts:
             raise ValueError("pileup_counts needs Workspace(keep_counts=True)")
-        self.insertions()
         self.dev.ablate = 4
         try:
             self.pileup()
@@ -163,12 +176,22 @@ class Workspace:
         return self.counts[: 6 * Lp * 4].view(torch.int32).cpu().numpy().view(np.uint32).reshape(6, Lp)
 
     def fetch(self):
-        """Synchronise and copy results: (stats[R,T,4] u64, blk_off[T*nb+1] u64, out bytes)."""
+        """Synchronise and copy results: (stats[R,T,4] u64, blk_off[T*nb+1] u64, out bytes).
+
+        stats[r, t] = Σ over reference r's tiles of the device's per-tile statistics
+        (tiles never straddle a reference; :352-397 sums)."""
         torch.cuda.synchronize(self.db.device)
         i = self.db.info
         R, T, nb = i.n_refs, self.T, i.n_blocks
-        stats = self.stats[: R * T * 32].view(torch.int64).cpu().numpy().view(np.uint64).reshape(R, T, 4)
-        offs = self.blk_len[: (T * nb + 1) * 8].view(torch.int64).cpu().numpy().view(np.uint64)
+        stats = np.zeros((R, T, 4), dtype=np.uint64)
+        if nb:
+            ts = self.tile_stats[: T * nb * 32].view(torch.int64).cpu().numpy().view(np.uint64).reshape(T, nb, 4)
+            ref = self.db.hb.blocks[:, 2].astype(np.int64)
+            for t in range(T):
+                np.add.at(stats[:, t, :], ref, ts[t])
+        if T * nb == 0:
+            return stats, np.zeros(1, dtype=np.uint64), b""
+        offs = self.blk_off[: (T * nb + 1) * 8].view(torch.int64).cpu().numpy().view(np.uint64)
         total = int(offs[-1])
         out = self.out[:total].cpu().numpy().tobytes()
         return stats, offs, out

@@ -59,9 +59,20 @@ class SubBatch:
         self.ins_off = (off[e0:e1 + 1] - off[e0]).astype(np.uint32)
         nib_all = _unpack_nibbles(hb.ins_bases, int(off[-1]))
         self.ins_bases = _pack_nibbles(nib_all[int(off[e0]):int(off[e1])])
-        u = hb.ins_units.astype(np.int64)
-        u = u[(u[:, 0] >= k0) & (u[:, 0] < k1)] - np.array([k0, e0])
-        self.ins_units = u.astype(np.uint32).reshape(-1, 2)
+        self.ins_ekey = (hb.ins_ekey[e0:e1].astype(np.int64) - k0).astype(np.uint32)
+        # device records: event column offsets are tile-relative (unchanged), nibble offsets
+        # and key columns rebase; the tiles' key/event/column ranges (block words 4-9) too
+        ev = hb.ins_ev[e0:e1].astype(np.int64)
+        ev[:, 2] -= int(off[e0])
+        self.ins_ev = ev.astype(np.uint32).reshape(-1, 4)
+        ki = hb.ins_kinfo[k0:k1].astype(np.int64)
+        ki[:, 1] -= int(kcol[k0])
+        self.ins_kinfo = ki.astype(np.uint32).reshape(-1, 4)
+        bl = self.blocks.astype(np.int64)
+        bl[:, 4:6] -= k0
+        bl[:, 6:8] -= e0
+        bl[:, 8:10] -= int(kcol[k0])
+        self.blocks = bl.astype(np.uint32)
         bits = np.zeros_like(hb.ins_bits)
         wa, wb = A >> 5, (B + 31) >> 5
         bits[wa:wb] = hb.ins_bits[wa:wb]
@@ -78,7 +89,6 @@ class SubBatch:
         info.n_ins_words = len(self.ins_bases)
         info.n_keys = k1 - k0
         info.n_cols = int(self.ins_kcol[-1])
-        info.n_units = len(self.ins_units)
         info.tile_max = int((self.blocks[:, 1] - self.blocks[:, 0]).max()) if len(self.blocks) else 64
         self.info = info   # chunk_recs is the parent's: the items' chunk indices refer to it
         self.names = hb.names

@@ -11,7 +11,7 @@ STEPS=${STEPS:-gpu,bench,prof}
 WL=${WL:-c2}
 echo "host: $(nproc) cpus; $(grep -m1 'model name' /proc/cpuinfo)" | tee "$OUT/host.txt"
 if [[ $STEPS == *gpu* ]]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q --maxfail=20 ${PYTEST_ARGS} > "$OUT/pytest_gpu.log" 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread ${PYTEST_ARGS} > "$OUT/pytest_gpu.log" 2>&1
   rc=$?; tail -30 "$OUT/pytest_gpu.log"; [ $rc -eq 0 ] || { echo "pytest gpu rc=$rc"; exit $rc; }
 fi
 if [[ $STEPS == *bench* ]]; then

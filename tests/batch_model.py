@@ -60,7 +60,7 @@ def check_plan(hb):
     for a, b, c, t in hb.items.astype(np.int64):
         chunks.setdefault(int(t), []).append(int(c))
         assert (int(hb.blocks[t, 0]), int(hb.blocks[t, 1])) == (a, b)
-    for t, (a, b, ref, deep) in enumerate(hb.blocks.astype(np.int64)):
+    for t, (a, b, ref, deep) in enumerate(hb.blocks[:, :4].astype(np.int64)):
         cs = sorted(chunks[t])
         assert cs == list(range(len(cs))), "tile %d chunks %r" % (t, cs)
         assert bool(deep) == (len(cs) > 1)
@@ -88,12 +88,35 @@ def check_ins_layout(hb):
                                                  for k in key] == np.arange(nk)).all()
     koff = hb.ins_koff.astype(np.int64)
     assert koff[0] == 0 and koff[-1] == hb.info.n_ins and (np.diff(koff) > 0).all()
-    cover = np.zeros(hb.info.n_ins, np.int64)
-    for k, e in hb.ins_units.astype(np.int64):
-        e1 = min(koff[k + 1], e + 256)
-        assert koff[k] <= e < koff[k + 1]
-        cover[e:e1] += 1
-    assert (cover == 1).all()
+    ekey = hb.ins_ekey.astype(np.int64)
+    assert (ekey == np.repeat(np.arange(nk), np.diff(koff))).all()
+    check_device_records(hb)
+
+
+def check_device_records(hb):
+    """The device's 16-B event/key records and the tiles' insertion ranges (block words
+    4-9) restate the grouped arrays exactly."""
+    koff, kcol = hb.ins_koff.astype(np.int64), hb.ins_kcol.astype(np.int64)
+    off = hb.ins_off.astype(np.int64)
+    ki = hb.ins_kinfo.astype(np.int64)
+    assert (ki[:, 0] == hb.ins_key).all() and (ki[:, 1] == kcol[:-1]).all() and (ki[:, 2] == np.diff(kcol)).all()
+    ev = hb.ins_ev.astype(np.int64)
+    rank = hb.ins_rank.astype(np.int64)
+    seen = np.zeros(len(ev), np.int64)
+    for a, b, _, _, klo, khi, e0, e1, cb0, cb1 in hb.blocks[:, :10].astype(np.int64):
+        assert (klo, khi) == (rank[a >> 5], rank[(b + 31) >> 5])
+        assert (e0, e1, cb0, cb1) == (koff[klo], koff[khi], kcol[klo], kcol[khi])
+        for k in range(klo, khi):
+            for e in range(koff[k], koff[k + 1]):
+                seen[e] += 1
+                n = off[e + 1] - off[e]
+                assert (ev[e, 0], ev[e, 1], ev[e, 2]) == (kcol[k] - cb0, n, off[e])
+                w0 = 0
+                for c in range(min(n, 8)):
+                    q = off[e] + c
+                    w0 |= ((int(hb.ins_bases[q >> 3]) >> (4 * (q & 7))) & 15) << (4 * c)
+                assert ev[e, 3] == w0
+    assert (seen == 1).all()
 
 
 def _vote(c, cov, t):
@@ -133,7 +156,7 @@ def model_pipeline(hb, thresholds, min_depth=1, fill=b"-"):
     pieces = [[None] * nb for _ in range(T)]
     fl = len(fill)
     fnd = sum(1 for ch in fill if ch != ord("-"))
-    for bi, (g0, g1, ref, _) in enumerate(hb.blocks):
+    for bi, (g0, g1, ref, _) in enumerate(hb.blocks[:, :4]):
         g0, g1, ref = int(g0), int(g1), int(ref)
         for ti, t in enumerate(thresholds):
             buf = bytearray()

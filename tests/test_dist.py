@@ -23,6 +23,7 @@ def _virtual(hb, opt, world):
     parts, stats = [], None
     for rank, (t0, t1) in enumerate(shard.split_tiles(hb, world)):
         sub = shard.SubBatch(hb, t0, t1)
+        bm.check_device_records(sub)
         st, offs, out = bm.model_pipeline(sub, opt.thresholds, opt.min_depth, opt.fill.encode("latin-1"))
         stats = st if stats is None else stats + st
         parts.append((t0, t1, offs, out))

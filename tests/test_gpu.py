@@ -149,3 +149,32 @@ def test_sharded_on_device(world):
         parts.append((t0, t1, offs, out))
     offs, out = shard.merge_outputs(parts, len(thr))
     assert files(stats, offs, out) == want
+
+
+@pytest.mark.parametrize("name,over,thr", [
+    ("c2", {"n_refs": 6}, [0.25, 0.5, 0.75]),
+    # long insertions: > 1024 insertion columns in a tile → the HBM column path
+    ("c2", {"n_refs": 2, "depth": 60.0, "ins_frac": 0.6, "ins_max": 60}, [0.1, 0.5]),
+    # deep tiles (several work items) with insertions: k_prep + k_consensus epilogue
+    ("c2", {"n_refs": 1, "ref_len": 700, "depth": 9000.0, "ins_frac": 0.05, "ins_max": 6}, [0.25, 0.75]),
+])
+def test_device_pipeline_equals_batch_model(name, over, thr):
+    """stats / block offsets / bytes of the HIP stages == the batch model (tests/batch_model.py)."""
+    from sam2consensus_amd import configs
+    hb = configs.synth_batch(name, **over)
+    ncol_tile = []
+    for a, b, _, _ in hb.blocks[:, :4].astype(np.int64):
+        klo, khi = int(hb.ins_rank[a >> 5]), int(hb.ins_rank[(b + 31) >> 5])
+        ncol_tile.append(int(hb.ins_kcol[khi]) - int(hb.ins_kcol[klo]))
+    if over.get("ins_max") == 60:
+        assert max(ncol_tile) > 1024, "case must exercise the HBM insertion-column path"
+    if over.get("depth") == 9000.0:
+        assert hb.info.n_deep > 0 and hb.info.n_keys > 0
+    ws = _ws(hb, thr)
+    for _ in range(2):   # second run: the look-back scan state of the first must not leak
+        ws.run()
+        st, offs, out = ws.fetch()
+        want = bm.model_pipeline(hb, thr)
+        assert (st == want[0]).all()
+        assert (offs == want[1]).all()
+        assert out == want[2]
