@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define S2C_ABI_VERSION 2
+#define S2C_ABI_VERSION 3
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define S2C_OK            0
@@ -52,8 +52,8 @@ int s2c_layout(int64_t *out, int n);
 #define S2C_POS_ALIGN    64    /* each reference starts at a multiple of this global coordinate */
 #define S2C_ITEM_WORDS    4    /* u32 words per pileup work item {a, b, chunk, tile} */
 #define S2C_BLOCK_WORDS  12    /* u32 words per tile {a, b, ref, deep, klo, khi, e0, e1, cb0, cb1, 0, 0} */
-#define S2C_CODE_FILL     0    /* codes[] value for a fill position */
-#define S2C_CODE_ERR   0xFF    /* codes[] value where the vote hit a missing amb key (:367) */
+#define S2C_CODE_FILL     0    /* internal vote char of a fill position */
+#define S2C_CODE_ERR   0xFF    /* vote char where the vote hit a missing amb key (:367) */
 #define S2C_TILE_MAX   2048    /* positions per tile */
 
 /* ======================================================================================
@@ -177,7 +177,7 @@ typedef struct {
     const uint32_t *wrec, *recs;   /* word-major seqout records (s2c_batch_arrays); recs holds
                                       n_recs + 1 records, the last all zero (sentinel) */
     const uint32_t *items, *blocks, *deep;
-    const uint32_t *ins_ev, *ins_kinfo, *ins_bases, *ins_bits, *ins_rank;   /* (s2c_batch_arrays) */
+    const uint32_t *ins_ev, *ins_kinfo, *ins_bases, *ins_bits;   /* (s2c_batch_arrays) */
     int64_t n_recs, chunk_recs, n_items, n_blocks, n_deep, n_keys, n_cols, padded_len;
     int32_t tile_max, n_refs;
 
@@ -191,45 +191,49 @@ typedef struct {
 
     /* ---- workspace (caller allocates; sizes from s2c_workspace_sizes) ---- */
     uint32_t *counts;          /* [6][padded_len] pileup counts of deep tiles (SoA by symbol) */
-    uint32_t *ins_cols;        /* [n_cols][6] column counts of tiles with > 1024 columns (else in LDS) */
-    uint32_t *ins_cnt;         /* [T][n_keys][4] {insertion chars emitted, first column, columns, 0} */
-    uint8_t  *ins_chr;         /* [T][n_cols] vote char of every insertion column of a called key
-                                  ('-' and 0xFF included; the emitted chars are the others) */
-    uint8_t  *codes;           /* [T][padded_len] per-position consensus char (0 = fill) */
-    uint64_t *blk_len;         /* [T*n_blocks] output bytes of block (t, tile) */
+    uint32_t *ins_cols;        /* [n_cols][6] column counts of tiles whose columns exceed LDS */
+    uint32_t *ins_cnt;         /* [T][n_keys][4] {chars emitted, first column, columns, 0}: tiles
+                                  with > 256 keys or HBM columns only */
+    uint8_t  *ins_chr;         /* [T][n_cols] column vote chars, same tiles only */
 
     /* ---- outputs ---- */
     uint64_t *tile_stats;      /* [T][n_blocks][4] {sumcov, len, nondash, vote_errors} per tile
                                   (:352-397; summed per reference by the host) */
-    uint64_t *blk_off;         /* [T*n_blocks + 1] byte offset of block (t, tile) in out; last = total */
-    uint8_t  *out;             /* assembled consensus bytes, [t][block] order */
-    int64_t   out_cap;
+    uint64_t *blk_len;         /* [T][n_blocks] FASTA body bytes of (t, tile) */
+    uint8_t  *out;             /* FASTA bodies (:350-389): tile (t, tile) at
+                                  t·(F·padded_len + n_cols) + F·a + cb0, F = max(1, len(fill)),
+                                  a = the tile's first position, cb0 its first insertion column;
+                                  blk_len bytes each.  A reference's body for threshold t is its
+                                  tiles' pieces in order. */
+    int64_t   out_cap;         /* ≥ T·(F·padded_len + n_cols) */
 
     /* ---- diagnostics, 0 in the product: bit 1 skips counting, bit 2 loads without
-     *      counting, bit 8 skips the histogram flush (timing ablations, results wrong:
-     *      scripts/ablate.py); bit 4 makes every tile store its counts to `counts`
-     *      (sized 6*padded_len*4) instead of voting (counts parity tests) ---- */
+     *      counting, bit 8 skips the
+     *      histogram flush, 0x200 skips the insertion columns, 0x800 returns at once
+     *      (timing ablations, results wrong: scripts/ablate.py); bit 4 makes every tile store
+     *      its counts to `counts` (sized 6*padded_len*4) instead of voting (counts parity
+     *      tests); 0x100 writes phase timestamps to `counts` (scripts/phases.py) ---- */
     int32_t   ablate;
     int32_t   reserved;
 } s2c_dev;
 
 /* Sizes (bytes) of every workspace / output buffer for a batch and T thresholds. */
 typedef struct {
-    int64_t counts, ins_cols, ins_cnt, ins_chr, codes, blk_len, blk_off, tile_stats;
+    int64_t counts, ins_cols, ins_cnt, ins_chr, blk_len, tile_stats;
+    int64_t out_per_fill, out_fixed;   /* out bytes = out_per_fill·max(1, len(fill)) + out_fixed */
 } s2c_ws_sizes;
 int s2c_workspace_sizes(const s2c_batch_info *info, int32_t n_thr, s2c_ws_sizes *out);
 
-/* Stage order (s2c_run): s2c_pileup → s2c_consensus → s2c_assemble.
+/* Stage order (s2c_run): s2c_pileup → s2c_consensus.
  * (2) pileup per tile; for tiles holding their whole depth in one work item also (3) the
- * insertion columns and (4) the vote (all thresholds, IUPAC, min-depth/fill, insertion
- * chars, tile statistics)                       (:206-221, :232-253, :256-311, :344-397) */
+ * insertion columns, (4) the vote (all thresholds, IUPAC, min-depth/fill, insertion
+ * chars, tile statistics) and the tile's FASTA body bytes
+ *                                          (:206-221, :232-253, :256-311, :344-397) */
 int s2c_pileup(const s2c_dev *d, void *stream);
-/* (3)+(4) for deep tiles (records split over several work items, counts summed in HBM)
- *                                                         (:232-253, :256-311, :344-397) */
+/* (3)+(4) and the bodies for deep tiles (records split over several work items, counts
+ * summed in HBM)                                   (:232-253, :256-311, :344-397) */
 int s2c_consensus(const s2c_dev *d, void *stream);
-/* device FASTA body assembly: block offsets (scan) + byte scatter       (:350-389 string build) */
-int s2c_assemble(const s2c_dev *d, void *stream);
-/* all three, in order, on one stream (graph-capturable: no allocation, no sync) */
+/* both, in order, on one stream (graph-capturable: no allocation, no sync) */
 int s2c_run(const s2c_dev *d, void *stream);
 
 #ifdef __cplusplus

@@ -80,7 +80,7 @@ class Dev(C.Structure):
     _fields_ = [
         ("wrec", _VP), ("recs", _VP),
         ("items", _VP), ("blocks", _VP), ("deep", _VP),
-        ("ins_ev", _VP), ("ins_kinfo", _VP), ("ins_bases", _VP), ("ins_bits", _VP), ("ins_rank", _VP),
+        ("ins_ev", _VP), ("ins_kinfo", _VP), ("ins_bases", _VP), ("ins_bits", _VP),
         ("n_recs", C.c_int64), ("chunk_recs", C.c_int64),
         ("n_items", C.c_int64), ("n_blocks", C.c_int64), ("n_deep", C.c_int64),
         ("n_keys", C.c_int64), ("n_cols", C.c_int64), ("padded_len", C.c_int64),
@@ -88,14 +88,13 @@ class Dev(C.Structure):
         ("thresholds", _VP), ("n_thr", C.c_int32), ("min_depth", C.c_int32),
         ("fill_len", C.c_int32), ("fill_nondash", C.c_int32), ("fill", _VP),
         ("counts", _VP), ("ins_cols", _VP), ("ins_cnt", _VP), ("ins_chr", _VP),
-        ("codes", _VP), ("blk_len", _VP),
-        ("tile_stats", _VP), ("blk_off", _VP), ("out", _VP), ("out_cap", C.c_int64),
+        ("tile_stats", _VP), ("blk_len", _VP), ("out", _VP), ("out_cap", C.c_int64),
         ("ablate", C.c_int32), ("reserved", C.c_int32)]
 
 
 class WsSizes(C.Structure):
     _fields_ = [(n, C.c_int64) for n in (
-        "counts", "ins_cols", "ins_cnt", "ins_chr", "codes", "blk_len", "blk_off", "tile_stats")]
+        "counts", "ins_cols", "ins_cnt", "ins_chr", "blk_len", "tile_stats", "out_per_fill", "out_fixed")]
 
 
 # every symbol include/s2c.h declares (tests/test_lib.py checks the export table)
@@ -104,7 +103,7 @@ EXPORTS = [
     "s2c_parser_new", "s2c_parser_feed", "s2c_parser_feed_file", "s2c_parser_finish", "s2c_parser_free",
     "s2c_batch_info_get", "s2c_batch_arrays_get", "s2c_batch_ref_name", "s2c_batch_free",
     "s2c_parsecigar", "s2c_synth_feed", "s2c_synth_write",
-    "s2c_workspace_sizes", "s2c_pileup", "s2c_consensus", "s2c_assemble", "s2c_run",
+    "s2c_workspace_sizes", "s2c_pileup", "s2c_consensus", "s2c_run",
 ]
 
 
@@ -139,7 +138,6 @@ def _load():
         "s2c_workspace_sizes": (C.c_int, [C.POINTER(BatchInfo), C.c_int32, C.POINTER(WsSizes)]),
         "s2c_pileup": (C.c_int, [C.POINTER(Dev), _VP]),
         "s2c_consensus": (C.c_int, [C.POINTER(Dev), _VP]),
-        "s2c_assemble": (C.c_int, [C.POINTER(Dev), _VP]),
         "s2c_run": (C.c_int, [C.POINTER(Dev), _VP]),
     }
     for name, (res, args) in sig.items():

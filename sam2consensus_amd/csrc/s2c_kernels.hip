@@ -116,11 +116,6 @@ __device__ __forceinline__ uint32_t vote_mask_u32(const uint32_t (&c)[NSYM], con
     return m;
 }
 
-// index of the insertion key at position p (p must carry a key): keys before p's word + the
-// key bits below p in it
-__device__ __forceinline__ uint32_t key_index(const s2c_dev &d, uint32_t p, uint32_t bits) {
-    return d.ins_rank[p >> 5] + (uint32_t)__popc(bits & ((1u << (p & 31)) - 1u));
-}
 
 // Diagnostic phase stamps (ablate bit 0x100, k_pileup only): thread 0 of work item i writes
 // s_memrealtime (100 MHz) for phase k to ((u64*)counts)[16i + k] (scripts/phases.py).
@@ -162,18 +157,21 @@ __global__ __launch_bounds__(WG) void k_prep(const s2c_dev d) {
 // to len / non-'-' / sumcov (cov per emitted char, :385).  The tile's statistics per
 // threshold go to tile_stats and its body lengths to blk_len — plain stores.
 
-constexpr int VT_TMAX = 16;                   // thresholds per pass over the tile's positions
-constexpr int VT_ACC = 2 + 4 * VT_TMAX;       // LDS u64: sumcov, len, {nondash, nerr, ins sumcov, ins len}[VT_TMAX]
+constexpr int VT_TMAX = 4;                    // thresholds per pass: one vote-char word per column
+constexpr int VT_ACC = 1 + 4 * VT_TMAX;       // LDS u64: position sumcov, {nondash, nerr, ins sumcov, ins len}[VT_TMAX]
 constexpr uint32_t PF = WG;                   // event / key records prefetched into LDS per tile
 constexpr int THR_MAX = WG;                   // thresholds (-c values) supported: all staged in LDS
+constexpr int FILL_LDS = 64;                  // -f bytes staged in LDS (longer fills read HBM)
+constexpr int TILE_WORDS = S2C_TILE_MAX / 32;
 
 // s_waitcnt vmcnt(0) as a real S_WAITCNT (the compiler's wait tracking sees it): ends the
 // rare HBM-reading branches of the epilogue so that no load is "maybe pending" after them —
 // a maybe-pending load makes the compiler wait on every later register reuse, and vmcnt is
-// in order, i.e. it waits for all the vote bytes stored meanwhile.
+// in order, i.e. it waits for all the bytes stored meanwhile.
 __device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 extern "C" __device__ __attribute__((const)) unsigned long long __ockl_wfred_add_u64(unsigned long long);
+extern "C" __device__ unsigned int __ockl_wfscan_add_u32(unsigned int, bool);   // (x, inclusive)
 
 // Sum over the wave's active lanes, every lane gets it: the device library's DPP reduction
 // (row shifts / broadcasts in the VALU) — a butterfly of __shfl_xor is a dependent chain
@@ -234,44 +232,72 @@ struct EpiLds {
     uint4 key[PF];                     // key records ins_kinfo[klo .. klo+PF)
     double thr[THR_MAX];               // -c thresholds, CLI order
     unsigned long long acc[VT_ACC];
+    uint64_t wsum[VT_TMAX][WG / 64];   // body-length scan: wave totals
     uint32_t kcov[PF];                 // coverage of each key's position if called, else 0
+    uint32_t bits[TILE_WORDS];         // key bitmap of the tile's words
+    uint32_t wrank[TILE_WORDS];        // keys of the tile before each word
+    uint16_t kem[VT_TMAX][PF];         // insertion chars emitted per key (this pass)
     uint16_t colkey[ICOL];             // key slot of each tile column
     uint32_t vchr[ICOL];               // vote chars of each tile column, 4 thresholds per word
+    uint8_t fill[FILL_LDS];
     uint8_t amb[64];
 };
 // issue the prefetch loads (registers; stored into LDS by prefetch_store)
 struct Prefetch {
     uint4 ev, key;
     double thr;
+    uint32_t bits;
+    uint8_t fill;
 };
-__device__ __forceinline__ void prefetch_load(const s2c_dev &d, const TileIns &ti, Prefetch &pf) {
+__device__ __forceinline__ void prefetch_load(const s2c_dev &d, uint32_t a, uint32_t n, const TileIns &ti, Prefetch &pf) {
     const uint32_t tid = threadIdx.x;
     pf.ev = make_uint4(0, 0, 0, 0);
     pf.key = make_uint4(0, 0, 0, 0);
     pf.thr = 0.0;
+    pf.bits = 0;
+    pf.fill = 0;
     if (ti.e0 + tid < ti.e1) pf.ev = ((const uint4 *)d.ins_ev)[ti.e0 + tid];
     if (ti.klo + tid < ti.khi) pf.key = ((const uint4 *)d.ins_kinfo)[ti.klo + tid];
     if (tid < (uint32_t)d.n_thr) pf.thr = d.thresholds[tid];
+    if (tid < (n + 31) / 32) pf.bits = d.ins_bits[(a >> 5) + tid];
+    if (tid < (uint32_t)min(d.fill_len, FILL_LDS)) pf.fill = d.fill[tid];
 }
 template <class EL>
-__device__ __forceinline__ void prefetch_store(const s2c_dev &d, EL &L, const Prefetch &pf) {
-    L.ev[threadIdx.x] = pf.ev;
-    L.key[threadIdx.x] = pf.key;
-    if (threadIdx.x < (uint32_t)d.n_thr) L.thr[threadIdx.x] = pf.thr;
+__device__ __forceinline__ void prefetch_store(const s2c_dev &d, EL &L, uint32_t n, const Prefetch &pf) {
+    const uint32_t tid = threadIdx.x;
+    L.ev[tid] = pf.ev;
+    L.key[tid] = pf.key;
+    if (tid < (uint32_t)d.n_thr) L.thr[tid] = pf.thr;
+    if (tid < (n + 31) / 32) L.bits[tid] = pf.bits;
+    if (tid < (uint32_t)min(d.fill_len, FILL_LDS)) L.fill[tid] = pf.fill;
+}
+
+// Tile (t, tile)'s body region in `out`: a static slot, so every tile writes its bytes
+// without waiting for any other — max(1, len(fill)) bytes per padded position plus one per
+// insertion column before it; threshold t's region starts at t·stride.
+__device__ __forceinline__ uint64_t body_stride(const s2c_dev &d) {
+    return (uint64_t)max(1, d.fill_len) * (uint64_t)d.padded_len + (uint64_t)d.n_cols;
+}
+__device__ __forceinline__ uint64_t body_slot(const s2c_dev &d, uint32_t a, uint32_t cb0) {
+    return (uint64_t)max(1, d.fill_len) * a + cb0;
 }
 
 // cols: LDS [ICOL][6] (LDSC) or the tile's HBM slice.  fetch(q, c) = count of symbol c at
-// tile position q.  Every thread calls (barriers inside).  Order: insertion columns counted,
-// then per threshold pass the insertion vote and the position vote (whose byte stores come
-// last, so nothing waits on them), then the tile totals.
+// tile position q.  Every thread calls (barriers inside).  Per pass of ≤ 4 thresholds:
+// (3)/(4) the insertion columns' votes, then per chunk of 512 positions the position vote
+// and the tile's FASTA body bytes (a block scan of the per-position lengths gives every
+// byte's offset in the tile's slot), then the tile's statistics.
 template <bool LDSC, class Fetch, class EL>
 __device__ __forceinline__ void tile_epilogue(const s2c_dev &d, uint32_t tile, uint32_t a, uint32_t n,
                                               const TileIns &ti, Fetch fetch, uint32_t *cols, EL &L) {
     const int T = d.n_thr;
-    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t F = (uint32_t)d.fill_len;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t nkeys = ti.khi - ti.klo, ncol = ti.cb1 - ti.cb0;
     const bool no_ins = (d.ablate & 0x200) != 0;   // diagnostic: skip (3)/(4) insertions
-    if (ti.khi > ti.klo && !no_ins) {   // (3) count the tile's insertion columns (uniform branch)
-        const uint32_t ncol = ti.cb1 - ti.cb0;
+    const bool has_ins = ti.khi > ti.klo && !no_ins;
+    const bool colpar = LDSC && nkeys <= PF;       // insertion summaries kept in LDS
+    if (has_ins) {   // (3) count the tile's insertion columns (uniform branch)
         for (uint32_t i = tid; i < ncol * NSYM; i += WG) cols[i] = 0;
         if constexpr (!LDSC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // zeros in L2 before any atomic
         lds_sync();   // also publishes the prefetched records
@@ -297,106 +323,101 @@ __device__ __forceinline__ void tile_epilogue(const s2c_dev &d, uint32_t tile, u
             add_event(r);
         }
         if constexpr (!LDSC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // atomics done before the reads
-        // published by the barrier after the accumulator zeroing below
+    }
+    // keys of the tile before each of its words (position → key slot)
+    const uint32_t nwords = (n + 31) / 32;
+    if (wv == 0) {
+        const uint32_t pc = lane < nwords ? (uint32_t)__popc(L.bits[lane]) : 0u;
+        const uint32_t inc = __ockl_wfscan_add_u32(pc, true);
+        if (lane < nwords) L.wrank[lane] = inc - pc;
+    }
+    if (has_ins && colpar && tid < nkeys) {   // key coverage (0 if not called) + column → key map
+        const uint4 kr = L.key[tid];
+        uint32_t cov = 0;
+#pragma unroll
+        for (uint32_t c = 0; c < NSYM; c++) cov += fetch(kr.x - a, c);
+        L.kcov[tid] = (cov > 0 && (int64_t)cov >= (int64_t)d.min_depth) ? cov : 0u;   // :356-358
+        for (uint32_t c = 0; c < kr.z; c++) L.colkey[kr.y - ti.cb0 + c] = (uint16_t)tid;
     }
     S2C_STAMP(d, 3);
+    uint8_t *const obase = d.out + body_slot(d, a, ti.cb0);
+    const uint64_t ostride = body_stride(d);
+    uint4 *cnt_out = (uint4 *)d.ins_cnt;
     for (int t0 = 0; t0 < T; t0 += VT_TMAX) {
-        const int t1 = min(T, t0 + VT_TMAX);
+        const int tn = min(VT_TMAX, T - t0);
         for (uint32_t i = tid; i < (uint32_t)VT_ACC; i += WG) L.acc[i] = 0;
         lds_sync();
-        // (4) insertion columns of called keys (:290-311, :370-385).  Every column's vote
-        // char goes to ins_chr[t][column] ('-' and vote errors included); k_assemble emits
-        // the key's chars that are neither; ins_cnt[t][k] = {emitted, first column, columns}.
-        uint4 *cnt_out = (uint4 *)d.ins_cnt;
-        const uint32_t nkeys = ti.khi - ti.klo, ncol = ti.cb1 - ti.cb0;
-        if (no_ins) {
-        } else if (LDSC && nkeys <= PF) {
-            // column-parallel: key coverage + column→key map, then one thread per column
-            if (tid < nkeys) {
-                const uint4 kr = L.key[tid];
-                uint32_t cov = 0;
+        // ---- (4) insertion columns of the called keys (:290-311, :370-385)
+        if (has_ins && colpar) {
+            // one thread per column; the tile totals of the emitted chars come from here
+            // (Σ over a key's columns = the key's chars): ballot counts, one u64 sum each
+            uint64_t cs[VT_TMAX] = {};        // Σ cov over emitted chars (:385)
+            uint32_t ec[VT_TMAX] = {}, nc[VT_TMAX] = {};   // emitted / error chars (wave)
+            for (uint32_t jb = 0; jb < ncol; jb += WG) {   // uniform trip count (ballots)
+                const uint32_t j = jb + tid;
+                const uint32_t cov = j < ncol ? L.kcov[L.colkey[j]] : 0u;
+                uint32_t word = 0x2D2D2D2Du;   // '-' (not called: never emitted)
+                if (cov) {
+                    const uint32_t m = column_masks(cols + (size_t)j * NSYM, cov, &L.thr[t0], tn);
+                    word = 0;
 #pragma unroll
-                for (uint32_t c = 0; c < NSYM; c++) cov += fetch(kr.x - a, c);
-                L.kcov[tid] = (cov > 0 && (int64_t)cov >= (int64_t)d.min_depth) ? cov : 0u;   // :356-358
-                for (uint32_t c = 0; c < kr.z; c++) L.colkey[kr.y - ti.cb0 + c] = (uint16_t)tid;
-            }
-            for (int tg = t0; tg < t1; tg += 4) {   // 4 thresholds per column pass
-                const int tn = min(4, t1 - tg);
-                lds_sync();
-                S2C_STAMP(d, 8);
-                // column votes; the tile totals of the emitted chars come from here (Σ over a
-                // key's columns = the key's chars): ballot counts, one u64 sum per threshold
-                uint64_t cs[4] = {0, 0, 0, 0};   // Σ cov over emitted chars (:385)
-                uint32_t ec[4] = {0, 0, 0, 0}, nc[4] = {0, 0, 0, 0};   // emitted / error chars (wave)
-                for (uint32_t jb = 0; jb < ncol; jb += WG) {   // uniform trip count (ballots)
-                    const uint32_t j = jb + tid;
-                    const uint32_t cov = j < ncol ? L.kcov[L.colkey[j]] : 0u;
-                    uint32_t word = 0x2D2D2D2Du;   // '-' (not called: never emitted)
-                    if (cov) {
-                        const uint32_t m = column_masks(cols + (size_t)j * NSYM, cov, &L.thr[tg], tn);
-                        word = 0;
-#pragma unroll
-                        for (int u = 0; u < 4; u++) word |= (uint32_t)L.amb[(m >> (8 * u)) & 63u] << (8 * u);
-                    }
-                    if (j < ncol) {
-                        L.vchr[j] = word;
-                        for (int u = 0; u < tn; u++)
-                            d.ins_chr[(size_t)(tg + u) * d.n_cols + ti.cb0 + j] = (uint8_t)(word >> (8 * u));
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const uint8_t ic = (uint8_t)(word >> (8 * u));
-                        const bool em = cov && ic != '-' && ic != 0xFF;
-                        ec[u] += (uint32_t)__popcll(__ballot(em));
-                        nc[u] += (uint32_t)__popcll(__ballot(cov && ic == 0xFF));
-                        cs[u] += em ? cov : 0u;
-                    }
+                    for (int u = 0; u < VT_TMAX; u++) word |= (uint32_t)L.amb[(m >> (8 * u)) & 63u] << (8 * u);
                 }
-                if (tid < ((ncol + 63) & ~63u)) {   // waves that held columns
+                if (j < ncol) L.vchr[j] = word;
 #pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        if (u >= tn) break;
-                        const uint64_t scs = wave_sum(cs[u]);
-                        if (lane == 0) {
-                            unsigned long long *at = L.acc + 2 + 4 * (tg + u - t0);
-                            if (nc[u]) atomicAdd(&at[1], (unsigned long long)nc[u]);
-                            if (ec[u]) {
-                                atomicAdd(&at[2], (unsigned long long)scs);
-                                atomicAdd(&at[3], (unsigned long long)ec[u]);
-                            }
+                for (int u = 0; u < VT_TMAX; u++) {
+                    const uint8_t ic = (uint8_t)(word >> (8 * u));
+                    const bool em = cov && ic != '-' && ic != 0xFF;
+                    ec[u] += (uint32_t)__popcll(__ballot(em));
+                    nc[u] += (uint32_t)__popcll(__ballot(cov && ic == 0xFF));
+                    cs[u] += em ? cov : 0u;
+                }
+            }
+            if (tid < ((ncol + 63) & ~63u)) {   // waves that held columns
+#pragma unroll
+                for (int u = 0; u < VT_TMAX; u++) {
+                    if (u >= tn) break;
+                    const uint64_t scs = wave_sum(cs[u]);
+                    if (lane == 0) {
+                        unsigned long long *at = L.acc + 1 + 4 * u;
+                        if (nc[u]) atomicAdd(&at[1], (unsigned long long)nc[u]);
+                        if (ec[u]) {
+                            atomicAdd(&at[2], (unsigned long long)scs);
+                            atomicAdd(&at[3], (unsigned long long)ec[u]);
                         }
                     }
                 }
-                S2C_STAMP(d, 9);
-                lds_sync();
-                S2C_STAMP(d, 10);
-                if (tid < nkeys && L.kcov[tid]) {   // per key: chars emitted per threshold
-                    const uint4 kr = L.key[tid];
-                    uint32_t em[4] = {0, 0, 0, 0};
+            }
+            lds_sync();
+            if (tid < nkeys) {   // per key: chars emitted per threshold
+                const uint4 kr = L.key[tid];
+                uint32_t em[VT_TMAX] = {};
+                if (L.kcov[tid])
                     for (uint32_t c = 0; c < kr.z; c++) {
-                        const uint32_t wv = L.vchr[kr.y - ti.cb0 + c];
+                        const uint32_t wd = L.vchr[kr.y - ti.cb0 + c];
 #pragma unroll
-                        for (int u = 0; u < 4; u++) {
-                            const uint8_t ic = (uint8_t)(wv >> (8 * u));
+                        for (int u = 0; u < VT_TMAX; u++) {
+                            const uint8_t ic = (uint8_t)(wd >> (8 * u));
                             em[u] += (ic != '-' && ic != 0xFF) ? 1u : 0u;
                         }
                     }
 #pragma unroll
-                    for (int u = 0; u < 4; u++)
-                        if (u < tn) cnt_out[(size_t)(tg + u) * d.n_keys + ti.klo + tid] = make_uint4(em[u], kr.y, kr.z, 0);
-                }
+                for (int u = 0; u < VT_TMAX; u++) L.kem[u][tid] = (uint16_t)min(em[u], 0xFFFFu);
             }
-        } else {
-            // general: one thread per key, its columns in turn (> PF keys or HBM columns)
+        } else if (has_ins) {
+            // general: one thread per key, its columns in turn (> PF keys or HBM columns);
+            // the chars go to ins_chr[t][column] and {emitted, first column, columns} to
+            // ins_cnt[t][key] in HBM, read back by the body writer below
             auto vote_key = [&](const uint32_t k, const uint4 kr) {
                 uint32_t cov = 0;
 #pragma unroll
                 for (uint32_t c = 0; c < NSYM; c++) cov += fetch(kr.x - a, c);
-                if (cov == 0 || (int64_t)cov < (int64_t)d.min_depth) return;   // not called: no chars
+                const bool called = cov > 0 && (int64_t)cov >= (int64_t)d.min_depth;   // :356-358
                 const uint32_t *kcols = cols + (size_t)(kr.y - ti.cb0) * NSYM;
-                for (int t = t0; t < t1; t++) {
+                for (int u = 0; u < tn; u++) {
+                    const int t = t0 + u;
                     uint32_t em = 0, ne = 0;
-                    for (uint32_t c = 0; c < kr.z; c++) {
+                    for (uint32_t c = 0; called && c < kr.z; c++) {
                         uint32_t v[NSYM];
 #pragma unroll
                         for (uint32_t j = 0; j < NSYM; j++) v[j] = col_load<LDSC>(kcols + c * NSYM + j);
@@ -406,7 +427,7 @@ __device__ __forceinline__ void tile_epilogue(const s2c_dev &d, uint32_t tile, u
                         d.ins_chr[(size_t)t * d.n_cols + kr.y + c] = ic;
                     }
                     cnt_out[(size_t)t * d.n_keys + k] = make_uint4(em, kr.y, kr.z, 0);
-                    unsigned long long *at = L.acc + 2 + 4 * (t - t0);
+                    unsigned long long *at = L.acc + 1 + 4 * u;
                     if (ne) atomicAdd(&at[1], (unsigned long long)ne);
                     if (em) {
                         atomicAdd(&at[2], (unsigned long long)cov * em);
@@ -420,72 +441,144 @@ __device__ __forceinline__ void tile_epilogue(const s2c_dev &d, uint32_t tile, u
                 vm_drain();
                 vote_key(k, kr);
             }
-            if (!LDSC) vm_drain();   // the sc1 column loads
-        }
-        S2C_STAMP(d, 4);
-        // positions: 2 consecutive per thread, each threshold's two codes in one 2-byte store
-        uint64_t sumcov = 0, len = 0;
-        for (uint32_t qb = 0; qb < n; qb += 2 * WG) {   // uniform trip count (ballots inside)
-            const uint32_t q0 = qb + 2 * tid;
-            // per-position coverage < 2^32 (the batch holds < 2^32 read pieces): u32 sums exact
-            uint32_t cnt[2][NSYM], gs[2][NSYM], cov[2];
-            bool in[2], called[2];
-            uint32_t n_unc = 0;
-#pragma unroll
-            for (int u = 0; u < 2; u++) {
-                in[u] = q0 + u < n;
-                cov[u] = 0;
-#pragma unroll
-                for (uint32_t c = 0; c < NSYM; c++) { cnt[u][c] = in[u] ? fetch(q0 + u, c) : 0u; cov[u] += cnt[u][c]; }
-                called[u] = in[u] && cov[u] > 0 && (int64_t)cov[u] >= (int64_t)d.min_depth;   // :356-359
-                sumcov += cov[u];
-                len += called[u] ? 1u : (in[u] ? (uint32_t)d.fill_len : 0u);
-                n_unc += (uint32_t)__popcll(__ballot(in[u] && !called[u]));
-                greater_sums(cnt[u], gs[u]);
-            }
-            uint8_t *crow = d.codes + (size_t)a + q0;
-            for (int t = t0; t < t1; t++) {
-                const double th = L.thr[t];
-                uint32_t nd = 0, ne = 0, word = 0;
-#pragma unroll
-                for (int u = 0; u < 2; u++) {
-                    const uint8_t code = called[u] ? L.amb[vote_mask_u32(cnt[u], gs[u], th * (double)cov[u])]
-                                                   : (uint8_t)S2C_CODE_FILL;
-                    word |= (uint32_t)code << (8 * u);
-                    nd += (uint32_t)__popcll(__ballot(called[u] && code != '-'));
-                    ne += (uint32_t)__popcll(__ballot(called[u] && code == 0xFF));
-                }
-                uint8_t *dst = crow + (size_t)t * d.padded_len;
-                if (d.ablate & 0x400) {   // diagnostic: no code stores
-                    if (word == 0x12345u) dst[0] = 1;
-                } else if (in[1]) *(uint16_t *)dst = (uint16_t)word;
-                else if (in[0]) dst[0] = (uint8_t)word;
-                if (lane == 0) {   // non-'-' chars: called non-'-' codes + fill chars of uncalled positions
-                    unsigned long long *at = L.acc + 2 + 4 * (t - t0);
-                    atomicAdd(&at[0], (unsigned long long)(nd + (uint64_t)d.fill_nondash * n_unc));
-                    if (ne) atomicAdd(&at[1], (unsigned long long)ne);
-                }
-            }
-        }
-        sumcov = wave_sum(sumcov);
-        len = wave_sum(len);
-        if (lane == 0) {
-            atomicAdd(&L.acc[0], (unsigned long long)sumcov);
-            atomicAdd(&L.acc[1], (unsigned long long)len);
+            // the summaries / chars are read back from HBM by other threads: stores done,
+            // then the barrier below
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         lds_sync();
-        S2C_STAMP(d, 5);
-        for (uint32_t i = tid; i < (uint32_t)(t1 - t0); i += WG) {   // tile totals per threshold
-            const unsigned long long *at = L.acc + 2 + 4 * i;
-            const size_t j = (size_t)(t0 + i) * d.n_blocks + tile;
-            uint64_t *st = d.tile_stats + j * 4;
-            st[0] = L.acc[0] + at[2];   // sumcov
-            st[1] = L.acc[1] + at[3];   // len
-            st[2] = at[0] + at[3];      // non-'-' chars (insertion chars are never '-')
-            st[3] = at[1];              // vote errors (KeyError, :367/:381)
-            d.blk_len[j] = L.acc[1] + at[3];
+        S2C_STAMP(d, 4);
+        // ---- positions: vote + body bytes, 2 consecutive positions per thread per chunk
+        // insertion summary of key slot s for pass threshold u: chars emitted, and the k-th
+        // emitted char (LDS in the column-parallel case, else HBM)
+        auto body = [&](auto get_em, auto put_chars) {
+            uint64_t base[VT_TMAX] = {};   // bytes of the tile's body written so far, per threshold
+            uint64_t sumcov = 0;
+            for (uint32_t qb = 0; qb < n; qb += 2 * WG) {   // uniform trip count (scans, ballots)
+                const uint32_t q0 = qb + 2 * tid;
+                // per-position coverage < 2^32 (the batch holds < 2^32 read pieces): u32 sums exact
+                uint32_t cnt[2][NSYM], gs[2][NSYM], cov[2], slot[2];
+                bool in[2], called[2], haskey[2];
+                uint32_t n_unc = 0;
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const uint32_t q = q0 + u;
+                    in[u] = q < n;
+                    cov[u] = 0;
+#pragma unroll
+                    for (uint32_t c = 0; c < NSYM; c++) { cnt[u][c] = in[u] ? fetch(q, c) : 0u; cov[u] += cnt[u][c]; }
+                    called[u] = in[u] && cov[u] > 0 && (int64_t)cov[u] >= (int64_t)d.min_depth;   // :356-359
+                    sumcov += cov[u];
+                    n_unc += (uint32_t)__popcll(__ballot(in[u] && !called[u]));
+                    greater_sums(cnt[u], gs[u]);
+                    const uint32_t bw = in[u] ? L.bits[q >> 5] : 0u;
+                    haskey[u] = has_ins && called[u] && ((bw >> (q & 31)) & 1u);
+                    slot[u] = in[u] ? L.wrank[q >> 5] + (uint32_t)__popc(bw & ((1u << (q & 31)) - 1u)) : 0u;
+                }
+                uint8_t code[VT_TMAX][2];
+                uint32_t my[VT_TMAX], incl[VT_TMAX];
+#pragma unroll
+                for (int u = 0; u < VT_TMAX; u++) {
+                    my[u] = 0;
+                    if (u >= tn) continue;
+                    const double th = L.thr[t0 + u];
+                    uint32_t nd = 0, ne = 0;
+#pragma unroll
+                    for (int v = 0; v < 2; v++) {
+                        code[u][v] = called[v] ? L.amb[vote_mask_u32(cnt[v], gs[v], th * (double)cov[v])]
+                                               : (uint8_t)S2C_CODE_FILL;
+                        my[u] += called[v] ? 1u + (haskey[v] ? get_em(u, slot[v]) : 0u) : (in[v] ? F : 0u);
+                        nd += (uint32_t)__popcll(__ballot(called[v] && code[u][v] != '-'));
+                        ne += (uint32_t)__popcll(__ballot(called[v] && code[u][v] == 0xFF));
+                    }
+                    incl[u] = __ockl_wfscan_add_u32(my[u], true);
+                    if (lane == 63) L.wsum[u][wv] = incl[u];
+                    if (lane == 0) {   // non-'-' chars: called non-'-' codes + fill chars of uncalled positions
+                        unsigned long long *at = L.acc + 1 + 4 * u;
+                        atomicAdd(&at[0], (unsigned long long)(nd + (uint64_t)d.fill_nondash * n_unc));
+                        if (ne) atomicAdd(&at[1], (unsigned long long)ne);
+                    }
+                }
+                lds_sync();
+#pragma unroll
+                for (int u = 0; u < VT_TMAX; u++) {
+                    if (u >= tn) continue;
+                    uint64_t wofs = 0, tot = 0;
+#pragma unroll
+                    for (uint32_t i = 0; i < WG / 64; i++) {
+                        wofs += i < wv ? L.wsum[u][i] : 0ull;
+                        tot += L.wsum[u][i];
+                    }
+                    uint8_t *dst = obase + (size_t)(t0 + u) * ostride + base[u] + wofs + incl[u] - my[u];
+#pragma unroll
+                    for (int v = 0; v < 2; v++) {
+                        if (!in[v]) continue;
+                        if (!called[v]) {   // fill (:356-359)
+                            if (F <= (uint32_t)FILL_LDS) {
+                                for (uint32_t f = 0; f < F; f++) dst[f] = L.fill[f];
+                            } else {   // long -f strings from HBM (rare)
+                                for (uint32_t f = 0; f < F; f++) {
+                                    const uint8_t b = d.fill[f];
+                                    vm_drain();
+                                    dst[f] = b;
+                                }
+                            }
+                            dst += F;
+                        } else {            // vote char, then the key's insertion chars (:370-385)
+                            *dst++ = code[u][v];
+                            if (haskey[v]) dst = put_chars(u, slot[v], dst);
+                        }
+                    }
+                    base[u] += tot;
+                }
+                lds_sync();   // wsum is rewritten by the next chunk
+            }
+            // tile totals per threshold (:352-397): len is the body length itself
+            sumcov = wave_sum(sumcov);
+            if (lane == 0) atomicAdd(&L.acc[0], (unsigned long long)sumcov);
+            lds_sync();
+            if (tid < (uint32_t)tn) {
+                uint64_t bl = 0;
+#pragma unroll
+                for (int u = 0; u < VT_TMAX; u++) bl = (uint32_t)u == tid ? base[u] : bl;
+                const unsigned long long *at = L.acc + 1 + 4 * tid;
+                const size_t j = (size_t)(t0 + tid) * d.n_blocks + tile;
+                uint64_t *st = d.tile_stats + j * 4;
+                st[0] = L.acc[0] + at[2];   // sumcov: positions + cov per insertion char
+                st[1] = bl;                 // len
+                st[2] = at[0] + at[3];      // non-'-' chars (insertion chars are never '-')
+                st[3] = at[1];              // vote errors (KeyError, :367/:381)
+                d.blk_len[j] = bl;
+            }
+            lds_sync();   // acc is rezeroed by the next pass
+        };
+        if (!has_ins || colpar) {
+            body([&](int u, uint32_t s) -> uint32_t { return L.kem[u][s]; },
+                 [&](int u, uint32_t s, uint8_t *dst) -> uint8_t * {
+                     const uint4 kr = L.key[s];
+                     for (uint32_t c = 0; c < kr.z; c++) {
+                         const uint8_t ic = (uint8_t)(L.vchr[kr.y - ti.cb0 + c] >> (8 * u));
+                         if (ic != '-' && ic != 0xFF) *dst++ = ic;
+                     }
+                     return dst;
+                 });
+        } else {
+            body([&](int u, uint32_t s) -> uint32_t {
+                     const uint32_t em = cnt_out[(size_t)(t0 + u) * d.n_keys + ti.klo + s].x;
+                     vm_drain();
+                     return em;
+                 },
+                 [&](int u, uint32_t s, uint8_t *dst) -> uint8_t * {
+                     const uint4 kr = ((const uint4 *)d.ins_kinfo)[ti.klo + s];
+                     vm_drain();
+                     const uint8_t *src = d.ins_chr + (size_t)(t0 + u) * d.n_cols + kr.y;
+                     for (uint32_t c = 0; c < kr.z; c++) {
+                         const uint8_t ic = src[c];
+                         vm_drain();
+                         if (ic != '-' && ic != 0xFF) *dst++ = ic;
+                     }
+                     return dst;
+                 });
         }
-        lds_sync();   // acc is rezeroed by the next threshold pass
     }
     S2C_STAMP(d, 6);
     S2C_STAMP(d, 7);
@@ -614,12 +707,13 @@ template <int NWP>
 __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
     constexpr int G = WG / NWP, TW = NWP * 32, HP = TW / 2 + TW / 32;
     // LDS insertion columns: ≤ 40 KB of LDS in all (4 workgroups per CU) at 512 positions
-    constexpr uint32_t ICOL = NWP <= 16 ? 736 : (NWP == 32 ? 512 : 256);
+    constexpr uint32_t ICOL = NWP <= 16 ? 640 : (NWP == 32 ? 448 : 192);
     __shared__ uint32_t hist[NSYM][HP];
     __shared__ uint32_t cols[ICOL * NSYM];
     __shared__ EpiLds<ICOL> L;
     const uint32_t tid = threadIdx.x;
     const uint32_t w = tid % NWP, g = tid / NWP;
+    if (d.ablate & 0x800) return;   // diagnostic: empty kernel (launch cost)
     S2C_STAMP(d, 0);
     if (tid < 64) L.amb[tid] = c_amb[tid];   // published by the barrier after the histogram zeroing
     const uint32_t *__restrict__ recs = d.recs;
@@ -642,7 +736,7 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
     }
     const bool finish = !deep && !(d.ablate & 4);
     Prefetch pf;   // epilogue records, in flight under the count stream
-    if (finish) prefetch_load(d, ti, pf);
+    if (finish) prefetch_load(d, a, n, ti, pf);
     for (uint32_t i = tid; i < NSYM * (uint32_t)HP; i += WG) (&hist[0][0])[i] = 0;
     lds_sync();
     S2C_STAMP(d, 1);
@@ -679,7 +773,7 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
     uint32_t P[8][3], Q[8][3];
     if (t < e0) load8(P, t, e0);
     __builtin_amdgcn_sched_barrier(0);
-    if (finish) prefetch_store(d, L, pf);   // their loads were issued before P's
+    if (finish) prefetch_store(d, L, n, pf);   // their loads were issued before P's
     if (t < e0) {
         // two groups of 8 per trip (one 16-record carry-save step), the next group always
         // in flight while one is counted.  sched_barrier keeps each group's loads issued
@@ -764,179 +858,11 @@ __global__ __launch_bounds__(WG) void k_consensus(const s2c_dev d) {
     const uint32_t a = uni(blk[0]), n = uni(blk[1]) - a;
     const TileIns ti = tile_ins(blk);
     Prefetch pf;
-    prefetch_load(d, ti, pf);
-    prefetch_store(d, L, pf);
+    prefetch_load(d, a, n, ti, pf);
+    prefetch_store(d, L, n, pf);
     const uint32_t *cts = d.counts + a;
     const size_t Lp = d.padded_len;
     tile_finish<ICOL>(d, tile, a, n, ti, [&](uint32_t q, uint32_t c) { return cts[(size_t)c * Lp + q]; }, cols, L);
-}
-
-// ======================================================================= assembly
-// Record body of (ref, t) = concatenation over its positions of fill (uncalled) or the
-// vote char followed by the emitted insertion chars (:367-389).  grid = n_blocks × T;
-// block j = t·n_blocks + tile writes at the exclusive prefix of blk_len ([t][tile] byte
-// order).  Up to ASM_DIRECT blocks each workgroup sums its own prefix (≤ 32 independent
-// loads per thread, L2-resident); beyond, k_scan writes blk_off first.
-constexpr uint64_t ASM_DIRECT = 32 * WG;
-
-__global__ __launch_bounds__(1024) void k_scan(const s2c_dev d) {   // one workgroup
-    __shared__ uint64_t sh[1024 / 64];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const uint64_t NB = (uint64_t)d.n_thr * (uint64_t)d.n_blocks;
-    const uint64_t per = (NB + 1023) / 1024, b0 = min(NB, tid * per), b1 = min(NB, b0 + per);
-    uint64_t s = 0;
-    for (uint64_t g = b0; g < b1; g += 16) {   // 16 independent loads in flight per thread
-        uint64_t v[16];
-#pragma unroll
-        for (int u = 0; u < 16; u++) v[u] = g + u < b1 ? d.blk_len[g + u] : 0ull;
-#pragma unroll
-        for (int u = 0; u < 16; u++) s += v[u];
-    }
-    uint64_t x = s;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t y = __shfl_up(x, o, 64);
-        if (lane >= (uint32_t)o) x += y;
-    }
-    if (lane == 63) sh[wv] = x;
-    lds_sync();
-    uint64_t run = x - s;
-    for (uint32_t i = 0; i < wv; i++) run += sh[i];
-    for (uint64_t g = b0; g < b1; g += 16) {
-        uint64_t v[16];
-#pragma unroll
-        for (int u = 0; u < 16; u++) v[u] = g + u < b1 ? d.blk_len[g + u] : 0ull;
-#pragma unroll
-        for (int u = 0; u < 16; u++)
-            if (g + u < b1) {
-                d.blk_off[g + u] = run;
-                run += v[u];
-            }
-    }
-    if (tid == 1023) d.blk_off[NB] = run;
-}
-
-extern "C" __device__ unsigned long long __ockl_wfscan_add_u64(unsigned long long, bool);   // (x, inclusive)
-
-// Two rounds of loads: the tile record and the prefix, then everything the tile's bytes
-// need at once — its codes, key bitmap/rank, the insertion summaries of its keys and the
-// vote chars of its columns (staged in LDS) — then one byte scatter.
-constexpr uint32_t ASM_KEYS = WG, ASM_COLS = 2048;
-template <int ASM_PER, bool DIRECT>   // consecutive positions per thread (tile_max / 256)
-__global__ __launch_bounds__(WG) void k_assemble(const s2c_dev d) {
-    __shared__ uint64_t sh[WG / 64];
-    __shared__ uint64_t sbase[WG / 64];
-    __shared__ uint4 kc[ASM_KEYS];           // ins_cnt of the tile's keys (this threshold)
-    __shared__ uint8_t kchr[ASM_COLS];       // ins_chr of the tile's columns (this threshold)
-    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint32_t bi = blockIdx.x;
-    const int t = (int)blockIdx.y;
-    const uint64_t nb = (uint64_t)d.n_blocks, NB = (uint64_t)d.n_thr * nb;
-    const uint64_t j = (uint64_t)t * nb + bi;
-    // ---- round 1: the tile record, the prefix
-    uint64_t pre = 0;   // this thread's share of the prefix
-    if constexpr (DIRECT) {
-        uint64_t v[ASM_DIRECT / WG];
-#pragma unroll
-        for (uint32_t u = 0; u < ASM_DIRECT / WG; u++) {
-            const uint64_t i = tid + (uint64_t)u * WG;
-            v[u] = i < j ? d.blk_len[i] : 0ull;
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < ASM_DIRECT / WG; u++) pre += v[u];
-    } else {
-        if (tid == 0) pre = d.blk_off[j];
-    }
-    const uint32_t *blk = d.blocks + (size_t)bi * S2C_BLOCK_WORDS;
-    const uint32_t g0 = uni(blk[0]), g1 = uni(blk[1]);
-    const TileIns ti = tile_ins(blk);
-    // ---- round 2: codes, key bitmap/rank, the tile's key summaries and column chars
-    const uint8_t *codes = d.codes + (size_t)t * d.padded_len;
-    const uint4 *cnt_in = (const uint4 *)d.ins_cnt + (size_t)t * d.n_keys;
-    const uint8_t *chr_in = d.ins_chr + (size_t)t * d.n_cols;
-    const uint32_t nkeys = ti.khi - ti.klo, ncol = ti.cb1 - ti.cb0;
-    const bool stage = nkeys <= ASM_KEYS && ncol <= ASM_COLS;   // uniform
-    if (stage) {
-        if (tid < nkeys) kc[tid] = cnt_in[ti.klo + tid];
-        for (uint32_t i = tid; i < ncol; i += WG) kchr[i] = chr_in[ti.cb0 + i];
-    }
-    const uint32_t p0 = g0 + ASM_PER * tid;
-    uint8_t cc[ASM_PER];
-    uint32_t bits[ASM_PER], rank[ASM_PER];
-#pragma unroll
-    for (int jj = 0; jj < ASM_PER; jj++) {
-        const uint32_t p = p0 + jj;
-        const bool in = p < g1;
-        cc[jj] = in ? codes[p] : (uint8_t)0;
-        bits[jj] = in ? d.ins_bits[p >> 5] : 0u;
-        rank[jj] = in ? d.ins_rank[p >> 5] : 0u;
-    }
-    lds_sync();   // staged summaries / chars
-    // the rest, with the summaries / chars read from LDS (staged) or HBM (tiles beyond the
-    // staging capacity): two instantiations, so no load becomes a flat (generic) load
-    auto body = [&](auto get_cnt, auto get_chr) {
-        uint32_t lens[ASM_PER], col0[ASM_PER], ncl[ASM_PER];
-        uint64_t my = 0;
-#pragma unroll
-        for (int jj = 0; jj < ASM_PER; jj++) {
-            const uint32_t p = p0 + jj;
-            lens[jj] = 0;
-            col0[jj] = 0;
-            ncl[jj] = 0;
-            if (p < g1) {
-                if (cc[jj] == S2C_CODE_FILL) {
-                    lens[jj] = (uint32_t)d.fill_len;
-                } else {
-                    lens[jj] = 1;
-                    if (bits[jj] >> (p & 31) & 1u) {
-                        const uint32_t k = rank[jj] + (uint32_t)__popc(bits[jj] & ((1u << (p & 31)) - 1u));
-                        const uint4 ic = get_cnt(k);   // {chars, first column, columns}
-                        lens[jj] += ic.x;
-                        col0[jj] = ic.y;
-                        ncl[jj] = ic.z;
-                    }
-                }
-            }
-            my += lens[jj];
-        }
-        pre = wave_sum(pre);
-        const uint64_t x = __ockl_wfscan_add_u64(my, true);   // inclusive (DPP)
-        if (lane == 63) sh[w] = x;
-        if (lane == 0) sbase[w] = pre;
-        lds_sync();
-        uint64_t wofs = 0, base = 0;
-#pragma unroll
-        for (uint32_t i = 0; i < WG / 64; i++) {
-            wofs += i < w ? sh[i] : 0;
-            base += sbase[i];
-        }
-        if (DIRECT && tid == 0) {   // offsets for the host
-            d.blk_off[j] = base;
-            if (j == NB - 1) d.blk_off[NB] = base + sh[0] + sh[1] + sh[2] + sh[3];
-        }
-        uint64_t off = base + wofs + x - my;
-#pragma unroll
-        for (int jj = 0; jj < ASM_PER; jj++) {
-            const uint32_t p = p0 + jj;
-            if (p >= g1) break;
-            if (cc[jj] == S2C_CODE_FILL) {
-                for (int f = 0; f < d.fill_len; f++) d.out[off + f] = d.fill[f];
-                off += (uint32_t)d.fill_len;
-            } else {
-                d.out[off++] = cc[jj];
-                if (lens[jj] > 1) {   // the key's column votes that are neither '-' nor an error
-                    for (uint32_t i = 0; i < ncl[jj]; i++) {
-                        const uint8_t ic = get_chr(col0[jj] + i);
-                        if (ic != '-' && ic != 0xFF) d.out[off++] = ic;
-                    }
-                }
-            }
-        }
-    };
-    if (stage)
-        body([&](uint32_t k) { return kc[k - ti.klo]; }, [&](uint32_t c) { return kchr[c - ti.cb0]; });
-    else
-        body([&](uint32_t k) { return cnt_in[k]; }, [&](uint32_t c) { return chr_in[c]; });
 }
 
 inline int hip_check(hipError_t e, const char *what) {
@@ -955,10 +881,11 @@ extern "C" int s2c_workspace_sizes(const s2c_batch_info *info, int32_t n_thr, s2
     o->ins_cols = nc * NSYM * 4;
     o->ins_cnt = T * nk * 16;
     o->ins_chr = T * nc;
-    o->codes = T * L;
     o->blk_len = std::max<int64_t>(NB, 1) * 8;
-    o->blk_off = (NB + 1) * 8;
     o->tile_stats = std::max<int64_t>(NB, 1) * 32;
+    // T body regions of max(1, len(fill))·L + n_cols bytes: the fill length is a run option
+    o->out_per_fill = T * L;
+    o->out_fixed = T * (info->n_cols + 16);
     return S2C_OK;
 }
 
@@ -980,12 +907,16 @@ static int check_dev(const s2c_dev *d) {
     }
     if (d->n_deep > 0 && (!d->deep || !d->counts)) return s2c_set_error(S2C_ERR_ARG, "missing deep-tile buffers");
     if ((d->ablate & 0x104) && !d->counts) return s2c_set_error(S2C_ERR_ARG, "ablate&0x104 writes `counts`: counts buffer required");
-    if (!d->ins_bits || !d->ins_rank) return s2c_set_error(S2C_ERR_ARG, "missing key bitmap/rank");
+    if (!d->ins_bits) return s2c_set_error(S2C_ERR_ARG, "missing key bitmap");
     if (d->n_keys > 0 && (!d->ins_ev || !d->ins_kinfo || !d->ins_bases || !d->ins_cols || !d->ins_cnt || !d->ins_chr))
         return s2c_set_error(S2C_ERR_ARG, "missing insertion buffers");
-    if (d->n_blocks > 0 && (!d->blocks || !d->codes || !d->blk_len || !d->blk_off || !d->tile_stats ||
-                            !d->out))
-        return s2c_set_error(S2C_ERR_ARG, "missing vote/assembly buffers");
+    if (d->n_blocks > 0 && (!d->blocks || !d->blk_len || !d->tile_stats || !d->out))
+        return s2c_set_error(S2C_ERR_ARG, "missing vote/body buffers");
+    if (d->fill_len < 0 || (d->fill_len > 0 && !d->fill)) return s2c_set_error(S2C_ERR_ARG, "bad fill");
+    {   // every tile's body slot must fit: T regions of max(1, len(fill))·L + n_cols bytes
+        const int64_t need = (int64_t)d->n_thr * ((int64_t)std::max(1, d->fill_len) * d->padded_len + d->n_cols);
+        if (d->out_cap < need) return s2c_set_error(S2C_ERR_ARG, "out buffer smaller than the body slots");
+    }
     return S2C_OK;
 }
 
@@ -1021,32 +952,8 @@ extern "C" int s2c_consensus(const s2c_dev *d, void *stream) {
     return S2C_OK;
 }
 
-template <bool DIRECT>
-static void launch_assemble(const s2c_dev *d, hipStream_t s) {
-    const dim3 g((unsigned)d->n_blocks, (unsigned)d->n_thr);
-    if (d->tile_max <= 256) k_assemble<1, DIRECT><<<g, WG, 0, s>>>(*d);
-    else if (d->tile_max <= 512) k_assemble<2, DIRECT><<<g, WG, 0, s>>>(*d);
-    else if (d->tile_max <= 1024) k_assemble<4, DIRECT><<<g, WG, 0, s>>>(*d);
-    else k_assemble<8, DIRECT><<<g, WG, 0, s>>>(*d);
-}
-
-extern "C" int s2c_assemble(const s2c_dev *d, void *stream) {
-    int rc = check_dev(d);
-    if (rc) return rc;
-    hipStream_t s = (hipStream_t)stream;
-    if (d->n_blocks == 0) return S2C_OK;
-    if ((uint64_t)d->n_thr * (uint64_t)d->n_blocks <= ASM_DIRECT) {
-        launch_assemble<true>(d, s);
-    } else {
-        k_scan<<<1, 1024, 0, s>>>(*d);
-        launch_assemble<false>(d, s);
-    }
-    return hip_check(hipGetLastError(), "k_assemble");
-}
-
 extern "C" int s2c_run(const s2c_dev *d, void *stream) {
     int rc;
     if ((rc = s2c_pileup(d, stream))) return rc;
-    if ((rc = s2c_consensus(d, stream))) return rc;
-    return s2c_assemble(d, stream);
+    return s2c_consensus(d, stream);
 }

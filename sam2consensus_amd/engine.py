@@ -91,18 +91,18 @@ class Workspace:
         self.ins_cols = u8(sz.ins_cols)
         self.ins_cnt = u8(sz.ins_cnt)
         self.ins_chr = u8(sz.ins_chr)
-        self.codes = u8(sz.codes)
         self.blk_len = u8(sz.blk_len)
-        self.blk_off = u8(sz.blk_off)
         self.tile_stats = u8(sz.tile_stats)
-        # output upper bound: every position fill or char + every insertion base, per threshold
-        cap = self.T * (i.total_len * max(1, len(fill)) + i.n_cols) + 16
+        # body slots: per threshold max(1, len(fill)) bytes per padded position + the columns
+        self.fill_w = max(1, len(fill))
+        self.out_stride = self.fill_w * i.padded_len + i.n_cols
+        cap = int(sz.out_per_fill) * self.fill_w + int(sz.out_fixed)
         self.out = u8(cap)
         d = L.Dev()
         d.wrec, d.recs = _ptr(db.wrec), _ptr(db.recs)
         d.items, d.blocks, d.deep = _ptr(db.items), _ptr(db.blocks), _ptr(db.deep)
         d.ins_ev, d.ins_kinfo, d.ins_bases = _ptr(db.ins_ev), _ptr(db.ins_kinfo), _ptr(db.ins_bases)
-        d.ins_bits, d.ins_rank = _ptr(db.ins_bits), _ptr(db.ins_rank)
+        d.ins_bits = _ptr(db.ins_bits)
         d.n_recs, d.chunk_recs = i.n_recs, i.chunk_recs
         d.n_items, d.n_blocks, d.n_deep = i.n_items, i.n_blocks, i.n_deep
         d.n_keys, d.n_cols, d.padded_len = i.n_keys, i.n_cols, i.padded_len
@@ -113,16 +113,14 @@ class Workspace:
         d.fill = _ptr(self.fill)
         d.counts = _ptr(self.counts)
         d.ins_cols, d.ins_cnt, d.ins_chr = _ptr(self.ins_cols), _ptr(self.ins_cnt), _ptr(self.ins_chr)
-        d.codes = _ptr(self.codes)
-        d.blk_len = _ptr(self.blk_len)
-        d.tile_stats, d.blk_off = _ptr(self.tile_stats), _ptr(self.blk_off)
+        d.tile_stats, d.blk_len = _ptr(self.tile_stats), _ptr(self.blk_len)
         d.out, d.out_cap = _ptr(self.out), cap
         self.dev = d
 
     def stream_handle(self):
         return C.c_void_p(torch.cuda.current_stream(self.db.device).cuda_stream)
 
-    # ---- the three stages in run order (each one C-ABI call; asynchronous on the current stream)
+    # ---- the two stages in run order (each one C-ABI call; asynchronous on the current stream)
     def pileup(self):
         if (self.dev.ablate & 4) and not self.keep_counts:
             raise ValueError("diagnostic ablate&4 stores every count: build the Workspace with keep_counts=True")
@@ -131,11 +129,8 @@ class Workspace:
     def consensus(self):
         L.check(lib.s2c_consensus(C.byref(self.dev), self.stream_handle()))
 
-    def assemble(self):
-        L.check(lib.s2c_assemble(C.byref(self.dev), self.stream_handle()))
-
     def run(self):
-        """pileup(+insertions, vote) → deep-tile consensus → assembly (no host sync)."""
+        """pileup (+ insertion columns, vote, FASTA bodies) → deep tiles (no host sync)."""
         L.check(lib.s2c_run(C.byref(self.dev), self.stream_handle()))
 
     # ---- HIP graph of one run (the stage launches replayed without host launch overhead)
@@ -176,7 +171,7 @@ class Workspace:
         return self.counts[: 6 * Lp * 4].view(torch.int32).cpu().numpy().view(np.uint32).reshape(6, Lp)
 
     def fetch(self):
-        """Synchronise and copy results: (stats[R,T,4] u64, blk_off[T*nb+1] u64, out bytes).
+        """Synchronise and copy results: (stats[R,T,4] u64, offs[T*nb+1] u64, out bytes).
 
         stats[r, t] = Σ over reference r's tiles of the device's per-tile statistics
         (tiles never straddle a reference; :352-397 sums)."""
@@ -191,7 +186,16 @@ class Workspace:
                 np.add.at(stats[:, t, :], ref, ts[t])
         if T * nb == 0:
             return stats, np.zeros(1, dtype=np.uint64), b""
-        offs = self.blk_off[: (T * nb + 1) * 8].view(torch.int64).cpu().numpy().view(np.uint64)
+        # each tile wrote its body into its slot; the references' bodies are their tiles'
+        # pieces in order: gather them into [t][tile] order (one vectorised index)
+        lens = self.blk_len[: T * nb * 8].view(torch.int64).cpu().numpy().astype(np.int64)
+        blocks = self.db.hb.blocks.astype(np.int64)
+        slot = self.fill_w * blocks[:, 0] + blocks[:, 8]                     # F·a + cb0
+        starts = (np.arange(T, dtype=np.int64)[:, None] * self.out_stride + slot[None, :]).reshape(-1)
+        offs = np.zeros(T * nb + 1, dtype=np.int64)
+        np.cumsum(lens, out=offs[1:])
         total = int(offs[-1])
-        out = self.out[:total].cpu().numpy().tobytes()
-        return stats, offs, out
+        raw = self.out[: T * self.out_stride].cpu().numpy()
+        idx = np.repeat(starts - offs[:-1], lens) + np.arange(total, dtype=np.int64)
+        out = raw[idx].tobytes()
+        return stats, offs.astype(np.uint64), out

@@ -13,7 +13,8 @@ from sam2consensus_amd import configs  # noqa: E402
 from sam2consensus_amd.engine import DeviceBatch, Workspace  # noqa: E402
 
 MODES = {0: "full", 1: "skip counting loop", 2: "loads only (no counting)",
-         4: "store counts, no vote", 5: "1|4 (zero+store only)", 6: "2|4", 12: "4|8 (no flush, no vote)"}
+         4: "store counts, no vote", 5: "1|4 (zero+store only)", 6: "2|4", 12: "4|8 (no flush, no vote)",
+         0x800: "empty kernel (launch)"}
 
 
 def main():
@@ -29,8 +30,7 @@ def main():
             e0.record()
             ws.pileup()
             e1.record()
-            ws.consensus()   # untimed: the stages run as a set (segment sums)
-            ws.assemble()
+            ws.consensus()   # untimed
             torch.cuda.synchronize()
             times[m].append(e0.elapsed_time(e1))
     ws.dev.ablate = 0

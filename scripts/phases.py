@@ -32,8 +32,6 @@ def main():
     ws.consensus()
     torch.cuda.synchronize()
     ws.dev.ablate = 0
-    ws.assemble()   # the stages run as a set (segment sums)
-    torch.cuda.synchronize()
     ws.dev.ablate = 0
     ts = ws.counts[: ni * 128].view(torch.int64).cpu().numpy().reshape(ni, 16).astype(np.float64) / 100.0  # µs
     t0 = ts[:, 0].min()

@@ -151,14 +151,18 @@ def test_sharded_on_device(world):
     assert files(stats, offs, out) == want
 
 
-@pytest.mark.parametrize("name,over,thr", [
-    ("c2", {"n_refs": 6}, [0.25, 0.5, 0.75]),
+@pytest.mark.parametrize("name,over,thr,md,fill", [
+    ("c2", {"n_refs": 6}, [0.25, 0.5, 0.75], 1, b"-"),
     # long insertions: > 1024 insertion columns in a tile → the HBM column path
-    ("c2", {"n_refs": 2, "depth": 60.0, "ins_frac": 0.6, "ins_max": 60}, [0.1, 0.5]),
+    ("c2", {"n_refs": 2, "depth": 60.0, "ins_frac": 0.6, "ins_max": 60}, [0.1, 0.5], 1, b"-"),
     # deep tiles (several work items) with insertions: k_prep + k_consensus epilogue
-    ("c2", {"n_refs": 1, "ref_len": 700, "depth": 9000.0, "ins_frac": 0.05, "ins_max": 6}, [0.25, 0.75]),
+    ("c2", {"n_refs": 1, "ref_len": 700, "depth": 9000.0, "ins_frac": 0.05, "ins_max": 6}, [0.25, 0.75], 1, b"-"),
+    # 6 thresholds (two passes of 4), min depth with uncalled positions, a 100-byte fill (HBM)
+    ("c2", {"n_refs": 3, "depth": 30.0}, [0.1, 0.3, 0.5, 0.6, 0.8, 0.95], 25, b"Nn" * 50),
+    # empty fill: uncalled positions write nothing
+    ("c2", {"n_refs": 2, "depth": 30.0}, [0.5], 25, b""),
 ])
-def test_device_pipeline_equals_batch_model(name, over, thr):
+def test_device_pipeline_equals_batch_model(name, over, thr, md, fill):
     """stats / block offsets / bytes of the HIP stages == the batch model (tests/batch_model.py)."""
     from sam2consensus_amd import configs
     hb = configs.synth_batch(name, **over)
@@ -170,11 +174,11 @@ def test_device_pipeline_equals_batch_model(name, over, thr):
         assert max(ncol_tile) > 1024, "case must exercise the HBM insertion-column path"
     if over.get("depth") == 9000.0:
         assert hb.info.n_deep > 0 and hb.info.n_keys > 0
-    ws = _ws(hb, thr)
-    for _ in range(2):   # second run: the look-back scan state of the first must not leak
+    ws = _ws(hb, thr, min_depth=md, fill=fill)
+    want = bm.model_pipeline(hb, thr, md, fill)
+    for _ in range(2):   # second run: no state of the first may leak
         ws.run()
         st, offs, out = ws.fetch()
-        want = bm.model_pipeline(hb, thr)
         assert (st == want[0]).all()
         assert (offs == want[1]).all()
         assert out == want[2]
