@@ -51,7 +51,13 @@ int s2c_layout(int64_t *out, int n);
 #define S2C_NSYM          6    /* symbols '-','A','C','G','N','T' — sorted() order (:367) */
 #define S2C_POS_ALIGN    64    /* each reference starts at a multiple of this global coordinate */
 #define S2C_ITEM_WORDS    4    /* u32 words per pileup work item {a, b, chunk, tile} */
-#define S2C_BLOCK_WORDS  12    /* u32 words per tile {a, b, ref, deep, klo, khi, e0, e1, cb0, cb1, 0, 0} */
+#define S2C_BLOCK_WORDS  12    /* u32 words per tile {a, b, ref, flags, klo, khi, e0, e1, cb0, cb1, 0, 0} */
+#define S2C_TILE_DEEP     1    /* flags: the tile's records take several work items (HBM counts) */
+#define S2C_TILE_GENERAL  2    /* flags: more insertion columns / keys than k_pileup's LDS holds:
+                                  its counts go to HBM and k_consensus votes it */
+#define S2C_EPI_KEYS    256    /* keys per tile the k_pileup epilogue holds in LDS */
+/* insertion columns per tile the k_pileup epilogue holds in LDS, by words per tile */
+#define S2C_LDS_COLS(nwp) ((nwp) <= 16 ? 640 : ((nwp) == 32 ? 448 : 192))
 #define S2C_CODE_FILL     0    /* internal vote char of a fill position */
 #define S2C_CODE_ERR   0xFF    /* vote char where the vote hit a missing amb key (:367) */
 #define S2C_TILE_MAX   2048    /* positions per tile */
@@ -99,7 +105,8 @@ typedef struct {
     int64_t n_items;           /* pileup work items */
     int64_t n_blocks;          /* tiles = consensus/assembly blocks (never straddle a ref) */
     int64_t tile_max;          /* max positions of any tile (≤ 2048) */
-    int64_t n_deep;            /* tiles split over several work items (voted by k_consensus) */
+    int64_t n_deep;            /* tiles voted by k_consensus: split over several work items
+                                  (S2C_TILE_DEEP) or beyond k_pileup's LDS (S2C_TILE_GENERAL) */
 } s2c_batch_info;
 
 typedef struct {               /* host pointers into the batch (valid until s2c_batch_free) */

@@ -684,13 +684,11 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
             uint32_t it[S2C_ITEM_WORDS] = {(uint32_t)T.a, (uint32_t)T.b, (uint32_t)c, (uint32_t)t};
             b->items.insert(b->items.end(), it, it + S2C_ITEM_WORDS);
         }
-        uint32_t blk[S2C_BLOCK_WORDS] = {(uint32_t)T.a, (uint32_t)T.b, (uint32_t)T.ref, nch > 1 ? 1u : 0u};   // words 4-9 below
+        uint32_t blk[S2C_BLOCK_WORDS] = {(uint32_t)T.a, (uint32_t)T.b, (uint32_t)T.ref, nch > 1 ? (uint32_t)S2C_TILE_DEEP : 0u};   // words 4-9 below
         b->blocks.insert(b->blocks.end(), blk, blk + S2C_BLOCK_WORDS);
-        if (nch > 1) b->deep.push_back((uint32_t)t);
     }
     I.n_items = (int64_t)(b->items.size() / S2C_ITEM_WORDS);
     I.n_blocks = (int64_t)(b->blocks.size() / S2C_BLOCK_WORDS);
-    I.n_deep = (int64_t)b->deep.size();
 
     // ---- insertion events grouped by key (:256-294), keys sorted by position ----
     // Keys in [0, LN) only (negative keys are never emitted, :371).  Per key: its events
@@ -784,6 +782,17 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
         I.n_ins_words = (int64_t)b->ins_bases.size();
         I.n_keys = (int64_t)nk;
         I.n_cols = (int64_t)ncol;
+    }
+    {   // tiles k_consensus votes: deep ones, and those whose insertion keys / columns exceed
+        // what k_pileup's epilogue holds in LDS (their counts go to HBM)
+        const size_t ntile = b->blocks.size() / S2C_BLOCK_WORDS;
+        const int64_t lcols = S2C_LDS_COLS(nwp);
+        for (size_t t = 0; t < ntile; t++) {
+            uint32_t *blk = &b->blocks[t * S2C_BLOCK_WORDS];
+            if (blk[5] - blk[4] > S2C_EPI_KEYS || (int64_t)(blk[9] - blk[8]) > lcols) blk[3] |= S2C_TILE_GENERAL;
+            if (blk[3]) b->deep.push_back((uint32_t)t);
+        }
+        I.n_deep = (int64_t)b->deep.size();
     }
     *out = b;
     return S2C_OK;

@@ -233,6 +233,7 @@ struct EpiLds {
     double thr[THR_MAX];               // -c thresholds, CLI order
     unsigned long long acc[VT_ACC];
     uint64_t wsum[VT_TMAX][WG / 64];   // body-length scan: wave totals
+    uint32_t fsum[VT_TMAX][WG / 64];   // the same, fast epilogue
     uint32_t kcov[PF];                 // coverage of each key's position if called, else 0
     uint32_t bits[TILE_WORDS];         // key bitmap of the tile's words
     uint32_t wrank[TILE_WORDS];        // keys of the tile before each word
@@ -499,6 +500,7 @@ __device__ __forceinline__ void tile_epilogue(const s2c_dev &d, uint32_t tile, u
                     }
                 }
                 lds_sync();
+                S2C_STAMP(d, 5);
 #pragma unroll
                 for (int u = 0; u < VT_TMAX; u++) {
                     if (u >= tn) continue;
@@ -530,7 +532,9 @@ __device__ __forceinline__ void tile_epilogue(const s2c_dev &d, uint32_t tile, u
                     }
                     base[u] += tot;
                 }
+                S2C_STAMP(d, 8);
                 lds_sync();   // wsum is rewritten by the next chunk
+                S2C_STAMP(d, 9);
             }
             // tile totals per threshold (:352-397): len is the body length itself
             sumcov = wave_sum(sumcov);
@@ -693,6 +697,340 @@ __device__ __forceinline__ uint32_t hist_get(const uint32_t *h, uint32_t q) {
     return (h[hslot(((q >> 5) << 4) | (q & 15))] >> ((q & 16) ? 16 : 0)) & 0xFFFFu;
 }
 
+// ======================================================================= fast tile epilogue
+// The common case of k_pileup (columns in LDS, ≤ PF keys, -f ≤ FILL_LDS bytes).  The
+// insertion events were already counted into `cols`, the column → key map and the key ranks
+// of the tile's words built in the prologue (under the record loads).  After the counts are
+// complete, per pass of ≤ 4 thresholds and chunk of 512 positions:
+//   A  the column votes (first chunk of a pass) and the position votes;
+//   B  each position's body length per threshold (1 + its key's emitted insertion chars,
+//      or len(fill)), a packed 16-bit row scan (DPP) per threshold, wave totals, the tile
+//      statistics into LDS;
+//   C  byte offsets → body bytes; the last chunk writes the tile statistics.
+// Three barriers per (pass, chunk).  A thread takes positions q and q + 16 of one
+// 32-position word: their u16 counts share a histogram word.  The vote is the closed form
+// (S9), evaluated in full only in waves holding a called position whose largest count is
+// not unique or is below t·cov of the pass's largest threshold; elsewhere the char is that
+// symbol's for every threshold (fl(t·cov) is monotone in t, so m ≥ tmax·cov ⇒ m ≥ t·cov).
+
+// Inclusive prefix sum inside each 16-lane row (DPP row_shr, zeros shifted in).
+__device__ __forceinline__ uint32_t row_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);
+    return x;
+}
+
+// char of a one-symbol mask, amb[1 << s] = "-ACGNT"[s]
+__device__ __forceinline__ uint32_t sym_char(uint32_t s) { return (uint32_t)(0x544E4743412DULL >> (8 * s)) & 0xFFu; }
+
+// One position of the fast epilogue: counts, coverage, called (:356-359), and the vote chars
+// of the pass's thresholds (byte u ↔ threshold t0 + u); `slow` = needs the full closed form.
+struct Pos {
+    uint32_t c[NSYM];
+    uint32_t cov, chars;
+    bool in, called, slow;
+};
+__device__ __forceinline__ void pos_vote_fast(Pos &p, int32_t min_depth, double tmax, bool fastok) {
+    p.cov = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < NSYM; s++) p.cov += p.c[s];
+    p.called = p.in && p.cov > 0 && (int64_t)p.cov >= (int64_t)min_depth;
+    // largest count (key = count << 3 | symbol) and the largest of the others
+    uint32_t k[NSYM];
+#pragma unroll
+    for (uint32_t s = 0; s < NSYM; s++) k[s] = (p.c[s] << 3) | s;
+    const uint32_t mk = max(max(max(k[0], k[1]), k[2]), max(max(k[3], k[4]), k[5]));
+    uint32_t m2 = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < NSYM; s++) m2 = max(m2, k[s] == mk ? 0u : k[s]);
+    const uint32_t m1 = mk >> 3;
+    const bool fast = fastok && (m2 >> 3) < m1 && (double)m1 >= tmax * (double)p.cov;
+    p.chars = sym_char(mk & 7u) * 0x01010101u;
+    p.slow = p.called && !fast;
+}
+template <class EL>
+__device__ __forceinline__ void pos_vote_slow(Pos &p, const EL &L, int t0, int tn) {
+    uint32_t gs[NSYM];
+    greater_sums(p.c, gs);
+    uint32_t w = 0;
+#pragma unroll
+    for (int u = 0; u < VT_TMAX; u++)
+        if (u < tn) w |= (uint32_t)L.amb[vote_mask_u32(p.c, gs, L.thr[t0 + u] * (double)p.cov)] << (8 * u);
+    if (p.slow) p.chars = w;
+}
+
+// per byte of a vote-char word: 1 if the char is emitted (neither '-' nor a vote error),
+// thresholds 0/2 in the 16-bit halves of the first result, 1/3 of the second
+__device__ __forceinline__ void emitted4(uint32_t w, uint32_t &e02, uint32_t &e13) {
+    const uint32_t x = w ^ 0x2D2D2D2Du, y = ~w;
+    const uint32_t nzx = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;   // bit 7 of a byte: byte != 0
+    const uint32_t nzy = ((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y;
+    const uint32_t f = (nzx & nzy) >> 7;                          // bit 0 of each byte
+    e02 += f & 0x00010001u;
+    e13 += (f >> 8) & 0x00010001u;
+}
+__device__ __forceinline__ uint32_t em_of(uint32_t e02, uint32_t e13, int u) {
+    return ((u & 1) ? (e13 >> (8 * (u & 2))) : (e02 >> (8 * (u & 2)))) & 0xFFFFu;
+}
+
+// Prologue part of the fast epilogue, while the first records are in flight: the tile's
+// insertion events added into the column counts (cols zeroed before the prologue barrier),
+// the column → key slot map and, in wave 0, the keys before each of the tile's words.  The
+// records come from the prefetch registers; events beyond PF (rare) from HBM.
+template <class EL>
+__device__ __forceinline__ void fast_prologue(const s2c_dev &d, EL &L, uint32_t *cols, const TileIns &ti,
+                                              uint32_t n, const Prefetch &pf) {
+    const uint32_t tid = threadIdx.x;
+    if (ti.khi <= ti.klo || (d.ablate & 0x200)) return;   // uniform
+    auto add_event = [&](const uint4 r) {   // :264-287 motif symbols into the key's columns
+        uint32_t *cc = cols + (size_t)r.x * NSYM;
+        for (uint32_t c = 0; c < r.y; c++) {
+            uint32_t sym;
+            if (c < 8) {
+                sym = (r.w >> (4 * c)) & 15u;
+            } else {
+                sym = nibble(d.ins_bases, (uint64_t)r.z + c);   // motifs > 8 bases (rare)
+                vm_drain();
+            }
+            atomicAdd(&cc[c * NSYM + sym], 1u);
+        }
+    };
+    if (ti.e0 + tid < ti.e1) add_event(pf.ev);
+    for (uint32_t e = ti.e0 + PF + tid; e < ti.e1; e += WG) {
+        const uint4 r = ((const uint4 *)d.ins_ev)[e];
+        vm_drain();
+        add_event(r);
+    }
+    if (ti.klo + tid < ti.khi)
+        for (uint32_t c = 0; c < pf.key.z; c++) L.colkey[pf.key.y - ti.cb0 + c] = (uint16_t)tid;
+    if (tid < 64) {   // wave 0: exclusive scan of the key counts of the tile's words
+        const uint32_t nwords = (n + 31) / 32;
+        const uint32_t pc = tid < nwords ? (uint32_t)__popc(pf.bits) : 0u;
+        const uint32_t inc = __ockl_wfscan_add_u32(pc, true);
+        if (tid < nwords) L.wrank[tid] = inc - pc;
+    }
+}
+
+// hist: the tile's LDS histogram, symbol c at hist[c·hp + hslot(·)]; cols: LDS [ncol][6].
+template <class EL>
+__device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t tile, uint32_t a, uint32_t n,
+                                                   const TileIns &ti, const uint32_t *hist, uint32_t nwp,
+                                                   const uint32_t *cols, EL &L) {
+    const int T = d.n_thr;
+    const uint32_t F = (uint32_t)d.fill_len;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, row = lane >> 4;
+    const uint32_t ncol = ti.cb1 - ti.cb0;
+    const bool has_ins = ti.khi > ti.klo && !(d.ablate & 0x200);
+    const uint32_t nchunk = (n + 2 * WG - 1) / (2 * WG);
+    uint8_t *const obase = d.out + body_slot(d, a, ti.cb0);
+    const uint64_t ostride = body_stride(d);
+    // count of symbol c at tile position q (columns: key positions)
+    const uint32_t hp = 17 * nwp;   // histogram words per symbol (hslot layout)
+    auto hget = [&](uint32_t q, uint32_t c) { return hist_get(hist + c * hp, q); };
+    for (int t0 = 0; t0 < T; t0 += VT_TMAX) {
+        const int tn = min(VT_TMAX, T - t0);
+        double tmax = L.thr[t0];
+        bool fastok = true;   // every threshold of the pass in (0, inf): x = t·cov > 0 for cov ≥ 1
+#pragma unroll
+        for (int u = 0; u < VT_TMAX; u++)
+            if (u < tn) {
+                const double th = L.thr[t0 + u];
+                fastok = fastok && th > 0.0 && th < __builtin_inf();
+                tmax = max(tmax, th);
+            }
+        uint64_t base[VT_TMAX] = {};   // tile body bytes of the previous chunks, per threshold
+        for (uint32_t ch = 0; ch < nchunk; ch++) {
+            // ---- A: column votes (once per pass) and position votes
+            uint64_t cs[VT_TMAX] = {};                      // Σ cov over emitted insertion chars (:385)
+            uint32_t ec[VT_TMAX] = {}, nc[VT_TMAX] = {};    // emitted / error insertion chars (wave)
+            if (ch == 0) {
+                for (uint32_t i = tid; i < (uint32_t)VT_ACC; i += WG) L.acc[i] = 0;
+                if (has_ins) {
+                    for (uint32_t jb = 0; jb < ncol; jb += WG) {   // uniform trip count (ballots)
+                        const uint32_t j = jb + tid;
+                        uint32_t cov = 0, word = 0x2D2D2D2Du;   // '-': never emitted
+                        bool kc = false;
+                        if (j < ncol) {
+                            const uint32_t kq = L.key[L.colkey[j]].x - a;
+#pragma unroll
+                            for (uint32_t c = 0; c < NSYM; c++) cov += hget(kq, c);
+                            kc = cov > 0 && (int64_t)cov >= (int64_t)d.min_depth;   // key called (:356-358)
+                            if (kc) {
+                                const uint32_t m = column_masks(cols + (size_t)j * NSYM, cov, &L.thr[t0], tn);
+                                word = 0;
+#pragma unroll
+                                for (int u = 0; u < VT_TMAX; u++) word |= (uint32_t)L.amb[(m >> (8 * u)) & 63u] << (8 * u);
+                            }
+                            L.vchr[j] = word;
+                        }
+#pragma unroll
+                        for (int u = 0; u < VT_TMAX; u++) {
+                            const uint32_t ic = (word >> (8 * u)) & 0xFFu;
+                            const bool em = kc && ic != '-' && ic != 0xFFu;
+                            ec[u] += (uint32_t)__popcll(__ballot(em));
+                            nc[u] += (uint32_t)__popcll(__ballot(kc && ic == 0xFFu));
+                            cs[u] += em ? cov : 0u;
+                        }
+                    }
+                }
+            }
+            const uint32_t wd = 16 * ch + (tid >> 4), i16 = tid & 15;   // word, lane in its row
+            const uint32_t q0 = 32 * wd + i16;                         // positions q0, q0 + 16
+            Pos P[2];
+            {
+                const uint32_t s = hslot(16 * wd + i16);
+#pragma unroll
+                for (uint32_t c = 0; c < NSYM; c++) {
+                    const uint32_t h = wd < nwp ? hist[c * hp + s] : 0u;
+                    P[0].c[c] = h & 0xFFFFu;
+                    P[1].c[c] = h >> 16;
+                }
+            }
+#pragma unroll
+            for (int v = 0; v < 2; v++) {
+                P[v].in = q0 + 16 * v < n;
+                pos_vote_fast(P[v], d.min_depth, tmax, fastok);
+            }
+            if (__ballot(P[0].slow || P[1].slow)) {   // a tie or a split vote in this wave
+                pos_vote_slow(P[0], L, t0, tn);
+                pos_vote_slow(P[1], L, t0, tn);
+            }
+            S2C_STAMP(d, 3);
+            lds_sync();   // (1) vote chars of the columns, zeroed statistics
+            S2C_STAMP(d, 4);
+            // ---- B: body lengths, row scans, wave totals, statistics
+            const uint32_t bw = (has_ins && wd < nwp) ? L.bits[wd] : 0u;
+            uint32_t slot[2];
+            bool hk[2];
+            uint32_t e02[2] = {0, 0}, e13[2] = {0, 0};
+#pragma unroll
+            for (int v = 0; v < 2; v++) {
+                const uint32_t b = i16 + 16 * v;   // bit of the position in its word
+                hk[v] = P[v].called && ((bw >> b) & 1u);
+                slot[v] = hk[v] ? L.wrank[wd] + (uint32_t)__popc(bw & ((1u << b) - 1u)) : 0u;
+                if (hk[v]) {
+                    const uint4 kr = L.key[slot[v]];
+                    for (uint32_t c = 0; c < kr.z; c++) emitted4(L.vchr[kr.y - ti.cb0 + c], e02[v], e13[v]);
+                }
+            }
+            uint32_t off[VT_TMAX][2];
+            const uint32_t lin0 = P[0].in ? (P[0].called ? 1u : F) : 0u, lin1 = P[1].in ? (P[1].called ? 1u : F) : 0u;
+#pragma unroll
+            for (int u = 0; u < VT_TMAX; u++) {
+                if (u >= tn) continue;
+                const uint32_t l0 = lin0 + em_of(e02[0], e13[0], u), l1 = lin1 + em_of(e02[1], e13[1], u);
+                const uint32_t p = l0 | (l1 << 16);   // ≤ 16·64 + ICOL per row half: no carry
+                const uint32_t incl = row_scan(p), excl = incl - p;
+                const uint32_t r0 = __builtin_amdgcn_readlane(incl, 15), r1 = __builtin_amdgcn_readlane(incl, 31);
+                const uint32_t r2 = __builtin_amdgcn_readlane(incl, 47), r3 = __builtin_amdgcn_readlane(incl, 63);
+                const uint32_t w0 = (r0 & 0xFFFFu) + (r0 >> 16), w1 = (r1 & 0xFFFFu) + (r1 >> 16);
+                const uint32_t w2 = (r2 & 0xFFFFu) + (r2 >> 16), w3 = (r3 & 0xFFFFu) + (r3 >> 16);
+                // this row's offset in the wave and its lo-half total: selects, no branches
+                const uint32_t rowoff = (row > 0 ? w0 : 0u) + (row > 1 ? w1 : 0u) + (row > 2 ? w2 : 0u);
+                uint32_t rt = r3;
+                rt = row == 2 ? r2 : rt;
+                rt = row == 1 ? r1 : rt;
+                rt = row == 0 ? r0 : rt;
+                const uint32_t rowlo = rt & 0xFFFFu;
+                off[u][0] = rowoff + (excl & 0xFFFFu);
+                off[u][1] = rowoff + rowlo + (excl >> 16);
+                if (lane == 0) L.fsum[u][wv] = w0 + w1 + w2 + w3;
+            }
+            {   // statistics of this chunk's positions (and of the pass's columns, chunk 0)
+                const uint32_t sc = wave_sum(P[0].cov + P[1].cov);   // ≤ 128 · 6 · 2^16 < 2^32
+                const uint32_t nunc = (uint32_t)__popcll(__ballot(P[0].in && !P[0].called)) +
+                                      (uint32_t)__popcll(__ballot(P[1].in && !P[1].called));
+                uint32_t nd[VT_TMAX], ne[VT_TMAX];
+                uint64_t scs[VT_TMAX];
+#pragma unroll
+                for (int u = 0; u < VT_TMAX; u++) {
+                    nd[u] = ne[u] = 0;
+                    scs[u] = 0;
+                    if (u >= tn) continue;
+#pragma unroll
+                    for (int v = 0; v < 2; v++) {
+                        const uint32_t ch8 = (P[v].chars >> (8 * u)) & 0xFFu;
+                        nd[u] += (uint32_t)__popcll(__ballot(P[v].called && ch8 != '-'));
+                        ne[u] += (uint32_t)__popcll(__ballot(P[v].called && ch8 == 0xFFu));
+                    }
+                    if (ch == 0 && has_ins) scs[u] = wave_sum(cs[u]);
+                }
+                if (lane == 0) {
+                    atomicAdd(&L.acc[0], (unsigned long long)sc);
+#pragma unroll
+                    for (int u = 0; u < VT_TMAX; u++) {
+                        if (u >= tn) continue;
+                        unsigned long long *at = L.acc + 1 + 4 * u;
+                        atomicAdd(&at[0], (unsigned long long)(nd[u] + (uint64_t)d.fill_nondash * nunc));
+                        if (ne[u] + nc[u]) atomicAdd(&at[1], (unsigned long long)(ne[u] + nc[u]));
+                        if (ec[u]) {
+                            atomicAdd(&at[2], (unsigned long long)scs[u]);
+                            atomicAdd(&at[3], (unsigned long long)ec[u]);
+                        }
+                    }
+                }
+            }
+            S2C_STAMP(d, 5);
+            lds_sync();   // (2) wave totals, statistics
+            S2C_STAMP(d, 8);
+            // ---- C: body bytes (:350-389): char, then the key's emitted insertion chars; fill
+#pragma unroll
+            for (int u = 0; u < VT_TMAX; u++) {
+                if (u >= tn) continue;
+                uint32_t wofs = 0, tot = 0;
+#pragma unroll
+                for (uint32_t k = 0; k < WG / 64; k++) {
+                    const uint32_t x = L.fsum[u][k];
+                    wofs += k < wv ? x : 0u;
+                    tot += x;
+                }
+                uint8_t *const ob = obase + (size_t)(t0 + u) * ostride + base[u];
+#pragma unroll
+                for (int v = 0; v < 2; v++) {
+                    if (!P[v].in) continue;
+                    uint32_t o = wofs + off[u][v];
+                    if (!P[v].called) {   // fill (:356-359)
+                        if (F <= (uint32_t)FILL_LDS) {
+                            for (uint32_t f = 0; f < F; f++) ob[o + f] = L.fill[f];
+                        } else {   // long -f strings from HBM (rare)
+                            for (uint32_t f = 0; f < F; f++) ob[o + f] = d.fill[f];
+                        }
+                        continue;
+                    }
+                    ob[o++] = (uint8_t)(P[v].chars >> (8 * u));
+                    if (hk[v]) {
+                        const uint4 kr = L.key[slot[v]];
+                        for (uint32_t c = 0; c < kr.z; c++) {
+                            const uint32_t ic = (L.vchr[kr.y - ti.cb0 + c] >> (8 * u)) & 0xFFu;
+                            if (ic != '-' && ic != 0xFFu) ob[o++] = (uint8_t)ic;
+                        }
+                    }
+                }
+                base[u] += tot;
+            }
+            S2C_STAMP(d, 9);
+            if (ch + 1 == nchunk && tid < (uint32_t)tn) {   // tile statistics (:352-397)
+                uint64_t bl = 0;
+#pragma unroll
+                for (int u = 0; u < VT_TMAX; u++) bl = (uint32_t)u == tid ? base[u] : bl;
+                const unsigned long long *at = L.acc + 1 + 4 * tid;
+                const size_t j = (size_t)(t0 + tid) * d.n_blocks + tile;
+                uint64_t *st = d.tile_stats + j * 4;
+                st[0] = L.acc[0] + at[2];   // sumcov: positions + cov per insertion char
+                st[1] = bl;                 // len
+                st[2] = at[0] + at[3];      // non-'-' chars (insertion chars are never '-')
+                st[3] = at[1];              // vote errors (KeyError, :367/:381)
+                d.blk_len[j] = bl;
+            }
+            if (ch + 1 < nchunk || t0 + VT_TMAX < T) lds_sync();   // (3) wsum / acc / vchr reused
+        }
+    }
+    S2C_STAMP(d, 6);
+    S2C_STAMP(d, 7);
+}
+
 // One workgroup per work item = (tile [a,b) of ≤ TW = 32·NWP positions, chunk k).  Lane
 // L owns 32-position word w = L mod NWP of the tile and lane group g = L / NWP (G = 256/NWP
 // lanes per word).  The word's seqout records [wrec[W], wrec[W+1]) are cut into chunks of
@@ -704,10 +1042,10 @@ __device__ __forceinline__ uint32_t hist_get(const uint32_t *h, uint32_t q) {
 // columns, vote, statistics), its event/key records prefetched under the count stream; a
 // deep tile's chunks add their histograms into HBM for k_consensus.
 template <int NWP>
-__global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_pileup(const s2c_dev d) {
     constexpr int G = WG / NWP, TW = NWP * 32, HP = TW / 2 + TW / 32;
     // LDS insertion columns: ≤ 40 KB of LDS in all (4 workgroups per CU) at 512 positions
-    constexpr uint32_t ICOL = NWP <= 16 ? 640 : (NWP == 32 ? 448 : 192);
+    constexpr uint32_t ICOL = S2C_LDS_COLS(NWP);
     __shared__ uint32_t hist[NSYM][HP];
     __shared__ uint32_t cols[ICOL * NSYM];
     __shared__ EpiLds<ICOL> L;
@@ -722,7 +1060,8 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
     const uint4 itv = ((const uint4 *)d.items)[item];
     const uint32_t a = uni(itv.x), b = uni(itv.y), chunk = uni(itv.z), tile = uni(itv.w);
     const uint32_t *blk = d.blocks + (size_t)tile * S2C_BLOCK_WORDS;
-    const uint32_t deep = uni(blk[3]);
+    const uint32_t flags = uni(blk[3]);
+    const bool deep = (flags & S2C_TILE_DEEP) != 0;
     const TileIns ti = tile_ins(blk);
     const uint32_t n = b - a;
     const uint32_t ws = 32u * w;                  // word start, tile-relative
@@ -734,10 +1073,15 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
         r0 = (uint32_t)min((uint64_t)we, (uint64_t)wb + (uint64_t)chunk * CH);
         r1 = (uint32_t)min((uint64_t)we, (uint64_t)r0 + CH);
     }
-    const bool finish = !deep && !(d.ablate & 4);
+    // the tile's whole depth is in this item and its insertion keys / columns fit the LDS:
+    // finished here by the epilogue (else its counts go to HBM for k_consensus)
+    const bool finish = flags == 0 && !(d.ablate & 4);
+    const bool fastp = finish;
     Prefetch pf;   // epilogue records, in flight under the count stream
     if (finish) prefetch_load(d, a, n, ti, pf);
     for (uint32_t i = tid; i < NSYM * (uint32_t)HP; i += WG) (&hist[0][0])[i] = 0;
+    if (fastp)
+        for (uint32_t i = tid; i < (ti.cb1 - ti.cb0) * NSYM; i += WG) cols[i] = 0;
     lds_sync();
     S2C_STAMP(d, 1);
     uint32_t V[NCTR][8];
@@ -774,6 +1118,7 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
     if (t < e0) load8(P, t, e0);
     __builtin_amdgcn_sched_barrier(0);
     if (finish) prefetch_store(d, L, n, pf);   // their loads were issued before P's
+    if (fastp) fast_prologue(d, L, cols, ti, n, pf);
     if (t < e0) {
         // two groups of 8 per trip (one 16-record carry-save step), the next group always
         // in flight while one is counted.  sched_barrier keeps each group's loads issued
@@ -829,10 +1174,13 @@ __global__ __launch_bounds__(WG) void k_pileup(const s2c_dev d) {
     lds_sync();
     S2C_STAMP(d, 2);
     if (finish) {   // the tile's whole depth is here: finish it now
-        tile_finish<ICOL>(d, tile, a, n, ti, [&](uint32_t q, uint32_t c) { return hist_get(hist[c], q); }, cols, L);
+        // diagnostic 0x1000: the same epilogue code runs twice (phase stamps of the warm run)
+        const int reps = (d.ablate & 0x1000) ? 2 : 1;
+#pragma nounroll
+        for (int rep = 0; rep < reps; rep++) tile_epilogue_fast(d, tile, a, n, ti, &hist[0][0], NWP, cols, L);
     } else {
-        // deep tile: this chunk's counts → HBM (symbol-major, coalesced atomics); with the
-        // diagnostic flag 4 every tile stores its counts instead of voting (parity tests)
+        // deep tile: this chunk's counts → HBM (symbol-major, coalesced atomics); a general
+        // tile's (and, with the diagnostic flag 4, every tile's) counts: plain stores
         for (uint32_t q = tid; q < n; q += WG)
 #pragma unroll
             for (uint32_t c = 0; c < NSYM; c++) {

@@ -1,7 +1,8 @@
 """Phase timeline of k_pileup (diagnostic): per work item, s_memrealtime stamps (100 MHz)
 at 0 start, 1 prologue done (after the histogram-zeroing barrier), 2 counting + flush done,
-3 insertion columns counted, 4 insertion vote done, 5 position vote done, 6 tile totals
-stored, 7 end; 8-10 inside the column-parallel insertion vote.  Prints, per phase, the distribution over work items of the time since
+then in the fast epilogue (last chunk / pass): 3 phase A (votes) done, 4 after its barrier,
+5 phase B (lengths, scans, statistics) done, 8 after its barrier, 9 phase C (body bytes)
+done, 6 tile statistics stored, 7 end.  Prints, per phase, the distribution over work items of the time since
 the earliest start (µs) and of the phase's own duration.
 
     python scripts/phases.py [workload] [extra_ablate_bits]
@@ -32,23 +33,20 @@ def main():
     ws.consensus()
     torch.cuda.synchronize()
     ws.dev.ablate = 0
-    ws.dev.ablate = 0
     ts = ws.counts[: ni * 128].view(torch.int64).cpu().numpy().reshape(ni, 16).astype(np.float64) / 100.0  # µs
     t0 = ts[:, 0].min()
     rel = ts - t0
-    names = ["start", "prologue", "count+flush", "ins count", "ins vote", "pos vote", "totals", "end"]
+    # stamp order of the fast epilogue (k_pileup's common case)
+    order = [(0, "start"), (1, "prologue"), (2, "count+flush"), (3, "A votes"), (4, "A barrier"),
+             (5, "B lengths+scan"), (8, "B barrier"), (9, "C bytes"), (6, "stats"), (7, "end")]
     print("items %d; kernel span %.2f us (earliest start -> latest end)" % (ni, rel[:, 7].max()))
-    for k, nm in enumerate(names):
+    prev = None
+    for k, nm in order:
         col = rel[:, k]
-        dur = rel[:, k] - rel[:, k - 1] if k else col
-        print("%-12s at  med %6.2f p90 %6.2f max %6.2f | dur med %6.2f p90 %6.2f max %6.2f" % (
+        dur = col - rel[:, prev] if prev is not None else col
+        print("%-16s at  med %6.2f p90 %6.2f max %6.2f | dur med %6.2f p90 %6.2f max %6.2f" % (
             nm, np.median(col), np.percentile(col, 90), col.max(), np.median(dur), np.percentile(dur, 90), dur.max()))
-    extra_names = {8: "col pass start", 9: "col votes (thread 0)", 10: "col votes synced"}
-    for k, nm in extra_names.items():
-        col = rel[:, k]
-        ok = ts[:, k] > 0
-        if ok.any():
-            print("%-20s at med %6.2f (items %d)" % (nm, np.median(col[ok]), ok.sum()))
+        prev = k
 
 
 if __name__ == "__main__":

@@ -50,7 +50,7 @@ def model_counts(hb, block=1 << 18):
 
 def check_plan(hb):
     """Every real position is owned by exactly one tile; a tile's items are chunks
-    0..nch-1 whose record ranges cover every word of the tile; deep = nch > 1."""
+    0..nch-1 whose record ranges cover every word of the tile; deep (flag bit 0) = nch > 1."""
     Lp = hb.info.padded_len
     own = np.zeros(Lp, dtype=np.int64)
     wrec = hb.wrec.astype(np.int64)
@@ -63,7 +63,7 @@ def check_plan(hb):
     for t, (a, b, ref, deep) in enumerate(hb.blocks[:, :4].astype(np.int64)):
         cs = sorted(chunks[t])
         assert cs == list(range(len(cs))), "tile %d chunks %r" % (t, cs)
-        assert bool(deep) == (len(cs) > 1)
+        assert bool(deep & 1) == (len(cs) > 1)
         assert a % 32 == 0
         words = np.arange(a // 32, (b + 31) // 32)
         assert (wrec[words + 1] - wrec[words]).max(initial=0) <= len(cs) * ch
@@ -172,7 +172,7 @@ def model_pipeline(hb, thresholds, min_depth=1, fill=b"-"):
                     continue
                 ch = _vote([int(x) for x in counts[:, p]], cv, t)
                 nerr += ch == 0xFF
-                buf.append(ch if ch != 0xFF else 63)
+                buf.append(ch)   # 0xFF at a vote error (the run raises KeyError; bytes unused)
                 emitted = 0
                 for col in cols.get(p, []):
                     v = list(col)

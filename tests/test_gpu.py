@@ -54,7 +54,7 @@ def test_pileup_counts_equal_batch_model(name, over):
         a, L = int(hb.ref_off[r]), int(hb.ref_len[r])
         assert (got[:, a:a + L] == want[:, a:a + L]).all(), hb.names[r]
     if name.startswith("c4"):
-        assert (hb.blocks[:, 3] == 1).any(), "deep config must exercise chunked (atomic) tiles"
+        assert (hb.blocks[:, 3] & 1 == 1).any(), "deep config must exercise chunked (atomic) tiles"
 
 
 def _sha_files(files):
@@ -161,6 +161,14 @@ def test_sharded_on_device(world):
     ("c2", {"n_refs": 3, "depth": 30.0}, [0.1, 0.3, 0.5, 0.6, 0.8, 0.95], 25, b"Nn" * 50),
     # empty fill: uncalled positions write nothing
     ("c2", {"n_refs": 2, "depth": 30.0}, [0.5], 25, b""),
+    # thresholds outside (0, inf): the max-count shortcut is off, every vote in full
+    ("c2", {"n_refs": 2, "depth": 40.0}, [0.0, 0.5, 1.0, 2.0], 1, b"-"),
+    ("c2", {"n_refs": 2, "depth": 40.0}, [-0.5, float("inf"), 0.25], 1, b"?"),
+    # the longest -f kept in LDS and one byte more (HBM)
+    ("c2", {"n_refs": 2, "depth": 20.0}, [0.3, 0.7], 18, b"x" * 64),
+    ("c2", {"n_refs": 2, "depth": 20.0}, [0.3, 0.7], 18, b"y" * 65),
+    # low depth: ties and split votes everywhere (full closed form), 1-5 thresholds
+    ("c2", {"n_refs": 4, "depth": 3.0}, [0.2, 0.4, 0.6, 0.8, 1.0], 1, b"N"),
 ])
 def test_device_pipeline_equals_batch_model(name, over, thr, md, fill):
     """stats / block offsets / bytes of the HIP stages == the batch model (tests/batch_model.py)."""
@@ -172,6 +180,7 @@ def test_device_pipeline_equals_batch_model(name, over, thr, md, fill):
         ncol_tile.append(int(hb.ins_kcol[khi]) - int(hb.ins_kcol[klo]))
     if over.get("ins_max") == 60:
         assert max(ncol_tile) > 1024, "case must exercise the HBM insertion-column path"
+        assert (hb.blocks[:, 3] & 2 == 2).any(), "case must exercise general (k_consensus) tiles"
     if over.get("depth") == 9000.0:
         assert hb.info.n_deep > 0 and hb.info.n_keys > 0
     ws = _ws(hb, thr, min_depth=md, fill=fill)
