@@ -228,16 +228,33 @@ __device__ __forceinline__ TileIns tile_ins(const uint32_t *blk) {
 // Everything the epilogue reads lives in LDS (see vm_drain).
 template <uint32_t ICOL>   // LDS insertion columns of the kernel variant
 struct EpiLds {
+    static constexpr bool kEvents = true;
     uint4 ev[PF];                      // event records ins_ev[e0 .. e0+PF)
     uint4 key[PF];                     // key records ins_kinfo[klo .. klo+PF)
     double thr[THR_MAX];               // -c thresholds, CLI order
     unsigned long long acc[VT_ACC];
     uint64_t wsum[VT_TMAX][WG / 64];   // body-length scan: wave totals
-    uint32_t fsum[VT_TMAX][WG / 64];   // the same, fast epilogue
     uint32_t kcov[PF];                 // coverage of each key's position if called, else 0
     uint32_t bits[TILE_WORDS];         // key bitmap of the tile's words
     uint32_t wrank[TILE_WORDS];        // keys of the tile before each word
     uint16_t kem[VT_TMAX][PF];         // insertion chars emitted per key (this pass)
+    uint16_t colkey[ICOL];             // key slot of each tile column
+    uint32_t vchr[ICOL];               // vote chars of each tile column, 4 thresholds per word
+    uint8_t fill[FILL_LDS];
+    uint8_t amb[64];
+};
+// LDS of the fast epilogue (k_pileup): no event records (counted from registers in the
+// prologue), per-key emitted counts as u16 pairs
+template <uint32_t ICOL>
+struct FastLds {
+    static constexpr bool kEvents = false;
+    uint4 key[PF];                     // key records ins_kinfo[klo .. klo+PF)
+    double thr[THR_MAX];               // -c thresholds, CLI order
+    unsigned long long acc[VT_ACC];
+    alignas(16) uint32_t fsum[VT_TMAX][WG / 64];   // body-length scan: wave totals (one 16-B read)
+    uint32_t bits[TILE_WORDS];         // key bitmap of the tile's words
+    uint32_t wrank[TILE_WORDS];        // keys of the tile before each word
+    uint32_t kem2[2][PF];              // insertion chars emitted per key: u16 pairs (thresholds 0/2, 1/3)
     uint16_t colkey[ICOL];             // key slot of each tile column
     uint32_t vchr[ICOL];               // vote chars of each tile column, 4 thresholds per word
     uint8_t fill[FILL_LDS];
@@ -266,7 +283,7 @@ __device__ __forceinline__ void prefetch_load(const s2c_dev &d, uint32_t a, uint
 template <class EL>
 __device__ __forceinline__ void prefetch_store(const s2c_dev &d, EL &L, uint32_t n, const Prefetch &pf) {
     const uint32_t tid = threadIdx.x;
-    L.ev[tid] = pf.ev;
+    if constexpr (EL::kEvents) L.ev[tid] = pf.ev;
     L.key[tid] = pf.key;
     if (tid < (uint32_t)d.n_thr) L.thr[tid] = pf.thr;
     if (tid < (n + 31) / 32) L.bits[tid] = pf.bits;
@@ -784,6 +801,8 @@ __device__ __forceinline__ void fast_prologue(const s2c_dev &d, EL &L, uint32_t 
                                               uint32_t n, const Prefetch &pf) {
     const uint32_t tid = threadIdx.x;
     if (ti.khi <= ti.klo || (d.ablate & 0x200)) return;   // uniform
+    L.kem2[0][tid] = 0;   // (PF == WG) per-key emitted insertion chars of the first pass
+    L.kem2[1][tid] = 0;
     auto add_event = [&](const uint4 r) {   // :264-287 motif symbols into the key's columns
         uint32_t *cc = cols + (size_t)r.x * NSYM;
         for (uint32_t c = 0; c < r.y; c++) {
@@ -813,6 +832,34 @@ __device__ __forceinline__ void fast_prologue(const s2c_dev &d, EL &L, uint32_t 
     }
 }
 
+// Vote of one insertion column (:290-311) for the pass's thresholds: the '-' count is
+// cov − Σ column (:294, signed).  Shortcut as for positions when every count is ≥ 0.
+template <class EL>
+__device__ __forceinline__ uint32_t column_word(const uint32_t *col, uint32_t cov, const EL &L, int t0, int tn,
+                                                double tmax, bool fastok) {
+    uint32_t v[NSYM], tot = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < NSYM; c++) { v[c] = col[c]; tot += v[c]; }
+    const int64_t dash = (int64_t)cov - (int64_t)tot;   // the column's own '-' count is in the sum
+    if (fastok && dash >= 0 && cov < (1u << 28)) {
+        v[0] = (uint32_t)dash;
+        uint32_t kk[NSYM];
+#pragma unroll
+        for (uint32_t c = 0; c < NSYM; c++) kk[c] = (v[c] << 3) | c;
+        const uint32_t mk = max(max(max(kk[0], kk[1]), kk[2]), max(max(kk[3], kk[4]), kk[5]));
+        uint32_t m2 = 0;
+#pragma unroll
+        for (uint32_t c = 0; c < NSYM; c++) m2 = max(m2, kk[c] == mk ? 0u : kk[c]);
+        const uint32_t m1 = mk >> 3;
+        if ((m2 >> 3) < m1 && (double)m1 >= tmax * (double)cov) return sym_char(mk & 7u) * 0x01010101u;
+    }
+    const uint32_t m = column_masks(col, cov, &L.thr[t0], tn);
+    uint32_t word = 0;
+#pragma unroll
+    for (int u = 0; u < VT_TMAX; u++) word |= (uint32_t)L.amb[(m >> (8 * u)) & 63u] << (8 * u);
+    return word;
+}
+
 // hist: the tile's LDS histogram, symbol c at hist[c·hp + hslot(·)]; cols: LDS [ncol][6].
 template <class EL>
 __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t tile, uint32_t a, uint32_t n,
@@ -826,7 +873,6 @@ __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t ti
     const uint32_t nchunk = (n + 2 * WG - 1) / (2 * WG);
     uint8_t *const obase = d.out + body_slot(d, a, ti.cb0);
     const uint64_t ostride = body_stride(d);
-    // count of symbol c at tile position q (columns: key positions)
     const uint32_t hp = 17 * nwp;   // histogram words per symbol (hslot layout)
     auto hget = [&](uint32_t q, uint32_t c) { return hist_get(hist + c * hp, q); };
     for (int t0 = 0; t0 < T; t0 += VT_TMAX) {
@@ -840,10 +886,11 @@ __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t ti
                 fastok = fastok && th > 0.0 && th < __builtin_inf();
                 tmax = max(tmax, th);
             }
+        const bool more_pass = t0 + VT_TMAX < T;
         uint64_t base[VT_TMAX] = {};   // tile body bytes of the previous chunks, per threshold
         for (uint32_t ch = 0; ch < nchunk; ch++) {
             // ---- A: column votes (once per pass) and position votes
-            uint64_t cs[VT_TMAX] = {};                      // Σ cov over emitted insertion chars (:385)
+            uint32_t cs[VT_TMAX] = {};                      // Σ cov over emitted insertion chars (:385)
             uint32_t ec[VT_TMAX] = {}, nc[VT_TMAX] = {};    // emitted / error insertion chars (wave)
             if (ch == 0) {
                 for (uint32_t i = tid; i < (uint32_t)VT_ACC; i += WG) L.acc[i] = 0;
@@ -851,19 +898,22 @@ __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t ti
                     for (uint32_t jb = 0; jb < ncol; jb += WG) {   // uniform trip count (ballots)
                         const uint32_t j = jb + tid;
                         uint32_t cov = 0, word = 0x2D2D2D2Du;   // '-': never emitted
+                        uint32_t s = 0;
                         bool kc = false;
                         if (j < ncol) {
-                            const uint32_t kq = L.key[L.colkey[j]].x - a;
+                            s = L.colkey[j];
+                            const uint32_t kq = L.key[s].x - a;
 #pragma unroll
                             for (uint32_t c = 0; c < NSYM; c++) cov += hget(kq, c);
                             kc = cov > 0 && (int64_t)cov >= (int64_t)d.min_depth;   // key called (:356-358)
-                            if (kc) {
-                                const uint32_t m = column_masks(cols + (size_t)j * NSYM, cov, &L.thr[t0], tn);
-                                word = 0;
-#pragma unroll
-                                for (int u = 0; u < VT_TMAX; u++) word |= (uint32_t)L.amb[(m >> (8 * u)) & 63u] << (8 * u);
-                            }
+                            if (kc) word = column_word(cols + (size_t)j * NSYM, cov, L, t0, tn, tmax, fastok);
                             L.vchr[j] = word;
+                        }
+                        uint32_t e02 = 0, e13 = 0;
+                        if (kc) emitted4(word, e02, e13);
+                        if (e02 | e13) {   // rare: chars of this column are emitted
+                            atomicAdd(&L.kem2[0][s], e02);
+                            atomicAdd(&L.kem2[1][s], e13);
                         }
 #pragma unroll
                         for (int u = 0; u < VT_TMAX; u++) {
@@ -893,34 +943,34 @@ __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t ti
                 P[v].in = q0 + 16 * v < n;
                 pos_vote_fast(P[v], d.min_depth, tmax, fastok);
             }
-            if (__ballot(P[0].slow || P[1].slow)) {   // a tie or a split vote in this wave
+            const bool any_slow = __ballot(P[0].slow || P[1].slow) != 0;   // a tie or a split vote
+            if (any_slow) {
                 pos_vote_slow(P[0], L, t0, tn);
                 pos_vote_slow(P[1], L, t0, tn);
             }
             S2C_STAMP(d, 3);
-            lds_sync();   // (1) vote chars of the columns, zeroed statistics
+            lds_sync();   // (1) column vote chars, per-key emitted counts, zeroed statistics
             S2C_STAMP(d, 4);
             // ---- B: body lengths, row scans, wave totals, statistics
             const uint32_t bw = (has_ins && wd < nwp) ? L.bits[wd] : 0u;
-            uint32_t slot[2];
+            uint32_t slot[2], em02[2], em13[2];
             bool hk[2];
-            uint32_t e02[2] = {0, 0}, e13[2] = {0, 0};
 #pragma unroll
             for (int v = 0; v < 2; v++) {
                 const uint32_t b = i16 + 16 * v;   // bit of the position in its word
                 hk[v] = P[v].called && ((bw >> b) & 1u);
                 slot[v] = hk[v] ? L.wrank[wd] + (uint32_t)__popc(bw & ((1u << b) - 1u)) : 0u;
-                if (hk[v]) {
-                    const uint4 kr = L.key[slot[v]];
-                    for (uint32_t c = 0; c < kr.z; c++) emitted4(L.vchr[kr.y - ti.cb0 + c], e02[v], e13[v]);
-                }
+                em02[v] = hk[v] ? L.kem2[0][slot[v]] : 0u;
+                em13[v] = hk[v] ? L.kem2[1][slot[v]] : 0u;
             }
-            uint32_t off[VT_TMAX][2];
+            // lengths differ between thresholds only by emitted insertion chars
+            const bool multi = __ballot((em02[0] | em13[0] | em02[1] | em13[1]) != 0) != 0;
             const uint32_t lin0 = P[0].in ? (P[0].called ? 1u : F) : 0u, lin1 = P[1].in ? (P[1].called ? 1u : F) : 0u;
+            uint32_t off[VT_TMAX][2];
 #pragma unroll
             for (int u = 0; u < VT_TMAX; u++) {
-                if (u >= tn) continue;
-                const uint32_t l0 = lin0 + em_of(e02[0], e13[0], u), l1 = lin1 + em_of(e02[1], e13[1], u);
+                if (u >= tn || (u > 0 && !multi)) continue;
+                const uint32_t l0 = lin0 + em_of(em02[0], em13[0], u), l1 = lin1 + em_of(em02[1], em13[1], u);
                 const uint32_t p = l0 | (l1 << 16);   // ≤ 16·64 + ICOL per row half: no carry
                 const uint32_t incl = row_scan(p), excl = incl - p;
                 const uint32_t r0 = __builtin_amdgcn_readlane(incl, 15), r1 = __builtin_amdgcn_readlane(incl, 31);
@@ -933,29 +983,48 @@ __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t ti
                 rt = row == 2 ? r2 : rt;
                 rt = row == 1 ? r1 : rt;
                 rt = row == 0 ? r0 : rt;
-                const uint32_t rowlo = rt & 0xFFFFu;
                 off[u][0] = rowoff + (excl & 0xFFFFu);
-                off[u][1] = rowoff + rowlo + (excl >> 16);
-                if (lane == 0) L.fsum[u][wv] = w0 + w1 + w2 + w3;
+                off[u][1] = rowoff + (rt & 0xFFFFu) + (excl >> 16);
+                if (lane == 0) {
+                    const uint32_t wt = w0 + w1 + w2 + w3;
+                    if (multi) {
+                        L.fsum[u][wv] = wt;
+                    } else {
+#pragma unroll
+                        for (int x = 0; x < VT_TMAX; x++) L.fsum[x][wv] = wt;
+                    }
+                }
+            }
+            if (!multi) {
+#pragma unroll
+                for (int u = 1; u < VT_TMAX; u++) { off[u][0] = off[0][0]; off[u][1] = off[0][1]; }
             }
             {   // statistics of this chunk's positions (and of the pass's columns, chunk 0)
                 const uint32_t sc = wave_sum(P[0].cov + P[1].cov);   // ≤ 128 · 6 · 2^16 < 2^32
                 const uint32_t nunc = (uint32_t)__popcll(__ballot(P[0].in && !P[0].called)) +
                                       (uint32_t)__popcll(__ballot(P[1].in && !P[1].called));
                 uint32_t nd[VT_TMAX], ne[VT_TMAX];
-                uint64_t scs[VT_TMAX];
 #pragma unroll
                 for (int u = 0; u < VT_TMAX; u++) {
                     nd[u] = ne[u] = 0;
-                    scs[u] = 0;
                     if (u >= tn) continue;
+                    if (u > 0 && !any_slow) {   // the same chars for every threshold
+                        nd[u] = nd[0];
+                        ne[u] = ne[0];
+                        continue;
+                    }
 #pragma unroll
                     for (int v = 0; v < 2; v++) {
                         const uint32_t ch8 = (P[v].chars >> (8 * u)) & 0xFFu;
                         nd[u] += (uint32_t)__popcll(__ballot(P[v].called && ch8 != '-'));
                         ne[u] += (uint32_t)__popcll(__ballot(P[v].called && ch8 == 0xFFu));
                     }
-                    if (ch == 0 && has_ins) scs[u] = wave_sum(cs[u]);
+                }
+                uint64_t scs[VT_TMAX] = {};
+                if (ch == 0 && has_ins) {
+#pragma unroll
+                    for (int u = 0; u < VT_TMAX; u++)
+                        if (u < tn && ec[u]) scs[u] = wave_sum((uint64_t)cs[u]);
                 }
                 if (lane == 0) {
                     atomicAdd(&L.acc[0], (unsigned long long)sc);
@@ -976,31 +1045,34 @@ __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t ti
             lds_sync();   // (2) wave totals, statistics
             S2C_STAMP(d, 8);
             // ---- C: body bytes (:350-389): char, then the key's emitted insertion chars; fill
+            const bool any_fill = F > 0 && __ballot((P[0].in && !P[0].called) || (P[1].in && !P[1].called)) != 0;
 #pragma unroll
             for (int u = 0; u < VT_TMAX; u++) {
                 if (u >= tn) continue;
-                uint32_t wofs = 0, tot = 0;
-#pragma unroll
-                for (uint32_t k = 0; k < WG / 64; k++) {
-                    const uint32_t x = L.fsum[u][k];
-                    wofs += k < wv ? x : 0u;
-                    tot += x;
-                }
+                const uint4 fs = *(const uint4 *)&L.fsum[u][0];   // WG / 64 == 4 waves
+                const uint32_t tot = fs.x + fs.y + fs.z + fs.w;
+                const uint32_t wofs = (wv > 0 ? fs.x : 0u) + (wv > 1 ? fs.y : 0u) + (wv > 2 ? fs.z : 0u);
                 uint8_t *const ob = obase + (size_t)(t0 + u) * ostride + base[u];
+                const uint32_t o0 = wofs + off[u][0], o1 = wofs + off[u][1];
+                if (P[0].called) ob[o0] = (uint8_t)(P[0].chars >> (8 * u));
+                if (P[1].called) ob[o1] = (uint8_t)(P[1].chars >> (8 * u));
+                if (any_fill) {   // fill (:356-359)
 #pragma unroll
-                for (int v = 0; v < 2; v++) {
-                    if (!P[v].in) continue;
-                    uint32_t o = wofs + off[u][v];
-                    if (!P[v].called) {   // fill (:356-359)
+                    for (int v = 0; v < 2; v++) {
+                        if (!P[v].in || P[v].called) continue;
+                        const uint32_t o = v ? o1 : o0;
                         if (F <= (uint32_t)FILL_LDS) {
                             for (uint32_t f = 0; f < F; f++) ob[o + f] = L.fill[f];
                         } else {   // long -f strings from HBM (rare)
                             for (uint32_t f = 0; f < F; f++) ob[o + f] = d.fill[f];
                         }
-                        continue;
                     }
-                    ob[o++] = (uint8_t)(P[v].chars >> (8 * u));
-                    if (hk[v]) {
+                }
+                if (multi) {   // insertion chars after the key's char (:370-385)
+#pragma unroll
+                    for (int v = 0; v < 2; v++) {
+                        if (!em_of(em02[v], em13[v], u)) continue;
+                        uint32_t o = (v ? o1 : o0) + 1;
                         const uint4 kr = L.key[slot[v]];
                         for (uint32_t c = 0; c < kr.z; c++) {
                             const uint32_t ic = (L.vchr[kr.y - ti.cb0 + c] >> (8 * u)) & 0xFFu;
@@ -1009,6 +1081,10 @@ __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t ti
                     }
                 }
                 base[u] += tot;
+            }
+            if (ch + 1 == nchunk && more_pass) {   // next pass counts its emitted chars afresh
+                L.kem2[0][tid] = 0;
+                L.kem2[1][tid] = 0;
             }
             S2C_STAMP(d, 9);
             if (ch + 1 == nchunk && tid < (uint32_t)tn) {   // tile statistics (:352-397)
@@ -1024,7 +1100,7 @@ __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t ti
                 st[3] = at[1];              // vote errors (KeyError, :367/:381)
                 d.blk_len[j] = bl;
             }
-            if (ch + 1 < nchunk || t0 + VT_TMAX < T) lds_sync();   // (3) wsum / acc / vchr reused
+            if (ch + 1 < nchunk || more_pass) lds_sync();   // (3) fsum / acc / vchr / kem2 reused
         }
     }
     S2C_STAMP(d, 6);
@@ -1048,7 +1124,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     constexpr uint32_t ICOL = S2C_LDS_COLS(NWP);
     __shared__ uint32_t hist[NSYM][HP];
     __shared__ uint32_t cols[ICOL * NSYM];
-    __shared__ EpiLds<ICOL> L;
+    __shared__ FastLds<ICOL> L;
     const uint32_t tid = threadIdx.x;
     const uint32_t w = tid % NWP, g = tid / NWP;
     if (d.ablate & 0x800) return;   // diagnostic: empty kernel (launch cost)
