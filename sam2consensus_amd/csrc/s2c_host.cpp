@@ -679,6 +679,11 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
         int64_t maxw = 0;
         for (int64_t W = T.a >> 5; W < (T.b + 31) >> 5; W++)
             maxw = std::max<int64_t>(maxw, (int64_t)(b->wrec[W + 1] - b->wrec[W]));
+        // k_pileup addresses a tile's records with 31-bit byte offsets from its first
+        if ((int64_t)(b->wrec[(T.b + 31) >> 5] - b->wrec[T.a >> 5]) * 12 >= ((int64_t)1 << 31) - 65536) {
+            delete b;
+            return s2c_set_error(S2C_ERR_LIMIT, "more than 2 GB of seqout records in one tile");
+        }
         const int64_t nch = std::max<int64_t>(1, ceil_div(maxw, chunk));
         for (int64_t c = 0; c < nch; c++) {
             uint32_t it[S2C_ITEM_WORDS] = {(uint32_t)T.a, (uint32_t)T.b, (uint32_t)c, (uint32_t)t};

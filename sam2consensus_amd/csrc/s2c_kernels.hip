@@ -172,6 +172,8 @@ __device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70);
 
 extern "C" __device__ __attribute__((const)) unsigned long long __ockl_wfred_add_u64(unsigned long long);
 extern "C" __device__ unsigned int __ockl_wfscan_add_u32(unsigned int, bool);   // (x, inclusive)
+extern "C" __device__ unsigned int __ockl_wfred_max_u32(unsigned int);
+extern "C" __device__ unsigned int __ockl_wfred_min_u32(unsigned int);
 
 // Sum over the wave's active lanes, every lane gets it: the device library's DPP reduction
 // (row shifts / broadcasts in the VALU) — a butterfly of __shfl_xor is a dependent chain
@@ -621,8 +623,8 @@ constexpr uint32_t FLUSH_RECS = 248;     // records per lane between flushes: 31
 // 0 '-', 1 A, 2 C, 3 G, 4 N, 5 T, 7 = no entry).  Six masks are counted per record, each
 // one VALU op from the planes: O = p1|p2 (C,G,N,T,none), A = p0&~O, Y = p1&~p2 (C,G),
 // G = Y&p0, Z = p2&~p1 (N,T), T = Z&p0; at the flush '-' = n − O − A, C = Y − G,
-// N = Z − T, n = records the lane counted.  A slot past the chunk's end loads the all-zero
-// sentinel record recs[n_recs] (no mask set) and is not counted in n.
+// N = Z − T, n = records the lane counted.  A slot past the lane's range reads zeros (an
+// out-of-range buffer offset: no mask set) and is not counted in n.
 // Each counter is 8 bit-planes (bit b of the per-position count): ones, twos, fours, eights
 // from a Harley–Seal carry-save tree over 16 records (15 CSAs of 2 v_bitop3 each), bits
 // 4..7 a ripple counter of the sixteens.  32 positions per VALU op, ≈20 VALU per record.
@@ -658,6 +660,15 @@ __device__ __forceinline__ void close16(uint32_t (&C)[8], uint32_t t8a, uint32_t
         const uint32_t t = C[b] & t16;
         C[b] ^= t16;
         t16 = t;
+    }
+}
+// one weight-8 carry into plane C[3], rippled into C[4..7] (an odd last group of 8)
+__device__ __forceinline__ void close8(uint32_t (&C)[8], uint32_t t8) {
+#pragma unroll
+    for (int b = 3; b < 8; b++) {
+        const uint32_t t = C[b] & t8;
+        C[b] ^= t8;
+        t8 = t;
     }
 }
 // one group of 8 records → the six counters' weight-8 carries
@@ -713,6 +724,24 @@ __device__ __forceinline__ uint32_t hslot(uint32_t s) { return s + (s >> 4); }
 __device__ __forceinline__ uint32_t hist_get(const uint32_t *h, uint32_t q) {
     return (h[hslot(((q >> 5) << 4) | (q & 15))] >> ((q & 16) ? 16 : 0)) & 0xFFFFu;
 }
+// The histogram layout, HC copies (lane group g adds into copy g mod HC; one copy: the
+// same-word lanes of a wave serialize on their LDS atomics, but more copies cost more in
+// the epilogue's reads and in occupancy than they save — measured), copy stride CS words.
+template <int NWP>
+struct Hist {
+    static constexpr int HC = 1, HP = 17 * NWP, CS = NSYM * HP + 8;
+    // packed u16 pair word s (hslot index) of symbol c, summed over the copies (counts per
+    // position ≤ 248·G < 2^16: the halves never carry)
+    static __device__ __forceinline__ uint32_t word(const uint32_t *h, uint32_t c, uint32_t s) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < HC; k++) v += h[k * CS + c * HP + s];
+        return v;
+    }
+    static __device__ __forceinline__ uint32_t get(const uint32_t *h, uint32_t c, uint32_t q) {
+        return (word(h, c, hslot(((q >> 5) << 4) | (q & 15))) >> ((q & 16) ? 16 : 0)) & 0xFFFFu;
+    }
+};
 
 // ======================================================================= fast tile epilogue
 // The common case of k_pileup (columns in LDS, ≤ PF keys, -f ≤ FILL_LDS bytes).  The
@@ -860,11 +889,13 @@ __device__ __forceinline__ uint32_t column_word(const uint32_t *col, uint32_t co
     return word;
 }
 
-// hist: the tile's LDS histogram, symbol c at hist[c·hp + hslot(·)]; cols: LDS [ncol][6].
-template <class EL>
+// hist: the tile's LDS histogram (Hist<NWP> layout); cols: LDS [ncol][6].
+template <int NWP, class EL>
 __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t tile, uint32_t a, uint32_t n,
-                                                   const TileIns &ti, const uint32_t *hist, uint32_t nwp,
+                                                   const TileIns &ti, const uint32_t *hist,
                                                    const uint32_t *cols, EL &L) {
+    using H = Hist<NWP>;
+    constexpr uint32_t nwp = NWP;
     const int T = d.n_thr;
     const uint32_t F = (uint32_t)d.fill_len;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, row = lane >> 4;
@@ -873,8 +904,7 @@ __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t ti
     const uint32_t nchunk = (n + 2 * WG - 1) / (2 * WG);
     uint8_t *const obase = d.out + body_slot(d, a, ti.cb0);
     const uint64_t ostride = body_stride(d);
-    const uint32_t hp = 17 * nwp;   // histogram words per symbol (hslot layout)
-    auto hget = [&](uint32_t q, uint32_t c) { return hist_get(hist + c * hp, q); };
+    auto hget = [&](uint32_t q, uint32_t c) { return H::get(hist, c, q); };
     for (int t0 = 0; t0 < T; t0 += VT_TMAX) {
         const int tn = min(VT_TMAX, T - t0);
         double tmax = L.thr[t0];
@@ -933,7 +963,7 @@ __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t ti
                 const uint32_t s = hslot(16 * wd + i16);
 #pragma unroll
                 for (uint32_t c = 0; c < NSYM; c++) {
-                    const uint32_t h = wd < nwp ? hist[c * hp + s] : 0u;
+                    const uint32_t h = wd < nwp ? H::word(hist, c, s) : 0u;
                     P[0].c[c] = h & 0xFFFFu;
                     P[1].c[c] = h >> 16;
                 }
@@ -1120,13 +1150,17 @@ __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t ti
 template <int NWP>
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_pileup(const s2c_dev d) {
     constexpr int G = WG / NWP, TW = NWP * 32, HP = TW / 2 + TW / 32;
+    using H = Hist<NWP>;
+    static_assert(H::HP == HP, "histogram layout");
     // LDS insertion columns: ≤ 40 KB of LDS in all (4 workgroups per CU) at 512 positions
     constexpr uint32_t ICOL = S2C_LDS_COLS(NWP);
-    __shared__ uint32_t hist[NSYM][HP];
+    __shared__ __attribute__((aligned(16))) uint32_t hist[H::HC * H::CS];
     __shared__ uint32_t cols[ICOL * NSYM];
     __shared__ FastLds<ICOL> L;
     const uint32_t tid = threadIdx.x;
-    const uint32_t w = tid % NWP, g = tid / NWP;
+    // diagnostic 0x2000: word-major lanes (a wave holds whole words) instead of interleaved
+    const bool wmaj = (d.ablate & 0x2000) != 0;
+    const uint32_t w = wmaj ? tid / G : tid % NWP, g = wmaj ? tid % G : tid / NWP;
     if (d.ablate & 0x800) return;   // diagnostic: empty kernel (launch cost)
     S2C_STAMP(d, 0);
     if (tid < 64) L.amb[tid] = c_amb[tid];   // published by the barrier after the histogram zeroing
@@ -1155,7 +1189,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const bool fastp = finish;
     Prefetch pf;   // epilogue records, in flight under the count stream
     if (finish) prefetch_load(d, a, n, ti, pf);
-    for (uint32_t i = tid; i < NSYM * (uint32_t)HP; i += WG) (&hist[0][0])[i] = 0;
+    for (uint32_t i = tid; i < (uint32_t)(H::HC * H::CS) / 4; i += WG) ((uint4 *)hist)[i] = make_uint4(0, 0, 0, 0);
     if (fastp)
         for (uint32_t i = tid; i < (ti.cb1 - ti.cb0) * NSYM; i += WG) cols[i] = 0;
     lds_sync();
@@ -1167,14 +1201,30 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #pragma unroll
             for (int bb = 0; bb < 8; bb++) V[c][bb] = 0;
     };
-    const uint32_t sentinel = (uint32_t)d.n_recs;   // all-zero record
-    auto load8 = [&](uint32_t (&P)[8][3], uint32_t t, uint32_t e0) {
+    // The item's records through a buffer resource based at its first word's first record
+    // (uniform): a load's address = lane offset (VGPR) + group offset (SGPR) + record slot
+    // (immediate); a slot past the lane's range gets an out-of-range offset and the
+    // hardware returns zeros (no mask set: nothing counted).
+    const uint32_t rbase = uni(d.wrec[a >> 5]);
+    const uint64_t rbytes = ((uint64_t)d.n_recs + 1 - rbase) * 12;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(recs + 3 * (size_t)rbase), (short)0, (int)min(rbytes, (uint64_t)0x7FFF0000u), 0x00020000);
+    constexpr uint32_t OOR = 0x80000000u;   // an offset past any record
+    const uint32_t e0 = (d.ablate & 1) ? r0 : r1;   // diagnostic 1: no records
+    const uint32_t t = r0 + g;                      // the lane's first record
+    const uint32_t nrec = t < e0 ? (e0 - t + G - 1) / G : 0u;   // records ≡ g (mod G) in [r0, e0)
+    const uint32_t voff = nrec ? (t - rbase) * 12u : OOR;
+    const uint32_t ngrp = uni(__ockl_wfred_max_u32((nrec + 7) / 8));   // groups of 8, busiest lane
+    auto loadg = [&](uint32_t (&P)[8][3], uint32_t gi) {
+        const uint32_t so = gi * 96u * G;   // group gi: records 8·gi·G.. of the lane's stride
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-            const uint32_t i = t + u * G < e0 ? t + u * G : sentinel;
-            const uint32_t *src = recs + 3 * (size_t)i;
-#pragma unroll
-            for (int k = 0; k < 3; k++) P[u][k] = src[k];
+            // (the empty asm keeps the offset one register + an immediate: the compiler would
+            // otherwise hoist the eight sums out of the loop and spill them)
+            uint32_t vo = 8 * gi + u < nrec ? voff : OOR;
+            asm volatile("" : "+v"(vo));
+            const auto v = __builtin_amdgcn_raw_buffer_load_b96(rsrc, vo + (uint32_t)(u * 12 * G), so, 0);
+            P[u][0] = v[0]; P[u][1] = v[1]; P[u][2] = v[2];
         }
     };
     uint32_t sink = 0;   // diagnostic ablate&2: loads consumed without counting
@@ -1182,30 +1232,24 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #pragma unroll
         for (int u = 0; u < 8; u++) sink ^= P[u][0] ^ P[u][1] ^ P[u][2];
     };
-    // valid records of the group starting at t
-    auto nvalid = [&](uint32_t t, uint32_t e0) -> uint32_t {
-        return t < e0 ? min(8u, (e0 - t + G - 1) / G) : 0u;
-    };
     zeroV();
     // ---- count this word's records of the chunk (one flush: chunk ≤ 248·G, check_dev) ----
-    const uint32_t e0 = (d.ablate & 1) ? r0 : r1;
-    uint32_t t = r0 + g, nrec = 0;
     uint32_t P[8][3], Q[8][3];
-    if (t < e0) load8(P, t, e0);
+    if (ngrp > 0) loadg(P, 0);
     __builtin_amdgcn_sched_barrier(0);
     if (finish) prefetch_store(d, L, n, pf);   // their loads were issued before P's
     if (fastp) fast_prologue(d, L, cols, ti, n, pf);
-    if (t < e0) {
+    {
         // two groups of 8 per trip (one 16-record carry-save step), the next group always
-        // in flight while one is counted.  sched_barrier keeps each group's loads issued
-        // ahead of the other group's count (the scheduler otherwise sinks them next to
-        // their use to save registers).
+        // in flight while one is counted; an odd last group closes alone.  sched_barrier
+        // keeps each group's loads issued ahead of the other group's count (the scheduler
+        // otherwise sinks them next to their use to save registers).
         uint32_t ta[NCTR], tb[NCTR];
-        for (; t < e0; t += 16 * G) {
-            load8(Q, t + 8 * G, e0);
+        for (uint32_t gi = 0; gi < ngrp; gi += 2) {   // uniform trip count
+            loadg(Q, gi + 1);
             __builtin_amdgcn_sched_barrier(0);
             if (d.ablate & 2) sink8(P); else count8(V, P, ta);
-            load8(P, t + 16 * G, e0);
+            loadg(P, gi + 2);
             __builtin_amdgcn_sched_barrier(0);
             if (d.ablate & 2) {
                 sink8(Q);
@@ -1214,19 +1258,18 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             count8(V, Q, tb);
 #pragma unroll
             for (int c = 0; c < NCTR; c++) close16(V[c], ta[c], tb[c]);
-            nrec += nvalid(t, e0) + nvalid(t + 8 * G, e0);
         }
     }
     // ---- flush: counters → six symbol counts → LDS histogram ----
     if (active && !(d.ablate & 8)) {
-        uint32_t *h0 = &hist[0][0] + 17 * w;
+        uint32_t *h0 = hist + (g % H::HC) * H::CS + 17 * w;   // this lane group's copy
         auto add = [&](uint32_t sym, const uint32_t (&R)[8]) {
             uint32_t *hw = h0 + sym * HP;
 #pragma unroll
             for (int r = 0; r < 8; r++) {
                 const uint32_t lo = R[r] & 0x00FF00FFu, hi = (R[r] >> 8) & 0x00FF00FFu;
-                if (lo) atomicAdd(hw + r, lo);
-                if (hi) atomicAdd(hw + 8 + r, hi);
+                atomicAdd(hw + r, lo);
+                atomicAdd(hw + 8 + r, hi);
             }
         };
         const uint32_t nb = nrec * 0x01010101u;
@@ -1243,7 +1286,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             add(pr == 0 ? 1 : (pr == 1 ? 3 : 5), Y);
         }
     }
-    if (sink == 0x9E3779B9u) hist[0][0] = 1;   // keeps the ablation's loads alive
+    if (sink == 0x9E3779B9u) hist[0] = 1;   // keeps the ablation's loads alive
     // the count loop's last prefetch group is never consumed: drain it here (long landed),
     // or every later reuse of its registers would wait behind the epilogue's stores
     vm_drain();
@@ -1253,7 +1296,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
         // diagnostic 0x1000: the same epilogue code runs twice (phase stamps of the warm run)
         const int reps = (d.ablate & 0x1000) ? 2 : 1;
 #pragma nounroll
-        for (int rep = 0; rep < reps; rep++) tile_epilogue_fast(d, tile, a, n, ti, &hist[0][0], NWP, cols, L);
+        for (int rep = 0; rep < reps; rep++) tile_epilogue_fast<NWP>(d, tile, a, n, ti, hist, cols, L);
     } else {
         // deep tile: this chunk's counts → HBM (symbol-major, coalesced atomics); a general
         // tile's (and, with the diagnostic flag 4, every tile's) counts: plain stores
@@ -1261,7 +1304,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #pragma unroll
             for (uint32_t c = 0; c < NSYM; c++) {
                 uint32_t *dst = d.counts + (size_t)c * d.padded_len + a + q;
-                const uint32_t v = hist_get(hist[c], q);
+                const uint32_t v = H::get(hist, c, q);
                 if (deep) {
                     if (v) atomicAdd(dst, v);
                 } else {

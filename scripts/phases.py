@@ -47,6 +47,20 @@ def main():
         print("%-16s at  med %6.2f p90 %6.2f max %6.2f | dur med %6.2f p90 %6.2f max %6.2f" % (
             nm, np.median(col), np.percentile(col, 90), col.max(), np.median(dur), np.percentile(dur, 90), dur.max()))
         prev = k
+    # what the slow items have in common: records streamed, XCD (blockIdx mod 8), start time
+    items = hb.items.astype(np.int64)
+    wrec = hb.wrec.astype(np.int64)
+    recs = np.array([wrec[(b + 31) >> 5] - wrec[a >> 5] for a, b, _, _ in items])
+    cnt = rel[:, 2] - rel[:, 1]
+    print("count+flush vs records: corr %.2f; records med %d max %d" % (
+        np.corrcoef(recs, cnt)[0, 1], np.median(recs), recs.max()))
+    xcd = np.arange(ni) % 8
+    print("per XCD: median count+flush " + " ".join("%.2f" % np.median(cnt[xcd == x]) for x in range(8)))
+    print("per XCD: max end            " + " ".join("%.2f" % rel[xcd == x, 7].max() for x in range(8)))
+    slow = np.argsort(-rel[:, 7])[:8]
+    for i in slow:
+        print("  item %4d xcd %d recs %6d start %.2f prologue-end %.2f count %.2f end %.2f" % (
+            i, i % 8, recs[i], rel[i, 0], rel[i, 1], cnt[i], rel[i, 7]))
 
 
 if __name__ == "__main__":
