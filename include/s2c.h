@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define S2C_ABI_VERSION 3
+#define S2C_ABI_VERSION 4
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define S2C_OK            0
@@ -50,7 +50,7 @@ int s2c_layout(int64_t *out, int n);
 /* ---- constants shared with the kernels -------------------------------------------- */
 #define S2C_NSYM          6    /* symbols '-','A','C','G','N','T' — sorted() order (:367) */
 #define S2C_POS_ALIGN    64    /* each reference starts at a multiple of this global coordinate */
-#define S2C_ITEM_WORDS    4    /* u32 words per pileup work item {a, b, chunk, tile} */
+#define S2C_ITEM_WORDS    8    /* u32 words per pileup work item {a, b, chunk, tile, fix_off, x0, x1, 0} */
 #define S2C_BLOCK_WORDS  12    /* u32 words per tile {a, b, ref, flags, klo, khi, e0, e1, cb0, cb1, 0, 0} */
 #define S2C_TILE_DEEP     1    /* flags: the tile's records take several work items (HBM counts) */
 #define S2C_TILE_GENERAL  2    /* flags: more insertion columns / keys than k_pileup's LDS holds:
@@ -107,6 +107,8 @@ typedef struct {
     int64_t tile_max;          /* max positions of any tile (≤ 2048) */
     int64_t n_deep;            /* tiles voted by k_consensus: split over several work items
                                   (S2C_TILE_DEEP) or beyond k_pileup's LDS (S2C_TILE_GENERAL) */
+    int64_t n_exc;             /* seqout '-' / 'N' entries (kept out of the 2-bit records) */
+    int64_t n_fix;             /* u32 words of per-item A-placeholder counts */
 } s2c_batch_info;
 
 typedef struct {               /* host pointers into the batch (valid until s2c_batch_free) */
@@ -118,8 +120,16 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
     const uint32_t *rd_span;   /* [n_reads]   seqout length (bits 0-30); bit31 = '-' not counted (maxdel :210) */
     const uint32_t *ops;       /* [n_ops]     (len << 1) | cls, cls 0 = M/=/X, 1 = D/N/P */
     const uint32_t *wrec;      /* [padded_len/32 + 1] CSR: records of global word W = [wrec[W], wrec[W+1]) */
-    const uint32_t *recs;      /* [n_recs][3] bit-planes {p0,p1,p2} of the 32 positions' codes
-                                  (p2·4+p1·2+p0: 0 '-' 1 A 2 C 3 G 4 N 5 T, 7 = no entry) */
+    const uint32_t *recs;      /* [n_recs][2] bit-planes {b0, b1} of the 32 positions' bases
+                                  (b1·2+b0: 0 A, 1 C, 2 G, 3 T).  A position without an A/C/G/T
+                                  entry — outside the read piece, a '-' of a maxdel-dropped read
+                                  (:214-218), or a '-' / 'N' (those are in exc) — holds 0 (A) and
+                                  is subtracted again through fix */
+    const uint32_t *fix;       /* [n_fix] per work item (from item word 4), 16 u32 per word of its
+                                  tile: u32 i of word w = the A placeholders among the item's
+                                  records at tile positions 32w+i (low u16) and 32w+i+16 (high) */
+    const uint32_t *exc;       /* [n_exc] the counted seqout '-' and 'N' of each work item (item
+                                  words 5-6): (position − tile start) << 1 | is_N */
     const uint32_t *ins_key;   /* [n_keys]    global coordinate of each key (:74), ascending */
     const uint32_t *ins_koff;  /* [n_keys+1]  events of key k = [koff[k], koff[k+1]) (file order) */
     const uint32_t *ins_kcol;  /* [n_keys+1]  columns of key k = [kcol[k], kcol[k+1]) */
@@ -131,10 +141,12 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
     const uint32_t *ins_kinfo; /* [n_keys][4] {position, first column, columns, 0} */
     const uint32_t *ins_bits;  /* [padded_len/32] bit p: position p is a key */
     const uint32_t *ins_rank;  /* [padded_len/32+1] keys before 32-position word W */
-    const uint32_t *items;     /* [n_items][S2C_ITEM_WORDS] pileup work items */
-    const uint32_t *blocks;    /* [n_blocks][S2C_BLOCK_WORDS] tiles {g_begin, g_end, ref, deep, then the
+    const uint32_t *items;     /* [n_items][S2C_ITEM_WORDS] pileup work items {a, b, chunk, tile,
+                                  fix_off, x0, x1, 0}: tile [a, b), records chunk `chunk` of each
+                                  word, its placeholder words and '-'/'N' entries [x0, x1) */
+    const uint32_t *blocks;    /* [n_blocks][S2C_BLOCK_WORDS] tiles {g_begin, g_end, ref, flags, then the
                                   tile's keys [klo,khi), events [e0,e1), columns [cb0,cb1)} */
-    const uint32_t *deep;      /* [n_deep] indices of deep tiles */
+    const uint32_t *deep;      /* [n_deep] indices of the tiles k_consensus votes (flags != 0) */
 } s2c_batch_arrays;
 
 int  s2c_batch_info_get(const s2c_batch *b, s2c_batch_info *out);
@@ -181,11 +193,11 @@ int s2c_synth_write(const s2c_synth_spec *spec, const char *path, int64_t *n_rea
  * ====================================================================================== */
 typedef struct {
     /* ---- packed batch (device copies of s2c_batch_arrays) ---- */
-    const uint32_t *wrec, *recs;   /* word-major seqout records (s2c_batch_arrays); recs holds
-                                      n_recs + 1 records, the last all zero (sentinel) */
+    const uint32_t *wrec, *recs;   /* word-major seqout records (s2c_batch_arrays) */
+    const uint32_t *fix, *exc;     /* A-placeholder counts, '-'/'N' entries (s2c_batch_arrays) */
     const uint32_t *items, *blocks, *deep;
     const uint32_t *ins_ev, *ins_kinfo, *ins_bases, *ins_bits;   /* (s2c_batch_arrays) */
-    int64_t n_recs, chunk_recs, n_items, n_blocks, n_deep, n_keys, n_cols, padded_len;
+    int64_t n_recs, chunk_recs, n_items, n_blocks, n_deep, n_keys, n_cols, padded_len, n_exc;
     int32_t tile_max, n_refs;
 
     /* ---- options (:117-138) ---- */

@@ -74,7 +74,11 @@ class HostBatch:
         self.ops = _view(a.ops, i.n_ops, np.uint32)
         # word-major seqout records (what the pileup kernel reads)
         self.wrec = _view(a.wrec, i.padded_len // 32 + 1, np.uint32)
-        self.recs = _view(a.recs, 3 * i.n_recs, np.uint32).reshape(-1, 3)
+        self.recs = _view(a.recs, 2 * i.n_recs, np.uint32).reshape(-1, 2)
+        # per work item: A-placeholder counts (16 u32 u16-pairs per tile word) and the
+        # seqout '-'/'N' entries
+        self.fix = _view(a.fix, i.n_fix, np.uint32)
+        self.exc = _view(a.exc, i.n_exc, np.uint32)
         # insertion events grouped by key (keys ascending)
         nw = i.padded_len // 32
         self.ins_key = _view(a.ins_key, i.n_keys, np.uint32)

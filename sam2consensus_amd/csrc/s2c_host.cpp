@@ -174,6 +174,7 @@ struct s2c_batch {
     std::vector<int64_t> ref_len, ref_off, ref_reads;
     std::vector<uint32_t> rd_pos, rd_op, rd_span, ops;   // host-side read-piece table
     std::vector<uint32_t> wrec, recs;                     // word-major seqout windows
+    std::vector<uint32_t> fix, exc;                       // A placeholders, '-'/'N' entries
     std::vector<uint32_t> ins_key, ins_koff, ins_kcol, ins_off, ins_bases, ins_ekey, ins_bits, ins_rank;
     std::vector<uint32_t> ins_ev, ins_kinfo;             // device-side event / key records
     std::vector<uint32_t> items, blocks, deep;
@@ -590,9 +591,11 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
     }
 
     // ---- word-major seqout windows: one record per (piece, global 32-position word) ----
-    // record = 3 bit-planes of the codes of the word's 32 positions (code = p2·4+p1·2+p0:
-    // 0 '-', 1 A, 2 C, 3 G, 4 N, 5 T; 7 = no entry: outside the piece, or a '-' of a
-    // maxdel-dropped read, :214-218).  Grouped by word (CSR wrec), piece order inside.
+    // record = 2 bit-planes {b0, b1} of the word's 32 bases (b1·2+b0: 0 A, 1 C, 2 G, 3 T),
+    // grouped by word (CSR wrec), piece order inside.  A position with no A/C/G/T entry in
+    // the record — outside the piece, a '-' of a maxdel-dropped read (:214-218, not
+    // counted), or a seqout '-' / 'N' — holds 0 (A) and is counted in fix (subtracted from A
+    // on the device); a counted '-' / 'N' is also listed in exc (added to its symbol).
     const int64_t NW = Lpad / 32;
     b->wrec.assign(NW + 1, 0);
     uint64_t nrec = 0;
@@ -609,34 +612,6 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
     }
     for (int64_t W = 0; W < NW; W++) b->wrec[W + 1] += b->wrec[W];
     I.n_recs = (int64_t)nrec;
-    b->recs.resize(3 * nrec);
-    {
-        std::vector<uint32_t> cur(b->wrec.begin(), b->wrec.end() - 1);
-        for (int64_t i = 0; i < NP; i++) {
-            const int64_t span = p->p_span[i];
-            if (!span) continue;
-            const uint32_t *pw = &p->words[p->p_base[i]];   // piece planes + zero pad triple
-            const bool drop = p->p_drop[i] != 0;
-            const int64_t s0 = (int64_t)gstart[i];
-            for (int64_t W = s0 >> 5; W <= (s0 + span - 1) >> 5; W++) {
-                const int64_t o = 32 * W - s0;                    // seqout index of the word's first position
-                const int64_t qs = std::max<int64_t>(o, 0), bl = std::max<int64_t>(-o, 0);
-                const uint32_t *lo = pw + 3 * (qs >> 5), *hi = lo + 3;
-                const uint32_t sh = (uint32_t)(qs & 31);
-                uint32_t P[3];
-                for (int k = 0; k < 3; k++) {
-                    const uint64_t v = ((uint64_t)hi[k] << 32 | lo[k]) >> sh;
-                    P[k] = (uint32_t)v << bl;
-                }
-                const int64_t nv = std::min<int64_t>(span - qs, 32 - bl);
-                uint32_t valid = (nv >= 32 ? 0xFFFFFFFFu : ((1u << nv) - 1u)) << bl;
-                if (drop) valid &= P[0] | P[1] | P[2];
-                uint32_t *r = &b->recs[3 * (size_t)cur[W]++];
-                for (int k = 0; k < 3; k++) r[k] = (P[k] & valid) | ~valid;
-            }
-        }
-    }
-
     // ---- tiles (consensus/assembly blocks) and pileup work items ----
     std::vector<int64_t> ref_events(R, 0);
     for (int64_t i = 0; i < NP; i++) ref_events[p->p_ref[i]] += p->p_span[i];
@@ -686,7 +661,7 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
         }
         const int64_t nch = std::max<int64_t>(1, ceil_div(maxw, chunk));
         for (int64_t c = 0; c < nch; c++) {
-            uint32_t it[S2C_ITEM_WORDS] = {(uint32_t)T.a, (uint32_t)T.b, (uint32_t)c, (uint32_t)t};
+            uint32_t it[S2C_ITEM_WORDS] = {(uint32_t)T.a, (uint32_t)T.b, (uint32_t)c, (uint32_t)t};   // 4-6 below
             b->items.insert(b->items.end(), it, it + S2C_ITEM_WORDS);
         }
         uint32_t blk[S2C_BLOCK_WORDS] = {(uint32_t)T.a, (uint32_t)T.b, (uint32_t)T.ref, nch > 1 ? (uint32_t)S2C_TILE_DEEP : 0u};   // words 4-9 below
@@ -694,6 +669,99 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
     }
     I.n_items = (int64_t)(b->items.size() / S2C_ITEM_WORDS);
     I.n_blocks = (int64_t)(b->blocks.size() / S2C_BLOCK_WORDS);
+
+    // ---- seqout records, filled per work item: a position without an A/C/G/T entry is
+    //      counted in its item's placeholder words (fix) and a '-' / 'N' listed in its
+    //      item's entries (exc), so each item's counts are complete on their own (a deep
+    //      tile's chunks add into HBM; per-item placeholders fit u16: ≤ chunk_recs) ----
+    {
+        const int64_t NI = I.n_items;
+        std::vector<uint32_t> tile_of_word(NW, 0xFFFFFFFFu), first_item(b->blocks.size() / S2C_BLOCK_WORDS);
+        for (int64_t it = NI - 1; it >= 0; it--) first_item[b->items[S2C_ITEM_WORDS * it + 3]] = (uint32_t)it;
+        for (size_t t = 0; t < first_item.size(); t++) {
+            const uint32_t *blk = &b->blocks[t * S2C_BLOCK_WORDS];
+            for (uint32_t W = blk[0] >> 5; W < (blk[1] + 31) >> 5; W++) tile_of_word[W] = (uint32_t)t;
+        }
+        uint64_t fo = 0;
+        for (int64_t it = 0; it < NI; it++) {
+            uint32_t *iv = &b->items[S2C_ITEM_WORDS * it];
+            iv[4] = (uint32_t)fo;
+            fo += 16 * (uint64_t)((iv[1] + 31) / 32 - iv[0] / 32);
+        }
+        if (fo >= (1ull << 32)) {
+            delete b;
+            return s2c_set_error(S2C_ERR_LIMIT, "placeholder words exceed 2^32 (split the input)");
+        }
+        b->recs.resize(2 * nrec);
+        b->fix.assign(fo, 0);
+        std::vector<uint32_t> xitem;          // item of each '-' / 'N' entry
+        std::vector<uint32_t> xent;           // (position − tile start) << 1 | is_N
+        std::vector<uint32_t> cur(b->wrec.begin(), b->wrec.end() - 1);
+        const uint64_t CH = (uint64_t)I.chunk_recs;
+        for (int64_t i = 0; i < NP; i++) {
+            const int64_t span = p->p_span[i];
+            if (!span) continue;
+            const uint32_t *pw = &p->words[p->p_base[i]];   // piece planes + zero pad triple
+            const bool drop = p->p_drop[i] != 0;
+            const int64_t s0 = (int64_t)gstart[i];
+            for (int64_t W = s0 >> 5; W <= (s0 + span - 1) >> 5; W++) {
+                const int64_t o = 32 * W - s0;                    // seqout index of the word's first position
+                const int64_t qs = std::max<int64_t>(o, 0), bl = std::max<int64_t>(-o, 0);
+                const uint32_t *lo = pw + 3 * (qs >> 5), *hi = lo + 3;
+                const uint32_t sh = (uint32_t)(qs & 31);
+                uint32_t P[3];
+                for (int k = 0; k < 3; k++) {
+                    const uint64_t v = ((uint64_t)hi[k] << 32 | lo[k]) >> sh;
+                    P[k] = (uint32_t)v << bl;
+                }
+                const int64_t nv = std::min<int64_t>(span - qs, 32 - bl);
+                uint32_t valid = (nv >= 32 ? 0xFFFFFFFFu : ((1u << nv) - 1u)) << bl;
+                if (drop) valid &= P[0] | P[1] | P[2];
+                // 3-bit codes (p2·4+p1·2+p0: 0 '-' 1 A 2 C 3 G 4 N 5 T) → 2-bit bases
+                const uint32_t c2 = P[1] & ~P[0] & ~P[2], t5 = P[2] & P[0] & ~P[1], g3 = P[1] & P[0] & ~P[2];
+                const uint32_t dash = valid & ~(P[0] | P[1] | P[2]), en = valid & P[2] & ~(P[0] | P[1]);
+                const uint64_t ri = cur[W]++;
+                uint32_t *r = &b->recs[2 * ri];
+                r[0] = valid & (c2 | t5);
+                r[1] = valid & (g3 | t5);
+                const uint32_t t = tile_of_word[W];
+                const uint32_t *blk = &b->blocks[(size_t)t * S2C_BLOCK_WORDS];
+                const uint32_t item = first_item[t] + (uint32_t)((ri - b->wrec[W]) / CH);
+                const uint32_t *iv = &b->items[S2C_ITEM_WORDS * (size_t)item];
+                uint32_t ph = ~valid | dash | en;   // A placeholders
+                uint32_t *fw = &b->fix[iv[4] + 16 * (size_t)(W - (iv[0] >> 5))];
+                while (ph) {
+                    const int j = __builtin_ctz(ph);
+                    ph &= ph - 1;
+                    fw[j & 15] += (j & 16) ? 0x10000u : 1u;
+                }
+                uint32_t x = dash | en;
+                while (x) {
+                    const int j = __builtin_ctz(x);
+                    x &= x - 1;
+                    xitem.push_back(item);
+                    xent.push_back((uint32_t)((32 * W + j - blk[0]) << 1) | ((en >> j) & 1u));
+                }
+            }
+        }
+        // '-' / 'N' entries grouped by item (counting sort; item words 5-6 = the range)
+        if (xent.size() >= (1ull << 32) - 1) {
+            delete b;
+            return s2c_set_error(S2C_ERR_LIMIT, "more than 2^32 seqout '-'/'N' entries (split the input)");
+        }
+        std::vector<uint32_t> xo(NI + 1, 0);
+        for (uint32_t it : xitem) xo[it + 1]++;
+        for (int64_t it = 0; it < NI; it++) xo[it + 1] += xo[it];
+        b->exc.resize(xent.size());
+        std::vector<uint32_t> at(xo.begin(), xo.end() - 1);
+        for (size_t k = 0; k < xent.size(); k++) b->exc[at[xitem[k]]++] = xent[k];
+        for (int64_t it = 0; it < NI; it++) {
+            b->items[S2C_ITEM_WORDS * it + 5] = xo[it];
+            b->items[S2C_ITEM_WORDS * it + 6] = xo[it + 1];
+        }
+        I.n_exc = (int64_t)xent.size();
+        I.n_fix = (int64_t)fo;
+    }
 
     // ---- insertion events grouped by key (:256-294), keys sorted by position ----
     // Keys in [0, LN) only (negative keys are never emitted, :371).  Per key: its events
@@ -820,6 +888,8 @@ extern "C" int s2c_batch_arrays_get(const s2c_batch *b, s2c_batch_arrays *o) {
     o->ops = b->ops.data();
     o->wrec = b->wrec.data();
     o->recs = b->recs.data();
+    o->fix = b->fix.data();
+    o->exc = b->exc.data();
     o->ins_key = b->ins_key.data();
     o->ins_koff = b->ins_koff.data();
     o->ins_kcol = b->ins_kcol.data();

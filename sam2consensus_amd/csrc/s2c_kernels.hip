@@ -132,7 +132,9 @@ __device__ __forceinline__ uint32_t vote_mask_u32(const uint32_t (&c)[NSYM], con
 // epilogues wraps back to zero by itself.)
 __global__ __launch_bounds__(WG) void k_prep(const s2c_dev d) {
     const uint32_t t = d.deep[blockIdx.x];
-    const uint32_t a = d.blocks[(size_t)t * S2C_BLOCK_WORDS], n = d.blocks[(size_t)t * S2C_BLOCK_WORDS + 1] - a;
+    const uint32_t *blk = d.blocks + (size_t)t * S2C_BLOCK_WORDS;
+    if (!(blk[3] & S2C_TILE_DEEP)) return;   // a general tile's item stores all its counts
+    const uint32_t a = blk[0], n = blk[1] - a;
     for (uint32_t c = 0; c < NSYM; c++)
         for (uint32_t i = threadIdx.x; i < n; i += WG) d.counts[(size_t)c * d.padded_len + a + i] = 0;
 }
@@ -619,16 +621,17 @@ __device__ __forceinline__ void tile_finish(const s2c_dev &d, uint32_t tile, uin
 constexpr int TILE_MAX = S2C_TILE_MAX;   // positions per tile (≤ 64 words of 32)
 constexpr uint32_t FLUSH_RECS = 248;     // records per lane between flushes: 31 groups of 8 (≤ 255)
 
-// Bit-sliced counting.  A record holds 3 planes of its 32 positions' codes (p2·4+p1·2+p0:
-// 0 '-', 1 A, 2 C, 3 G, 4 N, 5 T, 7 = no entry).  Six masks are counted per record, each
-// one VALU op from the planes: O = p1|p2 (C,G,N,T,none), A = p0&~O, Y = p1&~p2 (C,G),
-// G = Y&p0, Z = p2&~p1 (N,T), T = Z&p0; at the flush '-' = n − O − A, C = Y − G,
-// N = Z − T, n = records the lane counted.  A slot past the lane's range reads zeros (an
-// out-of-range buffer offset: no mask set) and is not counted in n.
-// Each counter is 8 bit-planes (bit b of the per-position count): ones, twos, fours, eights
-// from a Harley–Seal carry-save tree over 16 records (15 CSAs of 2 v_bitop3 each), bits
-// 4..7 a ripple counter of the sixteens.  32 positions per VALU op, ≈20 VALU per record.
-constexpr int NCTR = 6;
+// Bit-sliced counting.  A record holds 2 planes of its 32 positions' bases (b1·2+b0: A C G
+// T; a position without a base — outside the piece, a '-' / 'N', a dropped '-' — holds A and
+// is taken off again by the host's placeholder counts, the '-'/'N' entries added on their
+// own).  Three masks are counted per record: X = b0 (C,T), Y = b1 (G,T), Z = b0&b1 (T); at
+// the flush T = Z, C = X − Z, G = Y − Z, A = n − X − Y + Z, n = records the lane counted.
+// A slot past the lane's range reads zeros (an out-of-range buffer offset) and is not
+// counted in n.  Each counter is 8 bit-planes (bit b of the per-position count): ones, twos,
+// fours, eights from a Harley–Seal carry-save tree over 16 records (15 CSAs of 2 v_bitop3
+// each), bits 4..7 a ripple counter of the sixteens.  32 positions per VALU op, ≈8 VALU per
+// record.
+constexpr int NCTR = 3;
 // carry-save adder a + b + c = 2h + l: two v_bitop3_b32 (truth tables 0x96 = xor3, 0xE8 =
 // majority; both symmetric, so operand order is free).  Written as asm because the
 // compiler shares a^b between the two and spends three ops.
@@ -671,27 +674,18 @@ __device__ __forceinline__ void close8(uint32_t (&C)[8], uint32_t t8) {
         t8 = t;
     }
 }
-// one group of 8 records → the six counters' weight-8 carries
-__device__ __forceinline__ void count8(uint32_t (&V)[NCTR][8], const uint32_t (&P)[8][3], uint32_t (&t8)[NCTR]) {
-    uint32_t m[8], y[8];
+// one group of 8 records → the three counters' weight-8 carries
+__device__ __forceinline__ void count8(uint32_t (&V)[NCTR][8], const uint32_t (&P)[8][2], uint32_t (&t8)[NCTR]) {
+    uint32_t m[8];
 #pragma unroll
-    for (int u = 0; u < 8; u++) m[u] = P[u][1] | P[u][2];
-    t8[0] = tree8(V[0], m);   // O
+    for (int u = 0; u < 8; u++) m[u] = P[u][0];
+    t8[0] = tree8(V[0], m);   // X = C|T
 #pragma unroll
-    for (int u = 0; u < 8; u++) m[u] = P[u][0] & ~(P[u][1] | P[u][2]);
-    t8[1] = tree8(V[1], m);   // A
+    for (int u = 0; u < 8; u++) m[u] = P[u][1];
+    t8[1] = tree8(V[1], m);   // Y = G|T
 #pragma unroll
-    for (int u = 0; u < 8; u++) y[u] = P[u][1] & ~P[u][2];
-    t8[2] = tree8(V[2], y);   // Y = C|G
-#pragma unroll
-    for (int u = 0; u < 8; u++) m[u] = y[u] & P[u][0];
-    t8[3] = tree8(V[3], m);   // G
-#pragma unroll
-    for (int u = 0; u < 8; u++) y[u] = P[u][2] & ~P[u][1];
-    t8[4] = tree8(V[4], y);   // Z = N|T
-#pragma unroll
-    for (int u = 0; u < 8; u++) m[u] = y[u] & P[u][0];
-    t8[5] = tree8(V[5], m);   // T
+    for (int u = 0; u < 8; u++) m[u] = P[u][0] & P[u][1];
+    t8[2] = tree8(V[2], m);   // Z = T
 }
 
 // 8 bit-planes of one counter → R[r] byte j = count of position 8j + r (8×8 bit transposes
@@ -1137,6 +1131,55 @@ __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t ti
     S2C_STAMP(d, 7);
 }
 
+// The host's corrections of a work item's records, added into its LDS histogram during the
+// prologue (the additions commute with the flush's: the packed u16 halves may borrow in
+// between, the final u32 words are exact), so the item's counts are complete on their own
+// (a deep tile's items then add true partial counts into HBM).  A placeholders: fix word
+// (w, i) = the count at tile positions 32w+i (low half) and 32w+i+16 (high half), the
+// histogram's own pairing, subtracted from A.  '-'/'N' entries: +1 on their symbol.
+template <int NWP>
+struct Corrections {
+    static constexpr int FN = NWP >= 16 ? NWP / 16 : 1;   // fix words per thread (16 per tile word)
+    static constexpr int XN = 4;                           // '-'/'N' entries per thread in registers
+    uint32_t fx[FN], xe[XN], x0, x1;
+    __device__ __forceinline__ void load(const s2c_dev &d, uint32_t n, uint32_t fix_off, uint32_t xa, uint32_t xb) {
+        const uint32_t tid = threadIdx.x;
+        x0 = xa;
+        x1 = xb;
+        const uint32_t nfix = 16u * ((n + 31) / 32);   // the tile's words
+#pragma unroll
+        for (int j = 0; j < FN; j++) {
+            const uint32_t i = tid + j * WG;
+            fx[j] = i < nfix ? d.fix[(size_t)fix_off + i] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < XN; j++) {
+            const uint32_t i = x0 + tid + j * WG;
+            xe[j] = i < x1 ? d.exc[i] : 0xFFFFFFFFu;
+        }
+    }
+    static __device__ __forceinline__ void add_entry(uint32_t *hist, uint32_t e) {
+        const uint32_t q = e >> 1, sym = (e & 1) ? 4u : 0u;   // 'N' : '-'
+        atomicAdd(hist + sym * (17 * NWP) + hslot(((q >> 5) << 4) | (q & 15)), (q & 16) ? 0x10000u : 1u);
+    }
+    __device__ __forceinline__ void apply(uint32_t *hist, const s2c_dev &d) const {
+        const uint32_t tid = threadIdx.x;
+#pragma unroll
+        for (int j = 0; j < FN; j++) {
+            const uint32_t i = tid + j * WG;
+            if (fx[j]) atomicSub(hist + 17 * NWP + 17 * (i >> 4) + (i & 15), fx[j]);   // symbol A
+        }
+#pragma unroll
+        for (int j = 0; j < XN; j++)
+            if (xe[j] != 0xFFFFFFFFu) add_entry(hist, xe[j]);
+        for (uint32_t i = x0 + tid + XN * WG; i < x1; i += WG) {   // beyond the registers (rare)
+            const uint32_t e = d.exc[i];
+            vm_drain();
+            add_entry(hist, e);
+        }
+    }
+};
+
 // One workgroup per work item = (tile [a,b) of ≤ TW = 32·NWP positions, chunk k).  Lane
 // L owns 32-position word w = L mod NWP of the tile and lane group g = L / NWP (G = 256/NWP
 // lanes per word).  The word's seqout records [wrec[W], wrec[W+1]) are cut into chunks of
@@ -1167,7 +1210,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const uint32_t *__restrict__ recs = d.recs;
     const uint32_t CH = (uint32_t)d.chunk_recs;
     const uint32_t item = blockIdx.x;   // grid = work items
-    const uint4 itv = ((const uint4 *)d.items)[item];
+    const uint4 itv = ((const uint4 *)d.items)[2 * (size_t)item];      // {a, b, chunk, tile}
+    const uint4 itc = ((const uint4 *)d.items)[2 * (size_t)item + 1];  // {fix_off, x0, x1, 0}
     const uint32_t a = uni(itv.x), b = uni(itv.y), chunk = uni(itv.z), tile = uni(itv.w);
     const uint32_t *blk = d.blocks + (size_t)tile * S2C_BLOCK_WORDS;
     const uint32_t flags = uni(blk[3]);
@@ -1189,6 +1233,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const bool fastp = finish;
     Prefetch pf;   // epilogue records, in flight under the count stream
     if (finish) prefetch_load(d, a, n, ti, pf);
+    Corrections<NWP> corr;   // A placeholders and '-'/'N' entries of this item's records
+    corr.load(d, n, uni(itc.x), uni(itc.y), uni(itc.z));
     for (uint32_t i = tid; i < (uint32_t)(H::HC * H::CS) / 4; i += WG) ((uint4 *)hist)[i] = make_uint4(0, 0, 0, 0);
     if (fastp)
         for (uint32_t i = tid; i < (ti.cb1 - ti.cb0) * NSYM; i += WG) cols[i] = 0;
@@ -1206,39 +1252,40 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     // (immediate); a slot past the lane's range gets an out-of-range offset and the
     // hardware returns zeros (no mask set: nothing counted).
     const uint32_t rbase = uni(d.wrec[a >> 5]);
-    const uint64_t rbytes = ((uint64_t)d.n_recs + 1 - rbase) * 12;
+    const uint64_t rbytes = ((uint64_t)d.n_recs - rbase) * 8;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(recs + 3 * (size_t)rbase), (short)0, (int)min(rbytes, (uint64_t)0x7FFF0000u), 0x00020000);
+        (void *)(recs + 2 * (size_t)rbase), (short)0, (int)min(rbytes, (uint64_t)0x7FFF0000u), 0x00020000);
     constexpr uint32_t OOR = 0x80000000u;   // an offset past any record
     const uint32_t e0 = (d.ablate & 1) ? r0 : r1;   // diagnostic 1: no records
     const uint32_t t = r0 + g;                      // the lane's first record
     const uint32_t nrec = t < e0 ? (e0 - t + G - 1) / G : 0u;   // records ≡ g (mod G) in [r0, e0)
-    const uint32_t voff = nrec ? (t - rbase) * 12u : OOR;
+    const uint32_t voff = nrec ? (t - rbase) * 8u : OOR;
     const uint32_t ngrp = uni(__ockl_wfred_max_u32((nrec + 7) / 8));   // groups of 8, busiest lane
-    auto loadg = [&](uint32_t (&P)[8][3], uint32_t gi) {
-        const uint32_t so = gi * 96u * G;   // group gi: records 8·gi·G.. of the lane's stride
+    auto loadg = [&](uint32_t (&P)[8][2], uint32_t gi) {
+        const uint32_t so = gi * 64u * G;   // group gi: records 8·gi·G.. of the lane's stride
 #pragma unroll
         for (int u = 0; u < 8; u++) {
             // (the empty asm keeps the offset one register + an immediate: the compiler would
             // otherwise hoist the eight sums out of the loop and spill them)
             uint32_t vo = 8 * gi + u < nrec ? voff : OOR;
             asm volatile("" : "+v"(vo));
-            const auto v = __builtin_amdgcn_raw_buffer_load_b96(rsrc, vo + (uint32_t)(u * 12 * G), so, 0);
-            P[u][0] = v[0]; P[u][1] = v[1]; P[u][2] = v[2];
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, vo + (uint32_t)(u * 8 * G), so, 0);
+            P[u][0] = v[0]; P[u][1] = v[1];
         }
     };
     uint32_t sink = 0;   // diagnostic ablate&2: loads consumed without counting
-    auto sink8 = [&](const uint32_t (&P)[8][3]) {
+    auto sink8 = [&](const uint32_t (&P)[8][2]) {
 #pragma unroll
-        for (int u = 0; u < 8; u++) sink ^= P[u][0] ^ P[u][1] ^ P[u][2];
+        for (int u = 0; u < 8; u++) sink ^= P[u][0] ^ P[u][1];
     };
     zeroV();
     // ---- count this word's records of the chunk (one flush: chunk ≤ 248·G, check_dev) ----
-    uint32_t P[8][3], Q[8][3];
+    uint32_t P[8][2], Q[8][2];
     if (ngrp > 0) loadg(P, 0);
     __builtin_amdgcn_sched_barrier(0);
     if (finish) prefetch_store(d, L, n, pf);   // their loads were issued before P's
     if (fastp) fast_prologue(d, L, cols, ti, n, pf);
+    corr.apply(hist, d);
     {
         // two groups of 8 per trip (one 16-record carry-save step), the next group always
         // in flight while one is counted; an odd last group closes alone.  sched_barrier
@@ -1272,19 +1319,26 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 atomicAdd(hw + 8 + r, hi);
             }
         };
+        // X = C|T, Y = G|T, Z = T → T, C = X − Z, G = Y − Z, A = n − X − Y + Z (no byte
+        // borrows: every difference is a count)
+        uint32_t X[8], Y[8], Z[8];
+#pragma unroll
+        for (int r = 0; r < 8; r++) { X[r] = V[0][r]; Y[r] = V[1][r]; Z[r] = V[2][r]; }
+        transpose8(X);
+        transpose8(Y);
+        transpose8(Z);
         const uint32_t nb = nrec * 0x01010101u;
+        add(5, Z);
 #pragma unroll
-        for (int pr = 0; pr < 3; pr++) {   // (O,A) → '-',A; (Y,G) → C,G; (Z,T) → N,T
-            uint32_t X[8], Y[8];
-#pragma unroll
-            for (int r = 0; r < 8; r++) { X[r] = V[2 * pr][r]; Y[r] = V[2 * pr + 1][r]; }
-            transpose8(X);
-            transpose8(Y);
-#pragma unroll
-            for (int r = 0; r < 8; r++) X[r] = pr == 0 ? nb - X[r] - Y[r] : X[r] - Y[r];   // no byte borrows
-            add(pr == 0 ? 0 : (pr == 1 ? 2 : 4), X);
-            add(pr == 0 ? 1 : (pr == 1 ? 3 : 5), Y);
+        for (int r = 0; r < 8; r++) {
+            const uint32_t a1 = nb - X[r] - Y[r] + Z[r];
+            X[r] -= Z[r];
+            Y[r] -= Z[r];
+            Z[r] = a1;
         }
+        add(2, X);
+        add(3, Y);
+        add(1, Z);
     }
     if (sink == 0x9E3779B9u) hist[0] = 1;   // keeps the ablation's loads alive
     // the count loop's last prefetch group is never consumed: drain it here (long landed),
@@ -1364,8 +1418,9 @@ static int check_dev(const s2c_dev *d) {
     if (d->padded_len <= 0 || d->padded_len >= ((int64_t)1 << 32)) return s2c_set_error(S2C_ERR_ARG, "bad padded_len");
     if (d->n_blocks >= ((int64_t)1 << 31) || (int64_t)d->n_thr * d->n_blocks >= ((int64_t)1 << 40))
         return s2c_set_error(S2C_ERR_LIMIT, "too many (threshold, tile) blocks");
-    if (d->n_items > 0 && (!d->items || !d->wrec || !d->recs || d->chunk_recs <= 0))
+    if (d->n_items > 0 && (!d->items || !d->wrec || !d->recs || !d->fix || d->chunk_recs <= 0))
         return s2c_set_error(S2C_ERR_ARG, "missing pileup buffers");
+    if (d->n_exc > 0 && !d->exc) return s2c_set_error(S2C_ERR_ARG, "missing '-'/'N' entries");
     {   // one flush per item: the LDS histogram's u16 halves hold ≤ 248·G per position
         int64_t nwp = 8;
         while (nwp * 32 < d->tile_max) nwp *= 2;

@@ -30,9 +30,19 @@ class SubBatch:
         for name, _ in L.BatchInfo._fields_:
             setattr(info, name, getattr(i, name))
         self.blocks = hb.blocks[t0:t1].copy()
-        sel = (hb.items[:, 3] >= t0) & (hb.items[:, 3] < t1)
-        it = hb.items[sel].copy()
+        sel = np.nonzero((hb.items[:, 3] >= t0) & (hb.items[:, 3] < t1))[0]
+        it = hb.items[sel].astype(np.int64)
+        # the items' placeholder words and '-'/'N' entries are contiguous ranges: slice, rebase
+        i0, i1 = (int(sel[0]), int(sel[-1]) + 1) if len(sel) else (0, 0)
+        nfix_all = np.append(hb.items[:, 4].astype(np.int64), hb.info.n_fix)
+        f0, f1 = int(nfix_all[i0]), int(nfix_all[i1])
+        x0 = int(hb.items[i0, 5]) if len(sel) else 0
+        x1 = int(hb.items[i1 - 1, 6]) if len(sel) else 0
+        self.fix = hb.fix[f0:f1].copy()
+        self.exc = hb.exc[x0:x1].copy()
         it[:, 3] -= t0
+        it[:, 4] -= f0
+        it[:, 5:7] -= x0
         self.items = it.astype(np.uint32)
         self.deep = (hb.deep[(hb.deep >= t0) & (hb.deep < t1)] - t0).astype(np.uint32)
         A = int(self.blocks[0, 0]) if len(self.blocks) else 0
@@ -84,6 +94,8 @@ class SubBatch:
         info.n_items = len(self.items)
         info.n_blocks = len(self.blocks)
         info.n_deep = len(self.deep)
+        info.n_exc = len(self.exc)
+        info.n_fix = len(self.fix)
         info.n_ins = e1 - e0
         info.n_ins_bases = int(self.ins_off[-1])
         info.n_ins_words = len(self.ins_bases)

@@ -25,27 +25,44 @@ def _amb():
     return AMB
 
 
-def record_codes(recs):
-    """Records [n][3] bit-planes → codes [n][32] (7 = no entry)."""
+SYM_OF_BASE = np.array([1, 2, 3, 5], dtype=np.int64)   # 2-bit base (A C G T) → symbol index of "-ACGNT"
+
+
+def record_bases(recs):
+    """Records [n][2] bit-planes → 2-bit bases [n][32] (b1·2+b0: A C G T)."""
     q = np.arange(32, dtype=np.int64)
     r = np.asarray(recs, dtype=np.int64)
-    return ((r[:, 0, None] >> q) & 1) + 2 * ((r[:, 1, None] >> q) & 1) + 4 * ((r[:, 2, None] >> q) & 1)
+    return ((r[:, 0, None] >> q) & 1) + 2 * ((r[:, 1, None] >> q) & 1)
 
 
 def model_counts(hb, block=1 << 18):
-    """counts[6][padded_len] from the word-major seqout records, as k_pileup adds them."""
+    """counts[6][padded_len] from the packed batch, as k_pileup forms them: every record
+    position counted as its 2-bit base (placeholders as A), minus the A placeholders (fix),
+    plus the '-'/'N' entries (exc), both per work item."""
     Lp = hb.info.padded_len
     wrec = hb.wrec.astype(np.int64)
     assert wrec[0] == 0 and wrec[-1] == hb.info.n_recs and (np.diff(wrec) >= 0).all()
     word_of = np.repeat(np.arange(Lp // 32, dtype=np.int64), np.diff(wrec))
     flat = np.zeros(NSYM * Lp, dtype=np.int64)
     for k in range(0, len(word_of), block):
-        codes = record_codes(hb.recs[k:k + block])
-        assert not (codes == 6).any(), "code 6 is never packed"
+        sym = SYM_OF_BASE[record_bases(hb.recs[k:k + block])]
         pos = word_of[k:k + block, None] * 32 + np.arange(32)
-        keep = codes < NSYM
-        flat += np.bincount((codes[keep] * Lp + pos[keep]), minlength=NSYM * Lp)
-    return flat.reshape(NSYM, Lp)
+        flat += np.bincount((sym * Lp + pos).reshape(-1), minlength=NSYM * Lp)
+    counts = flat.reshape(NSYM, Lp)
+    fix = hb.fix.astype(np.int64)
+    for a, b, _, _, fo, x0, x1 in hb.items[:, :7].astype(np.int64):   # per work item
+        nw = (b + 31) // 32 - a // 32
+        f = fix[fo:fo + 16 * nw].reshape(nw, 16)
+        ph = np.concatenate([f & 0xFFFF, f >> 16], axis=1).reshape(-1)   # tile positions a..a+32·nw
+        counts[1, a:a + 32 * nw] -= ph
+        e = hb.exc[x0:x1].astype(np.int64)
+        pos = a + (e >> 1)
+        assert (pos < b).all()
+        np.add.at(counts, (np.where(e & 1, 4, 0), pos), 1)
+    for a, b in hb.blocks[:, :2].astype(np.int64):
+        w1 = (b + 31) // 32 * 32
+        assert (counts[1, a:w1] >= 0).all(), "A placeholders exceed the A-counted record positions"
+    return counts
 
 
 def check_plan(hb):
@@ -57,7 +74,7 @@ def check_plan(hb):
     ch = int(hb.info.chunk_recs)
     assert ch > 0
     chunks = {}
-    for a, b, c, t in hb.items.astype(np.int64):
+    for a, b, c, t in hb.items[:, :4].astype(np.int64):
         chunks.setdefault(int(t), []).append(int(c))
         assert (int(hb.blocks[t, 0]), int(hb.blocks[t, 1])) == (a, b)
     for t, (a, b, ref, deep) in enumerate(hb.blocks[:, :4].astype(np.int64)):
