@@ -1201,8 +1201,10 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     __shared__ uint32_t cols[ICOL * NSYM];
     __shared__ FastLds<ICOL> L;
     const uint32_t tid = threadIdx.x;
-    // diagnostic 0x2000: word-major lanes (a wave holds whole words) instead of interleaved
-    const bool wmaj = (d.ablate & 0x2000) != 0;
+    // word-major lanes: a wave holds 64/G whole words, so one load instruction reads G
+    // consecutive records of each (full memory requests); diagnostic 0x2000: interleaved
+    // (a wave holds 64/G lanes of every word)
+    const bool wmaj = (d.ablate & 0x2000) == 0;
     const uint32_t w = wmaj ? tid / G : tid % NWP, g = wmaj ? tid % G : tid / NWP;
     if (d.ablate & 0x800) return;   // diagnostic: empty kernel (launch cost)
     S2C_STAMP(d, 0);
@@ -1307,8 +1309,39 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             for (int c = 0; c < NCTR; c++) close16(V[c], ta[c], tb[c]);
         }
     }
-    // ---- flush: counters → six symbol counts → LDS histogram ----
-    if (active && !(d.ablate & 8)) {
+    // ---- flush: counters → four symbol counts → LDS histogram ----
+    {
+        // X = C|T, Y = G|T, Z = T → T, C = X − Z, G = Y − Z, A = n − X − Y + Z (no byte
+        // borrows: every difference is a count)
+        uint32_t X[8], Y[8], Z[8];
+#pragma unroll
+        for (int r = 0; r < 8; r++) { X[r] = V[0][r]; Y[r] = V[1][r]; Z[r] = V[2][r]; }
+        transpose8(X);
+        transpose8(Y);
+        transpose8(Z);
+        // The G lanes of a word sit side by side (word-major): add pairs, then quads of them
+        // with DPP row shifts while a byte cannot carry (≤ 255), so that one lane in `red`
+        // adds into the histogram — the lanes of a word hit the same LDS words, and those
+        // atomics serialize.  Whole words are active or not, and G ≥ 4: no sum mixes words.
+        uint32_t nsum = nrec, red = 1;
+        auto shr1 = [](uint32_t &v) { v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true); };
+        auto shr2 = [](uint32_t &v) { v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true); };
+        if (wmaj) {
+            const uint32_t nmax = uni(__ockl_wfred_max_u32(nrec));
+            if (nmax < 128) {   // pair sums ≤ 254
+                red = 2;
+                shr1(nsum);
+#pragma unroll
+                for (int r = 0; r < 8; r++) { shr1(X[r]); shr1(Y[r]); shr1(Z[r]); }
+                if (nmax < 64) {   // quad sums ≤ 252
+                    red = 4;
+                    shr2(nsum);
+#pragma unroll
+                    for (int r = 0; r < 8; r++) { shr2(X[r]); shr2(Y[r]); shr2(Z[r]); }
+                }
+            }
+        }
+        if (active && (g % red) == red - 1 && !(d.ablate & 8)) {
         uint32_t *h0 = hist + (g % H::HC) * H::CS + 17 * w;   // this lane group's copy
         auto add = [&](uint32_t sym, const uint32_t (&R)[8]) {
             uint32_t *hw = h0 + sym * HP;
@@ -1319,15 +1352,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 atomicAdd(hw + 8 + r, hi);
             }
         };
-        // X = C|T, Y = G|T, Z = T → T, C = X − Z, G = Y − Z, A = n − X − Y + Z (no byte
-        // borrows: every difference is a count)
-        uint32_t X[8], Y[8], Z[8];
-#pragma unroll
-        for (int r = 0; r < 8; r++) { X[r] = V[0][r]; Y[r] = V[1][r]; Z[r] = V[2][r]; }
-        transpose8(X);
-        transpose8(Y);
-        transpose8(Z);
-        const uint32_t nb = nrec * 0x01010101u;
+        const uint32_t nb = nsum * 0x01010101u;
         add(5, Z);
 #pragma unroll
         for (int r = 0; r < 8; r++) {
@@ -1339,6 +1364,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
         add(2, X);
         add(3, Y);
         add(1, Z);
+        }
     }
     if (sink == 0x9E3779B9u) hist[0] = 1;   // keeps the ablation's loads alive
     // the count loop's last prefetch group is never consumed: drain it here (long landed),

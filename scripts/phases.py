@@ -48,7 +48,7 @@ def main():
             nm, np.median(col), np.percentile(col, 90), col.max(), np.median(dur), np.percentile(dur, 90), dur.max()))
         prev = k
     # what the slow items have in common: records streamed, XCD (blockIdx mod 8), start time
-    items = hb.items.astype(np.int64)
+    items = hb.items[:, :4].astype(np.int64)
     wrec = hb.wrec.astype(np.int64)
     recs = np.array([wrec[(b + 31) >> 5] - wrec[a >> 5] for a, b, _, _ in items])
     cnt = rel[:, 2] - rel[:, 1]
