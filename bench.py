@@ -2,9 +2,10 @@
 """bench.py — BASELINE.json metric: aligned bases/s into consensus on MI355X.
 
 A step = one pass of the device hot path (pileup + fused insertion columns, vote and FASTA
-body bytes → deep tiles) over one synthetic batch resident in
-HBM, replayed as one captured HIP graph (host SAM parse and H2D excluded; parse time
-reported separately).
+body bytes → flagged tiles) over one synthetic batch resident in HBM:
+one `s2c_run` (direct kernel launches, queued back to back — a HIP graph replay costs
+≈5 µs more GPU time per step on this ROCm, scripts/launch_overhead.py; `--graph` times
+replays instead).  Host SAM parse and H2D are excluded; parse time is reported separately.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2]
 
@@ -84,6 +85,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-scale", type=float, default=0.4)
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="time HIP graph replays of the step")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -118,22 +120,26 @@ def main():
     db = DeviceBatch(hb, dev)
     ws = Workspace(db, thresholds, min_depth, b"-")
     K = args.steps
-    # k_pileup's own duration (roofline): HIP events on the launch stream around the pileup
-    # stage alone, the other stages between them (untimed); also the warm-up.
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    # k_pileup's own duration (roofline): one pair of HIP events on the launch stream around
+    # K back-to-back pileup launches (per-launch event pairs would add their own packets to
+    # every measured kernel); also the warm-up.
     for _ in range(args.warmup):
         ws.run()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
     for k in range(K):
-        ev[k][0].record()
         ws.pileup()
-        ev[k][1].record()
-        ws.consensus()
+    e1.record()
     torch.cuda.synchronize(dev)
-    pileup_ms = sum(a.elapsed_time(b) for a, b in ev) / K
-    # the step: one replay of the captured HIP graph of all stages
-    ws.capture()
+    pileup_ms = e0.elapsed_time(e1) / K
+    # the step: one s2c_run (or one replay of its captured HIP graph)
+    if args.graph:
+        ws.capture()
+        step = ws.replay
+    else:
+        step = ws.run
     for _ in range(args.warmup):
-        ws.replay()
+        step()
     torch.cuda.synchronize(dev)
 
     if world > 1:
@@ -141,7 +147,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(K):
-        ws.replay()
+        step()
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     if world > 1:
