@@ -1237,11 +1237,6 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     if (finish) prefetch_load(d, a, n, ti, pf);
     Corrections<NWP> corr;   // A placeholders and '-'/'N' entries of this item's records
     corr.load(d, n, uni(itc.x), uni(itc.y), uni(itc.z));
-    for (uint32_t i = tid; i < (uint32_t)(H::HC * H::CS) / 4; i += WG) ((uint4 *)hist)[i] = make_uint4(0, 0, 0, 0);
-    if (fastp)
-        for (uint32_t i = tid; i < (ti.cb1 - ti.cb0) * NSYM; i += WG) cols[i] = 0;
-    lds_sync();
-    S2C_STAMP(d, 1);
     uint32_t V[NCTR][8];
     auto zeroV = [&]() {
 #pragma unroll
@@ -1282,9 +1277,15 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     };
     zeroV();
     // ---- count this word's records of the chunk (one flush: chunk ≤ 248·G, check_dev) ----
+    // the first group is issued before the LDS zeroing and its barrier
     uint32_t P[8][2], Q[8][2];
     if (ngrp > 0) loadg(P, 0);
     __builtin_amdgcn_sched_barrier(0);
+    for (uint32_t i = tid; i < (uint32_t)(H::HC * H::CS) / 4; i += WG) ((uint4 *)hist)[i] = make_uint4(0, 0, 0, 0);
+    if (fastp)
+        for (uint32_t i = tid; i < (ti.cb1 - ti.cb0) * NSYM; i += WG) cols[i] = 0;
+    lds_sync();
+    S2C_STAMP(d, 1);
     if (finish) prefetch_store(d, L, n, pf);   // their loads were issued before P's
     if (fastp) fast_prologue(d, L, cols, ti, n, pf);
     corr.apply(hist, d);
