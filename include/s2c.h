@@ -50,7 +50,8 @@ int s2c_layout(int64_t *out, int n);
 /* ---- constants shared with the kernels -------------------------------------------- */
 #define S2C_NSYM          6    /* symbols '-','A','C','G','N','T' — sorted() order (:367) */
 #define S2C_POS_ALIGN    64    /* each reference starts at a multiple of this global coordinate */
-#define S2C_ITEM_WORDS    8    /* u32 words per pileup work item {a, b, chunk, tile, fix_off, x0, x1, 0} */
+#define S2C_ITEM_WORDS   16    /* u32 words per pileup work item {a, b, chunk, tile, fix_off, x0, x1,
+                                  flags, klo, khi, e0, e1, cb0, cb1, rbase, 0} */
 #define S2C_BLOCK_WORDS  12    /* u32 words per tile {a, b, ref, flags, klo, khi, e0, e1, cb0, cb1, 0, 0} */
 #define S2C_TILE_DEEP     1    /* flags: the tile's records take several work items (HBM counts) */
 #define S2C_TILE_GENERAL  2    /* flags: more insertion columns / keys than k_pileup's LDS holds:
@@ -109,6 +110,7 @@ typedef struct {
                                   (S2C_TILE_DEEP) or beyond k_pileup's LDS (S2C_TILE_GENERAL) */
     int64_t n_exc;             /* seqout '-' / 'N' entries (kept out of the 2-bit records) */
     int64_t n_fix;             /* u32 words of per-item A-placeholder counts */
+    int64_t n_iwr;             /* u32 words of per-item word record ranges (n_items · words · 2) */
 } s2c_batch_info;
 
 typedef struct {               /* host pointers into the batch (valid until s2c_batch_free) */
@@ -142,8 +144,13 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
     const uint32_t *ins_bits;  /* [padded_len/32] bit p: position p is a key */
     const uint32_t *ins_rank;  /* [padded_len/32+1] keys before 32-position word W */
     const uint32_t *items;     /* [n_items][S2C_ITEM_WORDS] pileup work items {a, b, chunk, tile,
-                                  fix_off, x0, x1, 0}: tile [a, b), records chunk `chunk` of each
-                                  word, its placeholder words and '-'/'N' entries [x0, x1) */
+                                  fix_off, x0, x1, flags, klo, khi, e0, e1, cb0, cb1, rbase, 0}:
+                                  tile [a, b), records chunk `chunk` of each word, its placeholder
+                                  words and '-'/'N' entries [x0, x1), a copy of the tile's block
+                                  words 3-9, and wrec[a/32] (the item's first record) */
+    const uint32_t *iwr;       /* [n_items][nwp][2] per item and tile word w: its record range
+                                  {r0, r1} (nwp = words of the widest tile rounded up to a power
+                                  of two ≥ 8; words past the tile: {0, 0}) */
     const uint32_t *blocks;    /* [n_blocks][S2C_BLOCK_WORDS] tiles {g_begin, g_end, ref, flags, then the
                                   tile's keys [klo,khi), events [e0,e1), columns [cb0,cb1)} */
     const uint32_t *deep;      /* [n_deep] indices of the tiles k_consensus votes (flags != 0) */
@@ -195,6 +202,7 @@ typedef struct {
     /* ---- packed batch (device copies of s2c_batch_arrays) ---- */
     const uint32_t *wrec, *recs;   /* word-major seqout records (s2c_batch_arrays) */
     const uint32_t *fix, *exc;     /* A-placeholder counts, '-'/'N' entries (s2c_batch_arrays) */
+    const uint32_t *iwr;           /* per-item word record ranges (s2c_batch_arrays) */
     const uint32_t *items, *blocks, *deep;
     const uint32_t *ins_ev, *ins_kinfo, *ins_bases, *ins_bits;   /* (s2c_batch_arrays) */
     int64_t n_recs, chunk_recs, n_items, n_blocks, n_deep, n_keys, n_cols, padded_len, n_exc;

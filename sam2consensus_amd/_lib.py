@@ -25,7 +25,7 @@ S2C_ERR_LIMIT = -13
 
 S2C_NSYM = 6
 S2C_POS_ALIGN = 64
-S2C_ITEM_WORDS = 8
+S2C_ITEM_WORDS = 16
 S2C_BLOCK_WORDS = 12
 S2C_CODE_FILL = 0
 
@@ -47,7 +47,7 @@ class BatchInfo(C.Structure):
         "n_refs", "total_len", "padded_len", "header_lines", "lines_total", "reads_mapped",
         "aligned_bases", "query_bases", "n_reads", "n_ops", "n_recs", "chunk_recs", "n_ins",
         "n_ins_bases", "n_ins_words", "n_keys", "n_cols", "n_items", "n_blocks", "tile_max",
-        "n_deep", "n_exc", "n_fix")]
+        "n_deep", "n_exc", "n_fix", "n_iwr")]
 
 
 _P64 = C.POINTER(C.c_int64)
@@ -61,7 +61,7 @@ class BatchArrays(C.Structure):
                 ("ins_key", _P32), ("ins_koff", _P32), ("ins_kcol", _P32), ("ins_off", _P32),
                 ("ins_bases", _P32), ("ins_ekey", _P32), ("ins_ev", _P32), ("ins_kinfo", _P32),
                 ("ins_bits", _P32), ("ins_rank", _P32),
-                ("items", _P32), ("blocks", _P32), ("deep", _P32)]
+                ("items", _P32), ("iwr", _P32), ("blocks", _P32), ("deep", _P32)]
 
 
 class SynthSpec(C.Structure):
@@ -78,7 +78,7 @@ _VP = C.c_void_p
 class Dev(C.Structure):
     """Mirror of ``s2c_dev`` (include/s2c.h)."""
     _fields_ = [
-        ("wrec", _VP), ("recs", _VP), ("fix", _VP), ("exc", _VP),
+        ("wrec", _VP), ("recs", _VP), ("fix", _VP), ("exc", _VP), ("iwr", _VP),
         ("items", _VP), ("blocks", _VP), ("deep", _VP),
         ("ins_ev", _VP), ("ins_kinfo", _VP), ("ins_bases", _VP), ("ins_bits", _VP),
         ("n_recs", C.c_int64), ("chunk_recs", C.c_int64),

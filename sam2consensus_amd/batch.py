@@ -79,6 +79,7 @@ class HostBatch:
         # seqout '-'/'N' entries
         self.fix = _view(a.fix, i.n_fix, np.uint32)
         self.exc = _view(a.exc, i.n_exc, np.uint32)
+        self.iwr = _view(a.iwr, i.n_iwr, np.uint32)
         # insertion events grouped by key (keys ascending)
         nw = i.padded_len // 32
         self.ins_key = _view(a.ins_key, i.n_keys, np.uint32)

@@ -175,6 +175,7 @@ struct s2c_batch {
     std::vector<uint32_t> rd_pos, rd_op, rd_span, ops;   // host-side read-piece table
     std::vector<uint32_t> wrec, recs;                     // word-major seqout windows
     std::vector<uint32_t> fix, exc;                       // A placeholders, '-'/'N' entries
+    std::vector<uint32_t> iwr;                            // per-item word record ranges
     std::vector<uint32_t> ins_key, ins_koff, ins_kcol, ins_off, ins_bases, ins_ekey, ins_bits, ins_rank;
     std::vector<uint32_t> ins_ev, ins_kinfo;             // device-side event / key records
     std::vector<uint32_t> items, blocks, deep;
@@ -867,6 +868,25 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
         }
         I.n_deep = (int64_t)b->deep.size();
     }
+    {   // item descriptors: the tile's flags and insertion ranges, the item's first record and,
+        // per word, its record range (k_pileup's first load round needs nothing else)
+        const int64_t NI = I.n_items;
+        const uint64_t CH = (uint64_t)I.chunk_recs;
+        b->iwr.assign((size_t)NI * nwp * 2, 0);
+        for (int64_t it = 0; it < NI; it++) {
+            uint32_t *iv = &b->items[S2C_ITEM_WORDS * it];
+            const uint32_t *blk = &b->blocks[(size_t)iv[3] * S2C_BLOCK_WORDS];
+            for (int k = 0; k < 7; k++) iv[7 + k] = blk[3 + k];
+            iv[14] = b->wrec[iv[0] >> 5];
+            for (int64_t w = 0; w < nwp && 32 * w < (int64_t)(iv[1] - iv[0]); w++) {
+                const uint64_t W = (iv[0] >> 5) + w, wb = b->wrec[W], we = b->wrec[W + 1];
+                const uint64_t r0 = std::min<uint64_t>(we, wb + (uint64_t)iv[2] * CH), r1 = std::min<uint64_t>(we, r0 + CH);
+                b->iwr[2 * ((size_t)it * nwp + w)] = (uint32_t)r0;
+                b->iwr[2 * ((size_t)it * nwp + w) + 1] = (uint32_t)r1;
+            }
+        }
+        I.n_iwr = (int64_t)b->iwr.size();
+    }
     *out = b;
     return S2C_OK;
 }
@@ -890,6 +910,7 @@ extern "C" int s2c_batch_arrays_get(const s2c_batch *b, s2c_batch_arrays *o) {
     o->recs = b->recs.data();
     o->fix = b->fix.data();
     o->exc = b->exc.data();
+    o->iwr = b->iwr.data();
     o->ins_key = b->ins_key.data();
     o->ins_koff = b->ins_koff.data();
     o->ins_kcol = b->ins_kcol.data();

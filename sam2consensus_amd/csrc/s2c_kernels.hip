@@ -1210,24 +1210,25 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     S2C_STAMP(d, 0);
     if (tid < 64) L.amb[tid] = c_amb[tid];   // published by the barrier after the histogram zeroing
     const uint32_t *__restrict__ recs = d.recs;
-    const uint32_t CH = (uint32_t)d.chunk_recs;
     const uint32_t item = blockIdx.x;   // grid = work items
-    const uint4 itv = ((const uint4 *)d.items)[2 * (size_t)item];      // {a, b, chunk, tile}
-    const uint4 itc = ((const uint4 *)d.items)[2 * (size_t)item + 1];  // {fix_off, x0, x1, 0}
+    // the item descriptor (64 B: its tile's block words and first record copied in) and this
+    // lane's word record range: one load round before the records
+    const uint4 *iv = (const uint4 *)d.items + 4 * (size_t)item;
+    const uint4 itv = iv[0], itc = iv[1], itk = iv[2], itx = iv[3];
     const uint32_t a = uni(itv.x), b = uni(itv.y), chunk = uni(itv.z), tile = uni(itv.w);
-    const uint32_t *blk = d.blocks + (size_t)tile * S2C_BLOCK_WORDS;
-    const uint32_t flags = uni(blk[3]);
+    (void)chunk;
+    const uint32_t flags = uni(itc.w);
     const bool deep = (flags & S2C_TILE_DEEP) != 0;
-    const TileIns ti = tile_ins(blk);
+    const TileIns ti = {uni(itk.x), uni(itk.y), uni(itk.z), uni(itk.w), uni(itx.x), uni(itx.y)};
+    const uint32_t rbase = uni(itx.z);   // the item's first record
     const uint32_t n = b - a;
     const uint32_t ws = 32u * w;                  // word start, tile-relative
     const bool active = ws < n;
-    uint32_t r0 = 0, r1 = 0;   // this word's records in chunk `chunk`
+    uint32_t r0 = 0, r1 = 0;   // this word's records in this item
     if (active) {
-        const uint32_t W = (a >> 5) + w;
-        const uint32_t wb = d.wrec[W], we = d.wrec[W + 1];
-        r0 = (uint32_t)min((uint64_t)we, (uint64_t)wb + (uint64_t)chunk * CH);
-        r1 = (uint32_t)min((uint64_t)we, (uint64_t)r0 + CH);
+        const uint2 rr = ((const uint2 *)d.iwr)[(size_t)item * NWP + w];
+        r0 = rr.x;
+        r1 = rr.y;
     }
     // the tile's whole depth is in this item and its insertion keys / columns fit the LDS:
     // finished here by the epilogue (else its counts go to HBM for k_consensus)
@@ -1248,7 +1249,6 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     // (uniform): a load's address = lane offset (VGPR) + group offset (SGPR) + record slot
     // (immediate); a slot past the lane's range gets an out-of-range offset and the
     // hardware returns zeros (no mask set: nothing counted).
-    const uint32_t rbase = uni(d.wrec[a >> 5]);
     const uint64_t rbytes = ((uint64_t)d.n_recs - rbase) * 8;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(recs + 2 * (size_t)rbase), (short)0, (int)min(rbytes, (uint64_t)0x7FFF0000u), 0x00020000);
@@ -1445,7 +1445,7 @@ static int check_dev(const s2c_dev *d) {
     if (d->padded_len <= 0 || d->padded_len >= ((int64_t)1 << 32)) return s2c_set_error(S2C_ERR_ARG, "bad padded_len");
     if (d->n_blocks >= ((int64_t)1 << 31) || (int64_t)d->n_thr * d->n_blocks >= ((int64_t)1 << 40))
         return s2c_set_error(S2C_ERR_LIMIT, "too many (threshold, tile) blocks");
-    if (d->n_items > 0 && (!d->items || !d->wrec || !d->recs || !d->fix || d->chunk_recs <= 0))
+    if (d->n_items > 0 && (!d->items || !d->iwr || !d->recs || !d->fix || d->chunk_recs <= 0))
         return s2c_set_error(S2C_ERR_ARG, "missing pileup buffers");
     if (d->n_exc > 0 && !d->exc) return s2c_set_error(S2C_ERR_ARG, "missing '-'/'N' entries");
     {   // one flush per item: the LDS histogram's u16 halves hold ≤ 248·G per position

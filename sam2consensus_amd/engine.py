@@ -53,7 +53,7 @@ class DeviceBatch:
         # word-major seqout records + work plan (the read-piece table stays on the host)
         self.wrec = up(hb.wrec)
         self.recs = up(hb.recs.reshape(-1))
-        self.fix, self.exc = up(hb.fix.reshape(-1)), up(hb.exc)
+        self.fix, self.exc, self.iwr = up(hb.fix.reshape(-1)), up(hb.exc), up(hb.iwr)
         self.items, self.blocks = up(hb.items.reshape(-1)), up(hb.blocks.reshape(-1))
         self.deep = up(hb.deep)
         self.ins_ev, self.ins_kinfo = up(hb.ins_ev.reshape(-1)), up(hb.ins_kinfo.reshape(-1))
@@ -62,7 +62,7 @@ class DeviceBatch:
 
     def nbytes(self):
         return sum(t.numel() * t.element_size() for t in (
-            self.wrec, self.recs, self.fix, self.exc, self.items, self.blocks, self.deep,
+            self.wrec, self.recs, self.fix, self.exc, self.iwr, self.items, self.blocks, self.deep,
             self.ins_ev, self.ins_kinfo, self.ins_bases, self.ins_bits, self.ins_rank))
 
 
@@ -97,7 +97,7 @@ class Workspace:
         self.out = u8(cap)
         d = L.Dev()
         d.wrec, d.recs = _ptr(db.wrec), _ptr(db.recs)
-        d.fix, d.exc, d.n_exc = _ptr(db.fix), _ptr(db.exc), i.n_exc
+        d.fix, d.exc, d.n_exc, d.iwr = _ptr(db.fix), _ptr(db.exc), i.n_exc, _ptr(db.iwr)
         d.items, d.blocks, d.deep = _ptr(db.items), _ptr(db.blocks), _ptr(db.deep)
         d.ins_ev, d.ins_kinfo, d.ins_bases = _ptr(db.ins_ev), _ptr(db.ins_kinfo), _ptr(db.ins_bases)
         d.ins_bits = _ptr(db.ins_bits)

@@ -43,7 +43,9 @@ class SubBatch:
         it[:, 3] -= t0
         it[:, 4] -= f0
         it[:, 5:7] -= x0
-        self.items = it.astype(np.uint32)
+        self._items64 = it   # the copied block words 8-13 and rbase are re-based below
+        nwp = hb.info.n_iwr // max(hb.info.n_items, 1) // 2
+        iw = hb.iwr.reshape(-1, nwp, 2)[sel].astype(np.int64)
         self.deep = (hb.deep[(hb.deep >= t0) & (hb.deep < t1)] - t0).astype(np.uint32)
         A = int(self.blocks[0, 0]) if len(self.blocks) else 0
         B = int(self.blocks[-1, 1]) if len(self.blocks) else 0
@@ -53,6 +55,10 @@ class SubBatch:
         r0, r1 = int(wrec[A >> 5]), int(wrec[(B + 31) >> 5])
         self.recs = hb.recs[r0:r1].copy()
         self.wrec = np.clip(wrec - r0, 0, r1 - r0).astype(np.uint32)
+        live = iw[:, :, 1] > iw[:, :, 0]   # words past a tile keep {0, 0}
+        iw = np.where(live[:, :, None], iw - r0, 0)
+        self.iwr = iw.astype(np.uint32).reshape(-1)
+        self._items64[:, 14] -= r0
         # the read-piece table stays with the parent (host-side only)
         self.rd_pos = self.rd_span = np.zeros(0, np.uint32)
         self.rd_op = np.zeros(1, np.uint32)
@@ -83,6 +89,10 @@ class SubBatch:
         bl[:, 6:8] -= e0
         bl[:, 8:10] -= int(kcol[k0])
         self.blocks = bl.astype(np.uint32)
+        it = self._items64
+        it[:, 7:14] = bl[it[:, 3], 3:10]   # the items' copies of their tiles' block words
+        self.items = it.astype(np.uint32)
+        del self._items64
         bits = np.zeros_like(hb.ins_bits)
         wa, wb = A >> 5, (B + 31) >> 5
         bits[wa:wb] = hb.ins_bits[wa:wb]
@@ -96,13 +106,15 @@ class SubBatch:
         info.n_deep = len(self.deep)
         info.n_exc = len(self.exc)
         info.n_fix = len(self.fix)
+        info.n_iwr = len(self.iwr)
         info.n_ins = e1 - e0
         info.n_ins_bases = int(self.ins_off[-1])
         info.n_ins_words = len(self.ins_bases)
         info.n_keys = k1 - k0
         info.n_cols = int(self.ins_kcol[-1])
-        info.tile_max = int((self.blocks[:, 1] - self.blocks[:, 0]).max()) if len(self.blocks) else 64
-        self.info = info   # chunk_recs is the parent's: the items' chunk indices refer to it
+        # tile_max and chunk_recs stay the parent's: the items' chunk indices and the per-item
+        # word ranges (iwr) are laid out for the parent's words per tile
+        self.info = info
         self.names = hb.names
         self.ref_len, self.ref_off = hb.ref_len, hb.ref_off
         self.ref_reads = hb.ref_reads

@@ -88,7 +88,29 @@ def check_plan(hb):
     for r in range(hb.info.n_refs):
         o, L = int(hb.ref_off[r]), int(hb.ref_len[r])
         assert (own[o:o + L] == 1).all(), "ref %d positions not tiled exactly once" % r
+    check_item_descriptors(hb)
     check_ins_layout(hb)
+
+
+def check_item_descriptors(hb):
+    """Item words 7-13 copy their tile's block words 3-9, word 14 is the item's first record,
+    and iwr holds each word's record range of the item's chunk."""
+    it = hb.items.astype(np.int64)
+    bl = hb.blocks.astype(np.int64)
+    wrec = hb.wrec.astype(np.int64)
+    ch = int(hb.info.chunk_recs)
+    assert (it[:, 7:14] == bl[it[:, 3], 3:10]).all()
+    assert (it[:, 14] == wrec[it[:, 0] >> 5]).all()
+    nwp = hb.info.n_iwr // max(hb.info.n_items, 1) // 2
+    iw = hb.iwr.astype(np.int64).reshape(-1, nwp, 2)
+    for k, (a, b, c) in enumerate(it[:, :3]):
+        for w in range(nwp):
+            if 32 * w < b - a:
+                W = (a >> 5) + w
+                r0 = min(wrec[W + 1], wrec[W] + c * ch)
+                assert (iw[k, w] == (r0, min(wrec[W + 1], r0 + ch))).all()
+            else:
+                assert (iw[k, w] == 0).all()
 
 
 def check_ins_layout(hb):
