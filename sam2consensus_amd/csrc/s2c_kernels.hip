@@ -271,7 +271,8 @@ struct Prefetch {
     uint32_t bits;
     uint8_t fill;
 };
-__device__ __forceinline__ void prefetch_load(const s2c_dev &d, uint32_t a, uint32_t n, const TileIns &ti, Prefetch &pf) {
+template <class D>
+__device__ __forceinline__ void prefetch_load(const D &d, uint32_t a, uint32_t n, const TileIns &ti, Prefetch &pf) {
     const uint32_t tid = threadIdx.x;
     pf.ev = make_uint4(0, 0, 0, 0);
     pf.key = make_uint4(0, 0, 0, 0);
@@ -284,8 +285,8 @@ __device__ __forceinline__ void prefetch_load(const s2c_dev &d, uint32_t a, uint
     if (tid < (n + 31) / 32) pf.bits = d.ins_bits[(a >> 5) + tid];
     if (tid < (uint32_t)min(d.fill_len, FILL_LDS)) pf.fill = d.fill[tid];
 }
-template <class EL>
-__device__ __forceinline__ void prefetch_store(const s2c_dev &d, EL &L, uint32_t n, const Prefetch &pf) {
+template <class D, class EL>
+__device__ __forceinline__ void prefetch_store(const D &d, EL &L, uint32_t n, const Prefetch &pf) {
     const uint32_t tid = threadIdx.x;
     if constexpr (EL::kEvents) L.ev[tid] = pf.ev;
     L.key[tid] = pf.key;
@@ -297,10 +298,12 @@ __device__ __forceinline__ void prefetch_store(const s2c_dev &d, EL &L, uint32_t
 // Tile (t, tile)'s body region in `out`: a static slot, so every tile writes its bytes
 // without waiting for any other — max(1, len(fill)) bytes per padded position plus one per
 // insertion column before it; threshold t's region starts at t·stride.
-__device__ __forceinline__ uint64_t body_stride(const s2c_dev &d) {
+template <class D>
+__device__ __forceinline__ uint64_t body_stride(const D &d) {
     return (uint64_t)max(1, d.fill_len) * (uint64_t)d.padded_len + (uint64_t)d.n_cols;
 }
-__device__ __forceinline__ uint64_t body_slot(const s2c_dev &d, uint32_t a, uint32_t cb0) {
+template <class D>
+__device__ __forceinline__ uint64_t body_slot(const D &d, uint32_t a, uint32_t cb0) {
     return (uint64_t)max(1, d.fill_len) * a + cb0;
 }
 
@@ -737,6 +740,34 @@ struct Hist {
     }
 };
 
+// ======================================================================= k_pileup arguments
+// What k_pileup reads of s2c_dev, compact (40 SGPRs instead of ≈72: the kernel arguments
+// stay in SGPRs for the whole kernel, and the full struct made the compiler spill them to
+// VGPR lanes).  Same member names: the device helpers are templates over either struct.
+struct PileArgs {
+    const uint32_t *items, *iwr, *recs, *fix, *exc;
+    const uint32_t *ins_ev, *ins_kinfo, *ins_bases, *ins_bits;
+    const double *thresholds;
+    const uint8_t *fill;
+    uint32_t *counts;
+    uint64_t *tile_stats, *blk_len;
+    uint8_t *out;
+    uint32_t n_recs, padded_len, n_cols, n_blocks;
+    int32_t n_thr, min_depth, fill_len, fill_nondash, ablate, n_deep;
+};
+static PileArgs pile_args(const s2c_dev &d) {
+    PileArgs p;
+    p.items = d.items; p.iwr = d.iwr; p.recs = d.recs; p.fix = d.fix; p.exc = d.exc;
+    p.ins_ev = d.ins_ev; p.ins_kinfo = d.ins_kinfo; p.ins_bases = d.ins_bases; p.ins_bits = d.ins_bits;
+    p.thresholds = d.thresholds; p.fill = d.fill; p.counts = d.counts;
+    p.tile_stats = d.tile_stats; p.blk_len = d.blk_len; p.out = d.out;
+    p.n_recs = (uint32_t)d.n_recs; p.padded_len = (uint32_t)d.padded_len;
+    p.n_cols = (uint32_t)d.n_cols; p.n_blocks = (uint32_t)d.n_blocks;
+    p.n_thr = d.n_thr; p.min_depth = d.min_depth; p.fill_len = d.fill_len;
+    p.fill_nondash = d.fill_nondash; p.ablate = d.ablate; p.n_deep = (int32_t)d.n_deep;
+    return p;
+}
+
 // ======================================================================= fast tile epilogue
 // The common case of k_pileup (columns in LDS, ≤ PF keys, -f ≤ FILL_LDS bytes).  The
 // insertion events were already counted into `cols`, the column → key map and the key ranks
@@ -770,13 +801,17 @@ __device__ __forceinline__ uint32_t sym_char(uint32_t s) { return (uint32_t)(0x5
 struct Pos {
     uint32_t c[NSYM];
     uint32_t cov, chars;
-    bool in, called, slow;
+    uint32_t fl;   // bit 0 in the tile, bit 1 called, bit 2 slow (a VGPR: lane masks held across
+                   // the epilogue's phases made the compiler spill SGPRs)
+    __device__ __forceinline__ bool in() const { return fl & 1u; }
+    __device__ __forceinline__ bool called() const { return fl & 2u; }
+    __device__ __forceinline__ bool slow() const { return fl & 4u; }
 };
-__device__ __forceinline__ void pos_vote_fast(Pos &p, int32_t min_depth, double tmax, bool fastok) {
+__device__ __forceinline__ void pos_vote_fast(Pos &p, bool in, int32_t min_depth, double tmax, bool fastok) {
     p.cov = 0;
 #pragma unroll
     for (uint32_t s = 0; s < NSYM; s++) p.cov += p.c[s];
-    p.called = p.in && p.cov > 0 && (int64_t)p.cov >= (int64_t)min_depth;
+    const bool called = in && p.cov > 0 && (int64_t)p.cov >= (int64_t)min_depth;
     // largest count (key = count << 3 | symbol) and the largest of the others
     uint32_t k[NSYM];
 #pragma unroll
@@ -788,7 +823,7 @@ __device__ __forceinline__ void pos_vote_fast(Pos &p, int32_t min_depth, double 
     const uint32_t m1 = mk >> 3;
     const bool fast = fastok && (m2 >> 3) < m1 && (double)m1 >= tmax * (double)p.cov;
     p.chars = sym_char(mk & 7u) * 0x01010101u;
-    p.slow = p.called && !fast;
+    p.fl = (in ? 1u : 0u) | (called ? 2u : 0u) | (called && !fast ? 4u : 0u);
 }
 template <class EL>
 __device__ __forceinline__ void pos_vote_slow(Pos &p, const EL &L, int t0, int tn) {
@@ -798,7 +833,7 @@ __device__ __forceinline__ void pos_vote_slow(Pos &p, const EL &L, int t0, int t
 #pragma unroll
     for (int u = 0; u < VT_TMAX; u++)
         if (u < tn) w |= (uint32_t)L.amb[vote_mask_u32(p.c, gs, L.thr[t0 + u] * (double)p.cov)] << (8 * u);
-    if (p.slow) p.chars = w;
+    if (p.slow()) p.chars = w;
 }
 
 // per byte of a vote-char word: 1 if the char is emitted (neither '-' nor a vote error),
@@ -819,8 +854,8 @@ __device__ __forceinline__ uint32_t em_of(uint32_t e02, uint32_t e13, int u) {
 // insertion events added into the column counts (cols zeroed before the prologue barrier),
 // the column → key slot map and, in wave 0, the keys before each of the tile's words.  The
 // records come from the prefetch registers; events beyond PF (rare) from HBM.
-template <class EL>
-__device__ __forceinline__ void fast_prologue(const s2c_dev &d, EL &L, uint32_t *cols, const TileIns &ti,
+template <class D, class EL>
+__device__ __forceinline__ void fast_prologue(const D &d, EL &L, uint32_t *cols, const TileIns &ti,
                                               uint32_t n, const Prefetch &pf) {
     const uint32_t tid = threadIdx.x;
     if (ti.khi <= ti.klo || (d.ablate & 0x200)) return;   // uniform
@@ -884,8 +919,8 @@ __device__ __forceinline__ uint32_t column_word(const uint32_t *col, uint32_t co
 }
 
 // hist: the tile's LDS histogram (Hist<NWP> layout); cols: LDS [ncol][6].
-template <int NWP, class EL>
-__device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t tile, uint32_t a, uint32_t n,
+template <int NWP, class D, class EL>
+__device__ __forceinline__ void tile_epilogue_fast(const D &d, uint32_t tile, uint32_t a, uint32_t n,
                                                    const TileIns &ti, const uint32_t *hist,
                                                    const uint32_t *cols, EL &L) {
     using H = Hist<NWP>;
@@ -963,11 +998,8 @@ __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t ti
                 }
             }
 #pragma unroll
-            for (int v = 0; v < 2; v++) {
-                P[v].in = q0 + 16 * v < n;
-                pos_vote_fast(P[v], d.min_depth, tmax, fastok);
-            }
-            const bool any_slow = __ballot(P[0].slow || P[1].slow) != 0;   // a tie or a split vote
+            for (int v = 0; v < 2; v++) pos_vote_fast(P[v], q0 + 16 * v < n, d.min_depth, tmax, fastok);
+            const bool any_slow = __ballot(P[0].slow() || P[1].slow()) != 0;   // a tie or a split vote
             if (any_slow) {
                 pos_vote_slow(P[0], L, t0, tn);
                 pos_vote_slow(P[1], L, t0, tn);
@@ -975,6 +1007,8 @@ __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t ti
             S2C_STAMP(d, 3);
             lds_sync();   // (1) column vote chars, per-key emitted counts, zeroed statistics
             S2C_STAMP(d, 4);
+#pragma unroll
+            for (int v = 0; v < 2; v++) asm volatile("" : "+v"(P[v].fl), "+v"(P[v].cov), "+v"(P[v].chars));
             // ---- B: body lengths, row scans, wave totals, statistics
             const uint32_t bw = (has_ins && wd < nwp) ? L.bits[wd] : 0u;
             uint32_t slot[2], em02[2], em13[2];
@@ -982,14 +1016,14 @@ __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t ti
 #pragma unroll
             for (int v = 0; v < 2; v++) {
                 const uint32_t b = i16 + 16 * v;   // bit of the position in its word
-                hk[v] = P[v].called && ((bw >> b) & 1u);
+                hk[v] = P[v].called() && ((bw >> b) & 1u);
                 slot[v] = hk[v] ? L.wrank[wd] + (uint32_t)__popc(bw & ((1u << b) - 1u)) : 0u;
                 em02[v] = hk[v] ? L.kem2[0][slot[v]] : 0u;
                 em13[v] = hk[v] ? L.kem2[1][slot[v]] : 0u;
             }
             // lengths differ between thresholds only by emitted insertion chars
             const bool multi = __ballot((em02[0] | em13[0] | em02[1] | em13[1]) != 0) != 0;
-            const uint32_t lin0 = P[0].in ? (P[0].called ? 1u : F) : 0u, lin1 = P[1].in ? (P[1].called ? 1u : F) : 0u;
+            const uint32_t lin0 = P[0].in() ? (P[0].called() ? 1u : F) : 0u, lin1 = P[1].in() ? (P[1].called() ? 1u : F) : 0u;
             uint32_t off[VT_TMAX][2];
 #pragma unroll
             for (int u = 0; u < VT_TMAX; u++) {
@@ -1025,8 +1059,8 @@ __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t ti
             }
             {   // statistics of this chunk's positions (and of the pass's columns, chunk 0)
                 const uint32_t sc = wave_sum(P[0].cov + P[1].cov);   // ≤ 128 · 6 · 2^16 < 2^32
-                const uint32_t nunc = (uint32_t)__popcll(__ballot(P[0].in && !P[0].called)) +
-                                      (uint32_t)__popcll(__ballot(P[1].in && !P[1].called));
+                const uint32_t nunc = (uint32_t)__popcll(__ballot((P[0].fl & 3u) == 1u)) +
+                                      (uint32_t)__popcll(__ballot((P[1].fl & 3u) == 1u));
                 uint32_t nd[VT_TMAX], ne[VT_TMAX];
 #pragma unroll
                 for (int u = 0; u < VT_TMAX; u++) {
@@ -1040,8 +1074,8 @@ __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t ti
 #pragma unroll
                     for (int v = 0; v < 2; v++) {
                         const uint32_t ch8 = (P[v].chars >> (8 * u)) & 0xFFu;
-                        nd[u] += (uint32_t)__popcll(__ballot(P[v].called && ch8 != '-'));
-                        ne[u] += (uint32_t)__popcll(__ballot(P[v].called && ch8 == 0xFFu));
+                        nd[u] += (uint32_t)__popcll(__ballot(P[v].called() && ch8 != '-'));
+                        ne[u] += (uint32_t)__popcll(__ballot(P[v].called() && ch8 == 0xFFu));
                     }
                 }
                 uint64_t scs[VT_TMAX] = {};
@@ -1068,8 +1102,10 @@ __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t ti
             S2C_STAMP(d, 5);
             lds_sync();   // (2) wave totals, statistics
             S2C_STAMP(d, 8);
+#pragma unroll
+            for (int v = 0; v < 2; v++) asm volatile("" : "+v"(P[v].fl), "+v"(P[v].chars), "+v"(slot[v]), "+v"(em02[v]), "+v"(em13[v]));
             // ---- C: body bytes (:350-389): char, then the key's emitted insertion chars; fill
-            const bool any_fill = F > 0 && __ballot((P[0].in && !P[0].called) || (P[1].in && !P[1].called)) != 0;
+            const bool any_fill = F > 0 && __ballot((P[0].fl & 3u) == 1u || (P[1].fl & 3u) == 1u) != 0;
 #pragma unroll
             for (int u = 0; u < VT_TMAX; u++) {
                 if (u >= tn) continue;
@@ -1078,12 +1114,12 @@ __device__ __forceinline__ void tile_epilogue_fast(const s2c_dev &d, uint32_t ti
                 const uint32_t wofs = (wv > 0 ? fs.x : 0u) + (wv > 1 ? fs.y : 0u) + (wv > 2 ? fs.z : 0u);
                 uint8_t *const ob = obase + (size_t)(t0 + u) * ostride + base[u];
                 const uint32_t o0 = wofs + off[u][0], o1 = wofs + off[u][1];
-                if (P[0].called) ob[o0] = (uint8_t)(P[0].chars >> (8 * u));
-                if (P[1].called) ob[o1] = (uint8_t)(P[1].chars >> (8 * u));
+                if (P[0].called()) ob[o0] = (uint8_t)(P[0].chars >> (8 * u));
+                if (P[1].called()) ob[o1] = (uint8_t)(P[1].chars >> (8 * u));
                 if (any_fill) {   // fill (:356-359)
 #pragma unroll
                     for (int v = 0; v < 2; v++) {
-                        if (!P[v].in || P[v].called) continue;
+                        if ((P[v].fl & 3u) != 1u) continue;   // in the tile, not called: fill
                         const uint32_t o = v ? o1 : o0;
                         if (F <= (uint32_t)FILL_LDS) {
                             for (uint32_t f = 0; f < F; f++) ob[o + f] = L.fill[f];
@@ -1142,7 +1178,8 @@ struct Corrections {
     static constexpr int FN = NWP >= 16 ? NWP / 16 : 1;   // fix words per thread (16 per tile word)
     static constexpr int XN = 4;                           // '-'/'N' entries per thread in registers
     uint32_t fx[FN], xe[XN], x0, x1;
-    __device__ __forceinline__ void load(const s2c_dev &d, uint32_t n, uint32_t fix_off, uint32_t xa, uint32_t xb) {
+    template <class D>
+    __device__ __forceinline__ void load(const D &d, uint32_t n, uint32_t fix_off, uint32_t xa, uint32_t xb) {
         const uint32_t tid = threadIdx.x;
         x0 = xa;
         x1 = xb;
@@ -1162,7 +1199,8 @@ struct Corrections {
         const uint32_t q = e >> 1, sym = (e & 1) ? 4u : 0u;   // 'N' : '-'
         atomicAdd(hist + sym * (17 * NWP) + hslot(((q >> 5) << 4) | (q & 15)), (q & 16) ? 0x10000u : 1u);
     }
-    __device__ __forceinline__ void apply(uint32_t *hist, const s2c_dev &d) const {
+    template <class D>
+    __device__ __forceinline__ void apply(uint32_t *hist, const D &d) const {
         const uint32_t tid = threadIdx.x;
 #pragma unroll
         for (int j = 0; j < FN; j++) {
@@ -1191,7 +1229,7 @@ struct Corrections {
 // columns, vote, statistics), its event/key records prefetched under the count stream; a
 // deep tile's chunks add their histograms into HBM for k_consensus.
 template <int NWP>
-__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_pileup(const s2c_dev d) {
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_pileup(const PileArgs d) {
     constexpr int G = WG / NWP, TW = NWP * 32, HP = TW / 2 + TW / 32;
     using H = Hist<NWP>;
     static_assert(H::HP == HP, "histogram layout");
@@ -1471,7 +1509,7 @@ static int check_dev(const s2c_dev *d) {
 
 template <int NWP>
 static int launch_pileup(const s2c_dev *d, hipStream_t s) {
-    k_pileup<NWP><<<(unsigned)d->n_items, WG, 0, s>>>(*d);
+    k_pileup<NWP><<<(unsigned)d->n_items, WG, 0, s>>>(pile_args(*d));
     return hip_check(hipGetLastError(), "k_pileup");
 }
 
