@@ -1317,8 +1317,10 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     // ---- count this word's records of the chunk (one flush: chunk ≤ 248·G, check_dev) ----
     // the first group is issued before the LDS zeroing and its barrier
     uint32_t P[8][2], Q[8][2];
+    S2C_STAMP(d, 10);   // word ranges known (ngrp needs every lane's)
     if (ngrp > 0) loadg(P, 0);
     __builtin_amdgcn_sched_barrier(0);
+    S2C_STAMP(d, 11);   // first records issued
     for (uint32_t i = tid; i < (uint32_t)(H::HC * H::CS) / 4; i += WG) ((uint4 *)hist)[i] = make_uint4(0, 0, 0, 0);
     if (fastp)
         for (uint32_t i = tid; i < (ti.cb1 - ti.cb0) * NSYM; i += WG) cols[i] = 0;

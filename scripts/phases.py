@@ -37,7 +37,7 @@ def main():
     t0 = ts[:, 0].min()
     rel = ts - t0
     # stamp order of the fast epilogue (k_pileup's common case)
-    order = [(0, "start"), (1, "prologue"), (2, "count+flush"), (3, "A votes"), (4, "A barrier"),
+    order = [(0, "start"), (10, "ranges known"), (11, "records issued"), (1, "prologue"), (2, "count+flush"), (3, "A votes"), (4, "A barrier"),
              (5, "B lengths+scan"), (8, "B barrier"), (9, "C bytes"), (6, "stats"), (7, "end")]
     print("items %d; kernel span %.2f us (earliest start -> latest end)" % (ni, rel[:, 7].max()))
     prev = None
