@@ -169,6 +169,8 @@ def test_sharded_on_device(world):
     ("c2", {"n_refs": 2, "depth": 20.0}, [0.3, 0.7], 18, b"y" * 65),
     # low depth: ties and split votes everywhere (full closed form), 1-5 thresholds
     ("c2", {"n_refs": 4, "depth": 3.0}, [0.2, 0.4, 0.6, 0.8, 1.0], 1, b"N"),
+    # many '-'/'N' entries per work item (> 1024: past the register prefetch, from HBM)
+    ("c2", {"n_refs": 2, "del_frac": 0.6, "del_max": 8, "n_rate": 0.05}, [0.25, 0.5], 1, b"-"),
 ])
 def test_device_pipeline_equals_batch_model(name, over, thr, md, fill):
     """stats / block offsets / bytes of the HIP stages == the batch model (tests/batch_model.py)."""
