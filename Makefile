@@ -6,7 +6,7 @@ ARCH    ?= gfx950
 SRC      = sam2consensus_amd/csrc
 OUT      = sam2consensus_amd/libs2c.so
 BUILD    = build
-CXXFLAGS = -O3 -std=c++17 -fPIC -Wall -Wextra -Iinclude
+CXXFLAGS = -O3 -std=c++17 -fPIC -pthread -Wall -Wextra -Iinclude
 HIPFLAGS = -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -Iinclude \
            -Wno-unused-result
 
@@ -22,7 +22,7 @@ $(BUILD)/s2c_kernels.o: $(SRC)/s2c_kernels.hip include/s2c.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OUT): $(BUILD)/s2c_host.o $(BUILD)/s2c_synth.o $(BUILD)/s2c_kernels.o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ -lz -o $@
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ -lz -lpthread -o $@
 
 $(BUILD):
 	mkdir -p $(BUILD)

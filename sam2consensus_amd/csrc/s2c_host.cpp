@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -472,35 +473,143 @@ static int feed_flush(s2c_parser *p) {
     return S2C_OK;
 }
 
+// ------------------------------------------------------------------ parallel file parse
+// A whole input file is parsed by worker threads: the header lines (:149-172) first, in
+// order; then the record lines, cut into chunks at line ends, each chunk parsed by its own
+// parser state (the same process_line) into its own piece / op / plane / insertion arrays;
+// the chunks are appended in file order.  The first failing record in file order decides
+// the error, as the reference's sequential loop (:188-228) would: a chunk stops at its
+// first error, and no later chunk is merged.
+namespace {
+void append_chunk(s2c_parser *p, const s2c_parser *w) {
+    p->lines_total += w->lines_total;
+    p->reads_mapped += w->reads_mapped;
+    p->aligned += w->aligned;
+    p->qbases += w->qbases;
+    p->p_ref.insert(p->p_ref.end(), w->p_ref.begin(), w->p_ref.end());
+    p->p_pos.insert(p->p_pos.end(), w->p_pos.begin(), w->p_pos.end());
+    p->p_span.insert(p->p_span.end(), w->p_span.begin(), w->p_span.end());
+    p->p_drop.insert(p->p_drop.end(), w->p_drop.begin(), w->p_drop.end());
+    const uint64_t o0 = p->ops.size(), b0 = p->words.size(), r0 = p->i_raw.size();
+    for (size_t i = 1; i < w->p_op.size(); i++) p->p_op.push_back(w->p_op[i] + o0);
+    for (size_t i = 1; i < w->p_base.size(); i++) p->p_base.push_back(w->p_base[i] + b0);
+    p->ops.insert(p->ops.end(), w->ops.begin(), w->ops.end());
+    p->words.insert(p->words.end(), w->words.begin(), w->words.end());
+    p->i_ref.insert(p->i_ref.end(), w->i_ref.begin(), w->i_ref.end());
+    p->i_key.insert(p->i_key.end(), w->i_key.begin(), w->i_key.end());
+    p->i_len.insert(p->i_len.end(), w->i_len.begin(), w->i_len.end());
+    for (uint64_t o : w->i_off) p->i_off.push_back(o + r0);
+    p->i_raw += w->i_raw;
+}
+
+int process_lines(s2c_parser *p, const char *s, size_t n) {
+    size_t i = 0;
+    while (i < n) {
+        const char *nl = (const char *)memchr(s + i, '\n', n - i);
+        const size_t e = nl ? (size_t)(nl - s) + 1 : n;   // a last line without '\n' counts (Py2)
+        int rc = process_line(p, s + i, e - i);
+        if (rc) return rc;
+        i = e;
+    }
+    return S2C_OK;
+}
+
+int parse_buffer(s2c_parser *p, const char *s, size_t n) {
+    size_t i = 0;
+    while (i < n && p->in_header && s[i] == '@') {   // header lines, in order
+        const char *nl = (const char *)memchr(s + i, '\n', n - i);
+        const size_t e = nl ? (size_t)(nl - s) + 1 : n;
+        int rc = process_line(p, s + i, e - i);
+        if (rc) return rc;
+        i = e;
+    }
+    if (i == n) return S2C_OK;
+    p->in_header = false;
+    const size_t body = n - i;
+    unsigned hw = std::thread::hardware_concurrency();
+    int nt = (int)std::min<size_t>(std::min<unsigned>(hw ? hw : 1, 16), std::max<size_t>(1, body >> 23));   // ≥ 8 MB each
+    if (const char *e = getenv("S2C_PARSE_THREADS")) nt = std::max(1, std::min(64, atoi(e)));
+    if (nt <= 1) return process_lines(p, s + i, body);
+    std::vector<size_t> cut(nt + 1, n);
+    cut[0] = i;
+    for (int k = 1; k < nt; k++) {   // chunk k starts after the line end nearest to its share
+        size_t c = std::max(cut[k - 1], i + body * k / nt);
+        const char *nl = c < n ? (const char *)memchr(s + c, '\n', n - c) : nullptr;
+        cut[k] = nl ? (size_t)(nl - s) + 1 : n;
+    }
+    std::vector<s2c_parser *> ws(nt);
+    std::vector<int> rcs(nt, S2C_OK);
+    std::vector<std::thread> th;
+    for (int k = 0; k < nt; k++) {
+        s2c_parser *w = new s2c_parser();
+        w->maxdel_active = p->maxdel_active;
+        w->maxdel = p->maxdel;
+        w->in_header = false;
+        w->ref_names = p->ref_names;
+        w->ref_len = p->ref_len;
+        w->ref_idx = p->ref_idx;
+        ws[k] = w;
+        th.emplace_back([&, k] {
+            rcs[k] = process_lines(ws[k], s + cut[k], cut[k + 1] - cut[k]);
+            if (rcs[k]) ws[k]->errmsg = s2c_last_error();   // thread-local text → the chunk
+        });
+    }
+    for (auto &t : th) t.join();
+    int rc = S2C_OK;
+    for (int k = 0; k < nt; k++) {
+        if (!rc) {
+            append_chunk(p, ws[k]);
+            if (rcs[k]) rc = perr(p, rcs[k], ws[k]->errmsg);
+        }
+        delete ws[k];
+    }
+    return rc;
+}
+}  // namespace
+
 extern "C" int s2c_parser_feed_file(s2c_parser *p, const char *path) {
     if (!p || !path) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
+    if (p->err) return s2c_set_error(p->err, p->errmsg);
     size_t n = strlen(path);
     bool gz = n >= 3 && strcmp(path + n - 3, ".gz") == 0;   // :111
-    std::vector<char> buf(1 << 22);
+    // the whole input in memory (gunzipped), then the parallel parse; a parser that already
+    // holds a partial line from s2c_parser_feed continues line by line
+    std::string data;
     if (gz) {
         gzFile g = gzopen(path, "rb");
         if (!g) return s2c_set_error(S2C_ERR_IO, std::string("cannot open ") + path);
         gzbuffer(g, 1 << 20);
+        std::vector<char> buf(1 << 22);
         for (;;) {
             int r = gzread(g, buf.data(), (unsigned)buf.size());
             if (r < 0) { gzclose(g); return s2c_set_error(S2C_ERR_IO, "gzip read error"); }
             if (r == 0) break;
-            int rc = s2c_parser_feed(p, buf.data(), (size_t)r);
-            if (rc) { gzclose(g); return rc; }
+            data.append(buf.data(), (size_t)r);
         }
         gzclose(g);
     } else {
         FILE *f = fopen(path, "rb");
         if (!f) return s2c_set_error(S2C_ERR_IO, std::string("cannot open ") + path);
+        if (fseek(f, 0, SEEK_END) == 0) {
+            long sz = ftell(f);
+            if (sz > 0) data.reserve((size_t)sz);
+            fseek(f, 0, SEEK_SET);
+        }
+        std::vector<char> buf(1 << 22);
         for (;;) {
             size_t r = fread(buf.data(), 1, buf.size(), f);
             if (r == 0) break;
-            int rc = s2c_parser_feed(p, buf.data(), r);
-            if (rc) { fclose(f); return rc; }
+            data.append(buf.data(), r);
         }
         fclose(f);
     }
-    return feed_flush(p);
+    if (!p->carry.empty()) {
+        int rc = s2c_parser_feed(p, data.data(), data.size());
+        return rc ? rc : feed_flush(p);
+    }
+    int rc = parse_buffer(p, data.data(), data.size());
+    if (rc && !p->err) { p->err = rc; p->errmsg = s2c_last_error(); }
+    return rc;
 }
 
 // ------------------------------------------------------------------ finish: plan

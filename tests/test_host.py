@@ -153,3 +153,42 @@ def test_c2_batch_stats():
     assert 176_000_000 < i.aligned_bases < 177_000_000
     assert i.n_items >= 512 and i.tile_max <= 2048   # enough work items to fill 256 CUs
     bm.check_plan(hb)
+
+
+def _batch_digest(path, maxdel_active):
+    import hashlib
+    try:
+        hb = batch.parse_file(path, maxdel_active, 150)
+    except (KeyError, IndexError, ValueError, ZeroDivisionError, OverflowError) as e:
+        return type(e).__name__
+    h = hashlib.sha256()
+    for a in (hb.recs, hb.wrec, hb.fix, hb.exc, hb.iwr, hb.items, hb.blocks, hb.ins_key, hb.ins_koff,
+              hb.ins_off, hb.ins_bases, hb.ins_ev, hb.ins_kinfo):
+        h.update(np.ascontiguousarray(a).tobytes())
+    i = hb.info
+    h.update(repr((i.lines_total, i.reads_mapped, i.aligned_bases, i.query_bases, i.header_lines)).encode())
+    return h.hexdigest()
+
+
+def test_parallel_file_parse_equals_sequential(tmp_path, monkeypatch):
+    """The threaded file parse (record lines cut into chunks, merged in file order) builds
+    the same batch as one thread, and raises the first error in file order."""
+    p = tmp_path / "in.sam"
+    for case in CASES[:400]:
+        opt = o.parse_argv(["-i", "in.sam"] + list(case["args"]))
+        p.write_bytes(case["sam"].encode("latin-1"))
+        got = {}
+        for t in ("1", "3", "7"):
+            monkeypatch.setenv("S2C_PARSE_THREADS", t)
+            got[t] = _batch_digest(str(p), opt.maxdel_active)
+        assert got["1"] == got["3"] == got["7"], case["name"]   # (the error class, if any)
+    # a larger input, chunks of many lines each
+    sp = configs.spec("c2", scale=0.02)
+    import ctypes as C
+    n = C.c_int64()
+    _lib.check(_lib.lib.s2c_synth_write(C.byref(sp), str(p).encode(), C.byref(n)))
+    got = {}
+    for t in ("1", "5"):
+        monkeypatch.setenv("S2C_PARSE_THREADS", t)
+        got[t] = _batch_digest(str(p), True)
+    assert got["1"] == got["5"]
