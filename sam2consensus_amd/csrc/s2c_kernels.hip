@@ -807,21 +807,26 @@ struct Pos {
     __device__ __forceinline__ bool called() const { return fl & 2u; }
     __device__ __forceinline__ bool slow() const { return fl & 4u; }
 };
-__device__ __forceinline__ void pos_vote_fast(Pos &p, bool in, int32_t min_depth, double tmax, bool fastok) {
+// The shortcut: the largest count m1 is a strict majority (so unique) and m1·2^15 ≥ uq·cov
+// with uq = ⌈tmax·2^15⌉ + 1 (per pass; 0 = off: some threshold outside (0, 1]).  Then
+// m1 ≥ tmax·cov + cov/2^15 ≥ tmax·cov·(1 + 2^-53) ≥ fl(tmax·cov) — every other symbol's
+// greater-sum is ≥ m1 ≥ t·cov for every t of the pass, and the symbol's own is 0 < t·cov.
+// Integer-only (counts < 2^17 here: uq·cov < 2^32); a position it misses takes the exact
+// closed form.
+__device__ __forceinline__ bool majority_fast(uint32_t m1, uint32_t cov, uint32_t uq) {
+    return uq && 2 * m1 > cov && (m1 << 15) >= __umul24(uq, cov);
+}
+__device__ __forceinline__ void pos_vote_fast(Pos &p, bool in, int32_t min_depth, uint32_t uq) {
     p.cov = 0;
 #pragma unroll
     for (uint32_t s = 0; s < NSYM; s++) p.cov += p.c[s];
     const bool called = in && p.cov > 0 && (int64_t)p.cov >= (int64_t)min_depth;
-    // largest count (key = count << 3 | symbol) and the largest of the others
+    // largest count and its symbol: key = count << 3 | symbol
     uint32_t k[NSYM];
 #pragma unroll
     for (uint32_t s = 0; s < NSYM; s++) k[s] = (p.c[s] << 3) | s;
     const uint32_t mk = max(max(max(k[0], k[1]), k[2]), max(max(k[3], k[4]), k[5]));
-    uint32_t m2 = 0;
-#pragma unroll
-    for (uint32_t s = 0; s < NSYM; s++) m2 = max(m2, k[s] == mk ? 0u : k[s]);
-    const uint32_t m1 = mk >> 3;
-    const bool fast = fastok && (m2 >> 3) < m1 && (double)m1 >= tmax * (double)p.cov;
+    const bool fast = majority_fast(mk >> 3, p.cov, uq);
     p.chars = sym_char(mk & 7u) * 0x01010101u;
     p.fl = (in ? 1u : 0u) | (called ? 2u : 0u) | (called && !fast ? 4u : 0u);
 }
@@ -894,22 +899,18 @@ __device__ __forceinline__ void fast_prologue(const D &d, EL &L, uint32_t *cols,
 // cov − Σ column (:294, signed).  Shortcut as for positions when every count is ≥ 0.
 template <class EL>
 __device__ __forceinline__ uint32_t column_word(const uint32_t *col, uint32_t cov, const EL &L, int t0, int tn,
-                                                double tmax, bool fastok) {
+                                                uint32_t uq) {
     uint32_t v[NSYM], tot = 0;
 #pragma unroll
     for (uint32_t c = 0; c < NSYM; c++) { v[c] = col[c]; tot += v[c]; }
     const int64_t dash = (int64_t)cov - (int64_t)tot;   // the column's own '-' count is in the sum
-    if (fastok && dash >= 0 && cov < (1u << 28)) {
+    if (uq && dash >= 0 && cov < (1u << 17)) {
         v[0] = (uint32_t)dash;
         uint32_t kk[NSYM];
 #pragma unroll
         for (uint32_t c = 0; c < NSYM; c++) kk[c] = (v[c] << 3) | c;
         const uint32_t mk = max(max(max(kk[0], kk[1]), kk[2]), max(max(kk[3], kk[4]), kk[5]));
-        uint32_t m2 = 0;
-#pragma unroll
-        for (uint32_t c = 0; c < NSYM; c++) m2 = max(m2, kk[c] == mk ? 0u : kk[c]);
-        const uint32_t m1 = mk >> 3;
-        if ((m2 >> 3) < m1 && (double)m1 >= tmax * (double)cov) return sym_char(mk & 7u) * 0x01010101u;
+        if (majority_fast(mk >> 3, cov, uq)) return sym_char(mk & 7u) * 0x01010101u;
     }
     const uint32_t m = column_masks(col, cov, &L.thr[t0], tn);
     uint32_t word = 0;
@@ -937,14 +938,15 @@ __device__ __forceinline__ void tile_epilogue_fast(const D &d, uint32_t tile, ui
     for (int t0 = 0; t0 < T; t0 += VT_TMAX) {
         const int tn = min(VT_TMAX, T - t0);
         double tmax = L.thr[t0];
-        bool fastok = true;   // every threshold of the pass in (0, inf): x = t·cov > 0 for cov ≥ 1
+        bool fastok = true;   // every threshold of the pass in (0, 1] (a lone symbol cannot reach t > 1)
 #pragma unroll
         for (int u = 0; u < VT_TMAX; u++)
             if (u < tn) {
                 const double th = L.thr[t0 + u];
-                fastok = fastok && th > 0.0 && th < __builtin_inf();
+                fastok = fastok && th > 0.0 && th <= 1.0;
                 tmax = max(tmax, th);
             }
+        const uint32_t uq = fastok ? (uint32_t)ceil(tmax * 32768.0) + 1u : 0u;   // majority_fast
         const bool more_pass = t0 + VT_TMAX < T;
         uint64_t base[VT_TMAX] = {};   // tile body bytes of the previous chunks, per threshold
         for (uint32_t ch = 0; ch < nchunk; ch++) {
@@ -965,7 +967,7 @@ __device__ __forceinline__ void tile_epilogue_fast(const D &d, uint32_t tile, ui
 #pragma unroll
                             for (uint32_t c = 0; c < NSYM; c++) cov += hget(kq, c);
                             kc = cov > 0 && (int64_t)cov >= (int64_t)d.min_depth;   // key called (:356-358)
-                            if (kc) word = column_word(cols + (size_t)j * NSYM, cov, L, t0, tn, tmax, fastok);
+                            if (kc) word = column_word(cols + (size_t)j * NSYM, cov, L, t0, tn, uq);
                             L.vchr[j] = word;
                         }
                         uint32_t e02 = 0, e13 = 0;
@@ -998,7 +1000,7 @@ __device__ __forceinline__ void tile_epilogue_fast(const D &d, uint32_t tile, ui
                 }
             }
 #pragma unroll
-            for (int v = 0; v < 2; v++) pos_vote_fast(P[v], q0 + 16 * v < n, d.min_depth, tmax, fastok);
+            for (int v = 0; v < 2; v++) pos_vote_fast(P[v], q0 + 16 * v < n, d.min_depth, uq);
             const bool any_slow = __ballot(P[0].slow() || P[1].slow()) != 0;   // a tie or a split vote
             if (any_slow) {
                 pos_vote_slow(P[0], L, t0, tn);

@@ -13,11 +13,16 @@ from sam2consensus_amd import configs  # noqa: E402
 from sam2consensus_amd.engine import DeviceBatch, Workspace  # noqa: E402
 
 
+def configs_thresholds(wl):
+    a = configs.cli_args(wl)
+    return [float(x) for x in a[a.index("-c") + 1].split(",")] if "-c" in a else [0.25]
+
+
 def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else "c2"
     mask = int(sys.argv[2], 0) if len(sys.argv) > 2 else 0
     hb = configs.synth_batch(wl)
-    ws = Workspace(DeviceBatch(hb), [0.25, 0.5, 0.75], keep_counts=True)
+    ws = Workspace(DeviceBatch(hb), configs_thresholds(wl), keep_counts=True)
     ws.dev.ablate = mask
     for _ in range(3):
         ws.pileup()
