@@ -232,7 +232,7 @@ __device__ __forceinline__ TileIns tile_ins(const uint32_t *blk) {
 // Everything the epilogue reads lives in LDS (see vm_drain).
 template <uint32_t ICOL>   // LDS insertion columns of the kernel variant
 struct EpiLds {
-    static constexpr bool kEvents = true;
+    static constexpr bool kEvents = true, kThr = true;
     uint4 ev[PF];                      // event records ins_ev[e0 .. e0+PF)
     uint4 key[PF];                     // key records ins_kinfo[klo .. klo+PF)
     double thr[THR_MAX];               // -c thresholds, CLI order
@@ -251,11 +251,11 @@ struct EpiLds {
 // prologue), per-key emitted counts as u16 pairs
 template <uint32_t ICOL>
 struct FastLds {
-    static constexpr bool kEvents = false;
+    static constexpr bool kEvents = false, kThr = false;   // thresholds: a pass's 4 in SGPRs
     uint4 key[PF];                     // key records ins_kinfo[klo .. klo+PF)
-    double thr[THR_MAX];               // -c thresholds, CLI order
     unsigned long long acc[VT_ACC];
-    alignas(16) uint32_t fsum[VT_TMAX][WG / 64];   // body-length scan: wave totals (one 16-B read)
+    alignas(16) uint32_t fsum[2][VT_TMAX][WG / 64];   // body-length scan: wave totals (one 16-B read),
+                                                      // by chunk parity
     uint32_t bits[TILE_WORDS];         // key bitmap of the tile's words
     uint32_t wrank[TILE_WORDS];        // keys of the tile before each word
     uint32_t kem2[2][PF];              // insertion chars emitted per key: u16 pairs (thresholds 0/2, 1/3)
@@ -271,7 +271,7 @@ struct Prefetch {
     uint32_t bits;
     uint8_t fill;
 };
-template <class D>
+template <bool kThr, class D>
 __device__ __forceinline__ void prefetch_load(const D &d, uint32_t a, uint32_t n, const TileIns &ti, Prefetch &pf) {
     const uint32_t tid = threadIdx.x;
     pf.ev = make_uint4(0, 0, 0, 0);
@@ -281,7 +281,7 @@ __device__ __forceinline__ void prefetch_load(const D &d, uint32_t a, uint32_t n
     pf.fill = 0;
     if (ti.e0 + tid < ti.e1) pf.ev = ((const uint4 *)d.ins_ev)[ti.e0 + tid];
     if (ti.klo + tid < ti.khi) pf.key = ((const uint4 *)d.ins_kinfo)[ti.klo + tid];
-    if (tid < (uint32_t)d.n_thr) pf.thr = d.thresholds[tid];
+    if (kThr && tid < (uint32_t)d.n_thr) pf.thr = d.thresholds[tid];
     if (tid < (n + 31) / 32) pf.bits = d.ins_bits[(a >> 5) + tid];
     if (tid < (uint32_t)min(d.fill_len, FILL_LDS)) pf.fill = d.fill[tid];
 }
@@ -290,7 +290,8 @@ __device__ __forceinline__ void prefetch_store(const D &d, EL &L, uint32_t n, co
     const uint32_t tid = threadIdx.x;
     if constexpr (EL::kEvents) L.ev[tid] = pf.ev;
     L.key[tid] = pf.key;
-    if (tid < (uint32_t)d.n_thr) L.thr[tid] = pf.thr;
+    if constexpr (EL::kThr)
+        if (tid < (uint32_t)d.n_thr) L.thr[tid] = pf.thr;
     if (tid < (n + 31) / 32) L.bits[tid] = pf.bits;
     if (tid < (uint32_t)min(d.fill_len, FILL_LDS)) L.fill[tid] = pf.fill;
 }
@@ -778,7 +779,7 @@ static PileArgs pile_args(const s2c_dev &d) {
 //      or len(fill)), a packed 16-bit row scan (DPP) per threshold, wave totals, the tile
 //      statistics into LDS;
 //   C  byte offsets → body bytes; the last chunk writes the tile statistics.
-// Three barriers per (pass, chunk).  A thread takes positions q and q + 16 of one
+// Barriers: (1) after a pass's column votes, (2) per chunk, (3) between passes.  A thread takes positions q and q + 16 of one
 // 32-position word: their u16 counts share a histogram word.  The vote is the closed form
 // (S9), evaluated in full only in waves holding a called position whose largest count is
 // not unique or is below t·cov of the pass's largest threshold; elsewhere the char is that
@@ -831,13 +832,13 @@ __device__ __forceinline__ void pos_vote_fast(Pos &p, bool in, int32_t min_depth
     p.fl = (in ? 1u : 0u) | (called ? 2u : 0u) | (called && !fast ? 4u : 0u);
 }
 template <class EL>
-__device__ __forceinline__ void pos_vote_slow(Pos &p, const EL &L, int t0, int tn) {
+__device__ __forceinline__ void pos_vote_slow(Pos &p, const EL &L, const double (&th)[VT_TMAX], int tn) {
     uint32_t gs[NSYM];
     greater_sums(p.c, gs);
     uint32_t w = 0;
 #pragma unroll
     for (int u = 0; u < VT_TMAX; u++)
-        if (u < tn) w |= (uint32_t)L.amb[vote_mask_u32(p.c, gs, L.thr[t0 + u] * (double)p.cov)] << (8 * u);
+        if (u < tn) w |= (uint32_t)L.amb[vote_mask_u32(p.c, gs, th[u] * (double)p.cov)] << (8 * u);
     if (p.slow()) p.chars = w;
 }
 
@@ -898,7 +899,7 @@ __device__ __forceinline__ void fast_prologue(const D &d, EL &L, uint32_t *cols,
 // Vote of one insertion column (:290-311) for the pass's thresholds: the '-' count is
 // cov − Σ column (:294, signed).  Shortcut as for positions when every count is ≥ 0.
 template <class EL>
-__device__ __forceinline__ uint32_t column_word(const uint32_t *col, uint32_t cov, const EL &L, int t0, int tn,
+__device__ __forceinline__ uint32_t column_word(const uint32_t *col, uint32_t cov, const EL &L, const double (&th)[VT_TMAX], int tn,
                                                 uint32_t uq) {
     uint32_t v[NSYM], tot = 0;
 #pragma unroll
@@ -912,7 +913,7 @@ __device__ __forceinline__ uint32_t column_word(const uint32_t *col, uint32_t co
         const uint32_t mk = max(max(max(kk[0], kk[1]), kk[2]), max(max(kk[3], kk[4]), kk[5]));
         if (majority_fast(mk >> 3, cov, uq)) return sym_char(mk & 7u) * 0x01010101u;
     }
-    const uint32_t m = column_masks(col, cov, &L.thr[t0], tn);
+    const uint32_t m = column_masks(col, cov, th, tn);
     uint32_t word = 0;
 #pragma unroll
     for (int u = 0; u < VT_TMAX; u++) word |= (uint32_t)L.amb[(m >> (8 * u)) & 63u] << (8 * u);
@@ -937,14 +938,16 @@ __device__ __forceinline__ void tile_epilogue_fast(const D &d, uint32_t tile, ui
     auto hget = [&](uint32_t q, uint32_t c) { return H::get(hist, c, q); };
     for (int t0 = 0; t0 < T; t0 += VT_TMAX) {
         const int tn = min(VT_TMAX, T - t0);
-        double tmax = L.thr[t0];
+        double th[VT_TMAX];   // the pass's thresholds (uniform loads)
+#pragma unroll
+        for (int u = 0; u < VT_TMAX; u++) th[u] = u < tn ? d.thresholds[t0 + u] : 0.0;
+        double tmax = th[0];
         bool fastok = true;   // every threshold of the pass in (0, 1] (a lone symbol cannot reach t > 1)
 #pragma unroll
         for (int u = 0; u < VT_TMAX; u++)
             if (u < tn) {
-                const double th = L.thr[t0 + u];
-                fastok = fastok && th > 0.0 && th <= 1.0;
-                tmax = max(tmax, th);
+                fastok = fastok && th[u] > 0.0 && th[u] <= 1.0;
+                tmax = max(tmax, th[u]);
             }
         const uint32_t uq = fastok ? (uint32_t)ceil(tmax * 32768.0) + 1u : 0u;   // majority_fast
         const bool more_pass = t0 + VT_TMAX < T;
@@ -967,7 +970,7 @@ __device__ __forceinline__ void tile_epilogue_fast(const D &d, uint32_t tile, ui
 #pragma unroll
                             for (uint32_t c = 0; c < NSYM; c++) cov += hget(kq, c);
                             kc = cov > 0 && (int64_t)cov >= (int64_t)d.min_depth;   // key called (:356-358)
-                            if (kc) word = column_word(cols + (size_t)j * NSYM, cov, L, t0, tn, uq);
+                            if (kc) word = column_word(cols + (size_t)j * NSYM, cov, L, th, tn, uq);
                             L.vchr[j] = word;
                         }
                         uint32_t e02 = 0, e13 = 0;
@@ -1003,11 +1006,11 @@ __device__ __forceinline__ void tile_epilogue_fast(const D &d, uint32_t tile, ui
             for (int v = 0; v < 2; v++) pos_vote_fast(P[v], q0 + 16 * v < n, d.min_depth, uq);
             const bool any_slow = __ballot(P[0].slow() || P[1].slow()) != 0;   // a tie or a split vote
             if (any_slow) {
-                pos_vote_slow(P[0], L, t0, tn);
-                pos_vote_slow(P[1], L, t0, tn);
+                pos_vote_slow(P[0], L, th, tn);
+                pos_vote_slow(P[1], L, th, tn);
             }
             S2C_STAMP(d, 3);
-            lds_sync();   // (1) column vote chars, per-key emitted counts, zeroed statistics
+            if (ch == 0) lds_sync();   // (1) column vote chars, per-key emitted counts, zeroed statistics
             S2C_STAMP(d, 4);
 #pragma unroll
             for (int v = 0; v < 2; v++) asm volatile("" : "+v"(P[v].fl), "+v"(P[v].cov), "+v"(P[v].chars));
@@ -1048,10 +1051,10 @@ __device__ __forceinline__ void tile_epilogue_fast(const D &d, uint32_t tile, ui
                 if (lane == 0) {
                     const uint32_t wt = w0 + w1 + w2 + w3;
                     if (multi) {
-                        L.fsum[u][wv] = wt;
+                        L.fsum[ch & 1][u][wv] = wt;
                     } else {
 #pragma unroll
-                        for (int x = 0; x < VT_TMAX; x++) L.fsum[x][wv] = wt;
+                        for (int x = 0; x < VT_TMAX; x++) L.fsum[ch & 1][x][wv] = wt;
                     }
                 }
             }
@@ -1111,7 +1114,7 @@ __device__ __forceinline__ void tile_epilogue_fast(const D &d, uint32_t tile, ui
 #pragma unroll
             for (int u = 0; u < VT_TMAX; u++) {
                 if (u >= tn) continue;
-                const uint4 fs = *(const uint4 *)&L.fsum[u][0];   // WG / 64 == 4 waves
+                const uint4 fs = *(const uint4 *)&L.fsum[ch & 1][u][0];   // WG / 64 == 4 waves
                 const uint32_t tot = fs.x + fs.y + fs.z + fs.w;
                 const uint32_t wofs = (wv > 0 ? fs.x : 0u) + (wv > 1 ? fs.y : 0u) + (wv > 2 ? fs.z : 0u);
                 uint8_t *const ob = obase + (size_t)(t0 + u) * ostride + base[u];
@@ -1162,7 +1165,10 @@ __device__ __forceinline__ void tile_epilogue_fast(const D &d, uint32_t tile, ui
                 st[3] = at[1];              // vote errors (KeyError, :367/:381)
                 d.blk_len[j] = bl;
             }
-            if (ch + 1 < nchunk || more_pass) lds_sync();   // (3) fsum / acc / vchr / kem2 reused
+            // (3) acc / vchr / kem2 reused by the next pass.  Between chunks no barrier: chunk k+1
+            // writes the other fsum half, and chunk k+2's writes come after barrier (2) of k+1,
+            // which every wave reaches only after its phase C of chunk k.
+            if (ch + 1 == nchunk && more_pass) lds_sync();
         }
     }
     S2C_STAMP(d, 6);
@@ -1275,7 +1281,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const bool finish = flags == 0 && !(d.ablate & 4);
     const bool fastp = finish;
     Prefetch pf;   // epilogue records, in flight under the count stream
-    if (finish) prefetch_load(d, a, n, ti, pf);
+    if (finish) prefetch_load<false>(d, a, n, ti, pf);
     Corrections<NWP> corr;   // A placeholders and '-'/'N' entries of this item's records
     corr.load(d, n, uni(itc.x), uni(itc.y), uni(itc.z));
     uint32_t V[NCTR][8];
@@ -1448,7 +1454,7 @@ __global__ __launch_bounds__(WG) void k_consensus(const s2c_dev d) {
     const uint32_t a = uni(blk[0]), n = uni(blk[1]) - a;
     const TileIns ti = tile_ins(blk);
     Prefetch pf;
-    prefetch_load(d, a, n, ti, pf);
+    prefetch_load<true>(d, a, n, ti, pf);
     prefetch_store(d, L, n, pf);
     const uint32_t *cts = d.counts + a;
     const size_t Lp = d.padded_len;
