@@ -18,10 +18,12 @@ $(BUILD)/s2c_host.o: $(SRC)/s2c_host.cpp include/s2c.h | $(BUILD)
 $(BUILD)/s2c_synth.o: $(SRC)/s2c_synth.cpp include/s2c.h | $(BUILD)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
-$(BUILD)/s2c_kernels.o: $(SRC)/s2c_kernels.hip include/s2c.h | $(BUILD)
+$(BUILD)/%.o: $(SRC)/%.hip $(SRC)/s2c_common.h include/s2c.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(OUT): $(BUILD)/s2c_host.o $(BUILD)/s2c_synth.o $(BUILD)/s2c_kernels.o
+KOBJ = $(BUILD)/s2c_reads.o $(BUILD)/s2c_tile.o $(BUILD)/s2c_dense.o
+
+$(OUT): $(BUILD)/s2c_host.o $(BUILD)/s2c_synth.o $(KOBJ)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ -lz -lpthread -o $@
 
 $(BUILD):
@@ -31,8 +33,9 @@ $(BUILD):
 ISA_DIR ?= /tmp/s2c_isa
 isa:
 	mkdir -p $(ISA_DIR)
-	$(HIPCC) $(HIPFLAGS) -c $(SRC)/s2c_kernels.hip -o $(ISA_DIR)/isa.o -save-temps=obj \
-	    -Rpass-analysis=kernel-resource-usage 2> $(ISA_DIR)/resource_usage.txt
+	for f in s2c_reads s2c_tile s2c_dense; do \
+	  $(HIPCC) $(HIPFLAGS) -c $(SRC)/$$f.hip -o $(ISA_DIR)/$$f.o -save-temps=obj \
+	    -Rpass-analysis=kernel-resource-usage 2> $(ISA_DIR)/$$f.resource_usage.txt; done
 
 clean:
 	rm -rf $(BUILD) $(OUT)

@@ -16,6 +16,20 @@
  *   - no torch / HIP C++ types in signatures: device buffers are plain pointers
  *     owned by the caller (torch tensors in the Python host); the stream is a
  *     hipStream_t passed as void*.
+ *
+ * Split of the work (north_star subsystems):
+ *   host   (1) SAM/SAM.gz parse, the reference's error classes in file order, the packed
+ *              read batch: CIGAR tokens, 2-bit base planes + a non-ACGT plane in QUERY
+ *              order, POS / reference as a global coordinate, pieces bucketed by their
+ *              start word (32 positions), and the tile plan (sizes and capacities only).
+ *   device (2) k_reads: parsecigar (:46-82) + the maxdel rule (:210) per piece → runs
+ *              (seqout intervals mapped to query bases or to '-'), and the insertion
+ *              events (:73-75, :221) hashed by (position, motif) into per-tile
+ *              open-addressing tables with per-entry counts (:262-271);
+ *              k_tile / k_tile_dense: pileup (:210-218) of the runs by bit-sliced
+ *              counting, insertion columns (:276-294), vote for all thresholds (:232-253,
+ *              :344-389) and the FASTA body bytes; k_consensus: tiles whose depth or
+ *              insertion layout exceeds one workgroup.
  */
 #ifndef S2C_H
 #define S2C_H
@@ -27,7 +41,7 @@
 extern "C" {
 #endif
 
-#define S2C_ABI_VERSION 4
+#define S2C_ABI_VERSION 5
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define S2C_OK            0
@@ -50,27 +64,63 @@ int s2c_layout(int64_t *out, int n);
 /* ---- constants shared with the kernels -------------------------------------------- */
 #define S2C_NSYM          6    /* symbols '-','A','C','G','N','T' — sorted() order (:367) */
 #define S2C_POS_ALIGN    64    /* each reference starts at a multiple of this global coordinate */
-#define S2C_ITEM_WORDS   16    /* u32 words per pileup work item {a, b, chunk, tile, fix_off, x0, x1,
-                                  flags, klo, khi, e0, e1, cb0, cb1, rbase, 0} */
-#define S2C_BLOCK_WORDS  12    /* u32 words per tile {a, b, ref, flags, klo, khi, e0, e1, cb0, cb1, 0, 0} */
-#define S2C_TILE_DEEP     1    /* flags: the tile's records take several work items (HBM counts) */
-#define S2C_TILE_GENERAL  2    /* flags: more insertion columns / keys than k_pileup's LDS holds:
-                                  its counts go to HBM and k_consensus votes it */
-#define S2C_EPI_KEYS    256    /* keys per tile the k_pileup epilogue holds in LDS */
-/* insertion columns per tile the k_pileup epilogue holds in LDS, by words per tile */
-#define S2C_LDS_COLS(nwp) ((nwp) <= 16 ? 640 : ((nwp) == 32 ? 448 : 192))
-#define S2C_CODE_FILL     0    /* internal vote char of a fill position */
-#define S2C_CODE_ERR   0xFF    /* vote char where the vote hit a missing amb key (:367) */
 #define S2C_TILE_MAX   2048    /* positions per tile */
 
+/* CIGAR token word (ops[]): length << 4 | opcode, opcodes in this order */
+#define S2C_OP_M   0
+#define S2C_OP_I   1
+#define S2C_OP_D   2
+#define S2C_OP_N   3
+#define S2C_OP_S   4
+#define S2C_OP_H   5
+#define S2C_OP_P   6
+#define S2C_OP_EQ  7
+#define S2C_OP_X   8
+#define S2C_OP_LEN_MAX 0x0FFFFFFFu
+
+/* piece record pc[i] = {gpos, qh, opoff, slen | flags << 24}:
+ *   gpos  global coordinate of seqout char ka (the piece's first position)
+ *   qh    the read's first SEQ base = 16·qh in the base planes
+ *   opoff the piece's op words are [pc[i].opoff, pc[i+1].opoff): prefix words (flags),
+ *         then the read's CIGAR tokens (:58 regex matches, in order)
+ *   slen  len(SEQ) (< 2^24)                                                             */
+#define S2C_PF_X      0x01   /* SEQ holds non-ACGT chars: read the non-ACGT plane bx      */
+#define S2C_PF_RANGE  0x02   /* prefix {ka, kb}: the piece is seqout[ka, kb) (else [0, len(seqout))) */
+#define S2C_PF_INS    0x04   /* prefix {key0 lo, key0 hi, ref_off}: this piece emits its read's
+                                insertion events; key0 = ref_off + POS-1 (int64), an event at
+                                seqout index k has global key key0 + k, used when ≥ ref_off */
+#define S2C_PF_LONG   0x08   /* span > the batch's window: reached through the tile long lists */
+
+/* run record (device-written by k_reads, parallel to ops[]): {gpos, len | kind << 24, qlo, qhi} */
+#define S2C_RUN_EMPTY   0u
+#define S2C_RUN_BASES   1u   /* seqout [gpos, gpos+len) = query bases [q, q+len) (q = qhi:qlo) */
+#define S2C_RUN_DASH    2u   /* seqout '-' (D/N/P, counted: not maxdel-dropped) */
+#define S2C_RUN_XBIT   0x04u /* (kind bits) BASES run of a read with non-ACGT chars */
+#define S2C_RUN_DROP   0x08u /* (kind bits) the read's '-' are not counted (maxdel, :210) */
+#define S2C_RUN_LONG   0x10u /* (kind bits) run of a long piece: skipped by the rs window */
+
+/* tile record tiles[t][S2C_TILE_WORDS] */
+#define S2C_TILE_WORDS   16  /* {a, b, ref, flags, boff, bcap, loff, lcap, cb0, ccap, lp0, lp1, nev, 0, 0, 0} */
+#define S2C_TILE_DEEP     1  /* several work items: counts summed in HBM, voted by k_consensus */
+#define S2C_TILE_GENERAL  2  /* insertion layout beyond k_tile's LDS: voted by k_consensus */
+#define S2C_TILE_DENSE    4  /* routed to k_tile_dense (one item, no insertion keys, no long pieces) */
+#define S2C_ITEM_WORDS    4  /* work item {tile, chunk, 0, 0} */
+#define S2C_EPI_KEYS    256  /* insertion keys per tile k_tile's epilogue holds in LDS */
+/* insertion columns per tile k_tile's epilogue holds in LDS, by words per tile */
+#define S2C_LDS_COLS(nwp) ((nwp) <= 16 ? 640 : ((nwp) == 32 ? 448 : 192))
+#define S2C_DENSE_RUNS 1024  /* runs a dense tile stages in LDS */
+#define S2C_SHORT_MOTIF  16  /* motifs up to this length are hashed inline (3-bit codes) */
+#define S2C_CODE_FILL     0  /* internal vote char of a fill position */
+#define S2C_CODE_ERR   0xFF  /* vote char where the vote hit a missing amb key (:367) */
+
 /* ======================================================================================
- * Host side: SAM/SAM.gz parser → packed read batch          (replaces :147-228, :256-294)
+ * Host side: SAM/SAM.gz parser → packed read batch          (replaces :147-228, :284-294)
  * ======================================================================================
- * The parser reproduces the reference's record handling exactly (header pass :149-172,
- * record filter :195, RNAME/POS :200-201, parsecigar :46-82, maxdel rule :210, error
- * classes in file order) and emits the packed batch: every read's seqout (:64-81) cut
- * at the global 32-position grid into word-major records of 3 bit-planes, insertion
- * events, the pileup / consensus work plan, and a host-side read-piece table.
+ * The parser reproduces the reference's record handling and error classes exactly
+ * (header pass :149-172, record filter :195, RNAME/POS :200-201, CIGAR tokens :58-59, the
+ * index/symbol checks of :211-218 in file order, insertion checks :284-294) and emits the
+ * packed batch.  It does NOT expand CIGARs: runs, '-' and insertion grouping are device
+ * work (k_reads).
  */
 typedef struct s2c_parser s2c_parser;
 typedef struct s2c_batch  s2c_batch;
@@ -79,9 +129,9 @@ typedef struct s2c_batch  s2c_batch;
 int  s2c_parser_new(int maxdel_active, int64_t maxdel, s2c_parser **out);
 /* Feed raw SAM text (any chunking; lines may straddle calls). */
 int  s2c_parser_feed(s2c_parser *p, const char *buf, size_t len);
-/* Parse a whole file; ".gz" suffix → zlib (:111-114). */
+/* Parse a whole file; ".gz" suffix → zlib (:111-114).  Read in bounded windows. */
 int  s2c_parser_feed_file(s2c_parser *p, const char *path);
-/* End of input: reformat-phase checks (:284-294), global layout and work plan. */
+/* End of input: reformat-phase checks (:284-294), global layout, bucketing, tile plan. */
 int  s2c_parser_finish(s2c_parser *p, s2c_batch **out);
 void s2c_parser_free(s2c_parser *p);
 
@@ -93,67 +143,47 @@ typedef struct {
     int64_t lines_total;       /* all lines seen (:194 counts from -header_lines) */
     int64_t reads_mapped;      /* records passing :195 */
     int64_t aligned_bases;     /* A = Σ len(seqout) over mapped reads (the metric's unit) */
-    int64_t query_bases;       /* Q = M/=/X + I bases packed (B_alg 0.5·Q) */
-    int64_t n_reads;           /* read pieces (after POS=0 wrap splitting, :212) */
-    int64_t n_ops;             /* effective op words (B_alg 4·K) */
-    int64_t n_recs;            /* (piece, 32-position word) seqout records */
-    int64_t chunk_recs;        /* records per word per work item (deep tiles take several) */
+    int64_t query_bases;       /* Q = M/=/X + I bases consumed (B_alg 0.5·Q) */
+    int64_t n_pieces;          /* pieces (a read, or its two parts around the POS<=0 wrap, :212) */
+    int64_t n_ops;             /* op words (prefix words + CIGAR tokens) = run slots */
+    int64_t n_tokens;          /* CIGAR tokens other than S/H (B_alg 4·K) */
+    int64_t n_qwords;          /* u32 words per base plane */
+    int64_t n_words;           /* padded_len / 32 */
+    int64_t n_tiles;           /* tiles (consensus / body blocks, never straddle a reference) */
+    int64_t n_items;           /* k_tile work items (non-dense tiles; deep tiles have several) */
+    int64_t n_dense;           /* dense tiles (k_tile_dense; k_tile when len(-f) != 1) */
+    int64_t n_deep;            /* tiles voted by k_consensus (deep or general) */
+    int64_t n_long;            /* long-list entries (tile, run slot of a long piece) */
+    int64_t kwin;              /* window: a short piece spans <= kwin + 1 words */
+    int64_t tile_max;          /* max positions of any tile (<= 2048) */
+    int64_t chunk;             /* candidate run slots per word per work item */
     int64_t n_ins;             /* insertion events kept (key in [0, LN), non-empty motif) */
     int64_t n_ins_bases;       /* Σ motif lengths */
-    int64_t n_ins_words;       /* u32 words of packed motif bases */
-    int64_t n_keys;            /* distinct insertion keys (:262-271 dict keys) */
-    int64_t n_cols;            /* insertion columns = Σ over keys of the longest motif (:278-281) */
-    int64_t n_items;           /* pileup work items */
-    int64_t n_blocks;          /* tiles = consensus/assembly blocks (never straddle a ref) */
-    int64_t tile_max;          /* max positions of any tile (≤ 2048) */
-    int64_t n_deep;            /* tiles voted by k_consensus: split over several work items
-                                  (S2C_TILE_DEEP) or beyond k_pileup's LDS (S2C_TILE_GENERAL) */
-    int64_t n_exc;             /* seqout '-' / 'N' entries (kept out of the 2-bit records) */
-    int64_t n_fix;             /* u32 words of per-item A-placeholder counts */
-    int64_t n_iwr;             /* u32 words of per-item word record ranges (n_items · words · 2) */
+    int64_t n_bkt;             /* hash-table slots over all tiles (Σ bcap) */
+    int64_t n_lng;             /* long-motif event slots over all tiles (Σ lcap) */
+    int64_t n_cols;            /* insertion column slots over all tiles (Σ ccap ≥ Σ columns) */
+    int64_t runs_max;          /* most run slots any tile's window holds */
 } s2c_batch_info;
 
 typedef struct {               /* host pointers into the batch (valid until s2c_batch_free) */
     const int64_t  *ref_len;   /* [n_refs] */
     const int64_t  *ref_off;   /* [n_refs] global coordinate of position 0 */
-    const int64_t  *ref_cov_reads; /* [n_refs] pileup records per ref (0 ⇒ Σcov may be 0) */
-    const uint32_t *rd_pos;    /* [n_reads]   global coordinate of seqout char 0 (file order) */
-    const uint32_t *rd_op;     /* [n_reads+1] op offset (CSR) */
-    const uint32_t *rd_span;   /* [n_reads]   seqout length (bits 0-30); bit31 = '-' not counted (maxdel :210) */
-    const uint32_t *ops;       /* [n_ops]     (len << 1) | cls, cls 0 = M/=/X, 1 = D/N/P */
-    const uint32_t *wrec;      /* [padded_len/32 + 1] CSR: records of global word W = [wrec[W], wrec[W+1]) */
-    const uint32_t *recs;      /* [n_recs][2] bit-planes {b0, b1} of the 32 positions' bases
-                                  (b1·2+b0: 0 A, 1 C, 2 G, 3 T).  A position without an A/C/G/T
-                                  entry — outside the read piece, a '-' of a maxdel-dropped read
-                                  (:214-218), or a '-' / 'N' (those are in exc) — holds 0 (A) and
-                                  is subtracted again through fix */
-    const uint32_t *fix;       /* [n_fix] per work item (from item word 4), 16 u32 per word of its
-                                  tile: u32 i of word w = the A placeholders among the item's
-                                  records at tile positions 32w+i (low u16) and 32w+i+16 (high) */
-    const uint32_t *exc;       /* [n_exc] the counted seqout '-' and 'N' of each work item (item
-                                  words 5-6): (position − tile start) << 1 | is_N */
-    const uint32_t *ins_key;   /* [n_keys]    global coordinate of each key (:74), ascending */
-    const uint32_t *ins_koff;  /* [n_keys+1]  events of key k = [koff[k], koff[k+1]) (file order) */
-    const uint32_t *ins_kcol;  /* [n_keys+1]  columns of key k = [kcol[k], kcol[k+1]) */
-    const uint32_t *ins_off;   /* [n_ins+1]   nibble offset of each event's motif in ins_bases */
-    const uint32_t *ins_bases; /* [n_ins_words] motif symbol codes, 8 nibbles per word */
-    const uint32_t *ins_ekey;  /* [n_ins]     key index of each event */
-    const uint32_t *ins_ev;    /* [n_ins][4]  {column offset in the key's tile, motif length,
-                                                nibble offset, first 8 motif nibbles} */
-    const uint32_t *ins_kinfo; /* [n_keys][4] {position, first column, columns, 0} */
-    const uint32_t *ins_bits;  /* [padded_len/32] bit p: position p is a key */
-    const uint32_t *ins_rank;  /* [padded_len/32+1] keys before 32-position word W */
-    const uint32_t *items;     /* [n_items][S2C_ITEM_WORDS] pileup work items {a, b, chunk, tile,
-                                  fix_off, x0, x1, flags, klo, khi, e0, e1, cb0, cb1, rbase, 0}:
-                                  tile [a, b), records chunk `chunk` of each word, its placeholder
-                                  words and '-'/'N' entries [x0, x1), a copy of the tile's block
-                                  words 3-9, and wrec[a/32] (the item's first record) */
-    const uint32_t *iwr;       /* [n_items][nwp][2] per item and tile word w: its record range
-                                  {r0, r1} (nwp = words of the widest tile rounded up to a power
-                                  of two ≥ 8; words past the tile: {0, 0}) */
-    const uint32_t *blocks;    /* [n_blocks][S2C_BLOCK_WORDS] tiles {g_begin, g_end, ref, flags, then the
-                                  tile's keys [klo,khi), events [e0,e1), columns [cb0,cb1)} */
-    const uint32_t *deep;      /* [n_deep] indices of the tiles k_consensus votes (flags != 0) */
+    const int64_t  *ref_cov_reads; /* [n_refs] pieces with a counted char (0 ⇒ Σcov == 0, :334-341) */
+    const uint32_t *pc;        /* [n_pieces+1][4] pieces sorted by start word (+ sentinel {0,0,n_ops,0}) */
+    const uint32_t *ops;       /* [n_ops] op words: prefix words, CIGAR tokens */
+    const uint32_t *bq;        /* [n_qwords][2] base planes {p0, p1} of 32 query bases:
+                                  A 00, C 01, G 10, T 11 (p1 p0); non-ACGT chars 00 */
+    const uint32_t *bx;        /* [n_qwords] 1 = non-ACGT char: 'N' (p0 0) or '-' (p0 1) */
+    const uint32_t *rs;        /* [n_words+1] run slots of the pieces starting in words [W0, W1)
+                                  are [rs[W0], rs[W1]); a run covering word W belongs to a short
+                                  piece starting in [W-kwin, W] or is listed in lp */
+    const uint32_t *tiles;     /* [n_tiles][S2C_TILE_WORDS] */
+    const uint32_t *items;     /* [n_items][S2C_ITEM_WORDS] */
+    const uint32_t *dense;     /* [n_dense][S2C_ITEM_WORDS] items of the dense tiles */
+    const uint32_t *deep;      /* [n_deep] tiles k_consensus votes */
+    const uint32_t *lp;        /* [n_long] run slots of the long pieces overlapping each tile:
+                                  tile t's are lp[tiles[t].lp0 .. tiles[t].lp1) */
+    const uint32_t *wtile;     /* [n_words] tile of each 32-position word (0xFFFFFFFF: padding) */
 } s2c_batch_arrays;
 
 int  s2c_batch_info_get(const s2c_batch *b, s2c_batch_info *out);
@@ -200,15 +230,14 @@ int s2c_synth_write(const s2c_synth_spec *spec, const char *path, int64_t *n_rea
  * ====================================================================================== */
 typedef struct {
     /* ---- packed batch (device copies of s2c_batch_arrays) ---- */
-    const uint32_t *wrec, *recs;   /* word-major seqout records (s2c_batch_arrays) */
-    const uint32_t *fix, *exc;     /* A-placeholder counts, '-'/'N' entries (s2c_batch_arrays) */
-    const uint32_t *iwr;           /* per-item word record ranges (s2c_batch_arrays) */
-    const uint32_t *items, *blocks, *deep;
-    const uint32_t *ins_ev, *ins_kinfo, *ins_bases, *ins_bits;   /* (s2c_batch_arrays) */
-    int64_t n_recs, chunk_recs, n_items, n_blocks, n_deep, n_keys, n_cols, padded_len, n_exc;
-    int32_t tile_max, n_refs;
+    const uint32_t *pc, *ops, *bq, *bx, *rs;
+    const uint32_t *tiles, *items, *dense, *deep, *lp, *wtile;
+    int64_t n_pieces, n_ops, n_qwords, n_tiles, n_items, n_dense, n_deep, padded_len, chunk;
+    int32_t kwin, tile_max;
 
-    /* ---- options (:117-138) ---- */
+    /* ---- options (:102, :117-138) ---- */
+    int32_t  maxdel_active;    /* 0 when -d was given (Python 2 int <= str, :210) */
+    int32_t  maxdel;           /* 150 (:102) */
     const double *thresholds;  /* [T] device copy of -c values, CLI order */
     int32_t  n_thr;
     int32_t  min_depth;        /* -m */
@@ -217,51 +246,51 @@ typedef struct {
     const uint8_t *fill;       /* [fill_len] device copy of -f bytes */
 
     /* ---- workspace (caller allocates; sizes from s2c_workspace_sizes) ---- */
-    uint32_t *counts;          /* [6][padded_len] pileup counts of deep tiles (SoA by symbol) */
-    uint32_t *ins_cols;        /* [n_cols][6] column counts of tiles whose columns exceed LDS */
-    uint32_t *ins_cnt;         /* [T][n_keys][4] {chars emitted, first column, columns, 0}: tiles
-                                  with > 256 keys or HBM columns only */
-    uint8_t  *ins_chr;         /* [T][n_cols] column vote chars, same tiles only */
+    uint32_t *runs;            /* [n_ops][4] run records (k_reads) */
+    uint32_t *ibkt;            /* [n_bkt][4] per-tile hash tables {key lo, key hi, count, 0}; zero
+                                  before the first run, left zero by every run */
+    uint32_t *ilong;           /* [n_lng][4] long-motif events {pos, len, q lo, q hi} */
+    uint32_t *ilong_n;         /* [n_tiles] long-motif events per tile (zero, left zero) */
+    uint32_t *counts;          /* [6][padded_len] counts of deep / general tiles (SoA by symbol) */
+    uint32_t *ins_cols;        /* [n_cols][6] column counts of general tiles */
+    uint8_t  *ins_chr;         /* [T][n_cols] column vote chars of general tiles */
+    int64_t   n_cols;
 
     /* ---- outputs ---- */
-    uint64_t *tile_stats;      /* [T][n_blocks][4] {sumcov, len, nondash, vote_errors} per tile
+    uint64_t *tile_stats;      /* [T][n_tiles][4] {sumcov, len, nondash, vote_errors} per tile
                                   (:352-397; summed per reference by the host) */
-    uint64_t *blk_len;         /* [T][n_blocks] FASTA body bytes of (t, tile) */
+    uint64_t *blk_len;         /* [T][n_tiles] FASTA body bytes of (t, tile) */
     uint8_t  *out;             /* FASTA bodies (:350-389): tile (t, tile) at
                                   t·(F·padded_len + n_cols) + F·a + cb0, F = max(1, len(fill)),
-                                  a = the tile's first position, cb0 its first insertion column;
+                                  a = the tile's first position, cb0 its column slot base;
                                   blk_len bytes each.  A reference's body for threshold t is its
                                   tiles' pieces in order. */
     int64_t   out_cap;         /* ≥ T·(F·padded_len + n_cols) */
-
-    /* ---- diagnostics, 0 in the product: bit 1 skips counting, bit 2 loads without
-     *      counting, bit 8 skips the
-     *      histogram flush, 0x200 skips the insertion columns, 0x800 returns at once
-     *      (timing ablations, results wrong: scripts/ablate.py); bit 4 makes every tile store
-     *      its counts to `counts` (sized 6*padded_len*4) instead of voting (counts parity
-     *      tests); 0x100 writes phase timestamps to `counts` (scripts/phases.py) ---- */
-    int32_t   ablate;
-    int32_t   reserved;
 } s2c_dev;
 
 /* Sizes (bytes) of every workspace / output buffer for a batch and T thresholds. */
 typedef struct {
-    int64_t counts, ins_cols, ins_cnt, ins_chr, blk_len, tile_stats;
+    int64_t runs, ibkt, ilong, ilong_n, counts, ins_cols, ins_chr, blk_len, tile_stats;
     int64_t out_per_fill, out_fixed;   /* out bytes = out_per_fill·max(1, len(fill)) + out_fixed */
 } s2c_ws_sizes;
 int s2c_workspace_sizes(const s2c_batch_info *info, int32_t n_thr, s2c_ws_sizes *out);
 
-/* Stage order (s2c_run): s2c_pileup → s2c_consensus.
- * (2) pileup per tile; for tiles holding their whole depth in one work item also (3) the
- * insertion columns, (4) the vote (all thresholds, IUPAC, min-depth/fill, insertion
- * chars, tile statistics) and the tile's FASTA body bytes
- *                                          (:206-221, :232-253, :256-311, :344-397) */
+/* Stage order (s2c_run): s2c_reads → s2c_pileup → s2c_consensus, one stream.
+ * (2) parsecigar + maxdel per piece → runs; insertion events → per-tile hash tables
+ *                                                           (:46-82, :210, :221, :262-271) */
+int s2c_reads(const s2c_dev *d, void *stream);
+/* (2)-(4) per tile: pileup of the runs, insertion columns, vote (all thresholds, IUPAC,
+ * min-depth/fill), tile statistics and FASTA body bytes; deep / general tiles leave their
+ * counts in HBM                         (:210-218, :232-253, :256-311, :344-397) */
 int s2c_pileup(const s2c_dev *d, void *stream);
-/* (3)+(4) and the bodies for deep tiles (records split over several work items, counts
- * summed in HBM)                                   (:232-253, :256-311, :344-397) */
+/* (3)+(4) and the bodies of deep / general tiles               (:232-253, :256-311, :344-397) */
 int s2c_consensus(const s2c_dev *d, void *stream);
-/* both, in order, on one stream (graph-capturable: no allocation, no sync) */
+/* all three, in order, on one stream (graph-capturable: no allocation, no sync) */
 int s2c_run(const s2c_dev *d, void *stream);
+
+/* Diagnostics (tests only, not part of the product path): s2c_pileup with every tile's
+ * counts stored to d->counts ([6][padded_len] u32) and no vote. */
+int s2c_pileup_counts(const s2c_dev *d, void *stream);
 
 #ifdef __cplusplus
 }

@@ -25,9 +25,15 @@ S2C_ERR_LIMIT = -13
 
 S2C_NSYM = 6
 S2C_POS_ALIGN = 64
-S2C_ITEM_WORDS = 16
-S2C_BLOCK_WORDS = 12
+S2C_TILE_WORDS = 16
+S2C_ITEM_WORDS = 4
 S2C_CODE_FILL = 0
+S2C_SHORT_MOTIF = 16
+S2C_TILE_DEEP, S2C_TILE_GENERAL, S2C_TILE_DENSE = 1, 2, 4
+S2C_PF_X, S2C_PF_RANGE, S2C_PF_INS, S2C_PF_LONG = 1, 2, 4, 8
+S2C_RUN_EMPTY, S2C_RUN_BASES, S2C_RUN_DASH = 0, 1, 2
+S2C_RUN_XBIT, S2C_RUN_DROP, S2C_RUN_LONG = 4, 8, 16
+OPS = "MIDNSHP=X"   # opcode order of the token words (len << 4 | opcode)
 
 # reference exception classes (SURVEY.md §5 "Failure detection")
 _EXC = {S2C_ERR_KEY: KeyError, S2C_ERR_INDEX: IndexError, S2C_ERR_VALUE: ValueError,
@@ -45,9 +51,9 @@ class S2CError(RuntimeError):
 class BatchInfo(C.Structure):
     _fields_ = [(n, C.c_int64) for n in (
         "n_refs", "total_len", "padded_len", "header_lines", "lines_total", "reads_mapped",
-        "aligned_bases", "query_bases", "n_reads", "n_ops", "n_recs", "chunk_recs", "n_ins",
-        "n_ins_bases", "n_ins_words", "n_keys", "n_cols", "n_items", "n_blocks", "tile_max",
-        "n_deep", "n_exc", "n_fix", "n_iwr")]
+        "aligned_bases", "query_bases", "n_pieces", "n_ops", "n_tokens", "n_qwords", "n_words",
+        "n_tiles", "n_items", "n_dense", "n_deep", "n_long", "kwin", "tile_max", "chunk",
+        "n_ins", "n_ins_bases", "n_bkt", "n_lng", "n_cols", "runs_max")]
 
 
 _P64 = C.POINTER(C.c_int64)
@@ -55,13 +61,8 @@ _P32 = C.POINTER(C.c_uint32)
 
 
 class BatchArrays(C.Structure):
-    _fields_ = [("ref_len", _P64), ("ref_off", _P64), ("ref_cov_reads", _P64),
-                ("rd_pos", _P32), ("rd_op", _P32), ("rd_span", _P32), ("ops", _P32),
-                ("wrec", _P32), ("recs", _P32), ("fix", _P32), ("exc", _P32),
-                ("ins_key", _P32), ("ins_koff", _P32), ("ins_kcol", _P32), ("ins_off", _P32),
-                ("ins_bases", _P32), ("ins_ekey", _P32), ("ins_ev", _P32), ("ins_kinfo", _P32),
-                ("ins_bits", _P32), ("ins_rank", _P32),
-                ("items", _P32), ("iwr", _P32), ("blocks", _P32), ("deep", _P32)]
+    _fields_ = [("ref_len", _P64), ("ref_off", _P64), ("ref_cov_reads", _P64)] + \
+        [(n, _P32) for n in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile")]
 
 
 class SynthSpec(C.Structure):
@@ -77,24 +78,22 @@ _VP = C.c_void_p
 
 class Dev(C.Structure):
     """Mirror of ``s2c_dev`` (include/s2c.h)."""
-    _fields_ = [
-        ("wrec", _VP), ("recs", _VP), ("fix", _VP), ("exc", _VP), ("iwr", _VP),
-        ("items", _VP), ("blocks", _VP), ("deep", _VP),
-        ("ins_ev", _VP), ("ins_kinfo", _VP), ("ins_bases", _VP), ("ins_bits", _VP),
-        ("n_recs", C.c_int64), ("chunk_recs", C.c_int64),
-        ("n_items", C.c_int64), ("n_blocks", C.c_int64), ("n_deep", C.c_int64),
-        ("n_keys", C.c_int64), ("n_cols", C.c_int64), ("padded_len", C.c_int64), ("n_exc", C.c_int64),
-        ("tile_max", C.c_int32), ("n_refs", C.c_int32),
+    _fields_ = [(n, _VP) for n in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile")] + \
+        [(n, C.c_int64) for n in ("n_pieces", "n_ops", "n_qwords", "n_tiles", "n_items", "n_dense", "n_deep",
+                                  "padded_len", "chunk")] + [
+        ("kwin", C.c_int32), ("tile_max", C.c_int32),
+        ("maxdel_active", C.c_int32), ("maxdel", C.c_int32),
         ("thresholds", _VP), ("n_thr", C.c_int32), ("min_depth", C.c_int32),
         ("fill_len", C.c_int32), ("fill_nondash", C.c_int32), ("fill", _VP),
-        ("counts", _VP), ("ins_cols", _VP), ("ins_cnt", _VP), ("ins_chr", _VP),
-        ("tile_stats", _VP), ("blk_len", _VP), ("out", _VP), ("out_cap", C.c_int64),
-        ("ablate", C.c_int32), ("reserved", C.c_int32)]
+        ("runs", _VP), ("ibkt", _VP), ("ilong", _VP), ("ilong_n", _VP), ("counts", _VP),
+        ("ins_cols", _VP), ("ins_chr", _VP), ("n_cols", C.c_int64),
+        ("tile_stats", _VP), ("blk_len", _VP), ("out", _VP), ("out_cap", C.c_int64)]
 
 
 class WsSizes(C.Structure):
     _fields_ = [(n, C.c_int64) for n in (
-        "counts", "ins_cols", "ins_cnt", "ins_chr", "blk_len", "tile_stats", "out_per_fill", "out_fixed")]
+        "runs", "ibkt", "ilong", "ilong_n", "counts", "ins_cols", "ins_chr", "blk_len", "tile_stats",
+        "out_per_fill", "out_fixed")]
 
 
 # every symbol include/s2c.h declares (tests/test_lib.py checks the export table)
@@ -103,7 +102,7 @@ EXPORTS = [
     "s2c_parser_new", "s2c_parser_feed", "s2c_parser_feed_file", "s2c_parser_finish", "s2c_parser_free",
     "s2c_batch_info_get", "s2c_batch_arrays_get", "s2c_batch_ref_name", "s2c_batch_free",
     "s2c_parsecigar", "s2c_synth_feed", "s2c_synth_write",
-    "s2c_workspace_sizes", "s2c_pileup", "s2c_consensus", "s2c_run",
+    "s2c_workspace_sizes", "s2c_reads", "s2c_pileup", "s2c_consensus", "s2c_run", "s2c_pileup_counts",
 ]
 
 
@@ -136,7 +135,9 @@ def _load():
         "s2c_synth_feed": (C.c_int, [C.POINTER(SynthSpec), _VP, C.POINTER(C.c_int64)]),
         "s2c_synth_write": (C.c_int, [C.POINTER(SynthSpec), C.c_char_p, C.POINTER(C.c_int64)]),
         "s2c_workspace_sizes": (C.c_int, [C.POINTER(BatchInfo), C.c_int32, C.POINTER(WsSizes)]),
+        "s2c_reads": (C.c_int, [C.POINTER(Dev), _VP]),
         "s2c_pileup": (C.c_int, [C.POINTER(Dev), _VP]),
+        "s2c_pileup_counts": (C.c_int, [C.POINTER(Dev), _VP]),
         "s2c_consensus": (C.c_int, [C.POINTER(Dev), _VP]),
         "s2c_run": (C.c_int, [C.POINTER(Dev), _VP]),
     }
@@ -154,8 +155,8 @@ def _layout_check():
     """Compare the ctypes mirrors with the C structs (sizeof / offsetof)."""
     buf = (C.c_int64 * 16)()
     n = lib.s2c_layout(buf, 16)
-    want = [C.sizeof(Dev), Dev.tile_max.offset, Dev.thresholds.offset, Dev.fill.offset,
-            Dev.counts.offset, Dev.ins_chr.offset, Dev.tile_stats.offset, Dev.out_cap.offset,
+    want = [C.sizeof(Dev), Dev.kwin.offset, Dev.thresholds.offset, Dev.fill.offset,
+            Dev.runs.offset, Dev.n_cols.offset, Dev.tile_stats.offset, Dev.out_cap.offset,
             C.sizeof(SynthSpec), SynthSpec.seed.offset, C.sizeof(BatchInfo), C.sizeof(BatchArrays),
             C.sizeof(WsSizes)]
     got = list(buf[:n])

@@ -21,6 +21,7 @@ class Parser:
     reference's behaviour when ``-d`` is given at all (:102, :210)."""
 
     def __init__(self, maxdel_active=True, maxdel=150):
+        self.maxdel_active, self.maxdel = bool(maxdel_active), int(maxdel)
         self._p = C.c_void_p()
         L.check(lib.s2c_parser_new(1 if maxdel_active else 0, int(maxdel), C.byref(self._p)))
 
@@ -33,7 +34,9 @@ class Parser:
     def finish(self) -> "HostBatch":
         b = C.c_void_p()
         L.check(lib.s2c_parser_finish(self._p, C.byref(b)))
-        return HostBatch(b)
+        hb = HostBatch(b)
+        hb.maxdel_active, hb.maxdel = self.maxdel_active, self.maxdel   # the device applies :210
+        return hb
 
     def close(self):
         if self._p:
@@ -67,40 +70,29 @@ class HostBatch:
         self.ref_len = _view(a.ref_len, i.n_refs, np.int64)
         self.ref_off = _view(a.ref_off, i.n_refs, np.int64)
         self.ref_reads = _view(a.ref_cov_reads, i.n_refs, np.int64)
-        # host-side read-piece table (file order)
-        self.rd_pos = _view(a.rd_pos, i.n_reads, np.uint32)
-        self.rd_op = _view(a.rd_op, i.n_reads + 1, np.uint32)
-        self.rd_span = _view(a.rd_span, i.n_reads, np.uint32)
+        # pieces bucketed by start word (+ sentinel), their op words, the query base planes
+        self.pc = _view(a.pc, 4 * (i.n_pieces + 1), np.uint32).reshape(-1, 4)
         self.ops = _view(a.ops, i.n_ops, np.uint32)
-        # word-major seqout records (what the pileup kernel reads)
-        self.wrec = _view(a.wrec, i.padded_len // 32 + 1, np.uint32)
-        self.recs = _view(a.recs, 2 * i.n_recs, np.uint32).reshape(-1, 2)
-        # per work item: A-placeholder counts (16 u32 u16-pairs per tile word) and the
-        # seqout '-'/'N' entries
-        self.fix = _view(a.fix, i.n_fix, np.uint32)
-        self.exc = _view(a.exc, i.n_exc, np.uint32)
-        self.iwr = _view(a.iwr, i.n_iwr, np.uint32)
-        # insertion events grouped by key (keys ascending)
-        nw = i.padded_len // 32
-        self.ins_key = _view(a.ins_key, i.n_keys, np.uint32)
-        self.ins_koff = _view(a.ins_koff, i.n_keys + 1, np.uint32)
-        self.ins_kcol = _view(a.ins_kcol, i.n_keys + 1, np.uint32)
-        self.ins_off = _view(a.ins_off, i.n_ins + 1, np.uint32)
-        self.ins_bases = _view(a.ins_bases, i.n_ins_words, np.uint32)
-        self.ins_ekey = _view(a.ins_ekey, i.n_ins, np.uint32)
-        self.ins_ev = _view(a.ins_ev, 4 * i.n_ins, np.uint32).reshape(-1, 4)
-        self.ins_kinfo = _view(a.ins_kinfo, 4 * i.n_keys, np.uint32).reshape(-1, 4)
-        self.ins_bits = _view(a.ins_bits, nw, np.uint32)
-        self.ins_rank = _view(a.ins_rank, nw + 1, np.uint32)
+        self.bq = _view(a.bq, 2 * i.n_qwords, np.uint32).reshape(-1, 2)
+        self.bx = _view(a.bx, i.n_qwords, np.uint32)
+        self.rs = _view(a.rs, i.n_words + 1, np.uint32)
+        # tile plan
+        self.tiles = _view(a.tiles, i.n_tiles * L.S2C_TILE_WORDS, np.uint32).reshape(-1, L.S2C_TILE_WORDS)
         self.items = _view(a.items, i.n_items * L.S2C_ITEM_WORDS, np.uint32).reshape(-1, L.S2C_ITEM_WORDS)
-        self.blocks = _view(a.blocks, i.n_blocks * L.S2C_BLOCK_WORDS, np.uint32).reshape(-1, L.S2C_BLOCK_WORDS)
+        self.dense = _view(a.dense, i.n_dense * L.S2C_ITEM_WORDS, np.uint32).reshape(-1, L.S2C_ITEM_WORDS)
         self.deep = _view(a.deep, i.n_deep, np.uint32)
+        self.lp = _view(a.lp, i.n_long, np.uint32)
+        self.wtile = _view(a.wtile, i.n_words, np.uint32)
         self.names = [lib.s2c_batch_ref_name(self._b, k).decode("latin-1") for k in range(i.n_refs)]
-        # per-ref block ranges (blocks are emitted ref by ref, in header order)
-        nb = np.bincount(self.blocks[:, 2].astype(np.int64), minlength=i.n_refs) if i.n_blocks else \
+        # per-ref tile ranges (tiles are emitted ref by ref, in header order)
+        nb = np.bincount(self.tiles[:, 2].astype(np.int64), minlength=i.n_refs) if i.n_tiles else \
             np.zeros(i.n_refs, dtype=np.int64)
         self.ref_nblocks = nb.astype(np.int64)
         self.ref_first_block = (np.cumsum(nb) - nb).astype(np.int64)
+
+    @property
+    def blocks(self):
+        return self.tiles
 
     @property
     def aligned_bases(self):

@@ -24,6 +24,9 @@ CONFIGS = {
     "c4u": dict(n_refs=1, ref_len=16569, depth=100000.0, args=[], prefix="chrM"),
     "c5": dict(n_refs=1, ref_len=64_444_167, depth=30.0, del_frac=0.01, del_max=5, long_del_frac=0.001,
                args=["-d", "150"], prefix="chr20_"),
+    # C5 without -d: the maxdel filter (:210) is active, the long-deletion reads' '-' are dropped
+    "c5nd": dict(n_refs=1, ref_len=64_444_167, depth=30.0, del_frac=0.01, del_max=5, long_del_frac=0.001,
+                 args=[], prefix="chr20_"),
 }
 SEED = 20260115
 

@@ -1,0 +1,247 @@
+// s2c_common.h — device helpers shared by the HIP kernels of libs2c.so (gfx950).
+//
+// IUPAC table (:317-329), the closed-form vote (:241-251, :359-366), wave reductions,
+// LDS-only barriers, and the bit-sliced Harley–Seal counters of the pileup.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/s2c.h"
+
+int s2c_set_error(int code, const std::string &msg);
+
+namespace s2c {
+
+constexpr int WG = 256;
+constexpr uint32_t NSYM = S2C_NSYM;
+constexpr int VT_TMAX = 4;        // thresholds per epilogue pass (one vote-char word per column)
+constexpr int THR_MAX = 256;      // -c values supported
+constexpr int FILL_LDS = 64;      // -f bytes staged in LDS (longer fills read HBM)
+constexpr uint32_t FLUSH_RECS = 248;   // records per lane between counter flushes (8-bit counters)
+
+// ----------------------------------------------------------------- IUPAC table (:317-329)
+// mask bit i = symbol "-ACGNT"[i]; value = output char, 0xFF where the reference's amb
+// dict has no key (mask 0 → KeyError '' ; {A,C,G,N,T} → KeyError 'ACGNT').
+struct AmbTable {
+    uint8_t v[64];
+    constexpr AmbTable() : v{} {
+        for (int m = 0; m < 64; m++) {
+            const bool dash = m & 1, n = m & 16;
+            const int b = ((m >> 1) & 1) | (((m >> 2) & 1) << 1) | (((m >> 3) & 1) << 2) | (((m >> 5) & 1) << 3);
+            // b: bit0 A, bit1 C, bit2 G, bit3 T
+            const char iupac[16] = {0, 'A', 'C', 'M', 'G', 'R', 'S', 'V', 'T', 'W', 'Y', 'H', 'K', 'D', 'B', 'N'};
+            uint8_t c = 0;
+            if (m == 0) c = 0xFF;
+            else if (b == 0) c = (dash && n) ? 'n' : (dash ? '-' : 'N');
+            else if (b == 15) c = (n && !dash) ? 0xFF : 'N';
+            else {
+                c = (uint8_t)iupac[b];
+                if (dash || n) c = (uint8_t)(c + ('a' - 'A'));
+            }
+            v[m] = c;
+        }
+    }
+};
+constexpr AmbTable AMB{};
+
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for
+// its global stores (__syncthreads also drains vmcnt, i.e. waits for every outstanding
+// store of the wave).  Global data shared inside a workgroup waits explicitly first.
+__device__ __forceinline__ void lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+// s_waitcnt vmcnt(0) as a real S_WAITCNT (the compiler's wait tracking sees it)
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+}  // namespace s2c
+
+extern "C" __device__ __attribute__((const)) unsigned long long __ockl_wfred_add_u64(unsigned long long);
+extern "C" __device__ __attribute__((const)) unsigned int __ockl_wfred_add_u32(unsigned int);
+extern "C" __device__ unsigned int __ockl_wfscan_add_u32(unsigned int, bool);   // (x, inclusive)
+extern "C" __device__ unsigned int __ockl_wfred_max_u32(unsigned int);
+
+namespace s2c {
+
+// Sum over the wave's active lanes, every lane gets it (the device library's DPP reduction).
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+    if constexpr (sizeof(T) == 8) return (T)__ockl_wfred_add_u64((unsigned long long)v);
+    else return (T)__ockl_wfred_add_u32((unsigned int)v);
+}
+
+// Closed form of the group-sort vote (proven equal to :241-251 +
+// :359-366 in tests/test_oracle.py): symbol i is taken iff c_i != 0 and the sum of the
+// counts strictly greater than c_i is < t·cov (fp64 product, exact integer compare).
+template <typename T, typename S>
+__device__ __forceinline__ void greater_sums(const T (&c)[NSYM], S (&s)[NSYM]) {
+#pragma unroll
+    for (int i = 0; i < (int)NSYM; i++) {
+        S a = 0;
+#pragma unroll
+        for (int j = 0; j < (int)NSYM; j++) a += (c[j] > c[i]) ? (S)c[j] : (S)0;
+        s[i] = a;
+    }
+}
+template <typename T, typename S>
+__device__ __forceinline__ uint32_t vote_mask(const T (&c)[NSYM], const S (&s)[NSYM], double tc) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < (int)NSYM; i++) m |= ((c[i] != 0) && ((double)s[i] < tc)) ? (1u << i) : 0u;
+    return m;
+}
+// The same mask for non-negative integer sums with one fp64 product x = t·cov per call:
+// for an integer S, S < x ⟺ S ≤ lim with lim = ⌈x⌉ − 1 (x > 0; no S ≥ 0 is < x ≤ 0 or
+// NaN), so the six tests are u32 compares.  Exact: x is the reference's own product.
+__device__ __forceinline__ uint32_t vote_mask_u32(const uint32_t (&c)[NSYM], const uint32_t (&s)[NSYM], double x) {
+    if (!(x > 0.0)) return 0u;
+    const uint32_t lim = x > 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)(ceil(x) - 1.0);
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < (int)NSYM; i++) m |= ((c[i] != 0) && (s[i] <= lim)) ? (1u << i) : 0u;
+    return m;
+}
+
+// char of a one-symbol mask, amb[1 << s] = "-ACGNT"[s]
+__device__ __forceinline__ uint32_t sym_char(uint32_t s) { return (uint32_t)(0x544E4743412DULL >> (8 * s)) & 0xFFu; }
+
+// The vote shortcut: the largest count m1 is a strict majority (so unique) and
+// m1·2^15 ≥ uq·cov with uq = ⌈tmax·2^15⌉ + 1 (per pass; 0 = off: some threshold outside
+// (0, 1]).  Then m1 ≥ tmax·cov + cov/2^15 ≥ tmax·cov·(1 + 2^-53) ≥ fl(tmax·cov) — every
+// other symbol's greater-sum is ≥ m1 ≥ t·cov for every t of the pass, and the symbol's own
+// is 0 < t·cov.  64-bit products: exact for any count.
+__device__ __forceinline__ bool majority_fast(uint32_t m1, uint32_t cov, uint32_t uq) {
+    return uq && 2ull * m1 > (uint64_t)cov && ((uint64_t)m1 << 15) >= (uint64_t)uq * cov;
+}
+__host__ __device__ inline uint32_t pass_uq(const double *th, int tn) {
+    double tmax = th[0];
+    bool ok = true;
+    for (int u = 0; u < tn; u++) {
+        ok = ok && th[u] > 0.0 && th[u] <= 1.0;
+        tmax = th[u] > tmax ? th[u] : tmax;
+    }
+    return ok ? (uint32_t)ceil(tmax * 32768.0) + 1u : 0u;
+}
+
+// ----------------------------------------------------------------- bit-sliced counters
+// A counter is 8 bit-planes of 32 positions (bit b of plane i = bit i of the count at
+// position b).  Harley–Seal carry-save adds: 16 masks per close, 2 v_bitop3 per CSA.
+__device__ __forceinline__ void csa(uint32_t &h, uint32_t &l, uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t lo, hi;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(lo) : "v"(a), "v"(b), "v"(c));
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe8" : "=v"(hi) : "v"(a), "v"(b), "v"(c));
+    l = lo;
+    h = hi;
+}
+// 8 masks into planes C[0..2]; returns the carry of weight 8
+__device__ __forceinline__ uint32_t tree8(uint32_t (&C)[8], const uint32_t (&m)[8]) {
+    uint32_t t2a, t2b, t4a, t4b, t8;
+    csa(t2a, C[0], C[0], m[0], m[1]);
+    csa(t2b, C[0], C[0], m[2], m[3]);
+    csa(t4a, C[1], C[1], t2a, t2b);
+    csa(t2a, C[0], C[0], m[4], m[5]);
+    csa(t2b, C[0], C[0], m[6], m[7]);
+    csa(t4b, C[1], C[1], t2a, t2b);
+    csa(t8, C[2], C[2], t4a, t4b);
+    return t8;
+}
+// two weight-8 carries into plane C[3], the weight-16 carry rippled into C[4..7]
+__device__ __forceinline__ void close16(uint32_t (&C)[8], uint32_t t8a, uint32_t t8b) {
+    uint32_t t16;
+    csa(t16, C[3], C[3], t8a, t8b);
+#pragma unroll
+    for (int b = 4; b < 8; b++) {
+        const uint32_t t = C[b] & t16;
+        C[b] ^= t16;
+        t16 = t;
+    }
+}
+// one weight-8 carry into plane C[3], rippled into C[4..7]
+__device__ __forceinline__ void close8(uint32_t (&C)[8], uint32_t t8) {
+#pragma unroll
+    for (int b = 3; b < 8; b++) {
+        const uint32_t t = C[b] & t8;
+        C[b] ^= t8;
+        t8 = t;
+    }
+}
+// one mask of weight 1 rippled into all planes (rare masks: '-')
+__device__ __forceinline__ void ripple1(uint32_t (&C)[8], uint32_t m) {
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+        const uint32_t t = C[b] & m;
+        C[b] ^= m;
+        m = t;
+    }
+}
+
+// 8 bit-planes of one counter → R[r] byte j = count of position 8j + r (8×8 bit transposes
+// on 4 byte lanes at once).
+__device__ __forceinline__ void transpose8(uint32_t (&R)[8]) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const uint32_t t = ((R[r] >> 4) ^ R[r + 4]) & 0x0F0F0F0Fu;
+        R[r + 4] ^= t;
+        R[r] ^= t << 4;
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        if (r & 2) continue;
+        const uint32_t t = ((R[r] >> 2) ^ R[r + 2]) & 0x33333333u;
+        R[r + 2] ^= t;
+        R[r] ^= t << 2;
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r += 2) {
+        const uint32_t t = ((R[r] >> 1) ^ R[r + 1]) & 0x55555555u;
+        R[r + 1] ^= t;
+        R[r] ^= t << 1;
+    }
+}
+
+// ----------------------------------------------------------------- runs (k_reads output)
+struct Run {
+    uint32_t gpos, len, kind;
+    uint64_t q;
+};
+__device__ __forceinline__ Run run_of(uint4 v) {
+    Run r;
+    r.gpos = v.x;
+    r.len = v.y & 0xFFFFFFu;
+    r.kind = v.y >> 24;
+    r.q = (uint64_t)v.z | ((uint64_t)v.w << 32);
+    return r;
+}
+
+// The 32-position record of run r at global word W: valid = positions of W the run covers
+// (0 if none); the base planes' bits are taken from query base q + (first covered − gpos).
+struct RecGeom {
+    uint32_t valid, lo;   // covered bits, first covered bit
+    uint64_t qs;          // query base of position 32W + lo
+};
+__device__ __forceinline__ RecGeom rec_geom(uint32_t gpos, uint32_t len, uint32_t W) {
+    RecGeom g;
+    const int64_t s = (int64_t)gpos - 32ll * W, e = s + (int64_t)len;   // run in word-relative coordinates
+    const int64_t lo = s > 0 ? s : 0, hi = e < 32 ? e : 32;
+    if (hi <= lo) {
+        g.valid = 0u;
+        g.lo = 0u;
+        g.qs = 0;
+        return g;
+    }
+    const uint32_t n = (uint32_t)(hi - lo);
+    g.valid = (n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u)) << (uint32_t)lo;
+    g.lo = (uint32_t)lo;
+    g.qs = (uint64_t)(lo - s);   // offset into the run
+    return g;
+}
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
+    return __builtin_amdgcn_alignbit(hi, lo, sh);
+}
+
+}  // namespace s2c

@@ -1,4 +1,4 @@
-"""Device side: packed batch → HBM, workspace, the four HIP stages, results → host.
+"""Device side: packed batch → HBM, workspace, the HIP stages, results → host.
 
 PyTorch is used only as the device allocator / stream provider; all compute is
 libs2c.so's hand-written HIP kernels (s2c_kernels.hip).  There is no CPU
@@ -44,32 +44,24 @@ def _ptr(t):
 class DeviceBatch:
     """The packed batch resident in HBM (inputs of every launch)."""
 
+    ARRAYS = ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile")
+
     def __init__(self, hb, device=None):
         self.device = _dev(device)
         self.hb = hb
-        i = hb.info
-        self.info = i
-        up = lambda a: _up(a, self.device)  # noqa: E731
-        # word-major seqout records + work plan (the read-piece table stays on the host)
-        self.wrec = up(hb.wrec)
-        self.recs = up(hb.recs.reshape(-1))
-        self.fix, self.exc, self.iwr = up(hb.fix.reshape(-1)), up(hb.exc), up(hb.iwr)
-        self.items, self.blocks = up(hb.items.reshape(-1)), up(hb.blocks.reshape(-1))
-        self.deep = up(hb.deep)
-        self.ins_ev, self.ins_kinfo = up(hb.ins_ev.reshape(-1)), up(hb.ins_kinfo.reshape(-1))
-        self.ins_bases = up(hb.ins_bases)
-        self.ins_bits, self.ins_rank = up(hb.ins_bits), up(hb.ins_rank)
+        self.info = hb.info
+        for name in self.ARRAYS:
+            setattr(self, name, _up(np.asarray(getattr(hb, name)).reshape(-1), self.device))
 
     def nbytes(self):
-        return sum(t.numel() * t.element_size() for t in (
-            self.wrec, self.recs, self.fix, self.exc, self.iwr, self.items, self.blocks, self.deep,
-            self.ins_ev, self.ins_kinfo, self.ins_bases, self.ins_bits, self.ins_rank))
+        return sum(getattr(self, n).numel() * getattr(self, n).element_size() for n in self.ARRAYS)
 
 
 class Workspace:
-    """All scratch + output buffers for one (batch, thresholds, fill) configuration."""
+    """All scratch + output buffers for one (batch, thresholds, fill, maxdel) configuration."""
 
-    def __init__(self, db: DeviceBatch, thresholds, min_depth=1, fill=b"-", keep_counts=False):
+    def __init__(self, db: DeviceBatch, thresholds, min_depth=1, fill=b"-", keep_counts=False,
+                 maxdel_active=None, maxdel=None):
         dev = db.device
         i = db.info
         self.db = db
@@ -78,15 +70,18 @@ class Workspace:
         L.check(lib.s2c_workspace_sizes(C.byref(i), self.T, C.byref(sz)))
         self.sizes = sz
         u8 = lambda n: torch.empty(max(int(n), 16), dtype=torch.uint8, device=dev)  # noqa: E731
+        z8 = lambda n: torch.zeros(max(int(n), 16), dtype=torch.uint8, device=dev)  # noqa: E731
         self.thr = torch.tensor([float(t) for t in thresholds], dtype=torch.float64, device=dev)
         fill = bytes(fill)
         self.fill_bytes = fill
         self.fill = torch.tensor(list(fill) or [0], dtype=torch.uint8, device=dev)
-        # counts live in HBM only for deep tiles (unless a test asks for all of them)
+        self.runs = u8(sz.runs)
+        # insertion hash tables: zero before the first run; every run leaves them zero
+        self.ibkt, self.ilong, self.ilong_n = z8(sz.ibkt), u8(sz.ilong), z8(sz.ilong_n)
+        # counts live in HBM only for deep / general tiles (unless a test asks for all of them)
         self.keep_counts = keep_counts
         self.counts = u8(6 * i.padded_len * 4 if keep_counts else sz.counts)
         self.ins_cols = u8(sz.ins_cols)
-        self.ins_cnt = u8(sz.ins_cnt)
         self.ins_chr = u8(sz.ins_chr)
         self.blk_len = u8(sz.blk_len)
         self.tile_stats = u8(sz.tile_stats)
@@ -96,21 +91,24 @@ class Workspace:
         cap = int(sz.out_per_fill) * self.fill_w + int(sz.out_fixed)
         self.out = u8(cap)
         d = L.Dev()
-        d.wrec, d.recs = _ptr(db.wrec), _ptr(db.recs)
-        d.fix, d.exc, d.n_exc, d.iwr = _ptr(db.fix), _ptr(db.exc), i.n_exc, _ptr(db.iwr)
-        d.items, d.blocks, d.deep = _ptr(db.items), _ptr(db.blocks), _ptr(db.deep)
-        d.ins_ev, d.ins_kinfo, d.ins_bases = _ptr(db.ins_ev), _ptr(db.ins_kinfo), _ptr(db.ins_bases)
-        d.ins_bits = _ptr(db.ins_bits)
-        d.n_recs, d.chunk_recs = i.n_recs, i.chunk_recs
-        d.n_items, d.n_blocks, d.n_deep = i.n_items, i.n_blocks, i.n_deep
-        d.n_keys, d.n_cols, d.padded_len = i.n_keys, i.n_cols, i.padded_len
-        d.tile_max, d.n_refs = i.tile_max, i.n_refs
+        for name in DeviceBatch.ARRAYS:
+            setattr(d, name, _ptr(getattr(db, name)))
+        d.n_pieces, d.n_ops, d.n_qwords, d.n_tiles = i.n_pieces, i.n_ops, i.n_qwords, i.n_tiles
+        d.n_items, d.n_dense, d.n_deep = i.n_items, i.n_dense, i.n_deep
+        d.padded_len, d.chunk, d.kwin, d.tile_max = i.padded_len, i.chunk, i.kwin, i.tile_max
+        # the maxdel rule (:210) runs on the device: the parser's setting unless overridden
+        if maxdel_active is None:
+            maxdel_active = getattr(db.hb, "maxdel_active", True)
+        if maxdel is None:
+            maxdel = getattr(db.hb, "maxdel", 150)
+        d.maxdel_active, d.maxdel = 1 if maxdel_active else 0, int(maxdel)
         d.thresholds, d.n_thr = _ptr(self.thr), self.T
         d.min_depth = int(max(min(min_depth, 2**31 - 1), -2**31))
         d.fill_len, d.fill_nondash = len(fill), sum(1 for c in fill if c != ord("-"))
         d.fill = _ptr(self.fill)
+        d.runs, d.ibkt, d.ilong, d.ilong_n = _ptr(self.runs), _ptr(self.ibkt), _ptr(self.ilong), _ptr(self.ilong_n)
         d.counts = _ptr(self.counts)
-        d.ins_cols, d.ins_cnt, d.ins_chr = _ptr(self.ins_cols), _ptr(self.ins_cnt), _ptr(self.ins_chr)
+        d.ins_cols, d.ins_chr, d.n_cols = _ptr(self.ins_cols), _ptr(self.ins_chr), i.n_cols
         d.tile_stats, d.blk_len = _ptr(self.tile_stats), _ptr(self.blk_len)
         d.out, d.out_cap = _ptr(self.out), cap
         self.dev = d
@@ -118,17 +116,19 @@ class Workspace:
     def stream_handle(self):
         return C.c_void_p(torch.cuda.current_stream(self.db.device).cuda_stream)
 
-    # ---- the two stages in run order (each one C-ABI call; asynchronous on the current stream)
+    # ---- the stages in run order (each one C-ABI call; asynchronous on the current stream)
+    def reads(self):
+        """parsecigar + maxdel per piece → run records; insertion events → hash tables."""
+        L.check(lib.s2c_reads(C.byref(self.dev), self.stream_handle()))
+
     def pileup(self):
-        if (self.dev.ablate & 4) and not self.keep_counts:
-            raise ValueError("diagnostic ablate&4 stores every count: build the Workspace with keep_counts=True")
         L.check(lib.s2c_pileup(C.byref(self.dev), self.stream_handle()))
 
     def consensus(self):
         L.check(lib.s2c_consensus(C.byref(self.dev), self.stream_handle()))
 
     def run(self):
-        """pileup (+ insertion columns, vote, FASTA bodies) → deep tiles (no host sync)."""
+        """reads → pileup (+ insertion columns, vote, FASTA bodies) → deep tiles (no host sync)."""
         L.check(lib.s2c_run(C.byref(self.dev), self.stream_handle()))
 
     # ---- HIP graph of one run (the stage launches replayed without host launch overhead)
@@ -152,15 +152,12 @@ class Workspace:
 
     # ---- results
     def pileup_counts(self):
-        """Diagnostic: run the pileup with every tile storing its counts (needs
-        keep_counts=True); returns counts[6][padded_len] as numpy u32."""
+        """Diagnostic: k_reads, then every tile's counts stored to `counts` (no vote); needs
+        keep_counts=True; returns counts[6][padded_len] as numpy u32."""
         if not self.keep_counts:
             raise ValueError("pileup_counts needs Workspace(keep_counts=True)")
-        self.dev.ablate = 4
-        try:
-            self.pileup()
-        finally:
-            self.dev.ablate = 0
+        self.reads()
+        L.check(lib.s2c_pileup_counts(C.byref(self.dev), self.stream_handle()))
         return self.counts_host()
 
     def counts_host(self):
@@ -175,11 +172,11 @@ class Workspace:
         (tiles never straddle a reference; :352-397 sums)."""
         torch.cuda.synchronize(self.db.device)
         i = self.db.info
-        R, T, nb = i.n_refs, self.T, i.n_blocks
+        R, T, nb = i.n_refs, self.T, i.n_tiles
         stats = np.zeros((R, T, 4), dtype=np.uint64)
         if nb:
             ts = self.tile_stats[: T * nb * 32].view(torch.int64).cpu().numpy().view(np.uint64).reshape(T, nb, 4)
-            ref = self.db.hb.blocks[:, 2].astype(np.int64)
+            ref = self.db.hb.tiles[:, 2].astype(np.int64)
             for t in range(T):
                 np.add.at(stats[:, t, :], ref, ts[t])
         if T * nb == 0:
@@ -187,7 +184,7 @@ class Workspace:
         # each tile wrote its body into its slot; the references' bodies are their tiles'
         # pieces in order: gather them into [t][tile] order (one vectorised index)
         lens = self.blk_len[: T * nb * 8].view(torch.int64).cpu().numpy().astype(np.int64)
-        blocks = self.db.hb.blocks.astype(np.int64)
+        blocks = self.db.hb.tiles.astype(np.int64)
         slot = self.fill_w * blocks[:, 0] + blocks[:, 8]                     # F·a + cb0
         starts = (np.arange(T, dtype=np.int64)[:, None] * self.out_stride + slot[None, :]).reshape(-1)
         offs = np.zeros(T * nb + 1, dtype=np.int64)

@@ -32,7 +32,7 @@ def build_records(hb, thresholds, prefix, stats, offs, out):
     KeyError (vote hit a missing amb key, :367/:381), ValueError / OverflowError
     (int(t*100) of nan / inf, :394), ZeroDivisionError (empty record, :395)."""
     i = hb.info
-    T, nb = len(thresholds), i.n_blocks
+    T, nb = len(thresholds), i.n_tiles
     fastas = {}
     pre = prefix.encode("latin-1") if isinstance(prefix, str) else prefix
     for r in range(i.n_refs):

@@ -1,10 +1,12 @@
-"""CPU model of the four HIP stages, reading the PACKED BATCH exactly as the kernels do
+"""CPU model of the HIP stages, reading the PACKED BATCH exactly as the kernels do
 (test infrastructure only).
 
-It lets the CPU suite check the host side of the product — parser, packing, wrap
-splitting, tile plan, block plan, insertion events, record formatting — against the
-reference's golden outputs without a GPU, and gives the GPU tests a second,
-kernel-shaped expectation (e.g. counts[6][L]) to diff against.
+It restates k_reads (the token walk of parsecigar :46-82 and the maxdel rule :210 per
+piece → run records; insertion events with their global keys), the counting of the runs
+(:210-218), the insertion columns (:262-294), the vote and the FASTA body layout, so the
+CPU suite checks the host side of the product — parser, packing, bucketing, tile plan —
+against the reference's golden outputs without a GPU, and the GPU tests get a
+kernel-shaped expectation (run records, counts[6][L], per-tile stats and bodies).
 """
 from __future__ import annotations
 
@@ -12,6 +14,11 @@ import numpy as np
 
 NSYM = 6
 AMB = None
+OP_BASES = (0, 7, 8)        # M = X
+OP_DASH = (2, 3, 6)         # D N P
+OP_I, OP_S = 1, 4
+PF_X, PF_RANGE, PF_INS, PF_LONG = 1, 2, 4, 8
+RUN_BASES, RUN_DASH, RUN_XBIT, RUN_DROP, RUN_LONG = 1, 2, 4, 8, 16
 
 
 def _amb():
@@ -25,137 +32,187 @@ def _amb():
     return AMB
 
 
-SYM_OF_BASE = np.array([1, 2, 3, 5], dtype=np.int64)   # 2-bit base (A C G T) → symbol index of "-ACGNT"
+def plane_codes(hb, q, n):
+    """3-bit plane codes x·4 + p1·2 + p0 of query bases [q, q + n) (A 0 C 1 G 2 T 3 N 4 '-' 5)."""
+    idx = np.arange(q, q + n, dtype=np.int64)
+    w, sh = idx >> 5, (idx & 31).astype(np.uint32)
+    bq = hb.bq
+    p0 = (bq[w, 0] >> sh) & 1
+    p1 = (bq[w, 1] >> sh) & 1
+    x = (hb.bx[w] >> sh) & 1
+    return (x << 2 | p1 << 1 | p0).astype(np.int64)
 
 
-def record_bases(recs):
-    """Records [n][2] bit-planes → 2-bit bases [n][32] (b1·2+b0: A C G T)."""
-    q = np.arange(32, dtype=np.int64)
-    r = np.asarray(recs, dtype=np.int64)
-    return ((r[:, 0, None] >> q) & 1) + 2 * ((r[:, 1, None] >> q) & 1)
+CODE_SYM = np.array([1, 2, 3, 5, 4, 0, -1, -1], dtype=np.int64)   # plane code → "-ACGNT" index
 
 
-def model_counts(hb, block=1 << 18):
-    """counts[6][padded_len] from the packed batch, as k_pileup forms them: every record
-    position counted as its 2-bit base (placeholders as A), minus the A placeholders (fix),
-    plus the '-'/'N' entries (exc), both per work item."""
+def model_reads(hb, maxdel_active=None, maxdel=None):
+    """k_reads: (runs [n_ops][4] u32, events [(gkey, (sym, ...))]) from the packed batch."""
+    if maxdel_active is None:
+        maxdel_active = getattr(hb, "maxdel_active", True)
+    if maxdel is None:
+        maxdel = getattr(hb, "maxdel", 150)
+    pc, ops = hb.pc.astype(np.int64), hb.ops.astype(np.int64)
+    runs = np.zeros((max(hb.info.n_ops, 1), 4), dtype=np.uint32)
+    events = []
+    for i in range(hb.info.n_pieces):
+        gpos, qh, o, w3 = (int(v) for v in pc[i])
+        oend = int(pc[i + 1, 2])
+        slen, fl = w3 & 0xFFFFFF, w3 >> 24
+        ka, kb = 0, 1 << 62
+        if fl & PF_RANGE:
+            ka, kb = int(ops[o]), int(ops[o + 1])
+            o += 2
+        key0 = roff = 0
+        if fl & PF_INS:
+            key0 = int(ops[o]) | (int(ops[o + 1]) << 32)
+            key0 = key0 - (1 << 64) if key0 >= 1 << 63 else key0
+            roff = int(ops[o + 2])
+            o += 3
+        q0 = 16 * qh
+        toks = [(int(w) & 15, int(w) >> 4) for w in ops[o:oend]]
+        drop = False
+        if maxdel_active:   # :210 — '-' of seqout: D/N/P lengths + '-' chars of the bases taken
+            dashes, start = 0, 0
+            for op, ln in toks:
+                if op in OP_BASES:
+                    take = max(0, min(ln, slen - start))
+                    if take and fl & PF_X:   # '-' chars of SEQ: only reads with non-ACGT chars
+                        dashes += int((plane_codes(hb, q0 + start, take) == 5).sum())
+                    start += ln
+                elif op in OP_DASH:
+                    dashes += ln
+                elif op in (OP_I, OP_S):
+                    start += ln
+            drop = dashes > maxdel
+        lng = RUN_LONG if fl & PF_LONG else 0
+        bkind = RUN_BASES | (RUN_XBIT if fl & PF_X else 0) | (RUN_DROP if drop else 0) | lng
+        k = start = 0
+        for j, (op, ln) in enumerate(toks):
+            if op in OP_BASES or op in OP_DASH:
+                bases = op in OP_BASES
+                take = max(0, min(ln, slen - start)) if bases else ln
+                s, e = max(k, ka), min(k + take, kb)
+                if e > s and (bases or not drop):
+                    g = gpos + (s - ka)
+                    if bases:
+                        q = q0 + start + (s - k)
+                        runs[o + j] = (g, (e - s) | (bkind << 24), q & 0xFFFFFFFF, q >> 32)
+                    else:
+                        runs[o + j] = (g, (e - s) | ((RUN_DASH | lng) << 24), 0, 0)
+                k += take
+                if bases:
+                    start += ln
+            elif op == OP_I:
+                take = max(0, min(ln, slen - start))
+                if fl & PF_INS and take and key0 + k >= roff:
+                    syms = tuple(int(CODE_SYM[c]) for c in plane_codes(hb, q0 + start, take))
+                    events.append((key0 + k, syms))
+                start += ln
+            elif op == OP_S:
+                start += ln
+    return runs, events
+
+
+def model_counts(hb, runs=None):
+    """counts[6][padded_len] of the run records, as the tile kernels form them."""
+    if runs is None:
+        runs, _ = model_reads(hb)
     Lp = hb.info.padded_len
-    wrec = hb.wrec.astype(np.int64)
-    assert wrec[0] == 0 and wrec[-1] == hb.info.n_recs and (np.diff(wrec) >= 0).all()
-    word_of = np.repeat(np.arange(Lp // 32, dtype=np.int64), np.diff(wrec))
-    flat = np.zeros(NSYM * Lp, dtype=np.int64)
-    for k in range(0, len(word_of), block):
-        sym = SYM_OF_BASE[record_bases(hb.recs[k:k + block])]
-        pos = word_of[k:k + block, None] * 32 + np.arange(32)
-        flat += np.bincount((sym * Lp + pos).reshape(-1), minlength=NSYM * Lp)
-    counts = flat.reshape(NSYM, Lp)
-    fix = hb.fix.astype(np.int64)
-    for a, b, _, _, fo, x0, x1 in hb.items[:, :7].astype(np.int64):   # per work item
-        nw = (b + 31) // 32 - a // 32
-        f = fix[fo:fo + 16 * nw].reshape(nw, 16)
-        ph = np.concatenate([f & 0xFFFF, f >> 16], axis=1).reshape(-1)   # tile positions a..a+32·nw
-        counts[1, a:a + 32 * nw] -= ph
-        e = hb.exc[x0:x1].astype(np.int64)
-        pos = a + (e >> 1)
-        assert (pos < b).all()
-        np.add.at(counts, (np.where(e & 1, 4, 0), pos), 1)
-    for a, b in hb.blocks[:, :2].astype(np.int64):
-        w1 = (b + 31) // 32 * 32
-        assert (counts[1, a:w1] >= 0).all(), "A placeholders exceed the A-counted record positions"
+    counts = np.zeros((NSYM, Lp), dtype=np.int64)
+    r = runs.astype(np.int64)
+    kind = r[:, 1] >> 24
+    ln = r[:, 1] & 0xFFFFFF
+    for sel, is_bases in (((kind & 3) == RUN_BASES, True), ((kind & 3) == RUN_DASH, False)):
+        g, n = r[sel, 0], ln[sel]
+        if not len(g):
+            continue
+        off = np.arange(int(n.sum()), dtype=np.int64) - np.repeat(np.cumsum(n) - n, n)
+        pos = np.repeat(g, n) + off
+        if not is_bases:
+            counts[0] += np.bincount(pos, minlength=Lp)
+            continue
+        q = np.repeat(r[sel, 2] | (r[sel, 3] << 32), n) + off
+        w, sh = q >> 5, (q & 31).astype(np.uint32)
+        code = ((hb.bx[w] >> sh) & 1).astype(np.int64) << 2 | ((hb.bq[w, 1] >> sh) & 1) << 1 | ((hb.bq[w, 0] >> sh) & 1)
+        sym = CODE_SYM[code]
+        assert (sym >= 0).all(), "a counted base outside -ACGNT"
+        keep = ~((sym == 0) & np.repeat((kind[sel] & RUN_DROP) != 0, n))   # '-' of SEQ dropped (:216)
+        np.add.at(counts, (sym[keep], pos[keep]), 1)
     return counts
 
 
 def check_plan(hb):
-    """Every real position is owned by exactly one tile; a tile's items are chunks
-    0..nch-1 whose record ranges cover every word of the tile; deep (flag bit 0) = nch > 1."""
-    Lp = hb.info.padded_len
-    own = np.zeros(Lp, dtype=np.int64)
-    wrec = hb.wrec.astype(np.int64)
-    ch = int(hb.info.chunk_recs)
-    assert ch > 0
-    chunks = {}
-    for a, b, c, t in hb.items[:, :4].astype(np.int64):
-        chunks.setdefault(int(t), []).append(int(c))
-        assert (int(hb.blocks[t, 0]), int(hb.blocks[t, 1])) == (a, b)
-    for t, (a, b, ref, deep) in enumerate(hb.blocks[:, :4].astype(np.int64)):
-        cs = sorted(chunks[t])
-        assert cs == list(range(len(cs))), "tile %d chunks %r" % (t, cs)
-        assert bool(deep & 1) == (len(cs) > 1)
-        assert a % 32 == 0
-        words = np.arange(a // 32, (b + 31) // 32)
-        assert (wrec[words + 1] - wrec[words]).max(initial=0) <= len(cs) * ch
+    """Pieces bucketed by start word with a matching run-slot CSR; every real position in
+    exactly one tile; short pieces within the window, long ones listed for every tile they
+    overlap; items / dense lists cover every tile once with its chunk count."""
+    i = hb.info
+    pc = hb.pc.astype(np.int64)
+    NP, K = i.n_pieces, i.kwin
+    sw = pc[:NP, 0] >> 5
+    assert (np.diff(sw) >= 0).all(), "pieces not bucketed by start word"
+    rs = hb.rs.astype(np.int64)
+    assert rs[0] == 0 and rs[-1] == i.n_ops and (np.diff(rs) >= 0).all()
+    assert (np.diff(pc[:, 2]) >= 0).all() and pc[NP, 2] == i.n_ops
+    if NP:
+        first = np.searchsorted(sw, np.arange(i.n_words + 1))
+        assert (rs == pc[first, 2]).all()
+    own = np.zeros(i.padded_len, dtype=np.int64)
+    T = hb.tiles.astype(np.int64)
+    for t, row in enumerate(T):
+        a, b = row[0], row[1]
+        assert a % 64 == 0 and 0 < b - a <= 2048
         own[a:b] += 1
-    for r in range(hb.info.n_refs):
+        assert (hb.wtile[a >> 5:(b + 31) >> 5] == t).all()
+    for r in range(i.n_refs):
         o, L = int(hb.ref_off[r]), int(hb.ref_len[r])
         assert (own[o:o + L] == 1).all(), "ref %d positions not tiled exactly once" % r
-    check_item_descriptors(hb)
-    check_ins_layout(hb)
+    items = {}
+    for t, c, _, _ in hb.items.astype(np.int64):
+        items.setdefault(int(t), []).append(int(c))
+    for t, c, _, _ in hb.dense.astype(np.int64):
+        assert int(t) not in items and c == 0
+        items[int(t)] = [0]
+        assert T[t, 3] == 4
+    assert sorted(items) == list(range(i.n_tiles))
+    for t, cs in items.items():
+        assert sorted(cs) == list(range(len(cs)))
+        assert bool(T[t, 3] & 1) == (len(cs) > 1)
+    lp = hb.lp.astype(np.int64)
+    for k in range(NP):
+        g, fl = pc[k, 0], pc[k, 3] >> 24
+        span = _span(hb, k)
+        if span == 0:
+            continue
+        w0, w1 = g >> 5, (g + span - 1) >> 5
+        if fl & PF_LONG:
+            for t in range(int(hb.wtile[w0]), int(hb.wtile[w1]) + 1):
+                sl = set(lp[T[t, 10]:T[t, 11]].tolist())
+                assert set(range(pc[k, 2], pc[k + 1, 2])) <= sl
+        else:
+            assert w1 - w0 <= K, "short piece beyond the window"
+    assert sorted(hb.deep.tolist()) == [t for t in range(i.n_tiles) if T[t, 3] & 3]
 
 
-def check_item_descriptors(hb):
-    """Item words 7-13 copy their tile's block words 3-9, word 14 is the item's first record,
-    and iwr holds each word's record range of the item's chunk."""
-    it = hb.items.astype(np.int64)
-    bl = hb.blocks.astype(np.int64)
-    wrec = hb.wrec.astype(np.int64)
-    ch = int(hb.info.chunk_recs)
-    assert (it[:, 7:14] == bl[it[:, 3], 3:10]).all()
-    assert (it[:, 14] == wrec[it[:, 0] >> 5]).all()
-    nwp = hb.info.n_iwr // max(hb.info.n_items, 1) // 2
-    iw = hb.iwr.astype(np.int64).reshape(-1, nwp, 2)
-    for k, (a, b, c) in enumerate(it[:, :3]):
-        for w in range(nwp):
-            if 32 * w < b - a:
-                W = (a >> 5) + w
-                r0 = min(wrec[W + 1], wrec[W] + c * ch)
-                assert (iw[k, w] == (r0, min(wrec[W + 1], r0 + ch))).all()
-            else:
-                assert (iw[k, w] == 0).all()
-
-
-def check_ins_layout(hb):
-    """Keys ascending and unique; bitmap/rank give each key's index; count units cover
-    every event of their key exactly once, ≤ S2C_INS_UNIT events each."""
-    nk = hb.info.n_keys
-    key = hb.ins_key.astype(np.int64)
-    assert (np.diff(key) > 0).all()
-    bits = hb.ins_bits.astype(np.int64)
-    pos = np.nonzero(((bits[:, None] >> np.arange(32)) & 1).reshape(-1))[0]
-    assert (pos == key).all()
-    rank = hb.ins_rank.astype(np.int64)
-    assert rank[-1] == nk and (rank[key >> 5] + [int(bin(int(bits[k >> 5]) & ((1 << (k & 31)) - 1)).count("1"))
-                                                 for k in key] == np.arange(nk)).all()
-    koff = hb.ins_koff.astype(np.int64)
-    assert koff[0] == 0 and koff[-1] == hb.info.n_ins and (np.diff(koff) > 0).all()
-    ekey = hb.ins_ekey.astype(np.int64)
-    assert (ekey == np.repeat(np.arange(nk), np.diff(koff))).all()
-    check_device_records(hb)
-
-
-def check_device_records(hb):
-    """The device's 16-B event/key records and the tiles' insertion ranges (block words
-    4-9) restate the grouped arrays exactly."""
-    koff, kcol = hb.ins_koff.astype(np.int64), hb.ins_kcol.astype(np.int64)
-    off = hb.ins_off.astype(np.int64)
-    ki = hb.ins_kinfo.astype(np.int64)
-    assert (ki[:, 0] == hb.ins_key).all() and (ki[:, 1] == kcol[:-1]).all() and (ki[:, 2] == np.diff(kcol)).all()
-    ev = hb.ins_ev.astype(np.int64)
-    rank = hb.ins_rank.astype(np.int64)
-    seen = np.zeros(len(ev), np.int64)
-    for a, b, _, _, klo, khi, e0, e1, cb0, cb1 in hb.blocks[:, :10].astype(np.int64):
-        assert (klo, khi) == (rank[a >> 5], rank[(b + 31) >> 5])
-        assert (e0, e1, cb0, cb1) == (koff[klo], koff[khi], kcol[klo], kcol[khi])
-        for k in range(klo, khi):
-            for e in range(koff[k], koff[k + 1]):
-                seen[e] += 1
-                n = off[e + 1] - off[e]
-                assert (ev[e, 0], ev[e, 1], ev[e, 2]) == (kcol[k] - cb0, n, off[e])
-                w0 = 0
-                for c in range(min(n, 8)):
-                    q = off[e] + c
-                    w0 |= ((int(hb.ins_bases[q >> 3]) >> (4 * (q & 7))) & 15) << (4 * c)
-                assert ev[e, 3] == w0
-    assert (seen == 1).all()
+def _span(hb, k):
+    """Seqout span of piece k (from its RANGE prefix or its tokens)."""
+    pc, ops = hb.pc, hb.ops
+    o, oend, w3 = int(pc[k, 2]), int(pc[k + 1, 2]), int(pc[k, 3])
+    fl, slen = w3 >> 24, w3 & 0xFFFFFF
+    if fl & PF_RANGE:
+        return int(ops[o + 1]) - int(ops[o])
+    o += 3 if fl & PF_INS else 0
+    n = start = 0
+    for w in ops[o:oend]:
+        op, ln = int(w) & 15, int(w) >> 4
+        if op in OP_BASES:
+            n += max(0, min(ln, slen - start))
+            start += ln
+        elif op in OP_DASH:
+            n += ln
+        elif op in (OP_I, OP_S):
+            start += ln
+    return n
 
 
 def _vote(c, cov, t):
@@ -168,34 +225,37 @@ def _vote(c, cov, t):
     return 0xFF if ch is None else ch
 
 
-def model_pipeline(hb, thresholds, min_depth=1, fill=b"-"):
+def model_columns(events):
+    """{gkey: [6-count column, ...]} (:262-287), motifs aggregated per (key, motif)."""
+    motifs = {}
+    for key, syms in events:
+        d = motifs.setdefault(key, {})
+        d[syms] = d.get(syms, 0) + 1
+    cols = {}
+    for key, d in motifs.items():
+        cl = [[0] * NSYM for _ in range(max(len(m) for m in d))]
+        for m, mult in d.items():
+            for c, s in enumerate(m):
+                cl[c][s] += mult
+        cols[key] = cl
+    return cols
+
+
+def model_pipeline(hb, thresholds, min_depth=1, fill=b"-", maxdel_active=None):
     """(stats[R,T,4], offs[T*nb+1], out bytes) as the device produces them."""
-    counts = model_counts(hb)
-    Lp = hb.info.padded_len
+    runs, events = model_reads(hb, maxdel_active)
+    counts = model_counts(hb, runs)
+    cols = model_columns(events)
     T = len(thresholds)
     cov = counts.sum(axis=0)
-    # insertion columns per key (:264-294)
-    cols = {}
-    for k in range(hb.info.n_keys):
-        key = int(hb.ins_key[k])
-        cl = cols.setdefault(key, [])
-        for e in range(int(hb.ins_koff[k]), int(hb.ins_koff[k + 1])):
-            o0, o1 = int(hb.ins_off[e]), int(hb.ins_off[e + 1])
-            for c in range(o1 - o0):
-                q = o0 + c
-                code = (int(hb.ins_bases[q >> 3]) >> (4 * (q & 7))) & 15
-                while len(cl) <= c:
-                    cl.append([0] * NSYM)
-                cl[c][code] += 1
-        assert len(cl) == int(hb.ins_kcol[k + 1]) - int(hb.ins_kcol[k])
-    nb = hb.info.n_blocks
+    nb = hb.info.n_tiles
     R = hb.info.n_refs
     stats = np.zeros((R, T, 4), dtype=np.uint64)
     blk_len = np.zeros(T * nb + 1, dtype=np.int64)
     pieces = [[None] * nb for _ in range(T)]
     fl = len(fill)
     fnd = sum(1 for ch in fill if ch != ord("-"))
-    for bi, (g0, g1, ref, _) in enumerate(hb.blocks[:, :4]):
+    for bi, (g0, g1, ref) in enumerate(hb.tiles[:, :3]):
         g0, g1, ref = int(g0), int(g1), int(ref)
         for ti, t in enumerate(thresholds):
             buf = bytearray()
