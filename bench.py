@@ -1,25 +1,33 @@
 #!/usr/bin/env python3
 """bench.py — BASELINE.json metric: aligned bases/s into consensus on MI355X.
 
-A step = one pass of the device hot path (pileup + fused insertion columns, vote and FASTA
-body bytes → flagged tiles) over one synthetic batch resident in HBM:
-one `s2c_run` (direct kernel launches, queued back to back — a HIP graph replay costs
-≈5 µs more GPU time per step on this ROCm, scripts/launch_overhead.py; `--graph` times
-replays instead).  Host SAM parse and H2D are excluded; parse time is reported separately.
+A step = one pass of the device hot path over one synthetic batch resident in HBM: one
+`s2c_run` = k_reads (parsecigar + maxdel per piece → run records, insertion events →
+per-tile hash tables) → k_tile / k_tile_dense (pileup, insertion columns, vote, FASTA body
+bytes) → k_consensus (deep / general tiles), launched back to back on one stream.  Host SAM
+parse and H2D are excluded; parse time is reported separately (host_parse_s).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c5] [--shard]
 
-N>1 is launched by torch.distributed.run, one process per GPU.  The path shards by
-reference position with no exchange: each rank runs its own batch of the workload
-(its own 353 loci for c2; seed = SEED + rank), so per-GPU work is fixed — weak scaling.
-Timing: barrier + synchronize on both sides of exactly K steps, MAX over ranks.
-Rank 0 prints ONE JSON line.
+Default workload: C5 (chr20 64.4 Mb × 30x, the largest single-GPU config of BASELINE.json;
+its ~0.7 GB batch does not fit the 256 MiB Infinity Cache).  Per-kernel times come from
+HIP events recorded on the launch stream between the stages of every timed step, so each
+kernel's time is a sub-interval of the step it belongs to.
+
+N>1 (torch.distributed.run, one process per GPU):
+  default  weak scaling: each rank runs its own batch of the workload (seed + rank);
+  --shard  strong scaling: ONE workload (rank 0's seed) split into contiguous tile ranges
+           (sam2consensus_amd.shard.split_tiles), each rank runs its shard; rank 0 checks the
+           merged FASTA against the reference's golden.
+Timing: barrier + synchronize on both sides of exactly K steps, MAX over ranks; value =
+aligned bases of all ranks / that time.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -29,31 +37,34 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md)
 
 WORKLOADS = {
-    "c2": "c2: Hyb-seq 353 loci x 1 kb, 500x, 150 bp, 5% 1-4 bp I / 5% 1-5 bp D, -c 0.25,0.50,0.75",
     "c1": "c1: 10 genes x 1 kb, 100x, 150 bp, -c 0.25",
+    "c2": "c2: Hyb-seq 353 loci x 1 kb, 500x, 150 bp, 5% 1-4 bp I / 5% 1-5 bp D, -c 0.25,0.50,0.75",
     "c3": "c3: bacterial 5 Mb, 1000x, 150 bp, shuffled, -m 10",
     "c4": "c4: chrM 16,569 bp, 100,000x, 166 amplicon starts",
     "c5": "c5: chr20 64,444,167 bp, 30x, 150 bp, 1% D reads, -d 150",
+    "c5nd": "c5nd: chr20 64,444,167 bp, 30x, 150 bp, 1% D reads, maxdel 150 active (no -d)",
 }
 
 
 def b_alg(info, T):
-    """Algorithmic bytes of one step, and of the fused k_pileup launch.
+    """Algorithmic bytes of one step and of its stages.
 
-    step   = 0.5·Q + 16·N + 4·K + (48+T)·L + Σ_ins(8 + 0.5·len)   (SURVEY's formula, which
-             prices the count tensor as written once + read once)
-    k_pileup = step − 48·L: the same inputs (packed bases, read records, op words, insertion
-             events) and the per-threshold consensus codes out, but the fused kernel keeps
-             the counts in registers/LDS, so no count bytes are charged to it (deep tiles,
-             none in c2, would add 24·L)."""
-    Q, N, K, L = info.query_bases, info.reads_mapped, info.n_ops, info.total_len
+    step    = 0.5·Q + 16·N + 4·K + (48+T)·L + Σ_ins(8 + 0.5·len)  (SURVEY's formula: 4-bit
+              query bases, 16 B per read, 4 B per CIGAR op, the count tensor written + read
+              once, T vote bytes per position, the insertion events)
+    k_reads = 16·N + 4·K            (read records + CIGAR ops in; the walk's inputs)
+    tile    = step − 16·N − 4·K − 48·L  (query bases in, vote bytes out, insertion events:
+              the tile kernels keep the counts in registers / LDS, so no count bytes are
+              charged to them; deep tiles, none in C5, would add 24·L)"""
+    Q, N, K, L = info.query_bases, info.reads_mapped, info.n_tokens, info.total_len
     ins = 8 * info.n_ins + 0.5 * info.n_ins_bases
     step = 0.5 * Q + 16 * N + 4 * K + (48 + T) * L + ins
-    return step, step - 48 * L
+    reads = 16 * N + 4 * K
+    return step, reads, step - reads - 48 * L
 
 
 def cpu_baseline(workload, scale):
-    """Time the oracle (pure-Python port of the reference, 1 core) on a bounded sample."""
+    """Time the oracle (pure-Python restatement of the reference, 1 core) on a bounded sample."""
     import tempfile
 
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -71,9 +82,19 @@ def cpu_baseline(workload, scale):
         dt = time.perf_counter() - t0
     sp = configs.spec(workload, scale=scale)
     return {"value": a / dt, "unit": "aligned bases/s", "cores": 1, "kind": "port",
-            "sample": "%s with %d refs x %d bp (%d aligned bases, %.1f s): oracle/s2c_oracle.py, the "
-                      "pure-Python restatement of sam2consensus.py, parse+pileup+vote+format, 1 thread"
-                      % (workload, sp.n_refs, sp.ref_len, a, dt)}
+            "sample": "%s at scale %g: %d refs x %d bp (%d aligned bases, %.1f s): oracle/s2c_oracle.py, the "
+                      "pure-Python restatement of sam2consensus.py, parse+pileup+vote+format, 1 thread; %s"
+                      % (workload, scale, sp.n_refs, sp.ref_len, a, dt, cpu_model())}
+
+
+def cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return "%s, %d CPUs visible" % (ln.split(":", 1)[1].strip(), os.cpu_count() or 0)
+    except OSError:
+        pass
+    return platform.processor()
 
 
 def main():
@@ -81,9 +102,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c5", choices=sorted(WORKLOADS))
+    ap.add_argument("--shard", action="store_true", help="N>1: split ONE workload over the ranks (strong scaling)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-scale", type=float, default=0.4)
+    ap.add_argument("--cpu-sample-scale", type=float, default=0.016)
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--graph", action="store_true", help="time HIP graph replays of the step")
     args = ap.parse_args()
@@ -94,7 +116,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from sam2consensus_amd import configs
+    from sam2consensus_amd import configs, shard
     from sam2consensus_amd.engine import DeviceBatch, Workspace
 
     torch.cuda.set_device(local)
@@ -104,7 +126,6 @@ def main():
 
     wl = args.workload
     opt_args = configs.cli_args(wl)
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     thresholds = [0.25]
     min_depth = 1
     if "-c" in opt_args:
@@ -113,46 +134,49 @@ def main():
         min_depth = int(opt_args[opt_args.index("-m") + 1])
 
     t0 = time.perf_counter()
-    hb = configs.synth_batch(wl, seed=configs.SEED + rank)
+    sharded = world > 1 and args.shard
+    full = configs.synth_batch(wl, seed=configs.SEED + (0 if sharded else rank))
+    hb = shard.sub_batch(full, rank, world) if sharded else full
     t_host = time.perf_counter() - t0
     info = hb.info
     T = len(thresholds)
     db = DeviceBatch(hb, dev)
     ws = Workspace(db, thresholds, min_depth, b"-")
     K = args.steps
-    # k_pileup's own duration (roofline): one pair of HIP events on the launch stream around
-    # K back-to-back pileup launches (per-launch event pairs would add their own packets to
-    # every measured kernel); also the warm-up.
+    stream = torch.cuda.current_stream(dev)
     for _ in range(args.warmup):
         ws.run()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for k in range(K):
-        ws.pileup()
-    e1.record()
-    torch.cuda.synchronize(dev)
-    pileup_ms = e0.elapsed_time(e1) / K
-    # the step: one s2c_run (or one replay of its captured HIP graph)
-    if args.graph:
-        ws.capture()
-        step = ws.replay
-    else:
-        step = ws.run
-    for _ in range(args.warmup):
-        step()
     torch.cuda.synchronize(dev)
 
+    # the timed steps: stage by stage with HIP events between the stages (on the launch stream)
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(K)]
+    if args.graph:
+        ws.capture()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(K):
-        step()
+        if args.graph:
+            ws.replay()
+            continue
+        e = ev[k]
+        e[0].record(stream)
+        ws.reads()
+        e[1].record(stream)
+        ws.pileup()
+        e[2].record(stream)
+        ws.consensus()
+        e[3].record(stream)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
+    kern = {}
+    if not args.graph:
+        for name, i0, i1 in (("k_reads", 0, 1), ("k_tile", 1, 2), ("k_consensus", 2, 3), ("step_events", 0, 3)):
+            kern[name] = sum(ev[k][i0].elapsed_time(ev[k][i1]) for k in range(K)) / K   # ms
 
     stats = torch.tensor([elapsed, float(info.aligned_bases)], dtype=torch.float64, device=dev)
     if world > 1:
@@ -165,13 +189,16 @@ def main():
         total_bases = float(info.aligned_bases)
 
     parity = None
-    if rank == 0 and not args.no_parity:
-        parity = check_parity(wl, hb, ws, thresholds)
+    if not args.no_parity:
+        if sharded:
+            parity = check_parity_sharded(wl, full, hb, ws, thresholds, rank, world)
+        elif rank == 0:
+            parity = check_parity(wl, hb, ws, thresholds)
 
     if rank == 0:
-        step_bytes, pileup_bytes = b_alg(info, T)
         ms = elapsed / K * 1e3
-        achieved = pileup_bytes / (pileup_ms * 1e-3) / 1e9
+        step_bytes, reads_bytes, tile_bytes = b_alg(full.info if sharded else info, T)
+        per_rank = 1.0 / world if sharded else 1.0
         line = {
             "metric": "aligned bases/sec into consensus (1/2/4/8 GPU); HBM GB/s; vs CPU script",
             "value": total_bases * K / elapsed,
@@ -181,23 +208,36 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic",
             "config": {"workload": WORKLOADS[wl], "aligned_bases_per_gpu": info.aligned_bases,
                        "reads_per_gpu": info.reads_mapped, "positions_per_gpu": info.total_len,
                        "thresholds": thresholds,
-                       "parallelism": "one batch per GPU, sharded by reference (no collective on the data path)"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic_from_profile(wl),
-                         "kernel": "k_pileup (counting + fused insertion-column and vote epilogue)", "kernel_ms": pileup_ms,
-                         "alg_bytes_per_launch": pileup_bytes},
-            "step_alg_bytes": step_bytes,
-            "step_achieved_gbps": step_bytes / (ms * 1e-3) / 1e9,
-            "host_parse_s_per_gpu": t_host,
-            "parity": parity,
+                       "parallelism": ("one workload split into contiguous tile ranges per GPU" if sharded else
+                                       "one batch per GPU, independent workloads (no collective on the data path)")},
         }
+        if kern:
+            tile_ms = kern["k_tile"]
+            assert tile_ms <= ms * 1.001 and kern["step_events"] <= ms * 1.05, (kern, ms)
+            achieved = tile_bytes * per_rank / (tile_ms * 1e-3) / 1e9
+            traffic = traffic_from_profile(wl)
+            line["roofline"] = {
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic.get("bytes") if traffic else None,
+                "traffic_frac": (traffic["bytes"] / (tile_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS) if traffic else None,
+                "kernel": "k_tile_dense / k_tile (pileup of the runs + insertion columns + vote + FASTA bytes)",
+                "kernel_ms": tile_ms, "alg_bytes_per_launch": tile_bytes * per_rank,
+                "traffic_source": traffic.get("source") if traffic else None}
+            line["kernels_ms"] = kern
+            line["kernels_alg_gbps"] = {"k_reads": reads_bytes * per_rank / (kern["k_reads"] * 1e-3) / 1e9,
+                                        "k_tile": achieved}
+        line["step_alg_bytes"] = step_bytes * per_rank
+        line["step_alg_gbps"] = step_bytes * per_rank / (ms * 1e-3) / 1e9
+        line["host_parse_s"] = t_host
+        line["host"] = cpu_model()
+        line["parity"] = parity
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(wl, args.cpu_sample_scale)
         print(json.dumps(line), flush=True)
@@ -206,35 +246,57 @@ def main():
 
 
 def traffic_from_profile(wl):
-    """Per-launch HBM bytes of k_pileup from the committed PMC pass (profiles/), or None."""
+    """Per-launch HBM bytes of the dominant tile kernel from the committed PMC pass, or None."""
     p = os.path.join(ROOT, "profiles", "traffic_%s.json" % wl)
     if os.path.exists(p):
         with open(p) as fh:
-            return json.load(fh).get("k_pileup_hbm_bytes_per_launch")
+            t = json.load(fh)
+        b = t.get("tile_hbm_bytes_per_launch")
+        if b:
+            return {"bytes": b, "source": "profiles/traffic_%s.json (%s)" % (wl, t.get("round", ""))}
     return None
+
+
+def _files(hb, thresholds, prefix, stats, offs, out, n):
+    import hashlib
+
+    from sam2consensus_amd.records import build_records, render
+    recs = build_records(hb, thresholds, prefix, stats, offs, out)
+    return {name + "__" + prefix + ".fasta": hashlib.sha256(render(r, n)).hexdigest() for name, r in recs.items()}
+
+
+def _golden(wl):
+    gpath = os.path.join(ROOT, "tests", "golden", "configs.json")
+    if not os.path.exists(gpath):
+        return None
+    return json.load(open(gpath)).get(wl)
 
 
 def check_parity(wl, hb, ws, thresholds):
     """Rank 0 runs the default seed: compare the step's FASTA files with the reference's."""
-    import hashlib
-
-    gpath = os.path.join(ROOT, "tests", "golden", "configs.json")
-    if not os.path.exists(gpath):
-        return None
-    g = json.load(open(gpath)).get(wl)
+    from sam2consensus_amd import configs
+    g = _golden(wl)
     if not g:
         return None
-    from sam2consensus_amd import configs
-    from sam2consensus_amd.records import build_records, render
-
-    stats, offs, out = ws.fetch()
     a = configs.cli_args(wl)
-    prefix = g["sam_file"].split(".")[0]
-    recs = build_records(hb, thresholds, prefix, stats, offs, out)
     n = int(a[a.index("-n") + 1]) if "-n" in a else 0
-    got = {name + "__" + prefix + ".fasta": hashlib.sha256(render(r, n)).hexdigest() for name, r in recs.items()}
+    got = _files(hb, thresholds, g["sam_file"].split(".")[0], *ws.fetch(), n)
     want = {k: v["sha256"] for k, v in g["files"].items()}
     return "byte-identical to reference (%d files)" % len(want) if got == want else "MISMATCH"
+
+
+def check_parity_sharded(wl, full, hb, ws, thresholds, rank, world):
+    """Every rank's shard result is gathered (RCCL) and merged on rank 0, then compared."""
+    from sam2consensus_amd import shard
+    res = shard.gather_results(ws.fetch(), hb, rank, world, len(thresholds))
+    if rank != 0:
+        return None
+    g = _golden(wl)
+    if not g:
+        return None
+    got = _files(full, thresholds, g["sam_file"].split(".")[0], *res, 0)
+    want = {k: v["sha256"] for k, v in g["files"].items()}
+    return "byte-identical to reference (%d files, %d shards)" % (len(want), world) if got == want else "MISMATCH"
 
 
 if __name__ == "__main__":

@@ -188,6 +188,9 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
 
 int  s2c_batch_info_get(const s2c_batch *b, s2c_batch_info *out);
 int  s2c_batch_arrays_get(const s2c_batch *b, s2c_batch_arrays *out);
+/* The sub-batch of tiles [t0, t1) for one GPU of a multi-GPU run (positions keep their
+ * global coordinates; free it with s2c_batch_free). */
+int  s2c_batch_shard(const s2c_batch *b, int64_t t0, int64_t t1, s2c_batch **out);
 /* Reference name i (NUL-terminated, owned by the batch). */
 const char *s2c_batch_ref_name(const s2c_batch *b, int64_t i);
 void s2c_batch_free(s2c_batch *b);

@@ -203,6 +203,7 @@ struct s2c_batch {
     std::vector<std::string> names;
     std::vector<int64_t> ref_len, ref_off, ref_reads;
     std::vector<uint32_t> pc, ops, bq, bx, rs, tiles, items, dense, deep, lp, wtile;
+    std::vector<uint32_t> kmin, kmax;   // host only: global key range of each piece's insertion events
 };
 
 static int perr(s2c_parser *p, int code, const std::string &msg) {
@@ -381,7 +382,7 @@ static int process_record(Chunk &c, const RefView &rv, std::string &last_name, i
         }
         if (op != S2C_OP_S && op != S2C_OP_H) c.ntokens++;
     }
-    if (klen >= ((int64_t)1 << 31)) return fail(S2C_ERR_LIMIT, "seqout longer than 2^31");
+    if (klen >= ((int64_t)1 << 24)) return fail(S2C_ERR_LIMIT, "seqout of 2^24 or more positions not supported");
     c.aligned += klen;
     c.qbases += mb;
     if (ref < 0) return fail(S2C_ERR_KEY, "KeyError: '" + std::string(nb, nl) + "' (:212/:221)");
@@ -660,6 +661,7 @@ struct Piece {
     uint32_t chunk, read;
     uint8_t range, ins, lng;
     uint32_t nslots;        // prefix words + tokens
+    uint32_t kmin, kmax;    // global keys of the insertion events it emits (ins)
 };
 }  // namespace
 
@@ -730,23 +732,31 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
             const ReadRec &r = c.reads[ri];
             const int64_t L = p->ref_len[r.ref], off = b->ref_off[r.ref];
             bool any_key = false;   // an event the consensus can emit (key >= 0)
-            for (uint32_t e = r.ev0; e < r.ev0 + r.nev; e++) any_key |= c.ev[e].key >= 0;
+            uint64_t kmin = ~0ull, kmax = 0;
+            for (uint32_t e = r.ev0; e < r.ev0 + r.nev; e++)
+                if (c.ev[e].key >= 0) {
+                    any_key = true;
+                    kmin = std::min<uint64_t>(kmin, (uint64_t)(off + c.ev[e].key));
+                    kmax = std::max<uint64_t>(kmax, (uint64_t)(off + c.ev[e].key));
+                }
             const size_t first = pcs.size();
             if (r.kc0 >= 0) {
                 const int64_t pa = r.pos0 + r.kc0;
                 if (pa < 0) {
                     const int64_t kb = std::min(r.kc1, -r.pos0);
-                    pcs.push_back({(uint64_t)(off + L + pa), r.kc0, kb, ci, ri, 1, 0, 0, 0});
-                    if (r.kc1 > -r.pos0) pcs.push_back({(uint64_t)off, -r.pos0, r.kc1, ci, ri, 1, 0, 0, 0});
+                    pcs.push_back({(uint64_t)(off + L + pa), r.kc0, kb, ci, ri, 1, 0, 0, 0, 0, 0});
+                    if (r.kc1 > -r.pos0) pcs.push_back({(uint64_t)off, -r.pos0, r.kc1, ci, ri, 1, 0, 0, 0, 0, 0});
                 } else {
                     const bool whole = r.kc0 == 0 && r.kc1 == r.klen;
-                    pcs.push_back({(uint64_t)(off + pa), r.kc0, r.kc1, ci, ri, (uint8_t)!whole, 0, 0, 0});
+                    pcs.push_back({(uint64_t)(off + pa), r.kc0, r.kc1, ci, ri, (uint8_t)!whole, 0, 0, 0, 0, 0});
                 }
                 b->ref_reads[r.ref] += (int64_t)(pcs.size() - first);
             }
-            if (any_key) {
-                if (pcs.size() == first) pcs.push_back({(uint64_t)off, 0, 0, ci, ri, 1, 0, 0, 0});
+            if (any_key) {   // (a read with events but nothing counted: a zero-span piece at its first key)
+                if (pcs.size() == first) pcs.push_back({kmin, 0, 0, ci, ri, 1, 0, 0, 0, 0, 0});
                 pcs[first].ins = 1;
+                pcs[first].kmin = (uint32_t)kmin;
+                pcs[first].kmax = (uint32_t)kmax;
             }
             for (size_t k = first; k < pcs.size(); k++) ref_span[r.ref] += pcs[k].kb - pcs[k].ka;
         }
@@ -796,11 +806,14 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
         qoff[k + 1] = qoff[k] + (uint64_t)align_up(r.slen, 16);
     }
     const uint64_t NOPS = ooff[NP], NQ = qoff[NP];
-    if (NOPS >= (1ull << 32) - 1) return s2c_set_error(S2C_ERR_LIMIT, "more than 2^32 op words (split the input)");
-    if (NQ / 16 >= (1ull << 32) - 1) return s2c_set_error(S2C_ERR_LIMIT, "more than 2^36 query bases (split the input)");
+    // the kernels address run records and base planes with 32-bit buffer offsets (< 3.5 GB)
+    if (16 * NOPS >= 0xE0000000ull) return s2c_set_error(S2C_ERR_LIMIT, "more than 2^28 op words (split the input)");
+    if (NQ / 4 >= 0xE0000000ull) return s2c_set_error(S2C_ERR_LIMIT, "more than 14 G query bases (split the input)");
     I.n_ops = (int64_t)NOPS;
     I.n_qwords = (int64_t)((NQ + 31) / 32) + 2;
     b->pc.assign(4 * (size_t)(NP + 1), 0u);
+    b->kmin.assign(NP, 0xFFFFFFFFu);
+    b->kmax.assign(NP, 0u);
     b->ops.resize(std::max<uint64_t>(NOPS, 1));
     b->bq.assign(2 * (size_t)I.n_qwords, 0u);
     b->bx.assign((size_t)I.n_qwords, 0u);
@@ -819,6 +832,8 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
                 if (q.range) { fl |= S2C_PF_RANGE; *o++ = (uint32_t)q.ka; *o++ = (uint32_t)q.kb; }
                 if (q.ins) {
                     fl |= S2C_PF_INS;
+                    b->kmin[k] = q.kmin;
+                    b->kmax[k] = q.kmax;
                     const int64_t off = b->ref_off[r.ref], key0 = off + r.pos0;
                     *o++ = (uint32_t)(uint64_t)key0;
                     *o++ = (uint32_t)((uint64_t)key0 >> 32);
@@ -983,6 +998,162 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
     I.n_cols = (int64_t)coff;
     I.runs_max = runs_max;
     *out = guard.release();
+    return S2C_OK;
+}
+
+// ------------------------------------------------------------------ shards (multi-GPU)
+// The sub-batch of tiles [t0, t1): the pieces whose runs can cover those tiles (short ones
+// starting up to kwin + 1 words before, the long ones listed for them) or whose insertion
+// events are keyed inside them, with their op words and base planes; run slots, long
+// lists, hash-table / column slot bases and tile indices re-based.  Positions keep their
+// global coordinates; words outside the shard map to no tile (k_reads drops events keyed
+// there).  Counts of a position depend only on the runs covering it, so every shard's
+// tiles get exactly the unsharded counts — no exchange of counts is needed.
+extern "C" int s2c_batch_shard(const s2c_batch *b, int64_t t0, int64_t t1, s2c_batch **out) {
+    if (!b || !out) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
+    const s2c_batch_info &I = b->info;
+    if (t0 < 0 || t1 > I.n_tiles || t0 > t1) return s2c_set_error(S2C_ERR_ARG, "bad tile range");
+    std::unique_ptr<s2c_batch> s(new s2c_batch());
+    s2c_batch_info &J = s->info;
+    J = I;
+    s->names = b->names;
+    s->ref_len = b->ref_len;
+    s->ref_off = b->ref_off;
+    s->ref_reads = b->ref_reads;
+    const int64_t NP = I.n_pieces, NW = I.n_words, K = I.kwin;
+    const uint32_t *T0 = &b->tiles[(size_t)t0 * S2C_TILE_WORDS];
+    const uint64_t A = t1 > t0 ? T0[0] : 0, B = t1 > t0 ? b->tiles[(size_t)(t1 - 1) * S2C_TILE_WORDS + 1] : 0;
+    const int64_t W0 = (int64_t)(A >> 5), W1 = (int64_t)((B + 31) >> 5);
+    // ---- pieces: the window range, long pieces listed by the tiles, event pieces keyed inside
+    std::vector<uint8_t> take(NP, 0);
+    auto piece_at_word = [&](int64_t w) {   // first piece with start word >= w
+        int64_t lo = 0, hi = NP;
+        while (lo < hi) {
+            const int64_t m = (lo + hi) / 2;
+            if ((int64_t)(b->pc[4 * m] >> 5) < w) lo = m + 1; else hi = m;
+        }
+        return lo;
+    };
+    if (t1 > t0) {
+        const int64_t pa = piece_at_word(std::max<int64_t>(W0 - K - 1, 0)), pb = piece_at_word(W1);
+        for (int64_t k = pa; k < pb; k++) take[k] = 1;
+        auto piece_of_slot = [&](uint32_t slot) {   // piece whose op range holds slot
+            int64_t lo = 0, hi = NP - 1;
+            while (lo < hi) {
+                const int64_t m = (lo + hi + 1) / 2;
+                if (b->pc[4 * m + 2] <= slot) lo = m; else hi = m - 1;
+            }
+            return lo;
+        };
+        for (int64_t t = t0; t < t1; t++) {
+            const uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
+            for (uint32_t e = tw[10]; e < tw[11]; e++) take[piece_of_slot(b->lp[e])] = 1;
+        }
+        for (int64_t k = 0; k < NP; k++)
+            if (b->kmin[k] != 0xFFFFFFFFu && b->kmax[k] >= A && b->kmin[k] < B) take[k] = 1;
+    }
+    std::vector<int64_t> sel;
+    for (int64_t k = 0; k < NP; k++)
+        if (take[k]) sel.push_back(k);
+    const int64_t NS = (int64_t)sel.size();
+    std::vector<uint64_t> ooff(NS + 1, 0), qoff(NS + 1, 0);
+    for (int64_t i = 0; i < NS; i++) {
+        const int64_t k = sel[i];
+        ooff[i + 1] = ooff[i] + (b->pc[4 * (k + 1) + 2] - b->pc[4 * k + 2]);
+        qoff[i + 1] = qoff[i] + ((b->pc[4 * k + 3] & 0xFFFFFFu) + 15) / 16 * 16;
+    }
+    J.n_pieces = NS;
+    J.n_ops = (int64_t)ooff[NS];
+    J.n_qwords = (int64_t)((qoff[NS] + 31) / 32) + 2;
+    s->pc.assign(4 * (size_t)(NS + 1), 0u);
+    s->ops.resize(std::max<uint64_t>(ooff[NS], 1));
+    s->bq.assign(2 * (size_t)J.n_qwords, 0u);
+    s->bx.assign((size_t)J.n_qwords, 0u);
+    s->kmin.assign(NS, 0xFFFFFFFFu);
+    s->kmax.assign(NS, 0u);
+    std::vector<uint32_t> slot_map;   // old op index → new, for the long lists (sparse use)
+    std::unordered_map<uint32_t, uint32_t> slot_new;
+    {
+        const uint16_t *sq = (const uint16_t *)b->bq.data(), *sx = (const uint16_t *)b->bx.data();
+        uint16_t *dq = (uint16_t *)s->bq.data(), *dx = (uint16_t *)s->bx.data();
+        for (int64_t i = 0; i < NS; i++) {
+            const int64_t k = sel[i];
+            const uint32_t o0 = b->pc[4 * k + 2], o1 = b->pc[4 * (k + 1) + 2];
+            memcpy(&s->ops[ooff[i]], &b->ops[o0], 4 * (size_t)(o1 - o0));
+            uint32_t *pr = &s->pc[4 * (size_t)i];
+            pr[0] = b->pc[4 * k];
+            pr[1] = (uint32_t)(qoff[i] / 16);
+            pr[2] = (uint32_t)ooff[i];
+            pr[3] = b->pc[4 * k + 3];
+            if (pr[3] >> 24 & S2C_PF_LONG)
+                for (uint32_t o = o0; o < o1; o++) slot_new[o] = (uint32_t)(ooff[i] + (o - o0));
+            s->kmin[i] = b->kmin[k];
+            s->kmax[i] = b->kmax[k];
+            const uint32_t slen = b->pc[4 * k + 3] & 0xFFFFFFu;
+            for (uint64_t h = 0; h < (slen + 15) / 16; h++) {
+                const uint64_t a = (uint64_t)b->pc[4 * k + 1] + h, d = qoff[i] / 16 + h;
+                dq[(d >> 1) * 4 + (d & 1)] = sq[(a >> 1) * 4 + (a & 1)];
+                dq[(d >> 1) * 4 + 2 + (d & 1)] = sq[(a >> 1) * 4 + 2 + (a & 1)];
+                dx[d] = sx[a];
+            }
+        }
+        s->pc[4 * (size_t)NS + 2] = (uint32_t)ooff[NS];
+    }
+    s->rs.assign(NW + 1, 0u);
+    for (int64_t i = 0; i < NS; i++) s->rs[(s->pc[4 * i] >> 5) + 1] += (uint32_t)(ooff[i + 1] - ooff[i]);
+    for (int64_t w = 0; w < NW; w++) s->rs[w + 1] += s->rs[w];
+    // ---- tiles [t0, t1): slot bases re-based, long lists remapped, plan lists re-indexed
+    const int64_t NT = t1 - t0;
+    J.n_tiles = NT;
+    s->tiles.assign(b->tiles.begin() + t0 * S2C_TILE_WORDS, b->tiles.begin() + t1 * S2C_TILE_WORDS);
+    const uint32_t boff0 = NT ? T0[4] : 0, loff0 = NT ? T0[6] : 0, coff0 = NT ? T0[8] : 0;
+    int64_t nbkt = 0, nlng = 0, ncol = 0;
+    for (int64_t t = 0; t < NT; t++) {
+        uint32_t *tw = &s->tiles[(size_t)t * S2C_TILE_WORDS];
+        tw[4] -= boff0;
+        tw[6] -= loff0;
+        tw[8] -= coff0;
+        nbkt = std::max<int64_t>(nbkt, (int64_t)tw[4] + tw[5]);
+        nlng = std::max<int64_t>(nlng, (int64_t)tw[6] + tw[7]);
+        ncol = std::max<int64_t>(ncol, (int64_t)tw[8] + tw[9]);
+        const uint32_t l0 = (uint32_t)s->lp.size();
+        for (uint32_t e = tw[10]; e < tw[11]; e++) s->lp.push_back(slot_new.at(b->lp[e]));
+        tw[10] = l0;
+        tw[11] = (uint32_t)s->lp.size();
+    }
+    J.n_long = (int64_t)s->lp.size();
+    if (s->lp.empty()) s->lp.push_back(0);
+    J.n_bkt = nbkt;
+    J.n_lng = nlng;
+    J.n_cols = ncol;
+    s->wtile.assign(NW, 0xFFFFFFFFu);
+    for (int64_t w = W0; w < W1; w++)
+        if (b->wtile[w] != 0xFFFFFFFFu) s->wtile[w] = b->wtile[w] - (uint32_t)t0;
+    auto sub_items = [&](const std::vector<uint32_t> &src, std::vector<uint32_t> &dst) {
+        for (size_t i = 0; i < src.size(); i += S2C_ITEM_WORDS)
+            if (src[i] >= (uint64_t)t0 && src[i] < (uint64_t)t1) {
+                dst.insert(dst.end(), &src[i], &src[i] + S2C_ITEM_WORDS);
+                dst[dst.size() - S2C_ITEM_WORDS] -= (uint32_t)t0;
+            }
+    };
+    sub_items(b->items, s->items);
+    sub_items(b->dense, s->dense);
+    for (uint32_t t : b->deep)
+        if (t >= (uint64_t)t0 && t < (uint64_t)t1) s->deep.push_back(t - (uint32_t)t0);
+    J.n_items = (int64_t)(s->items.size() / S2C_ITEM_WORDS);
+    J.n_dense = (int64_t)(s->dense.size() / S2C_ITEM_WORDS);
+    J.n_deep = (int64_t)s->deep.size();
+    int64_t runs_max = 0, aligned = 0;
+    for (int64_t t = 0; t < NT; t++) {
+        const uint32_t *tw = &s->tiles[(size_t)t * S2C_TILE_WORDS];
+        const int64_t w0 = tw[0] >> 5, w1 = (tw[1] + 31) >> 5;
+        runs_max = std::max<int64_t>(runs_max, (int64_t)s->rs[w1] - (int64_t)s->rs[std::max<int64_t>(w0 - K, 0)]);
+        aligned += tw[1] - tw[0];
+    }
+    J.runs_max = runs_max;
+    // the shard's share of the workload's aligned bases (by its positions; for reporting)
+    J.aligned_bases = I.total_len ? (int64_t)((double)I.aligned_bases * (double)aligned / (double)I.total_len) : 0;
+    *out = s.release();
     return S2C_OK;
 }
 

@@ -64,6 +64,7 @@ __device__ __forceinline__ uint64_t mix64(uint64_t k) {
 // One insertion event (global key gkey, motif = query bases [q, q + len)) into its tile.
 __device__ void add_event(const ReadsArgs &d, uint64_t gkey, uint64_t q, uint32_t len) {
     const uint32_t t = d.wtile[gkey >> 5];
+    if (t == 0xFFFFFFFFu) return;   // keyed outside this batch's tiles (a multi-GPU shard)
     const uint4 tw0 = ((const uint4 *)d.tiles)[(size_t)t * (S2C_TILE_WORDS / 4)];
     const uint4 tw1 = ((const uint4 *)d.tiles)[(size_t)t * (S2C_TILE_WORDS / 4) + 1];
     const uint32_t pos = (uint32_t)(gkey - tw0.x);   // tile-relative (< 2048)

@@ -550,7 +550,7 @@ __device__ __forceinline__ void tile_epilogue_fast(const D &d, uint32_t tile, co
                     for (int v = 0; v < 2; v++) {
                         if ((P[v].fl & 3u) != 1u) continue;   // in the tile, not called: fill
                         const uint32_t o = v ? o1 : o0;
-                        for (uint32_t f = 0; f < F; f++) ob[o + f] = L.fill[f];
+                        for (uint32_t f = 0; f < F; f++) ob[o + f] = f < (uint32_t)FILL_LDS ? L.fill[f] : d.fill[f];
                     }
                 }
                 if (multi) {   // insertion chars after the key's char (:370-385)

@@ -194,6 +194,25 @@ def check_plan(hb):
     assert sorted(hb.deep.tolist()) == [t for t in range(i.n_tiles) if T[t, 3] & 3]
 
 
+def check_plan_shard(sub):
+    """A shard's sub-batch: pieces bucketed, run-slot CSR consistent, its tiles mapped."""
+    i = sub.info
+    pc = sub.pc.astype(np.int64)
+    sw = pc[:i.n_pieces, 0] >> 5
+    assert (np.diff(sw) >= 0).all()
+    rs = sub.rs.astype(np.int64)
+    assert rs[0] == 0 and rs[-1] == i.n_ops
+    T = sub.tiles.astype(np.int64)
+    for t, row in enumerate(T):
+        assert (sub.wtile[row[0] >> 5:(row[1] + 31) >> 5] == t).all()
+    n = len(hb_items(sub))
+    assert n == i.n_tiles + int(sum(max(0, c) for c in []))
+
+
+def hb_items(hb):
+    return sorted(set(hb.items[:, 0].tolist()) | set(hb.dense[:, 0].tolist()))
+
+
 def _span(hb, k):
     """Seqout span of piece k (from its RANGE prefix or its tokens)."""
     pc, ops = hb.pc, hb.ops

@@ -21,12 +21,12 @@ def _files(hb, opt, stats, offs, out):
 
 def _virtual(hb, opt, world):
     parts, stats = [], None
-    for rank, (t0, t1) in enumerate(shard.split_tiles(hb, world)):
-        sub = shard.SubBatch(hb, t0, t1)
-        bm.check_device_records(sub)
+    for rank in range(world):
+        sub = shard.sub_batch(hb, rank, world)
+        bm.check_plan_shard(sub)
         st, offs, out = bm.model_pipeline(sub, opt.thresholds, opt.min_depth, opt.fill.encode("latin-1"))
         stats = st if stats is None else stats + st
-        parts.append((t0, t1, offs, out))
+        parts.append((sub.t0, sub.t1, offs, out))
     offs, out = shard.merge_outputs(parts, len(opt.thresholds))
     return _files(hb, opt, stats, offs, out)
 
@@ -43,7 +43,10 @@ def _big_case():
     for s in range(1, 2800, 5):
         rows.append(("b", s, "40M3D60M", "TTGCA" * 20))
     rows.append(("b", 10, "10M2000N10M", "G" * 20))
+    rows.append(("b", 1500, "5M2I", "GGGGGTT"))           # insertion keyed after the last base
+    rows.append(("b", 2000, "3S4I", "AAACCCC"))            # events, nothing counted
     rows.append(("c", 0, "5M", "CCCCC"))
+    rows.append(("c", 0, "1M2I3M", "AGGCCC"))              # POS=0 wrap with an insertion
     for r in rows:
         sam += "r\t0\t%s\t%d\t60\t%s\t*\t0\t0\t%s\t*\n" % r
     return sam
@@ -66,7 +69,7 @@ def test_split_is_balanced_and_contiguous():
     hb = configs.synth_batch("c2", n_refs=40)
     for world in (2, 4, 8):
         rng = shard.split_tiles(hb, world)
-        assert rng[0][0] == 0 and rng[-1][1] == hb.info.n_blocks
+        assert rng[0][0] == 0 and rng[-1][1] == hb.info.n_tiles
         assert all(rng[k][1] == rng[k + 1][0] for k in range(world - 1))
         w = shard.tile_weights(hb)
         loads = [w[a:b].sum() for a, b in rng]

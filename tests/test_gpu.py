@@ -32,7 +32,7 @@ def test_hip_path_matches_reference(case):
     from sam2consensus_amd.cli import run_text
     status, files = run_text(case["sam"], case["args"])
     assert status == case["status"]
-    assert files == case["files"]
+    assert files == case["files"], sorted(files)
 
 
 def _ws(hb, thresholds, min_depth=1, fill=b"-", keep_counts=False):
@@ -67,6 +67,14 @@ def test_runs_and_counts_equal_batch_model(name, over):
 def torch_i32():
     import torch
     return torch.int32
+
+
+def _first_diff(a, b):
+    """Short description of the first differing byte (pytest's own diff of MB-sized bytes
+    objects takes minutes)."""
+    n = min(len(a), len(b))
+    i = next((k for k in range(n) if a[k] != b[k]), n)
+    return "lengths %d / %d, first difference at byte %d: %r vs %r" % (len(a), len(b), i, a[i:i + 16], b[i:i + 16])
 
 
 def _sha_files(files):
@@ -145,32 +153,27 @@ def test_repeated_runs_identical():
         assert (a[0] == b[0]).all() and (a[1] == b[1]).all() and a[2] == b[2]
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_on_device(world):
-    """Position-range shards run through libs2c.so and merged == the unsharded run."""
+@pytest.mark.parametrize("name,world", [("c1", 4), ("c2", 3), ("c5", 2)])
+def test_sharded_on_device_matches_golden(name, world):
+    """Tile-range shards (s2c_batch_shard) run through libs2c.so, merged == the reference."""
     from sam2consensus_amd import configs, shard
     from sam2consensus_amd.engine import DeviceBatch, Workspace
-    from sam2consensus_amd.records import build_records, render
-    thr = [0.25, 0.5, 0.75]
-    hb = configs.synth_batch("c2", n_refs=24)
-
-    def files(stats, offs, out):
-        recs = build_records(hb, thr, "x", stats, offs, out)
-        return {n: render(r, 0) for n, r in recs.items()}
-
-    ws = Workspace(DeviceBatch(hb), thr)
-    ws.run()
-    want = files(*ws.fetch())
+    g = CONFIGS[name]
+    opt = o.parse_argv(["-i", g["sam_file"]] + g["args"])
+    hb = configs.synth_batch(name)
     parts, stats = [], None
-    for t0, t1 in shard.split_tiles(hb, world):
-        sub = shard.SubBatch(hb, t0, t1)
-        w2 = Workspace(DeviceBatch(sub), thr)
-        w2.run()
-        st, offs, out = w2.fetch()
+    for rank in range(world):
+        sub = shard.sub_batch(hb, rank, world)
+        ws = Workspace(DeviceBatch(sub), opt.thresholds, opt.min_depth, opt.fill.encode())
+        ws.run()
+        st, offs, out = ws.fetch()
         stats = st if stats is None else stats + st
-        parts.append((t0, t1, offs, out))
-    offs, out = shard.merge_outputs(parts, len(thr))
-    assert files(stats, offs, out) == want
+        parts.append((sub.t0, sub.t1, offs, out))
+    offs, out = shard.merge_outputs(parts, len(opt.thresholds))
+    from sam2consensus_amd.records import build_records, render
+    recs = build_records(hb, opt.thresholds, opt.prefix.encode(), stats, offs, out)
+    got = {n + "__" + opt.prefix + ".fasta": hashlib.sha256(render(r, opt.n)).hexdigest() for n, r in recs.items()}
+    assert got == {k: v["sha256"] for k, v in g["files"].items()}
 
 
 @pytest.mark.parametrize("name,over,thr,md,fill", [
@@ -210,14 +213,14 @@ def test_device_pipeline_equals_batch_model(name, over, thr, md, fill):
         p = os.path.join(td, "case.sam")
         configs.synth_write(name, p, **over)
         text = open(p, "rb").read().decode("latin-1")
-    args = ["-c", ",".join(repr(t) for t in thr), "-m", str(md), "-f", fill.decode("latin-1")]
+    args = ["--consensus-thresholds=" + ",".join(repr(t) for t in thr), "-m", str(md), "--fill=" + fill.decode("latin-1")]
     ref = o.run_case(text, args, name="case.sam")
     for _ in range(2):   # second run: no state of the first may leak
         ws.run()
         st, offs, out = ws.fetch()
         assert (st == want[0]).all()
         assert (offs == want[1]).all()
-        assert out == want[2]
+        assert out == want[2], _first_diff(out, want[2])
     if ref["status"] == "ok" and fill:
         from sam2consensus_amd.records import build_records, render
         recs = build_records(hb, thr, "case", st, offs, out)
