@@ -90,6 +90,8 @@ int s2c_layout(int64_t *out, int n);
                                 insertion events; key0 = ref_off + POS-1 (int64), an event at
                                 seqout index k has global key key0 + k, used when ≥ ref_off */
 #define S2C_PF_LONG   0x08   /* span > the batch's window: reached through the tile long lists */
+#define S2C_PF_RUNS   0x10   /* a non-dense tile reads its runs: k_reads writes them (dense tiles
+                                walk their window's pieces themselves) */
 
 /* run record (device-written by k_reads, parallel to ops[]): {gpos, len | kind << 24, qlo, qhi} */
 #define S2C_RUN_EMPTY   0u
@@ -100,7 +102,10 @@ int s2c_layout(int64_t *out, int n);
 #define S2C_RUN_LONG   0x10u /* (kind bits) run of a long piece: skipped by the rs window */
 
 /* tile record tiles[t][S2C_TILE_WORDS] */
-#define S2C_TILE_WORDS   16  /* {a, b, ref, flags, boff, bcap, loff, lcap, cb0, ccap, lp0, lp1, nev, 0, 0, 0} */
+#define S2C_TILE_WORDS   20  /* {a, b, ref, flags, boff, bcap, loff, lcap, cb0, ccap, lp0, lp1, nev,
+                                 pf0, pf1, o0, o1, qw0, qw1, 0}: the window's pieces [pf0, pf1) (short
+                                 pieces starting in [a/32 - kwin, b/32)), their op slots [o0, o1) and
+                                 base plane words [qw0, qw1) */
 #define S2C_TILE_DEEP     1  /* several work items: counts summed in HBM, voted by k_consensus */
 #define S2C_TILE_GENERAL  2  /* insertion layout beyond k_tile's LDS: voted by k_consensus */
 #define S2C_TILE_DENSE    4  /* routed to k_tile_dense (one item, no insertion keys, no long pieces) */
@@ -108,7 +113,9 @@ int s2c_layout(int64_t *out, int n);
 #define S2C_EPI_KEYS    256  /* insertion keys per tile k_tile's epilogue holds in LDS */
 /* insertion columns per tile k_tile's epilogue holds in LDS, by words per tile */
 #define S2C_LDS_COLS(nwp) ((nwp) <= 16 ? 640 : ((nwp) == 32 ? 448 : 192))
-#define S2C_DENSE_RUNS 1024  /* runs a dense tile stages in LDS */
+#define S2C_DENSE_LDS 24576  /* bytes of LDS a dense tile stages its window in: 12 per base plane
+                                 word, 12 per op slot (op word + run record), 16 per piece record
+                                 (+1), and 1 KB of DMA slack */
 #define S2C_SHORT_MOTIF  16  /* motifs up to this length are hashed inline (3-bit codes) */
 #define S2C_CODE_FILL     0  /* internal vote char of a fill position */
 #define S2C_CODE_ERR   0xFF  /* vote char where the vote hit a missing amb key (:367) */
@@ -154,6 +161,7 @@ typedef struct {
     int64_t n_dense;           /* dense tiles (k_tile_dense; k_tile when len(-f) != 1) */
     int64_t n_deep;            /* tiles voted by k_consensus (deep or general) */
     int64_t n_long;            /* long-list entries (tile, run slot of a long piece) */
+    int64_t n_rlist;           /* pieces k_reads walks */
     int64_t kwin;              /* window: a short piece spans <= kwin + 1 words */
     int64_t tile_max;          /* max positions of any tile (<= 2048) */
     int64_t chunk;             /* candidate run slots per word per work item */
@@ -181,6 +189,7 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
     const uint32_t *items;     /* [n_items][S2C_ITEM_WORDS] */
     const uint32_t *dense;     /* [n_dense][S2C_ITEM_WORDS] items of the dense tiles */
     const uint32_t *deep;      /* [n_deep] tiles k_consensus votes */
+    const uint32_t *rlist;     /* [n_rlist] pieces k_reads walks (PF_RUNS or PF_INS) */
     const uint32_t *lp;        /* [n_long] run slots of the long pieces overlapping each tile:
                                   tile t's are lp[tiles[t].lp0 .. tiles[t].lp1) */
     const uint32_t *wtile;     /* [n_words] tile of each 32-position word (0xFFFFFFFF: padding) */
@@ -234,8 +243,8 @@ int s2c_synth_write(const s2c_synth_spec *spec, const char *path, int64_t *n_rea
 typedef struct {
     /* ---- packed batch (device copies of s2c_batch_arrays) ---- */
     const uint32_t *pc, *ops, *bq, *bx, *rs;
-    const uint32_t *tiles, *items, *dense, *deep, *lp, *wtile;
-    int64_t n_pieces, n_ops, n_qwords, n_tiles, n_items, n_dense, n_deep, padded_len, chunk;
+    const uint32_t *tiles, *items, *dense, *deep, *lp, *wtile, *rlist;
+    int64_t n_pieces, n_ops, n_qwords, n_tiles, n_items, n_dense, n_deep, padded_len, chunk, n_rlist;
     int32_t kwin, tile_max;
 
     /* ---- options (:102, :117-138) ---- */
@@ -291,8 +300,8 @@ int s2c_consensus(const s2c_dev *d, void *stream);
 /* all three, in order, on one stream (graph-capturable: no allocation, no sync) */
 int s2c_run(const s2c_dev *d, void *stream);
 
-/* Diagnostics (tests only, not part of the product path): s2c_pileup with every tile's
- * counts stored to d->counts ([6][padded_len] u32) and no vote. */
+/* Diagnostics (tests only, not part of the product path): k_reads over every piece, then
+ * every tile's counts stored to d->counts ([6][padded_len] u32) and no vote. */
 int s2c_pileup_counts(const s2c_dev *d, void *stream);
 
 #ifdef __cplusplus

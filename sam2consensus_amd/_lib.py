@@ -25,12 +25,12 @@ S2C_ERR_LIMIT = -13
 
 S2C_NSYM = 6
 S2C_POS_ALIGN = 64
-S2C_TILE_WORDS = 16
+S2C_TILE_WORDS = 20
 S2C_ITEM_WORDS = 4
 S2C_CODE_FILL = 0
 S2C_SHORT_MOTIF = 16
 S2C_TILE_DEEP, S2C_TILE_GENERAL, S2C_TILE_DENSE = 1, 2, 4
-S2C_PF_X, S2C_PF_RANGE, S2C_PF_INS, S2C_PF_LONG = 1, 2, 4, 8
+S2C_PF_X, S2C_PF_RANGE, S2C_PF_INS, S2C_PF_LONG, S2C_PF_RUNS = 1, 2, 4, 8, 16
 S2C_RUN_EMPTY, S2C_RUN_BASES, S2C_RUN_DASH = 0, 1, 2
 S2C_RUN_XBIT, S2C_RUN_DROP, S2C_RUN_LONG = 4, 8, 16
 OPS = "MIDNSHP=X"   # opcode order of the token words (len << 4 | opcode)
@@ -52,7 +52,7 @@ class BatchInfo(C.Structure):
     _fields_ = [(n, C.c_int64) for n in (
         "n_refs", "total_len", "padded_len", "header_lines", "lines_total", "reads_mapped",
         "aligned_bases", "query_bases", "n_pieces", "n_ops", "n_tokens", "n_qwords", "n_words",
-        "n_tiles", "n_items", "n_dense", "n_deep", "n_long", "kwin", "tile_max", "chunk",
+        "n_tiles", "n_items", "n_dense", "n_deep", "n_long", "n_rlist", "kwin", "tile_max", "chunk",
         "n_ins", "n_ins_bases", "n_bkt", "n_lng", "n_cols", "runs_max")]
 
 
@@ -62,7 +62,7 @@ _P32 = C.POINTER(C.c_uint32)
 
 class BatchArrays(C.Structure):
     _fields_ = [("ref_len", _P64), ("ref_off", _P64), ("ref_cov_reads", _P64)] + \
-        [(n, _P32) for n in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile")]
+        [(n, _P32) for n in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "rlist", "lp", "wtile")]
 
 
 class SynthSpec(C.Structure):
@@ -78,9 +78,10 @@ _VP = C.c_void_p
 
 class Dev(C.Structure):
     """Mirror of ``s2c_dev`` (include/s2c.h)."""
-    _fields_ = [(n, _VP) for n in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile")] + \
+    _fields_ = [(n, _VP) for n in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile",
+                                   "rlist")] + \
         [(n, C.c_int64) for n in ("n_pieces", "n_ops", "n_qwords", "n_tiles", "n_items", "n_dense", "n_deep",
-                                  "padded_len", "chunk")] + [
+                                  "padded_len", "chunk", "n_rlist")] + [
         ("kwin", C.c_int32), ("tile_max", C.c_int32),
         ("maxdel_active", C.c_int32), ("maxdel", C.c_int32),
         ("thresholds", _VP), ("n_thr", C.c_int32), ("min_depth", C.c_int32),

@@ -59,6 +59,109 @@ __device__ __forceinline__ void lds_sync() {
 // s_waitcnt vmcnt(0) as a real S_WAITCNT (the compiler's wait tracking sees it)
 __device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
+
+// ----------------------------------------------------------------- parsecigar on the device
+__device__ __forceinline__ bool op_bases(uint32_t op) { return op == S2C_OP_M || op == S2C_OP_EQ || op == S2C_OP_X; }
+__device__ __forceinline__ bool op_dash(uint32_t op) { return op == S2C_OP_D || op == S2C_OP_N || op == S2C_OP_P; }
+
+// The token walk of the reference's parsecigar (:64-81) over one piece (start = query
+// index, k = seqout index):
+//   M / = / X   take = min(l, len(SEQ) - start) bases (SEQ truncation, :67), k += take
+//   D / N / P   l '-' (:70-72), k += l
+//   I           event (start_ref, SEQ[start:start+l]) if the slice is non-empty (:73-75)
+//   S           start += l (:76-77);  H nothing (:78-79)
+// with the maxdel rule (:210): the '-' of a read whose seqout holds more than maxdel of them
+// (D/N/P lengths + '-' chars of the bases taken) are not counted.  run(j, gpos, len, kind, q)
+// is called for every op word j of the piece (kind S2C_RUN_EMPTY for prefix words, I / S / H
+// and parts outside the piece's seqout range); ev(gkey, q, len) for every insertion event of
+// an S2C_PF_INS piece keyed at a position ≥ 0 of its reference.  Mem gives op words and base
+// plane words (global index): op(j), p0(w), p1(w), x(w).
+template <class Mem, class RunFn, class EvFn>
+__device__ __forceinline__ void walk_piece(const Mem &m, const uint4 P, uint32_t oend, bool maxdel_active, uint32_t maxdel,
+                                           RunFn &&run, EvFn &&ev) {
+    const uint32_t slen = P.w & 0xFFFFFFu, fl = P.w >> 24;
+    const uint64_t q0 = (uint64_t)P.y * 16;
+    uint32_t o = P.z;
+    int64_t ka = 0, kb = INT64_MAX;
+    if (fl & S2C_PF_RANGE) {
+        ka = m.op(o);
+        kb = m.op(o + 1);
+        run(o, 0u, 0u, S2C_RUN_EMPTY, 0ull);
+        run(o + 1, 0u, 0u, S2C_RUN_EMPTY, 0ull);
+        o += 2;
+    }
+    int64_t key0 = 0;
+    uint32_t roff = 0;
+    const bool ins = (fl & S2C_PF_INS) != 0;
+    if (ins) {
+        key0 = (int64_t)((uint64_t)m.op(o) | ((uint64_t)m.op(o + 1) << 32));
+        roff = m.op(o + 2);
+        for (uint32_t j = 0; j < 3; j++) run(o + j, 0u, 0u, S2C_RUN_EMPTY, 0ull);
+        o += 3;
+    }
+    bool drop = false;
+    if (maxdel_active) {   // :210
+        uint64_t dashes = 0, start = 0;
+        for (uint32_t j = o; j < oend; j++) {
+            const uint32_t w = m.op(j), op = w & 15u;
+            const uint64_t l = w >> 4;
+            if (op_bases(op)) {
+                uint64_t take = start < slen ? (l < slen - start ? l : slen - start) : 0;
+                if (fl & S2C_PF_X) {   // '-' chars of SEQ: x = 1, p1 = 0, p0 = 1
+                    uint64_t q = q0 + start;
+                    while (take) {
+                        const uint64_t qw = q >> 5;
+                        const uint32_t sh = (uint32_t)(q & 31), n = (uint32_t)(take < 32 - sh ? take : 32 - sh);
+                        const uint32_t mask = (n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u)) << sh;
+                        dashes += (uint32_t)__popc(m.x(qw) & m.p0(qw) & ~m.p1(qw) & mask);
+                        q += n;
+                        take -= n;
+                    }
+                }
+                start += l;
+            } else if (op_dash(op)) {
+                dashes += l;
+            } else if (op == S2C_OP_I || op == S2C_OP_S) {
+                start += l;
+            }
+        }
+        drop = dashes > (uint64_t)maxdel;
+    }
+    const uint32_t lng = (fl & S2C_PF_LONG) ? S2C_RUN_LONG : 0u;
+    const uint32_t bkind = S2C_RUN_BASES | ((fl & S2C_PF_X) ? S2C_RUN_XBIT : 0u) | (drop ? S2C_RUN_DROP : 0u) | lng;
+    int64_t k = 0;
+    uint64_t start = 0;
+    for (uint32_t j = o; j < oend; j++) {
+        const uint32_t w = m.op(j), op = w & 15u;
+        const uint64_t l = w >> 4;
+        uint32_t rg = 0, rl = 0, rk = S2C_RUN_EMPTY;
+        uint64_t rq = 0;
+        if (op_bases(op) || op_dash(op)) {
+            const bool bases = op_bases(op);
+            const uint64_t take = bases ? (start < slen ? (l < slen - start ? l : slen - start) : 0) : l;
+            const int64_t s = k > ka ? k : ka, e = (k + (int64_t)take) < kb ? k + (int64_t)take : kb;
+            if (e > s && (bases || !drop)) {
+                rg = P.x + (uint32_t)(s - ka);
+                rl = (uint32_t)(e - s);
+                rk = bases ? bkind : (S2C_RUN_DASH | lng);
+                rq = bases ? q0 + start + (uint64_t)(s - k) : 0ull;
+            }
+            k += (int64_t)take;
+            if (bases) start += l;
+        } else if (op == S2C_OP_I) {
+            const uint64_t take = start < slen ? (l < slen - start ? l : slen - start) : 0;
+            if (ins && take) {
+                const int64_t gkey = key0 + k;   // start_ref (:74) = POS-1 + seqout index here
+                if (gkey >= (int64_t)roff) ev((uint64_t)gkey, q0 + start, (uint32_t)take);
+            }
+            start += l;
+        } else if (op == S2C_OP_S) {
+            start += l;
+        }
+        run(j, rg, rl, rk, rq);
+    }
+}
+
 }  // namespace s2c
 
 extern "C" __device__ __attribute__((const)) unsigned long long __ockl_wfred_add_u64(unsigned long long);
@@ -243,5 +346,6 @@ __device__ __forceinline__ RecGeom rec_geom(uint32_t gpos, uint32_t len, uint32_
 __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
     return __builtin_amdgcn_alignbit(hi, lo, sh);
 }
+
 
 }  // namespace s2c

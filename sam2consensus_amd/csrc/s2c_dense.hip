@@ -1,11 +1,13 @@
 // s2c_dense.hip — k_tile_dense: shallow tiles without insertion keys (-f of one char).
 //
 // Such a tile's body is one char per position (:355-389 with no insertion columns and a
-// one-char fill), so the byte offset of position q is q: no length scan.  Its window of
-// run records (≤ S2C_DENSE_RUNS) is staged in LDS with one coalesced sweep, each lane
-// counts the records covering its word (bit-sliced counters as in k_tile), and — every
-// position's total being ≤ 255 (host plan) — the word's G lanes all-reduce their byte
-// counters with DPP, so each lane holds the counts of the whole word in registers.  Lane g
+// one-char fill), so the byte offset of position q is q: no length scan.  The tile walks
+// its window's pieces itself (the short pieces starting up to kwin words before it): the
+// base planes of the window — one contiguous range — are staged in LDS with one coalesced
+// sweep, one thread per piece runs parsecigar + maxdel (walk_piece, :46-82, :210) into run
+// records in LDS, each lane counts the records covering its word (bit-sliced counters as in
+// k_tile), and — every position's total being ≤ 255 (host plan) — the word's G lanes
+// all-reduce their byte counters with DPP, so each lane holds the counts of the whole word.  Lane g
 // of a word then votes its 32/G consecutive positions for every threshold (closed form of
 // :241-251 / :359-366 with the strict-majority shortcut) and stores their chars with one
 // wide store.  Counts never touch LDS or HBM.
@@ -24,16 +26,38 @@ __constant__ uint8_t c_amb[64] = {
 };
 
 struct DenseArgs {
-    const uint32_t *rs, *runs, *bq, *bx, *tiles, *items;
+    const uint32_t *rs, *pc, *ops, *bq, *bx, *tiles, *items;
     const double *thresholds;
     uint64_t *tile_stats, *blk_len;
     uint8_t *out;
-    uint32_t padded_len, n_cols, n_tiles, kwin, n_qwords, fill_nondash;
+    uint32_t padded_len, n_cols, n_tiles, kwin, fill_nondash, maxdel_active, maxdel;
     int32_t n_thr, min_depth;
     const uint8_t *fill;   // the one -f char
 };
 
-constexpr uint32_t OOR = 0xF0000000u;
+// walk_piece's view of the window staged in LDS
+struct LdsMem {
+    const uint32_t *ops;    // op words from o0
+    const uint2 *bql;       // base planes {p0, p1} from qw0
+    const uint32_t *bxl;    // non-ACGT plane from qw0
+    uint32_t o0, qw0;
+    __device__ __forceinline__ uint32_t op(uint32_t j) const { return ops[j - o0]; }
+    __device__ __forceinline__ uint32_t p0(uint64_t w) const { return bql[(uint32_t)w - qw0].x; }
+    __device__ __forceinline__ uint32_t p1(uint64_t w) const { return bql[(uint32_t)w - qw0].y; }
+    __device__ __forceinline__ uint32_t x(uint64_t w) const { return bxl[(uint32_t)w - qw0]; }
+};
+
+// n dwords src[0..n) → LDS dst[0..n) by LDS-DMA (no VGPR round trip; the wave's 64 lanes copy
+// 64 consecutive dwords per instruction; lanes past n re-copy src[n-1] into the 64-dword slack
+// after dst).  Completion: s_waitcnt vmcnt(0) + a barrier.
+__device__ __forceinline__ void dma_dwords(uint32_t *dst, const uint32_t *src, uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (uint32_t base = 64 * wv; base < n; base += WG) {
+        const uint32_t i = min(base + lane, n - 1);
+        __builtin_amdgcn_global_load_lds(src + i, dst + base, 4, 0, 0);
+    }
+}
+
 constexpr int GSD = 4;   // records per counting group
 
 // all-reduce of one register over the G adjacent lanes of a word
@@ -50,33 +74,66 @@ __device__ __forceinline__ uint32_t word_allreduce(uint32_t v) {
 template <int NWP>
 __global__ __launch_bounds__(WG) void k_tile_dense(const DenseArgs d) {
     constexpr int G = WG / NWP, PPL = 32 / G;
-    __shared__ uint4 runs_l[S2C_DENSE_RUNS];
-    __shared__ uint32_t nb[8 * NWP];          // 'N' counts of SEQ, one byte per position
-    __shared__ uint32_t acc[2 * THR_MAX + 1];  // sumcov; per threshold {non-'-', vote errors}
+    __shared__ uint4 arena[S2C_DENSE_LDS / 16 + 4];   // the tile's window (layout below)
+    __shared__ uint32_t nb[8 * NWP];                   // 'N' counts of SEQ, one byte per position
+    __shared__ uint32_t acc[2 * THR_MAX + 1];          // sumcov; per threshold {non-'-', vote errors}
     __shared__ uint8_t amb[64];
     const uint32_t tid = threadIdx.x;
     const uint32_t w = tid / G, g = tid % G;
     const uint32_t tile = uni(d.items[4 * (size_t)blockIdx.x]);
-    const uint4 tw = ((const uint4 *)d.tiles)[(size_t)tile * (S2C_TILE_WORDS / 4)];
-    const uint32_t cb0 = uni(d.tiles[(size_t)tile * S2C_TILE_WORDS + 8]);
+    const uint32_t *twp = d.tiles + (size_t)tile * S2C_TILE_WORDS;
+    const uint4 tw = *(const uint4 *)twp;
+    const uint4 tw3 = *(const uint4 *)(twp + 12), tw4 = *(const uint4 *)(twp + 16);
+    const uint32_t cb0 = uni(twp[8]);
     const uint32_t a = uni(tw.x), n = uni(tw.y) - a;
+    const uint32_t pf0 = uni(tw3.y), pf1 = uni(tw3.z), o0 = uni(tw3.w), o1 = uni(tw4.x), qw0 = uni(tw4.y), qw1 = uni(tw4.z);
     const uint32_t W0 = a >> 5, nwords = (n + 31) / 32, W = W0 + w;
     const bool active = w < nwords;
     const uint32_t K = d.kwin;
-    const uint32_t cbase = uni(d.rs[W0 >= K ? W0 - K : 0u]), cend = uni(d.rs[W0 + nwords]);
-    const uint32_t nrun = min(cend - cbase, (uint32_t)S2C_DENSE_RUNS);
+    const uint32_t nqw = qw1 - qw0, nslot = o1 - o0, npc = pf1 - pf0;
+    // ---- one round of LDS-DMA: piece records, base planes, non-ACGT plane, op words (each
+    //      region 16-B aligned with 64 dwords of slack); the run records are written later
+    auto up4 = [](uint32_t x) { return (x + 3u) & ~3u; };
+    uint32_t *L0 = (uint32_t *)arena;
+    uint32_t *pcl = L0;
+    uint32_t *bq_l = pcl + up4(4 * npc + 64);
+    uint32_t *bx_l = bq_l + up4(2 * nqw + 64);
+    uint32_t *op_l = bx_l + up4(nqw + 64);
+    uint2 *runl = (uint2 *)(op_l + up4(nslot + 64));
+    if (npc) dma_dwords(pcl, d.pc + 4 * (size_t)pf0, 4 * npc);
+    if (nqw) {
+        dma_dwords(bq_l, d.bq + 2 * (size_t)qw0, 2 * nqw);
+        dma_dwords(bx_l, d.bx + (size_t)qw0, nqw);
+    }
+    if (nslot) dma_dwords(op_l, d.ops + (size_t)o0, nslot);
     uint32_t cw0 = 0, cw1 = 0;
     if (active) {
-        cw0 = d.rs[W >= K ? W - K : 0u] - cbase;
-        cw1 = min(d.rs[W + 1] - cbase, nrun);
+        cw0 = d.rs[W >= K ? W - K : 0u] - o0;
+        cw1 = d.rs[W + 1] - o0;
     }
-    for (uint32_t i = tid; i < nrun; i += WG) runs_l[i] = ((const uint4 *)d.runs)[(size_t)cbase + i];
     for (uint32_t i = tid; i < 8 * NWP; i += WG) nb[i] = 0;
     for (uint32_t i = tid; i < 2 * (uint32_t)d.n_thr + 1; i += WG) acc[i] = 0;
     if (tid < 64) amb[tid] = c_amb[tid];
-    const __amdgpu_buffer_rsrc_t rbq = __builtin_amdgcn_make_buffer_rsrc((void *)d.bq, (short)0, (int)(8u * d.n_qwords), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rbx = __builtin_amdgcn_make_buffer_rsrc((void *)d.bx, (short)0, (int)(4u * d.n_qwords), 0x00020000);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_sync();
+    // ---- parsecigar + maxdel of the window's pieces (one thread per piece) → run records:
+    //      {gpos, (query bit − 32·qw0) << 15 | len << 4 | kind}
+    const uint2 *bql = (const uint2 *)bq_l;
+    const LdsMem mem{op_l, bql, bx_l, o0, qw0};
+    for (uint32_t k = tid; k < npc; k += WG) {
+        const uint4 P = ((const uint4 *)pcl)[k];
+        const uint32_t oend = k + 1 < npc ? pcl[4 * (k + 1) + 2] : o1;
+        walk_piece(mem, P, oend, d.maxdel_active != 0, d.maxdel,
+                   [&](uint32_t j, uint32_t gp, uint32_t l, uint32_t kind, uint64_t q) {
+                       uint2 r = make_uint2(0u, 0u);
+                       if (kind != S2C_RUN_EMPTY && !(kind & S2C_RUN_LONG))   // a long piece here does not overlap the tile
+                           r = make_uint2(gp, ((uint32_t)(q - 32ull * qw0) << 15) | (l << 4) | (kind & 15u));
+                       runl[j - o0] = r;
+                   },
+                   [&](uint64_t, uint64_t, uint32_t) {});   // dense tiles hold no insertion keys
+    }
+    lds_sync();
+    const uint32_t *bxl = bx_l;
 
     // ---- count the records of this lane's word: candidates cw0 + g + G·m < cw1
     uint32_t C[5][8];   // X, Y, Z, V, '-'
@@ -87,41 +144,26 @@ __global__ __launch_bounds__(WG) void k_tile_dense(const DenseArgs d) {
     const uint32_t nrec = cw0 + g < cw1 ? (cw1 - cw0 - g + G - 1) / G : 0u;
     const uint32_t ngrp = uni(__ockl_wfred_max_u32((nrec + GSD - 1) / GSD));
     for (uint32_t gi = 0; gi < ngrp; gi++) {
-        uint4 R[GSD], Wn[GSD];
-        uint32_t X0[GSD], X1[GSD], sh[GSD];
-        RecGeom gm[GSD];
-#pragma unroll
-        for (int u = 0; u < GSD; u++) {
-            const uint32_t m = gi * GSD + u;
-            R[u] = m < nrec ? runs_l[cw0 + g + G * m] : make_uint4(0, 0, 0, 0);
-            const Run r = run_of(R[u]);
-            gm[u] = rec_geom(r.gpos, r.len, W);
-            const uint64_t qs = r.q + gm[u].qs;
-            sh[u] = (uint32_t)(qs & 31);
-            const bool bases = (r.kind & 3u) == S2C_RUN_BASES && gm[u].valid;
-            const uint32_t wo = bases ? (uint32_t)(qs >> 5) * 8u : OOR;
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rbq, wo, 0, 0);
-            Wn[u] = make_uint4(v[0], v[1], v[2], v[3]);
-            const uint32_t xo = (bases && (r.kind & S2C_RUN_XBIT)) ? (uint32_t)(qs >> 5) * 4u : OOR;
-            const auto xv = __builtin_amdgcn_raw_buffer_load_b64(rbx, xo, 0, 0);
-            X0[u] = xv[0];
-            X1[u] = xv[1];
-        }
         uint32_t mx[8], my[8], mz[8], mv[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) mx[u] = my[u] = mz[u] = mv[u] = 0;
 #pragma unroll
         for (int u = 0; u < GSD; u++) {
-            const uint32_t kind = R[u].y >> 24, kd = kind & 3u;
+            const uint32_t m = gi * GSD + u;
+            const uint2 rv = m < nrec ? runl[cw0 + g + G * m] : make_uint2(0u, 0u);
+            const uint32_t kind = rv.y & 15u, kd = kind & 3u, len = (rv.y >> 4) & 0x7FFu;
+            const RecGeom gm = rec_geom(rv.x, len, W);
             if (kd == S2C_RUN_DASH) {
-                ripple1(C[4], gm[u].valid);
-            } else if (kd == S2C_RUN_BASES && gm[u].valid) {
-                const uint32_t lo = gm[u].lo, vd = gm[u].valid;
-                const uint32_t b0 = (funnel(Wn[u].z, Wn[u].x, sh[u]) << lo) & vd;
-                const uint32_t b1 = (funnel(Wn[u].w, Wn[u].y, sh[u]) << lo) & vd;
+                ripple1(C[4], gm.valid);
+            } else if (kd == S2C_RUN_BASES && gm.valid) {
+                const uint32_t qs = (rv.y >> 15) + (uint32_t)gm.qs, k = qs >> 5, sh = qs & 31u;
+                const uint2 lo = bql[k], hi = bql[k + 1];
+                const uint32_t vd = gm.valid;
+                const uint32_t b0 = (funnel(hi.x, lo.x, sh) << gm.lo) & vd;
+                const uint32_t b1 = (funnel(hi.y, lo.y, sh) << gm.lo) & vd;
                 uint32_t v = vd, x = b0, y = b1;
                 if (kind & S2C_RUN_XBIT) {
-                    const uint32_t xm = (funnel(X1[u], X0[u], sh[u]) << lo) & vd;
+                    const uint32_t xm = (funnel(bxl[k + 1], bxl[k], sh) << gm.lo) & vd;
                     const uint32_t en = xm & ~b0 & ~b1, sd = xm & b0 & ~b1;   // 'N', '-' of SEQ
                     v &= ~xm;
                     x &= ~xm;
@@ -263,10 +305,12 @@ int s2c_launch_dense(const s2c_dev *dv, hipStream_t st) {
     if (dv->n_dense <= 0) return S2C_OK;
     if (dv->fill_len != 1) return s2c_set_error(S2C_ERR_ARG, "dense tiles need a one-char fill");
     DenseArgs a;
-    a.rs = dv->rs; a.runs = dv->runs; a.bq = dv->bq; a.bx = dv->bx; a.tiles = dv->tiles; a.items = dv->dense;
+    a.rs = dv->rs; a.pc = dv->pc; a.ops = dv->ops; a.bq = dv->bq; a.bx = dv->bx; a.tiles = dv->tiles; a.items = dv->dense;
     a.thresholds = dv->thresholds; a.tile_stats = dv->tile_stats; a.blk_len = dv->blk_len; a.out = dv->out;
     a.padded_len = (uint32_t)dv->padded_len; a.n_cols = (uint32_t)dv->n_cols; a.n_tiles = (uint32_t)dv->n_tiles;
-    a.kwin = (uint32_t)dv->kwin; a.n_qwords = (uint32_t)dv->n_qwords; a.fill_nondash = (uint32_t)dv->fill_nondash;
+    a.kwin = (uint32_t)dv->kwin; a.fill_nondash = (uint32_t)dv->fill_nondash;
+    a.maxdel_active = dv->maxdel_active ? 1u : 0u;
+    a.maxdel = dv->maxdel < 0 ? 0u : (uint32_t)dv->maxdel;
     a.n_thr = dv->n_thr; a.min_depth = dv->min_depth;
     a.fill = dv->fill;
     const int64_t n = dv->n_dense;

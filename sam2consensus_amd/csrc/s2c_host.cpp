@@ -202,7 +202,7 @@ struct s2c_batch {
     s2c_batch_info info{};
     std::vector<std::string> names;
     std::vector<int64_t> ref_len, ref_off, ref_reads;
-    std::vector<uint32_t> pc, ops, bq, bx, rs, tiles, items, dense, deep, lp, wtile;
+    std::vector<uint32_t> pc, ops, bq, bx, rs, tiles, items, dense, deep, lp, wtile, rlist;
     std::vector<uint32_t> kmin, kmax;   // host only: global key range of each piece's insertion events
 };
 
@@ -665,6 +665,71 @@ struct Piece {
 };
 }  // namespace
 
+// The window of tile [a, b): the short pieces starting in words [a/32 - K, ceil(b/32)) — a
+// contiguous range of the bucketed pieces — their op slots and base plane words (+1 word for
+// the funnel shift of the last one).  Tile words 13-18.
+static void tile_window(const s2c_batch *b, int64_t K, uint64_t a, uint64_t e, uint32_t *tw) {
+    const int64_t NP = b->info.n_pieces;
+    auto piece_at_word = [&](int64_t w) {   // first piece with start word >= w
+        int64_t lo = 0, hi = NP;
+        while (lo < hi) {
+            const int64_t m = (lo + hi) / 2;
+            if ((int64_t)(b->pc[4 * m] >> 5) < w) lo = m + 1; else hi = m;
+        }
+        return lo;
+    };
+    const int64_t pf0 = piece_at_word(std::max<int64_t>((int64_t)(a >> 5) - K, 0)), pf1 = piece_at_word((int64_t)((e + 31) >> 5));
+    tw[13] = (uint32_t)pf0;
+    tw[14] = (uint32_t)pf1;
+    tw[15] = b->pc[4 * pf0 + 2];
+    tw[16] = b->pc[4 * pf1 + 2];
+    tw[17] = pf1 > pf0 ? (uint32_t)(((uint64_t)b->pc[4 * pf0 + 1] * 16) >> 5) : 0u;
+    tw[18] = pf1 > pf0 ? (uint32_t)(((uint64_t)b->pc[4 * (pf1 - 1) + 1] * 16 + (b->pc[4 * (pf1 - 1) + 3] & 0xFFFFFFu) + 31) / 32 + 1)
+                       : tw[17];
+}
+
+// LDS bytes k_tile_dense stages a tile's window in (s2c_dense.hip)
+static int64_t dense_bytes(const uint32_t *tw) {
+    return 12 * (int64_t)(tw[18] - tw[17]) + 12 * (int64_t)(tw[16] - tw[15]) + 16 * (int64_t)(tw[14] - tw[13] + 1) + 1024;
+}
+
+// PF_RUNS on the pieces a non-dense tile reads runs of (its window, its long pieces), and
+// the list of pieces k_reads walks (those, and the pieces emitting insertion events).
+static void mark_runs(s2c_batch *b) {
+    const int64_t NP = b->info.n_pieces, NT = b->info.n_tiles;
+    std::vector<int32_t> diff(NP + 1, 0);
+    for (int64_t t = 0; t < NT; t++) {
+        const uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
+        if (tw[3] & S2C_TILE_DENSE) continue;
+        diff[tw[13]]++;
+        diff[tw[14]]--;
+    }
+    std::vector<uint8_t> need(NP, 0);
+    int32_t run = 0;
+    for (int64_t k = 0; k < NP; k++) {
+        run += diff[k];
+        need[k] = run > 0;
+    }
+    for (uint32_t slot : b->lp) {   // long pieces (listed by slot)
+        if (b->info.n_long == 0) break;
+        int64_t lo = 0, hi = NP - 1;
+        while (lo < hi) {
+            const int64_t m = (lo + hi + 1) / 2;
+            if (b->pc[4 * m + 2] <= slot) lo = m; else hi = m - 1;
+        }
+        need[lo] = 1;
+    }
+    b->rlist.clear();
+    for (int64_t k = 0; k < NP; k++) {
+        uint32_t &w3 = b->pc[4 * k + 3];
+        if (need[k]) w3 |= (uint32_t)S2C_PF_RUNS << 24;
+        else w3 &= ~((uint32_t)S2C_PF_RUNS << 24);
+        if (need[k] || ((w3 >> 24) & S2C_PF_INS)) b->rlist.push_back((uint32_t)k);
+    }
+    b->info.n_rlist = (int64_t)b->rlist.size();
+    if (b->rlist.empty()) b->rlist.push_back(0);
+}
+
 extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
     if (!p || !out) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
     int rc = feed_flush(p);
@@ -877,10 +942,13 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
     int64_t tile_force = 0;   // diagnostic override (S2C_TILE_POS, a multiple of 64 in [64, 2048])
     if (const char *e = getenv("S2C_TILE_POS"))
         tile_force = align_up(std::min<int64_t>(std::max<int64_t>(atoll(e), 64), TP_MAX), S2C_POS_ALIGN);
-    std::vector<int64_t> ref_slots(R, 0);
+    std::vector<int64_t> ref_slots(R, 0), ref_np(R, 0), ref_qw(R, 0);
     for (int64_t k = 0; k < NP; k++) {
         const Piece &q = pcs[order[k]];
-        ref_slots[CH[q.chunk]->reads[q.read].ref] += q.nslots;
+        const ReadRec &rr = CH[q.chunk]->reads[q.read];
+        ref_slots[rr.ref] += q.nslots;
+        ref_np[rr.ref]++;
+        ref_qw[rr.ref] += (int64_t)align_up(rr.slen, 16);
     }
     for (int64_t r = 0; r < R; r++) {
         const int64_t L = p->ref_len[r], off = b->ref_off[r];
@@ -888,9 +956,13 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
         const double depth = (double)ref_span[r] / (double)L, spp = (double)ref_slots[r] / (double)L;
         int64_t tp = depth > 0 ? align_up((int64_t)std::ceil(E_TARGET / depth), S2C_POS_ALIGN) : TP_MAX;
         const double win = 32.0 * (double)(K + 1) * spp;    // run slots per word's window
-        if (win <= 200.0 && spp > 0) {                     // shallow: the dense kernel's LDS
-            const int64_t lim = (int64_t)((0.75 * S2C_DENSE_RUNS / spp - 32.0 * (double)(K + 1)) / 64.0) * 64;
-            tp = std::min(tp, std::max<int64_t>(lim, TP_MIN));
+        if (win <= 200.0 && spp > 0) {
+            // shallow: the widest tile whose window (8 B per run slot + 12 B per base plane word,
+            // with a margin for the depth's spread) fits the dense kernel's LDS
+            const double bpp = (12.0 * (double)ref_slots[r] + 16.0 * (double)ref_np[r] +
+                                12.0 * ((double)ref_qw[r] / 32.0 + (double)ref_np[r])) / (double)L;
+            tp = TP_MAX;
+            while (tp > TP_MIN && ((double)tp + 32.0 * (double)(K + 1)) * bpp + 1100.0 > 0.9 * S2C_DENSE_LDS) tp /= 2;
         }
         tp = std::min(std::max(tp, TP_MIN), TP_MAX);
         if (tile_force > 0) tp = tile_force;
@@ -965,11 +1037,13 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
         const int64_t nch = std::max<int64_t>(1, ceil_div(maxc, CHK));
         const int64_t wruns = (int64_t)b->rs[w1] - (int64_t)b->rs[std::max<int64_t>(w0 - K, 0)];
         runs_max = std::max(runs_max, wruns);
+        uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
+        tile_window(b, K, T.a, T.b, tw);
+        const int64_t wbytes = dense_bytes(tw);
         uint32_t fl = nch > 1 ? S2C_TILE_DEEP : 0u;
         if (nev[t] > S2C_EPI_KEYS || (int64_t)ccap[t] > lcols) fl |= S2C_TILE_GENERAL;
-        if (fl == 0 && nev[t] == 0 && nlg == 0 && maxc <= 255 && wruns <= S2C_DENSE_RUNS) fl = S2C_TILE_DENSE;
+        if (fl == 0 && nev[t] == 0 && nlg == 0 && maxc <= 255 && wbytes <= S2C_DENSE_LDS) fl = S2C_TILE_DENSE;
         const uint32_t bcap = nshort[t] ? pow2_at_least(2 * (uint64_t)nshort[t]) : 0u;
-        uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
         tw[0] = (uint32_t)T.a; tw[1] = (uint32_t)T.b; tw[2] = (uint32_t)T.ref; tw[3] = fl;
         tw[4] = (uint32_t)boff; tw[5] = bcap; tw[6] = (uint32_t)loff; tw[7] = nlong[t];
         tw[8] = (uint32_t)coff; tw[9] = (uint32_t)ccap[t]; tw[10] = lcnt[t]; tw[11] = lcnt[t + 1];
@@ -997,6 +1071,7 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
     I.n_lng = (int64_t)loff;
     I.n_cols = (int64_t)coff;
     I.runs_max = runs_max;
+    mark_runs(b);
     *out = guard.release();
     return S2C_OK;
 }
@@ -1151,6 +1226,13 @@ extern "C" int s2c_batch_shard(const s2c_batch *b, int64_t t0, int64_t t1, s2c_b
         aligned += tw[1] - tw[0];
     }
     J.runs_max = runs_max;
+    for (int64_t t = 0; t < NT; t++) {
+        uint32_t *tw = &s->tiles[(size_t)t * S2C_TILE_WORDS];
+        tile_window(s.get(), K, tw[0], tw[1], tw);
+        if ((tw[3] & S2C_TILE_DENSE) && dense_bytes(tw) > S2C_DENSE_LDS)
+            return s2c_set_error(S2C_ERR_LIMIT, "shard window beyond the dense kernel's LDS");
+    }
+    mark_runs(s.get());
     // the shard's share of the workload's aligned bases (by its positions; for reporting)
     J.aligned_bases = I.total_len ? (int64_t)((double)I.aligned_bases * (double)aligned / (double)I.total_len) : 0;
     *out = s.release();
@@ -1179,6 +1261,7 @@ extern "C" int s2c_batch_arrays_get(const s2c_batch *b, s2c_batch_arrays *o) {
     o->deep = b->deep.data();
     o->lp = b->lp.data();
     o->wtile = b->wtile.data();
+    o->rlist = b->rlist.data();
     return S2C_OK;
 }
 

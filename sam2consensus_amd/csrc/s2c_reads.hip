@@ -21,27 +21,18 @@ namespace s2c {
 namespace {
 
 struct ReadsArgs {
-    const uint32_t *pc, *ops, *bq, *bx, *tiles, *wtile;
+    const uint32_t *pc, *ops, *bq, *bx, *tiles, *wtile, *rlist;
     uint32_t *runs, *ibkt, *ilong, *ilong_n;
-    uint32_t n_pieces, maxdel_active, maxdel;
+    uint32_t n, maxdel_active, maxdel, all;   // all: every piece (else the pieces of rlist)
 };
 
-__device__ __forceinline__ bool op_bases(uint32_t op) { return op == S2C_OP_M || op == S2C_OP_EQ || op == S2C_OP_X; }
-__device__ __forceinline__ bool op_dash(uint32_t op) { return op == S2C_OP_D || op == S2C_OP_N || op == S2C_OP_P; }
-
-// '-' chars of SEQ in query bases [q, q + n): x = 1, p1 = 0, p0 = 1
-__device__ uint32_t seq_dashes(const ReadsArgs &d, uint64_t q, uint64_t n) {
-    uint32_t c = 0;
-    while (n) {
-        const uint64_t w = q >> 5;
-        const uint32_t sh = (uint32_t)(q & 31), m = (uint32_t)(n < 32 - sh ? n : 32 - sh);
-        const uint32_t mask = (m >= 32 ? 0xFFFFFFFFu : ((1u << m) - 1u)) << sh;
-        c += (uint32_t)__popc(d.bx[w] & d.bq[2 * w] & ~d.bq[2 * w + 1] & mask);
-        q += m;
-        n -= m;
-    }
-    return c;
-}
+struct GlobalMem {   // walk_piece's view of the batch in HBM
+    const uint32_t *ops, *bq, *bx;
+    __device__ __forceinline__ uint32_t op(uint32_t j) const { return ops[j]; }
+    __device__ __forceinline__ uint32_t p0(uint64_t w) const { return bq[2 * w]; }
+    __device__ __forceinline__ uint32_t p1(uint64_t w) const { return bq[2 * w + 1]; }
+    __device__ __forceinline__ uint32_t x(uint64_t w) const { return bx[w]; }
+};
 
 // symbol code ("-ACGNT" index) of query base q
 __device__ __forceinline__ uint32_t base_code(const ReadsArgs &d, uint64_t q) {
@@ -91,106 +82,37 @@ __device__ void add_event(const ReadsArgs &d, uint64_t gkey, uint64_t q, uint32_
 }
 
 __global__ __launch_bounds__(WG) void k_reads(const ReadsArgs d) {
-    const uint32_t i = blockIdx.x * WG + threadIdx.x;
-    if (i >= d.n_pieces) return;
+    const uint32_t n = blockIdx.x * WG + threadIdx.x;
+    if (n >= d.n) return;
+    const uint32_t i = d.all ? n : d.rlist[n];
     const uint4 P = ((const uint4 *)d.pc)[i];
     const uint32_t oend = d.pc[4 * (size_t)i + 6];   // next piece's opoff (sentinel at the end)
-    const uint32_t slen = P.w & 0xFFFFFFu, fl = P.w >> 24;
-    const uint64_t q0 = (uint64_t)P.y * 16;
-    uint4 *runs = (uint4 *)d.runs;
-    const uint4 EMPTY = make_uint4(0u, 0u, 0u, 0u);
-    uint32_t o = P.z;
-    int64_t ka = 0, kb = INT64_MAX;
-    if (fl & S2C_PF_RANGE) {
-        ka = d.ops[o];
-        kb = d.ops[o + 1];
-        runs[o] = EMPTY;
-        runs[o + 1] = EMPTY;
-        o += 2;
-    }
-    int64_t key0 = 0;
-    uint32_t roff = 0;
-    const bool ins = (fl & S2C_PF_INS) != 0;
-    if (ins) {
-        key0 = (int64_t)((uint64_t)d.ops[o] | ((uint64_t)d.ops[o + 1] << 32));
-        roff = d.ops[o + 2];
-        runs[o] = EMPTY;
-        runs[o + 1] = EMPTY;
-        runs[o + 2] = EMPTY;
-        o += 3;
-    }
-    // ---- the maxdel rule (:210): '-' in seqout = D/N/P lengths + '-' chars of the bases taken
-    bool drop = false;
-    if (d.maxdel_active) {
-        uint64_t dashes = 0, start = 0;
-        for (uint32_t j = o; j < oend; j++) {
-            const uint32_t w = d.ops[j], op = w & 15u;
-            const uint64_t l = w >> 4;
-            if (op_bases(op)) {
-                const uint64_t take = start < slen ? (l < slen - start ? l : slen - start) : 0;
-                if ((fl & S2C_PF_X) && take) dashes += seq_dashes(d, q0 + start, take);
-                start += l;
-            } else if (op_dash(op)) {
-                dashes += l;
-            } else if (op == S2C_OP_I || op == S2C_OP_S) {
-                start += l;
-            }
-        }
-        drop = dashes > (uint64_t)d.maxdel;
-    }
-    // ---- runs of the piece's seqout range [ka, kb), insertion events
-    const uint32_t lng = (fl & S2C_PF_LONG) ? S2C_RUN_LONG : 0u;
-    const uint32_t bkind = S2C_RUN_BASES | ((fl & S2C_PF_X) ? S2C_RUN_XBIT : 0u) | (drop ? S2C_RUN_DROP : 0u) | lng;
-    int64_t k = 0;
-    uint64_t start = 0;
-    for (uint32_t j = o; j < oend; j++) {
-        const uint32_t w = d.ops[j], op = w & 15u;
-        const uint64_t l = w >> 4;
-        uint4 r = EMPTY;
-        if (op_bases(op) || op_dash(op)) {
-            const bool bases = op_bases(op);
-            const uint64_t take = bases ? (start < slen ? (l < slen - start ? l : slen - start) : 0) : l;
-            const int64_t s = k > ka ? k : ka, e = (k + (int64_t)take) < kb ? k + (int64_t)take : kb;
-            if (e > s && (bases || !drop)) {
-                const uint32_t gpos = P.x + (uint32_t)(s - ka);
-                if (bases) {
-                    const uint64_t q = q0 + start + (uint64_t)(s - k);
-                    r = make_uint4(gpos, (uint32_t)(e - s) | (bkind << 24), (uint32_t)q, (uint32_t)(q >> 32));
-                } else {
-                    r = make_uint4(gpos, (uint32_t)(e - s) | ((S2C_RUN_DASH | lng) << 24), 0u, 0u);
-                }
-            }
-            k += (int64_t)take;
-            if (bases) start += l;
-        } else if (op == S2C_OP_I) {
-            const uint64_t take = start < slen ? (l < slen - start ? l : slen - start) : 0;
-            if (ins && take) {
-                const int64_t gkey = key0 + k;   // start_ref (:74) = POS-1 + seqout index here
-                if (gkey >= (int64_t)roff) add_event(d, (uint64_t)gkey, q0 + start, (uint32_t)take);
-            }
-            start += l;
-        } else if (op == S2C_OP_S) {
-            start += l;
-        }
-        runs[j] = r;
-    }
+    const bool runs = d.all || ((P.w >> 24) & S2C_PF_RUNS);
+    uint4 *out = (uint4 *)d.runs;
+    walk_piece(GlobalMem{d.ops, d.bq, d.bx}, P, oend, d.maxdel_active != 0, d.maxdel,
+               [&](uint32_t j, uint32_t g, uint32_t l, uint32_t k, uint64_t q) {
+                   if (runs) out[j] = make_uint4(g, l | (k << 24), (uint32_t)q, (uint32_t)(q >> 32));
+               },
+               [&](uint64_t gkey, uint64_t q, uint32_t len) { add_event(d, gkey, q, len); });
 }
 
 }  // namespace
 }  // namespace s2c
 
-// Launcher (called by s2c_reads in s2c_tile.hip)
-int s2c_launch_reads(const s2c_dev *dv, hipStream_t st) {
+// Launcher (called by s2c_reads in s2c_tile.hip): the pieces of rlist, or all of them
+int s2c_launch_reads(const s2c_dev *dv, hipStream_t st, bool all) {
     using namespace s2c;
-    if (dv->n_pieces == 0) return S2C_OK;
+    const int64_t n = all ? dv->n_pieces : dv->n_rlist;
+    if (n == 0) return S2C_OK;
     ReadsArgs a;
     a.pc = dv->pc; a.ops = dv->ops; a.bq = dv->bq; a.bx = dv->bx; a.tiles = dv->tiles; a.wtile = dv->wtile;
+    a.rlist = dv->rlist;
     a.runs = dv->runs; a.ibkt = dv->ibkt; a.ilong = dv->ilong; a.ilong_n = dv->ilong_n;
-    a.n_pieces = (uint32_t)dv->n_pieces;
+    a.n = (uint32_t)n;
     a.maxdel_active = dv->maxdel_active ? 1u : 0u;
     a.maxdel = dv->maxdel < 0 ? 0u : (uint32_t)dv->maxdel;
-    const unsigned grid = (unsigned)((dv->n_pieces + WG - 1) / WG);
-    k_reads<<<grid, WG, 0, st>>>(a);
+    a.all = all ? 1u : 0u;
+    k_reads<<<(unsigned)((n + WG - 1) / WG), WG, 0, st>>>(a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? S2C_OK : s2c_set_error(S2C_ERR_HIP, std::string("k_reads: ") + hipGetErrorString(e));
 }

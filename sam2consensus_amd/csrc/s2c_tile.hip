@@ -25,7 +25,7 @@
 
 #include "s2c_common.h"
 
-int s2c_launch_reads(const s2c_dev *d, hipStream_t s);
+int s2c_launch_reads(const s2c_dev *d, hipStream_t s, bool all);
 int s2c_launch_dense(const s2c_dev *d, hipStream_t s);
 
 namespace s2c {
@@ -77,7 +77,7 @@ struct TileRec {
 };
 __device__ __forceinline__ TileRec tile_rec(const uint32_t *tiles, uint32_t t) {
     const uint4 *p = (const uint4 *)tiles + (size_t)t * (S2C_TILE_WORDS / 4);
-    const uint4 v0 = p[0], v1 = p[1], v2 = p[2], v3 = p[3];
+    const uint4 v0 = p[0], v1 = p[1], v2 = p[2], v3 = p[3];   // words 0-15 (13-19: the window)
     return {uni(v0.x), uni(v0.y), uni(v0.z), uni(v0.w), uni(v1.x), uni(v1.y), uni(v1.z), uni(v1.w),
             uni(v2.x), uni(v2.y), uni(v2.z), uni(v2.w), uni(v3.x)};
 }
@@ -631,7 +631,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const bool deep = (T.flags & S2C_TILE_DEEP) != 0;
     // ---- candidates of this lane: window slots [cw0, cw1) then long slots [lp0, lp1)
     const uint32_t K = d.kwin;
-    const uint32_t cbase = uni(d.rs[(a >> 5) >= K ? (a >> 5) - K : 0u]);   // the tile's first window slot
+    const uint32_t cbase = uni(d.tiles[(size_t)tile * S2C_TILE_WORDS + 15]);   // the tile's first window slot (o0)
     uint32_t cw0 = 0, cw1 = 0;
     if (active) {
         cw0 = d.rs[W >= K ? W - K : 0u];
@@ -1122,7 +1122,9 @@ static int check_dev(const s2c_dev *d) {
 extern "C" int s2c_reads(const s2c_dev *d, void *stream) {
     int rc = check_dev(d);
     if (rc) return rc;
-    return s2c_launch_reads(d, (hipStream_t)stream);
+    // dense tiles walk their own pieces, unless len(-f) != 1 routes them to k_tile (which
+    // reads run records): then every piece's runs are written
+    return s2c_launch_reads(d, (hipStream_t)stream, d->n_dense > 0 && d->fill_len != 1);
 }
 
 extern "C" int s2c_pileup(const s2c_dev *d, void *stream) {
@@ -1164,6 +1166,7 @@ extern "C" int s2c_pileup_counts(const s2c_dev *d, void *stream) {
     if (rc) return rc;
     if (!d->counts) return s2c_set_error(S2C_ERR_ARG, "counts buffer required");
     hipStream_t s = (hipStream_t)stream;
+    if ((rc = s2c_launch_reads(d, s, true))) return rc;   // run records of every piece
     TileArgs a = tile_args(*d);
     a.mode = 1;
     if (d->n_deep > 0) {

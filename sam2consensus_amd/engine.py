@@ -44,7 +44,7 @@ def _ptr(t):
 class DeviceBatch:
     """The packed batch resident in HBM (inputs of every launch)."""
 
-    ARRAYS = ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile")
+    ARRAYS = ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile", "rlist")
 
     def __init__(self, hb, device=None):
         self.device = _dev(device)
@@ -96,6 +96,7 @@ class Workspace:
         d.n_pieces, d.n_ops, d.n_qwords, d.n_tiles = i.n_pieces, i.n_ops, i.n_qwords, i.n_tiles
         d.n_items, d.n_dense, d.n_deep = i.n_items, i.n_dense, i.n_deep
         d.padded_len, d.chunk, d.kwin, d.tile_max = i.padded_len, i.chunk, i.kwin, i.tile_max
+        d.n_rlist = i.n_rlist
         # the maxdel rule (:210) runs on the device: the parser's setting unless overridden
         if maxdel_active is None:
             maxdel_active = getattr(db.hb, "maxdel_active", True)
@@ -156,7 +157,6 @@ class Workspace:
         keep_counts=True; returns counts[6][padded_len] as numpy u32."""
         if not self.keep_counts:
             raise ValueError("pileup_counts needs Workspace(keep_counts=True)")
-        self.reads()
         L.check(lib.s2c_pileup_counts(C.byref(self.dev), self.stream_handle()))
         return self.counts_host()
 

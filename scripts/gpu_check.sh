@@ -12,7 +12,7 @@ WLS=${WLS:-c5}
 TAG=${TAG:-r02}
 echo "host: $(nproc) cpus; $(grep -m1 'model name' /proc/cpuinfo)" | tee "$OUT/host.txt"
 if [[ $STEPS == *gpu* ]]; then
-  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS} > "$OUT/pytest_gpu.log" 2>&1
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > "$OUT/pytest_gpu.log" 2>&1
   rc=$?; grep -E "passed|failed|error" "$OUT/pytest_gpu.log" | tail -3; [ $rc -eq 0 ] || { tail -40 "$OUT/pytest_gpu.log"; echo "pytest gpu rc=$rc"; exit $rc; }
 fi
 for WL in $WLS; do

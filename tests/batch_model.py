@@ -192,6 +192,23 @@ def check_plan(hb):
         else:
             assert w1 - w0 <= K, "short piece beyond the window"
     assert sorted(hb.deep.tolist()) == [t for t in range(i.n_tiles) if T[t, 3] & 3]
+    # window fields: pieces [pf0, pf1) start in words [a/32 - kwin, ceil(b/32)); slots, planes
+    for t, row in enumerate(T):
+        w0, w1 = max((row[0] >> 5) - K, 0), (row[1] + 31) >> 5
+        pf0, pf1 = np.searchsorted(sw, [w0, w1])
+        assert (row[13], row[14]) == (pf0, pf1) and (row[15], row[16]) == (pc[pf0, 2], pc[pf1, 2])
+        if pf1 > pf0:
+            assert row[17] == (16 * pc[pf0, 1]) >> 5 and row[18] >= (16 * pc[pf1 - 1, 1] + (pc[pf1 - 1, 3] & 0xFFFFFF) + 31) // 32
+        if row[3] == 4:
+            assert 12 * (row[18] - row[17]) + 12 * (row[16] - row[15]) + 16 * (row[14] - row[13] + 1) + 1024 <= 24576
+    # k_reads' list: the pieces non-dense tiles read runs of, and the insertion emitters
+    need = np.zeros(NP, bool)
+    for row in T:
+        if row[3] != 4:
+            need[row[13]:row[14]] = True
+    fl = pc[:NP, 3] >> 24
+    assert (need <= ((fl & 16) != 0)).all()
+    assert set(hb.rlist.tolist()) == set(np.nonzero(((fl & 16) != 0) | ((fl & PF_INS) != 0))[0].tolist())
 
 
 def check_plan_shard(sub):
