@@ -87,6 +87,66 @@ def cpu_baseline(workload, scale):
                       % (workload, scale, sp.n_refs, sp.ref_len, a, dt, cpu_model())}
 
 
+def cpu_threads():
+    """Host threads this process may use (the GPU box's CPU share: OMP_NUM_THREADS)."""
+    n = os.environ.get("OMP_NUM_THREADS")
+    if n and n.isdigit() and int(n) > 0:
+        return int(n)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_baseline_mc(workload, scale):
+    """Time oracle/s2c_oracle_mc — the C restatement of sam2consensus.py, parse + pileup +
+    vote + FASTA on every host thread of this process — on the workload itself (scale 1)
+    or a bounded sample of it; its FASTA is checked against the golden sha256 at scale 1."""
+    import hashlib
+    import subprocess
+    import tempfile
+
+    from sam2consensus_amd import configs
+
+    binary = os.path.join(ROOT, "oracle", "build", "s2c_oracle_mc")
+    if not os.path.exists(binary):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    T = cpu_threads()
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, workload + ".sam")
+        configs.synth_write(workload, p, scale=scale)
+        hb = configs.synth_batch(workload, scale=scale)
+        a = hb.aligned_bases
+        hb.free()
+        out = os.path.join(td, "out")
+        t0 = time.perf_counter()
+        r = subprocess.run([binary, str(T), "-i", p, "-o", out] + configs.cli_args(workload),
+                           capture_output=True, text=True)
+        dt = time.perf_counter() - t0
+        ok = r.returncode == 0 and "status: ok" in r.stdout
+        check = None
+        if ok and scale == 1.0:
+            g = golden_for(workload)
+            if g and g.get("files"):
+                got = {f: hashlib.sha256(open(os.path.join(out, f), "rb").read()).hexdigest() for f in os.listdir(out)}
+                check = got == {f: v["sha256"] for f, v in g["files"].items()}
+    sp = configs.spec(workload, scale=scale)
+    return {"value": a / dt if ok else None, "unit": "aligned bases/s", "cores": T, "kind": "port",
+            "sample": "%s at scale %g: %d refs x %d bp (%d aligned bases, %.2f s incl. file read): "
+                      "oracle/s2c_oracle_mc.c, the C restatement of sam2consensus.py, parse+pileup+vote+format "
+                      "on %d threads; %s" % (workload, scale, sp.n_refs, sp.ref_len, a, dt, T, cpu_model()),
+            "output_matches_golden": check}
+
+
+def golden_for(workload):
+    p = os.path.join(ROOT, "tests", "golden", "configs.json")
+    try:
+        with open(p) as fh:
+            return json.load(fh).get(workload)
+    except OSError:
+        return None
+
+
 def cpu_model():
     try:
         for ln in open("/proc/cpuinfo"):
@@ -106,6 +166,8 @@ def main():
     ap.add_argument("--shard", action="store_true", help="N>1: split ONE workload over the ranks (strong scaling)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-scale", type=float, default=0.016)
+    ap.add_argument("--no-cpu-mc", action="store_true", help="skip the multi-threaded C baseline")
+    ap.add_argument("--cpu-mc-scale", type=float, default=1.0)
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--graph", action="store_true", help="time HIP graph replays of the step")
     args = ap.parse_args()
@@ -240,6 +302,8 @@ def main():
         line["parity"] = parity
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(wl, args.cpu_sample_scale)
+            if not args.no_cpu_mc:
+                line["cpu_baseline_mc"] = cpu_baseline_mc(wl, args.cpu_mc_scale)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define S2C_ABI_VERSION 5
+#define S2C_ABI_VERSION 6
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define S2C_OK            0
@@ -113,9 +113,12 @@ int s2c_layout(int64_t *out, int n);
 #define S2C_EPI_KEYS    256  /* insertion keys per tile k_tile's epilogue holds in LDS */
 /* insertion columns per tile k_tile's epilogue holds in LDS, by words per tile */
 #define S2C_LDS_COLS(nwp) ((nwp) <= 16 ? 640 : ((nwp) == 32 ? 448 : 192))
-#define S2C_DENSE_LDS 24576  /* bytes of LDS a dense tile stages its window in: 12 per base plane
-                                 word, 12 per op slot (op word + run record), 16 per piece record
-                                 (+1), and 1 KB of DMA slack */
+#define S2C_DENSE_LDS 32768  /* bytes of LDS a dense tile may keep its window in (one wave per tile) */
+/* LDS bytes of a dense tile's window of ns op slots and nq base plane words: op words (+64
+   dwords of LDS-DMA slack, 8-B aligned), planes {p0, p1} (+32 words of slack), the non-ACGT
+   plane (+64 words of slack, 8-B aligned), run records */
+#define S2C_DENSE_BYTES(ns, nq) (4 * (((ns) + 65) & ~1) + 8 * ((nq) + 32) + 4 * (((nq) + 65) & ~1) + 8 * (ns))
+#define S2C_DENSE_QW   4096  /* base plane words of a dense tile's window (17-bit query offsets) */
 #define S2C_SHORT_MOTIF  16  /* motifs up to this length are hashed inline (3-bit codes) */
 #define S2C_CODE_FILL     0  /* internal vote char of a fill position */
 #define S2C_CODE_ERR   0xFF  /* vote char where the vote hit a missing amb key (:367) */
@@ -171,6 +174,7 @@ typedef struct {
     int64_t n_lng;             /* long-motif event slots over all tiles (Σ lcap) */
     int64_t n_cols;            /* insertion column slots over all tiles (Σ ccap ≥ Σ columns) */
     int64_t runs_max;          /* most run slots any tile's window holds */
+    int64_t dense_lds;         /* most LDS bytes any dense tile's window takes (S2C_DENSE_BYTES) */
 } s2c_batch_info;
 
 typedef struct {               /* host pointers into the batch (valid until s2c_batch_free) */
@@ -244,7 +248,7 @@ typedef struct {
     /* ---- packed batch (device copies of s2c_batch_arrays) ---- */
     const uint32_t *pc, *ops, *bq, *bx, *rs;
     const uint32_t *tiles, *items, *dense, *deep, *lp, *wtile, *rlist;
-    int64_t n_pieces, n_ops, n_qwords, n_tiles, n_items, n_dense, n_deep, padded_len, chunk, n_rlist;
+    int64_t n_pieces, n_ops, n_qwords, n_tiles, n_items, n_dense, n_deep, padded_len, chunk, n_rlist, dense_lds;
     int32_t kwin, tile_max;
 
     /* ---- options (:102, :117-138) ---- */

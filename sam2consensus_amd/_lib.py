@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libs2c.so")
+LIB_PATH = os.path.join(_HERE, os.environ.get("S2C_LIB", "libs2c.so"))
 
 S2C_OK = 0
 S2C_ERR_KEY = -1
@@ -53,7 +53,7 @@ class BatchInfo(C.Structure):
         "n_refs", "total_len", "padded_len", "header_lines", "lines_total", "reads_mapped",
         "aligned_bases", "query_bases", "n_pieces", "n_ops", "n_tokens", "n_qwords", "n_words",
         "n_tiles", "n_items", "n_dense", "n_deep", "n_long", "n_rlist", "kwin", "tile_max", "chunk",
-        "n_ins", "n_ins_bases", "n_bkt", "n_lng", "n_cols", "runs_max")]
+        "n_ins", "n_ins_bases", "n_bkt", "n_lng", "n_cols", "runs_max", "dense_lds")]
 
 
 _P64 = C.POINTER(C.c_int64)
@@ -81,7 +81,7 @@ class Dev(C.Structure):
     _fields_ = [(n, _VP) for n in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile",
                                    "rlist")] + \
         [(n, C.c_int64) for n in ("n_pieces", "n_ops", "n_qwords", "n_tiles", "n_items", "n_dense", "n_deep",
-                                  "padded_len", "chunk", "n_rlist")] + [
+                                  "padded_len", "chunk", "n_rlist", "dense_lds")] + [
         ("kwin", C.c_int32), ("tile_max", C.c_int32),
         ("maxdel_active", C.c_int32), ("maxdel", C.c_int32),
         ("thresholds", _VP), ("n_thr", C.c_int32), ("min_depth", C.c_int32),

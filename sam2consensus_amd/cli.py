@@ -82,6 +82,28 @@ def consensus_batch(hb, thresholds, prefix, min_depth=1, fill=b"-", nchar=0, dev
     return files
 
 
+PROGRESS_EVERY = 500000   # :224
+
+
+def progress_lines(header_lines, lines_total):
+    """The reference's progress lines (:182, :194, :224-225): its counter starts at
+    -header_length, is incremented for every line of the data pass (header lines
+    included) and a line is printed whenever it is a multiple of 500000 — "0 reads
+    processed." right after a non-empty header, negative multiples for headers longer
+    than 500000 lines."""
+    lo, hi = 1 - header_lines, lines_total - header_lines   # counter values after each increment
+    first = -((-lo) // PROGRESS_EVERY) * PROGRESS_EVERY      # smallest multiple >= lo
+    return [str(v) + " reads processed." for v in range(first, hi + 1, PROGRESS_EVERY)]
+
+
+def _log_summary(log, info):
+    log("SAM header processed, " + str(info.n_refs) + " references found.\n")
+    for line in progress_lines(info.header_lines, info.lines_total):
+        log(line)
+    log("A total of " + str(info.lines_total - info.header_lines) + " reads were processed, out of which, " +
+        str(info.reads_mapped) + " reads were mapped.\n")
+
+
 def consensus_files(filename, thresholds, prefix, min_depth=1, fill=b"-", nchar=0, maxdel_active=True,
                     device=None, log=None):
     """Run the whole pipeline on one SAM/SAM.gz file; returns a RunResult whose
@@ -93,10 +115,7 @@ def consensus_files(filename, thresholds, prefix, min_depth=1, fill=b"-", nchar=
     hb = parse_file(filename, maxdel_active, 150)
     t["parse"] = time.perf_counter() - t0
     if log:
-        log("SAM header processed, " + str(hb.info.n_refs) + " references found.\n")
-        reads_total = hb.info.lines_total - hb.info.header_lines
-        log("A total of " + str(reads_total) + " reads were processed, out of which, " +
-            str(hb.info.reads_mapped) + " reads were mapped.\n")
+        _log_summary(log, hb.info)
     files = consensus_batch(hb, thresholds, prefix, min_depth, fill, nchar, device, t)
     return RunResult(files, t, hb.info)
 
@@ -141,9 +160,7 @@ def consensus_files_sharded(filename, thresholds, prefix, min_depth, fill, nchar
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     hb = parse_file(filename, maxdel_active, 150)
     if log and rank == 0:
-        log("SAM header processed, " + str(hb.info.n_refs) + " references found.\n")
-        log("A total of " + str(hb.info.lines_total - hb.info.header_lines) + " reads were processed, out of "
-            "which, " + str(hb.info.reads_mapped) + " reads were mapped.\n")
+        _log_summary(log, hb.info)
 
     def runner(sub):
         ws = Workspace(DeviceBatch(sub, "cuda:%d" % local), thresholds, min_depth, fill)

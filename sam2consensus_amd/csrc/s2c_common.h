@@ -283,6 +283,16 @@ __device__ __forceinline__ void ripple1(uint32_t (&C)[8], uint32_t m) {
     }
 }
 
+// minus one at the positions of mask m (each counted before: no borrow out of plane 7)
+__device__ __forceinline__ void ripple_dec(uint32_t (&C)[8], uint32_t m) {
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+        const uint32_t t = ~C[b] & m;
+        C[b] ^= m;
+        m = t;
+    }
+}
+
 // 8 bit-planes of one counter → R[r] byte j = count of position 8j + r (8×8 bit transposes
 // on 4 byte lanes at once).
 __device__ __forceinline__ void transpose8(uint32_t (&R)[8]) {
@@ -325,22 +335,18 @@ __device__ __forceinline__ Run run_of(uint4 v) {
 // (0 if none); the base planes' bits are taken from query base q + (first covered − gpos).
 struct RecGeom {
     uint32_t valid, lo;   // covered bits, first covered bit
-    uint64_t qs;          // query base of position 32W + lo
+    uint32_t qs;          // offset into the run of position 32W + lo
 };
+// 32-bit arithmetic: positions < 2^32, a run's length < 2^24 and the runs a word looks at
+// start within 2^31 positions of it
 __device__ __forceinline__ RecGeom rec_geom(uint32_t gpos, uint32_t len, uint32_t W) {
     RecGeom g;
-    const int64_t s = (int64_t)gpos - 32ll * W, e = s + (int64_t)len;   // run in word-relative coordinates
-    const int64_t lo = s > 0 ? s : 0, hi = e < 32 ? e : 32;
-    if (hi <= lo) {
-        g.valid = 0u;
-        g.lo = 0u;
-        g.qs = 0;
-        return g;
-    }
-    const uint32_t n = (uint32_t)(hi - lo);
-    g.valid = (n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u)) << (uint32_t)lo;
-    g.lo = (uint32_t)lo;
-    g.qs = (uint64_t)(lo - s);   // offset into the run
+    const int32_t s = (int32_t)(gpos - 32u * W), e = s + (int32_t)len;   // run in word-relative coordinates
+    const int32_t lo = max(s, 0), hi = min(e, 32), n = hi - lo;
+    const uint32_t m = n >= 32 ? 0xFFFFFFFFu : ((1u << (n & 31)) - 1u);
+    g.valid = n > 0 ? m << (lo & 31) : 0u;
+    g.lo = n > 0 ? (uint32_t)lo : 0u;
+    g.qs = n > 0 ? (uint32_t)(lo - s) : 0u;
     return g;
 }
 __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {

@@ -688,9 +688,13 @@ static void tile_window(const s2c_batch *b, int64_t K, uint64_t a, uint64_t e, u
                        : tw[17];
 }
 
-// LDS bytes k_tile_dense stages a tile's window in (s2c_dense.hip)
+// LDS bytes k_tile_dense keeps a tile's window in (s2c_dense.hip), and whether it fits (with
+// query offsets of the window's base planes in 17 bits)
 static int64_t dense_bytes(const uint32_t *tw) {
-    return 12 * (int64_t)(tw[18] - tw[17]) + 12 * (int64_t)(tw[16] - tw[15]) + 16 * (int64_t)(tw[14] - tw[13] + 1) + 1024;
+    return S2C_DENSE_BYTES((int64_t)(tw[16] - tw[15]), (int64_t)(tw[18] - tw[17]));
+}
+static bool dense_fits(const uint32_t *tw) {
+    return dense_bytes(tw) <= S2C_DENSE_LDS && (int64_t)(tw[18] - tw[17]) <= S2C_DENSE_QW;
 }
 
 // PF_RUNS on the pieces a non-dense tile reads runs of (its window, its long pieces), and
@@ -957,12 +961,15 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
         int64_t tp = depth > 0 ? align_up((int64_t)std::ceil(E_TARGET / depth), S2C_POS_ALIGN) : TP_MAX;
         const double win = 32.0 * (double)(K + 1) * spp;    // run slots per word's window
         if (win <= 200.0 && spp > 0) {
-            // shallow: the widest tile whose window (8 B per run slot + 12 B per base plane word,
-            // with a margin for the depth's spread) fits the dense kernel's LDS
-            const double bpp = (12.0 * (double)ref_slots[r] + 16.0 * (double)ref_np[r] +
-                                12.0 * ((double)ref_qw[r] / 32.0 + (double)ref_np[r])) / (double)L;
+            // shallow: the widest tile whose window (12 B per op slot and 12 B per base plane word
+            // in LDS, plane words below S2C_DENSE_QW; with a margin for the depth's spread) fits
+            // the dense kernel
+            const double qpp = ((double)ref_qw[r] / 32.0 + 0.25 * (double)ref_np[r]) / (double)L;
+            const double bpp = (12.0 * (double)ref_slots[r] / (double)L) + 12.0 * qpp;
             tp = TP_MAX;
-            while (tp > TP_MIN && ((double)tp + 32.0 * (double)(K + 1)) * bpp + 1100.0 > 0.9 * S2C_DENSE_LDS) tp /= 2;
+            while (tp > TP_MIN && (((double)tp + 32.0 * (double)(K + 1)) * bpp + 1024.0 > 0.75 * S2C_DENSE_LDS ||
+                                   ((double)tp + 32.0 * (double)(K + 1)) * qpp > 0.8 * S2C_DENSE_QW))
+                tp /= 2;
         }
         tp = std::min(std::max(tp, TP_MIN), TP_MAX);
         if (tile_force > 0) tp = tile_force;
@@ -1039,10 +1046,9 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
         runs_max = std::max(runs_max, wruns);
         uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
         tile_window(b, K, T.a, T.b, tw);
-        const int64_t wbytes = dense_bytes(tw);
         uint32_t fl = nch > 1 ? S2C_TILE_DEEP : 0u;
         if (nev[t] > S2C_EPI_KEYS || (int64_t)ccap[t] > lcols) fl |= S2C_TILE_GENERAL;
-        if (fl == 0 && nev[t] == 0 && nlg == 0 && maxc <= 255 && wbytes <= S2C_DENSE_LDS) fl = S2C_TILE_DENSE;
+        if (fl == 0 && nev[t] == 0 && nlg == 0 && maxc <= 255 && dense_fits(tw)) fl = S2C_TILE_DENSE;
         const uint32_t bcap = nshort[t] ? pow2_at_least(2 * (uint64_t)nshort[t]) : 0u;
         tw[0] = (uint32_t)T.a; tw[1] = (uint32_t)T.b; tw[2] = (uint32_t)T.ref; tw[3] = fl;
         tw[4] = (uint32_t)boff; tw[5] = bcap; tw[6] = (uint32_t)loff; tw[7] = nlong[t];
@@ -1052,6 +1058,7 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
         loff += nlong[t];
         coff += ccap[t];
         if (fl == S2C_TILE_DENSE) {
+            I.dense_lds = std::max<int64_t>(I.dense_lds, dense_bytes(tw));
             const uint32_t it[S2C_ITEM_WORDS] = {(uint32_t)t, 0u, 0u, 0u};
             b->dense.insert(b->dense.end(), it, it + S2C_ITEM_WORDS);
         } else {
@@ -1226,11 +1233,13 @@ extern "C" int s2c_batch_shard(const s2c_batch *b, int64_t t0, int64_t t1, s2c_b
         aligned += tw[1] - tw[0];
     }
     J.runs_max = runs_max;
+    J.dense_lds = 0;
     for (int64_t t = 0; t < NT; t++) {
         uint32_t *tw = &s->tiles[(size_t)t * S2C_TILE_WORDS];
         tile_window(s.get(), K, tw[0], tw[1], tw);
-        if ((tw[3] & S2C_TILE_DENSE) && dense_bytes(tw) > S2C_DENSE_LDS)
-            return s2c_set_error(S2C_ERR_LIMIT, "shard window beyond the dense kernel's LDS");
+        if (!(tw[3] & S2C_TILE_DENSE)) continue;
+        if (!dense_fits(tw)) return s2c_set_error(S2C_ERR_LIMIT, "shard window beyond the dense kernel's LDS");
+        J.dense_lds = std::max<int64_t>(J.dense_lds, dense_bytes(tw));
     }
     mark_runs(s.get());
     // the shard's share of the workload's aligned bases (by its positions; for reporting)

@@ -96,6 +96,7 @@ class Workspace:
         d.n_pieces, d.n_ops, d.n_qwords, d.n_tiles = i.n_pieces, i.n_ops, i.n_qwords, i.n_tiles
         d.n_items, d.n_dense, d.n_deep = i.n_items, i.n_dense, i.n_deep
         d.padded_len, d.chunk, d.kwin, d.tile_max = i.padded_len, i.chunk, i.kwin, i.tile_max
+        d.dense_lds = i.dense_lds
         d.n_rlist = i.n_rlist
         # the maxdel rule (:210) runs on the device: the parser's setting unless overridden
         if maxdel_active is None:

@@ -12,6 +12,8 @@ from __future__ import annotations
 
 import numpy as np
 
+S2C_DENSE_LDS = 32768   # include/s2c.h
+
 NSYM = 6
 AMB = None
 OP_BASES = (0, 7, 8)        # M = X
@@ -200,7 +202,8 @@ def check_plan(hb):
         if pf1 > pf0:
             assert row[17] == (16 * pc[pf0, 1]) >> 5 and row[18] >= (16 * pc[pf1 - 1, 1] + (pc[pf1 - 1, 3] & 0xFFFFFF) + 31) // 32
         if row[3] == 4:
-            assert 12 * (row[18] - row[17]) + 12 * (row[16] - row[15]) + 16 * (row[14] - row[13] + 1) + 1024 <= 24576
+            ns, nq = row[16] - row[15], row[18] - row[17]
+            assert 4 * ((ns + 65) & ~1) + 8 * (nq + 32) + 4 * ((nq + 65) & ~1) + 8 * ns <= S2C_DENSE_LDS and nq <= 4096
     # k_reads' list: the pieces non-dense tiles read runs of, and the insertion emitters
     need = np.zeros(NP, bool)
     for row in T:

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
     assert declared <= exported, declared - exported
     assert declared == set(_lib.EXPORTS)
-    assert _lib.lib.s2c_abi_version() == 5
+    assert _lib.lib.s2c_abi_version() == 6
 
 
 def _model_case(sam, args):
@@ -196,3 +196,21 @@ def test_parallel_file_parse_equals_sequential(tmp_path, monkeypatch):
         monkeypatch.setenv("S2C_PARSE_THREADS", t)
         got[t] = _batch_digest(str(p), True)
     assert got["1"] == got["5"]
+
+
+# ---------------------------------------------------------------- CLI progress lines
+def _ref_progress(header_lines, lines_total):
+    """:182, :194, :224-225 restated line by line (the counter starts at -header_length)."""
+    out, t = [], -header_lines
+    for _ in range(lines_total):
+        t += 1
+        if t % 500000 == 0:
+            out.append(str(t) + " reads processed.")
+    return out
+
+
+@pytest.mark.parametrize("h,n", [(0, 0), (0, 10), (3, 3), (3, 10), (0, 500000), (2, 500002), (2, 500001),
+                                 (5, 1500005), (600000, 600001), (600000, 1200000)])
+def test_progress_lines_match_reference_counter(h, n):
+    from sam2consensus_amd.cli import progress_lines
+    assert progress_lines(h, n) == _ref_progress(h, n)

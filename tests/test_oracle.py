@@ -58,3 +58,66 @@ def test_configs_c1_oracle_matches_reference_content():
     r = o.run_case(text, g["args"], name="c1.sam")
     assert r["status"] == "ok"
     assert {k: v for k, v in r["files"].items()} == g["content"]
+
+
+# ------------------------------------------------ the multi-threaded C restatement
+ORACLE_DIR = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.dirname(
+    __import__("os").path.abspath(__file__))), "oracle")
+
+
+@pytest.fixture(scope="module")
+def mc_bin():
+    import os
+    import subprocess
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+    return os.path.join(ORACLE_DIR, "build", "s2c_oracle_mc")
+
+
+def run_mc(binary, sam_text, args, threads, name="in.sam"):
+    """oracle/s2c_oracle_mc on SAM text → {"status", "files"} (the golden cases' form)."""
+    import os
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, name)
+        with open(p, "w", encoding="latin-1", newline="") as fh:
+            fh.write(sam_text)
+        out = os.path.join(td, "out")
+        r = subprocess.run([binary, str(threads), "-i", p, "-o", out] + list(args), capture_output=True, text=True)
+        status = r.stdout.split("status: ")[1].split()[0] if "status: " in r.stdout else "crash rc=%d" % r.returncode
+        files = {}
+        if status == "ok" and os.path.isdir(out):
+            for f in sorted(os.listdir(out)):
+                with open(os.path.join(out, f), encoding="latin-1", newline="") as fh:
+                    files[f] = fh.read()
+        return {"status": status, "files": files}
+
+
+def test_c_oracle_matches_reference_cases(mc_bin):
+    """Every KAT / fuzz case (reference outputs) through the C restatement, 1 and 3 threads."""
+    bad = []
+    for i, case in enumerate(CASES):
+        for threads in ((1, 3) if i % 4 == 0 else (2,)):
+            r = run_mc(mc_bin, case["sam"], case["args"], threads)
+            if r["status"] != case["status"] or r["files"] != case["files"]:
+                bad.append((case["name"], threads, r["status"], case["status"]))
+    assert not bad, bad[:10]
+
+
+@pytest.mark.parametrize("wl", ["c1", "c2s"])
+def test_c_oracle_matches_python_oracle_on_configs(mc_bin, wl):
+    """Synthetic configurations (insertions, deletions, N, several references): the C
+    restatement on 4 threads equals the Python oracle."""
+    import os
+    import tempfile
+    from sam2consensus_amd import configs
+    name, kw = (wl, {}) if wl != "c2s" else ("c2", {"n_refs": 6, "depth": 40.0})
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, name + ".sam")
+        configs.synth_write(name, p, **kw)
+        text = open(p, "rb").read().decode("latin-1")
+    args = configs.cli_args(name)
+    want = o.run_case(text, args, name=name + ".sam")
+    got = run_mc(mc_bin, text, args, 4, name=name + ".sam")
+    assert got["status"] == want["status"] == "ok"
+    assert got["files"] == want["files"]
