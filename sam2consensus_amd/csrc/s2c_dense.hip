@@ -1,19 +1,36 @@
 // s2c_dense.hip — k_tile_dense: shallow tiles without insertion keys (-f of one char).
 //
 // Such a tile's body is one char per position (:355-389 with no insertion columns and a
-// one-char fill), so the byte offset of position q is q: no length scan.  One wave per tile
-// walks the tile's window itself (the short pieces starting up to kwin words before it):
-// the window's op words, base planes {p0, p1} and non-ACGT plane (one contiguous range
-// each) arrive in LDS by one LDS-DMA sweep, one lane per piece runs parsecigar + maxdel
-// (walk_piece, :46-82, :210) into run records in LDS, and the G = 64 / (tile words) lanes
-// of a word count the records covering it — A C G T into bit-sliced counters (as in
-// k_tile), a group of 8 records at a time; the rare '-' and 'N' into per-position byte
-// counters in LDS.  The word's lanes all-reduce their byte counters with DPP (every
-// position's total is ≤ 255, host plan), and each lane votes its 32/G consecutive
-// positions for every threshold (closed form of :241-251 / :359-366 with the
-// strict-majority shortcut) and stores their chars with wide stores.  Counts never touch
-// HBM.  The host sizes the tiles so the window takes ≤ S2C_DENSE_LDS bytes
-// (S2C_DENSE_BYTES; ≈ 1024 positions at 30x coverage).
+// one-char fill), so the byte offset of position q is q: no length scan.  One wave per tile:
+//
+//   1. DMA     the tile's window — the op words, base planes {p0, p1} and non-ACGT plane of
+//              the short pieces starting up to kwin words before the tile (one contiguous
+//              range each) — into LDS by buffer LDS-DMA with SGPR offsets (no per-lane address
+//              arithmetic); the lane's piece records into registers.
+//   2. walk    one lane per piece.  The common piece — one M / = / X token, no range, prefix
+//              or long flag — is one run of min(l, len(SEQ)) bases (parsecigar :64-69) and
+//              takes a few instructions; every other piece (D / I / S / H tokens, wrap ranges,
+//              maxdel with '-' chars in SEQ) is queued, and the queue is walked afterwards by
+//              the general parsecigar + maxdel walk (:46-82, :210) with all lanes busy.  Runs
+//              of reads holding N / '-' chars are queued too: their SEQ chars go into the
+//              per-position byte counters in one dense pass.
+//   3. count   the G = 64 / (tile words) lanes of a word count the runs covering it — A C G T
+//              into bit-sliced Harley–Seal counters, 8 records at a time.
+//   4. vote    each lane holds 8 / G counter rows (a row = positions 8j + r, j = 0..3, one
+//              byte each — the transposed counters' own layout, and the byte counters' layout
+//              in LDS) and votes them four positions per register: coverage by byte adds, the
+//              largest count by packed 16-bit max over (count << 3 | symbol) keys, the strict
+//              majority (2·m1 > cov) by a packed subtract — for thresholds in (0, 0.5] that
+//              alone decides the char (fl(t·cov) ≤ cov/2 < m1), for (0.5, 1] one more integer
+//              test per position; the rest take the closed form of :241-251 / :359-366.
+//              Chars come from a byte permute, rows are byte-transposed into consecutive
+//              positions and stored.  Counts never touch HBM.
+//
+// Tiles are mapped XCD-major (blocks b, b + 8, ... — one XCD — take consecutive tiles), so
+// the window overlap of neighbouring tiles is served by that XCD's L2.  The host sizes the
+// tiles so the window takes ≤ S2C_DENSE_LDS bytes (S2C_DENSE_BYTES).
+#include <algorithm>
+
 #include "s2c_common.h"
 
 #ifdef S2C_PROF
@@ -52,7 +69,9 @@ struct DenseArgs {
     const double *thresholds;
     uint64_t *tile_stats, *blk_len;
     uint8_t *out;
-    uint32_t padded_len, n_cols, n_tiles, kwin, fill_nondash, maxdel_active, maxdel;
+    uint32_t padded_len, n_cols, n_tiles, kwin, fill_nondash, maxdel_active, maxdel, n_items;
+    const void *ops_end, *bq_end, *bx_end;   // ends of the DMA sources
+    uint32_t buf_bytes;                                        // the window's LDS (16-byte multiple)
     int32_t n_thr, min_depth;
     const uint8_t *fill;   // the one -f char
 };
@@ -128,19 +147,67 @@ __device__ __forceinline__ void walk_window(const uint32_t *opl, const uint2 *bq
     }
 }
 
-// n dwords src[0..n) → LDS dst[0..n) by LDS-DMA (no VGPR round trip; the wave's 64 lanes copy
-// 64 consecutive dwords per instruction; lanes past n re-copy src[n-1] into the 64-dword slack
-// after dst).  Completion: s_waitcnt vmcnt(0).
-__device__ __forceinline__ void dma_dwords(uint32_t *dst, const uint32_t *src, uint32_t n) {
-    const uint32_t lane = threadIdx.x & 63;
-    for (uint32_t base = 0; base < n; base += 64) {
-        const uint32_t i = min(base + lane, n - 1);
-        __builtin_amdgcn_global_load_lds(src + i, dst + base, 4, 0, 0);
-    }
-}
-
 constexpr int WGD = 64;   // one wave per tile
 constexpr int GSD = 8;    // records per counting group (one Harley–Seal tree)
+
+// LDS byte address of a shared-memory pointer
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+typedef int v4i __attribute__((ext_vector_type(4)));
+// Scalar loads of uniform read-only words (tile records, items): s_load through the scalar
+// cache, waited here — the compiler would otherwise emit vector loads (the kernel stores to
+// global memory) and wait on vmcnt, i.e. on the window DMA in flight.
+__device__ __forceinline__ const uint32_t *uni_ptr(const uint32_t *p) {
+    const uint64_t v = (uint64_t)(uintptr_t)p;
+    return (const uint32_t *)(uintptr_t)((uint64_t)uni((uint32_t)v) | ((uint64_t)uni((uint32_t)(v >> 32)) << 32));
+}
+__device__ __forceinline__ uint32_t sload1(const uint32_t *p) {
+    uint32_t r;
+    asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(uni_ptr(p)) : "memory");
+    return r;
+}
+__device__ __forceinline__ double sload_f64(const double *p) {
+    uint64_t r;
+    asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(uni_ptr((const uint32_t *)p)) : "memory");
+    return __builtin_bit_cast(double, r);
+}
+__device__ __forceinline__ uint4 sload4(const uint32_t *p) {
+    v4i r;
+    asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(uni_ptr(p)) : "memory");
+    return make_uint4((uint32_t)r.x, (uint32_t)r.y, (uint32_t)r.z, (uint32_t)r.w);
+}
+
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"   // m0 (reserved) is set and clobbered by the DMA
+// n dwords src[0..n) of an array ending at `end` → LDS by 16-byte LDS-DMA (1 KB per wave
+// instruction, the source offset in an SGPR: no per-lane address arithmetic).  The copy
+// starts at the 16-byte boundary below src into the 16-byte aligned LDS region `dst`, so the
+// dwords land at dst + (src & 15); lanes past the copy's end are masked off (the region
+// needs dma16_bytes(n)).  The buffer range ends at `end` rounded up to 16 bytes (device
+// arrays are allocated in 512-byte granules).  Issued as inline asm: the compiler neither
+// sees the LDS writes nor counts these loads, so it never waits on them; completion is an
+// explicit s_waitcnt vmcnt(0) before the window is read.
+__device__ __forceinline__ void dma16(uint8_t *dst, const uint32_t *src, uint32_t n, const void *end) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uintptr_t s0 = (uintptr_t)src, sal = s0 & ~(uintptr_t)15, delta = s0 - sal;
+    const uintptr_t eal = ((uintptr_t)end + 15) & ~(uintptr_t)15;
+    const uint32_t nbytes = (uint32_t)delta + 4 * n;
+    v4i r;
+    r.x = (int)uni((uint32_t)sal);
+    r.y = (int)uni((uint32_t)(sal >> 32) & 0xFFFFu);
+    r.z = (int)uni((uint32_t)min((uint64_t)(eal - sal), (uint64_t)0x7FFFFFF0u));
+    r.w = 0x00020000;
+    const uint32_t m0 = uni(lds_addr(dst));
+    for (uint32_t base = 0; base < nbytes; base += 1024) {
+        if (base + 16 * lane < nbytes)
+            asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                         :: "s"(uni(m0 + base)), "v"(16 * lane), "s"(r), "s"(uni(base)) : "memory", "m0");
+    }
+}
+#pragma clang diagnostic pop
+// LDS bytes of a dma16 region for n dwords (16-byte phase of the source + rounding)
+__host__ __device__ constexpr uint32_t dma16_bytes(uint32_t n) { return (4 * n + 15 + 15) & ~15u; }
 
 // all-reduce of one register over the G adjacent lanes of a word
 template <int G>
@@ -152,14 +219,25 @@ __device__ __forceinline__ uint32_t word_allreduce(uint32_t v) {
     return v;
 }
 
-// +1 at the tile-relative positions [r0, r1) (clipped to [0, lim)), one byte counter per
-// position: byte adds at the ends, 4 positions per add in between
-__device__ __forceinline__ void lds_range(uint32_t *cnt, int32_t r0, int32_t r1, int32_t lim) {
-    uint32_t q = (uint32_t)max(r0, 0);
-    const uint32_t e = (uint32_t)max(min(r1, lim), 0);
-    for (; q < e && (q & 3); q++) atomicAdd(&cnt[q >> 2], 1u << (8 * (q & 3)));
-    for (; q + 4 <= e; q += 4) atomicAdd(&cnt[q >> 2], 0x01010101u);
-    for (; q < e; q++) atomicAdd(&cnt[q >> 2], 1u << (8 * (q & 3)));
+// Per-position byte counters in the ROW layout of the transposed counters: tile-relative
+// position p = 32w + 8j + r is byte j of dword 8w + r.
+__device__ __forceinline__ void cnt_add1(uint32_t *cnt, uint32_t p) {
+    atomicAdd(&cnt[((p >> 5) << 3) | (p & 7u)], 1u << (8 * ((p >> 3) & 3u)));
+}
+// +1 at the tile-relative positions [r0, r1) clipped to [0, lim): whole words 8 dwords at once
+__device__ __forceinline__ void cnt_range(uint32_t *cnt, int32_t r0, int32_t r1, int32_t lim) {
+    int32_t p = max(r0, 0);
+    const int32_t e = max(min(r1, lim), 0);
+    while (p < e) {
+        if ((p & 31) == 0 && p + 32 <= e) {
+#pragma unroll
+            for (int r = 0; r < 8; r++) atomicAdd(&cnt[((uint32_t)p >> 2) + r], 0x01010101u);
+            p += 32;
+        } else {
+            cnt_add1(cnt, (uint32_t)p);
+            p++;
+        }
+    }
 }
 
 // The non-ACGT chars of SEQ in a run of bases (window-relative query bases [q, q + l), tile-
@@ -187,118 +265,182 @@ __device__ __forceinline__ void x_events(const uint32_t *bxl, const uint2 *bql, 
                 xm &= xm - 1;
                 const int32_t r = r0 + b0 + (int32_t)bit;
                 if (r < 0 || r >= lim || ((pp.y >> bit) & 1u)) continue;
-                const uint32_t one = 1u << (8 * (r & 3));
                 if ((pp.x >> bit) & 1u) {
-                    atomicAdd(&ccnt[r >> 2], one);
-                    if (!drop) atomicAdd(&dcnt[r >> 2], one);
+                    cnt_add1(ccnt, (uint32_t)r);
+                    if (!drop) cnt_add1(dcnt, (uint32_t)r);
                 } else {
-                    atomicAdd(&ncnt[r >> 2], one);
+                    cnt_add1(ncnt, (uint32_t)r);
                 }
             }
         }
     }
 }
 
-// One wave per tile of NWP words; G = 64 / NWP lanes per word.
+// lane index among the active lanes of a ballot below this one
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// 16-bit halves (positions j = 0, 2 / j = 1, 3) of a register of 4 byte counts
+__device__ __forceinline__ uint32_t lo16(uint32_t v) { return v & 0x00FF00FFu; }
+__device__ __forceinline__ uint32_t hi16(uint32_t v) { return (v >> 8) & 0x00FF00FFu; }
+// the low bytes of the halves of e (j = 0, 2) and o (j = 1, 3) back into j order
+__device__ __forceinline__ uint32_t merge16(uint32_t o, uint32_t e) { return __builtin_amdgcn_perm(o, e, 0x06020400u); }
+typedef short v2s __attribute__((ext_vector_type(2)));
+typedef unsigned short v2u __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(v2u, a), __builtin_bit_cast(v2u, b)));
+}
+__device__ __forceinline__ uint32_t pk_sub(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2u, a) - __builtin_bit_cast(v2u, b));
+}
+// 0xFFFF in each half whose bit 15 is set
+__device__ __forceinline__ uint32_t pk_sign(uint32_t a) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2s, a) >> (v2s){15, 15});
+}
+// bit j (j = 0..3) = top bit of byte j
+__device__ __forceinline__ uint32_t byte_bits(uint32_t m) { return ((m & 0x80808080u) * 0x00204081u) >> 28; }
+
+// A tile's window (uniform values from its tile record; S2C_TILE_WORDS layout)
+struct Win {
+    uint32_t tile, a, n, cb0, pf0, npc, o0, nslot, qw0, nqw, W0, nwords;
+};
+__device__ __forceinline__ Win win_of(const DenseArgs &d, uint32_t item) {
+    Win v;
+    v.tile = sload1(d.items + 4 * (size_t)item);
+    const uint32_t *twp = d.tiles + (size_t)v.tile * S2C_TILE_WORDS;
+    const uint4 tw = sload4(twp), tw3 = sload4(twp + 12), tw4 = sload4(twp + 16);
+    v.cb0 = sload1(twp + 8);
+    v.a = tw.x;
+    v.n = tw.y - v.a;
+    v.pf0 = tw3.y;
+    v.npc = tw3.z - v.pf0;
+    v.o0 = tw3.w;
+    v.nslot = tw4.x - v.o0;
+    v.qw0 = tw4.y;
+    v.nqw = tw4.z - v.qw0;
+    v.W0 = v.a >> 5;
+    v.nwords = (v.n + 31) / 32;
+    return v;
+}
+// The window's arrays in LDS (S2C_DENSE_BYTES layout): op words, planes, non-ACGT plane
+// (each at its source's 16-byte phase, dma16), run records, the walk's two queues.
+struct WinLds {
+    const uint32_t *opl, *bxl;
+    const uint2 *bql;
+    uint2 *runl;
+    uint32_t *slowq, *xq;
+};
+__device__ __forceinline__ const uint32_t *phase16(const uint8_t *region, const void *src) {
+    return (const uint32_t *)(region + ((uintptr_t)src & 15));
+}
+__device__ __forceinline__ WinLds win_lds(const DenseArgs &d, const Win &v, uint8_t *buf) {
+    WinLds L;
+    const uint32_t *sop = d.ops + v.o0, *sbq = d.bq + 2 * (size_t)v.qw0, *sbx = d.bx + v.qw0;
+    L.opl = phase16(buf, sop);
+    buf += dma16_bytes(v.nslot);
+    L.bql = (const uint2 *)phase16(buf, sbq);
+    buf += dma16_bytes(2 * v.nqw);
+    L.bxl = phase16(buf, sbx);
+    buf += dma16_bytes(v.nqw);
+    L.runl = (uint2 *)buf;
+    L.slowq = (uint32_t *)(L.runl + v.nslot);
+    L.xq = L.slowq + v.nslot;
+    return L;
+}
+// issue the LDS-DMA of window v into buf (completion: s_waitcnt vmcnt(0))
+__device__ __forceinline__ void win_issue(const DenseArgs &d, const Win &v, uint8_t *buf) {
+    dma16(buf, d.ops + v.o0, v.nslot, d.ops_end);
+    buf += dma16_bytes(v.nslot);
+    dma16(buf, d.bq + 2 * (size_t)v.qw0, 2 * v.nqw, d.bq_end);
+    buf += dma16_bytes(2 * v.nqw);
+    dma16(buf, d.bx + v.qw0, v.nqw, d.bx_end);
+}
+
+// One tile of NWP words from its window in LDS; G = 64 / NWP lanes per word, RPL = 8 / G
+// counter rows (4 positions each) voted per lane.  dcnt / ncnt / ccnt: zeroed byte counters.
+constexpr int PFN = 4;   // piece records per lane loaded with the DMA (windows of ≤ 256 pieces)
 template <int NWP>
-__global__ __launch_bounds__(WGD) void k_tile_dense(const DenseArgs d) {
-    constexpr int G = WGD / NWP, PPL = 32 / G;
-    static_assert(PPL >= 4 && PPL % 4 == 0, "a lane votes whole dwords of positions");
-    extern __shared__ uint4 arena[];          // the window (S2C_DENSE_BYTES layout)
-    // one byte per position: '-' (D/N/P runs, '-' of SEQ unless maxdel drops the read's), 'N'
-    // of SEQ, '-' of SEQ (all: the planes count them as C, and 'N' as A)
-    __shared__ uint32_t dcnt[8 * NWP], ncnt[8 * NWP], ccnt[8 * NWP];
-    __shared__ uint8_t amb[64];
+__device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, const WinLds &L, uint32_t *dcnt,
+                                           uint32_t *ncnt, uint32_t *ccnt, const uint8_t *amb, uint32_t fill0,
+                                           const uint4 (&Pp)[PFN], const uint32_t (&oe)[PFN], uint32_t cw0, uint32_t cw1) {
+    constexpr int G = WGD / NWP, RPL = 8 / G;
 #ifdef S2C_PROF
     unsigned long long prof_t = 0;
 #endif
     PROF_MARK(0);
     const uint32_t lane = threadIdx.x;
     const uint32_t w = lane / G, g = lane % G;
-    const uint32_t tile = uni(d.items[4 * (size_t)blockIdx.x]);
-    const uint32_t *twp = d.tiles + (size_t)tile * S2C_TILE_WORDS;
-    const uint4 tw = *(const uint4 *)twp;
-    const uint4 tw3 = *(const uint4 *)(twp + 12), tw4 = *(const uint4 *)(twp + 16);
-    const uint32_t cb0 = uni(twp[8]);
-    const uint32_t a = uni(tw.x), n = uni(tw.y) - a;
-    const uint32_t pf0 = uni(tw3.y), pf1 = uni(tw3.z), o0 = uni(tw3.w), o1 = uni(tw4.x), qw0 = uni(tw4.y), qw1 = uni(tw4.z);
-    const uint32_t W0 = a >> 5, nwords = (n + 31) / 32, W = W0 + w;
+    const uint32_t tile = v.tile, a = v.a, n = v.n, cb0 = v.cb0, npc = v.npc, o0 = v.o0, qw0 = v.qw0;
+    const uint32_t W0 = v.W0, nwords = v.nwords, W = W0 + w;
     const bool active = w < nwords;
     const uint32_t K = d.kwin;
-    const uint32_t nslot = o1 - o0, npc = pf1 - pf0, nqw = qw1 - qw0;
-    // ---- one round trip: the window's op words and planes by LDS-DMA, this lane's first
-    //      piece record and its word's run-slot range
-    uint32_t *opl = (uint32_t *)arena;
-    uint2 *bql = (uint2 *)(opl + ((nslot + 65) & ~1u));
-    uint32_t *bxl = (uint32_t *)(bql + nqw + 32);
-    uint2 *runl = (uint2 *)(bxl + ((nqw + 65) & ~1u));
-    if (nslot) dma_dwords(opl, d.ops + o0, nslot);
-    if (nqw) {
-        dma_dwords((uint32_t *)bql, d.bq + 2 * (size_t)qw0, 2 * nqw);
-        dma_dwords(bxl, d.bx + qw0, nqw);
-    }
-    constexpr int PFN = 4;   // piece records per lane in flight with the DMA
-    uint4 Pp[PFN];
-    uint32_t oe[PFN];
-#pragma unroll
-    for (int i = 0; i < PFN; i++) {
-        const uint32_t k = lane + WGD * i;
-        Pp[i] = make_uint4(0u, 0u, 0u, 0u);
-        oe[i] = 0;
-        if (k < npc) {
-            Pp[i] = ((const uint4 *)d.pc)[pf0 + k];
-            oe[i] = d.pc[4 * (size_t)(pf0 + k + 1) + 2];
-        }
-    }
-    uint32_t cw0 = 0, cw1 = 0;
-    if (active) {
-        cw0 = d.rs[W >= K ? W - K : 0u] - o0;
-        cw1 = d.rs[W + 1] - o0;
-    }
-    for (uint32_t i = lane; i < 8 * NWP; i += WGD) {
-        dcnt[i] = 0;
-        ncnt[i] = 0;
-        ccnt[i] = 0;
-    }
-    amb[lane] = c_amb[lane];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_sync();
+    const uint32_t pf0 = v.pf0;
+    const uint32_t *opl = L.opl, *bxl = L.bxl;
+    const uint2 *bql = L.bql;
+    uint2 *runl = L.runl;
+    uint32_t *slowq = L.slowq, *xq = L.xq;
     PROF_MARK(1);
-    // ---- parsecigar + maxdel of the window's pieces (one lane per piece) → run records of the
-    //      bases {gpos, (query base − 32·qw0) << 15 | len << 4 | kind}; '-' runs and the
-    //      non-ACGT chars of SEQ straight into the byte counters
+
+    // ---- walk: one lane per piece → run records {gpos, (query base − 32·qw0) << 15 | len << 4
+    //      | kind} of the bases; the common piece here, the others queued
     const int32_t T0 = (int32_t)(32 * W0), TL = (int32_t)(32 * nwords);   // the tile's words
-    auto walk = [&](const uint4 &P, uint32_t oend) {
-        const bool lng = ((P.w >> 24) & S2C_PF_LONG) != 0;   // (a long piece starting here does not overlap the tile)
-        walk_window(opl, bql, bxl, P, P.z - o0, oend - o0, (uint32_t)((uint64_t)P.y * 16 - 32ull * qw0),
-                    d.maxdel_active != 0, d.maxdel, [&](uint32_t j, uint32_t gp, uint32_t l, uint32_t kind, uint32_t q) {
-                        const uint32_t kd = (lng || kind == S2C_RUN_EMPTY) ? 0u : (kind & 3u);
-                        runl[j] = kd == S2C_RUN_BASES ? make_uint2(gp, (q << 15) | (l << 4) | kind) : make_uint2(0u, 0u);
-                        const int32_t r0 = (int32_t)gp - T0;
-                        if (kd == S2C_RUN_DASH) lds_range(dcnt, r0, r0 + (int32_t)l, TL);
-                        if (kd == S2C_RUN_BASES && (kind & S2C_RUN_XBIT))
-                            x_events(bxl, bql, q, l, r0, TL, (kind & S2C_RUN_DROP) != 0, dcnt, ncnt, ccnt);
-                    });
-    };
+    const bool mda = d.maxdel_active != 0;
+    uint32_t nslow = 0, nx = 0;   // queue lengths (uniform)
     const uint32_t nit = ABL(4) ? 0u : (npc + WGD - 1) / WGD;
-    for (uint32_t i = 0; i < nit; i++) {   // (one copy of the walk: the prefetched records by a select chain)
-        const uint32_t k = lane + WGD * i;
+    for (uint32_t it = 0; it < nit; it++) {
+        const uint32_t k = lane + WGD * it;
         uint4 P = Pp[0];
         uint32_t oend = oe[0];
 #pragma unroll
-        for (int u = 1; u < PFN; u++) {
-            P.x = i == (uint32_t)u ? Pp[u].x : P.x;
-            P.y = i == (uint32_t)u ? Pp[u].y : P.y;
-            P.z = i == (uint32_t)u ? Pp[u].z : P.z;
-            P.w = i == (uint32_t)u ? Pp[u].w : P.w;
-            oend = i == (uint32_t)u ? oe[u] : oend;
-            asm volatile("" : "+v"(P.x), "+v"(P.y), "+v"(P.z), "+v"(P.w), "+v"(oend));
+        for (int u = 1; u < PFN; u++) {   // (the loaded records by a select chain)
+            P.x = it == (uint32_t)u ? Pp[u].x : P.x;
+            P.y = it == (uint32_t)u ? Pp[u].y : P.y;
+            P.z = it == (uint32_t)u ? Pp[u].z : P.z;
+            P.w = it == (uint32_t)u ? Pp[u].w : P.w;
+            oend = it == (uint32_t)u ? oe[u] : oend;
         }
-        if (i >= (uint32_t)PFN && k < npc) {   // (windows of more than 256 pieces)
+        const bool in = k < npc;
+        if (it >= (uint32_t)PFN && in) {   // (windows of more than 256 pieces)
             P = ((const uint4 *)d.pc)[pf0 + k];
             oend = d.pc[4 * (size_t)(pf0 + k + 1) + 2];
         }
-        if (k < npc) walk(P, oend);
+        const uint32_t fl = P.w >> 24, slen = P.w & 0xFFFFFFu, j = P.z - o0;
+        const uint32_t w0 = in ? opl[j] : 0u, op = w0 & 15u, l = w0 >> 4;
+        const bool xf = (fl & S2C_PF_X) != 0;
+        // one M / = / X token and nothing else: seqout = SEQ[0 : min(l, len(SEQ))] (:64-69)
+        const bool fast = in && oend - P.z == 1u && (fl & ~(uint32_t)S2C_PF_X) == 0u && op_bases(op) && !(xf && mda);
+        if (fast) {
+            const uint32_t take = min(l, slen), q = 16u * (P.y - 2u * qw0);
+            runl[j] = make_uint2(P.x, (q << 15) | (take << 4) | S2C_RUN_BASES | (xf ? S2C_RUN_XBIT : 0u));
+        }
+        const uint64_t bs = __ballot(in && !fast), bxm = __ballot(fast && xf);
+        if (in && !fast) slowq[nslow + mbcnt(bs)] = k;
+        if (fast && xf) xq[nx + mbcnt(bxm)] = j;
+        nslow += (uint32_t)__popcll(bs);
+        nx += (uint32_t)__popcll(bxm);
+    }
+    lds_sync();
+    // queued pieces: the general walk; '-' runs and SEQ N / '-' straight into the byte counters
+    for (uint32_t i = lane; i < nslow; i += WGD) {
+        const uint32_t k = slowq[i];
+        const uint4 P = ((const uint4 *)d.pc)[pf0 + k];
+        const uint32_t oend = d.pc[4 * (size_t)(pf0 + k + 1) + 2];
+        const bool lng = ((P.w >> 24) & S2C_PF_LONG) != 0;   // (a long piece starting here does not overlap the tile)
+        walk_window(opl, bql, bxl, P, P.z - o0, oend - o0, 16u * (P.y - 2u * qw0), mda, d.maxdel,
+                    [&](uint32_t j, uint32_t gp, uint32_t l, uint32_t kind, uint32_t q) {
+                        const uint32_t kd = (lng || kind == S2C_RUN_EMPTY) ? 0u : (kind & 3u);
+                        runl[j] = kd == S2C_RUN_BASES ? make_uint2(gp, (q << 15) | (l << 4) | kind) : make_uint2(0u, 0u);
+                        const int32_t r0 = (int32_t)gp - T0;
+                        if (kd == S2C_RUN_DASH) cnt_range(dcnt, r0, r0 + (int32_t)l, TL);
+                        if (kd == S2C_RUN_BASES && (kind & S2C_RUN_XBIT))
+                            x_events(bxl, bql, q, l, r0, TL, (kind & S2C_RUN_DROP) != 0, dcnt, ncnt, ccnt);
+                    });
+    }
+    // queued single-token runs of reads with N / '-' in SEQ (never dropped: maxdel is off)
+    for (uint32_t i = lane; i < nx; i += WGD) {
+        const uint2 rv = runl[xq[i]];
+        x_events(bxl, bql, rv.y >> 15, (rv.y >> 4) & 0x7FFu, (int32_t)rv.x - T0, TL, false, dcnt, ncnt, ccnt);
     }
     lds_sync();
     PROF_MARK(2);
@@ -372,145 +514,196 @@ __global__ __launch_bounds__(WGD) void k_tile_dense(const DenseArgs d) {
         C[0][r] = x - z;           // C
         C[1][r] = y - z;           // G
     }
+    // this lane's rows g·RPL .. g·RPL + RPL − 1, all-reduced over the word's G lanes
+    // (DPP needs the same register in every lane: all 8 rows reduced, then this lane's selected)
     if constexpr (G > 1) {
 #pragma unroll
         for (int c = 0; c < 4; c++)
 #pragma unroll
             for (int r = 0; r < 8; r++) C[c][r] = word_allreduce<G>(C[c][r]);
     }
+    uint32_t rA[RPL], rC[RPL], rG[RPL], rT[RPL];
+#pragma unroll
+    for (int rr = 0; rr < RPL; rr++) {
+        rA[rr] = C[3][rr];
+        rC[rr] = C[0][rr];
+        rG[rr] = C[1][rr];
+        rT[rr] = C[2][rr];
+#pragma unroll
+        for (int k = 1; k < G; k++) {
+            const bool mine = g == (uint32_t)k;
+            rA[rr] = mine ? C[3][k * RPL + rr] : rA[rr];
+            rC[rr] = mine ? C[0][k * RPL + rr] : rC[rr];
+            rG[rr] = mine ? C[1][k * RPL + rr] : rG[rr];
+            rT[rr] = mine ? C[2][k * RPL + rr] : rT[rr];
+        }
+    }
     PROF_MARK(4);
 
-    // ---- vote of this lane's PPL consecutive positions p0 .. p0+PPL-1 of its word
-    const uint32_t p0 = g * PPL;                 // word-relative
-    const uint32_t jb = p0 >> 3, rs0 = p0 & 7;   // PPL ≥ 8: bytes jb.. of every R[r]; PPL = 4: R[rs0 + i] byte jb
-    const uint32_t q0 = 32 * w + p0;             // tile-relative
-    const uint32_t npos = active ? (q0 < n ? min((uint32_t)PPL, n - q0) : 0u) : 0u;
-    uint32_t dv[PPL / 4], nv[PPL / 4], cv[PPL / 4];   // '-', 'N', '-' of SEQ counts, 4 positions a dword
+    // ---- vote of this lane's rows: row rr = word positions 8j + g·RPL + rr (j = 0..3)
+    const uint32_t rbase = 8 * w + g * RPL;   // the rows' dword index in the byte counters
+    uint32_t rD[RPL], rN[RPL], rX[RPL];       // '-', 'N', '-' of SEQ
 #pragma unroll
-    for (int v = 0; v < PPL / 4; v++) {
-        dv[v] = dcnt[(q0 >> 2) + v];
-        nv[v] = ncnt[(q0 >> 2) + v];
-        cv[v] = ccnt[(q0 >> 2) + v];
+    for (int rr = 0; rr < RPL; rr++) {
+        rD[rr] = active ? dcnt[rbase + rr] : 0u;
+        rN[rr] = active ? ncnt[rbase + rr] : 0u;
+        rX[rr] = active ? ccnt[rbase + rr] : 0u;
     }
-    uint32_t jbt = jb;   // (re-made opaque per threshold: the counts stay packed, not hoisted)
-    // count of symbol sym (A C G T = C[3] C[0] C[1] C[2]) at p0 + i: byte jb + i/8 of
-    // R[i % 8] (PPL ≥ 8), byte jb of R[rs0 + i] (PPL = 4)
-    auto cnt = [&](int sym, int i) -> uint32_t {
-        if constexpr (PPL >= 8) {
-            return (C[sym][i & 7] >> (8 * (jbt + (uint32_t)(i >> 3)))) & 0xFFu;
-        } else {
-            const uint32_t v = rs0 ? C[sym][4 + i] : C[sym][i];
-            return (v >> (8 * jbt)) & 0xFFu;
+    const uint32_t md = (uint32_t)min(max(d.min_depth, 1), 0x7FFF);   // called: cov ≥ max(-m, 1) (:356-359)
+    const uint32_t md16 = md | (md << 16);
+    // per row: chars of the largest count, masks (one byte per position) of strict majority
+    // and of "not called", the largest count m1 and coverage (bytes), in-tile bytes
+    uint32_t chr[RPL], fmk[RPL], ncm[RPL], m1b[RPL], cvb[RPL], inb[RPL];
+    uint32_t sc = 0;
+#pragma unroll
+    for (int rr = 0; rr < RPL; rr++) {
+        const uint32_t cA = rA[rr] - rN[rr], cC = rC[rr] - rX[rr];   // 'N' counted as A, SEQ '-' as C
+        const uint32_t cv = cA + cC + rG[rr] + rT[rr] + rD[rr] + rN[rr];   // ≤ 255 per byte
+        // in-tile positions: p = 32w + 8j + r < n
+        const uint32_t pr = 32 * w + g * RPL + rr;
+        uint32_t im = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) im |= (active && pr + 8 * j < n) ? (0xFFu << (8 * j)) : 0u;
+        inb[rr] = im;
+        cvb[rr] = cv;
+        sc = __builtin_amdgcn_udot4(cv & im, 0x01010101u, sc, false);   // Σ cov over the tile (:357)
+        // keys count << 3 | symbol ("-ACGNT" index), halves e (j = 0, 2) and o (j = 1, 3)
+        const uint32_t cnt[NSYM] = {rD[rr], cA, cC, rG[rr], rN[rr], rT[rr]};
+        uint32_t ke = 0, ko = 0;
+#pragma unroll
+        for (uint32_t s = 0; s < NSYM; s++) {
+            ke = pk_max(ke, (lo16(cnt[s]) << 3) | (s * 0x00010001u));
+            ko = pk_max(ko, (hi16(cnt[s]) << 3) | (s * 0x00010001u));
         }
-    };
-    // the same for a run-time i (rare paths: a select chain, no indexed registers)
-    auto sel = [&](const auto &R, uint32_t r) -> uint32_t {
-        constexpr int nr = (int)(sizeof(R) / sizeof(R[0]));
+        const uint32_t ce = lo16(cv), co = hi16(cv);
+        // strict majority 2·m1 > cov ⟺ 8·m1 − 4·cov > 0: the half's bit 15 of 4·cov − 8·m1
+        const uint32_t mje = pk_sign(pk_sub(ce << 2, ke & 0xFFF8FFF8u)), mjo = pk_sign(pk_sub(co << 2, ko & 0xFFF8FFF8u));
+        // not called: cov < md
+        const uint32_t nce = pk_sign(pk_sub(ce, md16)), nco = pk_sign(pk_sub(co, md16));
+        const uint32_t sym = merge16(ko & 0x00070007u, ke & 0x00070007u);
+        chr[rr] = __builtin_amdgcn_perm(0x0000544Eu, 0x4743412Du, sym);   // "-ACGNT"[sym]
+        fmk[rr] = merge16(mjo, mje);
+        ncm[rr] = merge16(nco, nce) | ~im;
+        m1b[rr] = merge16(ko >> 3, ke >> 3);
+    }
+    const uint32_t fill4 = fill0 * 0x01010101u;
+    const uint64_t ostride = (uint64_t)d.padded_len + d.n_cols;   // max(1, len(fill)) = 1
+    uint8_t *const obase = d.out + (uint64_t)a + cb0 + 32 * w + g * RPL;
+    const bool full = active && 32 * w + 32 <= n;
+    // the count of symbol s at row rr, byte j (slow path: run-time indices, select chains)
+    auto sel = [&](const uint32_t (&R)[RPL], uint32_t r) -> uint32_t {
         uint32_t v = R[0];
 #pragma unroll
-        for (int k = 1; k < nr; k++) {
+        for (int k = 1; k < RPL; k++) {
             v = r == (uint32_t)k ? R[k] : v;
             asm volatile("" : "+v"(v));   // keeps the chain of selects (no indexed copy)
         }
         return v;
     };
-    auto cnt_rt = [&](int sym, uint32_t i) -> uint32_t {
-        const uint32_t r = PPL >= 8 ? (i & 7u) : rs0 + i, by = PPL >= 8 ? jb + (i >> 3) : jb;
-        return (sel(C[sym], r) >> (8 * by)) & 0xFFu;
-    };
-    const uint64_t ostride = (uint64_t)d.padded_len + d.n_cols;   // max(1, len(fill)) = 1
-    const uint32_t fill0 = d.fill[0];
-    uint8_t *const obase = d.out + (uint64_t)a + cb0 + q0;
-    const uint32_t inmask = npos >= 32 ? 0xFFFFFFFFu : (1u << npos) - 1u;
-    uint32_t sc = 0;
     for (int t = 0; t < (ABL(8) ? 0 : d.n_thr); t++) {
-        const double th = d.thresholds[t];
-        const uint32_t uq = pass_uq(&th, 1);
-        const bool uqok = uq != 0;
-        jbt = jb;
-        asm volatile("" : "+v"(jbt));
-        uint32_t ow[PPL / 4];
-        uint32_t nd = 0, ne = 0, slow = 0;
-        // fast path: fill, or the strict-majority symbol
+        const double th = sload_f64(d.thresholds + t);
+        // threshold class: (0, 0.5] the majority decides; (0.5, 1] plus m1·2^15 ≥ uq·cov; else none
+        const bool clsA = th > 0.0 && th <= 0.5, clsB = th > 0.5 && th <= 1.0;
+        const uint32_t uq = clsB ? (uint32_t)ceil(th * 32768.0) + 1u : 0u;
+        uint32_t ow[RPL], slow = 0, nd = 0, ne = 0;
 #pragma unroll
-        for (int i = 0; i < PPL; i++) {
-            uint32_t c6[NSYM];   // "-ACGNT"
-            c6[0] = (dv[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-            c6[4] = (nv[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-            c6[1] = cnt(3, i) - c6[4];
-            c6[2] = cnt(0, i) - ((cv[i >> 2] >> (8 * (i & 3))) & 0xFFu);
-            c6[3] = cnt(1, i);
-            c6[5] = cnt(2, i);
-            const bool in = (uint32_t)i < npos;
-            const uint32_t cov = c6[0] + c6[1] + c6[2] + c6[3] + c6[4] + c6[5];
-            if (t == 0) sc += in ? cov : 0u;   // Σ cov, uncalled positions included (:357)
-            const bool called = (cov > 0) & ((int32_t)cov >= d.min_depth);   // :356-359
-            uint32_t k6[NSYM];
+        for (int rr = 0; rr < RPL; rr++) {
+            uint32_t fm = (clsA || clsB) ? fmk[rr] & ~ncm[rr] : 0u;
+            if (clsB) {   // m1·2^15 ≥ uq·cov per position (m1, cov ≤ 255: 32-bit products)
+                uint32_t ok = 0;
 #pragma unroll
-            for (uint32_t s = 0; s < NSYM; s++) k6[s] = (c6[s] << 3) | s;
-            const uint32_t mk = max(max(max(k6[0], k6[1]), k6[2]), max(max(k6[3], k6[4]), k6[5]));
-            // majority_fast in 32 bits (counts ≤ 255: m1·2^15 and uq·cov < 2^24)
-            const uint32_t m1 = mk >> 3;
-            const bool fast = uqok & (2u * m1 > cov) & ((m1 << 15) >= uq * cov);
-            slow |= (called && !fast) ? (1u << i) : 0u;
-            // "-ACGNT"[mk & 7] by a byte permute
-            const uint32_t sc6 = __builtin_amdgcn_perm(0x0000544Eu, 0x4743412Du, (mk & 7u) | 0x0C0C0C00u);
-            const uint32_t ch = called ? sc6 : fill0;
-            nd += (in && (!called || fast)) ? (called ? (ch != '-') : d.fill_nondash) : 0u;
-            if ((i & 3) == 0) ow[i >> 2] = 0;
-            ow[i >> 2] |= ch << (8 * (i & 3));
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t m1 = (m1b[rr] >> (8 * j)) & 0xFFu, cv = (cvb[rr] >> (8 * j)) & 0xFFu;
+                    ok |= (m1 << 15) >= uq * cv ? (0xFFu << (8 * j)) : 0u;
+                }
+                fm &= ok;
+            }
+            ow[rr] = (chr[rr] & fm) | (fill4 & ncm[rr]);   // fast chars; fill; slow bytes 0 for now
+            slow |= byte_bits(~(fm | ncm[rr])) << (4 * rr);
+            // non-'-' chars: fast chars ≠ '-' and in-tile fill chars
+            const uint32_t nz = (chr[rr] ^ 0x2D2D2D2Du) & fm;   // nonzero byte ⟺ fast char ≠ '-'
+            const uint32_t nzb = (((nz & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | nz) & 0x80808080u;
+            nd += (uint32_t)__popc(nzb) + d.fill_nondash * (uint32_t)__popc(ncm[rr] & inb[rr] & 0x01010101u);
         }
-        // the other called positions: closed form of the group-sort vote
-        slow &= inmask;
+        // the other called positions: closed form of the group-sort vote (:241-251, :359-366)
         while (slow) {
             const uint32_t i = (uint32_t)__builtin_ctz(slow);
             slow &= slow - 1;
-            uint32_t c6[NSYM];
-            c6[0] = (sel(dv, i >> 2) >> (8 * (i & 3))) & 0xFFu;
-            c6[4] = (sel(nv, i >> 2) >> (8 * (i & 3))) & 0xFFu;
-            c6[1] = cnt_rt(3, i) - c6[4];
-            c6[2] = cnt_rt(0, i) - ((sel(cv, i >> 2) >> (8 * (i & 3))) & 0xFFu);
-            c6[3] = cnt_rt(1, i);
-            c6[5] = cnt_rt(2, i);
+            const uint32_t rr = i >> 2, sh = 8 * (i & 3);
+            uint32_t c6[NSYM];   // "-ACGNT"
+            c6[0] = (sel(rD, rr) >> sh) & 0xFFu;
+            c6[4] = (sel(rN, rr) >> sh) & 0xFFu;
+            c6[1] = ((sel(rA, rr) >> sh) & 0xFFu) - c6[4];
+            c6[2] = ((sel(rC, rr) >> sh) & 0xFFu) - ((sel(rX, rr) >> sh) & 0xFFu);
+            c6[3] = (sel(rG, rr) >> sh) & 0xFFu;
+            c6[5] = (sel(rT, rr) >> sh) & 0xFFu;
             const uint32_t cov = c6[0] + c6[1] + c6[2] + c6[3] + c6[4] + c6[5];
             uint32_t gs[NSYM];
             greater_sums(c6, gs);
             const uint32_t ch = amb[vote_mask_u32(c6, gs, th * (double)cov)];
             nd += ch != '-';
             ne += ch == 0xFFu;
-            const uint32_t sh = 8 * (i & 3), keep = ~(0xFFu << sh);
 #pragma unroll
-            for (int v = 0; v < PPL / 4; v++) {
-                ow[v] = (i >> 2) == (uint32_t)v ? (ow[v] & keep) | (ch << sh) : ow[v];
+            for (int v = 0; v < RPL; v++) {
+                ow[v] = rr == (uint32_t)v ? ow[v] | (ch << sh) : ow[v];
                 asm volatile("" : "+v"(ow[v]));
             }
         }
+        // rows → consecutive positions: byte j of row rr is position 8j + g·RPL + rr
         uint8_t *dst = obase + (uint64_t)t * ostride;
-        if (npos == (uint32_t)PPL) {
-            if constexpr (PPL >= 16) {
+        uint32_t cj[4];   // RPL ≤ 4 bytes of each j (RPL = 8: two halves, below)
+        auto tr4 = [](uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t (&o)[4]) {   // 4×4 byte transpose
+            const uint32_t t0 = __builtin_amdgcn_perm(r1, r0, 0x05010400u);
+            const uint32_t t1 = __builtin_amdgcn_perm(r1, r0, 0x07030602u);
+            const uint32_t t2 = __builtin_amdgcn_perm(r3, r2, 0x05010400u);
+            const uint32_t t3 = __builtin_amdgcn_perm(r3, r2, 0x07030602u);
+            o[0] = __builtin_amdgcn_perm(t2, t0, 0x05040100u);
+            o[1] = __builtin_amdgcn_perm(t2, t0, 0x07060302u);
+            o[2] = __builtin_amdgcn_perm(t3, t1, 0x05040100u);
+            o[3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
+        };
+        if constexpr (RPL == 8) {
+            uint32_t c2[4];
+            tr4(ow[0], ow[1], ow[2], ow[3], cj);
+            tr4(ow[4 % RPL], ow[5 % RPL], ow[6 % RPL], ow[7 % RPL], c2);
+            if (full) {
 #pragma unroll
-                for (int v = 0; v < PPL / 4; v += 4) *(uint4 *)(dst + 4 * v) = make_uint4(ow[v], ow[v + 1], ow[v + 2], ow[v + 3]);
-            } else if constexpr (PPL == 8) {
-                *(uint2 *)dst = make_uint2(ow[0], ow[1]);
-            } else {
-                *(uint32_t *)dst = ow[0];
+                for (int j = 0; j < 4; j++) *(uint2 *)(dst + 8 * j) = make_uint2(cj[j], c2[j]);
+            } else if (active) {
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+#pragma unroll
+                    for (int b = 0; b < 8; b++)
+                        if (32 * w + 8 * j + b < n) dst[8 * j + b] = (uint8_t)((b < 4 ? cj[j] : c2[j]) >> (8 * (b & 3)));
             }
         } else {
+            tr4(ow[0], RPL > 1 ? ow[1 % RPL] : 0u, RPL > 2 ? ow[2 % RPL] : 0u, RPL > 3 ? ow[3 % RPL] : 0u, cj);
+            if (full) {
 #pragma unroll
-            for (int i = 0; i < PPL; i++)
-                if ((uint32_t)i < npos) dst[i] = (uint8_t)(ow[i >> 2] >> (8 * (i & 3)));
+                for (int j = 0; j < 4; j++) {
+                    if constexpr (RPL == 4) *(uint32_t *)(dst + 8 * j) = cj[j];
+                    else if constexpr (RPL == 2) *(uint16_t *)(dst + 8 * j) = (uint16_t)cj[j];
+                    else dst[8 * j] = (uint8_t)cj[j];
+                }
+            } else if (active) {
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+#pragma unroll
+                    for (int b = 0; b < RPL; b++)
+                        if (32 * w + 8 * j + g * RPL + b < n) dst[8 * j + b] = (uint8_t)(cj[j] >> (8 * b));
+            }
         }
         if (t == 0) sc = wave_sum(sc);
         nd = wave_sum(nd);
         ne = wave_sum(ne);
         if (lane == 0) {   // tile statistics (:352-397)
-            const size_t j = (size_t)t * d.n_tiles + tile;
-            uint64_t *st = d.tile_stats + j * 4;
+            const size_t jt = (size_t)t * d.n_tiles + tile;
+            uint64_t *st = d.tile_stats + jt * 4;
             st[0] = sc;
             st[1] = n;
             st[2] = nd;
             st[3] = ne;
-            d.blk_len[j] = n;
+            d.blk_len[jt] = n;
         }
     }
     PROF_MARK(5);
@@ -519,14 +712,64 @@ __global__ __launch_bounds__(WGD) void k_tile_dense(const DenseArgs d) {
         atomicAdd(&g_prof[8], 1ull);
         atomicAdd(&g_prof[9], (unsigned long long)ngrp);
         atomicAdd(&g_prof[10], (unsigned long long)npc);
-        atomicAdd(&g_prof[11], (unsigned long long)(nslot + 3 * nqw));
+        atomicAdd(&g_prof[11], (unsigned long long)(v.nslot + 3 * v.nqw));
+        atomicAdd(&g_prof[12], (unsigned long long)nslow);
+        atomicAdd(&g_prof[13], (unsigned long long)nx);
     }
 #endif
 }
 
+// One wave per tile (block b → item, XCD-major: the blocks of one XCD, b ≡ x mod 8, take a
+// contiguous range of items, so neighbouring windows meet in that XCD's L2).  Everything the
+// tile needs arrives by one LDS-DMA round trip after the scalar loads of its tile record.
 template <int NWP>
-int launch(const DenseArgs &a, int64_t n, int64_t lds, hipStream_t s) {
-    k_tile_dense<NWP><<<(unsigned)n, WGD, (unsigned)lds, s>>>(a);
+__global__ __launch_bounds__(WGD) void k_tile_dense(const DenseArgs d) {
+    extern __shared__ uint4 arena[];   // the window (S2C_DENSE_BYTES layout)
+    // one byte per position (row layout): '-' (D/N/P runs, '-' of SEQ unless maxdel drops
+    // the read's), 'N' of SEQ, '-' of SEQ (all: the planes count them as C, and 'N' as A)
+    __shared__ __attribute__((aligned(16))) uint32_t dcnt[8 * NWP], ncnt[8 * NWP], ccnt[8 * NWP];
+    __shared__ uint8_t amb[64];
+    const uint32_t lane = threadIdx.x, b = blockIdx.x;
+    const uint32_t x = b & 7u, per = d.n_items >> 3, rem = d.n_items & 7u;
+    const uint32_t item = x * per + min(x, rem) + (b >> 3);
+    const Win v = win_of(d, item);
+    uint8_t *const buf = (uint8_t *)arena;
+    win_issue(d, v, buf);
+    // with the DMA: the lane's piece records and its word's run-slot range
+    constexpr int G = WGD / NWP;
+    uint4 Pp[PFN];
+    uint32_t oe[PFN];
+#pragma unroll
+    for (int i = 0; i < PFN; i++) {
+        const uint32_t k = lane + WGD * i;
+        Pp[i] = make_uint4(0u, 0u, 0u, 0u);
+        oe[i] = 0;
+        if (k < v.npc) {
+            Pp[i] = ((const uint4 *)d.pc)[v.pf0 + k];
+            oe[i] = d.pc[4 * (size_t)(v.pf0 + k + 1) + 2];
+        }
+    }
+    const uint32_t w = lane / G, W = v.W0 + w, K = d.kwin;
+    uint32_t cw0 = 0, cw1 = 0;
+    if (w < v.nwords) {
+        cw0 = d.rs[W >= K ? W - K : 0u] - v.o0;
+        cw1 = d.rs[W + 1] - v.o0;
+    }
+    amb[lane] = c_amb[lane];
+    const uint32_t fill0 = uni((uint32_t)d.fill[0]);
+    for (uint32_t k = lane; k < 8 * NWP; k += WGD) {
+        dcnt[k] = 0;
+        ncnt[k] = 0;
+        ccnt[k] = 0;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the window landed
+    lds_sync();
+    dense_tile<NWP>(d, v, win_lds(d, v, buf), dcnt, ncnt, ccnt, amb, fill0, Pp, oe, cw0, cw1);
+}
+
+template <int NWP>
+int launch(const DenseArgs &a, int64_t n, hipStream_t s) {
+    k_tile_dense<NWP><<<(unsigned)n, WGD, a.buf_bytes, s>>>(a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? S2C_OK : s2c_set_error(S2C_ERR_HIP, std::string("k_tile_dense: ") + hipGetErrorString(e));
 }
@@ -552,6 +795,7 @@ int s2c_launch_dense(const s2c_dev *dv, hipStream_t st) {
     using namespace s2c;
     if (dv->n_dense <= 0) return S2C_OK;
     if (dv->fill_len != 1) return s2c_set_error(S2C_ERR_ARG, "dense tiles need a one-char fill");
+    if (dv->n_dense >= ((int64_t)1 << 31)) return s2c_set_error(S2C_ERR_LIMIT, "too many dense tiles");
     DenseArgs a;
     a.rs = dv->rs; a.pc = dv->pc; a.ops = dv->ops; a.bq = dv->bq; a.bx = dv->bx; a.tiles = dv->tiles; a.items = dv->dense;
     a.thresholds = dv->thresholds; a.tile_stats = dv->tile_stats; a.blk_len = dv->blk_len; a.out = dv->out;
@@ -559,14 +803,19 @@ int s2c_launch_dense(const s2c_dev *dv, hipStream_t st) {
     a.kwin = (uint32_t)dv->kwin; a.fill_nondash = (uint32_t)dv->fill_nondash;
     a.maxdel_active = dv->maxdel_active ? 1u : 0u;
     a.maxdel = dv->maxdel < 0 ? 0u : (uint32_t)dv->maxdel;
+    a.n_items = (uint32_t)dv->n_dense;
+    a.ops_end = dv->ops + dv->n_ops;
+    a.bq_end = dv->bq + 2 * dv->n_qwords;
+    a.bx_end = dv->bx + dv->n_qwords;
     a.n_thr = dv->n_thr; a.min_depth = dv->min_depth;
     a.fill = dv->fill;
     const int64_t n = dv->n_dense;
     // LDS: the largest window of the batch (S2C_DENSE_BYTES, host plan)
     const int64_t lds = dv->dense_lds;
-    if (lds <= 0 || lds > S2C_DENSE_LDS) return s2c_set_error(S2C_ERR_ARG, "dense_lds outside (0, S2C_DENSE_LDS]");
-    if (dv->tile_max <= 256) return launch<8>(a, n, lds, st);
-    if (dv->tile_max <= 512) return launch<16>(a, n, lds, st);
-    if (dv->tile_max <= 1024) return launch<32>(a, n, lds, st);
-    return launch<64>(a, n, lds, st);   // tile_max ≤ 2048 (host plan)
+    if (lds <= 0 || lds > S2C_DENSE_LDS || (lds & 15)) return s2c_set_error(S2C_ERR_ARG, "dense_lds outside (0, S2C_DENSE_LDS] or not 16-byte aligned");
+    a.buf_bytes = (uint32_t)lds;
+    if (dv->tile_max <= 256) return launch<8>(a, n, st);
+    if (dv->tile_max <= 512) return launch<16>(a, n, st);
+    if (dv->tile_max <= 1024) return launch<32>(a, n, st);
+    return launch<64>(a, n, st);   // tile_max ≤ 2048 (host plan)
 }

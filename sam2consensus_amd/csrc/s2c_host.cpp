@@ -646,6 +646,9 @@ extern "C" int s2c_parser_feed_file(s2c_parser *p, const char *path) {
 namespace {
 constexpr int64_t TP_MIN = 256, TP_MAX = 2048;      // tile bounds (positions)
 constexpr double E_TARGET = 262144.0;                // aligned bases per deep tile
+// LDS a shallow tile's window is planned to (one wave per tile: ~9 resident per CU; C5's
+// 30x gives 512-position tiles — measured faster than 1024 or 256, profiles/r02)
+constexpr double DENSE_PLAN_BYTES = 16384.0;
 constexpr uint32_t FLUSH_RECS = 248;                 // records per lane between counter flushes
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline int64_t align_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }
@@ -690,11 +693,11 @@ static void tile_window(const s2c_batch *b, int64_t K, uint64_t a, uint64_t e, u
 
 // LDS bytes k_tile_dense keeps a tile's window in (s2c_dense.hip), and whether it fits (with
 // query offsets of the window's base planes in 17 bits)
-static int64_t dense_bytes(const uint32_t *tw) {
+static int64_t dense_bytes(const uint32_t *tw, int64_t) {
     return S2C_DENSE_BYTES((int64_t)(tw[16] - tw[15]), (int64_t)(tw[18] - tw[17]));
 }
-static bool dense_fits(const uint32_t *tw) {
-    return dense_bytes(tw) <= S2C_DENSE_LDS && (int64_t)(tw[18] - tw[17]) <= S2C_DENSE_QW;
+static bool dense_fits(const uint32_t *tw, int64_t K) {
+    return dense_bytes(tw, K) <= S2C_DENSE_LDS && (int64_t)(tw[18] - tw[17]) <= S2C_DENSE_QW;
 }
 
 // PF_RUNS on the pieces a non-dense tile reads runs of (its window, its long pieces), and
@@ -944,6 +947,7 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
     std::vector<Tile> tiles;
     int64_t tile_max = S2C_POS_ALIGN;
     int64_t tile_force = 0;   // diagnostic override (S2C_TILE_POS, a multiple of 64 in [64, 2048])
+    const bool no_dense = getenv("S2C_NO_DENSE") != nullptr;   // diagnostic: every tile through k_tile
     if (const char *e = getenv("S2C_TILE_POS"))
         tile_force = align_up(std::min<int64_t>(std::max<int64_t>(atoll(e), 64), TP_MAX), S2C_POS_ALIGN);
     std::vector<int64_t> ref_slots(R, 0), ref_np(R, 0), ref_qw(R, 0);
@@ -965,9 +969,9 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
             // in LDS, plane words below S2C_DENSE_QW; with a margin for the depth's spread) fits
             // the dense kernel
             const double qpp = ((double)ref_qw[r] / 32.0 + 0.25 * (double)ref_np[r]) / (double)L;
-            const double bpp = (12.0 * (double)ref_slots[r] / (double)L) + 12.0 * qpp;
+            const double bpp = (20.0 * (double)ref_slots[r] / (double)L) + 12.0 * qpp;
             tp = TP_MAX;
-            while (tp > TP_MIN && (((double)tp + 32.0 * (double)(K + 1)) * bpp + 1024.0 > 0.75 * S2C_DENSE_LDS ||
+            while (tp > TP_MIN && (((double)tp + 32.0 * (double)(K + 1)) * bpp + 1024.0 > DENSE_PLAN_BYTES ||
                                    ((double)tp + 32.0 * (double)(K + 1)) * qpp > 0.8 * S2C_DENSE_QW))
                 tp /= 2;
         }
@@ -1048,7 +1052,7 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
         tile_window(b, K, T.a, T.b, tw);
         uint32_t fl = nch > 1 ? S2C_TILE_DEEP : 0u;
         if (nev[t] > S2C_EPI_KEYS || (int64_t)ccap[t] > lcols) fl |= S2C_TILE_GENERAL;
-        if (fl == 0 && nev[t] == 0 && nlg == 0 && maxc <= 255 && dense_fits(tw)) fl = S2C_TILE_DENSE;
+        if (fl == 0 && nev[t] == 0 && nlg == 0 && maxc <= 255 && !no_dense && dense_fits(tw, K)) fl = S2C_TILE_DENSE;
         const uint32_t bcap = nshort[t] ? pow2_at_least(2 * (uint64_t)nshort[t]) : 0u;
         tw[0] = (uint32_t)T.a; tw[1] = (uint32_t)T.b; tw[2] = (uint32_t)T.ref; tw[3] = fl;
         tw[4] = (uint32_t)boff; tw[5] = bcap; tw[6] = (uint32_t)loff; tw[7] = nlong[t];
@@ -1058,7 +1062,7 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
         loff += nlong[t];
         coff += ccap[t];
         if (fl == S2C_TILE_DENSE) {
-            I.dense_lds = std::max<int64_t>(I.dense_lds, dense_bytes(tw));
+            I.dense_lds = std::max<int64_t>(I.dense_lds, dense_bytes(tw, K));
             const uint32_t it[S2C_ITEM_WORDS] = {(uint32_t)t, 0u, 0u, 0u};
             b->dense.insert(b->dense.end(), it, it + S2C_ITEM_WORDS);
         } else {
@@ -1238,8 +1242,8 @@ extern "C" int s2c_batch_shard(const s2c_batch *b, int64_t t0, int64_t t1, s2c_b
         uint32_t *tw = &s->tiles[(size_t)t * S2C_TILE_WORDS];
         tile_window(s.get(), K, tw[0], tw[1], tw);
         if (!(tw[3] & S2C_TILE_DENSE)) continue;
-        if (!dense_fits(tw)) return s2c_set_error(S2C_ERR_LIMIT, "shard window beyond the dense kernel's LDS");
-        J.dense_lds = std::max<int64_t>(J.dense_lds, dense_bytes(tw));
+        if (!dense_fits(tw, K)) return s2c_set_error(S2C_ERR_LIMIT, "shard window beyond the dense kernel's LDS");
+        J.dense_lds = std::max<int64_t>(J.dense_lds, dense_bytes(tw, K));
     }
     mark_runs(s.get());
     // the shard's share of the workload's aligned bases (by its positions; for reporting)
