@@ -242,30 +242,33 @@ __device__ __forceinline__ void cnt_range(uint32_t *cnt, int32_t r0, int32_t r1,
 
 // The non-ACGT chars of SEQ in a run of bases (window-relative query bases [q, q + l), tile-
 // relative position r0 of q): 'N' (p0 0) into ncnt, '-' (p0 1) into ccnt and, unless maxdel
-// drops the read's '-', into dcnt.  The run's x-plane words are read 4 at a time (one LDS
-// round trip), the base planes only of words holding such chars.
+// drops the read's '-', into dcnt.  Eight x-plane and base-plane words per round trip.
 __device__ __forceinline__ void x_events(const uint32_t *bxl, const uint2 *bql, uint32_t q, uint32_t l, int32_t r0,
                                          int32_t lim, bool drop, uint32_t *dcnt, uint32_t *ncnt, uint32_t *ccnt) {
     const uint32_t wa = q >> 5, wb = (q + l - 1) >> 5;
-    for (uint32_t w0 = wa; w0 <= wb; w0 += 4) {
-        uint32_t xs[4];
+    for (uint32_t w0 = wa; w0 <= wb; w0 += 8) {
+        uint32_t xs[8];
+        uint2 ps[8];
 #pragma unroll
-        for (int u = 0; u < 4; u++) xs[u] = bxl[min(w0 + u, wb)];
+        for (int u = 0; u < 8; u++) {
+            const uint32_t qw = min(w0 + u, wb);
+            xs[u] = bxl[qw];
+            ps[u] = bql[qw];
+        }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < 8; u++) {
             const uint32_t qw = w0 + u;
             const int32_t b0 = (int32_t)(32 * qw) - (int32_t)q;   // run offset of the word's bit 0
             uint32_t xm = qw <= wb ? xs[u] : 0u;
             if (b0 < 0) xm &= 0xFFFFFFFFu << (uint32_t)(-b0);
             if (b0 + 32 > (int32_t)l) xm &= 0xFFFFFFFFu >> (uint32_t)(b0 + 32 - (int32_t)l);
-            if (!xm) continue;
-            const uint2 pp = bql[qw];
+            xm &= ~ps[u].y;   // (p1 = 0 for every non-ACGT char)
             while (xm) {
                 const uint32_t bit = (uint32_t)__builtin_ctz(xm);
                 xm &= xm - 1;
                 const int32_t r = r0 + b0 + (int32_t)bit;
-                if (r < 0 || r >= lim || ((pp.y >> bit) & 1u)) continue;
-                if ((pp.x >> bit) & 1u) {
+                if (r < 0 || r >= lim) continue;
+                if ((ps[u].x >> bit) & 1u) {
                     cnt_add1(ccnt, (uint32_t)r);
                     if (!drop) cnt_add1(dcnt, (uint32_t)r);
                 } else {
@@ -329,7 +332,7 @@ struct WinLds {
     const uint32_t *opl, *bxl;
     const uint2 *bql;
     uint2 *runl;
-    uint32_t *slowq, *xq;
+    uint2 *q;   // [nslot]: queued pieces {k, 0} from the front, X runs {q | len << 17, r0} from the back
 };
 __device__ __forceinline__ const uint32_t *phase16(const uint8_t *region, const void *src) {
     return (const uint32_t *)(region + ((uintptr_t)src & 15));
@@ -344,8 +347,7 @@ __device__ __forceinline__ WinLds win_lds(const DenseArgs &d, const Win &v, uint
     L.bxl = phase16(buf, sbx);
     buf += dma16_bytes(v.nqw);
     L.runl = (uint2 *)buf;
-    L.slowq = (uint32_t *)(L.runl + v.nslot);
-    L.xq = L.slowq + v.nslot;
+    L.q = L.runl + v.nslot;
     return L;
 }
 // issue the LDS-DMA of window v into buf (completion: s_waitcnt vmcnt(0))
@@ -378,8 +380,8 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     const uint32_t pf0 = v.pf0;
     const uint32_t *opl = L.opl, *bxl = L.bxl;
     const uint2 *bql = L.bql;
-    uint2 *runl = L.runl;
-    uint32_t *slowq = L.slowq, *xq = L.xq;
+    uint2 *runl = L.runl, *queue = L.q;
+    const uint32_t qcap = v.nslot;
     PROF_MARK(1);
 
     // ---- walk: one lane per piece → run records {gpos, (query base − 32·qw0) << 15 | len << 4
@@ -388,10 +390,13 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     const bool mda = d.maxdel_active != 0;
     uint32_t nslow = 0, nx = 0;   // queue lengths (uniform)
     const uint32_t nit = ABL(4) ? 0u : (npc + WGD - 1) / WGD;
+    uint32_t opw[PFN];   // the pieces' first op words, read together
+#pragma unroll
+    for (int u = 0; u < PFN; u++) opw[u] = (lane + WGD * u < npc) ? opl[Pp[u].z - o0] : 0u;
     for (uint32_t it = 0; it < nit; it++) {
         const uint32_t k = lane + WGD * it;
         uint4 P = Pp[0];
-        uint32_t oend = oe[0];
+        uint32_t oend = oe[0], w0 = opw[0];
 #pragma unroll
         for (int u = 1; u < PFN; u++) {   // (the loaded records by a select chain)
             P.x = it == (uint32_t)u ? Pp[u].x : P.x;
@@ -399,51 +404,73 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             P.z = it == (uint32_t)u ? Pp[u].z : P.z;
             P.w = it == (uint32_t)u ? Pp[u].w : P.w;
             oend = it == (uint32_t)u ? oe[u] : oend;
+            w0 = it == (uint32_t)u ? opw[u] : w0;
         }
         const bool in = k < npc;
         if (it >= (uint32_t)PFN && in) {   // (windows of more than 256 pieces)
             P = ((const uint4 *)d.pc)[pf0 + k];
             oend = d.pc[4 * (size_t)(pf0 + k + 1) + 2];
+            w0 = opl[P.z - o0];
         }
         const uint32_t fl = P.w >> 24, slen = P.w & 0xFFFFFFu, j = P.z - o0;
-        const uint32_t w0 = in ? opl[j] : 0u, op = w0 & 15u, l = w0 >> 4;
+        const uint32_t op = w0 & 15u, l = w0 >> 4;
         const bool xf = (fl & S2C_PF_X) != 0;
         // one M / = / X token and nothing else: seqout = SEQ[0 : min(l, len(SEQ))] (:64-69)
         const bool fast = in && oend - P.z == 1u && (fl & ~(uint32_t)S2C_PF_X) == 0u && op_bases(op) && !(xf && mda);
-        if (fast) {
-            const uint32_t take = min(l, slen), q = 16u * (P.y - 2u * qw0);
-            runl[j] = make_uint2(P.x, (q << 15) | (take << 4) | S2C_RUN_BASES | (xf ? S2C_RUN_XBIT : 0u));
-        }
+        const uint32_t take = min(l, slen), q = 16u * (P.y - 2u * qw0);
+        if (fast) runl[j] = make_uint2(P.x, (q << 15) | (take << 4) | S2C_RUN_BASES | (xf ? S2C_RUN_XBIT : 0u));
         const uint64_t bs = __ballot(in && !fast), bxm = __ballot(fast && xf);
-        if (in && !fast) slowq[nslow + mbcnt(bs)] = k;
-        if (fast && xf) xq[nx + mbcnt(bxm)] = j;
+        if (in && !fast) queue[nslow + mbcnt(bs)] = make_uint2(k, 0u);
+        if (fast && xf) queue[qcap - 1u - nx - mbcnt(bxm)] = make_uint2(q | (take << 17), (uint32_t)((int32_t)P.x - T0));
         nslow += (uint32_t)__popcll(bs);
         nx += (uint32_t)__popcll(bxm);
     }
     lds_sync();
-    // queued pieces: the general walk; '-' runs and SEQ N / '-' straight into the byte counters
-    for (uint32_t i = lane; i < nslow; i += WGD) {
-        const uint32_t k = slowq[i];
-        const uint4 P = ((const uint4 *)d.pc)[pf0 + k];
-        const uint32_t oend = d.pc[4 * (size_t)(pf0 + k + 1) + 2];
-        const bool lng = ((P.w >> 24) & S2C_PF_LONG) != 0;   // (a long piece starting here does not overlap the tile)
-        walk_window(opl, bql, bxl, P, P.z - o0, oend - o0, 16u * (P.y - 2u * qw0), mda, d.maxdel,
-                    [&](uint32_t j, uint32_t gp, uint32_t l, uint32_t kind, uint32_t q) {
-                        const uint32_t kd = (lng || kind == S2C_RUN_EMPTY) ? 0u : (kind & 3u);
-                        runl[j] = kd == S2C_RUN_BASES ? make_uint2(gp, (q << 15) | (l << 4) | kind) : make_uint2(0u, 0u);
-                        const int32_t r0 = (int32_t)gp - T0;
-                        if (kd == S2C_RUN_DASH) cnt_range(dcnt, r0, r0 + (int32_t)l, TL);
-                        if (kd == S2C_RUN_BASES && (kind & S2C_RUN_XBIT))
-                            x_events(bxl, bql, q, l, r0, TL, (kind & S2C_RUN_DROP) != 0, dcnt, ncnt, ccnt);
-                    });
+    PROF_MARK(2);
+    // queued pieces: the general walk; '-' runs and SEQ N / '-' straight into the byte counters.
+    // A queued piece's record comes from the lane that loaded it (ds_bpermute, all lanes on).
+    for (uint32_t base = 0; base < nslow; base += WGD) {
+        const uint32_t i = base + lane;
+        const uint32_t k = i < nslow ? queue[i].x : 0u, it = k / WGD;
+        const int src = (int)(4 * (k % WGD));
+        uint4 P = make_uint4(0u, 0u, 0u, 0u);
+        uint32_t oend = 0;
+#pragma unroll
+        for (int u = 0; u < PFN; u++) {
+            const uint32_t px = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)Pp[u].x);
+            const uint32_t py = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)Pp[u].y);
+            const uint32_t pz = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)Pp[u].z);
+            const uint32_t pw = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)Pp[u].w);
+            const uint32_t pe = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)oe[u]);
+            const bool me = it == (uint32_t)u;
+            P = me ? make_uint4(px, py, pz, pw) : P;
+            oend = me ? pe : oend;
+        }
+        if (i < nslow) {
+            if (it >= (uint32_t)PFN) {   // (windows of more than 256 pieces)
+                P = ((const uint4 *)d.pc)[pf0 + k];
+                oend = d.pc[4 * (size_t)(pf0 + k + 1) + 2];
+            }
+            const bool lng = ((P.w >> 24) & S2C_PF_LONG) != 0;   // (a long piece starting here does not overlap the tile)
+            walk_window(opl, bql, bxl, P, P.z - o0, oend - o0, 16u * (P.y - 2u * qw0), mda, d.maxdel,
+                        [&](uint32_t j, uint32_t gp, uint32_t l, uint32_t kind, uint32_t q) {
+                            const uint32_t kd = (lng || kind == S2C_RUN_EMPTY) ? 0u : (kind & 3u);
+                            runl[j] = kd == S2C_RUN_BASES ? make_uint2(gp, (q << 15) | (l << 4) | kind) : make_uint2(0u, 0u);
+                            const int32_t r0 = (int32_t)gp - T0;
+                            if (kd == S2C_RUN_DASH) cnt_range(dcnt, r0, r0 + (int32_t)l, TL);
+                            if (kd == S2C_RUN_BASES && (kind & S2C_RUN_XBIT))
+                                x_events(bxl, bql, q, l, r0, TL, (kind & S2C_RUN_DROP) != 0, dcnt, ncnt, ccnt);
+                        });
+        }
     }
+    PROF_MARK(3);
     // queued single-token runs of reads with N / '-' in SEQ (never dropped: maxdel is off)
     for (uint32_t i = lane; i < nx; i += WGD) {
-        const uint2 rv = runl[xq[i]];
-        x_events(bxl, bql, rv.y >> 15, (rv.y >> 4) & 0x7FFu, (int32_t)rv.x - T0, TL, false, dcnt, ncnt, ccnt);
+        const uint2 e = queue[qcap - 1u - i];
+        x_events(bxl, bql, e.x & 0x1FFFFu, e.x >> 17, (int32_t)e.y, TL, false, dcnt, ncnt, ccnt);
     }
     lds_sync();
-    PROF_MARK(2);
+    PROF_MARK(4);
 
     // ---- count the base records of this lane's word (candidates cw0 + g + G·m < cw1),
     //      bit-sliced by the planes (non-ACGT chars of SEQ as A / C: taken back in the vote), a
@@ -503,7 +530,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             }
         }
     }
-    PROF_MARK(3);
+    PROF_MARK(5);
     // ---- counters → byte counts: R[r] byte j = count of position 8j + r
 #pragma unroll
     for (int c = 0; c < 4; c++) transpose8(C[c]);
@@ -538,7 +565,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             rT[rr] = mine ? C[2][k * RPL + rr] : rT[rr];
         }
     }
-    PROF_MARK(4);
+    PROF_MARK(6);
 
     // ---- vote of this lane's rows: row rr = word positions 8j + g·RPL + rr (j = 0..3)
     const uint32_t rbase = 8 * w + g * RPL;   // the rows' dword index in the byte counters
@@ -706,7 +733,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             d.blk_len[jt] = n;
         }
     }
-    PROF_MARK(5);
+    PROF_MARK(7);
 #ifdef S2C_PROF
     if (threadIdx.x == 0 && (blockIdx.x & 63) == 0) {
         atomicAdd(&g_prof[8], 1ull);

@@ -28,6 +28,30 @@
 int s2c_launch_reads(const s2c_dev *d, hipStream_t s, bool all);
 int s2c_launch_dense(const s2c_dev *d, hipStream_t s);
 
+#ifdef S2C_PROF
+// phase clocks of k_tile (diagnostic build `make prof`, scripts/prof_tile.py): Σ over sampled
+// workgroups (one in 16, wave 0) of the s_memtime deltas of each phase; [15] = workgroups
+__device__ unsigned long long g_tprof[16];
+#define TPROF_MARK(i)                                                                                 \
+    do {                                                                                              \
+        const unsigned long long _t = __builtin_amdgcn_s_memtime();                                   \
+        if (threadIdx.x == 0 && (blockIdx.x & 15) == 0 && (i) > 0) atomicAdd(&g_tprof[(i)-1], _t - tprof_t); \
+        tprof_t = _t;                                                                                 \
+    } while (0)
+extern "C" int s2c_prof_tile(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tprof), sizeof(g_tprof)) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long z[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_tprof), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#else
+#define TPROF_MARK(i) \
+    do {              \
+    } while (0)
+#endif
+
 namespace s2c {
 namespace {
 
@@ -610,7 +634,7 @@ constexpr int GS = 8;   // records per counting group
 constexpr uint32_t OOR = 0xF0000000u;
 
 template <int NWP>
-__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_tile(const TileArgs d, const uint32_t *items) {
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(3))) void k_tile(const TileArgs d, const uint32_t *items) {
     constexpr int G = WG / NWP, HP = 17 * NWP;
     using H = Hist<NWP>;
     constexpr uint32_t ICOL = S2C_LDS_COLS(NWP);
@@ -619,6 +643,10 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     __shared__ FastLds<ICOL> L;
     const uint32_t tid = threadIdx.x;
     const uint32_t w = tid / G, g = tid % G;
+#ifdef S2C_PROF
+    unsigned long long tprof_t = 0;
+#endif
+    TPROF_MARK(0);
     if (tid < 64) L.amb[tid] = c_amb[tid];
     const uint4 itv = ((const uint4 *)items)[blockIdx.x];
     const uint32_t tile = uni(itv.x), chunk = uni(itv.y);
@@ -662,7 +690,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
     if (finish && tid < (uint32_t)min(d.fill_len, FILL_LDS)) L.fill[tid] = d.fill[tid];
     lds_sync();
     InsLayout il = {0, 0};
+    TPROF_MARK(1);
     if (has_ins) il = build_layout<PF, false>(d, T, tile, L.bits, L.wrank, L.klen, L.key, cols, L.colkey, L.scan);
+    TPROF_MARK(2);
     if (counts_only && T.nev > 0 && chunk == 0) {   // no vote: leave the tile's tables zero for the next run
         for (uint32_t e = tid; e < T.bcap; e += WG) ((uint4 *)d.ibkt)[T.boff + e] = make_uint4(0, 0, 0, 0);
         if (tid == 0) d.ilong_n[tile] = 0;
@@ -747,6 +777,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
         close8(V[2], t2);
         close8(V[3], t3);
     }
+    TPROF_MARK(3);
     nmax_rec = nrec;
     // ---- long-piece records (rare): one at a time
     {
@@ -772,6 +803,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
             nmax_rec++;
         }
     }
+    TPROF_MARK(4);
     // ---- flush: counters → symbol counts → LDS histogram
     {
         transpose8(V[0]);
@@ -822,6 +854,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
         }
     }
     lds_sync();
+    TPROF_MARK(5);
     if (finish) {
         tile_epilogue_fast<NWP>(d, tile, T, il, hist, cols, L);
     } else {
@@ -839,6 +872,13 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 }
             }
     }
+    TPROF_MARK(6);
+#ifdef S2C_PROF
+    if (threadIdx.x == 0 && (blockIdx.x & 15) == 0) {
+        atomicAdd(&g_tprof[15], 1ull);
+        atomicAdd(&g_tprof[14], (unsigned long long)ngrp);
+    }
+#endif
 }
 
 // ======================================================================= k_prep / k_consensus

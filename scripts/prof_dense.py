@@ -25,7 +25,7 @@ f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 abl = _lib.lib.s2c_prof_ablate
 abl.argtypes = [C.c_uint32]
 buf = (C.c_ulonglong * 16)()
-names = ["dma+first loads", "walk", "count", "fixup+transpose", "vote+store"]
+names = ["setup", "walk fast", "walk slow", "walk N/-", "count", "fixup+transpose", "vote+store"]
 bits_list = [int(b) for b in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0]
 for bits in bits_list:
     abl(bits)
@@ -41,10 +41,10 @@ for bits in bits_list:
     torch.cuda.synchronize()
     f(buf, 0)
     waves = max(buf[8], 1)
-    tot = sum(buf[i] for i in range(5))
+    tot = sum(buf[i] for i in range(len(names)))
     print("ablate %d (1 events, 2 count, 4 walk, 8 vote): step %.3f ms" % (bits, ev0.elapsed_time(ev1) / N))
     for i, nm in enumerate(names):
         print("  %-18s %9.0f cyc/wave  %5.1f%%" % (nm, buf[i] / waves, 100.0 * buf[i] / max(tot, 1)))
-    print("  groups/wave %.1f pieces/wave %.1f staged dwords/wave %.0f" % (buf[9] / waves, buf[10] / waves,
-                                                                         buf[11] / waves), flush=True)
+    print("  groups/wave %.1f pieces/wave %.1f staged dwords/wave %.0f slow/wave %.2f xq/wave %.2f" % (
+        buf[9] / waves, buf[10] / waves, buf[11] / waves, buf[12] / waves, buf[13] / waves), flush=True)
 abl(0)
