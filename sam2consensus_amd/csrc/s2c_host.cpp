@@ -26,6 +26,8 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <condition_variable>
+#include <mutex>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -609,37 +611,83 @@ extern "C" int s2c_parser_feed_file(s2c_parser *p, const char *path) {
         rd.f = fopen(path, "rb");
         if (!rd.f) return s2c_set_error(S2C_ERR_IO, std::string("cannot open ") + path);
     }
-    std::vector<char> buf(WIN + (1 << 20));
-    size_t have = 0;
-    if (!p->carry.empty()) {   // a partial line from s2c_parser_feed continues here
-        have = p->carry.size();
-        if (have > buf.size() / 2) buf.resize(2 * have + WIN);
-        memcpy(buf.data(), p->carry.data(), have);
-        p->carry.clear();
-    }
-    for (;;) {
-        if (buf.size() - have < WIN / 2) buf.resize(buf.size() + WIN);   // a line longer than a window
-        const long r = rd.read(buf.data() + have, buf.size() - have);
-        if (r < 0) return perr(p, S2C_ERR_IO, "gzip read error");
-        have += (size_t)r;
-        const bool eof = r == 0;
-        size_t cut = have;
-        if (!eof) {
-            const char *nl = nullptr;
-            for (size_t k = have; k > 0; k--)
-                if (buf[k - 1] == '\n') { nl = &buf[k - 1]; break; }
-            if (!nl) continue;   // no complete line yet: read more
-            cut = (size_t)(nl - buf.data()) + 1;
+    // A reader thread inflates / reads window k + 1 while the workers parse window k (two
+    // buffers).  The reader cuts each window after its last '\n' and carries the partial
+    // line into the next one.
+    struct Slot {
+        std::vector<char> buf;
+        size_t len = 0;
+        bool full = false, eof = false, err = false;
+    };
+    Slot slots[2];
+    std::mutex m;
+    std::condition_variable cv;
+    bool stop = false;
+    std::vector<char> tail(p->carry.begin(), p->carry.end());   // a partial line from s2c_parser_feed
+    p->carry.clear();
+    std::thread reader([&] {
+        for (int k = 0;; k ^= 1) {
+            Slot &sl = slots[k];
+            {
+                std::unique_lock<std::mutex> lk(m);
+                cv.wait(lk, [&] { return !sl.full || stop; });
+                if (stop) return;
+            }
+            std::vector<char> &buf = sl.buf;
+            if (buf.size() < tail.size() + WIN) buf.resize(tail.size() + WIN + (1 << 20));
+            memcpy(buf.data(), tail.data(), tail.size());
+            size_t have = tail.size(), cut = 0;
+            bool eof = false, err = false;
+            for (;;) {
+                if (buf.size() - have < WIN / 2) buf.resize(buf.size() + WIN);   // a line longer than a window
+                const long r = rd.read(buf.data() + have, buf.size() - have);
+                if (r < 0) { err = true; break; }
+                have += (size_t)r;
+                if (r == 0) { eof = true; cut = have; break; }
+                size_t k2 = have;
+                while (k2 > 0 && buf[k2 - 1] != '\n') k2--;
+                if (k2) { cut = k2; break; }   // else: no complete line yet, read more
+            }
+            tail.assign(buf.data() + cut, buf.data() + have);
+            {
+                std::lock_guard<std::mutex> lk(m);
+                sl.len = cut;
+                sl.eof = eof;
+                sl.err = err;
+                sl.full = true;
+            }
+            cv.notify_all();
+            if (eof || err) return;
         }
-        if (cut) {
-            int rc = parse_window(p, buf.data(), cut);
-            if (rc) return rc;
+    });
+    int rc = S2C_OK;
+    for (int k = 0;; k ^= 1) {
+        Slot &sl = slots[k];
+        {
+            std::unique_lock<std::mutex> lk(m);
+            cv.wait(lk, [&] { return sl.full; });
         }
-        memmove(buf.data(), buf.data() + cut, have - cut);
-        have -= cut;
-        if (eof) break;
+        if (sl.err) {
+            rc = perr(p, S2C_ERR_IO, "gzip read error");
+            break;
+        }
+        if (sl.len) rc = parse_window(p, sl.buf.data(), sl.len);
+        const bool eof = sl.eof;
+        {
+            std::lock_guard<std::mutex> lk(m);
+            sl.full = false;
+            if (rc) stop = true;
+        }
+        cv.notify_all();
+        if (rc || eof) break;
     }
-    return S2C_OK;
+    {
+        std::lock_guard<std::mutex> lk(m);
+        stop = true;
+    }
+    cv.notify_all();
+    reader.join();
+    return rc;
 }
 
 // ------------------------------------------------------------------ finish: layout + plan
