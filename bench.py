@@ -52,16 +52,17 @@ def b_alg(info, T):
     step    = 0.5·Q + 16·N + 4·K + (48+T)·L + Σ_ins(8 + 0.5·len)  (SURVEY's formula: 4-bit
               query bases, 16 B per read, 4 B per CIGAR op, the count tensor written + read
               once, T vote bytes per position, the insertion events)
-    k_reads = 16·N + 4·K            (read records + CIGAR ops in; the walk's inputs)
-    tile    = step − 16·N − 4·K − 48·L  (query bases in, vote bytes out, insertion events:
-              the tile kernels keep the counts in registers / LDS, so no count bytes are
-              charged to them; deep tiles, none in C5, would add 24·L)"""
+    pileup  = step − 48·L, less 16·N + 4·K when no tile is dense: the tile kernels keep the
+              counts in registers / LDS (never the count tensor); the dense kernel walks its
+              pieces' records and CIGAR ops itself (k_reads then only walks the pieces of
+              non-dense tiles: C5 0.2 %), otherwise k_reads walks every piece
+    reads   = the rest of the step (16·N + 4·K without dense tiles, else ≈ 0)"""
     Q, N, K, L = info.query_bases, info.reads_mapped, info.n_tokens, info.total_len
     ins = 8 * info.n_ins + 0.5 * info.n_ins_bases
     step = 0.5 * Q + 16 * N + 4 * K + (48 + T) * L + ins
-    reads = 16 * N + 4 * K
-    return step, reads, step - reads - 48 * L
-
+    walk = 16 * N + 4 * K
+    pile = step - 48 * L - (0 if info.n_dense > 0 else walk)
+    return step, step - 48 * L - pile, pile
 
 def cpu_baseline(workload, scale):
     """Time the oracle (pure-Python restatement of the reference, 1 core) on a bounded sample."""
@@ -289,7 +290,8 @@ def main():
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic.get("bytes") if traffic else None,
                 "traffic_frac": (traffic["bytes"] / (tile_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS) if traffic else None,
-                "kernel": "k_tile_dense / k_tile (pileup of the runs + insertion columns + vote + FASTA bytes)",
+                "kernel": "s2c_pileup = k_tile_dense + k_tile (CIGAR walk of dense tiles, pileup, insertion "
+                          "columns, vote, FASTA bytes); time from HIP events around the stage in every timed step",
                 "kernel_ms": tile_ms, "alg_bytes_per_launch": tile_bytes * per_rank,
                 "traffic_source": traffic.get("source") if traffic else None}
             line["kernels_ms"] = kern

@@ -38,13 +38,15 @@ def main():
         f_raw, w_raw = fetch.get(k, 0.0), write.get(k, 0.0)
         kernels[k] = {"fetch_kib_raw": f_raw, "write_kib_raw": w_raw,
                       "hbm_bytes_per_launch": (2.0 * f_raw + w_raw) * 1024.0}
-    pile = [v for k, v in kernels.items() if k.startswith("k_pileup")]
+    # the pileup stage of one step: k_tile_dense + k_tile (+ k_prep), summed per launch
+    pile = sum(v["hbm_bytes_per_launch"] for k, v in kernels.items()
+               if k.split("<")[0] in ("s2c::k_tile_dense", "s2c::k_tile", "s2c::k_prep"))
     out = {"workload": wl, "round": tag, "kernels": kernels,
-           "k_pileup_hbm_bytes_per_launch": pile[0]["hbm_bytes_per_launch"] if pile else None,
+           "tile_hbm_bytes_per_launch": pile or None,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (scripts/pmc.sh); "
                      "bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 per dispatch, averaged; the x2 is the gfx950 "
                      "read correction of MI355X_MICROARCH.md; WRITE_SIZE is uncalibrated for byte stores/atomics. "
-                     "The C2 batch (~90 MB) fits the 256 MiB Infinity Cache, whose hits these counters include."}
+                     "Infinity Cache hits are included (a batch below 256 MiB, e.g. C2, is largely served from it)."}
     dst = os.path.join(ROOT, "profiles", "traffic_%s.json" % wl)
     with open(dst, "w") as fh:
         json.dump(out, fh, indent=1)
