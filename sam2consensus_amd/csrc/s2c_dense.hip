@@ -70,7 +70,7 @@ struct DenseArgs {
     uint64_t *tile_stats, *blk_len;
     uint8_t *out;
     uint32_t padded_len, n_cols, n_tiles, kwin, fill_nondash, maxdel_active, maxdel, n_items;
-    const void *ops_end, *bq_end, *bx_end;   // ends of the DMA sources
+    const void *ops_end, *bq_end;   // ends of the DMA sources
     uint32_t buf_bytes;                                        // the window's LDS (16-byte multiple)
     int32_t n_thr, min_depth;
     const uint8_t *fill;   // the one -f char
@@ -329,25 +329,23 @@ __device__ __forceinline__ Win win_of(const DenseArgs &d, uint32_t item) {
 // The window's arrays in LDS (S2C_DENSE_BYTES layout): op words, planes, non-ACGT plane
 // (each at its source's 16-byte phase, dma16), run records, the walk's two queues.
 struct WinLds {
-    const uint32_t *opl, *bxl;
+    const uint32_t *opl;
     const uint2 *bql;
     uint2 *runl;
-    uint2 *q;   // [nslot]: queued pieces {k, 0} from the front, X runs {q | len << 17, r0} from the back
+    uint32_t *q;   // [nslot]: queued pieces (window index) from the front, X-run slots from the back
 };
 __device__ __forceinline__ const uint32_t *phase16(const uint8_t *region, const void *src) {
     return (const uint32_t *)(region + ((uintptr_t)src & 15));
 }
 __device__ __forceinline__ WinLds win_lds(const DenseArgs &d, const Win &v, uint8_t *buf) {
     WinLds L;
-    const uint32_t *sop = d.ops + v.o0, *sbq = d.bq + 2 * (size_t)v.qw0, *sbx = d.bx + v.qw0;
+    const uint32_t *sop = d.ops + v.o0, *sbq = d.bq + 2 * (size_t)v.qw0;
     L.opl = phase16(buf, sop);
     buf += dma16_bytes(v.nslot);
     L.bql = (const uint2 *)phase16(buf, sbq);
     buf += dma16_bytes(2 * v.nqw);
-    L.bxl = phase16(buf, sbx);
-    buf += dma16_bytes(v.nqw);
     L.runl = (uint2 *)buf;
-    L.q = L.runl + v.nslot;
+    L.q = (uint32_t *)(L.runl + v.nslot);
     return L;
 }
 // issue the LDS-DMA of window v into buf (completion: s_waitcnt vmcnt(0))
@@ -355,8 +353,6 @@ __device__ __forceinline__ void win_issue(const DenseArgs &d, const Win &v, uint
     dma16(buf, d.ops + v.o0, v.nslot, d.ops_end);
     buf += dma16_bytes(v.nslot);
     dma16(buf, d.bq + 2 * (size_t)v.qw0, 2 * v.nqw, d.bq_end);
-    buf += dma16_bytes(2 * v.nqw);
-    dma16(buf, d.bx + v.qw0, v.nqw, d.bx_end);
 }
 
 // One tile of NWP words from its window in LDS; G = 64 / NWP lanes per word, RPL = 8 / G
@@ -378,9 +374,12 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     const bool active = w < nwords;
     const uint32_t K = d.kwin;
     const uint32_t pf0 = v.pf0;
-    const uint32_t *opl = L.opl, *bxl = L.bxl;
+    // the non-ACGT plane stays in HBM (read only for the ~14 % of runs with N / '-' in SEQ, in
+    // one round trip per queue pass); window-relative word index as for the planes
+    const uint32_t *opl = L.opl, *bxl = d.bx + qw0;
     const uint2 *bql = L.bql;
-    uint2 *runl = L.runl, *queue = L.q;
+    uint2 *runl = L.runl;
+    uint32_t *queue = L.q;
     const uint32_t qcap = v.nslot;
     PROF_MARK(1);
 
@@ -420,8 +419,8 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         const uint32_t take = min(l, slen), q = 16u * (P.y - 2u * qw0);
         if (fast) runl[j] = make_uint2(P.x, (q << 15) | (take << 4) | S2C_RUN_BASES | (xf ? S2C_RUN_XBIT : 0u));
         const uint64_t bs = __ballot(in && !fast), bxm = __ballot(fast && xf);
-        if (in && !fast) queue[nslow + mbcnt(bs)] = make_uint2(k, 0u);
-        if (fast && xf) queue[qcap - 1u - nx - mbcnt(bxm)] = make_uint2(q | (take << 17), (uint32_t)((int32_t)P.x - T0));
+        if (in && !fast) queue[nslow + mbcnt(bs)] = k;
+        if (fast && xf) queue[qcap - 1u - nx - mbcnt(bxm)] = j;
         nslow += (uint32_t)__popcll(bs);
         nx += (uint32_t)__popcll(bxm);
     }
@@ -431,7 +430,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     // A queued piece's record comes from the lane that loaded it (ds_bpermute, all lanes on).
     for (uint32_t base = 0; base < nslow; base += WGD) {
         const uint32_t i = base + lane;
-        const uint32_t k = i < nslow ? queue[i].x : 0u, it = k / WGD;
+        const uint32_t k = i < nslow ? queue[i] : 0u, it = k / WGD;
         const int src = (int)(4 * (k % WGD));
         uint4 P = make_uint4(0u, 0u, 0u, 0u);
         uint32_t oend = 0;
@@ -466,8 +465,8 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     PROF_MARK(3);
     // queued single-token runs of reads with N / '-' in SEQ (never dropped: maxdel is off)
     for (uint32_t i = lane; i < nx; i += WGD) {
-        const uint2 e = queue[qcap - 1u - i];
-        x_events(bxl, bql, e.x & 0x1FFFFu, e.x >> 17, (int32_t)e.y, TL, false, dcnt, ncnt, ccnt);
+        const uint2 rv = runl[queue[qcap - 1u - i]];
+        x_events(bxl, bql, rv.y >> 15, (rv.y >> 4) & 0x7FFu, (int32_t)rv.x - T0, TL, false, dcnt, ncnt, ccnt);
     }
     lds_sync();
     PROF_MARK(4);
@@ -833,7 +832,6 @@ int s2c_launch_dense(const s2c_dev *dv, hipStream_t st) {
     a.n_items = (uint32_t)dv->n_dense;
     a.ops_end = dv->ops + dv->n_ops;
     a.bq_end = dv->bq + 2 * dv->n_qwords;
-    a.bx_end = dv->bx + dv->n_qwords;
     a.n_thr = dv->n_thr; a.min_depth = dv->min_depth;
     a.fill = dv->fill;
     const int64_t n = dv->n_dense;

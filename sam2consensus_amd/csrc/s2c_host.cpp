@@ -694,8 +694,8 @@ extern "C" int s2c_parser_feed_file(s2c_parser *p, const char *path) {
 namespace {
 constexpr int64_t TP_MIN = 256, TP_MAX = 2048;      // tile bounds (positions)
 constexpr double E_TARGET = 262144.0;                // aligned bases per deep tile
-// LDS a shallow tile's window is planned to (one wave per tile: ~9 resident per CU; C5's
-// 30x gives 512-position tiles — measured faster than 1024 or 256, profiles/r02)
+// LDS a shallow tile's window is planned to (one wave per tile, ~10 resident per CU; C5's
+// 30x gives 1024-position tiles — measured faster than 512, profiles/r02)
 constexpr double DENSE_PLAN_BYTES = 16384.0;
 constexpr uint32_t FLUSH_RECS = 248;                 // records per lane between counter flushes
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
@@ -1017,7 +1017,7 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
             // in LDS, plane words below S2C_DENSE_QW; with a margin for the depth's spread) fits
             // the dense kernel
             const double qpp = ((double)ref_qw[r] / 32.0 + 0.25 * (double)ref_np[r]) / (double)L;
-            const double bpp = (20.0 * (double)ref_slots[r] / (double)L) + 12.0 * qpp;
+            const double bpp = (16.0 * (double)ref_slots[r] / (double)L) + 8.0 * qpp;   // S2C_DENSE_BYTES per position
             tp = TP_MAX;
             while (tp > TP_MIN && (((double)tp + 32.0 * (double)(K + 1)) * bpp + 1024.0 > DENSE_PLAN_BYTES ||
                                    ((double)tp + 32.0 * (double)(K + 1)) * qpp > 0.8 * S2C_DENSE_QW))
