@@ -279,6 +279,39 @@ __device__ __forceinline__ void x_events(const uint32_t *bxl, const uint2 *bql, 
     }
 }
 
+// x_events with the first 8 words (xs: non-ACGT plane, ps: base planes, words q/32 ..) loaded
+// by the caller
+__device__ __forceinline__ void x_events_pre(const uint32_t *bxl, const uint2 *bql, const uint32_t (&xs)[8],
+                                             const uint2 (&ps)[8], uint32_t q, uint32_t l, int32_t r0, int32_t lim,
+                                             bool drop, uint32_t *dcnt, uint32_t *ncnt, uint32_t *ccnt) {
+    const uint32_t wa = q >> 5, wb = (q + l - 1) >> 5;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        const uint32_t qw = wa + u;
+        const int32_t b0 = (int32_t)(32 * qw) - (int32_t)q;
+        uint32_t xm = qw <= wb ? xs[u] : 0u;
+        if (b0 < 0) xm &= 0xFFFFFFFFu << (uint32_t)(-b0);
+        if (b0 + 32 > (int32_t)l) xm &= 0xFFFFFFFFu >> (uint32_t)(b0 + 32 - (int32_t)l);
+        xm &= ~ps[u].y;
+        while (xm) {
+            const uint32_t bit = (uint32_t)__builtin_ctz(xm);
+            xm &= xm - 1;
+            const int32_t r = r0 + b0 + (int32_t)bit;
+            if (r < 0 || r >= lim) continue;
+            if ((ps[u].x >> bit) & 1u) {
+                cnt_add1(ccnt, (uint32_t)r);
+                if (!drop) cnt_add1(dcnt, (uint32_t)r);
+            } else {
+                cnt_add1(ncnt, (uint32_t)r);
+            }
+        }
+    }
+    if (wb >= wa + 8) {   // (runs over more than 8 words): the rest from word wa + 8 on
+        const uint32_t q2 = 32 * (wa + 8);
+        x_events(bxl, bql, q2, q + l - q2, r0 + (int32_t)(q2 - q), lim, drop, dcnt, ncnt, ccnt);
+    }
+}
+
 // lane index among the active lanes of a ballot below this one
 __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -426,6 +459,19 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     }
     lds_sync();
     PROF_MARK(2);
+    // the first 64 queued X runs: their run records, plane words (LDS) and non-ACGT words (HBM)
+    // requested now, so the HBM round trip overlaps the general walk of the queued pieces
+    const bool xin = lane < nx;
+    const uint2 xrv = xin ? runl[queue[qcap - 1u - lane]] : make_uint2(0u, 0u);
+    const uint32_t xq0 = xrv.y >> 15, xl = (xrv.y >> 4) & 0x7FFu, xwa = xq0 >> 5;
+    uint32_t xs[8];
+    uint2 xp[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        const uint32_t qw = xin ? min(xwa + u, (xq0 + xl - 1) >> 5) : 0u;
+        xs[u] = xin ? bxl[qw] : 0u;
+        xp[u] = bql[qw];
+    }
     // queued pieces: the general walk; '-' runs and SEQ N / '-' straight into the byte counters.
     // A queued piece's record comes from the lane that loaded it (ds_bpermute, all lanes on).
     for (uint32_t base = 0; base < nslow; base += WGD) {
@@ -464,7 +510,8 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     }
     PROF_MARK(3);
     // queued single-token runs of reads with N / '-' in SEQ (never dropped: maxdel is off)
-    for (uint32_t i = lane; i < nx; i += WGD) {
+    if (xin) x_events_pre(bxl, bql, xs, xp, xq0, xl, (int32_t)xrv.x - T0, TL, false, dcnt, ncnt, ccnt);
+    for (uint32_t i = lane + WGD; i < nx; i += WGD) {
         const uint2 rv = runl[queue[qcap - 1u - i]];
         x_events(bxl, bql, rv.y >> 15, (rv.y >> 4) & 0x7FFu, (int32_t)rv.x - T0, TL, false, dcnt, ncnt, ccnt);
     }
@@ -481,13 +528,23 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         for (int b = 0; b < 8; b++) C[c][b] = 0;
     const uint32_t nrec = cw0 + g < cw1 ? (cw1 - cw0 - g + G - 1) / G : 0u;
     const uint32_t ngrp = ABL(2) ? 0u : uni(__ockl_wfred_max_u32((nrec + GSD - 1) / GSD));
+    // the next group's run records are read while this group's plane words are in flight
+    uint2 rvn[GSD];
+    auto load_runs = [&](uint32_t gi) {
+#pragma unroll
+        for (int u = 0; u < GSD; u++) {
+            const uint32_t m = gi * GSD + u;
+            rvn[u] = runl[m < nrec ? cw0 + g + G * m : 0u];   // (unconditional: the group's reads in flight together)
+        }
+    };
+    if (ngrp) load_runs(0);
     for (uint32_t gi = 0; gi < ngrp; gi++) {
         uint32_t vd[GSD], gk[GSD];   // covered bits; first bit | shift << 5
         uint2 pa[GSD], pb[GSD];
 #pragma unroll
         for (int u = 0; u < GSD; u++) {
             const uint32_t m = gi * GSD + u;
-            uint2 rv = runl[m < nrec ? cw0 + g + G * m : 0u];   // (unconditional: the group's reads in flight together)
+            uint2 rv = rvn[u];
             if (m >= nrec) rv = make_uint2(0u, 0u);
             const RecGeom gm = rec_geom(rv.x, (rv.y >> 4) & 0x7FFu, W);   // (zero records: valid 0)
             const uint32_t qs = (rv.y >> 15) + gm.qs;
@@ -497,6 +554,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             pa[u] = bql[kw];
             pb[u] = bql[kw + 1];
         }
+        if (gi + 1 < ngrp) load_runs(gi + 1);
         // one Harley–Seal tree per plane (tree8 + close8), fed a pair of records at a time
         uint32_t pend[4], t2a[4], t4a[4];
 #pragma unroll
@@ -530,6 +588,15 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         }
     }
     PROF_MARK(5);
+    // the byte counters of this lane's rows (final since the walk): read now, used by the vote
+    const uint32_t rbase = 8 * w + g * RPL;   // the rows' dword index in the byte counters
+    uint32_t rD[RPL], rN[RPL], rX[RPL];       // '-', 'N', '-' of SEQ
+#pragma unroll
+    for (int rr = 0; rr < RPL; rr++) {
+        rD[rr] = active ? dcnt[rbase + rr] : 0u;
+        rN[rr] = active ? ncnt[rbase + rr] : 0u;
+        rX[rr] = active ? ccnt[rbase + rr] : 0u;
+    }
     // ---- counters → byte counts: R[r] byte j = count of position 8j + r
 #pragma unroll
     for (int c = 0; c < 4; c++) transpose8(C[c]);
@@ -567,14 +634,6 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     PROF_MARK(6);
 
     // ---- vote of this lane's rows: row rr = word positions 8j + g·RPL + rr (j = 0..3)
-    const uint32_t rbase = 8 * w + g * RPL;   // the rows' dword index in the byte counters
-    uint32_t rD[RPL], rN[RPL], rX[RPL];       // '-', 'N', '-' of SEQ
-#pragma unroll
-    for (int rr = 0; rr < RPL; rr++) {
-        rD[rr] = active ? dcnt[rbase + rr] : 0u;
-        rN[rr] = active ? ncnt[rbase + rr] : 0u;
-        rX[rr] = active ? ccnt[rbase + rr] : 0u;
-    }
     const uint32_t md = (uint32_t)min(max(d.min_depth, 1), 0x7FFF);   // called: cov ≥ max(-m, 1) (:356-359)
     const uint32_t md16 = md | (md << 16);
     // per row: chars of the largest count, masks (one byte per position) of strict majority
