@@ -188,8 +188,9 @@ __device__ __forceinline__ uint4 sload4(const uint32_t *p) {
 // arrays are allocated in 512-byte granules).  Issued as inline asm: the compiler neither
 // sees the LDS writes nor counts these loads, so it never waits on them; completion is an
 // explicit s_waitcnt vmcnt(0) before the window is read.
+template <int WPT>
 __device__ __forceinline__ void dma16(uint8_t *dst, const uint32_t *src, uint32_t n, const void *end) {
-    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);   // the waves share the 1 KB blocks
     const uintptr_t s0 = (uintptr_t)src, sal = s0 & ~(uintptr_t)15, delta = s0 - sal;
     const uintptr_t eal = ((uintptr_t)end + 15) & ~(uintptr_t)15;
     const uint32_t nbytes = (uint32_t)delta + 4 * n;
@@ -199,7 +200,7 @@ __device__ __forceinline__ void dma16(uint8_t *dst, const uint32_t *src, uint32_
     r.z = (int)uni((uint32_t)min((uint64_t)(eal - sal), (uint64_t)0x7FFFFFF0u));
     r.w = 0x00020000;
     const uint32_t m0 = uni(lds_addr(dst));
-    for (uint32_t base = 0; base < nbytes; base += 1024) {
+    for (uint32_t base = 1024 * wv; base < nbytes; base += 1024 * WPT) {
         if (base + 16 * lane < nbytes)
             asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
                          :: "s"(uni(m0 + base)), "v"(16 * lane), "s"(r), "s"(uni(base)) : "memory", "m0");
@@ -381,27 +382,35 @@ __device__ __forceinline__ WinLds win_lds(const DenseArgs &d, const Win &v, uint
     L.q = (uint32_t *)(L.runl + v.nslot);
     return L;
 }
-// issue the LDS-DMA of window v into buf (completion: s_waitcnt vmcnt(0))
+// issue the LDS-DMA of window v into buf, shared by the tile's waves (completion: every wave's
+// s_waitcnt vmcnt(0), then a barrier)
+template <int WPT>
 __device__ __forceinline__ void win_issue(const DenseArgs &d, const Win &v, uint8_t *buf) {
-    dma16(buf, d.ops + v.o0, v.nslot, d.ops_end);
+    dma16<WPT>(buf, d.ops + v.o0, v.nslot, d.ops_end);
     buf += dma16_bytes(v.nslot);
-    dma16(buf, d.bq + 2 * (size_t)v.qw0, 2 * v.nqw, d.bq_end);
+    dma16<WPT>(buf, d.bq + 2 * (size_t)v.qw0, 2 * v.nqw, d.bq_end);
 }
 
-// One tile of NWP words from its window in LDS; G = 64 / NWP lanes per word, RPL = 8 / G
-// counter rows (4 positions each) voted per lane.  dcnt / ncnt / ccnt: zeroed byte counters.
-constexpr int PFN = 4;   // piece records per lane loaded with the DMA (windows of ≤ 256 pieces)
+// One tile of NWP words from its window in LDS, WPT waves (WT threads): a wave holds NWP / WPT
+// words, G lanes per word, RPL = 8 / G counter rows (4 positions each) voted per lane.
+// dcnt / ncnt / ccnt: zeroed byte counters; stl: the waves' partial tile statistics.
+constexpr int WPT = 2;            // waves per tile (they share the window)
+constexpr int WT = WGD * WPT;     // threads per tile
+constexpr int PFN = 2;            // piece records per thread loaded with the DMA (windows of ≤ 256 pieces)
 template <int NWP>
 __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, const WinLds &L, uint32_t *dcnt,
                                            uint32_t *ncnt, uint32_t *ccnt, const uint8_t *amb, uint32_t fill0,
-                                           const uint4 (&Pp)[PFN], const uint32_t (&oe)[PFN], uint32_t cw0, uint32_t cw1) {
-    constexpr int G = WGD / NWP, RPL = 8 / G;
+                                           const uint4 (&Pp)[PFN], const uint32_t (&oe)[PFN], uint32_t cw0, uint32_t cw1,
+                                           unsigned long long t_entry, uint32_t (*stl)[WPT][4]) {
+    constexpr int NWPW = NWP / WPT, G = WGD / NWPW, RPL = 8 / G;
 #ifdef S2C_PROF
-    unsigned long long prof_t = 0;
+    unsigned long long prof_t = t_entry;
+#else
+    (void)t_entry;
 #endif
-    PROF_MARK(0);
-    const uint32_t lane = threadIdx.x;
-    const uint32_t w = lane / G, g = lane % G;
+    PROF_MARK(1);   // phase 0: entry → window landed (scalar tile loads, DMA, piece records)
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t w = wv * NWPW + lane / G, g = lane % G;   // tile-relative word of this lane
     const uint32_t tile = v.tile, a = v.a, n = v.n, cb0 = v.cb0, npc = v.npc, o0 = v.o0, qw0 = v.qw0;
     const uint32_t W0 = v.W0, nwords = v.nwords, W = W0 + w;
     const bool active = w < nwords;
@@ -412,21 +421,21 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     const uint32_t *opl = L.opl, *bxl = d.bx + qw0;
     const uint2 *bql = L.bql;
     uint2 *runl = L.runl;
-    uint32_t *queue = L.q;
-    const uint32_t qcap = v.nslot;
-    PROF_MARK(1);
+    // this wave's queue: 64 entries per walk iteration (its pieces' share of the window)
+    const uint32_t nitw = (npc + WT - 1) / WT, qcap = WGD * nitw;
+    uint32_t *queue = L.q + wv * qcap;
 
     // ---- walk: one lane per piece → run records {gpos, (query base − 32·qw0) << 15 | len << 4
     //      | kind} of the bases; the common piece here, the others queued
     const int32_t T0 = (int32_t)(32 * W0), TL = (int32_t)(32 * nwords);   // the tile's words
     const bool mda = d.maxdel_active != 0;
     uint32_t nslow = 0, nx = 0;   // queue lengths (uniform)
-    const uint32_t nit = ABL(4) ? 0u : (npc + WGD - 1) / WGD;
+    const uint32_t nit = ABL(4) ? 0u : nitw;
     uint32_t opw[PFN];   // the pieces' first op words, read together
 #pragma unroll
-    for (int u = 0; u < PFN; u++) opw[u] = (lane + WGD * u < npc) ? opl[Pp[u].z - o0] : 0u;
+    for (int u = 0; u < PFN; u++) opw[u] = (tid + WT * u < npc) ? opl[Pp[u].z - o0] : 0u;
     for (uint32_t it = 0; it < nit; it++) {
-        const uint32_t k = lane + WGD * it;
+        const uint32_t k = tid + WT * it;
         uint4 P = Pp[0];
         uint32_t oend = oe[0], w0 = opw[0];
 #pragma unroll
@@ -439,7 +448,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             w0 = it == (uint32_t)u ? opw[u] : w0;
         }
         const bool in = k < npc;
-        if (it >= (uint32_t)PFN && in) {   // (windows of more than 256 pieces)
+        if (it >= (uint32_t)PFN && in) {   // (windows of more than WT·PFN pieces)
             P = ((const uint4 *)d.pc)[pf0 + k];
             oend = d.pc[4 * (size_t)(pf0 + k + 1) + 2];
             w0 = opl[P.z - o0];
@@ -476,8 +485,8 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     // A queued piece's record comes from the lane that loaded it (ds_bpermute, all lanes on).
     for (uint32_t base = 0; base < nslow; base += WGD) {
         const uint32_t i = base + lane;
-        const uint32_t k = i < nslow ? queue[i] : 0u, it = k / WGD;
-        const int src = (int)(4 * (k % WGD));
+        const uint32_t k = i < nslow ? queue[i] : 0u, it = k / WT;
+        const int src = (int)(4 * (k % WGD));   // (k ≡ this wave's lane mod 64: WT is a multiple of 64)
         uint4 P = make_uint4(0u, 0u, 0u, 0u);
         uint32_t oend = 0;
 #pragma unroll
@@ -492,7 +501,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             oend = me ? pe : oend;
         }
         if (i < nslow) {
-            if (it >= (uint32_t)PFN) {   // (windows of more than 256 pieces)
+            if (it >= (uint32_t)PFN) {   // (windows of more than WT·PFN pieces)
                 P = ((const uint4 *)d.pc)[pf0 + k];
                 oend = d.pc[4 * (size_t)(pf0 + k + 1) + 2];
             }
@@ -781,13 +790,26 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         if (t == 0) sc = wave_sum(sc);
         nd = wave_sum(nd);
         ne = wave_sum(ne);
-        if (lane == 0) {   // tile statistics (:352-397)
+        if (lane == 0) {   // this wave's share (by threshold parity: one barrier per threshold)
+            stl[t & 1][wv][0] = sc;
+            stl[t & 1][wv][1] = nd;
+            stl[t & 1][wv][2] = ne;
+        }
+        lds_sync();
+        if (tid == 0) {   // tile statistics (:352-397); ≤ 2048 positions: u32 partial sums
+            uint64_t s0 = 0, s2 = 0, s3 = 0;
+#pragma unroll
+            for (int k = 0; k < WPT; k++) {
+                s0 += stl[t & 1][k][0];
+                s2 += stl[t & 1][k][1];
+                s3 += stl[t & 1][k][2];
+            }
             const size_t jt = (size_t)t * d.n_tiles + tile;
             uint64_t *st = d.tile_stats + jt * 4;
-            st[0] = sc;
+            st[0] = s0;
             st[1] = n;
-            st[2] = nd;
-            st[3] = ne;
+            st[2] = s2;
+            st[3] = s3;
             d.blk_len[jt] = n;
         }
     }
@@ -808,25 +830,31 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
 // contiguous range of items, so neighbouring windows meet in that XCD's L2).  Everything the
 // tile needs arrives by one LDS-DMA round trip after the scalar loads of its tile record.
 template <int NWP>
-__global__ __launch_bounds__(WGD) void k_tile_dense(const DenseArgs d) {
+__global__ __launch_bounds__(WT) void k_tile_dense(const DenseArgs d) {
     extern __shared__ uint4 arena[];   // the window (S2C_DENSE_BYTES layout)
     // one byte per position (row layout): '-' (D/N/P runs, '-' of SEQ unless maxdel drops
     // the read's), 'N' of SEQ, '-' of SEQ (all: the planes count them as C, and 'N' as A)
     __shared__ __attribute__((aligned(16))) uint32_t dcnt[8 * NWP], ncnt[8 * NWP], ccnt[8 * NWP];
     __shared__ uint8_t amb[64];
-    const uint32_t lane = threadIdx.x, b = blockIdx.x;
+    __shared__ uint32_t stl[2][WPT][4];
+#ifdef S2C_PROF
+    const unsigned long long t_entry = __builtin_amdgcn_s_memtime();
+#else
+    const unsigned long long t_entry = 0;
+#endif
+    const uint32_t tid = threadIdx.x, b = blockIdx.x;
     const uint32_t x = b & 7u, per = d.n_items >> 3, rem = d.n_items & 7u;
     const uint32_t item = x * per + min(x, rem) + (b >> 3);
     const Win v = win_of(d, item);
     uint8_t *const buf = (uint8_t *)arena;
-    win_issue(d, v, buf);
-    // with the DMA: the lane's piece records and its word's run-slot range
-    constexpr int G = WGD / NWP;
+    win_issue<WPT>(d, v, buf);
+    // with the DMA: the thread's piece records and its word's run-slot range
+    constexpr int G = WGD / (NWP / WPT);
     uint4 Pp[PFN];
     uint32_t oe[PFN];
 #pragma unroll
     for (int i = 0; i < PFN; i++) {
-        const uint32_t k = lane + WGD * i;
+        const uint32_t k = tid + WT * i;
         Pp[i] = make_uint4(0u, 0u, 0u, 0u);
         oe[i] = 0;
         if (k < v.npc) {
@@ -834,27 +862,27 @@ __global__ __launch_bounds__(WGD) void k_tile_dense(const DenseArgs d) {
             oe[i] = d.pc[4 * (size_t)(v.pf0 + k + 1) + 2];
         }
     }
-    const uint32_t w = lane / G, W = v.W0 + w, K = d.kwin;
+    const uint32_t w = (tid >> 6) * (NWP / WPT) + (tid & 63) / G, W = v.W0 + w, K = d.kwin;
     uint32_t cw0 = 0, cw1 = 0;
     if (w < v.nwords) {
         cw0 = d.rs[W >= K ? W - K : 0u] - v.o0;
         cw1 = d.rs[W + 1] - v.o0;
     }
-    amb[lane] = c_amb[lane];
+    if (tid < 64) amb[tid] = c_amb[tid];
     const uint32_t fill0 = uni((uint32_t)d.fill[0]);
-    for (uint32_t k = lane; k < 8 * NWP; k += WGD) {
+    for (uint32_t k = tid; k < 8 * NWP; k += WT) {
         dcnt[k] = 0;
         ncnt[k] = 0;
         ccnt[k] = 0;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the window landed
     lds_sync();
-    dense_tile<NWP>(d, v, win_lds(d, v, buf), dcnt, ncnt, ccnt, amb, fill0, Pp, oe, cw0, cw1);
+    dense_tile<NWP>(d, v, win_lds(d, v, buf), dcnt, ncnt, ccnt, amb, fill0, Pp, oe, cw0, cw1, t_entry, stl);
 }
 
 template <int NWP>
 int launch(const DenseArgs &a, int64_t n, hipStream_t s) {
-    k_tile_dense<NWP><<<(unsigned)n, WGD, a.buf_bytes, s>>>(a);
+    k_tile_dense<NWP><<<(unsigned)n, WT, a.buf_bytes, s>>>(a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? S2C_OK : s2c_set_error(S2C_ERR_HIP, std::string("k_tile_dense: ") + hipGetErrorString(e));
 }
@@ -898,8 +926,7 @@ int s2c_launch_dense(const s2c_dev *dv, hipStream_t st) {
     const int64_t lds = dv->dense_lds;
     if (lds <= 0 || lds > S2C_DENSE_LDS || (lds & 15)) return s2c_set_error(S2C_ERR_ARG, "dense_lds outside (0, S2C_DENSE_LDS] or not 16-byte aligned");
     a.buf_bytes = (uint32_t)lds;
-    if (dv->tile_max <= 256) return launch<8>(a, n, st);
-    if (dv->tile_max <= 512) return launch<16>(a, n, st);
+    if (dv->tile_max <= 512) return launch<16>(a, n, st);   // (two waves: ≥ 8 words per wave)
     if (dv->tile_max <= 1024) return launch<32>(a, n, st);
     return launch<64>(a, n, st);   // tile_max ≤ 2048 (host plan)
 }
