@@ -547,19 +547,26 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         }
     };
     if (ngrp) load_runs(0);
+    const int32_t W32 = (int32_t)(32 * W);
+    const uint32_t kwmax = v.nqw;   // (plane word index clamp: a record outside the word reads a harmless word)
     for (uint32_t gi = 0; gi < ngrp; gi++) {
-        uint32_t vd[GSD], gk[GSD];   // covered bits; first bit | shift << 5
+        uint32_t vd[GSD], lo[GSD], sh[GSD];   // covered bits, first covered bit, plane shift
         uint2 pa[GSD], pb[GSD];
 #pragma unroll
         for (int u = 0; u < GSD; u++) {
             const uint32_t m = gi * GSD + u;
-            uint2 rv = rvn[u];
-            if (m >= nrec) rv = make_uint2(0u, 0u);
-            const RecGeom gm = rec_geom(rv.x, (rv.y >> 4) & 0x7FFu, W);   // (zero records: valid 0)
-            const uint32_t qs = (rv.y >> 15) + gm.qs;
-            const uint32_t kw = gm.valid ? qs >> 5 : 0u;   // window-relative plane word (uncovered: one broadcast address)
-            vd[u] = gm.valid;
-            gk[u] = gm.lo | (qs & 31u) << 5;
+            const uint2 rv = rvn[u];
+            // the run in word coordinates, clamped to [0, 32]: covered bits [l0, h0)
+            const int32_t s0 = m < nrec ? (int32_t)rv.x - W32 : 64;   // (padding slots: outside the word)
+            const int32_t e0 = s0 + (int32_t)((rv.y >> 4) & 0x7FFu);
+            const uint32_t l0 = (uint32_t)min(max(s0, 0), 32);
+            const uint32_t h0 = (uint32_t)min(max(e0, 0), 32);
+            const uint32_t nb = h0 > l0 ? h0 - l0 : 0u;
+            vd[u] = nb >= 32 ? 0xFFFFFFFFu : __builtin_amdgcn_ubfe(0xFFFFFFFFu, 0, nb) << l0;
+            const uint32_t qs = (rv.y >> 15) + l0 - (uint32_t)s0;   // query base of the first covered position
+            const uint32_t kw = min(qs >> 5, kwmax);
+            lo[u] = l0;
+            sh[u] = qs & 31u;
             pa[u] = bql[kw];
             pb[u] = bql[kw + 1];
         }
@@ -568,9 +575,9 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         uint32_t pend[4], t2a[4], t4a[4];
 #pragma unroll
         for (int u = 0; u < GSD; u++) {
-            const uint32_t v0 = vd[u], lo = gk[u] & 31u, sh = gk[u] >> 5;
-            const uint32_t x = (funnel(pb[u].x, pa[u].x, sh) << lo) & v0;
-            const uint32_t y = (funnel(pb[u].y, pa[u].y, sh) << lo) & v0;
+            const uint32_t v0 = vd[u];
+            const uint32_t x = (funnel(pb[u].x, pa[u].x, sh[u]) << lo[u]) & v0;
+            const uint32_t y = (funnel(pb[u].y, pa[u].y, sh[u]) << lo[u]) & v0;
             const uint32_t mk[4] = {x, y, x & y, v0};
 #pragma unroll
             for (int c = 0; c < 4; c++) {

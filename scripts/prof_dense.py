@@ -25,7 +25,7 @@ f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 abl = _lib.lib.s2c_prof_ablate
 abl.argtypes = [C.c_uint32]
 buf = (C.c_ulonglong * 16)()
-names = ["setup", "walk fast", "walk slow", "walk N/-", "count", "fixup+transpose", "vote+store"]
+names = ["prologue (tile loads, DMA, wait)", "walk fast", "walk slow", "walk N/-", "count", "fixup+transpose", "vote+store"]
 bits_list = [int(b) for b in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0]
 for bits in bits_list:
     abl(bits)
