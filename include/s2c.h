@@ -147,6 +147,23 @@ int  s2c_parser_feed_file(s2c_parser *p, const char *path);
 int  s2c_parser_finish(s2c_parser *p, s2c_batch **out);
 void s2c_parser_free(s2c_parser *p);
 
+/* Streamed batches over coordinate-sorted input (bounded host memory; the reference reads
+ * the whole file first, :185-228, so this has no reference counterpart — its outputs
+ * are the same bytes).  A driver (sam2consensus_amd/stream.py) feeds blocks, takes a
+ * snapshot, runs the tiles every later read must start after (s2c_batch_shard), and
+ * retains only the reads that reach the tiles not yet run.
+ *   set_tile_width: the same tiles in every snapshot (0 = plan from depth; else a multiple
+ *                   of 64 in [64, 2048]).
+ *   snapshot:       the batch of all reads held (no end-of-input flush; the parser goes on).
+ *   retain:         drop the reads that change no global position >= gmin.
+ *   stream_state:   [0] a read parsed after a retain reaches below its gmin (not sorted:
+ *                   the driver falls back to one batch), [1] [2] reference index and POS-1
+ *                   of the last mapped read (-1 if none), [3] reads held. */
+int  s2c_parser_set_tile_width(s2c_parser *p, int64_t width);
+int  s2c_parser_snapshot(s2c_parser *p, s2c_batch **out);
+int  s2c_parser_retain(s2c_parser *p, int64_t gmin);
+int  s2c_parser_stream_state(const s2c_parser *p, int64_t *state);
+
 typedef struct {
     int64_t n_refs;            /* @SQ references (:160-169) */
     int64_t total_len;         /* Σ LN over refs (real positions) */

@@ -197,8 +197,15 @@ def main(argv=None):
         if files is None:
             return 0
     else:
-        files = consensus_files(filename, thresholds, os.fsencode(prefix), args.min_depth, os.fsencode(args.fill),
-                                args.n, maxdel_active, log=lambda s: print(s)).files
+        from .stream import consensus_files_streamed, stream_bytes_from_env
+        sb = stream_bytes_from_env()
+        if sb > 0:   # coordinate-sorted input in bounded host memory (stream.py)
+            files = consensus_files_streamed(filename, thresholds, os.fsencode(prefix), args.min_depth,
+                                             os.fsencode(args.fill), args.n, maxdel_active, log=print,
+                                             batch_bytes=sb).files
+        else:
+            files = consensus_files(filename, thresholds, os.fsencode(prefix), args.min_depth,
+                                    os.fsencode(args.fill), args.n, maxdel_active, log=lambda s: print(s)).files
     for fname, body in files.items():                                             # :411-424
         path = os.fsencode(outfolder) + fname
         with open(path, "wb") as fh:

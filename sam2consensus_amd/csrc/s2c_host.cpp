@@ -197,6 +197,13 @@ struct s2c_parser {
     std::string errmsg;
     std::string last_name;
     int64_t last_ref = -1;
+    // streamed batches (s2c_parser_retain): tile width of every reference, the first global
+    // position not yet emitted, chunks [0, n_kept) hold the reads kept from earlier batches,
+    // and whether a later read reached below the frontier (input not coordinate-sorted)
+    int64_t tile_width = 0;
+    int64_t frontier = 0;
+    size_t n_kept = 0;
+    bool late = false;
     s2c_parser() { chunks.emplace_back(new Chunk()); }
 };
 
@@ -473,6 +480,10 @@ extern "C" int s2c_parser_new(int maxdel_active, int64_t maxdel, s2c_parser **ou
 
 extern "C" void s2c_parser_free(s2c_parser *p) { delete p; }
 
+namespace {
+int parse_window(s2c_parser *p, const char *s, size_t n);
+}
+
 extern "C" int s2c_parser_feed(s2c_parser *p, const char *buf, size_t len) {
     if (!p) return s2c_set_error(S2C_ERR_ARG, "parser is NULL");
     if (p->err) return s2c_set_error(p->err, p->errmsg);
@@ -485,6 +496,17 @@ extern "C" int s2c_parser_feed(s2c_parser *p, const char *buf, size_t len) {
         p->carry.clear();
         if (rc) return rc;
         s = nl + 1;
+    }
+    if (end - s >= (ptrdiff_t)(4 << 20)) {   // a large block: its whole lines in parallel pieces
+        const char *cut = end;
+        while (cut > s && cut[-1] != '\n') cut--;
+        if (cut > s) {
+            int rc = parse_window(p, s, (size_t)(cut - s));
+            if (rc) return rc;
+            s = cut;
+        }
+        if (s < end) p->carry.assign(s, end - s);
+        return S2C_OK;
     }
     while (s < end) {
         const char *nl = (const char *)memchr(s, '\n', end - s);
@@ -785,10 +807,159 @@ static void mark_runs(s2c_batch *b) {
     if (b->rlist.empty()) b->rlist.push_back(0);
 }
 
+// Global coordinate of each reference's position 0 (header order, S2C_POS_ALIGN-aligned).
+static std::vector<int64_t> ref_offsets(const s2c_parser *p, int64_t *padded) {
+    std::vector<int64_t> off(p->ref_len.size());
+    int64_t g = 0;
+    for (size_t r = 0; r < off.size(); r++) {
+        off[r] = g;
+        g = (g + p->ref_len[r] + S2C_POS_ALIGN - 1) / S2C_POS_ALIGN * S2C_POS_ALIGN;
+    }
+    if (padded) *padded = g;
+    return off;
+}
+
+// Global positions a read can change: its counted chars (the POS<=0 wrap puts the leading
+// part at the reference's end, :212) and its emitted insertion keys.  false: none.
+static bool read_extent(const Chunk &c, const ReadRec &r, int64_t off, int64_t L, int64_t *lo, int64_t *hi) {
+    int64_t a = INT64_MAX, b = INT64_MIN;
+    if (r.kc0 >= 0) {
+        const int64_t pa = r.pos0 + r.kc0, pb = r.pos0 + r.kc1;   // [pa, pb) reference-relative
+        if (pa < 0) {
+            a = std::min(a, off + L + pa);
+            b = std::max(b, off + L + std::min<int64_t>(pb, 0) - 1);
+            if (pb > 0) { a = off; b = std::max(b, off + pb - 1); }
+        } else {
+            a = off + pa;
+            b = off + pb - 1;
+        }
+    }
+    for (uint32_t e = r.ev0; e < r.ev0 + r.nev; e++)
+        if (c.ev[e].key >= 0) {
+            a = std::min(a, off + c.ev[e].key);
+            b = std::max(b, off + c.ev[e].key);
+        }
+    *lo = a;
+    *hi = b;
+    return a <= b;
+}
+
+static int build_batch(s2c_parser *p, s2c_batch **out);
+
+// Whether a read parsed since the last retain reaches below its frontier.
+static void check_late(s2c_parser *p) {
+    if (p->frontier <= 0 || p->late) return;
+    const std::vector<int64_t> off = ref_offsets(p, nullptr);
+    for (size_t ci = p->n_kept; ci < p->chunks.size(); ci++) {
+        const Chunk &c = *p->chunks[ci];
+        for (const ReadRec &r : c.reads) {
+            int64_t lo, hi;
+            if (read_extent(c, r, off[r.ref], p->ref_len[r.ref], &lo, &hi) && lo < p->frontier) {
+                p->late = true;
+                return;
+            }
+        }
+    }
+}
+
 extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
     if (!p || !out) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
     int rc = feed_flush(p);
     if (rc) return rc;
+    check_late(p);
+    return build_batch(p, out);
+}
+
+extern "C" int s2c_parser_set_tile_width(s2c_parser *p, int64_t width) {
+    if (!p) return s2c_set_error(S2C_ERR_ARG, "parser is NULL");
+    if (width != 0 && (width < S2C_POS_ALIGN || width > 2048 || width % S2C_POS_ALIGN))
+        return s2c_set_error(S2C_ERR_ARG, "tile width must be 0 or a multiple of 64 in [64, 2048]");
+    p->tile_width = width;
+    return S2C_OK;
+}
+
+// The batch of everything parsed so far (the partial last line stays unparsed); the
+// parser keeps going.
+extern "C" int s2c_parser_snapshot(s2c_parser *p, s2c_batch **out) {
+    if (!p || !out) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
+    if (p->err) return s2c_set_error(p->err, p->errmsg);
+    check_late(p);
+    return build_batch(p, out);
+}
+
+// Drop the reads that cannot change a global position >= gmin (their positions below it
+// are emitted); the kept reads move into one chunk and count no lines again.
+extern "C" int s2c_parser_retain(s2c_parser *p, int64_t gmin) {
+    if (!p) return s2c_set_error(S2C_ERR_ARG, "parser is NULL");
+    if (p->err) return s2c_set_error(p->err, p->errmsg);
+    if (gmin < p->frontier) return s2c_set_error(S2C_ERR_ARG, "retain: frontier moves backwards");
+    const std::vector<int64_t> off = ref_offsets(p, nullptr);
+    std::unique_ptr<Chunk> k(new Chunk());
+    Chunk &d = *k;
+    for (auto &cp : p->chunks) {
+        const Chunk &c = *cp;
+        for (const ReadRec &r : c.reads) {
+            int64_t lo, hi;
+            if (!read_extent(c, r, off[r.ref], p->ref_len[r.ref], &lo, &hi) || hi < gmin) continue;
+            ReadRec n = r;
+            n.tok = d.toks.size();
+            d.toks.insert(d.toks.end(), c.toks.begin() + r.tok, c.toks.begin() + r.tok + r.ntok);
+            n.ev0 = (uint32_t)d.ev.size();
+            if (r.kc0 >= 0 || r.nev > 0) {   // its planes, 16 bases at a time
+                const uint64_t q0 = (d.nq + 15) & ~(uint64_t)15, q1 = q0 + r.slen;
+                const size_t need = (size_t)((q1 + 31) >> 5) + 1;
+                if (d.bx.size() < need) {
+                    const size_t cap = std::max(need, d.bx.size() * 2);
+                    d.bq.resize(2 * cap, 0u);
+                    d.bx.resize(cap, 0u);
+                }
+                const uint16_t *sq = (const uint16_t *)c.bq.data(), *sx = (const uint16_t *)c.bx.data();
+                uint16_t *dq = (uint16_t *)d.bq.data(), *dx = (uint16_t *)d.bx.data();
+                for (uint64_t h = 0; h < (r.slen + 15) / 16; h++) {
+                    const uint64_t s = r.q / 16 + h, t = q0 / 16 + h;
+                    dq[(t >> 1) * 4 + (t & 1)] = sq[(s >> 1) * 4 + (s & 1)];
+                    dq[(t >> 1) * 4 + 2 + (t & 1)] = sq[(s >> 1) * 4 + 2 + (s & 1)];
+                    dx[t] = sx[s];
+                }
+                d.nq = q1;
+                n.q = q0;
+            }
+            for (uint32_t e = r.ev0; e < r.ev0 + r.nev; e++) {
+                Event ev = c.ev[e];
+                ev.q = ev.q - r.q + n.q;
+                ev.read = (uint32_t)d.reads.size();
+                d.ev.push_back(ev);
+            }
+            d.reads.push_back(n);
+        }
+    }
+    p->chunks.clear();
+    p->chunks.push_back(std::move(k));
+    p->chunks.emplace_back(new Chunk());   // the sequential feed appends here
+    p->n_kept = 1;
+    p->frontier = gmin;
+    return S2C_OK;
+}
+
+// state[0] = 1 if a read parsed after a retain reached below its frontier; state[1..2] =
+// (reference index, POS - 1) of the last mapped read in file order (-1, 0: none yet);
+// state[3] = reads held.
+extern "C" int s2c_parser_stream_state(const s2c_parser *p, int64_t *state) {
+    if (!p || !state) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
+    state[0] = p->late ? 1 : 0;
+    state[1] = -1;
+    state[2] = 0;
+    state[3] = 0;
+    for (auto it = p->chunks.rbegin(); it != p->chunks.rend(); ++it)
+        if (!(*it)->reads.empty() && state[1] < 0) {
+            state[1] = (*it)->reads.back().ref;
+            state[2] = (*it)->reads.back().pos0;
+        }
+    for (auto &cp : p->chunks) state[3] += (int64_t)cp->reads.size();
+    return S2C_OK;
+}
+
+static int build_batch(s2c_parser *p, s2c_batch **out) {
     const int64_t R = (int64_t)p->ref_names.size();
     auto &CH = p->chunks;
 
@@ -998,6 +1169,7 @@ extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
     const bool no_dense = getenv("S2C_NO_DENSE") != nullptr;   // diagnostic: every tile through k_tile
     if (const char *e = getenv("S2C_TILE_POS"))
         tile_force = align_up(std::min<int64_t>(std::max<int64_t>(atoll(e), 64), TP_MAX), S2C_POS_ALIGN);
+    if (p->tile_width > 0) tile_force = p->tile_width;   // streamed batches: the same tiles every time
     std::vector<int64_t> ref_slots(R, 0), ref_np(R, 0), ref_qw(R, 0);
     for (int64_t k = 0; k < NP; k++) {
         const Piece &q = pcs[order[k]];

@@ -1,0 +1,242 @@
+"""Streamed batches: coordinate-sorted SAM input in bounded host memory.
+
+The reference reads the whole file into per-reference lists before any consensus work
+(sam2consensus.py:185-228); the whole-batch path here does the same with a packed batch.
+For a coordinate-sorted file (SO:coordinate — what aligners emit after ``samtools sort``)
+the positions a later read can change all lie at or after the last read's POS, so the
+tiles that end before it are final.  The driver
+
+1. feeds the file in blocks (``s2c_parser_feed``; large blocks parse in parallel pieces),
+2. every ``batch_bytes`` of input takes a snapshot batch of the reads held
+   (``s2c_parser_snapshot``, tile width fixed so every snapshot has the same tiles),
+3. runs the tiles [t_done, t1) that end at or before the last read's position — the same
+   ``s2c_batch_shard`` sub-batch the multi-GPU path runs (sam2consensus_amd/shard.py) —
+4. keeps only the reads that reach tile t1 or later (``s2c_parser_retain``),
+
+and at end of input runs the remaining tiles, merges the tile ranges' bodies and stats
+(``shard.merge_outputs``) and formats the records as the whole-batch path does.  The
+bytes are the reference's: a position's counts, insertion columns and vote depend only on
+the reads that reach it, and each tile runs once with all of them.
+
+Errors keep the reference's precedence: a read-pass error (:195-218) raises when its block
+is fed; an insertion-check error (:284-294) seen in a snapshot stops the streaming and is
+raised by the final ``s2c_parser_finish`` (which sees every read of the failing reference
+and every later one, and no read pass error can follow it unseen); vote errors raise from
+``build_records`` over the merged stats.
+
+Input that is not coordinate-sorted is detected (a read parsed after a retain reaching
+below it) and the driver raises ``NotSorted``; ``consensus_files_streamed`` then re-parses
+the file as one batch.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import gzip
+import os
+import time
+
+import numpy as np
+
+from . import _lib as L
+from .batch import HostBatch, Parser
+
+DEFAULT_TILE = 1024               # positions per tile (C5's planner choice at 30x)
+DEFAULT_BATCH = 256 << 20         # input bytes per streamed batch
+BLOCK = 32 << 20                  # bytes per feed call
+
+
+class NotSorted(Exception):
+    """A read changes positions already emitted: the input is not coordinate-sorted."""
+
+
+class StreamParser(Parser):
+    """``Parser`` with the streamed-batch entry points (include/s2c.h)."""
+
+    def __init__(self, maxdel_active=True, maxdel=150, tile_width=DEFAULT_TILE):
+        super().__init__(maxdel_active, maxdel)
+        L.check(L.lib.s2c_parser_set_tile_width(self._p, int(tile_width)))
+
+    def _wrap(self, h):
+        hb = HostBatch(h)
+        hb.maxdel_active, hb.maxdel = self.maxdel_active, self.maxdel
+        return hb
+
+    def snapshot(self) -> HostBatch:
+        h = C.c_void_p()
+        L.check(L.lib.s2c_parser_snapshot(self._p, C.byref(h)))
+        return self._wrap(h)
+
+    def retain(self, gmin):
+        L.check(L.lib.s2c_parser_retain(self._p, int(gmin)))
+
+    def state(self):
+        """(late, last reference index, last POS-1, reads held)."""
+        s = (C.c_int64 * 4)()
+        L.check(L.lib.s2c_parser_stream_state(self._p, s))
+        return bool(s[0]), int(s[1]), int(s[2]), int(s[3])
+
+
+def _sub(hb, t0, t1):
+    h = C.c_void_p()
+    L.check(L.lib.s2c_batch_shard(hb._b, t0, t1, C.byref(h)))
+    sub = HostBatch(h)
+    sub.t0, sub.t1 = t0, t1
+    sub.parent_tiles = hb.info.n_tiles
+    sub.maxdel_active, sub.maxdel = hb.maxdel_active, hb.maxdel
+    return sub
+
+
+class StreamResult:
+    """What ``stream_batches`` hands back: the final batch (tile plan, names, per-reference
+    coverage flags over all batches), the merged (stats, offs, out) and the line counters."""
+
+    def __init__(self, hb, stats, offs, out, header_lines, lines_total, reads_mapped, batches, held_max):
+        self.hb, self.stats, self.offs, self.out = hb, stats, offs, out
+        self.header_lines, self.lines_total, self.reads_mapped = header_lines, lines_total, reads_mapped
+        self.n_refs = hb.info.n_refs
+        self.batches = batches        # tile ranges run
+        self.held_max = held_max      # most reads the parser held at a snapshot
+
+
+def stream_batches(blocks, thresholds, runner, maxdel_active=True, tile_width=DEFAULT_TILE,
+                   batch_bytes=DEFAULT_BATCH, stats_hook=None):
+    """Run ``runner(sub) -> (stats, offs, out)`` over the streamed tile ranges of the SAM
+    text in ``blocks`` (an iterable of bytes).  Raises NotSorted for unsorted input."""
+    T = len(thresholds)
+    p = StreamParser(maxdel_active, 150, tile_width)
+    parts, stats, cov = [], None, None
+    t_done, pending, broken = 0, 0, False
+    lines = mapped = 0
+    held_max = 0
+
+    def run(hb, t0, t1):
+        nonlocal stats
+        sub = _sub(hb, t0, t1)
+        try:
+            st, offs, out = runner(sub)
+        finally:
+            sub.free()
+        stats = st.copy() if stats is None else stats + st
+        parts.append((t0, t1, np.asarray(offs, dtype=np.uint64), out))
+
+    def absorb(hb):
+        nonlocal cov, lines, mapped
+        flag = (hb.ref_reads > 0)
+        cov = flag.copy() if cov is None else (cov | flag)
+        lines += int(hb.info.lines_total)
+        mapped += int(hb.info.reads_mapped)
+
+    try:
+        for blk in blocks:
+            p.feed(blk)
+            pending += len(blk)
+            if broken or pending < batch_bytes:
+                continue
+            pending = 0
+            try:
+                hb = p.snapshot()
+            except (KeyError, IndexError):
+                broken = True          # s2c_parser_finish raises it once the input is read
+                continue
+            try:
+                late, ref, pos0, held = p.state()
+                held_max = max(held_max, held)
+                if late:
+                    raise NotSorted("a read reaches positions already emitted")
+                if ref < 0:
+                    continue
+                bound = int(hb.ref_off[ref]) + max(pos0, 0)
+                NT = int(hb.info.n_tiles)
+                t1 = int(np.searchsorted(hb.tiles[:, 1].astype(np.int64), bound, side="right"))
+                if t1 <= t_done:
+                    continue
+                run(hb, t_done, t1)
+                absorb(hb)
+                gmin = int(hb.tiles[t1, 0]) if t1 < NT else int(hb.info.padded_len)
+                p.retain(gmin)
+                t_done = t1
+                if stats_hook:
+                    stats_hook(t_done, NT, held)
+            finally:
+                hb.free()
+        hb = p.finish()
+        late, _, _, held = p.state()
+        held_max = max(held_max, held)
+        if late:
+            hb.free()
+            raise NotSorted("a read reaches positions already emitted")
+        NT = int(hb.info.n_tiles)
+        if t_done < NT:
+            run(hb, t_done, NT)
+        absorb(hb)
+    finally:
+        p.close()
+    hb.ref_reads = cov.astype(np.int64)          # Σcoverage > 0 in any batch (:334-341)
+    offs, out = _merge(parts, T)
+    if stats is None:
+        stats = np.zeros((hb.info.n_refs, T, 4), np.uint64)
+    return StreamResult(hb, stats, offs, out, int(hb.info.header_lines), lines, mapped,
+                        [(a, b) for a, b, _, _ in parts], held_max)
+
+
+def _merge(parts, T):
+    from .shard import merge_outputs
+    return merge_outputs(parts, T)
+
+
+def file_blocks(filename, block=BLOCK):
+    """The file's bytes in blocks (".gz" → gzip, :111-114)."""
+    op = gzip.open if filename.endswith(".gz") else open
+    with op(filename, "rb") as fh:
+        while True:
+            b = fh.read(block)
+            if not b:
+                return
+            yield b
+
+
+def device_runner(thresholds, min_depth, fill, device=None):
+    """runner(sub) on the GPU: upload, s2c_run, fetch (sam2consensus_amd/engine.py)."""
+    from .engine import DeviceBatch, Workspace
+
+    def runner(sub):
+        ws = Workspace(DeviceBatch(sub, device), thresholds, min_depth, fill)
+        ws.run()
+        return ws.fetch()
+    return runner
+
+
+def consensus_files_streamed(filename, thresholds, prefix, min_depth=1, fill=b"-", nchar=0, maxdel_active=True,
+                             device=None, log=None, batch_bytes=DEFAULT_BATCH, tile_width=DEFAULT_TILE):
+    """``cli.consensus_files`` in streamed batches; unsorted input falls back to one batch."""
+    from .cli import RunResult, _log_summary, consensus_files
+    from .records import build_records, render
+
+    t = {}
+    t0 = time.perf_counter()
+    try:
+        res = stream_batches(file_blocks(filename), thresholds, device_runner(thresholds, min_depth, fill, device),
+                             maxdel_active, tile_width, batch_bytes)
+    except NotSorted:
+        return consensus_files(filename, thresholds, prefix, min_depth, fill, nchar, maxdel_active, device, log)
+    t["stream"] = time.perf_counter() - t0
+    if log:
+        _log_summary(log, res)
+    t0 = time.perf_counter()
+    fastas = build_records(res.hb, thresholds, prefix, res.stats, res.offs, res.out)
+    pre = prefix.encode("latin-1") if isinstance(prefix, str) else prefix
+    files = {n.encode("latin-1") + b"__" + pre + b".fasta": render(r, nchar) for n, r in fastas.items()}
+    t["format"] = time.perf_counter() - t0
+    r = RunResult(files, t, res.hb.info)
+    r.batches = res.batches
+    r.held_max = res.held_max
+    return r
+
+
+def stream_bytes_from_env():
+    """S2C_STREAM=<bytes>[K|M|G] turns on streamed batches in the CLI (0 / unset: one batch)."""
+    v = os.environ.get("S2C_STREAM", "").strip().upper()
+    if not v:
+        return 0
+    mult = {"K": 1 << 10, "M": 1 << 20, "G": 1 << 30}.get(v[-1], 1)
+    return int(float(v.rstrip("KMG")) * mult)

@@ -1,0 +1,74 @@
+"""Host memory of the whole-batch path vs streamed batches (stream.py) on one config's
+coordinate-sorted SAM file: each mode runs in its own child process (peak RSS from
+getrusage), and the FASTA bytes of both must agree.
+
+    python scripts/stream_rss.py c5 [batch_MB] > gpurun_out/stream_rss_c5.json
+"""
+import hashlib
+import json
+import os
+import resource
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def child(mode, path, name, batch_mb):
+    from sam2consensus_amd import configs
+    from sam2consensus_amd.cli import consensus_files
+    from sam2consensus_amd.cli import build_parser
+    from sam2consensus_amd.stream import consensus_files_streamed
+    a = build_parser().parse_args(["-i", path] + configs.cli_args(name))
+    thr = [float(x) for x in a.thresholds.split(",")]
+    prefix = os.path.basename(path).split(".")[0].encode()
+    common = (thr, prefix, a.min_depth, a.fill.encode(), a.n, not isinstance(a.maxdel, str))
+    t0 = time.perf_counter()
+    if mode == "whole":
+        r = consensus_files(path, *common)
+    else:
+        r = consensus_files_streamed(path, *common, batch_bytes=batch_mb << 20)
+    dt = time.perf_counter() - t0
+    h = hashlib.sha256()
+    for k in sorted(r.files):
+        h.update(k)
+        h.update(r.files[k])
+    print(json.dumps({"mode": mode, "seconds": round(dt, 3),
+                      "peak_rss_mb": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0, 1),
+                      "sha256": h.hexdigest(), "batches": len(getattr(r, "batches", [])) or 1,
+                      "reads_held_max": getattr(r, "held_max", None)}))
+
+
+def main():
+    if sys.argv[1] == "--child":
+        child(sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]))
+        return 0
+    name = sys.argv[1]
+    batch_mb = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+    from sam2consensus_amd import configs
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+        path = os.path.join(td, name + ".sam")
+        n = configs.synth_write(name, path)
+        size = os.path.getsize(path)
+        res = {"config": name, "reads": n, "sam_bytes": size, "batch_mb": batch_mb}
+        sys.stderr.write("wrote %d reads, %d bytes\n" % (n, size))
+        sys.stderr.flush()
+        for mode in ("whole", "stream"):
+            out = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", mode, path, name,
+                                  str(batch_mb)], capture_output=True, text=True, timeout=600)
+            if out.returncode != 0:
+                sys.stderr.write(out.stderr)
+                return out.returncode
+            res[mode] = json.loads(out.stdout.strip().splitlines()[-1])
+            sys.stderr.write(json.dumps(res[mode]) + "\n")
+            sys.stderr.flush()
+        res["identical"] = res["whole"]["sha256"] == res["stream"]["sha256"]
+        print(json.dumps(res))
+        return 0 if res["identical"] else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -176,6 +176,49 @@ def test_sharded_on_device_matches_golden(name, world):
     assert got == {k: v["sha256"] for k, v in g["files"].items()}
 
 
+@pytest.mark.parametrize("name,nbatch", [("c2", 8), ("c1", 5)])
+def test_streamed_batches_on_device_match_golden(tmp_path, name, nbatch):
+    """Coordinate-sorted SAM file fed in blocks, run as nbatch streamed tile ranges through
+    libs2c.so (sam2consensus_amd/stream.py) == the reference's files."""
+    from sam2consensus_amd import configs, stream
+    from sam2consensus_amd.records import build_records, render
+    g = CONFIGS[name]
+    opt = o.parse_argv(["-i", g["sam_file"]] + g["args"])
+    path = str(tmp_path / g["sam_file"])
+    configs.synth_write(name, path)
+    size = os.path.getsize(path)
+    res = stream.stream_batches(stream.file_blocks(path, 4 << 20), opt.thresholds,
+                                stream.device_runner(opt.thresholds, opt.min_depth, opt.fill.encode()),
+                                opt.maxdel_active, 512, size // nbatch + 1)
+    assert len(res.batches) >= nbatch - 1
+    assert res.reads_mapped == g["n_reads"]
+    recs = build_records(res.hb, opt.thresholds, opt.prefix.encode(), res.stats, res.offs, res.out)
+    got = {n + "__" + opt.prefix + ".fasta": hashlib.sha256(render(r, opt.n)).hexdigest() for n, r in recs.items()}
+    assert got == {k: v["sha256"] for k, v in g["files"].items()}
+
+
+def test_cli_streamed_and_unsorted_fallback(tmp_path, monkeypatch):
+    """S2C_STREAM turns on streamed batches in the CLI: C1 (sorted) streams, a shuffled
+    .sam.gz (C3's record order, reduced) falls back to one batch; both == the oracle."""
+    from sam2consensus_amd import configs
+    from sam2consensus_amd.cli import main
+    monkeypatch.setenv("S2C_STREAM", "64K")
+    g = CONFIGS["c1"]
+    sam = str(tmp_path / "c1.sam")
+    configs.synth_write("c1", sam)
+    out = tmp_path / "out"
+    assert main(["-i", sam, "-o", str(out)] + g["args"]) == 0
+    got = {fn: open(os.path.join(out, fn), "rb").read().decode("latin-1") for fn in os.listdir(out)}
+    assert got == g["content"]
+    gz = str(tmp_path / "c3s.sam.gz")
+    configs.synth_write("c3", gz, scale=0.004)
+    out2 = tmp_path / "out2"
+    assert main(["-i", gz, "-o", str(out2), "-m", "10", "-p", "c3s"]) == 0
+    want, _ = o.run_path(gz, ["-m", "10", "-p", "c3s"])
+    got = {fn: open(os.path.join(out2, fn), "rb").read().decode("latin-1") for fn in os.listdir(out2)}
+    assert got == want
+
+
 @pytest.mark.parametrize("name,over,thr,md,fill", [
     ("c2", {"n_refs": 6}, [0.25, 0.5, 0.75], 1, b"-"),
     # long insertions: > 1024 insertion columns in a tile → the HBM column path

@@ -1,0 +1,149 @@
+"""Streamed batches (sam2consensus_amd/stream.py) on CPU: coordinate-sorted input fed in
+blocks, cut into tile ranges by snapshot / shard / retain, must give the reference's bytes
+and the whole-batch path's errors; unsorted input must be detected.  The per-range runner
+is the kernel-shaped CPU model (tests/batch_model.py); tests/test_gpu.py runs the same
+driver through libs2c.so's kernels."""
+import os
+
+import numpy as np
+import pytest
+
+import batch_model as bm
+import golden_io
+import s2c_oracle as o
+from sam2consensus_amd import batch, configs, records, stream
+
+
+def _blocks(data, n):
+    for k in range(0, len(data), n):
+        yield data[k:k + n]
+
+
+def _runner(opt):
+    return lambda sub: bm.model_pipeline(sub, opt.thresholds, opt.min_depth, opt.fill.encode("latin-1"))
+
+
+def _files(res, opt):
+    fastas = records.build_records(res.hb, opt.thresholds, opt.prefix, res.stats, res.offs, res.out)
+    return {n + "__" + opt.prefix + ".fasta": records.render(r, opt.n).decode("latin-1") for n, r in fastas.items()}
+
+
+def _stream(sam, args, block=97, batch_bytes=300, tile=64):
+    opt = o.parse_argv(["-i", "in.sam"] + list(args))
+    data = sam.encode("latin-1") if isinstance(sam, str) else sam
+    res = stream.stream_batches(_blocks(data, block), opt.thresholds, _runner(opt), opt.maxdel_active,
+                                tile, batch_bytes)
+    return res, _files(res, opt)
+
+
+def _sorted_case():
+    """Several refs (header order = file order) with insertions, deletions, N runs, a POS=0
+    wrap with an insertion and events with nothing counted."""
+    sam = "@HD\tVN:1.6\tSO:coordinate\n@SQ\tSN:a\tLN:900\n@SQ\tSN:b\tLN:3000\n@SQ\tSN:c\tLN:40\n" \
+          "@SQ\tSN:d\tLN:500\n"
+    rows = []
+    for s in range(1, 760, 3):
+        rows.append(("a", s, "60M2I50M", "ACGT" * 28))
+    rows.append(("b", 0, "1M2I3M", "AGGCCC"))                 # POS=0 wrap: changes b's end
+    for s in range(1, 2800, 5):
+        rows.append(("b", s, "40M3D60M", "TTGCA" * 20))
+        if s == 10:
+            rows.append(("b", 10, "10M2000N10M", "G" * 20))  # spans most of b
+        if s == 1496:
+            rows.append(("b", 1500, "5M2I", "GGGGGTT"))       # insertion after the last base
+        if s == 1996:
+            rows.append(("b", 2000, "3S4I", "AAACCCC"))       # events, nothing counted
+    rows.append(("c", 0, "5M", "CCCCC"))
+    rows.append(("c", 3, "4M", "NNAC"))
+    for r in rows:
+        sam += "r\t0\t%s\t%d\t60\t%s\t*\t0\t0\t%s\t*\n" % r
+    sam += "u\t4\t*\t0\t0\t*\t*\t0\t0\tACGT\t*\n"             # unmapped tail
+    return sam
+
+
+@pytest.mark.parametrize("args", [[], ["-c", "0.25,0.75"], ["-d", "9"], ["-m", "3", "-f", "N"], ["-n", "50"]])
+def test_sorted_stream_matches_reference(args):
+    sam = _sorted_case()
+    res, files = _stream(sam, args)
+    assert len(res.batches) > 3, res.batches          # really cut into tile ranges
+    assert files == o.run_case(sam, args)["files"]
+    # line counters of the CLI summary (:224-228) over all batches
+    hb = batch.parse_text(sam)
+    assert (res.header_lines, res.lines_total, res.reads_mapped) == \
+        (hb.info.header_lines, hb.info.lines_total, hb.info.reads_mapped)
+
+
+@pytest.mark.parametrize("block,batch_bytes,tile", [(1, 1, 64), (4096, 2048, 128), (10 ** 6, 10 ** 6, 1024)])
+def test_block_and_batch_sizes(block, batch_bytes, tile):
+    sam = _sorted_case()
+    _, files = _stream(sam, ["-c", "0.5"], block, batch_bytes, tile)
+    assert files == o.run_case(sam, ["-c", "0.5"])["files"]
+
+
+def test_golden_cases_stream_or_detect_unsorted():
+    """Every KAT case: byte-identical when streamed, or NotSorted (then the CLI runs one batch)."""
+    n_streamed = 0
+    for case in golden_io.load("kat"):
+        try:
+            _, files = _stream(case["sam"], case["args"], block=13, batch_bytes=40, tile=64)
+        except stream.NotSorted:
+            continue
+        except (KeyError, IndexError, ValueError, ZeroDivisionError, OverflowError) as e:
+            assert type(e).__name__ == case["status"], case["name"]
+            n_streamed += 1
+            continue
+        assert case["status"] == "ok" and files == case["files"], case["name"]
+        n_streamed += 1
+    assert n_streamed >= 10
+
+
+def test_unsorted_input_is_detected(tmp_path):
+    sam = _sorted_case()
+    head = [ln for ln in sam.splitlines(True) if ln.startswith("@")]
+    body = [ln for ln in sam.splitlines(True) if not ln.startswith("@")]
+    body = body[len(body) // 2:] + body[: len(body) // 2]
+    with pytest.raises(stream.NotSorted):
+        _stream("".join(head + body), [])
+    # a synthetic shuffled config (C3's record order)
+    path = str(tmp_path / "c3.sam")
+    configs.synth_write("c3", path, scale=0.002)
+    opt = o.parse_argv(["-i", path, "-m", "10"])
+    with pytest.raises(stream.NotSorted):
+        stream.stream_batches(stream.file_blocks(path, 1 << 16), opt.thresholds, _runner(opt), True, 256, 1 << 17)
+
+
+def test_reformat_error_then_read_pass_error_keeps_precedence():
+    """An insertion-key error (:294) in an early batch, a bad POS (:201) later: the read
+    pass error wins, as in the reference; without the later line the IndexError is raised."""
+    sam = "@SQ\tSN:a\tLN:10\n@SQ\tSN:b\tLN:2000\n"
+    sam += "r\t0\ta\t9\t60\t2M3I\t*\t0\t0\tACGGG\t*\n"     # key 10 == LN → IndexError (:294)
+    for s in range(1, 1800, 7):
+        sam += "r\t0\tb\t%d\t60\t20M\t*\t0\t0\t%s\t*\n" % (s, "ACGTA" * 4)
+    good = o.run_case(sam, [])
+    assert good["status"] == "IndexError"
+    with pytest.raises(IndexError):
+        _stream(sam, [], block=50, batch_bytes=100)
+    bad = sam + "r\t0\tb\tx\t60\t20M\t*\t0\t0\tACGT\t*\n"
+    assert o.run_case(bad, [])["status"] == "ValueError"
+    with pytest.raises(ValueError):
+        _stream(bad, [], block=50, batch_bytes=100)
+
+
+def test_retain_bounds_the_reads_held(tmp_path):
+    """A sorted synthetic config (C2's shape, 30 loci): byte-identical to the whole batch,
+    and the parser never holds more than a few batches' reads."""
+    path = str(tmp_path / "c2.sam")
+    configs.synth_write("c2", path, n_refs=30, depth=60.0)
+    args = configs.cli_args("c2")
+    opt = o.parse_argv(["-i", path] + args)
+    size = os.path.getsize(path)
+    res = stream.stream_batches(stream.file_blocks(path, 1 << 14), opt.thresholds, _runner(opt),
+                                opt.maxdel_active, 512, size // 8)
+    assert len(res.batches) >= 6
+    hb = batch.parse_file(path, opt.maxdel_active)
+    st, offs, out = bm.model_pipeline(hb, opt.thresholds, opt.min_depth, opt.fill.encode("latin-1"))
+    whole = {n + "__" + opt.prefix + ".fasta": records.render(r, opt.n).decode("latin-1")
+             for n, r in records.build_records(hb, opt.thresholds, opt.prefix, st, offs, out).items()}
+    assert _files(res, opt) == whole
+    assert res.held_max < 0.4 * hb.info.reads_mapped
+    assert np.array_equal(res.stats.sum(axis=0), st.sum(axis=0))
