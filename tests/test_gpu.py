@@ -187,7 +187,7 @@ def test_streamed_batches_on_device_match_golden(tmp_path, name, nbatch):
     path = str(tmp_path / g["sam_file"])
     configs.synth_write(name, path)
     size = os.path.getsize(path)
-    res = stream.stream_batches(stream.file_blocks(path, 4 << 20), opt.thresholds,
+    res = stream.stream_batches(stream.file_blocks(path, max(4096, size // (4 * nbatch))), opt.thresholds,
                                 stream.device_runner(opt.thresholds, opt.min_depth, opt.fill.encode()),
                                 opt.maxdel_active, 512, size // nbatch + 1)
     assert len(res.batches) >= nbatch - 1
