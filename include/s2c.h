@@ -163,6 +163,10 @@ int  s2c_parser_set_tile_width(s2c_parser *p, int64_t width);
 int  s2c_parser_snapshot(s2c_parser *p, s2c_batch **out);
 int  s2c_parser_retain(s2c_parser *p, int64_t gmin);
 int  s2c_parser_stream_state(const s2c_parser *p, int64_t *state);
+/* Unsorted input (counts added to running totals batch by batch, s2c_accumulate): keep
+ * only the reads with insertion events, their counted ranges cleared; the last batch
+ * (s2c_parser_finish) then holds every insertion event of the file. */
+int  s2c_parser_retain_events(s2c_parser *p);
 
 typedef struct {
     int64_t n_refs;            /* @SQ references (:160-169) */
@@ -326,6 +330,12 @@ int s2c_run(const s2c_dev *d, void *stream);
 /* Diagnostics (tests only, not part of the product path): k_reads over every piece, then
  * every tile's counts stored to d->counts ([6][padded_len] u32) and no vote. */
 int s2c_pileup_counts(const s2c_dev *d, void *stream);
+/* Streamed batches of unsorted input: run records of every piece, then every tile's counts
+ * ADDED to d->counts (the running totals [6][padded_len], zeroed by the caller before the
+ * first batch; no k_prep).  keep_tables = 0: the batch's insertion tables are cleared;
+ * 1 (the last batch): kept for s2c_consensus, which the caller runs with d->deep listing
+ * every tile so all of them are voted from the totals. */
+int s2c_accumulate(const s2c_dev *d, int keep_tables, void *stream);
 
 #ifdef __cplusplus
 }

@@ -102,6 +102,7 @@ EXPORTS = [
     "s2c_last_error", "s2c_abi_version", "s2c_layout",
     "s2c_parser_new", "s2c_parser_feed", "s2c_parser_feed_file", "s2c_parser_finish", "s2c_parser_free",
     "s2c_parser_set_tile_width", "s2c_parser_snapshot", "s2c_parser_retain", "s2c_parser_stream_state",
+    "s2c_parser_retain_events", "s2c_accumulate",
     "s2c_batch_info_get", "s2c_batch_arrays_get", "s2c_batch_ref_name", "s2c_batch_free", "s2c_batch_shard",
     "s2c_parsecigar", "s2c_synth_feed", "s2c_synth_write",
     "s2c_workspace_sizes", "s2c_reads", "s2c_pileup", "s2c_consensus", "s2c_run", "s2c_pileup_counts",
@@ -131,6 +132,8 @@ def _load():
         "s2c_parser_snapshot": (C.c_int, [_VP, pp]),
         "s2c_parser_retain": (C.c_int, [_VP, C.c_int64]),
         "s2c_parser_stream_state": (C.c_int, [_VP, C.POINTER(C.c_int64)]),
+        "s2c_parser_retain_events": (C.c_int, [_VP]),
+        "s2c_accumulate": (C.c_int, [C.POINTER(Dev), C.c_int, _VP]),
         "s2c_batch_info_get": (C.c_int, [_VP, C.POINTER(BatchInfo)]),
         "s2c_batch_arrays_get": (C.c_int, [_VP, C.POINTER(BatchArrays)]),
         "s2c_batch_ref_name": (C.c_char_p, [_VP, C.c_int64]),

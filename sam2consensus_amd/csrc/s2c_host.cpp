@@ -887,21 +887,20 @@ extern "C" int s2c_parser_snapshot(s2c_parser *p, s2c_batch **out) {
     return build_batch(p, out);
 }
 
-// Drop the reads that cannot change a global position >= gmin (their positions below it
-// are emitted); the kept reads move into one chunk and count no lines again.
-extern "C" int s2c_parser_retain(s2c_parser *p, int64_t gmin) {
-    if (!p) return s2c_set_error(S2C_ERR_ARG, "parser is NULL");
-    if (p->err) return s2c_set_error(p->err, p->errmsg);
-    if (gmin < p->frontier) return s2c_set_error(S2C_ERR_ARG, "retain: frontier moves backwards");
+// Move the reads `keep` selects into one chunk (their tokens, planes and events; no line
+// counted again); with events_only they keep only their insertion events (counted range
+// cleared: their counts are already in the running totals).
+template <class Keep>
+static void compact_reads(s2c_parser *p, Keep keep, bool events_only) {
     const std::vector<int64_t> off = ref_offsets(p, nullptr);
     std::unique_ptr<Chunk> k(new Chunk());
     Chunk &d = *k;
     for (auto &cp : p->chunks) {
         const Chunk &c = *cp;
         for (const ReadRec &r : c.reads) {
-            int64_t lo, hi;
-            if (!read_extent(c, r, off[r.ref], p->ref_len[r.ref], &lo, &hi) || hi < gmin) continue;
+            if (!keep(c, r, off[r.ref])) continue;
             ReadRec n = r;
+            if (events_only) n.kc0 = n.kc1 = -1;
             n.tok = d.toks.size();
             d.toks.insert(d.toks.end(), c.toks.begin() + r.tok, c.toks.begin() + r.tok + r.ntok);
             n.ev0 = (uint32_t)d.ev.size();
@@ -937,7 +936,29 @@ extern "C" int s2c_parser_retain(s2c_parser *p, int64_t gmin) {
     p->chunks.push_back(std::move(k));
     p->chunks.emplace_back(new Chunk());   // the sequential feed appends here
     p->n_kept = 1;
+}
+
+// Drop the reads that cannot change a global position >= gmin (their positions below it
+// are emitted).
+extern "C" int s2c_parser_retain(s2c_parser *p, int64_t gmin) {
+    if (!p) return s2c_set_error(S2C_ERR_ARG, "parser is NULL");
+    if (p->err) return s2c_set_error(p->err, p->errmsg);
+    if (gmin < p->frontier) return s2c_set_error(S2C_ERR_ARG, "retain: frontier moves backwards");
+    compact_reads(p, [&](const Chunk &c, const ReadRec &r, int64_t off) {
+        int64_t lo, hi;
+        return read_extent(c, r, off, p->ref_len[r.ref], &lo, &hi) && hi >= gmin;
+    }, false);
     p->frontier = gmin;
+    return S2C_OK;
+}
+
+// Unsorted input: the counts of every read held are in the running totals; keep only the
+// reads with insertion events, as event-only reads (their motifs are counted once, by the
+// last batch, which holds every event — and the insertion checks of :284-294 see them all).
+extern "C" int s2c_parser_retain_events(s2c_parser *p) {
+    if (!p) return s2c_set_error(S2C_ERR_ARG, "parser is NULL");
+    if (p->err) return s2c_set_error(p->err, p->errmsg);
+    compact_reads(p, [](const Chunk &, const ReadRec &r, int64_t) { return r.nev > 0; }, true);
     return S2C_OK;
 }
 

@@ -6,6 +6,7 @@
 // Everything is derived from splitmix64 streams keyed by (seed, read index), so the
 // bytes are identical on every machine; the same generator feeds the golden run of the
 // reference (oracle/gen_golden_configs.py), the CLI tests and bench.py.
+#include <thread>
 #include "../../include/s2c.h"
 
 #include <zlib.h>
@@ -202,12 +203,51 @@ extern "C" int s2c_synth_write(const s2c_synth_spec *spec, const char *path, int
     if (!spec || !path) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
     size_t n = strlen(path);
     if (n >= 3 && strcmp(path + n - 3, ".gz") == 0) {
-        gzFile g = gzopen(path, "wb6");
-        if (!g) return s2c_set_error(S2C_ERR_IO, std::string("cannot open ") + path);
-        int rc = generate(*spec, [g](const char *b, size_t k) {
-            return gzwrite(g, b, (unsigned)k) == (int)k ? S2C_OK : s2c_set_error(S2C_ERR_IO, "gzwrite failed");
+        // concatenated gzip members (one per 16 MB of text, deflated level 1 on all host
+        // threads): a valid .gz stream that zlib / gzip / Python read as one file
+        FILE *f = fopen(path, "wb");
+        if (!f) return s2c_set_error(S2C_ERR_IO, std::string("cannot open ") + path);
+        constexpr size_t BLK = (size_t)16 << 20;
+        unsigned hw = std::thread::hardware_concurrency();
+        const size_t nt = std::max<size_t>(1, std::min<unsigned>(hw ? hw : 1, 16));
+        std::vector<std::string> in(1);
+        auto deflate_all = [&]() -> int {
+            std::vector<std::string> out(in.size());
+            std::vector<int> ok(in.size(), 1);
+            auto work = [&](size_t i) {
+                z_stream z{};
+                if (deflateInit2(&z, 1, Z_DEFLATED, 31, 8, Z_DEFAULT_STRATEGY) != Z_OK) { ok[i] = 0; return; }
+                out[i].resize(deflateBound(&z, in[i].size()));
+                z.next_in = (Bytef *)in[i].data();
+                z.avail_in = (uInt)in[i].size();
+                z.next_out = (Bytef *)&out[i][0];
+                z.avail_out = (uInt)out[i].size();
+                ok[i] = deflate(&z, Z_FINISH) == Z_STREAM_END;
+                out[i].resize(z.total_out);
+                deflateEnd(&z);
+            };
+            std::vector<std::thread> th;
+            for (size_t i = 0; i < in.size(); i++)
+                if (!in[i].empty()) th.emplace_back(work, i);
+            for (auto &t : th) t.join();
+            for (size_t i = 0; i < in.size(); i++) {
+                if (in[i].empty()) continue;
+                if (!ok[i]) return s2c_set_error(S2C_ERR_IO, "deflate failed");
+                if (fwrite(out[i].data(), 1, out[i].size(), f) != out[i].size()) return s2c_set_error(S2C_ERR_IO, "write failed");
+            }
+            in.assign(1, std::string());
+            return S2C_OK;
+        };
+        int rc = generate(*spec, [&](const char *b, size_t k) {
+            in.back().append(b, k);
+            if (in.back().size() >= BLK) {
+                if (in.size() == nt) return deflate_all();
+                in.emplace_back();
+            }
+            return S2C_OK;
         }, n_reads_out);
-        gzclose(g);
+        if (!rc) rc = deflate_all();
+        fclose(f);
         return rc;
     }
     FILE *f = fopen(path, "wb");

@@ -71,6 +71,11 @@ constexpr int VT_ACC = 1 + 4 * VT_TMAX;       // LDS u64: position sumcov, {nond
 static_assert(PF == S2C_EPI_KEYS, "k_tile key capacity");
 
 // What the tile kernels read of s2c_dev, compact (kernel arguments stay in SGPRs).
+// k_tile modes: the run (vote in the epilogue); counts stored (s2c_pileup_counts); counts
+// added to running totals with the insertion tables cleared (a streamed batch) or kept for
+// k_consensus (the last streamed batch)
+constexpr uint32_t MODE_RUN = 0, MODE_STORE = 1, MODE_ADD = 2, MODE_ADD_KEEP = 3;
+
 struct TileArgs {
     const uint32_t *rs, *runs, *bq, *bx, *tiles, *lp;
     uint32_t *ibkt, *ilong, *ilong_n;
@@ -80,7 +85,7 @@ struct TileArgs {
     uint8_t *ins_chr;
     uint64_t *tile_stats, *blk_len;
     uint8_t *out;
-    uint32_t padded_len, n_cols, n_tiles, kwin, chunk, n_qwords, runs_bytes, mode;   // mode 1: counts only
+    uint32_t padded_len, n_cols, n_tiles, kwin, chunk, n_qwords, runs_bytes, mode;   // MODE_* below
     int32_t n_thr, min_depth, fill_len, fill_nondash;
 };
 
@@ -654,7 +659,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(3))) void k_
     const uint32_t a = T.a, n = T.b - T.a;
     const uint32_t W = (a >> 5) + w;
     const bool active = 32u * w < n;
-    const bool counts_only = d.mode == 1;
+    const bool counts_only = d.mode != MODE_RUN;
+    const bool accumulate = d.mode >= MODE_ADD;
     const bool finish = !(T.flags & (S2C_TILE_DEEP | S2C_TILE_GENERAL)) && !counts_only;
     const bool deep = (T.flags & S2C_TILE_DEEP) != 0;
     // ---- candidates of this lane: window slots [cw0, cw1) then long slots [lp0, lp1)
@@ -693,7 +699,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(3))) void k_
     TPROF_MARK(1);
     if (has_ins) il = build_layout<PF, false>(d, T, tile, L.bits, L.wrank, L.klen, L.key, cols, L.colkey, L.scan);
     TPROF_MARK(2);
-    if (counts_only && T.nev > 0 && chunk == 0) {   // no vote: leave the tile's tables zero for the next run
+    if (counts_only && d.mode != MODE_ADD_KEEP && T.nev > 0 && chunk == 0) {   // no vote: leave the tile's tables zero for the next run
         for (uint32_t e = tid; e < T.bcap; e += WG) ((uint4 *)d.ibkt)[T.boff + e] = make_uint4(0, 0, 0, 0);
         if (tid == 0) d.ilong_n[tile] = 0;
     }
@@ -859,13 +865,14 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(3))) void k_
         tile_epilogue_fast<NWP>(d, tile, T, il, hist, cols, L);
     } else {
         // deep tile: this chunk's counts → HBM (symbol-major, coalesced atomics); a general
-        // tile's (and in counts-only mode every tile's) counts: plain stores
+        // tile's (and in counts-only mode every tile's) counts: plain stores; streamed
+        // batches of unsorted input add every tile's counts to the running totals
         for (uint32_t q = tid; q < n; q += WG)
 #pragma unroll
             for (uint32_t c = 0; c < NSYM; c++) {
                 uint32_t *dst = d.counts + (size_t)c * d.padded_len + a + q;
                 const uint32_t v = H::get(hist, c, q);
-                if (deep) {
+                if (deep || accumulate) {
                     if (v) atomicAdd(dst, v);
                 } else {
                     *dst = v;
@@ -1084,7 +1091,7 @@ TileArgs tile_args(const s2c_dev &d) {
     p.padded_len = (uint32_t)d.padded_len; p.n_cols = (uint32_t)d.n_cols; p.n_tiles = (uint32_t)d.n_tiles;
     p.kwin = (uint32_t)d.kwin; p.chunk = (uint32_t)d.chunk; p.n_qwords = (uint32_t)d.n_qwords;
     p.runs_bytes = (uint32_t)std::min<int64_t>(16 * std::max<int64_t>(d.n_ops, 1), 0xFFFFFFF0ll);
-    p.mode = 0;
+    p.mode = MODE_RUN;
     p.n_thr = d.n_thr; p.min_depth = d.min_depth; p.fill_len = d.fill_len; p.fill_nondash = d.fill_nondash;
     return p;
 }
@@ -1208,11 +1215,23 @@ extern "C" int s2c_pileup_counts(const s2c_dev *d, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     if ((rc = s2c_launch_reads(d, s, true))) return rc;   // run records of every piece
     TileArgs a = tile_args(*d);
-    a.mode = 1;
+    a.mode = MODE_STORE;
     if (d->n_deep > 0) {
         k_prep<<<(unsigned)d->n_deep, WG, 0, s>>>(a, d->deep);
         if ((rc = hip_check(hipGetLastError(), "k_prep"))) return rc;
     }
+    if ((rc = launch_tiles(a, d->tile_max, d->dense, d->n_dense, s))) return rc;
+    return launch_tiles(a, d->tile_max, d->items, d->n_items, s);
+}
+
+extern "C" int s2c_accumulate(const s2c_dev *d, int keep_tables, void *stream) {
+    int rc = check_dev(d);
+    if (rc) return rc;
+    if (!d->counts) return s2c_set_error(S2C_ERR_ARG, "counts buffer required");
+    hipStream_t s = (hipStream_t)stream;
+    if ((rc = s2c_launch_reads(d, s, true))) return rc;   // run records of every piece; events hashed
+    TileArgs a = tile_args(*d);
+    a.mode = keep_tables ? MODE_ADD_KEEP : MODE_ADD;
     if ((rc = launch_tiles(a, d->tile_max, d->dense, d->n_dense, s))) return rc;
     return launch_tiles(a, d->tile_max, d->items, d->n_items, s);
 }

@@ -61,7 +61,7 @@ class Workspace:
     """All scratch + output buffers for one (batch, thresholds, fill, maxdel) configuration."""
 
     def __init__(self, db: DeviceBatch, thresholds, min_depth=1, fill=b"-", keep_counts=False,
-                 maxdel_active=None, maxdel=None):
+                 maxdel_active=None, maxdel=None, counts=None):
         dev = db.device
         i = db.info
         self.db = db
@@ -80,7 +80,12 @@ class Workspace:
         self.ibkt, self.ilong, self.ilong_n = z8(sz.ibkt), u8(sz.ilong), z8(sz.ilong_n)
         # counts live in HBM only for deep / general tiles (unless a test asks for all of them)
         self.keep_counts = keep_counts
-        self.counts = u8(6 * i.padded_len * 4 if keep_counts else sz.counts)
+        if counts is not None:   # running totals shared by streamed batches (u8 view, 6·L u32)
+            if counts.numel() * counts.element_size() < 6 * i.padded_len * 4:
+                raise ValueError("counts buffer smaller than 6 x padded_len u32")
+            self.counts = counts
+        else:
+            self.counts = u8(6 * i.padded_len * 4 if keep_counts else sz.counts)
         self.ins_cols = u8(sz.ins_cols)
         self.ins_chr = u8(sz.ins_chr)
         self.blk_len = u8(sz.blk_len)
@@ -153,6 +158,21 @@ class Workspace:
         self.graph.replay()
 
     # ---- results
+    def accumulate(self, keep_tables=False):
+        """Streamed batch of unsorted input: this batch's counts added to ``counts``."""
+        L.check(lib.s2c_accumulate(C.byref(self.dev), 1 if keep_tables else 0, self.stream_handle()))
+
+    def vote_all(self):
+        """Last streamed batch of unsorted input: k_consensus votes every tile from ``counts``
+        (after ``accumulate(keep_tables=True)``)."""
+        nt = int(self.db.info.n_tiles)
+        if nt == 0:
+            return
+        self._all_tiles = torch.arange(nt, dtype=torch.int32, device=self.db.device)
+        d = L.Dev.from_buffer_copy(self.dev)
+        d.deep, d.n_deep = _ptr(self._all_tiles), nt
+        L.check(lib.s2c_consensus(C.byref(d), self.stream_handle()))
+
     def pileup_counts(self):
         """Diagnostic: k_reads, then every tile's counts stored to `counts` (no vote); needs
         keep_counts=True; returns counts[6][padded_len] as numpy u32."""

@@ -25,8 +25,12 @@ and every later one, and no read pass error can follow it unseen); vote errors r
 ``build_records`` over the merged stats.
 
 Input that is not coordinate-sorted is detected (a read parsed after a retain reaching
-below it) and the driver raises ``NotSorted``; ``consensus_files_streamed`` then re-parses
-the file as one batch.
+below it) and ``stream_batches`` raises ``NotSorted``; ``consensus_files_streamed`` then
+re-reads the file with ``stream_unsorted``: each batch's counts are added into running
+totals counts[6][padded_len] in HBM (``s2c_accumulate``) and its reads dropped except their
+insertion events, which the last batch holds all of and votes every tile over the totals.
+Host memory is then bounded by one batch plus the reads with insertions, as the
+reference's is by its count tables (:206-221).
 """
 from __future__ import annotations
 
@@ -68,6 +72,9 @@ class StreamParser(Parser):
 
     def retain(self, gmin):
         L.check(L.lib.s2c_parser_retain(self._p, int(gmin)))
+
+    def retain_events(self):
+        L.check(L.lib.s2c_parser_retain_events(self._p))
 
     def state(self):
         """(late, last reference index, last POS-1, reads held)."""
@@ -179,6 +186,90 @@ def stream_batches(blocks, thresholds, runner, maxdel_active=True, tile_width=DE
                         [(a, b) for a, b, _, _ in parts], held_max)
 
 
+class DeviceAccumulator:
+    """Running totals counts[6][padded_len] u32 in HBM for unsorted input: ``add`` runs a
+    batch's pileup into them (s2c_accumulate), ``finish`` adds the last batch and votes every
+    tile from them (s2c_consensus over all tiles)."""
+
+    def __init__(self, thresholds, min_depth=1, fill=b"-", device=None):
+        self.thresholds, self.min_depth, self.fill, self.device = thresholds, min_depth, fill, device
+        self.counts = None
+
+    def _ws(self, hb):
+        import torch
+
+        from .engine import DeviceBatch, Workspace
+        db = DeviceBatch(hb, self.device)
+        if self.counts is None:
+            self.counts = torch.zeros(max(6 * int(hb.info.padded_len) * 4, 16), dtype=torch.uint8, device=db.device)
+        return Workspace(db, self.thresholds, self.min_depth, self.fill, counts=self.counts)
+
+    def add(self, hb):
+        import torch
+        ws = self._ws(hb)
+        ws.accumulate(keep_tables=False)
+        torch.cuda.synchronize(ws.db.device)   # the batch's buffers are freed after this
+
+    def finish(self, hb):
+        ws = self._ws(hb)
+        ws.accumulate(keep_tables=True)
+        ws.vote_all()
+        return ws.fetch()
+
+
+def stream_unsorted(blocks, thresholds, acc, maxdel_active=True, batch_bytes=DEFAULT_BATCH):
+    """Unsorted input in bounded host memory: every ``batch_bytes`` the reads held are
+    counted into the accumulator's running totals and dropped, except their insertion
+    events (``s2c_parser_retain_events``); the last batch holds every event of the file and
+    is voted over the totals.  Same bytes and error precedence as one batch: the read-pass
+    checks run as blocks are fed, and the last ``s2c_parser_finish`` sees every insertion
+    event for the checks of :284-294."""
+    p = StreamParser(maxdel_active, 150, 0)
+    cov = None
+    lines = mapped = pending = nb = held_max = 0
+    broken = False
+
+    def absorb(hb):
+        nonlocal cov, lines, mapped
+        flag = (hb.ref_reads > 0)
+        cov = flag.copy() if cov is None else (cov | flag)
+        lines += int(hb.info.lines_total)
+        mapped += int(hb.info.reads_mapped)
+
+    try:
+        for blk in blocks:
+            p.feed(blk)
+            pending += len(blk)
+            if broken or pending < batch_bytes:
+                continue
+            pending = 0
+            _, ref, _, held = p.state()
+            if ref < 0:
+                continue
+            held_max = max(held_max, held)
+            try:
+                hb = p.snapshot()
+            except (KeyError, IndexError):
+                broken = True          # raised by s2c_parser_finish once the input is read
+                continue
+            try:
+                acc.add(hb)
+                absorb(hb)
+            finally:
+                hb.free()
+            p.retain_events()
+            nb += 1
+        hb = p.finish()
+        held_max = max(held_max, p.state()[3])
+    finally:
+        p.close()
+    stats, offs, out = acc.finish(hb)
+    absorb(hb)
+    hb.ref_reads = cov.astype(np.int64)
+    return StreamResult(hb, stats, offs, out, int(hb.info.header_lines), lines, mapped,
+                        [(0, int(hb.info.n_tiles))] * (nb + 1), held_max)
+
+
 def _merge(parts, T):
     from .shard import merge_outputs
     return merge_outputs(parts, T)
@@ -208,8 +299,8 @@ def device_runner(thresholds, min_depth, fill, device=None):
 
 def consensus_files_streamed(filename, thresholds, prefix, min_depth=1, fill=b"-", nchar=0, maxdel_active=True,
                              device=None, log=None, batch_bytes=DEFAULT_BATCH, tile_width=DEFAULT_TILE):
-    """``cli.consensus_files`` in streamed batches; unsorted input falls back to one batch."""
-    from .cli import RunResult, _log_summary, consensus_files
+    """``cli.consensus_files`` in streamed batches (unsorted input: counts accumulated)."""
+    from .cli import RunResult, _log_summary
     from .records import build_records, render
 
     t = {}
@@ -217,8 +308,9 @@ def consensus_files_streamed(filename, thresholds, prefix, min_depth=1, fill=b"-
     try:
         res = stream_batches(file_blocks(filename), thresholds, device_runner(thresholds, min_depth, fill, device),
                              maxdel_active, tile_width, batch_bytes)
-    except NotSorted:
-        return consensus_files(filename, thresholds, prefix, min_depth, fill, nchar, maxdel_active, device, log)
+    except NotSorted:   # counts added batch by batch into running totals in HBM
+        res = stream_unsorted(file_blocks(filename), thresholds,
+                              DeviceAccumulator(thresholds, min_depth, fill, device), maxdel_active, batch_bytes)
     t["stream"] = time.perf_counter() - t0
     if log:
         _log_summary(log, res)

@@ -50,7 +50,7 @@ def main():
     batch_mb = int(sys.argv[2]) if len(sys.argv) > 2 else 256
     from sam2consensus_amd import configs
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
-        path = os.path.join(td, name + ".sam")
+        path = os.path.join(td, name + (".sam.gz" if name == "c3" else ".sam"))   # C3 is a SAM.gz config
         n = configs.synth_write(name, path)
         size = os.path.getsize(path)
         res = {"config": name, "reads": n, "sam_bytes": size, "batch_mb": batch_mb}

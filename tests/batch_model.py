@@ -280,10 +280,13 @@ def model_columns(events):
     return cols
 
 
-def model_pipeline(hb, thresholds, min_depth=1, fill=b"-", maxdel_active=None):
-    """(stats[R,T,4], offs[T*nb+1], out bytes) as the device produces them."""
+def model_pipeline(hb, thresholds, min_depth=1, fill=b"-", maxdel_active=None, counts_add=None):
+    """(stats[R,T,4], offs[T*nb+1], out bytes) as the device produces them; ``counts_add``:
+    running totals of earlier streamed batches added to this batch's counts."""
     runs, events = model_reads(hb, maxdel_active)
     counts = model_counts(hb, runs)
+    if counts_add is not None:
+        counts = counts + counts_add
     cols = model_columns(events)
     T = len(thresholds)
     cov = counts.sum(axis=0)

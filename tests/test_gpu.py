@@ -219,6 +219,51 @@ def test_cli_streamed_and_unsorted_fallback(tmp_path, monkeypatch):
     assert got == want
 
 
+def test_unsorted_accumulation_on_device_kat():
+    """Every KAT case through streamed batches of unsorted input on the device (counts added
+    into HBM running totals, the last batch voted over them): the reference's bytes / class."""
+    from sam2consensus_amd import stream
+    from sam2consensus_amd.records import build_records, render
+    for case in golden_io.load("kat"):
+        opt = o.parse_argv(["-i", "in.sam"] + case["args"])
+        data = case["sam"].encode("latin-1")
+        blocks = (data[k:k + 29] for k in range(0, len(data), 29))
+        try:
+            res = stream.stream_unsorted(blocks, opt.thresholds,
+                                         stream.DeviceAccumulator(opt.thresholds, opt.min_depth,
+                                                                  opt.fill.encode("latin-1")),
+                                         opt.maxdel_active, 60)
+            recs = build_records(res.hb, opt.thresholds, opt.prefix, res.stats, res.offs, res.out)
+            files = {n + "__" + opt.prefix + ".fasta": render(r, opt.n).decode("latin-1") for n, r in recs.items()}
+        except (KeyError, IndexError, ValueError, ZeroDivisionError, OverflowError) as e:
+            assert type(e).__name__ == case["status"], case["name"]
+            continue
+        assert case["status"] == "ok" and files == case["files"], case["name"]
+
+
+@pytest.mark.parametrize("name,over,args", [
+    ("c2", {"n_refs": 40, "shuffle": 1}, ["-c", "0.25,0.50,0.75"]),
+    ("c5nd", {"ref_len": 300_000, "shuffle": 1, "long_del_frac": 0.05}, []),
+    ("c4", {"ref_len": 3000, "depth": 10000.0, "shuffle": 1}, [])])
+def test_unsorted_accumulation_on_device_configs(tmp_path, name, over, args):
+    """Shuffled synthetic configs (insertions, maxdel drops, deep tiles) in 7+ streamed
+    batches through s2c_accumulate == the oracle."""
+    from sam2consensus_amd import configs, stream
+    from sam2consensus_amd.records import build_records, render
+    path = str(tmp_path / (name + ".sam"))
+    configs.synth_write(name, path, **over)
+    opt = o.parse_argv(["-i", path] + args)
+    size = os.path.getsize(path)
+    res = stream.stream_unsorted(stream.file_blocks(path, max(4096, size // 32)), opt.thresholds,
+                                 stream.DeviceAccumulator(opt.thresholds, opt.min_depth, opt.fill.encode()),
+                                 opt.maxdel_active, size // 7 + 1)
+    assert len(res.batches) >= 7
+    recs = build_records(res.hb, opt.thresholds, opt.prefix.encode(), res.stats, res.offs, res.out)
+    got = {n + "__" + opt.prefix + ".fasta": render(r, opt.n).decode("latin-1") for n, r in recs.items()}
+    want, _ = o.run_path(path, args)
+    assert got == want
+
+
 @pytest.mark.parametrize("name,over,thr,md,fill", [
     ("c2", {"n_refs": 6}, [0.25, 0.5, 0.75], 1, b"-"),
     # long insertions: > 1024 insertion columns in a tile → the HBM column path

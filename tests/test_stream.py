@@ -147,3 +147,72 @@ def test_retain_bounds_the_reads_held(tmp_path):
     assert _files(res, opt) == whole
     assert res.held_max < 0.4 * hb.info.reads_mapped
     assert np.array_equal(res.stats.sum(axis=0), st.sum(axis=0))
+
+
+class ModelAccumulator:
+    """stream.DeviceAccumulator on the CPU model: running totals of the batches' counts."""
+
+    def __init__(self, opt):
+        self.opt, self.counts = opt, None
+
+    def add(self, hb):
+        c = bm.model_counts(hb)
+        self.counts = c if self.counts is None else self.counts + c
+
+    def finish(self, hb):
+        o_ = self.opt
+        return bm.model_pipeline(hb, o_.thresholds, o_.min_depth, o_.fill.encode("latin-1"), counts_add=self.counts)
+
+
+def _stream_unsorted(sam, args, block=97, batch_bytes=300):
+    opt = o.parse_argv(["-i", "in.sam"] + list(args))
+    data = sam.encode("latin-1") if isinstance(sam, str) else sam
+    res = stream.stream_unsorted(_blocks(data, block), opt.thresholds, ModelAccumulator(opt), opt.maxdel_active,
+                                 batch_bytes)
+    return res, _files(res, opt)
+
+
+def _shuffled_case(seed=5):
+    sam = _sorted_case()
+    head = [ln for ln in sam.splitlines(True) if ln.startswith("@")]
+    body = [ln for ln in sam.splitlines(True) if not ln.startswith("@")]
+    np.random.default_rng(seed).shuffle(body)
+    return "".join(head + body)
+
+
+@pytest.mark.parametrize("args", [[], ["-c", "0.25,0.75"], ["-d", "9"], ["-m", "3", "-f", "N"]])
+def test_unsorted_accumulation_matches_reference(args):
+    sam = _shuffled_case()
+    res, files = _stream_unsorted(sam, args)
+    assert len(res.batches) > 5
+    assert files == o.run_case(sam, args)["files"]
+    hb = batch.parse_text(sam)
+    assert (res.lines_total, res.reads_mapped) == (hb.info.lines_total, hb.info.reads_mapped)
+    # only reads with insertion events are carried to the last batch
+    assert res.held_max < hb.info.reads_mapped / 2
+
+
+def test_unsorted_accumulation_on_every_kat_case():
+    """Every KAT case through the accumulation driver: the reference's files or exception."""
+    for case in golden_io.load("kat"):
+        try:
+            _, files = _stream_unsorted(case["sam"], case["args"], block=11, batch_bytes=30)
+        except (KeyError, IndexError, ValueError, ZeroDivisionError, OverflowError) as e:
+            assert type(e).__name__ == case["status"], case["name"]
+            continue
+        assert case["status"] == "ok" and files == case["files"], case["name"]
+
+
+def test_unsorted_accumulation_shuffled_config(tmp_path):
+    """C3's shuffled record order (reduced) in 6+ batches == the whole batch."""
+    path = str(tmp_path / "c3.sam.gz")
+    configs.synth_write("c3", path, scale=0.001)
+    opt = o.parse_argv(["-i", path, "-m", "10"])
+    with pytest.raises(stream.NotSorted):
+        stream.stream_batches(stream.file_blocks(path, 1 << 16), opt.thresholds, _runner(opt), True, 256, 1 << 17)
+    size = sum(len(b) for b in stream.file_blocks(path))
+    res = stream.stream_unsorted(stream.file_blocks(path, 1 << 15), opt.thresholds, ModelAccumulator(opt), True,
+                                 size // 6)
+    assert len(res.batches) >= 6
+    want, _ = o.run_path(path, ["-m", "10"])
+    assert _files(res, opt) == want
