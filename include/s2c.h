@@ -119,7 +119,7 @@ int s2c_layout(int64_t *out, int n);
    at the boundary below the source), run records, the walk's queues (64 entries per wave and
    walk iteration: ≤ pieces + 128).  Device arrays must be
    readable up to their end rounded up to 16 bytes. */
-#define S2C_DENSE_BYTES(ns, nq) (((4 * (ns) + 30) & ~15) + ((8 * (nq) + 30) & ~15) + ((12 * (ns) + 512 + 15) & ~15))
+#define S2C_DENSE_BYTES(ns, nq) (((4 * (ns) + 30) & ~15) + ((8 * (nq) + 30) & ~15) + ((12 * (ns) + 1024 + 15) & ~15))
 #define S2C_DENSE_QW   4096  /* base plane words of a dense tile's window (17-bit query offsets) */
 #define S2C_SHORT_MOTIF  16  /* motifs up to this length are hashed inline (3-bit codes) */
 #define S2C_CODE_FILL     0  /* internal vote char of a fill position */

@@ -360,8 +360,9 @@ __device__ __forceinline__ Win win_of(const DenseArgs &d, uint32_t item) {
     v.nwords = (v.n + 31) / 32;
     return v;
 }
-// The window's arrays in LDS (S2C_DENSE_BYTES layout): op words, planes, non-ACGT plane
-// (each at its source's 16-byte phase, dma16), run records, the walk's two queues.
+// The window's arrays in LDS (S2C_DENSE_BYTES layout): op words, planes (each at its
+// source's 16-byte phase, dma16), run records + RUN_PAD zero records, the walk's queues.
+constexpr uint32_t RUN_PAD = 64;   // zero records after the last: a count group's reads past it
 struct WinLds {
     const uint32_t *opl;
     const uint2 *bql;
@@ -379,7 +380,7 @@ __device__ __forceinline__ WinLds win_lds(const DenseArgs &d, const Win &v, uint
     L.bql = (const uint2 *)phase16(buf, sbq);
     buf += dma16_bytes(2 * v.nqw);
     L.runl = (uint2 *)buf;
-    L.q = (uint32_t *)(L.runl + v.nslot);
+    L.q = (uint32_t *)(L.runl + v.nslot + RUN_PAD);
     return L;
 }
 // issue the LDS-DMA of window v into buf, shared by the tile's waves (completion: every wave's
@@ -537,48 +538,45 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         for (int b = 0; b < 8; b++) C[c][b] = 0;
     const uint32_t nrec = cw0 + g < cw1 ? (cw1 - cw0 - g + G - 1) / G : 0u;
     const uint32_t ngrp = ABL(2) ? 0u : uni(__ockl_wfred_max_u32((nrec + GSD - 1) / GSD));
-    // the next group's run records are read while this group's plane words are in flight
-    uint2 rvn[GSD];
-    auto load_runs = [&](uint32_t gi) {
-#pragma unroll
-        for (int u = 0; u < GSD; u++) {
-            const uint32_t m = gi * GSD + u;
-            rvn[u] = runl[m < nrec ? cw0 + g + G * m : 0u];   // (unconditional: the group's reads in flight together)
-        }
-    };
-    if (ngrp) load_runs(0);
+    // Group gi reads records cw0 + g + G·(8 gi + u), u < 8, by immediate offsets from one base
+    // clamped to the end of the records: every slot past this lane's candidates is a record of
+    // a piece starting in a later word (or a zero pad record), so it covers nothing here.
+    // The planes are aligned to the word's bit 0 (query base b of position 32·W; a record
+    // outside the word reads any LDS word, masked off).
+    const uint32_t rend = v.nslot;
     const int32_t W32 = (int32_t)(32 * W);
-    const uint32_t kwmax = v.nqw;   // (plane word index clamp: a record outside the word reads a harmless word)
-    for (uint32_t gi = 0; gi < ngrp; gi++) {
-        uint32_t vd[GSD], lo[GSD], sh[GSD];   // covered bits, first covered bit, plane shift
+    auto load_runs = [&](uint2 (&rv)[GSD], uint32_t gi) {
+        const uint2 *rb = runl + min(cw0 + g + G * GSD * gi, rend);
+#pragma unroll
+        for (int u = 0; u < GSD; u++) rv[u] = rb[G * u];
+    };
+    // one group's 8 records → Harley–Seal tree of each plane; returns the weight-8 carries
+    auto count_group = [&](const uint2 (&rv)[GSD], uint32_t (&t8o)[4]) {
+        uint32_t bm[GSD], fx[GSD], sh[GSD];
         uint2 pa[GSD], pb[GSD];
 #pragma unroll
         for (int u = 0; u < GSD; u++) {
-            const uint32_t m = gi * GSD + u;
-            const uint2 rv = rvn[u];
-            // the run in word coordinates, clamped to [0, 32]: covered bits [l0, h0)
-            const int32_t s0 = m < nrec ? (int32_t)rv.x - W32 : 64;   // (padding slots: outside the word)
-            const int32_t e0 = s0 + (int32_t)((rv.y >> 4) & 0x7FFu);
-            const uint32_t l0 = (uint32_t)min(max(s0, 0), 32);
-            const uint32_t h0 = (uint32_t)min(max(e0, 0), 32);
-            const uint32_t nb = h0 > l0 ? h0 - l0 : 0u;
-            vd[u] = nb >= 32 ? 0xFFFFFFFFu : __builtin_amdgcn_ubfe(0xFFFFFFFFu, 0, nb) << l0;
-            const uint32_t qs = (rv.y >> 15) + l0 - (uint32_t)s0;   // query base of the first covered position
-            const uint32_t kw = min(qs >> 5, kwmax);
-            lo[u] = l0;
-            sh[u] = qs & 31u;
-            pa[u] = bql[kw];
-            pb[u] = bql[kw + 1];
+            const int32_t s0 = (int32_t)rv[u].x - W32;
+            const int32_t e0 = s0 + (int32_t)__builtin_amdgcn_ubfe(rv[u].y, 4, 11);
+            const uint32_t l0 = (uint32_t)min(max(s0, 0), 32);   // (v_med3_i32)
+            const uint32_t nb = (uint32_t)min(max(e0, 0), 32) - l0;
+            uint32_t m;
+            asm("v_bfm_b32 %0, %1, %2" : "=v"(m) : "v"(nb), "v"(l0));   // nb bits at l0 (nb < 32)
+            bm[u] = m;
+            fx[u] = (uint32_t)__builtin_amdgcn_sbfe((int32_t)nb, 5, 1);    // all ones iff nb = 32
+            const int32_t b = (int32_t)(rv[u].y >> 15) - s0;
+            sh[u] = (uint32_t)b;
+            const uint2 *pw = bql + (b >> 5);
+            pa[u] = pw[0];
+            pb[u] = pw[1];
         }
-        if (gi + 1 < ngrp) load_runs(gi + 1);
-        // one Harley–Seal tree per plane (tree8 + close8), fed a pair of records at a time
         uint32_t pend[4], t2a[4], t4a[4];
 #pragma unroll
         for (int u = 0; u < GSD; u++) {
-            const uint32_t v0 = vd[u];
-            const uint32_t x = (funnel(pb[u].x, pa[u].x, sh[u]) << lo[u]) & v0;
-            const uint32_t y = (funnel(pb[u].y, pa[u].y, sh[u]) << lo[u]) & v0;
-            const uint32_t mk[4] = {x, y, x & y, v0};
+            uint32_t x, y;   // x & (bm | fx)
+            asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe0" : "=v"(x) : "v"(funnel(pb[u].x, pa[u].x, sh[u])), "v"(bm[u]), "v"(fx[u]));
+            asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe0" : "=v"(y) : "v"(funnel(pb[u].y, pa[u].y, sh[u])), "v"(bm[u]), "v"(fx[u]));
+            const uint32_t mk[4] = {x, y, x & y, bm[u] | fx[u]};
 #pragma unroll
             for (int c = 0; c < 4; c++) {
                 if ((u & 1) == 0) {
@@ -597,11 +595,27 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
                     t4a[c] = t4;
                     continue;
                 }
-                uint32_t t8;
-                csa(t8, C[c][2], C[c][2], t4a[c], t4);
-                close8(C[c], t8);
+                csa(t8o[c], C[c][2], C[c][2], t4a[c], t4);
             }
         }
+    };
+    // two groups per trip (ping-pong record buffers; the next group's records are read while
+    // this group's plane words are in flight), their weight-8 carries closed together
+    uint2 ra[GSD], rb2[GSD];
+    if (ngrp) load_runs(ra, 0);
+    for (uint32_t gi = 0; gi < ngrp; gi += 2) {
+        uint32_t t8a[4], t8b[4];
+        if (gi + 1 < ngrp) load_runs(rb2, gi + 1);
+        count_group(ra, t8a);
+        if (gi + 1 >= ngrp) {
+#pragma unroll
+            for (int c = 0; c < 4; c++) close8(C[c], t8a[c]);
+            break;
+        }
+        if (gi + 2 < ngrp) load_runs(ra, gi + 2);
+        count_group(rb2, t8b);
+#pragma unroll
+        for (int c = 0; c < 4; c++) close16(C[c], t8a[c], t8b[c]);
     }
     PROF_MARK(5);
     // the byte counters of this lane's rows (final since the walk): read now, used by the vote
@@ -855,6 +869,8 @@ __global__ __launch_bounds__(WT) void k_tile_dense(const DenseArgs d) {
     const Win v = win_of(d, item);
     uint8_t *const buf = (uint8_t *)arena;
     win_issue<WPT>(d, v, buf);
+    const WinLds wl = win_lds(d, v, buf);
+    if (tid < RUN_PAD) wl.runl[v.nslot + tid] = make_uint2(0u, 0u);   // (the DMA does not write there)
     // with the DMA: the thread's piece records and its word's run-slot range
     constexpr int G = WGD / (NWP / WPT);
     uint4 Pp[PFN];
@@ -884,7 +900,7 @@ __global__ __launch_bounds__(WT) void k_tile_dense(const DenseArgs d) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the window landed
     lds_sync();
-    dense_tile<NWP>(d, v, win_lds(d, v, buf), dcnt, ncnt, ccnt, amb, fill0, Pp, oe, cw0, cw1, t_entry, stl);
+    dense_tile<NWP>(d, v, wl, dcnt, ncnt, ccnt, amb, fill0, Pp, oe, cw0, cw1, t_entry, stl);
 }
 
 template <int NWP>
