@@ -48,4 +48,11 @@ isa:
 clean:
 	rm -rf $(BUILD) $(OUT)
 
-.PHONY: all clean isa prof
+.PHONY: all clean isa prof variant
+
+# experiment build: k_tile_dense with extra defines (V=name VDEFS='-D...'): libs2c_$(V).so
+V ?= var
+VDEFS ?=
+variant: $(BUILD)/s2c_host.o $(BUILD)/s2c_synth.o $(BUILD)/s2c_reads.o $(BUILD)/s2c_tile.o
+	$(HIPCC) $(HIPFLAGS) $(VDEFS) -c $(SRC)/s2c_dense.hip -o $(BUILD)/s2c_dense_$(V).o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ $(BUILD)/s2c_dense_$(V).o -lz -lpthread -o sam2consensus_amd/libs2c_$(V).so

@@ -457,12 +457,31 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         const uint32_t fl = P.w >> 24, slen = P.w & 0xFFFFFFu, j = P.z - o0;
         const uint32_t op = w0 & 15u, l = w0 >> 4;
         const bool xf = (fl & S2C_PF_X) != 0;
+        const bool plain = in && (fl & ~(uint32_t)S2C_PF_X) == 0u && op_bases(op) && !(xf && mda);
+        const uint32_t nops = oend - P.z;
         // one M / = / X token and nothing else: seqout = SEQ[0 : min(l, len(SEQ))] (:64-69)
-        const bool fast = in && oend - P.z == 1u && (fl & ~(uint32_t)S2C_PF_X) == 0u && op_bases(op) && !(xf && mda);
+        const bool fast = plain && nops == 1u;
         const uint32_t take = min(l, slen), q = 16u * (P.y - 2u * qw0);
         if (fast) runl[j] = make_uint2(P.x, (q << 15) | (take << 4) | S2C_RUN_BASES | (xf ? S2C_RUN_XBIT : 0u));
-        const uint64_t bs = __ballot(in && !fast), bxm = __ballot(fast && xf);
-        if (in && !fast) queue[nslow + mbcnt(bs)] = k;
+        // bases, D / N / P, bases (the deletion reads; no N / '-' in SEQ): two base runs here
+        // (:64-72: k = take, then l1 '-', then SEQ[l : l + min(l2, len(SEQ) − l)]), the '-' run
+        // queued for the byte counters unless maxdel drops it (:210: l1 dashes)
+        bool fdel = false, fdash = false;
+        if (plain && nops == 3u && !xf) {
+            const uint32_t w1 = opl[j + 1], w2 = opl[j + 2];
+            if (op_dash(w1 & 15u) && op_bases(w2 & 15u)) {
+                const uint32_t l1 = w1 >> 4, t2 = l < slen ? min(w2 >> 4, slen - l) : 0u;
+                fdel = true;
+                fdash = l1 != 0u && !(mda && l1 > d.maxdel);
+                runl[j] = make_uint2(P.x, (q << 15) | (take << 4) | S2C_RUN_BASES);
+                runl[j + 1] = make_uint2(0u, 0u);
+                runl[j + 2] = make_uint2(P.x + take + l1, ((q + l) << 15) | (t2 << 4) | S2C_RUN_BASES);
+            }
+        }
+        // queue: pieces for the general walk, and (tagged) the '-' runs of the deletion reads
+        const bool qd = (in && !fast && !fdel) || fdash;
+        const uint64_t bs = __ballot(qd), bxm = __ballot(fast && xf);
+        if (qd) queue[nslow + mbcnt(bs)] = k | (fdel ? 0x80000000u : 0u);
         if (fast && xf) queue[qcap - 1u - nx - mbcnt(bxm)] = j;
         nslow += (uint32_t)__popcll(bs);
         nx += (uint32_t)__popcll(bxm);
@@ -486,7 +505,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     // A queued piece's record comes from the lane that loaded it (ds_bpermute, all lanes on).
     for (uint32_t base = 0; base < nslow; base += WGD) {
         const uint32_t i = base + lane;
-        const uint32_t k = i < nslow ? queue[i] : 0u, it = k / WT;
+        const uint32_t qe = i < nslow ? queue[i] : 0u, k = qe & 0x7FFFFFFFu, it = k / WT;
         const int src = (int)(4 * (k % WGD));   // (k ≡ this wave's lane mod 64: WT is a multiple of 64)
         uint4 P = make_uint4(0u, 0u, 0u, 0u);
         uint32_t oend = 0;
@@ -506,6 +525,12 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
                 P = ((const uint4 *)d.pc)[pf0 + k];
                 oend = d.pc[4 * (size_t)(pf0 + k + 1) + 2];
             }
+        }
+        if (i < nslow && (qe >> 31)) {   // a deletion read's '-' run (its base runs are written)
+            const uint32_t w0 = opl[P.z - o0], l1 = opl[P.z - o0 + 1] >> 4;
+            const int32_t r0 = (int32_t)(P.x + min(w0 >> 4, P.w & 0xFFFFFFu)) - T0;
+            cnt_range(dcnt, r0, r0 + (int32_t)l1, TL);
+        } else if (i < nslow) {
             const bool lng = ((P.w >> 24) & S2C_PF_LONG) != 0;   // (a long piece starting here does not overlap the tile)
             walk_window(opl, bql, bxl, P, P.z - o0, oend - o0, 16u * (P.y - 2u * qw0), mda, d.maxdel,
                         [&](uint32_t j, uint32_t gp, uint32_t l, uint32_t kind, uint32_t q) {
@@ -847,11 +872,16 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
 #endif
 }
 
+// waves per SIMD the register budget is cut for (variant builds: -DS2C_DENSE_OCC=...)
+#ifndef S2C_DENSE_OCC
+#define S2C_DENSE_OCC
+#endif
+
 // One wave per tile (block b → item, XCD-major: the blocks of one XCD, b ≡ x mod 8, take a
 // contiguous range of items, so neighbouring windows meet in that XCD's L2).  Everything the
 // tile needs arrives by one LDS-DMA round trip after the scalar loads of its tile record.
 template <int NWP>
-__global__ __launch_bounds__(WT) void k_tile_dense(const DenseArgs d) {
+__global__ __launch_bounds__(WT) S2C_DENSE_OCC void k_tile_dense(const DenseArgs d) {
     extern __shared__ uint4 arena[];   // the window (S2C_DENSE_BYTES layout)
     // one byte per position (row layout): '-' (D/N/P runs, '-' of SEQ unless maxdel drops
     // the read's), 'N' of SEQ, '-' of SEQ (all: the planes count them as C, and 'N' as A)
