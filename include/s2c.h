@@ -168,6 +168,26 @@ int  s2c_parser_stream_state(const s2c_parser *p, int64_t *state);
  * (s2c_parser_finish) then holds every insertion event of the file. */
 int  s2c_parser_retain_events(s2c_parser *p);
 
+/* Distributed parse for the multi-GPU CLI (sam2consensus_amd/dparse.py; the reference
+ * parses on one core, :185-228).  Each rank parses its blocks of the file with its own
+ * parser, routes every read to the ranks whose tile range it can change, and plans its
+ * sub-batch from the reads it receives.  Each call first parses a pending last line.
+ *   pos_weights: w[g >> shift] += len(counted seqout) of each read held, g = the first
+ *                global position it can change (n entries).
+ *   checks:      per reference r, bad[2r] = an insertion motif base outside -ACGNT (:287),
+ *                bad[2r + 1] = an insertion key outside the coverage list (:294).
+ *   counters:    {header_lines, lines_total, reads_mapped, aligned_bases} of this parser.
+ *   pack:        the reads held that can change a global position in [g0, g1) (tokens,
+ *                planes, events; no line counters) into a blob of *len bytes, kept by the
+ *                parser until the next pack; blob_copy copies it out.
+ *   unpack:      append a blob's reads (read order = order of the unpack calls). */
+int  s2c_parser_pos_weights(s2c_parser *p, int64_t shift, int64_t *w, int64_t n);
+int  s2c_parser_checks(s2c_parser *p, uint8_t *bad, int64_t n_refs);
+int  s2c_parser_counters(s2c_parser *p, int64_t *out);
+int  s2c_parser_pack(s2c_parser *p, int64_t g0, int64_t g1, size_t *len);
+int  s2c_parser_blob_copy(const s2c_parser *p, void *dst, size_t cap);
+int  s2c_parser_unpack(s2c_parser *p, const void *blob, size_t len);
+
 typedef struct {
     int64_t n_refs;            /* @SQ references (:160-169) */
     int64_t total_len;         /* Σ LN over refs (real positions) */

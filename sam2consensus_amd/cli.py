@@ -142,35 +142,44 @@ def _dist_env():
         int(os.environ.get("LOCAL_RANK", "0"))
 
 
+class _Counters:
+    """The summary counters of the distributed read pass (``_log_summary``'s fields)."""
+
+    def __init__(self, n_refs, parsed):
+        self.n_refs = n_refs
+        self.header_lines, self.lines_total, self.reads_mapped = \
+            parsed.header_lines, parsed.lines_total, parsed.reads_mapped
+
+
 def consensus_files_sharded(filename, thresholds, prefix, min_depth, fill, nchar, maxdel_active, log=None):
-    """One process per GPU (torchrun): every rank parses, runs its position-range shard
-    (sam2consensus_amd.shard), stats are all-reduced over RCCL and the FASTA bodies
-    gathered; rank 0 returns the files, other ranks None."""
+    """One process per GPU (torchrun): the file is parsed once across the ranks and each
+    rank receives the reads of its tile range (sam2consensus_amd.dparse), runs it, the
+    stats are all-reduced and the FASTA bodies gathered over the process group (RCCL; the
+    gloo backend with S2C_DIST_BACKEND=gloo); rank 0 returns the files, other ranks None."""
     import torch
     import torch.distributed as dist
 
-    from .batch import parse_file
+    from .dparse import parse_distributed
     from .engine import DeviceBatch, Workspace
     from .records import build_records, render
-    from .shard import run_sharded
+    from .shard import gather_results
 
     world, rank, local = _dist_env()
+    local %= max(torch.cuda.device_count(), 1)   # (ranks sharing a device: gloo tests on one GPU)
     torch.cuda.set_device(local)
     if not dist.is_initialized():
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    hb = parse_file(filename, maxdel_active, 150)
+        backend = os.environ.get("S2C_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend, device_id=torch.device("cuda", local) if backend == "nccl" else None)
+    P = parse_distributed(filename, rank, world, maxdel_active)
     if log and rank == 0:
-        _log_summary(log, hb.info)
-
-    def runner(sub):
-        ws = Workspace(DeviceBatch(sub, "cuda:%d" % local), thresholds, min_depth, fill)
-        ws.run()
-        return ws.fetch()
-
-    res = run_sharded(hb, rank, world, thresholds, runner)
+        _log_summary(log, _Counters(P.hb.info.n_refs, P))
+    ws = Workspace(DeviceBatch(P.sub, "cuda:%d" % local), thresholds, min_depth, fill)
+    ws.run()
+    res = gather_results(ws.fetch(), P.sub, rank, world, len(thresholds))
     if rank != 0:
         return None
-    fastas = build_records(hb, thresholds, prefix, *res)
+    P.hb.ref_reads = P.ref_flags   # Σcoverage > 0 over every rank's reads (:334-341)
+    fastas = build_records(P.hb, thresholds, prefix, *res)
     pre = prefix.encode("latin-1") if isinstance(prefix, str) else prefix
     return {n.encode("latin-1") + b"__" + pre + b".fasta": render(r, nchar) for n, r in fastas.items()}
 

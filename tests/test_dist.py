@@ -116,3 +116,83 @@ def test_gloo_two_ranks_match_reference():
         p.join(timeout=120)
         assert p.exitcode == 0
     assert got == o.run_case(sam, args)["files"]
+
+
+# ---- distributed parse (sam2consensus_amd/dparse.py): every line parsed once, by one rank
+
+def _dparse_worker(rank, world, port, cases, paths, block, q):
+    import torch.distributed as dist
+
+    from sam2consensus_amd import dparse
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = []
+    try:
+        for sam, args, path in [(s, a, None) for s, a in cases] + [(None, a, p) for p, a in paths]:
+            opt = o.parse_argv(["-i", "in.sam"] + args)
+            try:
+                P = dparse.parse_distributed(path, rank, world, opt.maxdel_active,
+                                             block=block if path is None else 1 << 20,
+                                             text=None if sam is None else sam.encode("latin-1"))
+                res = shard.gather_results(bm.model_pipeline(P.sub, opt.thresholds, opt.min_depth,
+                                                             opt.fill.encode("latin-1")),
+                                           P.sub, rank, world, len(opt.thresholds))
+                got = ("ok", None, None)
+                if rank == 0:
+                    P.hb.ref_reads = P.ref_flags
+                    got = ("ok", _files(P.hb, opt, *res), (P.header_lines, P.lines_total, P.reads_mapped))
+            except Exception as e:  # noqa: BLE001 - compared with the reference's class
+                got = (type(e).__name__, {}, None)
+            out.append(got)
+        if rank == 0:
+            q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_dparse(world, cases, paths, block):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dparse_worker, args=(r, world, port, cases, paths, block, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return got
+
+
+@pytest.mark.parametrize("world,block", [(2, 90), (3, 400)])
+def test_distributed_parse_matches_reference(world, block, tmp_path):
+    """KAT cases (errors included: the first failing line in file order, the insertion checks
+    in reference order) and the multi-reference case, cut into many small blocks; plus a
+    scaled C2 as .sam and .sam.gz files against the whole-file parse."""
+    kat = golden_io.load("kat")
+    cases = [(c["sam"], c["args"]) for c in kat]
+    big = _big_case()
+    cases += [(big, a) for a in ([], ["-c", "0.25,0.75"], ["-d", "9"])]
+    want = [(c["status"], c["files"]) for c in kat]
+    want += [("ok", o.run_case(big, a)["files"]) for a in ([], ["-c", "0.25,0.75"], ["-d", "9"])]
+    paths = []
+    if world == 2:
+        for ext in (".sam", ".sam.gz"):
+            p = str(tmp_path / ("c2s" + ext))
+            configs.synth_write("c2", p, scale=0.03)
+            paths.append((p, configs.cli_args("c2")))
+    got = _run_dparse(world, cases, paths, block)
+    assert len(got) == len(want) + len(paths)
+    for k, (g, w) in enumerate(zip(got, want)):
+        assert g[0] == w[0], (k, g[0], w[0])
+        if g[0] == "ok":
+            assert g[1] == w[1], k
+    for (p, args), g in zip(paths, got[len(want):]):
+        opt = o.parse_argv(["-i", "in.sam"] + args)
+        hb = batch.parse_file(p, opt.maxdel_active, 150)
+        assert g[0] == "ok"
+        assert g[1] == _virtual(hb, opt, 1)
+        i = hb.info
+        assert g[2] == (i.header_lines, i.lines_total, i.reads_mapped)

@@ -130,6 +130,54 @@ def test_cli_end_to_end_c1(tmp_path):
     assert got == g["content"]
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_cli_torchrun_distributed_parse(tmp_path):
+    """The multi-GPU CLI (2 ranks under torchrun, the file parsed once across them —
+    sam2consensus_amd/dparse.py — each rank's tile range on the device, bodies gathered):
+    C1 == the reference's files; a scaled C2 .sam.gz == the one-process CLI's files.  Both
+    ranks share this box's one GPU, so the collectives run over gloo."""
+    import subprocess
+    import sys
+    from sam2consensus_amd import configs
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, S2C_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
+
+    def torchrun(inp, out, args):
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+               os.path.join(root, "sam2consensus.py"), "-i", inp, "-o", str(out)] + args
+        r = subprocess.run(cmd, env=env, capture_output=True, timeout=240)
+        assert r.returncode == 0, r.stderr.decode()[-2000:]
+        return r.stdout.decode()
+
+    g = CONFIGS["c1"]
+    sam = str(tmp_path / "c1.sam")
+    configs.synth_write("c1", sam)
+    out = tmp_path / "o1"
+    so = torchrun(sam, out, g["args"])
+    got = {fn: open(os.path.join(out, fn), "rb").read().decode("latin-1") for fn in os.listdir(out)}
+    assert got == g["content"]
+    assert "reads processed." in so and "Done." in so
+    from sam2consensus_amd.cli import main
+    gz = str(tmp_path / "c2.sam.gz")
+    configs.synth_write("c2", gz, scale=0.05)
+    args = configs.cli_args("c2")
+    o2, o1 = tmp_path / "o2", tmp_path / "o1p"
+    torchrun(gz, o2, args)
+    assert main(["-i", gz, "-o", str(o1)] + args) == 0
+    assert sorted(os.listdir(o2)) == sorted(os.listdir(o1))
+    for fn in os.listdir(o1):
+        assert open(os.path.join(o2, fn), "rb").read() == open(os.path.join(o1, fn), "rb").read()
+
+
 def test_cli_failure_writes_nothing(tmp_path):
     from sam2consensus_amd.cli import main
     p = tmp_path / "bad.sam"
