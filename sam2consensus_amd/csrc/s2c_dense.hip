@@ -155,6 +155,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
 }
 typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
 // Scalar loads of uniform read-only words (tile records, items): s_load through the scalar
 // cache, waited here — the compiler would otherwise emit vector loads (the kernel stores to
 // global memory) and wait on vmcnt, i.e. on the window DMA in flight.
@@ -345,17 +346,21 @@ struct Win {
 __device__ __forceinline__ Win win_of(const DenseArgs &d, uint32_t item) {
     Win v;
     v.tile = sload1(d.items + 4 * (size_t)item);
-    const uint32_t *twp = d.tiles + (size_t)v.tile * S2C_TILE_WORDS;
-    const uint4 tw = sload4(twp), tw3 = sload4(twp + 12), tw4 = sload4(twp + 16);
-    v.cb0 = sload1(twp + 8);
-    v.a = tw.x;
-    v.n = tw.y - v.a;
-    v.pf0 = tw3.y;
-    v.npc = tw3.z - v.pf0;
-    v.o0 = tw3.w;
-    v.nslot = tw4.x - v.o0;
-    v.qw0 = tw4.y;
-    v.nqw = tw4.z - v.qw0;
+    // the whole 20-word tile record in one scalar round trip
+    const uint32_t *twp = uni_ptr(d.tiles + (size_t)v.tile * S2C_TILE_WORDS);
+    v16i r;
+    v4i r4;
+    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx4 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
+                 : "=s"(r), "=s"(r4) : "s"(twp) : "memory");
+    v.cb0 = (uint32_t)r[8];
+    v.a = (uint32_t)r[0];
+    v.n = (uint32_t)r[1] - v.a;
+    v.pf0 = (uint32_t)r[13];
+    v.npc = (uint32_t)r[14] - v.pf0;
+    v.o0 = (uint32_t)r[15];
+    v.nslot = (uint32_t)r4.x - v.o0;
+    v.qw0 = (uint32_t)r4.y;
+    v.nqw = (uint32_t)r4.z - v.qw0;
     v.W0 = v.a >> 5;
     v.nwords = (v.n + 31) / 32;
     return v;
@@ -467,45 +472,49 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         // (:64-72: k = take, then l1 '-', then SEQ[l : l + min(l2, len(SEQ) − l)]), the '-' run
         // queued for the byte counters unless maxdel drops it (:210: l1 dashes)
         bool fdel = false, fdash = false;
+        uint32_t da = 0, db = 0;   // the '-' run's tile-relative range, clipped to the tile
         if (plain && nops == 3u && !xf) {
             const uint32_t w1 = opl[j + 1], w2 = opl[j + 2];
             if (op_dash(w1 & 15u) && op_bases(w2 & 15u)) {
                 const uint32_t l1 = w1 >> 4, t2 = l < slen ? min(w2 >> 4, slen - l) : 0u;
+                const int32_t r0 = (int32_t)(P.x + take) - T0;
+                da = (uint32_t)min(max(r0, 0), TL);
+                db = (uint32_t)min(max(r0 + (int32_t)l1, 0), TL);
                 fdel = true;
-                fdash = l1 != 0u && !(mda && l1 > d.maxdel);
+                fdash = db > da && !(mda && l1 > d.maxdel);
                 runl[j] = make_uint2(P.x, (q << 15) | (take << 4) | S2C_RUN_BASES);
                 runl[j + 1] = make_uint2(0u, 0u);
                 runl[j + 2] = make_uint2(P.x + take + l1, ((q + l) << 15) | (t2 << 4) | S2C_RUN_BASES);
             }
         }
-        // queue: pieces for the general walk, and (tagged) the '-' runs of the deletion reads
+        // queue: pieces for the general walk (their index), and the '-' runs of the deletion
+        // reads (1 << 31 | begin << 12 | end, tile-relative: TL ≤ 2048)
         const bool qd = (in && !fast && !fdel) || fdash;
         const uint64_t bs = __ballot(qd), bxm = __ballot(fast && xf);
-        if (qd) queue[nslow + mbcnt(bs)] = k | (fdel ? 0x80000000u : 0u);
+        if (qd) queue[nslow + mbcnt(bs)] = fdel ? 0x80000000u | (da << 12) | db : k;
         if (fast && xf) queue[qcap - 1u - nx - mbcnt(bxm)] = j;
         nslow += (uint32_t)__popcll(bs);
         nx += (uint32_t)__popcll(bxm);
     }
     lds_sync();
     PROF_MARK(2);
-    // the first 64 queued X runs: their run records, plane words (LDS) and non-ACGT words (HBM)
-    // requested now, so the HBM round trip overlaps the general walk of the queued pieces
+    // the first 64 queued X runs: their run records now, and their non-ACGT words from HBM,
+    // so the round trip overlaps the queued walks and the count (the X pass runs after it)
     const bool xin = lane < nx;
     const uint2 xrv = xin ? runl[queue[qcap - 1u - lane]] : make_uint2(0u, 0u);
     const uint32_t xq0 = xrv.y >> 15, xl = (xrv.y >> 4) & 0x7FFu, xwa = xq0 >> 5;
     uint32_t xs[8];
-    uint2 xp[8];
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
-        const uint32_t qw = xin ? min(xwa + u, (xq0 + xl - 1) >> 5) : 0u;
-        xs[u] = xin ? bxl[qw] : 0u;
-        xp[u] = bql[qw];
-    }
+    for (int u = 0; u < 8; u++) xs[u] = xin ? bxl[min(xwa + u, (xq0 + xl - 1) >> 5)] : 0u;
     // queued pieces: the general walk; '-' runs and SEQ N / '-' straight into the byte counters.
     // A queued piece's record comes from the lane that loaded it (ds_bpermute, all lanes on).
     for (uint32_t base = 0; base < nslow; base += WGD) {
         const uint32_t i = base + lane;
-        const uint32_t qe = i < nslow ? queue[i] : 0u, k = qe & 0x7FFFFFFFu, it = k / WT;
+        const uint32_t qe = i < nslow ? queue[i] : 0u;
+        if (i < nslow && (qe >> 31)) cnt_range(dcnt, (int32_t)((qe >> 12) & 0xFFFu), (int32_t)(qe & 0xFFFu), TL);
+        const bool gen = i < nslow && !(qe >> 31);
+        if (!__ballot(gen)) continue;   // (only '-' runs in this round)
+        const uint32_t k = gen ? qe : 0u, it = k / WT;
         const int src = (int)(4 * (k % WGD));   // (k ≡ this wave's lane mod 64: WT is a multiple of 64)
         uint4 P = make_uint4(0u, 0u, 0u, 0u);
         uint32_t oend = 0;
@@ -520,17 +529,11 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             P = me ? make_uint4(px, py, pz, pw) : P;
             oend = me ? pe : oend;
         }
-        if (i < nslow) {
+        if (gen) {
             if (it >= (uint32_t)PFN) {   // (windows of more than WT·PFN pieces)
                 P = ((const uint4 *)d.pc)[pf0 + k];
                 oend = d.pc[4 * (size_t)(pf0 + k + 1) + 2];
             }
-        }
-        if (i < nslow && (qe >> 31)) {   // a deletion read's '-' run (its base runs are written)
-            const uint32_t w0 = opl[P.z - o0], l1 = opl[P.z - o0 + 1] >> 4;
-            const int32_t r0 = (int32_t)(P.x + min(w0 >> 4, P.w & 0xFFFFFFu)) - T0;
-            cnt_range(dcnt, r0, r0 + (int32_t)l1, TL);
-        } else if (i < nslow) {
             const bool lng = ((P.w >> 24) & S2C_PF_LONG) != 0;   // (a long piece starting here does not overlap the tile)
             walk_window(opl, bql, bxl, P, P.z - o0, oend - o0, 16u * (P.y - 2u * qw0), mda, d.maxdel,
                         [&](uint32_t j, uint32_t gp, uint32_t l, uint32_t kind, uint32_t q) {
@@ -543,15 +546,8 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
                         });
         }
     }
+    lds_sync();   // every run record written
     PROF_MARK(3);
-    // queued single-token runs of reads with N / '-' in SEQ (never dropped: maxdel is off)
-    if (xin) x_events_pre(bxl, bql, xs, xp, xq0, xl, (int32_t)xrv.x - T0, TL, false, dcnt, ncnt, ccnt);
-    for (uint32_t i = lane + WGD; i < nx; i += WGD) {
-        const uint2 rv = runl[queue[qcap - 1u - i]];
-        x_events(bxl, bql, rv.y >> 15, (rv.y >> 4) & 0x7FFu, (int32_t)rv.x - T0, TL, false, dcnt, ncnt, ccnt);
-    }
-    lds_sync();
-    PROF_MARK(4);
 
     // ---- count the base records of this lane's word (candidates cw0 + g + G·m < cw1),
     //      bit-sliced by the planes (non-ACGT chars of SEQ as A / C: taken back in the vote), a
@@ -643,7 +639,20 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         for (int c = 0; c < 4; c++) close16(C[c], t8a[c], t8b[c]);
     }
     PROF_MARK(5);
-    // the byte counters of this lane's rows (final since the walk): read now, used by the vote
+    // queued single-token runs of reads with N / '-' in SEQ (never dropped: maxdel is off)
+    if (xin) {
+        uint2 xp[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) xp[u] = bql[min(xwa + u, (xq0 + xl - 1) >> 5)];
+        x_events_pre(bxl, bql, xs, xp, xq0, xl, (int32_t)xrv.x - T0, TL, false, dcnt, ncnt, ccnt);
+    }
+    for (uint32_t i = lane + WGD; i < nx; i += WGD) {
+        const uint2 rv = runl[queue[qcap - 1u - i]];
+        x_events(bxl, bql, rv.y >> 15, (rv.y >> 4) & 0x7FFu, (int32_t)rv.x - T0, TL, false, dcnt, ncnt, ccnt);
+    }
+    lds_sync();   // the byte counters are final
+    PROF_MARK(4);
+    // the byte counters of this lane's rows: read now, used by the vote
     const uint32_t rbase = 8 * w + g * RPL;   // the rows' dword index in the byte counters
     uint32_t rD[RPL], rN[RPL], rX[RPL];       // '-', 'N', '-' of SEQ
 #pragma unroll
