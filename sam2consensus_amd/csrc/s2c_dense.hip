@@ -149,6 +149,10 @@ __device__ __forceinline__ void walk_window(const uint32_t *opl, const uint2 *bq
 
 constexpr int WGD = 64;   // one wave per tile
 constexpr int GSD = 8;    // records per counting group (one Harley–Seal tree)
+#ifndef S2C_CNT_PART
+#define S2C_CNT_PART 2
+#endif
+constexpr int CNT_PART = S2C_CNT_PART;   // records whose geometry and plane words are in registers at once
 
 // LDS byte address of a shared-memory pointer
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
@@ -573,10 +577,13 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     };
     // one group's 8 records → Harley–Seal tree of each plane; returns the weight-8 carries
     auto count_group = [&](const uint2 (&rv)[GSD], uint32_t (&t8o)[4]) {
+        uint32_t pend[4], t2a[4], t4a[4];
+#pragma unroll
+        for (int h = 0; h < GSD; h += CNT_PART) {   // (parts of CNT_PART records: fewer live registers)
         uint32_t bm[GSD], fx[GSD], sh[GSD];
         uint2 pa[GSD], pb[GSD];
 #pragma unroll
-        for (int u = 0; u < GSD; u++) {
+        for (int u = h; u < h + CNT_PART; u++) {
             const int32_t s0 = (int32_t)rv[u].x - W32;
             const int32_t e0 = s0 + (int32_t)__builtin_amdgcn_ubfe(rv[u].y, 4, 11);
             const uint32_t l0 = (uint32_t)min(max(s0, 0), 32);   // (v_med3_i32)
@@ -591,9 +598,8 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             pa[u] = pw[0];
             pb[u] = pw[1];
         }
-        uint32_t pend[4], t2a[4], t4a[4];
 #pragma unroll
-        for (int u = 0; u < GSD; u++) {
+        for (int u = h; u < h + CNT_PART; u++) {
             uint32_t x, y;   // x & (bm | fx)
             asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe0" : "=v"(x) : "v"(funnel(pb[u].x, pa[u].x, sh[u])), "v"(bm[u]), "v"(fx[u]));
             asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe0" : "=v"(y) : "v"(funnel(pb[u].y, pa[u].y, sh[u])), "v"(bm[u]), "v"(fx[u]));
@@ -618,6 +624,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
                 }
                 csa(t8o[c], C[c][2], C[c][2], t4a[c], t4);
             }
+        }
         }
     };
     // two groups per trip (ping-pong record buffers; the next group's records are read while

@@ -1427,6 +1427,23 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     b->tiles.assign((size_t)NT * S2C_TILE_WORDS, 0u);
     uint64_t boff = 0, loff = 0, coff = 0;
     int64_t runs_max = 0;
+    // Launch LDS of k_tile_dense = the largest dense window, so one outlier window sets every
+    // tile's occupancy: when all but ≤ 0.2 % of the windows fit the share of a CU's 160 KB
+    // that lets 8 two-wave tiles reside (4 waves per SIMD, the kernel's register budget),
+    // the rest are not dense (k_tile runs them).
+    int64_t dense_cap = S2C_DENSE_LDS;
+    {
+        const int64_t nwp = tile_max <= 512 ? 16 : tile_max <= 1024 ? 32 : 64;
+        const int64_t cap8 = 163840 / 8 - (96 * nwp + 128);   // (the kernel's static LDS)
+        std::vector<int64_t> db;
+        uint32_t tw[S2C_TILE_WORDS];
+        for (int64_t t = 0; t < NT; t++) {
+            tile_window(b, K, tiles[t].a, tiles[t].b, tw);
+            if (dense_fits(tw, K)) db.push_back(dense_bytes(tw, K));
+        }
+        const int64_t over = (int64_t)std::count_if(db.begin(), db.end(), [&](int64_t x) { return x > cap8; });
+        if (over > 0 && over * 500 <= (int64_t)db.size()) dense_cap = cap8;
+    }
     for (int64_t t = 0; t < NT; t++) {
         const Tile &T = tiles[t];
         const int64_t w0 = T.a >> 5, w1 = (T.b + 31) >> 5;
@@ -1441,7 +1458,9 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
         tile_window(b, K, T.a, T.b, tw);
         uint32_t fl = nch > 1 ? S2C_TILE_DEEP : 0u;
         if (nev[t] > S2C_EPI_KEYS || (int64_t)ccap[t] > lcols) fl |= S2C_TILE_GENERAL;
-        if (fl == 0 && nev[t] == 0 && nlg == 0 && maxc <= 255 && !no_dense && dense_fits(tw, K)) fl = S2C_TILE_DENSE;
+        if (fl == 0 && nev[t] == 0 && nlg == 0 && maxc <= 255 && !no_dense && dense_fits(tw, K) &&
+            dense_bytes(tw, K) <= dense_cap)
+            fl = S2C_TILE_DENSE;
         const uint32_t bcap = nshort[t] ? pow2_at_least(2 * (uint64_t)nshort[t]) : 0u;
         tw[0] = (uint32_t)T.a; tw[1] = (uint32_t)T.b; tw[2] = (uint32_t)T.ref; tw[3] = fl;
         tw[4] = (uint32_t)boff; tw[5] = bcap; tw[6] = (uint32_t)loff; tw[7] = nlong[t];
