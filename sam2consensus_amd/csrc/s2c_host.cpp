@@ -598,14 +598,178 @@ int parse_window(s2c_parser *p, const char *s, size_t n) {
     return S2C_OK;
 }
 
-struct Reader {   // plain or gzip (:111-114) byte source
+// BGZF (the blocked gzip of samtools / bgzip: members of <= 64 KB, each with a 'BC' extra
+// field holding its compressed size) inflated block-parallel: the compressed stream is read
+// in 32 MB pieces, the complete blocks of a piece are located by their sizes and inflated on
+// all host threads straight into their output offsets (ISIZE from each trailer), CRC-checked.
+// A member that is not BGZF-shaped switches the rest of the stream to sequential inflate.
+struct Bgzf {
+    FILE *f = nullptr;
+    std::vector<unsigned char> cb;   // compressed bytes not yet inflated
+    std::vector<char> out;           // inflated bytes of the last piece
+    size_t opos = 0;
+    bool eof = false, seq = false, seq_end = false;
+    z_stream z{};
+    unsigned nt = 1;
+    ~Bgzf() {
+        if (seq) inflateEnd(&z);
+        if (f) fclose(f);
+    }
+    static bool block_at(const unsigned char *p, size_t n, size_t *bsize) {   // a BGZF header at p
+        if (n < 18 || p[0] != 0x1f || p[1] != 0x8b || p[2] != 8 || !(p[3] & 4)) return false;
+        const size_t xlen = p[10] | (p[11] << 8);
+        for (size_t k = 12; k + 4 <= 12 + xlen && k + 4 <= n; ) {   // the 'BC' subfield
+            const size_t sl = p[k + 2] | (p[k + 3] << 8);
+            if (p[k] == 'B' && p[k + 1] == 'C' && sl == 2 && k + 6 <= n) {
+                *bsize = (size_t)(p[k + 4] | (p[k + 5] << 8)) + 1;
+                return *bsize >= 12 + xlen + 8;
+            }
+            k += 4 + sl;
+        }
+        return false;
+    }
+    bool fill_cb() {   // append up to 32 MB; false at end of file
+        const size_t h = cb.size(), want = (size_t)32 << 20;
+        cb.resize(h + want);
+        const size_t r = fread(cb.data() + h, 1, want, f);
+        cb.resize(h + r);
+        return r > 0;
+    }
+    // next piece of output into out; false: no more data (err set on a corrupt stream)
+    bool next(bool &err) {
+        out.clear();
+        opos = 0;
+        if (!seq) {
+            if (!eof && cb.size() < ((size_t)32 << 20)) eof = !fill_cb();
+            std::vector<size_t> off, len, isz;
+            size_t k = 0, total = 0;
+            while (true) {
+                size_t bs;
+                if (!block_at(cb.data() + k, cb.size() - k, &bs)) {
+                    if (cb.size() - k >= 18 || (eof && cb.size() > k)) seq = true;   // not BGZF from here on
+                    break;
+                }
+                if (k + bs > cb.size()) break;   // partial block: the next piece
+                const unsigned char *t = cb.data() + k + bs - 4;
+                const size_t is = (size_t)t[0] | ((size_t)t[1] << 8) | ((size_t)t[2] << 16) | ((size_t)t[3] << 24);
+                off.push_back(k);
+                len.push_back(bs);
+                isz.push_back(total);
+                total += is;
+                k += bs;
+            }
+            if (!off.empty()) {
+                out.resize(total);
+                std::atomic<size_t> nextb{0};
+                std::atomic<bool> bad{false};
+                auto work = [&] {
+                    z_stream zz{};
+                    if (inflateInit2(&zz, -15) != Z_OK) { bad = true; return; }
+                    for (size_t b; (b = nextb++) < off.size();) {
+                        const unsigned char *p = cb.data() + off[b];
+                        const size_t hl = 12 + (size_t)(p[10] | (p[11] << 8));
+                        const size_t dl = len[b] - hl - 8;
+                        const size_t ol = (b + 1 < off.size() ? isz[b + 1] : total) - isz[b];
+                        inflateReset(&zz);
+                        zz.next_in = (Bytef *)(p + hl);
+                        zz.avail_in = (uInt)dl;
+                        zz.next_out = (Bytef *)out.data() + isz[b];
+                        zz.avail_out = (uInt)ol;
+                        const int r = inflate(&zz, Z_FINISH);
+                        const unsigned char *t = p + len[b] - 8;
+                        const uint32_t crc = (uint32_t)t[0] | ((uint32_t)t[1] << 8) | ((uint32_t)t[2] << 16) | ((uint32_t)t[3] << 24);
+                        if (r != Z_STREAM_END || zz.total_out != ol ||
+                            (uint32_t)crc32(0L, (const Bytef *)out.data() + isz[b], (uInt)ol) != crc)
+                            bad = true;
+                    }
+                    inflateEnd(&zz);
+                };
+                std::vector<std::thread> th;
+                const unsigned n = (unsigned)std::min<size_t>(nt, off.size());
+                for (unsigned i = 1; i < n; i++) th.emplace_back(work);
+                work();
+                for (auto &x : th) x.join();
+                if (bad) { err = true; return false; }
+            }
+            cb.erase(cb.begin(), cb.begin() + k);
+            if (seq) {
+                if (inflateInit2(&z, 31) != Z_OK) { err = true; return false; }
+                z.avail_in = 0;
+            }
+            if (!out.empty()) return true;
+            if (!seq) {
+                if (eof) {
+                    if (!cb.empty()) { err = true; return false; }   // a truncated block
+                    return false;
+                }
+                return next(err);
+            }
+        }
+        // sequential inflate of the rest (gzip members one after the other)
+        if (seq_end) return false;
+        out.resize((size_t)8 << 20);
+        size_t have = 0;
+        while (have < out.size()) {
+            if (z.avail_in == 0) {
+                if (cb.empty()) {
+                    if (eof || !fill_cb()) { eof = true; if (cb.empty()) { seq_end = true; break; } }
+                }
+                z.next_in = cb.data();
+                z.avail_in = (uInt)cb.size();
+            }
+            z.next_out = (Bytef *)out.data() + have;
+            z.avail_out = (uInt)(out.size() - have);
+            const uInt before = z.avail_in;
+            const int r = inflate(&z, Z_NO_FLUSH);
+            have = out.size() - z.avail_out;
+            const size_t used = before - z.avail_in;
+            cb.erase(cb.begin(), cb.begin() + used);
+            z.next_in = cb.data();
+            z.avail_in = (uInt)cb.size();
+            if (r == Z_STREAM_END) {
+                if (cb.empty() && eof) { seq_end = true; break; }
+                inflateReset(&z);   // the next member
+                if (cb.empty() && !fill_cb()) { eof = true; seq_end = true; break; }
+                z.next_in = cb.data();
+                z.avail_in = (uInt)cb.size();
+            } else if (r == Z_BUF_ERROR && cb.empty() && eof) {
+                err = true; return false;   // truncated
+            } else if (r != Z_OK && r != Z_BUF_ERROR) {
+                err = true; return false;
+            }
+        }
+        out.resize(have);
+        return have > 0;
+    }
+    long read(char *dst, size_t n) {
+        size_t tot = 0;
+        while (tot < n) {
+            if (opos == out.size()) {
+                bool err = false;
+                if (!next(err)) {
+                    if (err) return -1;
+                    break;
+                }
+            }
+            const size_t k = std::min(n - tot, out.size() - opos);
+            memcpy(dst + tot, out.data() + opos, k);
+            opos += k;
+            tot += k;
+        }
+        return (long)tot;
+    }
+};
+
+struct Reader {   // plain, gzip or BGZF (:111-114) byte source
     FILE *f = nullptr;
     gzFile g = nullptr;
+    std::unique_ptr<Bgzf> bz;
     ~Reader() {
         if (f) fclose(f);
         if (g) gzclose(g);
     }
     long read(char *dst, size_t n) {
+        if (bz) return bz->read(dst, n);
         if (g) {
             size_t tot = 0;
             while (tot < n) {
@@ -627,9 +791,23 @@ extern "C" int s2c_parser_feed_file(s2c_parser *p, const char *path) {
     const size_t n = strlen(path);
     Reader rd;
     if (n >= 3 && strcmp(path + n - 3, ".gz") == 0) {   // :111
-        rd.g = gzopen(path, "rb");
-        if (!rd.g) return s2c_set_error(S2C_ERR_IO, std::string("cannot open ") + path);
-        gzbuffer(rd.g, 1 << 20);
+        unsigned char h[18];
+        size_t bs = 0, hn = 0;
+        if (FILE *t = fopen(path, "rb")) {
+            hn = fread(h, 1, sizeof(h), t);
+            fclose(t);
+        }
+        if (Bgzf::block_at(h, hn, &bs)) {   // BGZF: block-parallel inflate
+            rd.bz.reset(new Bgzf());
+            rd.bz->f = fopen(path, "rb");
+            if (!rd.bz->f) return s2c_set_error(S2C_ERR_IO, std::string("cannot open ") + path);
+            const unsigned hw = std::thread::hardware_concurrency();
+            rd.bz->nt = std::max(1u, std::min(hw ? hw : 1u, 16u));
+        } else {
+            rd.g = gzopen(path, "rb");
+            if (!rd.g) return s2c_set_error(S2C_ERR_IO, std::string("cannot open ") + path);
+            gzbuffer(rd.g, 1 << 20);
+        }
     } else {
         rd.f = fopen(path, "rb");
         if (!rd.f) return s2c_set_error(S2C_ERR_IO, std::string("cannot open ") + path);

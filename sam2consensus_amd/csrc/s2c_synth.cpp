@@ -203,11 +203,13 @@ extern "C" int s2c_synth_write(const s2c_synth_spec *spec, const char *path, int
     if (!spec || !path) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
     size_t n = strlen(path);
     if (n >= 3 && strcmp(path + n - 3, ".gz") == 0) {
-        // concatenated gzip members (one per 16 MB of text, deflated level 1 on all host
-        // threads): a valid .gz stream that zlib / gzip / Python read as one file
+        // BGZF (the blocked gzip samtools / bgzip write: gzip members of <= 60000 text bytes,
+        // each with a 'BC' extra field holding its size; 16 MB of text per host thread,
+        // deflated at level 1): a valid .gz stream that zlib / gzip / Python read as one
+        // file, and that s2c_parser_feed_file inflates block-parallel
         FILE *f = fopen(path, "wb");
         if (!f) return s2c_set_error(S2C_ERR_IO, std::string("cannot open ") + path);
-        constexpr size_t BLK = (size_t)16 << 20;
+        constexpr size_t BLK = (size_t)16 << 20, BGZF_IN = 60000;
         unsigned hw = std::thread::hardware_concurrency();
         const size_t nt = std::max<size_t>(1, std::min<unsigned>(hw ? hw : 1, 16));
         std::vector<std::string> in(1);
@@ -216,14 +218,30 @@ extern "C" int s2c_synth_write(const s2c_synth_spec *spec, const char *path, int
             std::vector<int> ok(in.size(), 1);
             auto work = [&](size_t i) {
                 z_stream z{};
-                if (deflateInit2(&z, 1, Z_DEFLATED, 31, 8, Z_DEFAULT_STRATEGY) != Z_OK) { ok[i] = 0; return; }
-                out[i].resize(deflateBound(&z, in[i].size()));
-                z.next_in = (Bytef *)in[i].data();
-                z.avail_in = (uInt)in[i].size();
-                z.next_out = (Bytef *)&out[i][0];
-                z.avail_out = (uInt)out[i].size();
-                ok[i] = deflate(&z, Z_FINISH) == Z_STREAM_END;
-                out[i].resize(z.total_out);
+                if (deflateInit2(&z, 1, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) { ok[i] = 0; return; }
+                std::string &o = out[i];
+                for (size_t a = 0; a < in[i].size(); a += BGZF_IN) {
+                    const size_t n = std::min(BGZF_IN, in[i].size() - a), h = o.size();
+                    const size_t cap = deflateBound(&z, n);
+                    o.resize(h + 18 + cap + 8);
+                    deflateReset(&z);
+                    z.next_in = (Bytef *)in[i].data() + a;
+                    z.avail_in = (uInt)n;
+                    z.next_out = (Bytef *)&o[h + 18];
+                    z.avail_out = (uInt)cap;
+                    if (deflate(&z, Z_FINISH) != Z_STREAM_END) { ok[i] = 0; break; }
+                    const size_t total = 18 + z.total_out + 8;
+                    if (total > 65536) { ok[i] = 0; break; }
+                    const unsigned char hdr[18] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 'B', 'C', 2, 0,
+                                                   (unsigned char)((total - 1) & 0xff), (unsigned char)((total - 1) >> 8)};
+                    memcpy(&o[h], hdr, 18);
+                    const uint32_t crc = (uint32_t)crc32(0L, (const Bytef *)in[i].data() + a, (uInt)n), isz = (uint32_t)n;
+                    for (int b = 0; b < 4; b++) {
+                        o[h + 18 + z.total_out + b] = (char)(crc >> (8 * b));
+                        o[h + 18 + z.total_out + 4 + b] = (char)(isz >> (8 * b));
+                    }
+                    o.resize(h + total);
+                }
                 deflateEnd(&z);
             };
             std::vector<std::thread> th;
@@ -247,6 +265,9 @@ extern "C" int s2c_synth_write(const s2c_synth_spec *spec, const char *path, int
             return S2C_OK;
         }, n_reads_out);
         if (!rc) rc = deflate_all();
+        static const unsigned char eof_block[28] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 'B', 'C', 2, 0, 0x1b, 0,
+                                                    3, 0, 0, 0, 0, 0, 0, 0, 0, 0};   // BGZF end-of-file marker
+        if (!rc && fwrite(eof_block, 1, sizeof(eof_block), f) != sizeof(eof_block)) rc = s2c_set_error(S2C_ERR_IO, "write failed");
         fclose(f);
         return rc;
     }

@@ -638,8 +638,11 @@ constexpr int GS = 8;   // records per counting group
 // still leaves room for the loads' immediate and group offsets: the hardware returns zeros.
 constexpr uint32_t OOR = 0xF0000000u;
 
+#ifndef S2C_TILE_WAVES
+#define S2C_TILE_WAVES 3
+#endif
 template <int NWP>
-__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(3))) void k_tile(const TileArgs d, const uint32_t *items) {
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(S2C_TILE_WAVES))) void k_tile(const TileArgs d, const uint32_t *items) {
     constexpr int G = WG / NWP, HP = 17 * NWP;
     using H = Hist<NWP>;
     constexpr uint32_t ICOL = S2C_LDS_COLS(NWP);

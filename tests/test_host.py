@@ -128,6 +128,43 @@ def test_text_and_file_and_gzip_parse_agree():
         _same(h, hbs[0])
 
 
+def test_bgzf_block_parallel_inflate(tmp_path):
+    """synth_write's .sam.gz is BGZF (the blocked gzip of bgzip / samtools): it reads back as
+    the same text through Python's gzip, and the parser's block-parallel inflate gives the
+    plain file's batch; a BGZF stream followed by an ordinary gzip member (sequential inflate
+    from there), and a truncated file (IOError), too."""
+    import gzip
+    p, pz = str(tmp_path / "c.sam"), str(tmp_path / "c.sam.gz")
+    configs.synth_write("c2", p, scale=0.02)
+    configs.synth_write("c2", pz, scale=0.02)
+    raw = open(p, "rb").read()
+    zb = open(pz, "rb").read()
+    assert zb[:4] == b"\x1f\x8b\x08\x04" and zb[12:14] == b"BC" and len(raw) > 200000
+    assert gzip.decompress(zb) == raw
+    a, b = batch.parse_file(p), batch.parse_file(pz)
+    _same(a, b)
+    assert a.info.lines_total == b.info.lines_total and a.info.reads_mapped == b.info.reads_mapped
+    # BGZF blocks (without the EOF marker) + one ordinary gzip member of the rest
+    cut = raw.rfind(b"\n", 0, len(raw) // 2) + 1
+    pm = str(tmp_path / "m.sam.gz")
+    import zlib
+    blocks = []
+    for i in range(0, cut, 60000):
+        piece = raw[i:min(i + 60000, cut)]
+        co = zlib.compressobj(1, zlib.DEFLATED, -15)
+        d = co.compress(piece) + co.flush()
+        total = 18 + len(d) + 8
+        hdr = bytes([0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 66, 67, 2, 0, (total - 1) & 0xff, (total - 1) >> 8])
+        blocks.append(hdr + d + zlib.crc32(piece).to_bytes(4, "little") + len(piece).to_bytes(4, "little"))
+    open(pm, "wb").write(b"".join(blocks) + gzip.compress(raw[cut:]))
+    c = batch.parse_file(pm)
+    _same(a, c)
+    pt = str(tmp_path / "t.sam.gz")
+    open(pt, "wb").write(zb[: len(zb) // 2])
+    with pytest.raises(IOError):
+        batch.parse_file(pt)
+
+
 def test_streaming_chunks_equal_whole():
     sam = "".join(c["sam"] for c in golden_io.load("kat")[:1])
     p = batch.Parser()
