@@ -50,10 +50,11 @@ clean:
 
 .PHONY: all clean isa prof variant
 
-# experiment build: k_tile_dense and k_tile with extra defines (V=name VDEFS='-D...'): libs2c_$(V).so
+# experiment build: k_reads, k_tile_dense and k_tile with extra defines (V=name VDEFS='-D...'): libs2c_$(V).so
 V ?= var
 VDEFS ?=
-variant: $(BUILD)/s2c_host.o $(BUILD)/s2c_synth.o $(BUILD)/s2c_reads.o
+variant: $(BUILD)/s2c_host.o $(BUILD)/s2c_synth.o
+	$(HIPCC) $(HIPFLAGS) $(VDEFS) -c $(SRC)/s2c_reads.hip -o $(BUILD)/s2c_reads_$(V).o
 	$(HIPCC) $(HIPFLAGS) $(VDEFS) -c $(SRC)/s2c_dense.hip -o $(BUILD)/s2c_dense_$(V).o
 	$(HIPCC) $(HIPFLAGS) $(VDEFS) -c $(SRC)/s2c_tile.hip -o $(BUILD)/s2c_tile_$(V).o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ $(BUILD)/s2c_dense_$(V).o $(BUILD)/s2c_tile_$(V).o -lz -lpthread -o sam2consensus_amd/libs2c_$(V).so
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ $(BUILD)/s2c_reads_$(V).o $(BUILD)/s2c_dense_$(V).o $(BUILD)/s2c_tile_$(V).o -lz -lpthread -o sam2consensus_amd/libs2c_$(V).so
