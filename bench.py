@@ -182,10 +182,12 @@ def main():
     from sam2consensus_amd import configs, shard
     from sam2consensus_amd.engine import DeviceBatch, Workspace
 
+    local %= max(torch.cuda.device_count(), 1)   # (ranks sharing a device: rehearsals on one GPU, gloo)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("S2C_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     wl = args.workload
     opt_args = configs.cli_args(wl)
