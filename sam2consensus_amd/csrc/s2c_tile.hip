@@ -638,11 +638,13 @@ constexpr int GS = 8;   // records per counting group
 // still leaves room for the loads' immediate and group offsets: the hardware returns zeros.
 constexpr uint32_t OOR = 0xF0000000u;
 
-#ifndef S2C_TILE_WAVES
-#define S2C_TILE_WAVES 3
-#endif
-template <int NWP>
-__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(S2C_TILE_WAVES))) void k_tile(const TileArgs d, const uint32_t *items) {
+// PIPE: the count loop software-pipelined (next group's run records in flight during this
+// group's base windows) at 2 waves/SIMD — it needs the registers; without, 3 waves/SIMD.
+// Measured crossover (profiles/r02): deep batches (C3 1000x, C4) gain 3-11 %, C2 (500x with
+// insertion epilogues) loses 7 %; launches pick PIPE for batches with >= 5 run slots per
+// position (s2c_pileup).
+template <int NWP, bool PIPE>
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(PIPE ? 2 : 3))) void k_tile(const TileArgs d, const uint32_t *items) {
     constexpr int G = WG / NWP, HP = 17 * NWP;
     using H = Hist<NWP>;
     constexpr uint32_t ICOL = S2C_LDS_COLS(NWP);
@@ -747,6 +749,101 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(S2C_TILE_WAV
             }
         }
     };
+    if constexpr (PIPE) {
+    // ---- window records, GS at a time, software-pipelined: a group's run records become
+    //      geometry (covered mask; first bit, funnel shift and kind packed) and base-window
+    //      requests as they arrive, then the NEXT group's run records are requested, then this
+    //      group's masks go into the counters (carry-save, one record at a time) — each group
+    //      waits for one HBM round trip instead of two, in the registers of the old loop
+    auto load_runs = [&](uint4 (&Rv)[GS], uint32_t gi) {
+#pragma unroll
+        for (int u = 0; u < GS; u++) {
+            uint32_t vo = gi * GS + u < nrec ? voff : OOR;
+            asm volatile("" : "+v"(vo));
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rrun, vo + (uint32_t)(u * 16 * G), gi * GS * 16 * G, 0);
+            Rv[u] = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+    };
+    uint4 R[GS];
+    if (ngrp) load_runs(R, 0);
+    for (uint32_t gi = 0; gi < ngrp; gi++) {
+        uint32_t gv[GS], gp[GS];   // covered bits; lo | sh << 8 | kind << 16 (kind 0: nothing)
+        uint2 Wa[GS], Wb[GS];
+        uint32_t X0[GS], X1[GS];
+#pragma unroll
+        for (int u = 0; u < GS; u++) {
+            const Run r = run_of(R[u]);
+            const uint32_t kind = (r.kind & S2C_RUN_LONG) ? 0u : r.kind;   // (long: reached through the long list)
+            const RecGeom gm = rec_geom(r.gpos, r.len, W);
+            const uint64_t qs = r.q + gm.qs;
+            const bool bases = (kind & 3u) == S2C_RUN_BASES && gm.valid;
+            const uint32_t wo = bases ? (uint32_t)(qs >> 5) * 8u : OOR;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rbq, wo, 0, 0);
+            Wa[u] = make_uint2(v[0], v[1]);
+            Wb[u] = make_uint2(v[2], v[3]);
+            const uint32_t xo = (bases && (kind & S2C_RUN_XBIT)) ? (uint32_t)(qs >> 5) * 4u : OOR;
+            const auto xv = __builtin_amdgcn_raw_buffer_load_b64(rbx, xo, 0, 0);
+            X0[u] = xv[0];
+            X1[u] = xv[1];
+            gv[u] = ((kind & 3u) == S2C_RUN_BASES || (kind & 3u) == S2C_RUN_DASH) ? gm.valid : 0u;
+            gp[u] = gm.lo | ((uint32_t)(qs & 31) << 8) | ((kind & 0xFFu) << 16);
+        }
+        uint4 Rn[GS];
+        if (gi + 1 < ngrp) load_runs(Rn, gi + 1);
+        uint32_t pend[4], t2a[4], t4a[4], t8[4];
+#pragma unroll
+        for (int u = 0; u < GS; u++) {
+            const uint32_t valid = gv[u], lo = gp[u] & 0xFFu, sh = (gp[u] >> 8) & 31u, kind = gp[u] >> 16;
+            uint32_t mx = 0, my = 0, mv = 0;
+            if ((kind & 3u) == S2C_RUN_DASH) {
+                ripple1(Dc, valid);
+            } else if ((kind & 3u) == S2C_RUN_BASES && valid) {
+                mx = (funnel(Wb[u].x, Wa[u].x, sh) << lo) & valid;
+                my = (funnel(Wb[u].y, Wa[u].y, sh) << lo) & valid;
+                mv = valid;
+                if (kind & S2C_RUN_XBIT) {
+                    const uint32_t xm = (funnel(X1[u], X0[u], sh) << lo) & valid;
+                    const uint32_t en = xm & ~mx & ~my, sd = xm & mx & ~my;   // 'N', '-' of SEQ
+                    mv &= ~xm;
+                    mx &= ~xm;
+                    my &= ~xm;
+                    if (sd && !(kind & S2C_RUN_DROP)) ripple1(Dc, sd);
+                    uint32_t e = en;
+                    while (e) {
+                        const uint32_t bit = (uint32_t)__builtin_ctz(e);
+                        e &= e - 1;
+                        H::add1(hist, 4, 32 * w + bit, 1u);
+                    }
+                }
+            }
+            const uint32_t mk[4] = {mx, my, mx & my, mv};
+#pragma unroll
+            for (int c = 0; c < 4; c++) {   // tree8 of the old loop, one record at a time
+                if ((u & 1) == 0) {
+                    pend[c] = mk[c];
+                    continue;
+                }
+                uint32_t t2;
+                csa(t2, V[c][0], V[c][0], pend[c], mk[c]);
+                if ((u & 3) == 1) {
+                    t2a[c] = t2;
+                    continue;
+                }
+                uint32_t t4;
+                csa(t4, V[c][1], V[c][1], t2a[c], t2);
+                if ((u & 7) == 3) {
+                    t4a[c] = t4;
+                    continue;
+                }
+                csa(t8[c], V[c][2], V[c][2], t4a[c], t4);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 4; c++) close8(V[c], t8[c]);
+#pragma unroll
+        for (int u = 0; u < GS; u++) R[u] = Rn[u];
+    }
+    } else {
     // ---- window records, GS at a time: run records, then their base windows
     for (uint32_t gi = 0; gi < ngrp; gi++) {
         uint4 R[GS];
@@ -785,6 +882,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(S2C_TILE_WAV
         close8(V[1], t1);
         close8(V[2], t2);
         close8(V[3], t3);
+    }
     }
     TPROF_MARK(3);
     nmax_rec = nrec;
@@ -1100,16 +1198,23 @@ TileArgs tile_args(const s2c_dev &d) {
 }
 
 template <int NWP>
-int launch_tile(const TileArgs &a, const uint32_t *items, int64_t n, hipStream_t s) {
+int launch_tile(const TileArgs &a, const uint32_t *items, int64_t n, hipStream_t s, bool pipe) {
     if (n <= 0) return S2C_OK;
-    k_tile<NWP><<<(unsigned)n, WG, 0, s>>>(a, items);
+    if (pipe) k_tile<NWP, true><<<(unsigned)n, WG, 0, s>>>(a, items);
+    else k_tile<NWP, false><<<(unsigned)n, WG, 0, s>>>(a, items);
     return hip_check(hipGetLastError(), "k_tile");
 }
-int launch_tiles(const TileArgs &a, int32_t tile_max, const uint32_t *items, int64_t n, hipStream_t s) {
-    if (tile_max <= 256) return launch_tile<8>(a, items, n, s);
-    if (tile_max <= 512) return launch_tile<16>(a, items, n, s);
-    if (tile_max <= 1024) return launch_tile<32>(a, items, n, s);
-    return launch_tile<64>(a, items, n, s);
+// pipe: the software-pipelined count loop, for deep batches (>= 5 run slots per position)
+int launch_tiles(const TileArgs &a, int32_t tile_max, const uint32_t *items, int64_t n, hipStream_t s, bool pipe) {
+    if (tile_max <= 256) return launch_tile<8>(a, items, n, s, pipe);
+    if (tile_max <= 512) return launch_tile<16>(a, items, n, s, pipe);
+    if (tile_max <= 1024) return launch_tile<32>(a, items, n, s, pipe);
+    return launch_tile<64>(a, items, n, s, pipe);
+}
+bool deep_batch(const s2c_dev *d) {
+    const char *e = getenv("S2C_TILE_PIPE");   // (A/B diagnostic: 0 / 1 forces)
+    if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
+    return d->n_ops >= 5 * d->padded_len;
 }
 
 }  // namespace
@@ -1188,10 +1293,10 @@ extern "C" int s2c_pileup(const s2c_dev *d, void *stream) {
     }
     if (d->n_dense > 0) {
         // dense tiles emit exactly one char per position: len(fill) must be 1, else k_tile
-        rc = d->fill_len == 1 ? s2c_launch_dense(d, s) : launch_tiles(a, d->tile_max, d->dense, d->n_dense, s);
+        rc = d->fill_len == 1 ? s2c_launch_dense(d, s) : launch_tiles(a, d->tile_max, d->dense, d->n_dense, s, deep_batch(d));
         if (rc) return rc;
     }
-    return launch_tiles(a, d->tile_max, d->items, d->n_items, s);
+    return launch_tiles(a, d->tile_max, d->items, d->n_items, s, deep_batch(d));
 }
 
 extern "C" int s2c_consensus(const s2c_dev *d, void *stream) {
@@ -1223,8 +1328,8 @@ extern "C" int s2c_pileup_counts(const s2c_dev *d, void *stream) {
         k_prep<<<(unsigned)d->n_deep, WG, 0, s>>>(a, d->deep);
         if ((rc = hip_check(hipGetLastError(), "k_prep"))) return rc;
     }
-    if ((rc = launch_tiles(a, d->tile_max, d->dense, d->n_dense, s))) return rc;
-    return launch_tiles(a, d->tile_max, d->items, d->n_items, s);
+    if ((rc = launch_tiles(a, d->tile_max, d->dense, d->n_dense, s, deep_batch(d)))) return rc;
+    return launch_tiles(a, d->tile_max, d->items, d->n_items, s, deep_batch(d));
 }
 
 extern "C" int s2c_accumulate(const s2c_dev *d, int keep_tables, void *stream) {
@@ -1235,6 +1340,6 @@ extern "C" int s2c_accumulate(const s2c_dev *d, int keep_tables, void *stream) {
     if ((rc = s2c_launch_reads(d, s, true))) return rc;   // run records of every piece; events hashed
     TileArgs a = tile_args(*d);
     a.mode = keep_tables ? MODE_ADD_KEEP : MODE_ADD;
-    if ((rc = launch_tiles(a, d->tile_max, d->dense, d->n_dense, s))) return rc;
-    return launch_tiles(a, d->tile_max, d->items, d->n_items, s);
+    if ((rc = launch_tiles(a, d->tile_max, d->dense, d->n_dense, s, deep_batch(d)))) return rc;
+    return launch_tiles(a, d->tile_max, d->items, d->n_items, s, deep_batch(d));
 }
