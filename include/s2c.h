@@ -92,6 +92,8 @@ int s2c_layout(int64_t *out, int n);
 #define S2C_PF_LONG   0x08   /* span > the batch's window: reached through the tile long lists */
 #define S2C_PF_RUNS   0x10   /* a non-dense tile reads its runs: k_reads writes them (dense tiles
                                 walk their window's pieces themselves) */
+#define S2C_PF_DASH   0x20   /* SEQ holds '-' chars (with S2C_PF_X): the maxdel rule (:210) counts
+                                them from the planes; without it a read's SEQ adds no '-' */
 
 /* run record (device-written by k_reads, parallel to ops[]): {gpos, len | kind << 24, qlo, qhi} */
 #define S2C_RUN_EMPTY   0u

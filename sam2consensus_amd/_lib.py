@@ -30,7 +30,7 @@ S2C_ITEM_WORDS = 4
 S2C_CODE_FILL = 0
 S2C_SHORT_MOTIF = 16
 S2C_TILE_DEEP, S2C_TILE_GENERAL, S2C_TILE_DENSE = 1, 2, 4
-S2C_PF_X, S2C_PF_RANGE, S2C_PF_INS, S2C_PF_LONG, S2C_PF_RUNS = 1, 2, 4, 8, 16
+S2C_PF_X, S2C_PF_RANGE, S2C_PF_INS, S2C_PF_LONG, S2C_PF_RUNS, S2C_PF_DASH = 1, 2, 4, 8, 16, 32
 S2C_RUN_EMPTY, S2C_RUN_BASES, S2C_RUN_DASH = 0, 1, 2
 S2C_RUN_XBIT, S2C_RUN_DROP, S2C_RUN_LONG = 4, 8, 16
 OPS = "MIDNSHP=X"   # opcode order of the token words (len << 4 | opcode)

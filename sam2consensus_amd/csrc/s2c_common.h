@@ -107,7 +107,7 @@ __device__ __forceinline__ void walk_piece(const Mem &m, const uint4 P, uint32_t
             const uint64_t l = w >> 4;
             if (op_bases(op)) {
                 uint64_t take = start < slen ? (l < slen - start ? l : slen - start) : 0;
-                if (fl & S2C_PF_X) {   // '-' chars of SEQ: x = 1, p1 = 0, p0 = 1
+                if (fl & S2C_PF_DASH) {   // '-' chars of SEQ: x = 1, p1 = 0, p0 = 1
                     uint64_t q = q0 + start;
                     while (take) {
                         const uint64_t qw = q >> 5;

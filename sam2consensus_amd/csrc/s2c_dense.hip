@@ -106,7 +106,7 @@ __device__ __forceinline__ void walk_window(const uint32_t *opl, const uint2 *bq
             const uint32_t w = opl[i], op = w & 15u, l = w >> 4;
             if (op_bases(op)) {
                 uint32_t take = start < slen ? min(l, slen - start) : 0u;
-                if (fl & S2C_PF_X) {   // '-' chars of SEQ: x = 1, p1 = 0, p0 = 1
+                if (fl & S2C_PF_DASH) {   // '-' chars of SEQ: x = 1, p1 = 0, p0 = 1
                     uint32_t q = q0 + start;
                     while (take) {
                         const uint32_t qw = q >> 5, sh = q & 31u, nb = min(take, 32u - sh);
@@ -466,7 +466,9 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         const uint32_t fl = P.w >> 24, slen = P.w & 0xFFFFFFu, j = P.z - o0;
         const uint32_t op = w0 & 15u, l = w0 >> 4;
         const bool xf = (fl & S2C_PF_X) != 0;
-        const bool plain = in && (fl & ~(uint32_t)S2C_PF_X) == 0u && op_bases(op) && !(xf && mda);
+        // (no maxdel count to take: the rule is off, or SEQ holds no '-')
+        const bool plain = in && (fl & ~(uint32_t)(S2C_PF_X | S2C_PF_DASH)) == 0u && op_bases(op) &&
+                           !((fl & S2C_PF_DASH) && mda);
         const uint32_t nops = oend - P.z;
         // one M / = / X token and nothing else: seqout = SEQ[0 : min(l, len(SEQ))] (:64-69)
         const bool fast = plain && nops == 1u;

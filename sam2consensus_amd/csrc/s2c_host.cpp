@@ -268,6 +268,7 @@ struct RefView {
 };
 
 // SEQ → planes at a 16-base boundary of the chunk; returns the first base index.
+// *has_x: bit 0 = a non-ACGT char, bit 1 = a '-' char (x = 1, p1 = 0, p0 = 1)
 static uint64_t pack_seq(Chunk &c, const char *seq, size_t slen, uint8_t *has_x) {
     const uint64_t q0 = (c.nq + 15) & ~(uint64_t)15;
     const uint64_t q1 = q0 + slen;
@@ -294,7 +295,7 @@ static uint64_t pack_seq(Chunk &c, const char *seq, size_t slen, uint8_t *has_x)
         c.bq[2 * w] |= p0 << sh;
         c.bq[2 * w + 1] |= p1 << sh;
         c.bx[w] |= x << sh;
-        anyx |= x != 0;
+        anyx |= (x != 0 ? 1 : 0) | ((x & p0 & ~p1) != 0 ? 2 : 0);
         b += m;
         i += m;
     }
@@ -1466,7 +1467,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
                 const Chunk &c = *CH[q.chunk];
                 const ReadRec &r = c.reads[q.read];
                 uint32_t *o = &b->ops[ooff[k]];
-                uint32_t fl = r.has_x ? S2C_PF_X : 0u;
+                uint32_t fl = (r.has_x ? S2C_PF_X : 0u) | ((r.has_x & 2) ? S2C_PF_DASH : 0u);
                 if (q.range) { fl |= S2C_PF_RANGE; *o++ = (uint32_t)q.ka; *o++ = (uint32_t)q.kb; }
                 if (q.ins) {
                     fl |= S2C_PF_INS;

@@ -37,7 +37,7 @@ from . import _lib as L
 from .batch import HostBatch, Parser
 
 BLOCK = 64 << 20          # bytes of SAM text per block
-NO_BLOCK = 1 << 40        # "no failing block"
+NO_BLOCK = 1 << 56        # "no failing block" (block keys: below 2^48)
 BIN_SHIFT = 8             # read-start histogram bins of 256 positions
 DENSE_DEPTH = 48.0        # at or below this mean depth: 1024-position dense tiles
 E_TARGET = 262144.0       # aligned bases per deep tile (the planner's, s2c_host.cpp)
@@ -177,8 +177,104 @@ def text_blocks(rest, block=BLOCK):
     return out
 
 
-def file_blocks(filename, rank, world, block=BLOCK):
-    return (gz_blocks if filename.endswith(".gz") else plain_blocks)(filename, rank, world, block)
+def bgzf_index(mm):
+    """[(offset, size)] of the BGZF blocks (members with the 'BC' size field) of a mapped
+    .gz file, or None if any member is not one."""
+    idx, off, n = [], 0, len(mm)
+    while off < n:
+        if n - off < 18 or mm[off:off + 4] != b"\x1f\x8b\x08\x04":
+            return None
+        xlen = mm[off + 10] | (mm[off + 11] << 8)
+        k, size = off + 12, 0
+        while k + 4 <= off + 12 + xlen:
+            sl = mm[k + 2] | (mm[k + 3] << 8)
+            if mm[k:k + 2] == b"BC" and sl == 2:
+                size = (mm[k + 4] | (mm[k + 5] << 8)) + 1
+            k += 4 + sl
+        if size < 12 + xlen + 8 or off + size > n:
+            return None
+        idx.append((off, size))
+        off += size
+    return idx
+
+
+def _inflate(mm, blocks):
+    import zlib
+    out = []
+    for off, size in blocks:
+        xlen = mm[off + 10] | (mm[off + 11] << 8)
+        out.append(zlib.decompress(mm[off + 12 + xlen:off + size - 8], -15))
+    return b"".join(out)
+
+
+def bgzf_text(filename, rank, world, group=None):
+    """A BGZF .sam.gz cut over the ranks by compressed bytes: rank r inflates only its blocks
+    (the header from the file's first blocks), and the lines cut by a range end are
+    completed with the next ranks' leading bytes (an all-gather of the small head pieces).
+    Returns (header, this rank's whole lines after the header), or None when the file is
+    not BGZF or a line would span a rank's whole range (then every rank inflates the stream)."""
+    import mmap
+
+    import torch.distributed as dist
+    with open(filename, "rb") as fh:
+        mm = mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ)
+        try:
+            idx = bgzf_index(mm)
+            ok = idx is not None and len(idx) > 0
+            flags = [None] * world
+            dist.all_gather_object(flags, ok, group=group)
+            if not all(flags):
+                return None
+            C = idx[-1][0] + idx[-1][1]
+            mine = [b for b in idx if rank * C // world <= b[0] < (rank + 1) * C // world]
+            text = _inflate(mm, mine)
+            head = b""
+            for k in range(0, len(idx), 64):   # the header: the file's first blocks until a record line
+                head += _inflate(mm, idx[k:k + 64])
+                if split_header(head) is not None:
+                    break
+        finally:
+            mm.close()
+    header, H = split_header(head) or (head, len(head))
+    # my range's bytes of the file's text: [text_start, text_start + len(text)); the records
+    # start at H.  Head piece: my bytes up to and including my first '\n' (all of them if none).
+    lens = [None] * world
+    dist.all_gather_object(lens, len(text), group=group)
+    start = sum(lens[:rank])
+    lo = max(0, H - start)                      # header bytes in my range
+    nl = text.find(b"\n", lo)
+    headpiece = text[lo:nl + 1] if nl >= 0 else text[lo:]
+    pieces = [None] * world
+    dist.all_gather_object(pieces, (headpiece, nl >= 0, start + len(text) <= H), group=group)
+    # a rank without a newline past the header would leave a line spanning its range
+    if any(not p[1] and not p[2] and lens[r] > 0 for r, p in enumerate(pieces)):
+        return None
+    body = text[lo:]
+    ends_nl = [None] * world
+    mine_end = body.endswith(b"\n") or not body
+    dist.all_gather_object(ends_nl, mine_end, group=group)
+    # my leading piece belongs to the previous rank holding bytes unless that one ended a line
+    prev = [r for r in range(rank) if lens[r] > 0 and not pieces[r][2]]
+    if prev and not ends_nl[prev[-1]]:
+        body = body[len(headpiece):]
+    if not mine_end:   # complete my last line from the next ranks' head pieces
+        for r in range(rank + 1, world):
+            if lens[r] == 0 or pieces[r][2]:
+                continue
+            body += pieces[r][0]
+            if pieces[r][1]:
+                break
+    return header, body
+
+
+def file_blocks(filename, rank, world, block=BLOCK, group=None):
+    if filename.endswith(".gz"):
+        r = bgzf_text(filename, rank, world, group)
+        if r is not None:   # block keys: rank << 32 | block of this rank's range (file order)
+            header, body = r
+            return header, [((rank << 32) | k, b) for k, b in enumerate(text_blocks(body, block))]
+        return gz_blocks(filename, rank, world, block)
+    return plain_blocks(filename, rank, world, block)
 
 
 def tile_width_for(depth):
@@ -241,7 +337,7 @@ def parse_distributed(filename, rank, world, maxdel_active=True, group=None, blo
         header, H = split_header(text) or (text, len(text))
         blocks = [(k, b) for k, b in enumerate(text_blocks(text[H:], block)) if k % world == rank]
     else:
-        header, blocks = file_blocks(filename, rank, world, block)
+        header, blocks = file_blocks(filename, rank, world, block, group)
 
     # the reference table and the fixed-width tile list come from the header alone
     hp = BlockParser(maxdel_active, 150)

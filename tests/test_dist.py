@@ -178,11 +178,14 @@ def test_distributed_parse_matches_reference(world, block, tmp_path):
     want = [(c["status"], c["files"]) for c in kat]
     want += [("ok", o.run_case(big, a)["files"]) for a in ([], ["-c", "0.25,0.75"], ["-d", "9"])]
     paths = []
-    if world == 2:
-        for ext in (".sam", ".sam.gz"):
-            p = str(tmp_path / ("c2s" + ext))
-            configs.synth_write("c2", p, scale=0.03)
-            paths.append((p, configs.cli_args("c2")))
+    for ext in (".sam", ".sam.gz"):   # (.sam.gz: BGZF, each rank inflates its own blocks)
+        p = str(tmp_path / ("c2s" + ext))
+        configs.synth_write("c2", p, scale=0.03 if world == 2 else 0.01)
+        paths.append((p, configs.cli_args("c2")))
+    if world == 3:   # a small BGZF file: few blocks per rank, lines cut at every range end
+        p = str(tmp_path / "c1.sam.gz")
+        configs.synth_write("c1", p)
+        paths.append((p, configs.cli_args("c1")))
     got = _run_dparse(world, cases, paths, block)
     assert len(got) == len(want) + len(paths)
     for k, (g, w) in enumerate(zip(got, want)):

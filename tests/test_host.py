@@ -165,6 +165,20 @@ def test_bgzf_block_parallel_inflate(tmp_path):
         batch.parse_file(pt)
 
 
+def test_piece_flags_mark_non_acgt_and_dash_seq():
+    """S2C_PF_X for a SEQ with any non-ACGT char, S2C_PF_DASH only when one is '-' (the maxdel
+    rule, :210, scans the planes of those reads alone)."""
+    sam = ("@SQ\tSN:g\tLN:100\n"
+           "r1\t0\tg\t1\t60\t8M\t*\t0\t0\tACGTACGT\t*\n"
+           "r2\t0\tg\t1\t60\t8M\t*\t0\t0\tACGNACGT\t*\n"
+           "r3\t0\tg\t1\t60\t8M\t*\t0\t0\tAC-TACGT\t*\n"
+           "r4\t0\tg\t1\t60\t8M\t*\t0\t0\tNC-TACGN\t*\n")
+    hb = batch.parse_text(sam, True, 150)
+    from sam2consensus_amd import _lib as L
+    fl = sorted(int(f) for f in (hb.pc[:-1, 3] >> 24) & (L.S2C_PF_X | L.S2C_PF_DASH))
+    assert fl == [0, L.S2C_PF_X, L.S2C_PF_X | L.S2C_PF_DASH, L.S2C_PF_X | L.S2C_PF_DASH]
+
+
 def test_streaming_chunks_equal_whole():
     sam = "".join(c["sam"] for c in golden_io.load("kat")[:1])
     p = batch.Parser()
