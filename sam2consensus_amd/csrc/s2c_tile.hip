@@ -643,6 +643,9 @@ constexpr uint32_t OOR = 0xF0000000u;
 // Measured crossover (profiles/r02): deep batches (C3 1000x, C4) gain 3-11 %, C2 (500x with
 // insertion epilogues) loses 7 %; launches pick PIPE for batches with >= 5 run slots per
 // position (s2c_pileup).
+#ifndef S2C_TILE_XCD
+#define S2C_TILE_XCD 1
+#endif
 template <int NWP, bool PIPE>
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(PIPE ? 2 : 3))) void k_tile(const TileArgs d, const uint32_t *items) {
     constexpr int G = WG / NWP, HP = 17 * NWP;
@@ -658,7 +661,14 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(PIPE ? 2 : 3
 #endif
     TPROF_MARK(0);
     if (tid < 64) L.amb[tid] = c_amb[tid];
+#if S2C_TILE_XCD
+    // XCD-major: the blocks of one XCD (b ≡ x mod 8) take a contiguous range of items, so
+    // neighbouring tiles' shared window reads meet in that XCD's L2
+    const uint32_t bx8 = blockIdx.x & 7u, per = gridDim.x >> 3, rem = gridDim.x & 7u;
+    const uint4 itv = ((const uint4 *)items)[bx8 * per + min(bx8, rem) + (blockIdx.x >> 3)];
+#else
     const uint4 itv = ((const uint4 *)items)[blockIdx.x];
+#endif
     const uint32_t tile = uni(itv.x), chunk = uni(itv.y);
     const TileRec T = tile_rec(d.tiles, tile);
     const uint32_t a = T.a, n = T.b - T.a;
