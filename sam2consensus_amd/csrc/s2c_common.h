@@ -264,6 +264,15 @@ __device__ __forceinline__ void close16(uint32_t (&C)[8], uint32_t t8a, uint32_t
         t16 = t;
     }
 }
+// one weight-4 carry into plane C[2], rippled into C[3..7]
+__device__ __forceinline__ void close4(uint32_t (&C)[8], uint32_t t4) {
+#pragma unroll
+    for (int b = 2; b < 8; b++) {
+        const uint32_t t = C[b] & t4;
+        C[b] ^= t4;
+        t4 = t;
+    }
+}
 // one weight-8 carry into plane C[3], rippled into C[4..7]
 __device__ __forceinline__ void close8(uint32_t (&C)[8], uint32_t t8) {
 #pragma unroll

@@ -30,6 +30,7 @@
 // the window overlap of neighbouring tiles is served by that XCD's L2.  The host sizes the
 // tiles so the window takes ≤ S2C_DENSE_LDS bytes (S2C_DENSE_BYTES).
 #include <algorithm>
+#include <type_traits>
 
 #include "s2c_common.h"
 
@@ -564,7 +565,10 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
 #pragma unroll
         for (int b = 0; b < 8; b++) C[c][b] = 0;
     const uint32_t nrec = cw0 + g < cw1 ? (cw1 - cw0 - g + G - 1) / G : 0u;
-    const uint32_t ngrp = ABL(2) ? 0u : uni(__ockl_wfred_max_u32((nrec + GSD - 1) / GSD));
+    // full groups of 8, then (when the wave's longest lane has 1-4 records left) a group of 4
+    const uint32_t nmx = ABL(2) ? 0u : uni(__ockl_wfred_max_u32(nrec));
+    const uint32_t ngrp = nmx / GSD + ((nmx % GSD) > 4u ? 1u : 0u);
+    const bool half = (nmx % GSD) != 0u && (nmx % GSD) <= 4u;
     // Group gi reads records cw0 + g + G·(8 gi + u), u < 8, by immediate offsets from one base
     // clamped to the end of the records: every slot past this lane's candidates is a record of
     // a piece starting in a later word (or a zero pad record), so it covers nothing here.
@@ -578,10 +582,12 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         for (int u = 0; u < GSD; u++) rv[u] = rb[G * u];
     };
     // one group's 8 records → Harley–Seal tree of each plane; returns the weight-8 carries
-    auto count_group = [&](const uint2 (&rv)[GSD], uint32_t (&t8o)[4]) {
+    // NR = 8: returns the weight-8 carries in t8o; NR = 4 (a tail group): the weight-4 carries
+    auto count_group = [&](const uint2 (&rv)[GSD], uint32_t (&t8o)[4], auto nr) {
+        constexpr int NR = decltype(nr)::value;
         uint32_t pend[4], t2a[4], t4a[4];
 #pragma unroll
-        for (int h = 0; h < GSD; h += CNT_PART) {   // (parts of CNT_PART records: fewer live registers)
+        for (int h = 0; h < NR; h += CNT_PART) {   // (parts of CNT_PART records: fewer live registers)
         uint32_t bm[GSD], fx[GSD], sh[GSD];
         uint2 pa[GSD], pb[GSD];
 #pragma unroll
@@ -622,6 +628,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
                 csa(t4, C[c][1], C[c][1], t2a[c], t2);
                 if ((u & 7) == 3) {
                     t4a[c] = t4;
+                    if constexpr (NR == 4) t8o[c] = t4;
                     continue;
                 }
                 csa(t8o[c], C[c][2], C[c][2], t4a[c], t4);
@@ -629,6 +636,8 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         }
         }
     };
+    using Full = std::integral_constant<int, 8>;
+    using Half = std::integral_constant<int, 4>;
     // two groups per trip (ping-pong record buffers; the next group's records are read while
     // this group's plane words are in flight), their weight-8 carries closed together
     uint2 ra[GSD], rb2[GSD];
@@ -636,16 +645,23 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     for (uint32_t gi = 0; gi < ngrp; gi += 2) {
         uint32_t t8a[4], t8b[4];
         if (gi + 1 < ngrp) load_runs(rb2, gi + 1);
-        count_group(ra, t8a);
+        count_group(ra, t8a, Full{});
         if (gi + 1 >= ngrp) {
 #pragma unroll
             for (int c = 0; c < 4; c++) close8(C[c], t8a[c]);
             break;
         }
         if (gi + 2 < ngrp) load_runs(ra, gi + 2);
-        count_group(rb2, t8b);
+        count_group(rb2, t8b, Full{});
 #pragma unroll
         for (int c = 0; c < 4; c++) close16(C[c], t8a[c], t8b[c]);
+    }
+    if (half) {   // records 8·ngrp .. 8·ngrp + 3 of each lane
+        uint32_t t4[4];
+        load_runs(ra, ngrp);
+        count_group(ra, t4, Half{});
+#pragma unroll
+        for (int c = 0; c < 4; c++) close4(C[c], t4[c]);
     }
     PROF_MARK(5);
     // queued single-token runs of reads with N / '-' in SEQ (never dropped: maxdel is off)
