@@ -171,6 +171,7 @@ def main():
     ap.add_argument("--cpu-mc-scale", type=float, default=1.0)
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--graph", action="store_true", help="time HIP graph replays of the step")
+    ap.add_argument("--stage-events", action="store_true", help="HIP events between all stages in the timed steps")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -213,7 +214,9 @@ def main():
         ws.run()
     torch.cuda.synchronize(dev)
 
-    # the timed steps: stage by stage with HIP events between the stages (on the launch stream)
+    # the timed steps: HIP events around the pileup stage of every step (on the launch stream;
+    # an event is a timestamp packet with a cache release on this GPU, so the timed loop
+    # carries only the two the roofline needs); --stage-events: events between all stages
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(K)]
     if args.graph:
         ws.capture()
@@ -226,13 +229,15 @@ def main():
             ws.replay()
             continue
         e = ev[k]
-        e[0].record(stream)
+        if args.stage_events:
+            e[0].record(stream)
         ws.reads()
         e[1].record(stream)
         ws.pileup()
         e[2].record(stream)
         ws.consensus()
-        e[3].record(stream)
+        if args.stage_events:
+            e[3].record(stream)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     if world > 1:
@@ -240,8 +245,25 @@ def main():
     elapsed = t1 - t0
     kern = {}
     if not args.graph:
-        for name, i0, i1 in (("k_reads", 0, 1), ("k_tile", 1, 2), ("k_consensus", 2, 3), ("step_events", 0, 3)):
-            kern[name] = sum(ev[k][i0].elapsed_time(ev[k][i1]) for k in range(K)) / K   # ms
+        kern["k_tile"] = sum(ev[k][1].elapsed_time(ev[k][2]) for k in range(K)) / K   # ms, the timed steps
+        if not args.stage_events:   # the other stages from a few more steps with all four events
+            ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(5)]
+            for e in ev:
+                e[0].record(stream)
+                ws.reads()
+                e[1].record(stream)
+                ws.pileup()
+                e[2].record(stream)
+                ws.consensus()
+                e[3].record(stream)
+            torch.cuda.synchronize(dev)
+        n_ev = len(ev)
+        stages = (("k_reads", 0, 1), ("k_consensus", 2, 3), ("step_events", 0, 3))
+        if not args.stage_events:   # (this loop's own pileup time, so its stages add up)
+            stages += (("k_tile_breakdown", 1, 2),)
+            kern["breakdown_steps"] = n_ev
+        for name, i0, i1 in stages:
+            kern[name] = sum(ev[k][i0].elapsed_time(ev[k][i1]) for k in range(n_ev)) / n_ev   # ms
 
     stats = torch.tensor([elapsed, float(info.aligned_bases)], dtype=torch.float64, device=dev)
     if world > 1:
