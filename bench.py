@@ -307,7 +307,9 @@ def main():
         }
         if kern:
             tile_ms = kern["k_tile"]
-            assert tile_ms <= ms * 1.001 and kern["step_events"] <= ms * 1.05, (kern, ms)
+            # (step_events comes from the breakdown steps, whose four events per step may add
+            # more than the timed loop's two: only the timed loop's own pileup time is checked)
+            assert tile_ms <= ms * 1.001 and (not args.stage_events or kern["step_events"] <= ms * 1.05), (kern, ms)
             achieved = tile_bytes * per_rank / (tile_ms * 1e-3) / 1e9
             traffic = traffic_from_profile(wl)
             line["roofline"] = {
