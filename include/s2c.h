@@ -22,14 +22,15 @@
  *              read batch: CIGAR tokens, 2-bit base planes + a non-ACGT plane in QUERY
  *              order, POS / reference as a global coordinate, pieces bucketed by their
  *              start word (32 positions), and the tile plan (sizes and capacities only).
- *   device (2) k_reads: parsecigar (:46-82) + the maxdel rule (:210) per piece → runs
- *              (seqout intervals mapped to query bases or to '-'), and the insertion
- *              events (:73-75, :221) hashed by (position, motif) into per-tile
- *              open-addressing tables with per-entry counts (:262-271);
- *              k_tile / k_tile_dense: pileup (:210-218) of the runs by bit-sliced
- *              counting, insertion columns (:276-294), vote for all thresholds (:232-253,
- *              :344-389) and the FASTA body bytes; k_consensus: tiles whose depth or
- *              insertion layout exceeds one workgroup.
+ *   device (2) k_tile_dense / k_tile: parsecigar (:46-82) + the maxdel rule (:210) of every
+ *              piece of the tile's window, staged in LDS (k_tile: layer by layer), its
+ *              runs (seqout intervals mapped to query bases or to '-') counted by bit-sliced
+ *              counters (:210-218), insertion columns (:276-294), vote for all thresholds
+ *              (:232-253, :344-389) and the FASTA body bytes;
+ *          (3) k_reads: the insertion events (:73-75, :221) hashed by (position, motif)
+ *              into per-tile open-addressing tables with per-entry counts (:262-271), and
+ *              the run records of the rare long pieces;
+ *          (4) k_consensus: tiles whose depth or insertion layout exceeds one workgroup.
  */
 #ifndef S2C_H
 #define S2C_H
@@ -41,7 +42,7 @@
 extern "C" {
 #endif
 
-#define S2C_ABI_VERSION 6
+#define S2C_ABI_VERSION 7
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define S2C_OK            0
@@ -90,10 +91,13 @@ int s2c_layout(int64_t *out, int n);
                                 insertion events; key0 = ref_off + POS-1 (int64), an event at
                                 seqout index k has global key key0 + k, used when ≥ ref_off */
 #define S2C_PF_LONG   0x08   /* span > the batch's window: reached through the tile long lists */
-#define S2C_PF_RUNS   0x10   /* a non-dense tile reads its runs: k_reads writes them (dense tiles
-                                walk their window's pieces themselves) */
+#define S2C_PF_RUNS   0x10   /* a long piece: k_reads writes its run records (the tile long lists read
+                                them; short pieces are walked by the tile kernels themselves) */
 #define S2C_PF_DASH   0x20   /* SEQ holds '-' chars (with S2C_PF_X): the maxdel rule (:210) counts
                                 them from the planes; without it a read's SEQ adds no '-' */
+#define S2C_PF_SIMPLE 0x40   /* one M / = / X token, no prefix words, not long, no '-' in SEQ: its
+                                seqout is SEQ[0:take] (:64-69) and slen holds take = min(l, len(SEQ))
+                                (every consumer's min(l, slen) is then take) */
 
 /* run record (device-written by k_reads, parallel to ops[]): {gpos, len | kind << 24, qlo, qhi} */
 #define S2C_RUN_EMPTY   0u
@@ -105,13 +109,16 @@ int s2c_layout(int64_t *out, int n);
 
 /* tile record tiles[t][S2C_TILE_WORDS] */
 #define S2C_TILE_WORDS   20  /* {a, b, ref, flags, boff, bcap, loff, lcap, cb0, ccap, lp0, lp1, nev,
-                                 pf0, pf1, o0, o1, qw0, qw1, 0}: the window's pieces [pf0, pf1) (short
-                                 pieces starting in [a/32 - kwin, b/32)), their op slots [o0, o1) and
-                                 base plane words [qw0, qw1) */
+                                 pf0, pf1, o0, o1, qw0, qw1, nl}: the window's pieces [pf0, pf1) (short
+                                 pieces starting in [a/32 - kwin, b/32)), their op slots [o0, o1),
+                                 base plane words [qw0, qw1), and nl, the window's LAYERS: layer l takes
+                                 from every start word s of the window its pieces
+                                 [ps[s] + n_s*l/nl, ps[s] + n_s*(l+1)/nl) (n_s = ps[s+1] - ps[s]) — one
+                                 LDS chunk of k_tile (S2C_CHUNK_*) */
 #define S2C_TILE_DEEP     1  /* several work items: counts summed in HBM, voted by k_consensus */
 #define S2C_TILE_GENERAL  2  /* insertion layout beyond k_tile's LDS: voted by k_consensus */
 #define S2C_TILE_DENSE    4  /* routed to k_tile_dense (one item, no insertion keys, no long pieces) */
-#define S2C_ITEM_WORDS    4  /* work item {tile, chunk, 0, 0} */
+#define S2C_ITEM_WORDS    4  /* work item {tile, chunk, l0, l1}: the tile's layers [l0, l1) */
 #define S2C_EPI_KEYS    256  /* insertion keys per tile k_tile's epilogue holds in LDS */
 /* insertion columns per tile k_tile's epilogue holds in LDS, by words per tile */
 #define S2C_LDS_COLS(nwp) ((nwp) <= 16 ? 640 : ((nwp) == 32 ? 448 : 192))
@@ -123,6 +130,21 @@ int s2c_layout(int64_t *out, int n);
    readable up to their end rounded up to 16 bytes. */
 #define S2C_DENSE_BYTES(ns, nq) (((4 * (ns) + 30) & ~15) + ((8 * (nq) + 30) & ~15) + ((12 * (ns) + 1024 + 15) & ~15))
 #define S2C_DENSE_QW   4096  /* base plane words of a dense tile's window (17-bit query offsets) */
+/* k_tile's LDS chunk (one layer of a tile window): per piece (one thread each) its base
+   plane words {p0, p1} through the word after its last base (funnel shift), its non-ACGT
+   words (pieces with S2C_PF_X) and its op words (pieces without S2C_PF_SIMPLE), each in
+   16-byte blocks from the 16-byte boundary below; its run records (= op slots).  Caps per
+   layer, and run records per 32-position word and counting lane (8-bit counters: <=
+   S2C_CHUNK_LANE_RECS * lanes per word).  A work item's run records per word are <=
+   S2C_ITEM_RECS (its u16 histogram). */
+#define S2C_CHUNK_PIECES     256
+#define S2C_CHUNK_PBLK      1280
+#define S2C_CHUNK_XBLK       256
+#define S2C_CHUNK_OBLK       128
+#define S2C_CHUNK_RECS       768
+#define S2C_CHUNK_LANE_RECS  248
+#define S2C_CHUNK_SEGS       128
+#define S2C_ITEM_RECS      60000
 #define S2C_SHORT_MOTIF  16  /* motifs up to this length are hashed inline (3-bit codes) */
 #define S2C_CODE_FILL     0  /* internal vote char of a fill position */
 #define S2C_CODE_ERR   0xFF  /* vote char where the vote hit a missing amb key (:367) */
@@ -226,7 +248,8 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
     const int64_t  *ref_len;   /* [n_refs] */
     const int64_t  *ref_off;   /* [n_refs] global coordinate of position 0 */
     const int64_t  *ref_cov_reads; /* [n_refs] pieces with a counted char (0 ⇒ Σcov == 0, :334-341) */
-    const uint32_t *pc;        /* [n_pieces+1][4] pieces sorted by start word (+ sentinel {0,0,n_ops,0}) */
+    const uint32_t *pc;        /* [n_pieces+1][4] pieces sorted by start word (+ sentinel {0, qh end, n_ops, 0}):
+                                  piece k's planes are query bases [16 qh_k, 16 qh_{k+1}) */
     const uint32_t *ops;       /* [n_ops] op words: prefix words, CIGAR tokens */
     const uint32_t *bq;        /* [n_qwords][2] base planes {p0, p1} of 32 query bases:
                                   A 00, C 01, G 10, T 11 (p1 p0); non-ACGT chars 00 */
@@ -242,6 +265,7 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
     const uint32_t *lp;        /* [n_long] run slots of the long pieces overlapping each tile:
                                   tile t's are lp[tiles[t].lp0 .. tiles[t].lp1) */
     const uint32_t *wtile;     /* [n_words] tile of each 32-position word (0xFFFFFFFF: padding) */
+    const uint32_t *ps;        /* [n_words+1] pieces starting in words [W0, W1) are [ps[W0], ps[W1]) */
 } s2c_batch_arrays;
 
 int  s2c_batch_info_get(const s2c_batch *b, s2c_batch_info *out);
@@ -292,7 +316,7 @@ int s2c_synth_write(const s2c_synth_spec *spec, const char *path, int64_t *n_rea
 typedef struct {
     /* ---- packed batch (device copies of s2c_batch_arrays) ---- */
     const uint32_t *pc, *ops, *bq, *bx, *rs;
-    const uint32_t *tiles, *items, *dense, *deep, *lp, *wtile, *rlist;
+    const uint32_t *tiles, *items, *dense, *deep, *lp, *wtile, *rlist, *ps;
     int64_t n_pieces, n_ops, n_qwords, n_tiles, n_items, n_dense, n_deep, padded_len, chunk, n_rlist, dense_lds;
     int32_t kwin, tile_max;
 
@@ -337,10 +361,12 @@ typedef struct {
 int s2c_workspace_sizes(const s2c_batch_info *info, int32_t n_thr, s2c_ws_sizes *out);
 
 /* Stage order (s2c_run): s2c_reads → s2c_pileup → s2c_consensus, one stream.
- * (2) parsecigar + maxdel per piece → runs; insertion events → per-tile hash tables
+ * (3) insertion events of the pieces that emit them → per-tile hash tables; parsecigar +
+ *     maxdel → run records of the long pieces (the tile long lists)
  *                                                           (:46-82, :210, :221, :262-271) */
 int s2c_reads(const s2c_dev *d, void *stream);
-/* (2)-(4) per tile: pileup of the runs, insertion columns, vote (all thresholds, IUPAC,
+/* (2)-(4) per tile: parsecigar + maxdel of its window's pieces and pileup of their runs,
+ * insertion columns, vote (all thresholds, IUPAC,
  * min-depth/fill), tile statistics and FASTA body bytes; deep / general tiles leave their
  * counts in HBM                         (:210-218, :232-253, :256-311, :344-397) */
 int s2c_pileup(const s2c_dev *d, void *stream);

@@ -62,7 +62,8 @@ _P32 = C.POINTER(C.c_uint32)
 
 class BatchArrays(C.Structure):
     _fields_ = [("ref_len", _P64), ("ref_off", _P64), ("ref_cov_reads", _P64)] + \
-        [(n, _P32) for n in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "rlist", "lp", "wtile")]
+        [(n, _P32) for n in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "rlist", "lp", "wtile",
+                             "ps")]
 
 
 class SynthSpec(C.Structure):
@@ -79,7 +80,7 @@ _VP = C.c_void_p
 class Dev(C.Structure):
     """Mirror of ``s2c_dev`` (include/s2c.h)."""
     _fields_ = [(n, _VP) for n in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile",
-                                   "rlist")] + \
+                                   "rlist", "ps")] + \
         [(n, C.c_int64) for n in ("n_pieces", "n_ops", "n_qwords", "n_tiles", "n_items", "n_dense", "n_deep",
                                   "padded_len", "chunk", "n_rlist", "dense_lds")] + [
         ("kwin", C.c_int32), ("tile_max", C.c_int32),

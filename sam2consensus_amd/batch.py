@@ -76,6 +76,7 @@ class HostBatch:
         self.bq = _view(a.bq, 2 * i.n_qwords, np.uint32).reshape(-1, 2)
         self.bx = _view(a.bx, i.n_qwords, np.uint32)
         self.rs = _view(a.rs, i.n_words + 1, np.uint32)
+        self.ps = _view(a.ps, i.n_words + 1, np.uint32)
         # tile plan
         self.tiles = _view(a.tiles, i.n_tiles * L.S2C_TILE_WORDS, np.uint32).reshape(-1, L.S2C_TILE_WORDS)
         self.items = _view(a.items, i.n_items * L.S2C_ITEM_WORDS, np.uint32).reshape(-1, L.S2C_ITEM_WORDS)

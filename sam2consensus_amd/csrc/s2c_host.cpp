@@ -212,7 +212,7 @@ struct s2c_batch {
     s2c_batch_info info{};
     std::vector<std::string> names;
     std::vector<int64_t> ref_len, ref_off, ref_reads;
-    std::vector<uint32_t> pc, ops, bq, bx, rs, tiles, items, dense, deep, lp, wtile, rlist;
+    std::vector<uint32_t> pc, ops, bq, bx, rs, tiles, items, dense, deep, lp, wtile, rlist, ps;
     std::vector<uint32_t> kmin, kmax;   // host only: global key range of each piece's insertion events
 };
 
@@ -899,7 +899,6 @@ constexpr double E_TARGET = 262144.0;                // aligned bases per deep t
 // LDS a shallow tile's window is planned to (one wave per tile, ~10 resident per CU; C5's
 // 30x gives 1024-position tiles — measured faster than 512, profiles/r02)
 constexpr double DENSE_PLAN_BYTES = 16384.0;
-constexpr uint32_t FLUSH_RECS = 248;                 // records per lane between counter flushes
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline int64_t align_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }
 inline uint32_t pow2_at_least(uint64_t v) {
@@ -950,23 +949,12 @@ static bool dense_fits(const uint32_t *tw, int64_t K) {
     return dense_bytes(tw, K) <= S2C_DENSE_LDS && (int64_t)(tw[18] - tw[17]) <= S2C_DENSE_QW;
 }
 
-// PF_RUNS on the pieces a non-dense tile reads runs of (its window, its long pieces), and
-// the list of pieces k_reads walks (those, and the pieces emitting insertion events).
+// PF_RUNS on the long pieces (the tile long lists read k_reads' run records of them; the
+// tile kernels walk every short piece of their windows themselves), and the list of pieces
+// k_reads walks (those, and the pieces emitting insertion events).
 static void mark_runs(s2c_batch *b) {
-    const int64_t NP = b->info.n_pieces, NT = b->info.n_tiles;
-    std::vector<int32_t> diff(NP + 1, 0);
-    for (int64_t t = 0; t < NT; t++) {
-        const uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
-        if (tw[3] & S2C_TILE_DENSE) continue;
-        diff[tw[13]]++;
-        diff[tw[14]]--;
-    }
+    const int64_t NP = b->info.n_pieces;
     std::vector<uint8_t> need(NP, 0);
-    int32_t run = 0;
-    for (int64_t k = 0; k < NP; k++) {
-        run += diff[k];
-        need[k] = run > 0;
-    }
     for (uint32_t slot : b->lp) {   // long pieces (listed by slot)
         if (b->info.n_long == 0) break;
         int64_t lo = 0, hi = NP - 1;
@@ -985,6 +973,114 @@ static void mark_runs(s2c_batch *b) {
     }
     b->info.n_rlist = (int64_t)b->rlist.size();
     if (b->rlist.empty()) b->rlist.push_back(0);
+}
+
+// ------------------------------------------------------------------ k_tile's layer plan
+// k_tile stages a tile's window in LDS one LAYER at a time: the window's start words
+// [S0, S1) (S0 = max(W0 - K, 0)) are its segments, and layer l of nl takes from segment s
+// its pieces [ps[s] + n_s*l/nl, ps[s] + n_s*(l+1)/nl) — every layer touches every word of
+// the tile alike.  A layer must fit the chunk (S2C_CHUNK_*): pieces, 16-byte blocks of base
+// planes / non-ACGT words / op words (per piece the kernel's count for the worst 16-byte
+// alignment, so a shard's re-laid planes fit too), run records, and per word <=
+// S2C_CHUNK_LANE_RECS records per counting lane.
+struct PieceBlocks {          // prefix sums over the sorted pieces (mod 2^32: differences exact)
+    std::vector<uint32_t> pb, xb, ob;
+};
+static void piece_blocks(const s2c_batch *b, PieceBlocks &B) {
+    const int64_t NP = b->info.n_pieces;
+    B.pb.assign(NP + 1, 0);
+    B.xb.assign(NP + 1, 0);
+    B.ob.assign(NP + 1, 0);
+    for (int64_t k = 0; k < NP; k++) {
+        const uint32_t w3 = b->pc[4 * k + 3], fl = w3 >> 24, len = w3 & 0xFFFFFFu;
+        const uint32_t nops = b->pc[4 * k + 6] - b->pc[4 * k + 2];
+        const uint32_t nw = ((16 + len + 31) >> 5) + 1;   // plane words, worst start phase
+        uint32_t pb = 0, xb = 0, ob = 0;
+        if (!(fl & S2C_PF_LONG)) {
+            pb = (8 * nw + 15) / 16 + 1;
+            if (fl & S2C_PF_X) xb = (4 * nw + 15) / 16 + 1;
+            if (!(fl & S2C_PF_SIMPLE)) ob = (4 * nops + 15) / 16 + 1;
+        }
+        B.pb[k + 1] = B.pb[k] + pb;
+        B.xb[k + 1] = B.xb[k] + xb;
+        B.ob[k + 1] = B.ob[k] + ob;
+    }
+}
+
+struct LayerSeg { uint64_t p0, n; };
+static inline uint64_t layer_lo(const LayerSeg &g, uint64_t l, uint64_t nl) { return g.p0 + g.n * l / nl; }
+
+static bool layer_fits(const s2c_batch *b, const PieceBlocks &B, const std::vector<LayerSeg> &seg, int64_t S0,
+                       int64_t W0, int64_t W1, int64_t K, int64_t G, uint64_t l, uint64_t nl, std::vector<int64_t> &recs) {
+    const size_t NS = seg.size();
+    uint64_t np = 0, pb = 0, xb = 0, ob = 0, rc = 0;
+    for (size_t i = 0; i < NS; i++) {
+        const uint64_t lo = layer_lo(seg[i], l, nl), hi = layer_lo(seg[i], l + 1, nl);
+        recs[i] = (int64_t)(b->pc[4 * hi + 2] - b->pc[4 * lo + 2]);
+        np += hi - lo;
+        pb += (uint32_t)(B.pb[hi] - B.pb[lo]);
+        xb += (uint32_t)(B.xb[hi] - B.xb[lo]);
+        ob += (uint32_t)(B.ob[hi] - B.ob[lo]);
+        rc += (uint64_t)recs[i];
+    }
+    if (np > S2C_CHUNK_PIECES || pb > S2C_CHUNK_PBLK || xb > S2C_CHUNK_XBLK || ob > S2C_CHUNK_OBLK || rc > S2C_CHUNK_RECS)
+        return false;
+    for (int64_t W = W0; W < W1; W++) {
+        int64_t r = 0;
+        for (int64_t s = std::max(W - K, S0); s <= W; s++) r += recs[s - S0];
+        if (r > (int64_t)S2C_CHUNK_LANE_RECS * G) return false;
+    }
+    return true;
+}
+
+// nl of tile [a, e) (0: a layer cannot fit, i.e. one piece alone exceeds the chunk)
+static int64_t plan_layers(const s2c_batch *b, const PieceBlocks &B, int64_t K, uint64_t a, uint64_t e, int64_t G) {
+    const int64_t W0 = (int64_t)(a >> 5), W1 = (int64_t)((e + 31) >> 5), S0 = std::max<int64_t>(W0 - K, 0);
+    std::vector<LayerSeg> seg;
+    uint64_t tp = 0, tb = 0, tr = 0, maxn = 0;
+    for (int64_t s = S0; s < W1; s++) {
+        const uint64_t p0 = b->ps[s], n = b->ps[s + 1] - p0;
+        seg.push_back({p0, n});
+        tp += n;
+        tb += (uint32_t)(B.pb[p0 + n] - B.pb[p0]);
+        tr += b->pc[4 * (p0 + n) + 2] - b->pc[4 * p0 + 2];
+        maxn = std::max(maxn, n);
+    }
+    if (maxn == 0) return 1;
+    std::vector<int64_t> recs(seg.size());
+    uint64_t nl = std::max<uint64_t>({1, (tp * 10 / 9) / S2C_CHUNK_PIECES + 1, (tb * 10 / 9) / S2C_CHUNK_PBLK + 1,
+                                      (tr * 10 / 9) / S2C_CHUNK_RECS + 1});
+    nl = std::min(nl, maxn);
+    for (;; nl = nl + 1 + nl / 16) {
+        if (nl > maxn) nl = maxn;
+        bool ok = true;
+        for (uint64_t l = 0; l < nl && ok; l++) ok = layer_fits(b, B, seg, S0, W0, W1, K, G, l, nl, recs);
+        if (ok) return (int64_t)nl;
+        if (nl == maxn) return 0;
+    }
+}
+
+// Work items of a tile of nl layers: {tile, c, l0, l1}, enough that each one's run records
+// per word stay <= S2C_ITEM_RECS (its u16 histogram) and, past 32 layers, an item takes
+// <= 16 (parallelism for the deep tiles: C4's 16.5 kb at 100,000x).
+static int64_t plan_items(const s2c_batch *b, int64_t K, uint64_t a, uint64_t e, int64_t nl) {
+    const int64_t W0 = (int64_t)(a >> 5), W1 = (int64_t)((e + 31) >> 5), S0 = std::max<int64_t>(W0 - K, 0);
+    int64_t nch = nl > 32 ? (nl + 15) / 16 : 1;
+    for (;; nch++) {
+        bool ok = true;
+        for (int64_t c = 0; c < nch && ok; c++) {
+            const uint64_t l0 = (uint64_t)(c * nl / nch), l1 = (uint64_t)((c + 1) * nl / nch);
+            for (int64_t W = W0; W < W1 && ok; W++) {
+                int64_t r = 0;
+                for (int64_t s = std::max(W - K, S0); s <= W; s++) {
+                    const LayerSeg g{b->ps[s], (uint64_t)(b->ps[s + 1] - b->ps[s])};
+                    r += b->pc[4 * layer_lo(g, l1, nl) + 2] - b->pc[4 * layer_lo(g, l0, nl) + 2];
+                }
+                ok = r <= S2C_ITEM_RECS;
+            }
+        }
+        if (ok || nch >= nl) return nch;
+    }
 }
 
 // Global coordinate of each reference's position 0 (header order, S2C_POS_ALIGN-aligned).
@@ -1480,11 +1576,16 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
                 }
                 if (q.lng) fl |= S2C_PF_LONG;
                 memcpy(o, &c.toks[r.tok], 4 * (size_t)r.ntok);
+                uint32_t slen = r.slen;
+                if (!q.range && !q.ins && !q.lng && r.ntok == 1 && op_bases(c.toks[r.tok] & 15u) && !(fl & S2C_PF_DASH)) {
+                    fl |= S2C_PF_SIMPLE;   // seqout = SEQ[0:take]: the field holds take (s2c.h)
+                    slen = std::min<uint32_t>(c.toks[r.tok] >> 4, r.slen);
+                }
                 uint32_t *pr = &b->pc[4 * (size_t)k];
                 pr[0] = (uint32_t)q.gpos;
                 pr[1] = (uint32_t)(qoff[k] / 16);
                 pr[2] = (uint32_t)ooff[k];
-                pr[3] = r.slen | (fl << 24);
+                pr[3] = slen | (fl << 24);
                 // the read's planes, 16 bases at a time (both sides start at multiples of 16)
                 const uint16_t *sq = (const uint16_t *)c.bq.data(), *sx = (const uint16_t *)c.bx.data();
                 for (uint64_t h = 0; h < (r.slen + 15) / 16; h++) {
@@ -1503,10 +1604,18 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
             for (auto &t : th) t.join();
         }
         uint32_t *pr = &b->pc[4 * (size_t)NP];   // sentinel
+        pr[1] = (uint32_t)(NQ / 16);
         pr[2] = (uint32_t)NOPS;
-        // run-slot CSR by start word
-        for (int64_t k = 0; k < NP; k++) b->rs[(pcs[order[k]].gpos >> 5) + 1] += pcs[order[k]].nslots;
-        for (int64_t w = 0; w < NW; w++) b->rs[w + 1] += b->rs[w];
+        // run-slot and piece CSRs by start word
+        b->ps.assign(NW + 1, 0);
+        for (int64_t k = 0; k < NP; k++) {
+            b->rs[(pcs[order[k]].gpos >> 5) + 1] += pcs[order[k]].nslots;
+            b->ps[(pcs[order[k]].gpos >> 5) + 1]++;
+        }
+        for (int64_t w = 0; w < NW; w++) {
+            b->rs[w + 1] += b->rs[w];
+            b->ps[w + 1] += b->ps[w];
+        }
     }
 
     // ---- tiles: width from depth; a shallow tile keeps its window's runs in LDS ----
@@ -1596,12 +1705,14 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
             I.n_ins_bases += e.len;
         }
 
-    // ---- work items: lane groups of G = 256 / nwp lanes per word, ≤ FLUSH_RECS candidate
-    //      slots per lane per item ----
+    // ---- work items: per tile its layers (k_tile's LDS chunks; lane groups of G = 256 / nwp
+    //      lanes per word) split into items ----
     int64_t nwp = 8;
     while (nwp * 32 < tile_max) nwp *= 2;
-    const int64_t G = 256 / nwp, CHK = (int64_t)FLUSH_RECS * G;
-    I.chunk = CHK;
+    const int64_t G = 256 / nwp;
+    I.chunk = 0;   // (the most layers of any tile)
+    PieceBlocks PB;
+    piece_blocks(b, PB);
     const int64_t lcols = S2C_LDS_COLS(nwp);
     b->tiles.assign((size_t)NT * S2C_TILE_WORDS, 0u);
     uint64_t boff = 0, loff = 0, coff = 0;
@@ -1630,7 +1741,10 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
         int64_t maxc = 0;
         for (int64_t W = w0; W < w1; W++)
             maxc = std::max<int64_t>(maxc, (int64_t)b->rs[W + 1] - (int64_t)b->rs[std::max<int64_t>(W - K, 0)] + nlg);
-        const int64_t nch = std::max<int64_t>(1, ceil_div(maxc, CHK));
+        const int64_t nl = plan_layers(b, PB, K, (uint64_t)T.a, (uint64_t)T.b, G);
+        if (nl <= 0) return s2c_set_error(S2C_ERR_LIMIT, "a read whose SEQ or CIGAR exceeds k_tile's LDS chunk");
+        const int64_t nch = plan_items(b, K, (uint64_t)T.a, (uint64_t)T.b, nl);
+        I.chunk = std::max<int64_t>(I.chunk, nl);
         const int64_t wruns = (int64_t)b->rs[w1] - (int64_t)b->rs[std::max<int64_t>(w0 - K, 0)];
         runs_max = std::max(runs_max, wruns);
         uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
@@ -1645,16 +1759,18 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
         tw[4] = (uint32_t)boff; tw[5] = bcap; tw[6] = (uint32_t)loff; tw[7] = nlong[t];
         tw[8] = (uint32_t)coff; tw[9] = (uint32_t)ccap[t]; tw[10] = lcnt[t]; tw[11] = lcnt[t + 1];
         tw[12] = nev[t];
+        tw[19] = (uint32_t)nl;
         boff += bcap;
         loff += nlong[t];
         coff += ccap[t];
         if (fl == S2C_TILE_DENSE) {
             I.dense_lds = std::max<int64_t>(I.dense_lds, dense_bytes(tw, K));
-            const uint32_t it[S2C_ITEM_WORDS] = {(uint32_t)t, 0u, 0u, 0u};
+            const uint32_t it[S2C_ITEM_WORDS] = {(uint32_t)t, 0u, 0u, (uint32_t)nl};
             b->dense.insert(b->dense.end(), it, it + S2C_ITEM_WORDS);
         } else {
             for (int64_t c = 0; c < nch; c++) {
-                const uint32_t it[S2C_ITEM_WORDS] = {(uint32_t)t, (uint32_t)c, 0u, 0u};
+                const uint32_t it[S2C_ITEM_WORDS] = {(uint32_t)t, (uint32_t)c, (uint32_t)(c * nl / nch),
+                                                     (uint32_t)((c + 1) * nl / nch)};
                 b->items.insert(b->items.end(), it, it + S2C_ITEM_WORDS);
             }
         }
@@ -1770,11 +1886,19 @@ extern "C" int s2c_batch_shard(const s2c_batch *b, int64_t t0, int64_t t1, s2c_b
                 dx[d] = sx[a];
             }
         }
+        s->pc[4 * (size_t)NS + 1] = (uint32_t)(qoff[NS] / 16);
         s->pc[4 * (size_t)NS + 2] = (uint32_t)ooff[NS];
     }
     s->rs.assign(NW + 1, 0u);
-    for (int64_t i = 0; i < NS; i++) s->rs[(s->pc[4 * i] >> 5) + 1] += (uint32_t)(ooff[i + 1] - ooff[i]);
-    for (int64_t w = 0; w < NW; w++) s->rs[w + 1] += s->rs[w];
+    s->ps.assign(NW + 1, 0u);
+    for (int64_t i = 0; i < NS; i++) {
+        s->rs[(s->pc[4 * i] >> 5) + 1] += (uint32_t)(ooff[i + 1] - ooff[i]);
+        s->ps[(s->pc[4 * i] >> 5) + 1]++;
+    }
+    for (int64_t w = 0; w < NW; w++) {
+        s->rs[w + 1] += s->rs[w];
+        s->ps[w + 1] += s->ps[w];
+    }
     // ---- tiles [t0, t1): slot bases re-based, long lists remapped, plan lists re-indexed
     const int64_t NT = t1 - t0;
     J.n_tiles = NT;
@@ -1862,6 +1986,7 @@ extern "C" int s2c_batch_arrays_get(const s2c_batch *b, s2c_batch_arrays *o) {
     o->lp = b->lp.data();
     o->wtile = b->wtile.data();
     o->rlist = b->rlist.data();
+    o->ps = b->ps.data();
     return S2C_OK;
 }
 

@@ -77,7 +77,9 @@ static_assert(PF == S2C_EPI_KEYS, "k_tile key capacity");
 constexpr uint32_t MODE_RUN = 0, MODE_STORE = 1, MODE_ADD = 2, MODE_ADD_KEEP = 3;
 
 struct TileArgs {
-    const uint32_t *rs, *runs, *bq, *bx, *tiles, *lp;
+    const uint32_t *rs, *runs, *bq, *bx, *tiles, *lp, *pc, *ops, *ps;
+    const void *bq_end, *bx_end, *ops_end, *pc_end;   // ends of the DMA sources (buffer ranges)
+    uint32_t maxdel_active, maxdel;
     uint32_t *ibkt, *ilong, *ilong_n;
     const double *thresholds;
     const uint8_t *fill;
@@ -621,46 +623,222 @@ __device__ __forceinline__ void tile_epilogue_fast(const D &d, uint32_t tile, co
 }
 
 // ======================================================================= k_tile
-// One workgroup per work item = (tile [a, b) of ≤ 32·NWP positions, chunk k).  Lane L owns
-// the 32-position word w = L / G of the tile (G = 256 / NWP lanes per word, a wave holds
-// whole words) and takes candidate j ≡ L mod G of the word's candidates: the run slots of
-// the short pieces starting in the kwin + 1 words up to w ([rs[W-kwin], rs[W+1])), then the
-// tile's long-piece slots; the item takes candidates [k·chunk, (k+1)·chunk).  A candidate
-// run covering the word gives one record: valid = the word positions it covers, planes =
-// its query bases there (a funnel shift of two plane words).  Records are counted 8 at a
-// time into bit-sliced counters X = C|T, Y = G|T, Z = T, V = covered A/C/G/T (and '-' as a
-// rare ripple counter); non-ACGT bases of SEQ (N / '-') are taken off their A / C counts
-// and added to N / '-' with LDS atomics.  The flush transposes the counters and adds, two
-// u16 per LDS atomic, A = V − X − Y + Z, C = X − Z, G = Y − Z, T = Z, '-' into the tile's
-// histogram.
-constexpr int GS = 8;   // records per counting group
+// One workgroup per work item = (tile [a, b) of ≤ 32·NWP positions, its layers [l0, l1)).
+// The tile's WINDOW — the short pieces starting in the kwin words before it and in it — is
+// cut into nl LAYERS (host plan, s2c_host.cpp plan_layers): layer ℓ takes from every start
+// word s of the window (a SEGMENT) its pieces [ps[s] + n_s·ℓ/nl, ps[s] + n_s·(ℓ+1)/nl), so
+// every layer reaches every word of the tile alike.  One layer at a time is a CHUNK in LDS:
+//   1 table  per segment its piece, op-slot and base-plane ranges and their LDS offsets
+//   2 DMA    each segment's base planes {p0, p1} into LDS (16-byte LDS-DMA, the source in
+//            SGPRs; the waves take segments round-robin)
+//   3 walk   thread per piece: the parsecigar token walk (:64-81) with the maxdel rule (:210)
+//            → one run record per op word in LDS {gpos, q << 11 | len} (q: the run's first
+//            base in the LDS planes); coverage and counted '-' runs (D/N/P) into position
+//            difference arrays; the N / '-' chars of SEQ (:212, :217) into the histogram
+//   4 count  lane (word w, g of G) takes the records of segments W-kwin .. W — one
+//            contiguous LDS range — g, g + G, ..., 8 at a time: two plane words from LDS,
+//            funnel shift, masks X = p0 (C|T), Y = p1 (G|T), Z = X & Y (T) into Harley–Seal
+//            carry-save counters (8 bit-planes each)
+// Counters are flushed (8×8 bit transposes, u16 pairs by LDS atomics) before they can
+// overflow; coverage V comes from the difference array, so per position A = V − X − Y + Z −
+// N, C = X − Z − '-'(SEQ), G = Y − Z, T = Z, N, '-' = D + counted '-'(SEQ).  Each base plane
+// word is fetched from HBM once per tile (chunks are disjoint; neighbouring tiles share kwin
+// start words).  Long pieces (span > the window) come from k_reads' run records through
+// the tile's long list.  Then the epilogue (a single-item tile) or the counts to HBM.
+constexpr int GS = 8;                 // records per counting group
+constexpr int CSEG = S2C_CHUNK_SEGS;  // segments of a window (≤ 64 words + kwin ≤ 32)
+constexpr uint32_t RPAD = 256;        // zero records after a chunk's last (a group's reads past it)
+// raw histogram slots while counting ("-ACGNT" slots after the reconstruction)
+constexpr uint32_t SL_SDC = 0, SL_SD = 1, SL_X = 2, SL_Y = 3, SL_N = 4, SL_Z = 5;
 // A buffer offset past every buffer (their sizes stay below it, checked on the host) that
-// still leaves room for the loads' immediate and group offsets: the hardware returns zeros.
+// still leaves room for the loads' immediate offsets: the hardware returns zeros.
 constexpr uint32_t OOR = 0xF0000000u;
 
-// PIPE: the count loop software-pipelined (next group's run records in flight during this
-// group's base windows) at 2 waves/SIMD — it needs the registers; without, 3 waves/SIMD.
-// Measured crossover (profiles/r02): deep batches (C3 1000x, C4) gain 3-11 %, C2 (500x with
-// insertion epilogues) loses 7 %; launches pick PIPE for batches with >= 5 run slots per
-// position (s2c_pileup).
+// A chunk in LDS: per chunk piece (segment-major, thread t stages and walks piece t) its
+// 16-byte blocks of base planes (pl, block 0 a pad so plane word −1 is readable), of
+// non-ACGT words (xl) and of op words (ol), at the block-scan offsets of the pieces before
+// it; its run records runl[recPre[t] + j − opoff] for op words j.  Segment σ (start word
+// S0 + σ) holds chunk pieces [segP[σ], segP[σ+1]) and records [segR[σ], segR[σ+1]).
+struct ChunkLds {
+    uint32_t ps[CSEG + 1];                  // first piece of each start word of the window (tile-constant)
+    uint32_t segP[2][CSEG + 1];             // by layer parity: the next layer's table is built during this one
+    uint32_t segR[CSEG + 1];
+    uint32_t recPre[S2C_CHUNK_PIECES + 1];
+    uint32_t wsumA[2][4], wsumB[2][4];      // block scans: wave totals
+    alignas(16) uint4 pl[1 + S2C_CHUNK_PBLK + 1];
+    alignas(16) uint4 xl[S2C_CHUNK_XBLK];
+    alignas(16) uint4 ol[S2C_CHUNK_OBLK];
+    uint2 runl[S2C_CHUNK_RECS + RPAD];
+};
+template <uint32_t ICOL>
+struct EpiLds {
+    FastLds<ICOL> L;
+    uint32_t cols[ICOL * NSYM];
+};
+template <uint32_t ICOL>
+union TileLds {
+    ChunkLds c;
+    EpiLds<ICOL> e;
+};
+
+// The N / '-' chars of SEQ among LDS plane bases [q, q + l), whose first lies at
+// tile-relative position r0: 'N' (counted as A by the planes) into SL_N; '-' (counted as C)
+// into SL_SD and, unless the read's '-' are maxdel-dropped (:210), SL_SDC.
+template <int NWP>
+__device__ void x_fix(const uint2 *bql, const uint32_t *xl, uint32_t xd, uint32_t q, uint32_t l, uint32_t r0, bool drop,
+                      uint32_t *hist) {
+    using H = Hist<NWP>;
+    for (uint32_t v = q >> 5; v <= (q + l - 1) >> 5; v++) {
+        uint32_t xm = xl[v + xd];
+        if (!xm) continue;
+        const int32_t b0 = (int32_t)(32 * v) - (int32_t)q;   // run offset of the word's bit 0
+        if (b0 < 0) xm &= 0xFFFFFFFFu << (uint32_t)(-b0);
+        if (b0 + 32 > (int32_t)l) xm &= 0xFFFFFFFFu >> (uint32_t)(b0 + 32 - (int32_t)l);
+        const uint32_t p0 = bql[v].x;
+        while (xm) {
+            const uint32_t bit = (uint32_t)__builtin_ctz(xm);
+            xm &= xm - 1;
+            const uint32_t p = r0 + (uint32_t)(b0 + (int32_t)bit);
+            if ((p0 >> bit) & 1u) {
+                H::add1(hist, SL_SD, p, 1u);
+                if (!drop) H::add1(hist, SL_SDC, p, 1u);
+            } else {
+                H::add1(hist, SL_N, p, 1u);
+            }
+        }
+    }
+}
+
+// One piece of a chunk (record P, op words [P.z, oend) in LDS at opl[j + od], its SEQ[0] at
+// LDS plane base 16·P.y + qadj): parsecigar (:64-81) + maxdel (:210) → run records
+// runl[j + rd] (bases: {gpos, q << 11 | len}; others zero); coverage / counted '-' of the
+// tile part into dV / dD; N / '-' of SEQ via x_fix.  Everything from LDS.
+template <int NWP>
+__device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *opl, uint32_t od, uint2 *runl, uint32_t rd,
+                                 const uint2 *bql, const uint32_t *xl, uint32_t xd, uint32_t qadj, bool maxdel_active,
+                                 uint32_t maxdel, uint32_t a, uint32_t n, uint32_t *hist, int32_t *dV, int32_t *dD) {
+    const uint32_t fl = P.w >> 24, slen = P.w & 0xFFFFFFu;
+    uint32_t j = P.z;
+    if (fl & S2C_PF_LONG) {   // (its runs come through the tile long lists)
+        for (; j < oend; j++) runl[j + rd] = make_uint2(0u, 0u);
+        return;
+    }
+    uint32_t ka = 0, kb = 0xFFFFFFFFu;
+    if (fl & S2C_PF_RANGE) {
+        ka = opl[j + od];
+        kb = opl[j + 1 + od];
+        runl[j + rd] = runl[j + 1 + rd] = make_uint2(0u, 0u);
+        j += 2;
+    }
+    if (fl & S2C_PF_INS) {   // (its events: k_reads)
+        runl[j + rd] = runl[j + 1 + rd] = runl[j + 2 + rd] = make_uint2(0u, 0u);
+        j += 3;
+    }
+    const uint32_t ql = 16u * P.y + qadj;     // SEQ[0] in the LDS planes
+    bool drop = false;
+    if (maxdel_active) {   // :210 — D/N/P lengths + '-' chars of the bases taken
+        uint32_t dashes = 0, start = 0;
+        for (uint32_t i = j; i < oend; i++) {
+            const uint32_t w = opl[i + od], op = w & 15u, l = w >> 4;
+            if (op_bases(op)) {
+                uint32_t take = start < slen ? min(l, slen - start) : 0u;
+                if (fl & S2C_PF_DASH) {   // '-' chars of SEQ: x = 1, p1 = 0, p0 = 1
+                    uint32_t q = ql + start;
+                    while (take) {
+                        const uint32_t v = q >> 5, sh = q & 31u, nb = min(take, 32u - sh);
+                        const uint32_t mask = (nb >= 32 ? 0xFFFFFFFFu : ((1u << nb) - 1u)) << sh;
+                        dashes += (uint32_t)__popc(xl[v + xd] & bql[v].x & ~bql[v].y & mask);
+                        q += nb;
+                        take -= nb;
+                    }
+                }
+                start += l;
+            } else if (op_dash(op)) {
+                dashes += l;
+            } else if (op == S2C_OP_I || op == S2C_OP_S) {
+                start += l;
+            }
+        }
+        drop = dashes > maxdel;
+    }
+    const uint32_t e_tile = a + n;
+    uint32_t kk = 0, start = 0;
+    for (; j < oend; j++) {
+        const uint32_t w = opl[j + od], op = w & 15u, l = w >> 4;
+        uint2 r = make_uint2(0u, 0u);
+        const bool bases = op_bases(op);
+        if (bases || op_dash(op)) {
+            const uint32_t take = bases ? (start < slen ? min(l, slen - start) : 0u) : l;
+            const uint32_t s = max(kk, ka), e = min(kk + take, kb);
+            if (e > s) {
+                const uint32_t gp = P.x + (s - ka), len = e - s;
+                const uint32_t c0 = max(gp, a), c1 = min(gp + len, e_tile);   // the tile's part
+                if (bases) {
+                    const uint32_t q = ql + start + (s - kk);
+                    r = make_uint2(gp, (q << 11) | len);
+                    if (c1 > c0) {
+                        atomicAdd(&dV[c0 - a], 1);
+                        atomicSub(&dV[c1 - a], 1);
+                        if (fl & S2C_PF_X) x_fix<NWP>(bql, xl, xd, q + (c0 - gp), c1 - c0, c0 - a, drop, hist);
+                    }
+                } else if (!drop && c1 > c0) {
+                    atomicAdd(&dD[c0 - a], 1);
+                    atomicSub(&dD[c1 - a], 1);
+                }
+            }
+            kk += take;
+        }
+        if (bases || op == S2C_OP_I || op == S2C_OP_S) start += l;
+        runl[j + rd] = r;
+    }
+}
+
+// Exclusive scans of x and y over the workgroup (every thread calls: one barrier); tx / ty:
+// the totals.  wsum: this scan's own wave-total slots.
+__device__ __forceinline__ void scan256x2(uint32_t x, uint32_t y, uint32_t (*wsum)[4], uint32_t &ex, uint32_t &ey,
+                                          uint32_t &tx, uint32_t &ty) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t ix = __ockl_wfscan_add_u32(x, true), iy = __ockl_wfscan_add_u32(y, true);
+    if (lane == 63) {
+        wsum[0][wv] = ix;
+        wsum[1][wv] = iy;
+    }
+    lds_sync();
+    uint32_t ox = 0, oy = 0;
+    tx = ty = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < WG / 64; k++) {
+        const uint32_t vx = wsum[0][k], vy = wsum[1][k];
+        ox += k < wv ? vx : 0u;
+        oy += k < wv ? vy : 0u;
+        tx += vx;
+        ty += vy;
+    }
+    ex = ox + ix - x;
+    ey = oy + iy - y;
+}
+
 #ifndef S2C_TILE_XCD
 #define S2C_TILE_XCD 1
 #endif
-template <int NWP, bool PIPE>
-__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(PIPE ? 2 : 3))) void k_tile(const TileArgs d, const uint32_t *items) {
+template <int NWP>
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 3 : 2))) void k_tile(const TileArgs d, const uint32_t *items) {
     constexpr int G = WG / NWP, HP = 17 * NWP;
+    constexpr uint32_t NPOS = 32 * NWP;
     using H = Hist<NWP>;
     constexpr uint32_t ICOL = S2C_LDS_COLS(NWP);
+    static_assert(NWP + 32 < CSEG, "segments of a window");
     __shared__ __attribute__((aligned(16))) uint32_t hist[H::CS];
-    __shared__ uint32_t cols[ICOL * NSYM];
-    __shared__ FastLds<ICOL> L;
-    const uint32_t tid = threadIdx.x;
+    __shared__ int32_t dV[NPOS + 1], dD[NPOS + 1];
+    __shared__ uint32_t wtot[2][WG / 64];
+    __shared__ __attribute__((aligned(16))) TileLds<ICOL> U;
+    ChunkLds &C = U.c;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t w = tid / G, g = tid % G;
 #ifdef S2C_PROF
     unsigned long long tprof_t = 0;
 #endif
     TPROF_MARK(0);
-    if (tid < 64) L.amb[tid] = c_amb[tid];
 #if S2C_TILE_XCD
     // XCD-major: the blocks of one XCD (b ≡ x mod 8) take a contiguous range of items, so
     // neighbouring tiles' shared window reads meet in that XCD's L2
@@ -669,287 +847,54 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(PIPE ? 2 : 3
 #else
     const uint4 itv = ((const uint4 *)items)[blockIdx.x];
 #endif
-    const uint32_t tile = uni(itv.x), chunk = uni(itv.y);
+    const uint32_t tile = uni(itv.x), chunk = uni(itv.y), l0 = uni(itv.z), l1 = uni(itv.w);
     const TileRec T = tile_rec(d.tiles, tile);
+    const uint32_t nl = uni(d.tiles[(size_t)tile * S2C_TILE_WORDS + 19]);
     const uint32_t a = T.a, n = T.b - T.a;
-    const uint32_t W = (a >> 5) + w;
-    const bool active = 32u * w < n;
+    const uint32_t W0 = a >> 5, nwords = (n + 31) / 32, W = W0 + w;
+    const bool active = w < nwords;
+    const uint32_t K = d.kwin;
+    const uint32_t S0 = W0 >= K ? W0 - K : 0u, NS = W0 + nwords - S0;
     const bool counts_only = d.mode != MODE_RUN;
     const bool accumulate = d.mode >= MODE_ADD;
     const bool finish = !(T.flags & (S2C_TILE_DEEP | S2C_TILE_GENERAL)) && !counts_only;
     const bool deep = (T.flags & S2C_TILE_DEEP) != 0;
-    // ---- candidates of this lane: window slots [cw0, cw1) then long slots [lp0, lp1)
-    const uint32_t K = d.kwin;
-    const uint32_t cbase = uni(d.tiles[(size_t)tile * S2C_TILE_WORDS + 15]);   // the tile's first window slot (o0)
-    uint32_t cw0 = 0, cw1 = 0;
-    if (active) {
-        cw0 = d.rs[W >= K ? W - K : 0u];
-        cw1 = d.rs[W + 1];
-    }
-    const uint32_t nwin = cw1 - cw0, nlong = T.lp1 - T.lp0;
-    const uint32_t j0 = chunk * d.chunk, j1 = min(j0 + d.chunk, active ? nwin + nlong : 0u);
-    // window candidates of this lane: j = j0 + g + G·m < min(j1, nwin)
-    const uint32_t jw1 = min(j1, nwin);
-    const uint32_t nrec = j0 + g < jw1 ? (jw1 - j0 - g + G - 1) / G : 0u;
-    const uint32_t ngrp = uni(__ockl_wfred_max_u32((nrec + GS - 1) / GS));
-    const uint32_t voff = nrec ? (cw0 - cbase + j0 + g) * 16u : OOR;
-    const __amdgpu_buffer_rsrc_t rrun = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(d.runs + 4 * (size_t)cbase), (short)0, (int)(d.runs_bytes - 16u * cbase), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rbq = __builtin_amdgcn_make_buffer_rsrc((void *)d.bq, (short)0, (int)(8u * d.n_qwords), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rbx = __builtin_amdgcn_make_buffer_rsrc((void *)d.bx, (short)0, (int)(4u * d.n_qwords), 0x00020000);
 
-    // ---- zero the histogram (and, for a finished tile with insertions, the layout arrays)
+    // ---- zero the histogram and the difference arrays; the window's piece CSR
     for (uint32_t i = tid; i < (uint32_t)H::CS / 4; i += WG) ((uint4 *)hist)[i] = make_uint4(0, 0, 0, 0);
-    const bool has_ins = finish && T.nev > 0;
-    if (has_ins) {
-        L.klen[tid] = 0;
-        L.kem2[0][tid] = 0;
-        L.kem2[1][tid] = 0;
-        if (tid < TILE_WORDS) L.bits[tid] = 0;
-        for (uint32_t i = tid; i < T.ccap * NSYM && i < ICOL * NSYM; i += WG) cols[i] = 0;
+    for (uint32_t i = tid; i <= NPOS; i += WG) {
+        dV[i] = 0;
+        dD[i] = 0;
     }
-    if (finish && tid < (uint32_t)min(d.fill_len, FILL_LDS)) L.fill[tid] = d.fill[tid];
-    lds_sync();
-    InsLayout il = {0, 0};
-    TPROF_MARK(1);
-    if (has_ins) il = build_layout<PF, false>(d, T, tile, L.bits, L.wrank, L.klen, L.key, cols, L.colkey, L.scan);
-    TPROF_MARK(2);
+    for (uint32_t i = tid; i <= NS; i += WG) C.ps[i] = d.ps[S0 + i];
     if (counts_only && d.mode != MODE_ADD_KEEP && T.nev > 0 && chunk == 0) {   // no vote: leave the tile's tables zero for the next run
         for (uint32_t e = tid; e < T.bcap; e += WG) ((uint4 *)d.ibkt)[T.boff + e] = make_uint4(0, 0, 0, 0);
         if (tid == 0) d.ilong_n[tile] = 0;
     }
+    lds_sync();
+    TPROF_MARK(1);
 
-    uint32_t V[4][8], Dc[8];   // counters X, Y, Z, V; '-'
+    uint32_t X[8], Y[8], Z[8];
 #pragma unroll
-    for (int c = 0; c < 4; c++)
-#pragma unroll
-        for (int b = 0; b < 8; b++) V[c][b] = 0;
-#pragma unroll
-    for (int b = 0; b < 8; b++) Dc[b] = 0;
-    uint32_t nmax_rec = 0;
-    // one record (run r at word W) → masks; rare parts ('-' runs, N / '-' of SEQ) applied here
-    auto record = [&](const uint4 rv, const uint4 win, uint32_t xw0, uint32_t xw1, uint32_t &mx, uint32_t &my, uint32_t &mv) {
-        mx = my = mv = 0;
-        const Run r = run_of(rv);
-        const uint32_t kd = r.kind & 3u;
-        const RecGeom gm = rec_geom(r.gpos, r.len, W);
-        if (kd == S2C_RUN_DASH) {
-            ripple1(Dc, gm.valid);
-        } else if (kd == S2C_RUN_BASES && gm.valid) {
-            const uint64_t qs = r.q + gm.qs;
-            const uint32_t sh = (uint32_t)(qs & 31);
-            const uint32_t b0 = (funnel(win.z, win.x, sh) << gm.lo) & gm.valid;
-            const uint32_t b1 = (funnel(win.w, win.y, sh) << gm.lo) & gm.valid;
-            mv = gm.valid;
-            mx = b0;
-            my = b1;
-            if (r.kind & S2C_RUN_XBIT) {
-                const uint32_t xm = (funnel(xw1, xw0, sh) << gm.lo) & gm.valid;
-                const uint32_t en = xm & ~b0 & ~b1, sd = xm & b0 & ~b1;   // 'N', '-' of SEQ
-                mv &= ~xm;
-                mx &= ~xm;
-                my &= ~xm;
-                if (sd && !(r.kind & S2C_RUN_DROP)) ripple1(Dc, sd);
-                uint32_t e = en;
-                while (e) {
-                    const uint32_t bit = (uint32_t)__builtin_ctz(e);
-                    e &= e - 1;
-                    H::add1(hist, 4, 32 * w + bit, 1u);
-                }
-            }
-        }
-    };
-    if constexpr (PIPE) {
-    // ---- window records, GS at a time, software-pipelined: a group's run records become
-    //      geometry (covered mask; first bit, funnel shift and kind packed) and base-window
-    //      requests as they arrive, then the NEXT group's run records are requested, then this
-    //      group's masks go into the counters (carry-save, one record at a time) — each group
-    //      waits for one HBM round trip instead of two, in the registers of the old loop
-    auto load_runs = [&](uint4 (&Rv)[GS], uint32_t gi) {
-#pragma unroll
-        for (int u = 0; u < GS; u++) {
-            uint32_t vo = gi * GS + u < nrec ? voff : OOR;
-            asm volatile("" : "+v"(vo));
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rrun, vo + (uint32_t)(u * 16 * G), gi * GS * 16 * G, 0);
-            Rv[u] = make_uint4(v[0], v[1], v[2], v[3]);
-        }
-    };
-    uint4 R[GS];
-    if (ngrp) load_runs(R, 0);
-    for (uint32_t gi = 0; gi < ngrp; gi++) {
-        uint32_t gv[GS], gp[GS];   // covered bits; lo | sh << 8 | kind << 16 (kind 0: nothing)
-        uint2 Wa[GS], Wb[GS];
-        uint32_t X0[GS], X1[GS];
-#pragma unroll
-        for (int u = 0; u < GS; u++) {
-            const Run r = run_of(R[u]);
-            const uint32_t kind = (r.kind & S2C_RUN_LONG) ? 0u : r.kind;   // (long: reached through the long list)
-            const RecGeom gm = rec_geom(r.gpos, r.len, W);
-            const uint64_t qs = r.q + gm.qs;
-            const bool bases = (kind & 3u) == S2C_RUN_BASES && gm.valid;
-            const uint32_t wo = bases ? (uint32_t)(qs >> 5) * 8u : OOR;
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rbq, wo, 0, 0);
-            Wa[u] = make_uint2(v[0], v[1]);
-            Wb[u] = make_uint2(v[2], v[3]);
-            const uint32_t xo = (bases && (kind & S2C_RUN_XBIT)) ? (uint32_t)(qs >> 5) * 4u : OOR;
-            const auto xv = __builtin_amdgcn_raw_buffer_load_b64(rbx, xo, 0, 0);
-            X0[u] = xv[0];
-            X1[u] = xv[1];
-            gv[u] = ((kind & 3u) == S2C_RUN_BASES || (kind & 3u) == S2C_RUN_DASH) ? gm.valid : 0u;
-            gp[u] = gm.lo | ((uint32_t)(qs & 31) << 8) | ((kind & 0xFFu) << 16);
-        }
-        uint4 Rn[GS];
-        if (gi + 1 < ngrp) load_runs(Rn, gi + 1);
-        uint32_t pend[4], t2a[4], t4a[4], t8[4];
-#pragma unroll
-        for (int u = 0; u < GS; u++) {
-            const uint32_t valid = gv[u], lo = gp[u] & 0xFFu, sh = (gp[u] >> 8) & 31u, kind = gp[u] >> 16;
-            uint32_t mx = 0, my = 0, mv = 0;
-            if ((kind & 3u) == S2C_RUN_DASH) {
-                ripple1(Dc, valid);
-            } else if ((kind & 3u) == S2C_RUN_BASES && valid) {
-                mx = (funnel(Wb[u].x, Wa[u].x, sh) << lo) & valid;
-                my = (funnel(Wb[u].y, Wa[u].y, sh) << lo) & valid;
-                mv = valid;
-                if (kind & S2C_RUN_XBIT) {
-                    const uint32_t xm = (funnel(X1[u], X0[u], sh) << lo) & valid;
-                    const uint32_t en = xm & ~mx & ~my, sd = xm & mx & ~my;   // 'N', '-' of SEQ
-                    mv &= ~xm;
-                    mx &= ~xm;
-                    my &= ~xm;
-                    if (sd && !(kind & S2C_RUN_DROP)) ripple1(Dc, sd);
-                    uint32_t e = en;
-                    while (e) {
-                        const uint32_t bit = (uint32_t)__builtin_ctz(e);
-                        e &= e - 1;
-                        H::add1(hist, 4, 32 * w + bit, 1u);
-                    }
-                }
-            }
-            const uint32_t mk[4] = {mx, my, mx & my, mv};
-#pragma unroll
-            for (int c = 0; c < 4; c++) {   // tree8 of the old loop, one record at a time
-                if ((u & 1) == 0) {
-                    pend[c] = mk[c];
-                    continue;
-                }
-                uint32_t t2;
-                csa(t2, V[c][0], V[c][0], pend[c], mk[c]);
-                if ((u & 3) == 1) {
-                    t2a[c] = t2;
-                    continue;
-                }
-                uint32_t t4;
-                csa(t4, V[c][1], V[c][1], t2a[c], t2);
-                if ((u & 7) == 3) {
-                    t4a[c] = t4;
-                    continue;
-                }
-                csa(t8[c], V[c][2], V[c][2], t4a[c], t4);
-            }
-        }
-#pragma unroll
-        for (int c = 0; c < 4; c++) close8(V[c], t8[c]);
-#pragma unroll
-        for (int u = 0; u < GS; u++) R[u] = Rn[u];
-    }
-    } else {
-    // ---- window records, GS at a time: run records, then their base windows
-    for (uint32_t gi = 0; gi < ngrp; gi++) {
-        uint4 R[GS];
-#pragma unroll
-        for (int u = 0; u < GS; u++) {
-            uint32_t vo = gi * GS + u < nrec ? voff : OOR;
-            asm volatile("" : "+v"(vo));
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rrun, vo + (uint32_t)(u * 16 * G), gi * GS * 16 * G, 0);
-            R[u] = make_uint4(v[0], v[1], v[2], v[3]);
-        }
-        uint4 Wn[GS];
-        uint32_t X0[GS], X1[GS];
-#pragma unroll
-        for (int u = 0; u < GS; u++) {
-            const Run r = run_of(R[u]);
-            const bool skip = (r.kind & 3u) != S2C_RUN_BASES || (r.kind & S2C_RUN_LONG);
-            const RecGeom gm = rec_geom(r.gpos, r.len, W);
-            const uint64_t qs = r.q + gm.qs;
-            const uint32_t wo = (!skip && gm.valid) ? (uint32_t)(qs >> 5) * 8u : OOR;
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rbq, wo, 0, 0);
-            Wn[u] = make_uint4(v[0], v[1], v[2], v[3]);
-            const uint32_t xo = (wo != OOR && (r.kind & S2C_RUN_XBIT)) ? (uint32_t)(qs >> 5) * 4u : OOR;
-            const auto xv = __builtin_amdgcn_raw_buffer_load_b64(rbx, xo, 0, 0);
-            X0[u] = xv[0];
-            X1[u] = xv[1];
-            if (r.kind & S2C_RUN_LONG) R[u].y = 0;   // reached through the long list instead
-        }
-        uint32_t mx[GS], my[GS], mz[GS], mv[GS];
-#pragma unroll
-        for (int u = 0; u < GS; u++) {
-            record(R[u], Wn[u], X0[u], X1[u], mx[u], my[u], mv[u]);
-            mz[u] = mx[u] & my[u];
-        }
-        const uint32_t t0 = tree8(V[0], mx), t1 = tree8(V[1], my), t2 = tree8(V[2], mz), t3 = tree8(V[3], mv);
-        close8(V[0], t0);
-        close8(V[1], t1);
-        close8(V[2], t2);
-        close8(V[3], t3);
-    }
-    }
-    TPROF_MARK(3);
-    nmax_rec = nrec;
-    // ---- long-piece records (rare): one at a time
-    {
-        const uint32_t jl0 = max(j0, nwin);
-        for (uint32_t j = jl0 + g; j < j1; j += G) {
-            const uint32_t slot = d.lp[T.lp0 + (j - nwin)];
-            const uint4 rv = ((const uint4 *)d.runs)[slot];
-            const Run r = run_of(rv);
-            const RecGeom gm = rec_geom(r.gpos, r.len, W);
-            uint4 win = make_uint4(0, 0, 0, 0);
-            uint32_t x0 = 0, x1 = 0;
-            if ((r.kind & 3u) == S2C_RUN_BASES && gm.valid) {
-                const uint64_t qw = (r.q + gm.qs) >> 5;
-                win = make_uint4(d.bq[2 * qw], d.bq[2 * qw + 1], d.bq[2 * qw + 2], d.bq[2 * qw + 3]);
-                if (r.kind & S2C_RUN_XBIT) { x0 = d.bx[qw]; x1 = d.bx[qw + 1]; }
-            }
-            uint32_t mx, my, mv;
-            record(rv, win, x0, x1, mx, my, mv);
-            ripple1(V[0], mx);
-            ripple1(V[1], my);
-            ripple1(V[2], mx & my);
-            ripple1(V[3], mv);
-            nmax_rec++;
-        }
-    }
-    TPROF_MARK(4);
-    // ---- flush: counters → symbol counts → LDS histogram
-    {
-        transpose8(V[0]);
-        transpose8(V[1]);
-        transpose8(V[2]);
-        transpose8(V[3]);
-        transpose8(Dc);
-        // A = V − X − Y + Z, C = X − Z, G = Y − Z, T = Z (bytes: every difference is a count)
-#pragma unroll
-        for (int r = 0; r < 8; r++) {
-            const uint32_t x = V[0][r], y = V[1][r], z = V[2][r], v = V[3][r];
-            V[3][r] = v - x - y + z;   // A
-            V[0][r] = x - z;           // C
-            V[1][r] = y - z;           // G
-        }
-        // the G lanes of a word sit side by side: pairs, then quads, pre-reduced with DPP row
-        // shifts while a byte cannot carry (≤ 255), so that one lane in `red` adds into LDS
+    for (int b = 0; b < 8; b++) X[b] = Y[b] = Z[b] = 0;
+    uint32_t acc = 0;   // records counted per lane since the last flush (wave-uniform bound)
+    // flush: counters → bytes (R[r] byte j = count of position 8j + r) → u16 pairs of the
+    // histogram; the G lanes of a word pre-reduced by DPP row shifts while a byte cannot carry
+    auto flush = [&]() {
+        transpose8(X);
+        transpose8(Y);
+        transpose8(Z);
         uint32_t red = 1;
         auto shr1 = [](uint32_t &v) { v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true); };
         auto shr2 = [](uint32_t &v) { v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true); };
-        const uint32_t nmax = uni(__ockl_wfred_max_u32(nmax_rec));
-        if (nmax < 128) {
+        if (acc < 128) {
             red = 2;
 #pragma unroll
-            for (int r = 0; r < 8; r++) { shr1(V[0][r]); shr1(V[1][r]); shr1(V[2][r]); shr1(V[3][r]); shr1(Dc[r]); }
-            if (nmax < 64) {
+            for (int r = 0; r < 8; r++) { shr1(X[r]); shr1(Y[r]); shr1(Z[r]); }
+            if (acc < 64) {
                 red = 4;
 #pragma unroll
-                for (int r = 0; r < 8; r++) { shr2(V[0][r]); shr2(V[1][r]); shr2(V[2][r]); shr2(V[3][r]); shr2(Dc[r]); }
+                for (int r = 0; r < 8; r++) { shr2(X[r]); shr2(Y[r]); shr2(Z[r]); }
             }
         }
         if (active && (g % red) == red - 1) {
@@ -963,19 +908,379 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(PIPE ? 2 : 3
                     if (hi) atomicAdd(hw + 8 + r, hi);
                 }
             };
-            add(1, V[3]);
-            add(2, V[0]);
-            add(3, V[1]);
-            add(5, V[2]);
-            add(0, Dc);
+            add(SL_X, X);
+            add(SL_Y, Y);
+            add(SL_Z, Z);
+        }
+#pragma unroll
+        for (int b = 0; b < 8; b++) X[b] = Y[b] = Z[b] = 0;
+        acc = 0;
+    };
+
+    // this lane's word reads the records of segments [sa, sb] (start words W - K .. W)
+    const uint32_t sa = active ? (W >= S0 + K ? W - K : S0) - S0 : 1u, sb = active ? W - S0 : 0u;
+    const uint2 *bql = (const uint2 *)(C.pl + 1);
+    const int32_t W32 = (int32_t)(32 * W);
+    // one group's records → carry-save trees of X, Y, Z; NR = 8: weight-8 carries in t8o,
+    // NR = 4 (a tail group): weight-4 carries
+    auto count_group = [&](const uint2 (&rv)[GS], uint32_t (&t8o)[3], auto nr) {
+        constexpr int NR = decltype(nr)::value;
+        uint32_t pend[3], t2a[3], t4a[3];
+#pragma unroll
+        for (int h = 0; h < NR; h += 2) {
+            uint32_t bm[GS], fx[GS], sh[GS];
+            uint2 pa[GS], pb[GS];
+#pragma unroll
+            for (int u = h; u < h + 2; u++) {
+                const int32_t s0 = (int32_t)rv[u].x - W32;
+                const int32_t e0 = s0 + (int32_t)(rv[u].y & 0x7FFu);
+                const uint32_t lo = (uint32_t)min(max(s0, 0), 32);
+                const uint32_t nb = (uint32_t)min(max(e0, 0), 32) - lo;
+                uint32_t m;
+                asm("v_bfm_b32 %0, %1, %2" : "=v"(m) : "v"(nb), "v"(lo));   // nb bits at lo (nb < 32)
+                bm[u] = m;
+                fx[u] = (uint32_t)__builtin_amdgcn_sbfe((int32_t)nb, 5, 1);   // all ones iff nb = 32
+                const int32_t b = (int32_t)(rv[u].y >> 11) - s0;
+                sh[u] = (uint32_t)b;
+                const uint2 *pw = bql + (b >> 5);
+                pa[u] = pw[0];
+                pb[u] = pw[1];
+            }
+#pragma unroll
+            for (int u = h; u < h + 2; u++) {
+                uint32_t x, y;   // plane & (bm | fx)
+                asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe0" : "=v"(x) : "v"(funnel(pb[u].x, pa[u].x, sh[u])), "v"(bm[u]), "v"(fx[u]));
+                asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe0" : "=v"(y) : "v"(funnel(pb[u].y, pa[u].y, sh[u])), "v"(bm[u]), "v"(fx[u]));
+                auto chain = [&](uint32_t (&Cc)[8], int c, uint32_t mk) {
+                    if ((u & 1) == 0) {
+                        pend[c] = mk;
+                        return;
+                    }
+                    uint32_t t2;
+                    csa(t2, Cc[0], Cc[0], pend[c], mk);
+                    if ((u & 3) == 1) {
+                        t2a[c] = t2;
+                        return;
+                    }
+                    uint32_t t4;
+                    csa(t4, Cc[1], Cc[1], t2a[c], t2);
+                    if ((u & 7) == 3) {
+                        t4a[c] = t4;
+                        if constexpr (NR == 4) t8o[c] = t4;
+                        return;
+                    }
+                    csa(t8o[c], Cc[2], Cc[2], t4a[c], t4);
+                };
+                chain(X, 0, x);
+                chain(Y, 1, y);
+                chain(Z, 2, x & y);
+            }
+        }
+    };
+    using Full = std::integral_constant<int, 8>;
+    using Half = std::integral_constant<int, 4>;
+
+    // ---- layer tables: segment σ's layer-ly pieces [lo, hi) by arithmetic on the window's
+    //      piece CSR; their prefix (a block scan) into segP[ly & 1]; thread t's piece
+    auto seg_range = [&](uint32_t sg, uint32_t ly, uint32_t &lo, uint32_t &hi) {
+        const uint32_t p0 = C.ps[sg], cnt = C.ps[sg + 1] - p0;
+        lo = p0 + (uint32_t)(((uint64_t)cnt * ly) / nl);
+        hi = p0 + (uint32_t)(((uint64_t)cnt * (ly + 1)) / nl);
+    };
+    auto layer_table = [&](uint32_t ly) -> uint32_t {   // (ends with the scan's barrier, not after the writes)
+        uint32_t np = 0;
+        if (tid < NS) {
+            uint32_t lo, hi;
+            seg_range(tid, ly, lo, hi);
+            np = hi - lo;
+        }
+        uint32_t ex, ey, tot, toty;
+        scan256x2(np, 0u, C.wsumB, ex, ey, tot, toty);
+        if (tid < NS) C.segP[ly & 1][tid] = ex;
+        if (tid == 0) C.segP[ly & 1][NS] = tot;
+        return uni(tot);
+    };
+    auto piece_of = [&](uint32_t t, uint32_t ly) -> uint32_t {   // largest σ with segP[σ] ≤ t
+        const uint32_t *sp = C.segP[ly & 1];
+        uint32_t lo2 = 0, hi2 = NS;
+        while (hi2 - lo2 > 1) {
+            const uint32_t m = (lo2 + hi2) >> 1;
+            if (sp[m] <= t) lo2 = m; else hi2 = m;
+        }
+        uint32_t lo, hi;
+        seg_range(lo2, ly, lo, hi);
+        return lo + (t - sp[lo2]);
+    };
+    const uint4 *const pc4 = (const uint4 *)d.pc;
+    const uint4 *const bq4 = (const uint4 *)d.bq;
+    const uint4 *const bx4 = (const uint4 *)d.bx;
+    const uint4 *const op4 = (const uint4 *)d.ops;
+    const uint32_t *const xl = (const uint32_t *)C.xl;
+    const uint32_t *const opl = (const uint32_t *)C.ol;
+    constexpr uint32_t PBF = 5, XBF = 3;   // blocks staged through registers at once (more: a serial tail)
+    uint4 P = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t oe = 0, npc = 0;
+    if (l0 < l1) {
+        npc = layer_table(l0);
+        lds_sync();
+        if (tid < npc) {
+            const uint32_t k = piece_of(tid, l0);
+            P = pc4[k];
+            oe = d.pc[4 * (size_t)k + 6];
+        }
+    }
+    for (uint32_t ly = l0; ly < l1; ly++) {
+        // ---- 1. this thread's piece: its blocks of planes / non-ACGT words / op words and
+        //      its run records; block scans → its LDS offsets
+        const bool valid = tid < npc;
+        const uint32_t fl = P.w >> 24, len = P.w & 0xFFFFFFu;
+        const bool simple = (fl & S2C_PF_SIMPLE) != 0, lng = (fl & S2C_PF_LONG) != 0;
+        const uint32_t gw0 = P.y >> 1;                                 // plane word of SEQ[0]
+        const uint32_t nw = ((16u * (P.y & 1u) + len + 31u) >> 5) + 1u;   // through the word after the last base
+        const uint32_t pb0 = gw0 >> 1, xb0 = gw0 >> 2, ob0 = P.z >> 2;
+        const uint32_t pb = (valid && !lng) ? ((gw0 + nw + 1u) >> 1) - pb0 : 0u;
+        const uint32_t xb = (valid && !lng && (fl & S2C_PF_X)) ? ((gw0 + nw + 3u) >> 2) - xb0 : 0u;
+        const uint32_t ob = (valid && !lng && !simple) ? ((oe + 3u) >> 2) - ob0 : 0u;
+        const uint32_t nr = valid ? oe - P.z : 0u;
+        uint32_t exA, exB, totA, totB;
+        scan256x2(pb | xb << 16, ob | nr << 16, C.wsumA, exA, exB, totA, totB);
+        TPROF_MARK(2);
+        const uint32_t pbPre = exA & 0xFFFFu, xbPre = exA >> 16, obPre = exB & 0xFFFFu, rPre = exB >> 16;
+        const uint32_t NR = uni(totB >> 16);
+        if (valid) C.recPre[tid] = rPre;
+        if (tid == 0) C.recPre[npc] = NR;
+        // the blocks: loads now, LDS writes after the next layer's table is built
+        uint4 pv[PBF], xv[XBF];
+#pragma unroll
+        for (uint32_t m = 0; m < PBF; m++) pv[m] = m < pb ? bq4[pb0 + m] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (uint32_t m = 0; m < XBF; m++) xv[m] = m < xb ? bx4[xb0 + m] : make_uint4(0u, 0u, 0u, 0u);
+        // ---- 2. the next layer's table and piece records (in flight through this layer's walk
+        //      and count)
+        uint4 Pn = make_uint4(0u, 0u, 0u, 0u);
+        uint32_t oen = 0, npcn = 0;
+        if (ly + 1 < l1) {
+            npcn = layer_table(ly + 1);
+            lds_sync();
+            if (tid < npcn) {
+                const uint32_t k = piece_of(tid, ly + 1);
+                Pn = pc4[k];
+                oen = d.pc[4 * (size_t)k + 6];
+            }
+        } else {
+            lds_sync();
+        }
+        TPROF_MARK(3);
+#pragma unroll
+        for (uint32_t m = 0; m < PBF; m++)
+            if (m < pb) C.pl[1 + pbPre + m] = pv[m];
+#pragma unroll
+        for (uint32_t m = 0; m < XBF; m++)
+            if (m < xb) C.xl[xbPre + m] = xv[m];
+        for (uint32_t m = PBF; m < pb; m++) C.pl[1 + pbPre + m] = bq4[pb0 + m];   // (long SEQ: serial)
+        for (uint32_t m = XBF; m < xb; m++) C.xl[xbPre + m] = bx4[xb0 + m];
+        for (uint32_t m = 0; m < ob; m++) C.ol[obPre + m] = op4[ob0 + m];
+        if (tid <= NS) C.segR[tid] = C.recPre[C.segP[ly & 1][tid]];
+        for (uint32_t i = tid; i < RPAD; i += WG) C.runl[NR + i] = make_uint2(0u, 0u);
+        lds_sync();
+        TPROF_MARK(4);
+        // ---- 3. walk this thread's piece (from registers and LDS)
+        if (valid) {
+            // LDS plane base of SEQ[0]; non-ACGT word of LDS plane word v: xl[v + xd]; op word j:
+            // opl[j + od]; its records runl[j + rd]
+            const uint32_t ql = 64u * pbPre + 32u * (gw0 & 1u) + 16u * (P.y & 1u);
+            const uint32_t xd = 4u * xbPre - 4u * xb0 - (2u * pbPre - 2u * pb0);
+            if (simple) {   // one run of SEQ[0:take] (:64-69)
+                const uint32_t c0 = max(P.x, a), c1 = min(P.x + len, a + n);
+                C.runl[rPre] = len ? make_uint2(P.x, (ql << 11) | len) : make_uint2(0u, 0u);
+                if (c1 > c0) {
+                    atomicAdd(&dV[c0 - a], 1);
+                    atomicSub(&dV[c1 - a], 1);
+                    if (fl & S2C_PF_X) x_fix<NWP>(bql, xl, xd, ql + (c0 - P.x), c1 - c0, c0 - a, false, hist);
+                }
+            } else if (lng) {   // (its runs come through the tile long lists)
+                for (uint32_t j = 0; j < nr; j++) C.runl[rPre + j] = make_uint2(0u, 0u);
+            } else {
+                walk_chunk_piece<NWP>(P, oe, opl, 4u * obPre - 4u * ob0, C.runl, rPre - P.z, bql, xl, xd, ql - 16u * P.y,
+                                      d.maxdel_active != 0, (uint32_t)d.maxdel, a, n, hist, dV, dD);
+            }
+        }
+        lds_sync();
+        TPROF_MARK(5);
+        // ---- 4. count this lane's records cw0 + g + G·m < cw1 (reads past them: records of
+        //      pieces starting after W, or the zero pad — they cover nothing of W)
+        const uint32_t cw0 = C.segR[sa], cw1 = C.segR[sb + 1];
+        const uint32_t nrec = cw0 + g < cw1 ? (cw1 - cw0 - g + G - 1) / G : 0u;
+        const uint32_t nmx = uni(__ockl_wfred_max_u32(nrec));
+        const uint32_t ngrp = nmx / GS + ((nmx % GS) > 4u ? 1u : 0u);
+        const bool half = (nmx % GS) != 0u && (nmx % GS) <= 4u;
+        const uint32_t add_recs = GS * ngrp + (half ? 4u : 0u);
+        if (acc + add_recs > 255u) flush();
+        acc += add_recs;
+        const uint32_t rend = NR;
+        auto load_runs = [&](uint2 (&rv)[GS], uint32_t gi) {
+            const uint2 *rb = C.runl + min(cw0 + g + G * GS * gi, rend);
+#pragma unroll
+            for (int u = 0; u < GS; u++) rv[u] = rb[G * u];
+        };
+        uint2 ra[GS], rb2[GS];
+        if (ngrp) load_runs(ra, 0);
+        for (uint32_t gi = 0; gi < ngrp; gi += 2) {
+            uint32_t t8a[3], t8b[3];
+            if (gi + 1 < ngrp) load_runs(rb2, gi + 1);
+            count_group(ra, t8a, Full{});
+            if (gi + 1 >= ngrp) {
+                close8(X, t8a[0]);
+                close8(Y, t8a[1]);
+                close8(Z, t8a[2]);
+                break;
+            }
+            if (gi + 2 < ngrp) load_runs(ra, gi + 2);
+            count_group(rb2, t8b, Full{});
+            close16(X, t8a[0], t8b[0]);
+            close16(Y, t8a[1], t8b[1]);
+            close16(Z, t8a[2], t8b[2]);
+        }
+        if (half) {   // records 8·ngrp .. 8·ngrp + 3 of each lane
+            uint32_t t4[3];
+            load_runs(ra, ngrp);
+            count_group(ra, t4, Half{});
+            close4(X, t4[0]);
+            close4(Y, t4[1]);
+            close4(Z, t4[2]);
+        }
+        lds_sync();   // the chunk's LDS is rewritten by the next layer
+        TPROF_MARK(6);
+        P = Pn;
+        oe = oen;
+        npc = npcn;
+    }
+
+    // ---- long-piece records (rare; k_reads' run records through the tile's long list,
+    //      counted once per tile: by its first item), one per lane and round
+    {
+        const uint32_t nlong = l0 == 0 ? T.lp1 - T.lp0 : 0u;
+        const uint32_t ntr = uni(__ockl_wfred_max_u32(active && g < nlong ? (nlong - g + G - 1) / G : 0u));
+        for (uint32_t m = 0; m < ntr; m++) {
+            if (acc >= 255u) flush();
+            acc++;
+            const uint32_t j = g + G * m;
+            if (!(active && j < nlong)) continue;
+            const uint32_t slot = d.lp[T.lp0 + j];
+            const Run r = run_of(((const uint4 *)d.runs)[slot]);
+            const RecGeom gm = rec_geom(r.gpos, r.len, W);
+            if (!gm.valid) continue;
+            const uint32_t p0 = 32 * w + gm.lo, p1 = p0 + (uint32_t)__popc(gm.valid);
+            if ((r.kind & 3u) == S2C_RUN_DASH) {
+                atomicAdd(&dD[p0], 1);
+                atomicSub(&dD[p1], 1);
+            } else if ((r.kind & 3u) == S2C_RUN_BASES) {
+                const uint64_t qs = r.q + gm.qs, qw = qs >> 5;
+                const uint32_t sh = (uint32_t)(qs & 31);
+                const uint32_t mx = (funnel(d.bq[2 * qw + 2], d.bq[2 * qw], sh) << gm.lo) & gm.valid;
+                const uint32_t my = (funnel(d.bq[2 * qw + 3], d.bq[2 * qw + 1], sh) << gm.lo) & gm.valid;
+                ripple1(X, mx);
+                ripple1(Y, my);
+                ripple1(Z, mx & my);
+                atomicAdd(&dV[p0], 1);
+                atomicSub(&dV[p1], 1);
+                if (r.kind & S2C_RUN_XBIT) {
+                    uint32_t xm = (funnel(d.bx[qw + 1], d.bx[qw], sh) << gm.lo) & gm.valid;
+                    while (xm) {
+                        const uint32_t bit = (uint32_t)__builtin_ctz(xm);
+                        xm &= xm - 1;
+                        if ((mx >> bit) & 1u) {   // '-' of SEQ (p0 = 1)
+                            H::add1(hist, SL_SD, 32 * w + bit, 1u);
+                            if (!(r.kind & S2C_RUN_DROP)) H::add1(hist, SL_SDC, 32 * w + bit, 1u);
+                        } else {
+                            H::add1(hist, SL_N, 32 * w + bit, 1u);
+                        }
+                    }
+                }
+            }
+        }
+    }
+    if (acc) flush();
+    lds_sync();
+    TPROF_MARK(7);
+    // ---- difference arrays → coverage and '-' per position (inclusive scans, thread blocks
+    //      of NPOS / WG positions)
+    {
+        constexpr uint32_t PER = NPOS / WG;   // NWP / 8
+        const uint32_t p0 = tid * PER;
+        int32_t sv = 0, sd = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++) {
+            sv += dV[p0 + i];
+            sd += dD[p0 + i];
+        }
+        uint32_t tv, td;
+        const uint32_t iv = __ockl_wfscan_add_u32((uint32_t)sv, true), idd = __ockl_wfscan_add_u32((uint32_t)sd, true);
+        if (lane == 63) {
+            wtot[0][wv] = iv;
+            wtot[1][wv] = idd;
+        }
+        lds_sync();
+        uint32_t ov = 0, od = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < WG / 64; k++) {
+            ov += k < wv ? wtot[0][k] : 0u;
+            od += k < wv ? wtot[1][k] : 0u;
+        }
+        tv = ov + iv - (uint32_t)sv;
+        td = od + idd - (uint32_t)sd;
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++) {
+            tv += (uint32_t)dV[p0 + i];
+            td += (uint32_t)dD[p0 + i];
+            dV[p0 + i] = (int32_t)tv;
+            dD[p0 + i] = (int32_t)td;
         }
     }
     lds_sync();
-    TPROF_MARK(5);
+    // ---- raw slots → "-ACGNT" counts in place (u16 pairs: positions 32·v + i, + 16)
+    for (uint32_t s = tid; s < 16u * NWP; s += WG) {
+        const uint32_t hs = hslot(s);
+        uint32_t raw[NSYM];
+#pragma unroll
+        for (uint32_t c = 0; c < NSYM; c++) raw[c] = hist[c * HP + hs];
+        const uint32_t q0 = 32 * (s >> 4) + (s & 15);
+        uint32_t outw[NSYM] = {};
+#pragma unroll
+        for (int hh = 0; hh < 2; hh++) {
+            const uint32_t sh = 16 * hh, q = q0 + 16 * hh;
+            auto f = [&](uint32_t c) { return (raw[c] >> sh) & 0xFFFFu; };
+            const uint32_t x = f(SL_X), y = f(SL_Y), z = f(SL_Z), nn = f(SL_N), sd = f(SL_SD), sdc = f(SL_SDC);
+            const uint32_t v = (uint32_t)dV[q], dd = (uint32_t)dD[q];
+            const uint32_t cnt[NSYM] = {dd + sdc, v - x - y + z - nn, x - z - sd, y - z, nn, z};
+#pragma unroll
+            for (uint32_t c = 0; c < NSYM; c++) outw[c] |= (cnt[c] & 0xFFFFu) << sh;
+        }
+#pragma unroll
+        for (uint32_t c = 0; c < NSYM; c++) hist[c * HP + hs] = outw[c];
+    }
+    lds_sync();
+    TPROF_MARK(8);
     if (finish) {
+        // the epilogue's LDS (aliases the chunk): layout arrays zeroed, tables, fill
+        FastLds<ICOL> &L = U.e.L;
+        uint32_t *cols = U.e.cols;
+        if (tid < 64) L.amb[tid] = c_amb[tid];
+        const bool has_ins = T.nev > 0;
+        if (has_ins) {
+            L.klen[tid] = 0;
+            L.kem2[0][tid] = 0;
+            L.kem2[1][tid] = 0;
+            if (tid < TILE_WORDS) L.bits[tid] = 0;
+            for (uint32_t i = tid; i < T.ccap * NSYM && i < ICOL * NSYM; i += WG) cols[i] = 0;
+        }
+        if (tid < (uint32_t)min(d.fill_len, FILL_LDS)) L.fill[tid] = d.fill[tid];
+        lds_sync();
+        InsLayout il = {0, 0};
+        if (has_ins) il = build_layout<PF, false>(d, T, tile, L.bits, L.wrank, L.klen, L.key, cols, L.colkey, L.scan);
         tile_epilogue_fast<NWP>(d, tile, T, il, hist, cols, L);
     } else {
-        // deep tile: this chunk's counts → HBM (symbol-major, coalesced atomics); a general
+        // deep tile: this item's counts → HBM (symbol-major, coalesced atomics); a general
         // tile's (and in counts-only mode every tile's) counts: plain stores; streamed
         // batches of unsorted input add every tile's counts to the running totals
         for (uint32_t q = tid; q < n; q += WG)
@@ -990,11 +1295,11 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(PIPE ? 2 : 3
                 }
             }
     }
-    TPROF_MARK(6);
+    TPROF_MARK(9);
 #ifdef S2C_PROF
     if (threadIdx.x == 0 && (blockIdx.x & 15) == 0) {
         atomicAdd(&g_tprof[15], 1ull);
-        atomicAdd(&g_tprof[14], (unsigned long long)ngrp);
+        atomicAdd(&g_tprof[14], (unsigned long long)(l1 - l0));
     }
 #endif
 }
@@ -1196,6 +1501,10 @@ inline int hip_check(hipError_t e, const char *what) {
 TileArgs tile_args(const s2c_dev &d) {
     TileArgs p;
     p.rs = d.rs; p.runs = d.runs; p.bq = d.bq; p.bx = d.bx; p.tiles = d.tiles; p.lp = d.lp;
+    p.pc = d.pc; p.ops = d.ops; p.ps = d.ps; p.bq_end = d.bq + 2 * d.n_qwords; p.bx_end = d.bx + d.n_qwords;
+    p.ops_end = d.ops + std::max<int64_t>(d.n_ops, 1); p.pc_end = d.pc + 4 * (d.n_pieces + 1);
+    p.maxdel_active = d.maxdel_active ? 1u : 0u;
+    p.maxdel = d.maxdel < 0 ? 0u : (uint32_t)d.maxdel;
     p.ibkt = d.ibkt; p.ilong = d.ilong; p.ilong_n = d.ilong_n;
     p.thresholds = d.thresholds; p.fill = d.fill; p.counts = d.counts; p.ins_cols = d.ins_cols; p.ins_chr = d.ins_chr;
     p.tile_stats = d.tile_stats; p.blk_len = d.blk_len; p.out = d.out;
@@ -1208,23 +1517,16 @@ TileArgs tile_args(const s2c_dev &d) {
 }
 
 template <int NWP>
-int launch_tile(const TileArgs &a, const uint32_t *items, int64_t n, hipStream_t s, bool pipe) {
+int launch_tile(const TileArgs &a, const uint32_t *items, int64_t n, hipStream_t s) {
     if (n <= 0) return S2C_OK;
-    if (pipe) k_tile<NWP, true><<<(unsigned)n, WG, 0, s>>>(a, items);
-    else k_tile<NWP, false><<<(unsigned)n, WG, 0, s>>>(a, items);
+    k_tile<NWP><<<(unsigned)n, WG, 0, s>>>(a, items);
     return hip_check(hipGetLastError(), "k_tile");
 }
-// pipe: the software-pipelined count loop, for deep batches (>= 5 run slots per position)
-int launch_tiles(const TileArgs &a, int32_t tile_max, const uint32_t *items, int64_t n, hipStream_t s, bool pipe) {
-    if (tile_max <= 256) return launch_tile<8>(a, items, n, s, pipe);
-    if (tile_max <= 512) return launch_tile<16>(a, items, n, s, pipe);
-    if (tile_max <= 1024) return launch_tile<32>(a, items, n, s, pipe);
-    return launch_tile<64>(a, items, n, s, pipe);
-}
-bool deep_batch(const s2c_dev *d) {
-    const char *e = getenv("S2C_TILE_PIPE");   // (A/B diagnostic: 0 / 1 forces)
-    if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
-    return d->n_ops >= 5 * d->padded_len;
+int launch_tiles(const TileArgs &a, int32_t tile_max, const uint32_t *items, int64_t n, hipStream_t s) {
+    if (tile_max <= 256) return launch_tile<8>(a, items, n, s);
+    if (tile_max <= 512) return launch_tile<16>(a, items, n, s);
+    if (tile_max <= 1024) return launch_tile<32>(a, items, n, s);
+    return launch_tile<64>(a, items, n, s);
 }
 
 }  // namespace
@@ -1268,11 +1570,11 @@ static int check_dev(const s2c_dev *d) {
         return s2c_set_error(S2C_ERR_ARG, "missing tile / output buffers");
     if ((d->n_items > 0 && !d->items) || (d->n_dense > 0 && !d->dense)) return s2c_set_error(S2C_ERR_ARG, "missing items");
     if (!d->ibkt || !d->ilong || !d->ilong_n) return s2c_set_error(S2C_ERR_ARG, "missing insertion tables");
-    {   // one flush per item: 8-bit counters hold ≤ FLUSH_RECS records per lane
+    if (d->n_tiles > 0 && !d->ps) return s2c_set_error(S2C_ERR_ARG, "missing piece CSR (ps)");
+    {   // k_tile's segments: a window of ≤ 64 words and kwin start words before it
         int64_t nwp = 8;
         while (nwp * 32 < d->tile_max) nwp *= 2;
-        if (d->chunk <= 0 || d->chunk > (int64_t)FLUSH_RECS * (WG / nwp))
-            return s2c_set_error(S2C_ERR_ARG, "chunk exceeds one flush per work item");
+        if (d->kwin < 0 || d->kwin + nwp > S2C_CHUNK_SEGS) return s2c_set_error(S2C_ERR_ARG, "kwin beyond k_tile's segments");
     }
     if (d->n_deep > 0 && (!d->deep || !d->counts || !d->ins_cols || !d->ins_chr))
         return s2c_set_error(S2C_ERR_ARG, "missing deep-tile buffers");
@@ -1287,9 +1589,9 @@ static int check_dev(const s2c_dev *d) {
 extern "C" int s2c_reads(const s2c_dev *d, void *stream) {
     int rc = check_dev(d);
     if (rc) return rc;
-    // dense tiles walk their own pieces, unless len(-f) != 1 routes them to k_tile (which
-    // reads run records): then every piece's runs are written
-    return s2c_launch_reads(d, (hipStream_t)stream, d->n_dense > 0 && d->fill_len != 1);
+    // the tile kernels walk their windows' pieces themselves: k_reads takes the insertion
+    // emitters and the long pieces (rlist)
+    return s2c_launch_reads(d, (hipStream_t)stream, false);
 }
 
 extern "C" int s2c_pileup(const s2c_dev *d, void *stream) {
@@ -1303,10 +1605,10 @@ extern "C" int s2c_pileup(const s2c_dev *d, void *stream) {
     }
     if (d->n_dense > 0) {
         // dense tiles emit exactly one char per position: len(fill) must be 1, else k_tile
-        rc = d->fill_len == 1 ? s2c_launch_dense(d, s) : launch_tiles(a, d->tile_max, d->dense, d->n_dense, s, deep_batch(d));
+        rc = d->fill_len == 1 ? s2c_launch_dense(d, s) : launch_tiles(a, d->tile_max, d->dense, d->n_dense, s);
         if (rc) return rc;
     }
-    return launch_tiles(a, d->tile_max, d->items, d->n_items, s, deep_batch(d));
+    return launch_tiles(a, d->tile_max, d->items, d->n_items, s);
 }
 
 extern "C" int s2c_consensus(const s2c_dev *d, void *stream) {
@@ -1331,15 +1633,15 @@ extern "C" int s2c_pileup_counts(const s2c_dev *d, void *stream) {
     if (rc) return rc;
     if (!d->counts) return s2c_set_error(S2C_ERR_ARG, "counts buffer required");
     hipStream_t s = (hipStream_t)stream;
-    if ((rc = s2c_launch_reads(d, s, true))) return rc;   // run records of every piece
+    if ((rc = s2c_launch_reads(d, s, true))) return rc;   // run records of every piece (compared by the tests)
     TileArgs a = tile_args(*d);
     a.mode = MODE_STORE;
     if (d->n_deep > 0) {
         k_prep<<<(unsigned)d->n_deep, WG, 0, s>>>(a, d->deep);
         if ((rc = hip_check(hipGetLastError(), "k_prep"))) return rc;
     }
-    if ((rc = launch_tiles(a, d->tile_max, d->dense, d->n_dense, s, deep_batch(d)))) return rc;
-    return launch_tiles(a, d->tile_max, d->items, d->n_items, s, deep_batch(d));
+    if ((rc = launch_tiles(a, d->tile_max, d->dense, d->n_dense, s))) return rc;
+    return launch_tiles(a, d->tile_max, d->items, d->n_items, s);
 }
 
 extern "C" int s2c_accumulate(const s2c_dev *d, int keep_tables, void *stream) {
@@ -1347,9 +1649,9 @@ extern "C" int s2c_accumulate(const s2c_dev *d, int keep_tables, void *stream) {
     if (rc) return rc;
     if (!d->counts) return s2c_set_error(S2C_ERR_ARG, "counts buffer required");
     hipStream_t s = (hipStream_t)stream;
-    if ((rc = s2c_launch_reads(d, s, true))) return rc;   // run records of every piece; events hashed
+    if ((rc = s2c_launch_reads(d, s, false))) return rc;   // events hashed, long pieces' runs
     TileArgs a = tile_args(*d);
     a.mode = keep_tables ? MODE_ADD_KEEP : MODE_ADD;
-    if ((rc = launch_tiles(a, d->tile_max, d->dense, d->n_dense, s, deep_batch(d)))) return rc;
-    return launch_tiles(a, d->tile_max, d->items, d->n_items, s, deep_batch(d));
+    if ((rc = launch_tiles(a, d->tile_max, d->dense, d->n_dense, s))) return rc;
+    return launch_tiles(a, d->tile_max, d->items, d->n_items, s);
 }

@@ -1,7 +1,7 @@
 """Device side: packed batch → HBM, workspace, the HIP stages, results → host.
 
 PyTorch is used only as the device allocator / stream provider; all compute is
-libs2c.so's hand-written HIP kernels (s2c_kernels.hip).  There is no CPU
+libs2c.so's hand-written HIP kernels (csrc/s2c_*.hip).  There is no CPU
 fallback: without a visible GPU ``DeviceBatch`` raises.
 """
 from __future__ import annotations
@@ -44,7 +44,7 @@ def _ptr(t):
 class DeviceBatch:
     """The packed batch resident in HBM (inputs of every launch)."""
 
-    ARRAYS = ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile", "rlist")
+    ARRAYS = ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile", "rlist", "ps")
 
     def __init__(self, hb, device=None):
         self.device = _dev(device)

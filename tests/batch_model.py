@@ -19,7 +19,7 @@ AMB = None
 OP_BASES = (0, 7, 8)        # M = X
 OP_DASH = (2, 3, 6)         # D N P
 OP_I, OP_S = 1, 4
-PF_X, PF_RANGE, PF_INS, PF_LONG = 1, 2, 4, 8
+PF_X, PF_RANGE, PF_INS, PF_LONG, PF_SIMPLE = 1, 2, 4, 8, 64
 RUN_BASES, RUN_DASH, RUN_XBIT, RUN_DROP, RUN_LONG = 1, 2, 4, 8, 16
 
 
@@ -170,16 +170,23 @@ def check_plan(hb):
         o, L = int(hb.ref_off[r]), int(hb.ref_len[r])
         assert (own[o:o + L] == 1).all(), "ref %d positions not tiled exactly once" % r
     items = {}
-    for t, c, _, _ in hb.items.astype(np.int64):
-        items.setdefault(int(t), []).append(int(c))
-    for t, c, _, _ in hb.dense.astype(np.int64):
-        assert int(t) not in items and c == 0
-        items[int(t)] = [0]
+    for t, c, l0, l1 in hb.items.astype(np.int64):
+        items.setdefault(int(t), []).append((int(c), int(l0), int(l1)))
+    for t, c, l0, l1 in hb.dense.astype(np.int64):
+        assert int(t) not in items and c == 0 and l0 == 0 and l1 == T[t, 19]
+        items[int(t)] = [(0, 0, int(l1))]
         assert T[t, 3] == 4
     assert sorted(items) == list(range(i.n_tiles))
     for t, cs in items.items():
-        assert sorted(cs) == list(range(len(cs)))
+        cs = sorted(cs)
+        assert [c for c, _, _ in cs] == list(range(len(cs)))
+        assert cs[0][1] == 0 and cs[-1][2] == T[t, 19] and all(cs[k][2] == cs[k + 1][1] for k in range(len(cs) - 1))
         assert bool(T[t, 3] & 1) == (len(cs) > 1)
+    # piece CSR by start word; the sentinel's qh ends the planes
+    if NP:
+        assert (hb.ps.astype(np.int64) == np.searchsorted(sw, np.arange(i.n_words + 1))).all()
+        assert pc[NP, 1] == pc[NP - 1, 1] + (((pc[NP - 1, 3] & 0xFFFFFF) + 15) // 16)
+    check_layers(hb)
     lp = hb.lp.astype(np.int64)
     for k in range(NP):
         g, fl = pc[k, 0], pc[k, 3] >> 24
@@ -204,14 +211,78 @@ def check_plan(hb):
         if row[3] == 4:
             ns, nq = row[16] - row[15], row[18] - row[17]
             assert 4 * ((ns + 65) & ~1) + 8 * (nq + 32) + 4 * ((nq + 65) & ~1) + 8 * ns <= S2C_DENSE_LDS and nq <= 4096
-    # k_reads' list: the pieces non-dense tiles read runs of, and the insertion emitters
-    need = np.zeros(NP, bool)
-    for row in T:
-        if row[3] != 4:
-            need[row[13]:row[14]] = True
+    # k_reads' list: the long pieces (their runs feed the tile long lists) and the insertion emitters
     fl = pc[:NP, 3] >> 24
-    assert (need <= ((fl & 16) != 0)).all()
+    assert (((fl & 16) != 0) <= ((fl & PF_LONG) != 0)).all()
     assert set(hb.rlist.tolist()) == set(np.nonzero(((fl & 16) != 0) | ((fl & PF_INS) != 0))[0].tolist())
+
+
+CHUNK_PIECES, CHUNK_PBLK, CHUNK_XBLK, CHUNK_OBLK, CHUNK_RECS = 256, 1280, 256, 128, 768   # include/s2c.h
+CHUNK_LANE_RECS, ITEM_RECS = 248, 60000
+
+
+def layer_ranges(hb, t, nl=None):
+    """k_tile's segments of tile t and, per layer l, [lo, hi) of each (s2c_tile.hip table)."""
+    i = hb.info
+    row = hb.tiles[t].astype(np.int64)
+    W0, W1 = row[0] >> 5, (row[1] + 31) >> 5
+    S0 = max(W0 - i.kwin, 0)
+    ps = hb.ps.astype(np.int64)
+    p0 = ps[S0:W1]
+    cnt = ps[S0 + 1:W1 + 1] - p0
+    nl = int(row[19]) if nl is None else nl
+    return S0, W0, W1, [(p0 + cnt * l // nl, p0 + cnt * (l + 1) // nl) for l in range(nl)]
+
+
+def piece_blocks(hb):
+    """Per piece the 16-byte blocks k_tile stages (s2c_tile.hip, thread per piece): base
+    planes through the word after its last base, non-ACGT words (PF_X), op words (not
+    PF_SIMPLE); none for long pieces."""
+    pc = hb.pc.astype(np.int64)
+    NP = hb.info.n_pieces
+    qh, oz, w3 = pc[:NP, 1], pc[:NP, 2], pc[:NP, 3]
+    oe = pc[1:NP + 1, 2]
+    fl, ln = w3 >> 24, w3 & 0xFFFFFF
+    gw0 = qh >> 1
+    nw = ((16 * (qh & 1) + ln + 31) >> 5) + 1
+    lng = (fl & PF_LONG) != 0
+    pb = np.where(lng, 0, ((gw0 + nw + 1) >> 1) - (gw0 >> 1))
+    xb = np.where(lng | ((fl & PF_X) == 0), 0, ((gw0 + nw + 3) >> 2) - (gw0 >> 2))
+    ob = np.where(lng | ((fl & PF_SIMPLE) != 0), 0, ((oe + 3) >> 2) - (oz >> 2))
+    return pb, xb, ob
+
+
+def check_layers(hb):
+    """Every layer of every tile fits k_tile's LDS chunk exactly as the kernel lays it out
+    (this batch's own 16-byte alignments); records per word and counting lane; every item's
+    records per word fit its u16 histogram."""
+    i = hb.info
+    pc = hb.pc.astype(np.int64)
+    nwp = 8
+    while nwp * 32 < i.tile_max:
+        nwp *= 2
+    G = 256 // nwp
+    K = i.kwin
+    pb, xb, ob = (np.concatenate([[0], np.cumsum(v)]) for v in piece_blocks(hb))
+    for t in range(i.n_tiles):
+        S0, W0, W1, lays = layer_ranges(hb, t)
+        assert W1 - S0 <= 128
+        for lo, hi in lays:
+            recs = pc[hi, 2] - pc[lo, 2]
+            assert (hi - lo).sum() <= CHUNK_PIECES and recs.sum() <= CHUNK_RECS
+            assert (pb[hi] - pb[lo]).sum() <= CHUNK_PBLK and (xb[hi] - xb[lo]).sum() <= CHUNK_XBLK
+            assert (ob[hi] - ob[lo]).sum() <= CHUNK_OBLK
+            for W in range(W0, W1):
+                a = max(W - K, S0) - S0
+                assert recs[a:W - S0 + 1].sum() <= CHUNK_LANE_RECS * G
+        items = [it for it in hb.items.astype(np.int64) if it[0] == t]
+        for _, _, l0, l1 in items:
+            lo0, _ = lays[l0]
+            _, hi1 = lays[l1 - 1]
+            rec = pc[hi1, 2] - pc[lo0, 2]
+            for W in range(W0, W1):
+                a = max(W - K, S0) - S0
+                assert rec[a:W - S0 + 1].sum() <= ITEM_RECS
 
 
 def check_plan_shard(sub):
@@ -227,6 +298,7 @@ def check_plan_shard(sub):
         assert (sub.wtile[row[0] >> 5:(row[1] + 31) >> 5] == t).all()
     n = len(hb_items(sub))
     assert n == i.n_tiles + int(sum(max(0, c) for c in []))
+    check_layers(sub)
 
 
 def hb_items(hb):
