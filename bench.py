@@ -15,10 +15,11 @@ HIP events recorded on the launch stream between the stages of every timed step,
 kernel's time is a sub-interval of the step it belongs to.
 
 N>1 (torch.distributed.run, one process per GPU):
-  default  weak scaling: each rank runs its own batch of the workload (seed + rank);
-  --shard  strong scaling: ONE workload (rank 0's seed) split into contiguous tile ranges
-           (sam2consensus_amd.shard.split_tiles), each rank runs its shard; rank 0 checks the
-           merged FASTA against the reference's golden.
+  default        strong scaling, the north_star position split: ONE workload split into
+                 contiguous tile ranges (sam2consensus_amd.shard.split_tiles), each rank runs
+                 its shard; the shards' FASTA bodies and statistics are gathered to rank 0
+                 (RCCL) and checked against the reference's golden;
+  --independent  weak scaling: each rank runs its own batch of the workload (seed + rank).
 Timing: barrier + synchronize on both sides of exactly K steps, MAX over ranks; value =
 aligned bases of all ranks / that time.  Rank 0 prints ONE JSON line.
 """
@@ -164,7 +165,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="c5", choices=sorted(WORKLOADS))
-    ap.add_argument("--shard", action="store_true", help="N>1: split ONE workload over the ranks (strong scaling)")
+    ap.add_argument("--independent", action="store_true",
+                    help="N>1: every rank its own batch (weak scaling) instead of one workload split by position")
+    ap.add_argument("--shard", action="store_true", help="(default for N>1; kept for old command lines)")
+    ap.add_argument("--no-file-parse", action="store_true", help="skip the timed SAM-file parse (host_parse_s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-scale", type=float, default=0.016)
     ap.add_argument("--no-cpu-mc", action="store_true", help="skip the multi-threaded C baseline")
@@ -183,11 +187,15 @@ def main():
     from sam2consensus_amd import configs, shard
     from sam2consensus_amd.engine import DeviceBatch, Workspace
 
-    local %= max(torch.cuda.device_count(), 1)   # (ranks sharing a device: rehearsals on one GPU, gloo)
+    backend = os.environ.get("S2C_DIST_BACKEND", "nccl")
+    ndev = max(torch.cuda.device_count(), 1)
+    if local >= ndev:
+        if backend != "gloo":   # RCCL needs one device per rank
+            raise SystemExit("LOCAL_RANK %d but only %d GPUs visible (S2C_DIST_BACKEND=gloo shares devices)" % (local, ndev))
+        local %= ndev   # (ranks sharing a device: rehearsals on one GPU, gloo)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        backend = os.environ.get("S2C_DIST_BACKEND", "nccl")
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     wl = args.workload
@@ -200,10 +208,13 @@ def main():
         min_depth = int(opt_args[opt_args.index("-m") + 1])
 
     t0 = time.perf_counter()
-    sharded = world > 1 and args.shard
+    sharded = world > 1 and not args.independent
     full = configs.synth_batch(wl, seed=configs.SEED + (0 if sharded else rank))
     hb = shard.sub_batch(full, rank, world) if sharded else full
-    t_host = time.perf_counter() - t0
+    t_synth = time.perf_counter() - t0
+    file_parse = None
+    if world == 1 and not args.no_file_parse:
+        file_parse = time_file_parse(wl, full)
     info = hb.info
     T = len(thresholds)
     db = DeviceBatch(hb, dev)
@@ -312,8 +323,9 @@ def main():
             assert tile_ms <= ms * 1.001 and (not args.stage_events or kern["step_events"] <= ms * 1.05), (kern, ms)
             achieved = tile_bytes * per_rank / (tile_ms * 1e-3) / 1e9
             traffic = traffic_from_profile(wl)
+            bound = bound_from_profile(wl)
             line["roofline"] = {
-                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "bound": bound.get("bound", "hbm"), "bound_evidence": bound.get("evidence"), "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic.get("bytes") if traffic else None,
                 "traffic_frac": (traffic["bytes"] / (tile_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS) if traffic else None,
                 "kernel": "s2c_pileup = k_tile_dense + k_tile (CIGAR walk of dense tiles, pileup, insertion "
@@ -323,9 +335,12 @@ def main():
             line["kernels_ms"] = kern
             line["kernels_alg_gbps"] = {"k_reads": reads_bytes * per_rank / (kern["k_reads"] * 1e-3) / 1e9,
                                         "k_tile": achieved}
-        line["step_alg_bytes"] = step_bytes * per_rank
-        line["step_alg_gbps"] = step_bytes * per_rank / (ms * 1e-3) / 1e9
-        line["host_parse_s"] = t_host
+        # SURVEY §8(d)'s formula counts a count tensor written and read (48 B per position) that
+        # the fused tile kernels never materialise: reported as bytes only, not as a rate
+        line["unfused_step_alg_bytes"] = step_bytes * per_rank
+        line["host_parse_s"] = file_parse["parse_s"] if file_parse else None
+        line["host_parse"] = file_parse
+        line["host_synth_feed_s"] = t_synth
         line["host"] = cpu_model()
         line["parity"] = parity
         if world == 1 and not args.no_cpu_baseline:
@@ -335,6 +350,49 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def bound_from_profile(wl):
+    """What bounds the dominant kernel, from the committed PMC summary (scripts/bound.py):
+    "valu" when its VALU instructions alone take most of its time, else "hbm"."""
+    p = os.path.join(ROOT, "profiles", "bound_%s.json" % wl)
+    if os.path.exists(p):
+        with open(p) as fh:
+            return json.load(fh)
+    return {}
+
+
+def time_file_parse(wl, ref_hb):
+    """North_star's separately reported host SAM parse: the workload's SAM text written to a
+    file (not timed), then parsed from it by the product parser (libs2c.so, threaded) into the
+    packed batch; its counters must equal the batch the bench runs."""
+    import tempfile
+
+    from sam2consensus_amd import configs
+    from sam2consensus_amd.batch import parse_file
+    td = tempfile.mkdtemp(prefix="s2c_parse_")
+    path = os.path.join(td, wl + ".sam")
+    try:
+        t0 = time.perf_counter()
+        configs.synth_write(wl, path)
+        tw = time.perf_counter() - t0
+        size = os.path.getsize(path)
+        t0 = time.perf_counter()
+        hb = parse_file(path, configs.maxdel_active(configs.cli_args(wl)), 150)
+        tp = time.perf_counter() - t0
+        same = (hb.info.reads_mapped == ref_hb.info.reads_mapped and hb.info.aligned_bases == ref_hb.info.aligned_bases
+                and hb.info.n_tiles == ref_hb.info.n_tiles)
+        hb.free()
+    finally:
+        try:
+            os.remove(path)
+            os.rmdir(td)
+        except OSError:
+            pass
+    return {"parse_s": tp, "file_bytes": size, "file_mb_per_s": size / tp / 1e6, "threads": cpu_threads(),
+            "write_s": tw, "same_batch": same,
+            "what": "libs2c.so s2c_parser_feed_file of the workload's .sam (read, parse, pack, plan) on %d threads"
+                    % cpu_threads()}
 
 
 def traffic_from_profile(wl):

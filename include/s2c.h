@@ -108,13 +108,17 @@ int s2c_layout(int64_t *out, int n);
 #define S2C_RUN_LONG   0x10u /* (kind bits) run of a long piece: skipped by the rs window */
 
 /* tile record tiles[t][S2C_TILE_WORDS] */
-#define S2C_TILE_WORDS   20  /* {a, b, ref, flags, boff, bcap, loff, lcap, cb0, ccap, lp0, lp1, nev,
-                                 pf0, pf1, o0, o1, qw0, qw1, nl}: the window's pieces [pf0, pf1) (short
-                                 pieces starting in [a/32 - kwin, b/32)), their op slots [o0, o1),
-                                 base plane words [qw0, qw1), and nl, the window's LAYERS: layer l takes
-                                 from every start word s of the window its pieces
-                                 [ps[s] + n_s*l/nl, ps[s] + n_s*(l+1)/nl) (n_s = ps[s+1] - ps[s]) — one
-                                 LDS chunk of k_tile (S2C_CHUNK_*) */
+#define S2C_TILE_WORDS   24  /* {a, b, ref, flags, boff, bcap, loff, lcap, cb0, ccap, lp0, lp1, nev,
+                                 pf0, pf1, o0, o1, qw0, qw1, nl, ly0, 0, 0, 0}: the window's pieces
+                                 [pf0, pf1) (short pieces starting in [a/32 - kwin, b/32)), their op
+                                 slots [o0, o1) and base plane words [qw0, qw1); nl LAYERS of the
+                                 window, copied for k_tile as layers ly0 .. ly0 + nl - 1 of the
+                                 layered arrays (lly): layer l holds, from every start word s of the
+                                 window, its short pieces [ps[s] + n_s*l/nl, ps[s] + n_s*(l+1)/nl)
+                                 (n_s = ps[s+1] - ps[s]), in start-word order — one LDS chunk of
+                                 k_tile (S2C_CHUNK_*); ly0 = S2C_LY_MAIN: one layer, the window read in
+                                 place from the sorted arrays (pf0 .. qw1) */
+#define S2C_LY_MAIN 0xFFFFFFFFu
 #define S2C_TILE_DEEP     1  /* several work items: counts summed in HBM, voted by k_consensus */
 #define S2C_TILE_GENERAL  2  /* insertion layout beyond k_tile's LDS: voted by k_consensus */
 #define S2C_TILE_DENSE    4  /* routed to k_tile_dense (one item, no insertion keys, no long pieces) */
@@ -130,17 +134,16 @@ int s2c_layout(int64_t *out, int n);
    readable up to their end rounded up to 16 bytes. */
 #define S2C_DENSE_BYTES(ns, nq) (((4 * (ns) + 30) & ~15) + ((8 * (nq) + 30) & ~15) + ((12 * (ns) + 1024 + 15) & ~15))
 #define S2C_DENSE_QW   4096  /* base plane words of a dense tile's window (17-bit query offsets) */
-/* k_tile's LDS chunk (one layer of a tile window): per piece (one thread each) its base
-   plane words {p0, p1} through the word after its last base (funnel shift), its non-ACGT
-   words (pieces with S2C_PF_X) and its op words (pieces without S2C_PF_SIMPLE), each in
-   16-byte blocks from the 16-byte boundary below; its run records (= op slots).  Caps per
-   layer, and run records per 32-position word and counting lane (8-bit counters: <=
-   S2C_CHUNK_LANE_RECS * lanes per word).  A work item's run records per word are <=
-   S2C_ITEM_RECS (its u16 histogram). */
-#define S2C_CHUNK_PIECES     256
-#define S2C_CHUNK_PBLK      1280
-#define S2C_CHUNK_XBLK       256
-#define S2C_CHUNK_OBLK       128
+/* k_tile's LDS chunk: one layer of a tile window, contiguous in the layered arrays: its
+   piece records, op words, base planes
+   {p0, p1} through the word after its last base (funnel shift) and non-ACGT words — caps
+   per layer — and its run records (= op slots), per 32-position word and counting lane <=
+   S2C_CHUNK_LANE_RECS * lanes per word (8-bit counters).  A work item's run records per
+   word are <= S2C_ITEM_RECS (its u16 histogram). */
+#define S2C_CHUNK_PIECES     512
+#define S2C_CHUNK_QBYTES   16384
+#define S2C_CHUNK_XBYTES    8192
+#define S2C_CHUNK_OBYTES    4096
 #define S2C_CHUNK_RECS       768
 #define S2C_CHUNK_LANE_RECS  248
 #define S2C_CHUNK_SEGS       128
@@ -165,6 +168,10 @@ typedef struct s2c_batch  s2c_batch;
 int  s2c_parser_new(int maxdel_active, int64_t maxdel, s2c_parser **out);
 /* Feed raw SAM text (any chunking; lines may straddle calls). */
 int  s2c_parser_feed(s2c_parser *p, const char *buf, size_t len);
+/* The header is over (its lines fed, ending in '\n'): a later '@' line is a body line that
+ * the read pass skips (:195), never an @SQ (:149-172) — for parsers fed the header and then
+ * a block from the middle of the file (sam2consensus_amd/dparse.py). */
+int  s2c_parser_end_header(s2c_parser *p);
 /* Parse a whole file; ".gz" suffix → zlib (:111-114).  Read in bounded windows. */
 int  s2c_parser_feed_file(s2c_parser *p, const char *path);
 /* End of input: reformat-phase checks (:284-294), global layout, bucketing, tile plan. */
@@ -242,6 +249,10 @@ typedef struct {
     int64_t n_cols;            /* insertion column slots over all tiles (Σ ccap ≥ Σ columns) */
     int64_t runs_max;          /* most run slots any tile's window holds */
     int64_t dense_lds;         /* most LDS bytes any dense tile's window takes (S2C_DENSE_BYTES) */
+    int64_t n_layers;          /* layers of the non-dense tiles' windows (lly) */
+    int64_t n_lpieces;         /* pieces of the layered arrays (lpc) */
+    int64_t n_lops;            /* op words of the layered arrays (lops) */
+    int64_t n_lqwords;         /* plane words of the layered arrays (lbq, lbx) */
 } s2c_batch_info;
 
 typedef struct {               /* host pointers into the batch (valid until s2c_batch_free) */
@@ -266,6 +277,15 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
                                   tile t's are lp[tiles[t].lp0 .. tiles[t].lp1) */
     const uint32_t *wtile;     /* [n_words] tile of each 32-position word (0xFFFFFFFF: padding) */
     const uint32_t *ps;        /* [n_words+1] pieces starting in words [W0, W1) are [ps[W0], ps[W1]) */
+    /* layered windows of the non-dense tiles (k_tile): tile t's layer l is layer
+       tiles[t].ly0 + l; layer L = pieces [lly[L].x, lly[L+1].x) of lpc, op words
+       [lly[L].y, lly[L+1].y) of lops, planes from half-word lly[L].z (16-base units) of lbq /
+       lbx; a piece record's qh and opoff index these arrays */
+    const uint32_t *lly;       /* [n_layers+1][4] {piece, op word, plane half-word, 0} */
+    const uint32_t *lpc;       /* [n_lpieces+1][4] */
+    const uint32_t *lops;      /* [n_lops] */
+    const uint32_t *lbq;       /* [n_lqwords][2] */
+    const uint32_t *lbx;       /* [n_lqwords] */
 } s2c_batch_arrays;
 
 int  s2c_batch_info_get(const s2c_batch *b, s2c_batch_info *out);
@@ -317,7 +337,9 @@ typedef struct {
     /* ---- packed batch (device copies of s2c_batch_arrays) ---- */
     const uint32_t *pc, *ops, *bq, *bx, *rs;
     const uint32_t *tiles, *items, *dense, *deep, *lp, *wtile, *rlist, *ps;
+    const uint32_t *lly, *lpc, *lops, *lbq, *lbx;   /* layered windows (s2c_batch_arrays) */
     int64_t n_pieces, n_ops, n_qwords, n_tiles, n_items, n_dense, n_deep, padded_len, chunk, n_rlist, dense_lds;
+    int64_t n_layers, n_lpieces, n_lops, n_lqwords;
     int32_t kwin, tile_max;
 
     /* ---- options (:102, :117-138) ---- */

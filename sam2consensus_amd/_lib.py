@@ -25,7 +25,8 @@ S2C_ERR_LIMIT = -13
 
 S2C_NSYM = 6
 S2C_POS_ALIGN = 64
-S2C_TILE_WORDS = 20
+S2C_TILE_WORDS = 24
+S2C_LY_MAIN = 0xFFFFFFFF
 S2C_ITEM_WORDS = 4
 S2C_CODE_FILL = 0
 S2C_SHORT_MOTIF = 16
@@ -53,7 +54,8 @@ class BatchInfo(C.Structure):
         "n_refs", "total_len", "padded_len", "header_lines", "lines_total", "reads_mapped",
         "aligned_bases", "query_bases", "n_pieces", "n_ops", "n_tokens", "n_qwords", "n_words",
         "n_tiles", "n_items", "n_dense", "n_deep", "n_long", "n_rlist", "kwin", "tile_max", "chunk",
-        "n_ins", "n_ins_bases", "n_bkt", "n_lng", "n_cols", "runs_max", "dense_lds")]
+        "n_ins", "n_ins_bases", "n_bkt", "n_lng", "n_cols", "runs_max", "dense_lds", "n_layers", "n_lpieces", "n_lops",
+        "n_lqwords")]
 
 
 _P64 = C.POINTER(C.c_int64)
@@ -63,7 +65,7 @@ _P32 = C.POINTER(C.c_uint32)
 class BatchArrays(C.Structure):
     _fields_ = [("ref_len", _P64), ("ref_off", _P64), ("ref_cov_reads", _P64)] + \
         [(n, _P32) for n in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "rlist", "lp", "wtile",
-                             "ps")]
+                             "ps", "lly", "lpc", "lops", "lbq", "lbx")]
 
 
 class SynthSpec(C.Structure):
@@ -80,9 +82,10 @@ _VP = C.c_void_p
 class Dev(C.Structure):
     """Mirror of ``s2c_dev`` (include/s2c.h)."""
     _fields_ = [(n, _VP) for n in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile",
-                                   "rlist", "ps")] + \
+                                   "rlist", "ps", "lly", "lpc", "lops", "lbq", "lbx")] + \
         [(n, C.c_int64) for n in ("n_pieces", "n_ops", "n_qwords", "n_tiles", "n_items", "n_dense", "n_deep",
-                                  "padded_len", "chunk", "n_rlist", "dense_lds")] + [
+                                  "padded_len", "chunk", "n_rlist", "dense_lds", "n_layers", "n_lpieces", "n_lops",
+                                  "n_lqwords")] + [
         ("kwin", C.c_int32), ("tile_max", C.c_int32),
         ("maxdel_active", C.c_int32), ("maxdel", C.c_int32),
         ("thresholds", _VP), ("n_thr", C.c_int32), ("min_depth", C.c_int32),
@@ -101,7 +104,7 @@ class WsSizes(C.Structure):
 # every symbol include/s2c.h declares (tests/test_lib.py checks the export table)
 EXPORTS = [
     "s2c_last_error", "s2c_abi_version", "s2c_layout",
-    "s2c_parser_new", "s2c_parser_feed", "s2c_parser_feed_file", "s2c_parser_finish", "s2c_parser_free",
+    "s2c_parser_new", "s2c_parser_feed", "s2c_parser_end_header", "s2c_parser_feed_file", "s2c_parser_finish", "s2c_parser_free",
     "s2c_parser_set_tile_width", "s2c_parser_snapshot", "s2c_parser_retain", "s2c_parser_stream_state",
     "s2c_parser_retain_events", "s2c_accumulate",
     "s2c_parser_pos_weights", "s2c_parser_checks", "s2c_parser_counters", "s2c_parser_pack",
@@ -128,6 +131,7 @@ def _load():
         "s2c_layout": (C.c_int, [C.POINTER(C.c_int64), C.c_int]),
         "s2c_parser_new": (C.c_int, [C.c_int, C.c_int64, pp]),
         "s2c_parser_feed": (C.c_int, [_VP, C.c_char_p, C.c_size_t]),
+        "s2c_parser_end_header": (C.c_int, [_VP]),
         "s2c_parser_feed_file": (C.c_int, [_VP, C.c_char_p]),
         "s2c_parser_finish": (C.c_int, [_VP, pp]),
         "s2c_parser_free": (None, [_VP]),

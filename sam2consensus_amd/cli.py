@@ -165,10 +165,15 @@ def consensus_files_sharded(filename, thresholds, prefix, min_depth, fill, nchar
     from .shard import gather_results
 
     world, rank, local = _dist_env()
-    local %= max(torch.cuda.device_count(), 1)   # (ranks sharing a device: gloo tests on one GPU)
+    backend = os.environ.get("S2C_DIST_BACKEND", "nccl")
+    ndev = max(torch.cuda.device_count(), 1)
+    if local >= ndev:
+        if backend != "gloo":   # RCCL: one device per rank
+            raise RuntimeError("LOCAL_RANK %d but %d GPU(s) visible: launch one process per GPU "
+                               "(S2C_DIST_BACKEND=gloo lets ranks share a device)" % (local, ndev))
+        local %= ndev   # (ranks sharing a device: gloo tests on one GPU)
     torch.cuda.set_device(local)
     if not dist.is_initialized():
-        backend = os.environ.get("S2C_DIST_BACKEND", "nccl")
         dist.init_process_group(backend, device_id=torch.device("cuda", local) if backend == "nccl" else None)
     P = parse_distributed(filename, rank, world, maxdel_active)
     if log and rank == 0:

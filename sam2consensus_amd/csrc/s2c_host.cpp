@@ -39,6 +39,20 @@ int s2c_set_error(int code, const std::string &msg) {
     return code;
 }
 extern "C" const char *s2c_last_error(void) { return g_err.c_str(); }
+// No C++ exception crosses the C-ABI: an allocation failure (e.g. a corrupt input's sizes)
+// or any other exception becomes an error code.
+template <class F>
+int s2c_guarded(F &&f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc &) {
+        return s2c_set_error(S2C_ERR_LIMIT, "out of host memory");
+    } catch (const std::length_error &e) {
+        return s2c_set_error(S2C_ERR_LIMIT, std::string("size beyond this build's limits: ") + e.what());
+    } catch (const std::exception &e) {
+        return s2c_set_error(S2C_ERR_IO, std::string("host exception: ") + e.what());
+    }
+}
 extern "C" int s2c_abi_version(void) { return S2C_ABI_VERSION; }
 
 // ------------------------------------------------------------------ tables
@@ -213,6 +227,7 @@ struct s2c_batch {
     std::vector<std::string> names;
     std::vector<int64_t> ref_len, ref_off, ref_reads;
     std::vector<uint32_t> pc, ops, bq, bx, rs, tiles, items, dense, deep, lp, wtile, rlist, ps;
+    std::vector<uint32_t> lly, lpc, lops, lbq, lbx;   // layered windows of the non-dense tiles
     std::vector<uint32_t> kmin, kmax;   // host only: global key range of each piece's insertion events
 };
 
@@ -471,13 +486,16 @@ static int process_line(s2c_parser *p, const char *s, size_t n) {
     return S2C_OK;
 }
 
-extern "C" int s2c_parser_new(int maxdel_active, int64_t maxdel, s2c_parser **out) {
+static int s2c_parser_new_impl(int maxdel_active, int64_t maxdel, s2c_parser **out) {
     if (!out) return s2c_set_error(S2C_ERR_ARG, "out is NULL");
     s2c_parser *p = new s2c_parser();
     p->maxdel_active = maxdel_active != 0;
     p->maxdel = maxdel;
     *out = p;
     return S2C_OK;
+}
+extern "C" int s2c_parser_new(int maxdel_active, int64_t maxdel, s2c_parser **out) {
+    return s2c_guarded([&] { return s2c_parser_new_impl(maxdel_active, maxdel, out); });
 }
 
 extern "C" void s2c_parser_free(s2c_parser *p) { delete p; }
@@ -486,7 +504,7 @@ namespace {
 int parse_window(s2c_parser *p, const char *s, size_t n);
 }
 
-extern "C" int s2c_parser_feed(s2c_parser *p, const char *buf, size_t len) {
+static int s2c_parser_feed_impl(s2c_parser *p, const char *buf, size_t len) {
     if (!p) return s2c_set_error(S2C_ERR_ARG, "parser is NULL");
     if (p->err) return s2c_set_error(p->err, p->errmsg);
     const char *s = buf, *end = buf + len;
@@ -517,6 +535,17 @@ extern "C" int s2c_parser_feed(s2c_parser *p, const char *buf, size_t len) {
         if (rc) return rc;
         s = nl + 1;
     }
+    return S2C_OK;
+}
+extern "C" int s2c_parser_feed(s2c_parser *p, const char *buf, size_t len) {
+    return s2c_guarded([&] { return s2c_parser_feed_impl(p, buf, len); });
+}
+
+extern "C" int s2c_parser_end_header(s2c_parser *p) {
+    if (!p) return s2c_set_error(S2C_ERR_ARG, "parser is NULL");
+    if (p->err) return s2c_set_error(p->err, p->errmsg);
+    if (!p->carry.empty()) return s2c_set_error(S2C_ERR_ARG, "header does not end with a newline");
+    p->in_header = false;
     return S2C_OK;
 }
 
@@ -653,6 +682,10 @@ struct Bgzf {
                 if (k + bs > cb.size()) break;   // partial block: the next piece
                 const unsigned char *t = cb.data() + k + bs - 4;
                 const size_t is = (size_t)t[0] | ((size_t)t[1] << 8) | ((size_t)t[2] << 16) | ((size_t)t[3] << 24);
+                if (is > 65536) {   // not a BGZF block (≤ 64 KiB inflated): zlib checks the rest sequentially
+                    seq = true;
+                    break;
+                }
                 off.push_back(k);
                 len.push_back(bs);
                 isz.push_back(total);
@@ -786,7 +819,7 @@ struct Reader {   // plain, gzip or BGZF (:111-114) byte source
 };
 }  // namespace
 
-extern "C" int s2c_parser_feed_file(s2c_parser *p, const char *path) {
+static int s2c_parser_feed_file_impl(s2c_parser *p, const char *path) {
     if (!p || !path) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
     if (p->err) return s2c_set_error(p->err, p->errmsg);
     const size_t n = strlen(path);
@@ -891,6 +924,9 @@ extern "C" int s2c_parser_feed_file(s2c_parser *p, const char *path) {
     reader.join();
     return rc;
 }
+extern "C" int s2c_parser_feed_file(s2c_parser *p, const char *path) {
+    return s2c_guarded([&] { return s2c_parser_feed_file_impl(p, path); });
+}
 
 // ------------------------------------------------------------------ finish: layout + plan
 namespace {
@@ -978,52 +1014,46 @@ static void mark_runs(s2c_batch *b) {
 // ------------------------------------------------------------------ k_tile's layer plan
 // k_tile stages a tile's window in LDS one LAYER at a time: the window's start words
 // [S0, S1) (S0 = max(W0 - K, 0)) are its segments, and layer l of nl takes from segment s
-// its pieces [ps[s] + n_s*l/nl, ps[s] + n_s*(l+1)/nl) — every layer touches every word of
-// the tile alike.  A layer must fit the chunk (S2C_CHUNK_*): pieces, 16-byte blocks of base
-// planes / non-ACGT words / op words (per piece the kernel's count for the worst 16-byte
-// alignment, so a shard's re-laid planes fit too), run records, and per word <=
-// S2C_CHUNK_LANE_RECS records per counting lane.
+// its short pieces among [ps[s] + n_s*l/nl, ps[s] + n_s*(l+1)/nl) — every layer touches
+// every word of the tile alike.  The layers are copied contiguously (build_layers), each
+// one 16-byte aligned in every array, so a layer is one DMA per array.  A layer must fit
+// the chunk (S2C_CHUNK_*): pieces, plane / non-ACGT / op bytes, run records, and per word
+// <= S2C_CHUNK_LANE_RECS records per counting lane.
 struct PieceBlocks {          // prefix sums over the sorted pieces (mod 2^32: differences exact)
-    std::vector<uint32_t> pb, xb, ob;
+    std::vector<uint32_t> n, h, o;   // short pieces, their plane half-words, their op words
 };
+static inline uint32_t piece_half_words(uint32_t w3) { return ((w3 & 0xFFFFFFu) + 15u) / 16u; }
 static void piece_blocks(const s2c_batch *b, PieceBlocks &B) {
     const int64_t NP = b->info.n_pieces;
-    B.pb.assign(NP + 1, 0);
-    B.xb.assign(NP + 1, 0);
-    B.ob.assign(NP + 1, 0);
+    B.n.assign(NP + 1, 0);
+    B.h.assign(NP + 1, 0);
+    B.o.assign(NP + 1, 0);
     for (int64_t k = 0; k < NP; k++) {
-        const uint32_t w3 = b->pc[4 * k + 3], fl = w3 >> 24, len = w3 & 0xFFFFFFu;
-        const uint32_t nops = b->pc[4 * k + 6] - b->pc[4 * k + 2];
-        const uint32_t nw = ((16 + len + 31) >> 5) + 1;   // plane words, worst start phase
-        uint32_t pb = 0, xb = 0, ob = 0;
-        if (!(fl & S2C_PF_LONG)) {
-            pb = (8 * nw + 15) / 16 + 1;
-            if (fl & S2C_PF_X) xb = (4 * nw + 15) / 16 + 1;
-            if (!(fl & S2C_PF_SIMPLE)) ob = (4 * nops + 15) / 16 + 1;
-        }
-        B.pb[k + 1] = B.pb[k] + pb;
-        B.xb[k + 1] = B.xb[k] + xb;
-        B.ob[k + 1] = B.ob[k] + ob;
+        const uint32_t w3 = b->pc[4 * k + 3];
+        const bool sh = !((w3 >> 24) & S2C_PF_LONG);
+        B.n[k + 1] = B.n[k] + (sh ? 1u : 0u);
+        B.h[k + 1] = B.h[k] + (sh ? piece_half_words(w3) : 0u);
+        B.o[k + 1] = B.o[k] + (sh ? b->pc[4 * k + 6] - b->pc[4 * k + 2] : 0u);
     }
 }
 
 struct LayerSeg { uint64_t p0, n; };
 static inline uint64_t layer_lo(const LayerSeg &g, uint64_t l, uint64_t nl) { return g.p0 + g.n * l / nl; }
 
-static bool layer_fits(const s2c_batch *b, const PieceBlocks &B, const std::vector<LayerSeg> &seg, int64_t S0,
-                       int64_t W0, int64_t W1, int64_t K, int64_t G, uint64_t l, uint64_t nl, std::vector<int64_t> &recs) {
+static bool layer_fits(const PieceBlocks &B, const std::vector<LayerSeg> &seg, int64_t S0, int64_t W0, int64_t W1,
+                       int64_t K, int64_t G, uint64_t l, uint64_t nl, std::vector<int64_t> &recs) {
     const size_t NS = seg.size();
-    uint64_t np = 0, pb = 0, xb = 0, ob = 0, rc = 0;
+    uint64_t np = 0, nh = 0, rc = 0;
     for (size_t i = 0; i < NS; i++) {
         const uint64_t lo = layer_lo(seg[i], l, nl), hi = layer_lo(seg[i], l + 1, nl);
-        recs[i] = (int64_t)(b->pc[4 * hi + 2] - b->pc[4 * lo + 2]);
-        np += hi - lo;
-        pb += (uint32_t)(B.pb[hi] - B.pb[lo]);
-        xb += (uint32_t)(B.xb[hi] - B.xb[lo]);
-        ob += (uint32_t)(B.ob[hi] - B.ob[lo]);
+        recs[i] = (int64_t)(uint32_t)(B.o[hi] - B.o[lo]);
+        np += (uint32_t)(B.n[hi] - B.n[lo]);
+        nh += (uint32_t)(B.h[hi] - B.h[lo]);
         rc += (uint64_t)recs[i];
     }
-    if (np > S2C_CHUNK_PIECES || pb > S2C_CHUNK_PBLK || xb > S2C_CHUNK_XBLK || ob > S2C_CHUNK_OBLK || rc > S2C_CHUNK_RECS)
+    // (planes: 8 B per 2 half-words, + the funnel word, rounded to 16 B; non-ACGT: half)
+    if (np > S2C_CHUNK_PIECES || 4 * nh + 32 > S2C_CHUNK_QBYTES || 2 * nh + 32 > S2C_CHUNK_XBYTES ||
+        4 * rc + 32 > S2C_CHUNK_OBYTES || rc > S2C_CHUNK_RECS)
         return false;
     for (int64_t W = W0; W < W1; W++) {
         int64_t r = 0;
@@ -1037,26 +1067,145 @@ static bool layer_fits(const s2c_batch *b, const PieceBlocks &B, const std::vect
 static int64_t plan_layers(const s2c_batch *b, const PieceBlocks &B, int64_t K, uint64_t a, uint64_t e, int64_t G) {
     const int64_t W0 = (int64_t)(a >> 5), W1 = (int64_t)((e + 31) >> 5), S0 = std::max<int64_t>(W0 - K, 0);
     std::vector<LayerSeg> seg;
-    uint64_t tp = 0, tb = 0, tr = 0, maxn = 0;
+    uint64_t tp = 0, th = 0, tr = 0, maxn = 0;
     for (int64_t s = S0; s < W1; s++) {
         const uint64_t p0 = b->ps[s], n = b->ps[s + 1] - p0;
         seg.push_back({p0, n});
-        tp += n;
-        tb += (uint32_t)(B.pb[p0 + n] - B.pb[p0]);
-        tr += b->pc[4 * (p0 + n) + 2] - b->pc[4 * p0 + 2];
+        tp += (uint32_t)(B.n[p0 + n] - B.n[p0]);
+        th += (uint32_t)(B.h[p0 + n] - B.h[p0]);
+        tr += (uint32_t)(B.o[p0 + n] - B.o[p0]);
         maxn = std::max(maxn, n);
     }
     if (maxn == 0) return 1;
     std::vector<int64_t> recs(seg.size());
-    uint64_t nl = std::max<uint64_t>({1, (tp * 10 / 9) / S2C_CHUNK_PIECES + 1, (tb * 10 / 9) / S2C_CHUNK_PBLK + 1,
+    uint64_t nl = std::max<uint64_t>({1, (tp * 10 / 9) / S2C_CHUNK_PIECES + 1, (4 * th * 10 / 9) / S2C_CHUNK_QBYTES + 1,
                                       (tr * 10 / 9) / S2C_CHUNK_RECS + 1});
     nl = std::min(nl, maxn);
     for (;; nl = nl + 1 + nl / 16) {
         if (nl > maxn) nl = maxn;
         bool ok = true;
-        for (uint64_t l = 0; l < nl && ok; l++) ok = layer_fits(b, B, seg, S0, W0, W1, K, G, l, nl, recs);
+        for (uint64_t l = 0; l < nl && ok; l++) ok = layer_fits(B, seg, S0, W0, W1, K, G, l, nl, recs);
         if (ok) return (int64_t)nl;
         if (nl == maxn) return 0;
+    }
+}
+
+// Whether tile tw's window, read in place from the sorted arrays (one layer: tile word 20 =
+// S2C_LY_MAIN), fits k_tile's chunk: its pieces (long ones included: their op words and
+// planes are in the range) [pf0, pf1), op words [o0, o1), plane words [qw0, qw1) at their
+// arrays' own 16-byte phases.
+static bool main_window_fits(const s2c_batch *b, const uint32_t *tw, int64_t K, int64_t G) {
+    const uint64_t np = tw[14] - tw[13], no = tw[16] - tw[15], nq = tw[18] - tw[17];
+    if (np > S2C_CHUNK_PIECES || no > S2C_CHUNK_RECS || 4 * no + 32 > S2C_CHUNK_OBYTES || 8 * nq + 32 > S2C_CHUNK_QBYTES ||
+        4 * nq + 32 > S2C_CHUNK_XBYTES)
+        return false;
+    const int64_t W0 = tw[0] >> 5, W1 = (tw[1] + 31) >> 5;
+    for (int64_t W = W0; W < W1; W++)
+        if ((int64_t)b->rs[W + 1] - (int64_t)b->rs[std::max<int64_t>(W - K, 0)] > (int64_t)S2C_CHUNK_LANE_RECS * G)
+            return false;
+    return true;
+}
+
+// The layered windows (s2c.h, tile words 19-20): for every tile whose window is not read in
+// place, its nl layers in order, each a copy of its short pieces (records with re-based qh /
+// opoff, op words, base planes and non-ACGT words of SEQ[0:len], len the record's length
+// field), contiguous (the kernel's DMA takes each array's 16-byte phase).
+static void build_layers(s2c_batch *b, const PieceBlocks &B, int64_t G) {
+    s2c_batch_info &I = b->info;
+    const int64_t NT = I.n_tiles, K = I.kwin;
+    std::vector<uint64_t> lyp, lyo, lyh;   // layer starts: pieces, op words, plane half-words
+    lyp.push_back(0); lyo.push_back(0); lyh.push_back(0);
+    struct TL { int64_t t, ly0, nl; };
+    std::vector<TL> tl;
+    for (int64_t t = 0; t < NT; t++) {
+        uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
+        if (tw[19] == 1 && main_window_fits(b, tw, K, G)) {
+            tw[20] = S2C_LY_MAIN;
+            continue;
+        }
+        const int64_t nl = tw[19], W0 = tw[0] >> 5, W1 = (tw[1] + 31) >> 5, S0 = std::max<int64_t>(W0 - K, 0);
+        tw[20] = (uint32_t)(lyp.size() - 1);
+        tl.push_back({t, (int64_t)lyp.size() - 1, nl});
+        for (int64_t l = 0; l < nl; l++) {
+            uint64_t np = 0, no = 0, nh = 0;
+            for (int64_t s = S0; s < W1; s++) {
+                const LayerSeg g{b->ps[s], (uint64_t)(b->ps[s + 1] - b->ps[s])};
+                const uint64_t lo = layer_lo(g, l, nl), hi = layer_lo(g, l + 1, nl);
+                np += (uint32_t)(B.n[hi] - B.n[lo]);
+                no += (uint32_t)(B.o[hi] - B.o[lo]);
+                nh += (uint32_t)(B.h[hi] - B.h[lo]);
+            }
+            lyp.push_back(lyp.back() + np);
+            lyo.push_back(lyo.back() + no);
+            lyh.push_back(lyh.back() + nh);
+        }
+    }
+    const int64_t NL = (int64_t)lyp.size() - 1;
+    I.n_layers = NL;
+    I.n_lpieces = (int64_t)lyp.back();
+    I.n_lops = (int64_t)lyo.back();
+    I.n_lqwords = (int64_t)(lyh.back() / 2) + 2;   // (+ the funnel word after the last)
+    b->lly.assign(4 * (size_t)(NL + 1), 0u);
+    for (int64_t L = 0; L <= NL; L++) {
+        b->lly[4 * L] = (uint32_t)lyp[L];
+        b->lly[4 * L + 1] = (uint32_t)lyo[L];
+        b->lly[4 * L + 2] = (uint32_t)lyh[L];
+    }
+    b->lpc.assign(4 * (size_t)(I.n_lpieces + 1), 0u);
+    b->lops.assign(std::max<int64_t>(I.n_lops, 4), 0u);
+    b->lbq.assign(2 * (size_t)I.n_lqwords, 0u);
+    b->lbx.assign((size_t)I.n_lqwords, 0u);
+    {
+        uint32_t *sp = &b->lpc[4 * (size_t)I.n_lpieces];   // sentinel
+        sp[1] = (uint32_t)lyh.back();
+        sp[2] = (uint32_t)lyo.back();
+    }
+    auto copy_tiles = [&](size_t i0, size_t i1) {
+        const uint16_t *sq = (const uint16_t *)b->bq.data(), *sx = (const uint16_t *)b->bx.data();
+        uint16_t *dq = (uint16_t *)b->lbq.data(), *dx = (uint16_t *)b->lbx.data();
+        for (size_t i = i0; i < i1; i++) {
+            const TL &T = tl[i];
+            const uint32_t *tw = &b->tiles[(size_t)T.t * S2C_TILE_WORDS];
+            const int64_t W0 = tw[0] >> 5, W1 = (tw[1] + 31) >> 5, S0 = std::max<int64_t>(W0 - K, 0);
+            for (int64_t l = 0; l < T.nl; l++) {
+                const int64_t L = T.ly0 + l;
+                uint64_t kp = lyp[L], ko = lyo[L], kh = lyh[L];
+                for (int64_t s = S0; s < W1; s++) {
+                    const LayerSeg g{b->ps[s], (uint64_t)(b->ps[s + 1] - b->ps[s])};
+                    const uint64_t lo = layer_lo(g, l, T.nl), hi = layer_lo(g, l + 1, T.nl);
+                    for (uint64_t k = lo; k < hi; k++) {
+                        const uint32_t *pr = &b->pc[4 * k];
+                        if ((pr[3] >> 24) & S2C_PF_LONG) continue;
+                        const uint32_t no = pr[6] - pr[2], nh = piece_half_words(pr[3]);
+                        uint32_t *dp = &b->lpc[4 * kp];
+                        dp[0] = pr[0];
+                        dp[1] = (uint32_t)kh;
+                        dp[2] = (uint32_t)ko;
+                        dp[3] = pr[3];
+                        memcpy(&b->lops[ko], &b->ops[pr[2]], 4 * (size_t)no);
+                        for (uint32_t h = 0; h < nh; h++) {
+                            const uint64_t a = (uint64_t)pr[1] + h, d = kh + h;
+                            dq[(d >> 1) * 4 + (d & 1)] = sq[(a >> 1) * 4 + (a & 1)];
+                            dq[(d >> 1) * 4 + 2 + (d & 1)] = sq[(a >> 1) * 4 + 2 + (a & 1)];
+                            dx[d] = sx[a];
+                        }
+                        kp++;
+                        ko += no;
+                        kh += nh;
+                    }
+                }
+            }
+        }
+    };
+    const size_t NTL = tl.size();
+    unsigned hw = std::thread::hardware_concurrency();
+    const int nt = (int)std::max<size_t>(1, std::min<size_t>(std::min<unsigned>(hw ? hw : 1, 16), NTL / 64));
+    if (nt <= 1) {
+        copy_tiles(0, NTL);
+    } else {
+        std::vector<std::thread> th;
+        for (int k = 0; k < nt; k++) th.emplace_back(copy_tiles, NTL * k / nt, NTL * (k + 1) / nt);
+        for (auto &x : th) x.join();
     }
 }
 
@@ -1138,29 +1287,38 @@ static void check_late(s2c_parser *p) {
     }
 }
 
-extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
+static int s2c_parser_finish_impl(s2c_parser *p, s2c_batch **out) {
     if (!p || !out) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
     int rc = feed_flush(p);
     if (rc) return rc;
     check_late(p);
     return build_batch(p, out);
 }
+extern "C" int s2c_parser_finish(s2c_parser *p, s2c_batch **out) {
+    return s2c_guarded([&] { return s2c_parser_finish_impl(p, out); });
+}
 
-extern "C" int s2c_parser_set_tile_width(s2c_parser *p, int64_t width) {
+static int s2c_parser_set_tile_width_impl(s2c_parser *p, int64_t width) {
     if (!p) return s2c_set_error(S2C_ERR_ARG, "parser is NULL");
     if (width != 0 && (width < S2C_POS_ALIGN || width > 2048 || width % S2C_POS_ALIGN))
         return s2c_set_error(S2C_ERR_ARG, "tile width must be 0 or a multiple of 64 in [64, 2048]");
     p->tile_width = width;
     return S2C_OK;
 }
+extern "C" int s2c_parser_set_tile_width(s2c_parser *p, int64_t width) {
+    return s2c_guarded([&] { return s2c_parser_set_tile_width_impl(p, width); });
+}
 
 // The batch of everything parsed so far (the partial last line stays unparsed); the
 // parser keeps going.
-extern "C" int s2c_parser_snapshot(s2c_parser *p, s2c_batch **out) {
+static int s2c_parser_snapshot_impl(s2c_parser *p, s2c_batch **out) {
     if (!p || !out) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
     if (p->err) return s2c_set_error(p->err, p->errmsg);
     check_late(p);
     return build_batch(p, out);
+}
+extern "C" int s2c_parser_snapshot(s2c_parser *p, s2c_batch **out) {
+    return s2c_guarded([&] { return s2c_parser_snapshot_impl(p, out); });
 }
 
 // Move the reads `keep` selects into one chunk (their tokens, planes and events; no line
@@ -1219,7 +1377,7 @@ static void compact_reads(s2c_parser *p, Keep keep, bool events_only) {
 
 // Drop the reads that cannot change a global position >= gmin (their positions below it
 // are emitted).
-extern "C" int s2c_parser_retain(s2c_parser *p, int64_t gmin) {
+static int s2c_parser_retain_impl(s2c_parser *p, int64_t gmin) {
     if (!p) return s2c_set_error(S2C_ERR_ARG, "parser is NULL");
     if (p->err) return s2c_set_error(p->err, p->errmsg);
     if (gmin < p->frontier) return s2c_set_error(S2C_ERR_ARG, "retain: frontier moves backwards");
@@ -1230,15 +1388,21 @@ extern "C" int s2c_parser_retain(s2c_parser *p, int64_t gmin) {
     p->frontier = gmin;
     return S2C_OK;
 }
+extern "C" int s2c_parser_retain(s2c_parser *p, int64_t gmin) {
+    return s2c_guarded([&] { return s2c_parser_retain_impl(p, gmin); });
+}
 
 // Unsorted input: the counts of every read held are in the running totals; keep only the
 // reads with insertion events, as event-only reads (their motifs are counted once, by the
 // last batch, which holds every event — and the insertion checks of :284-294 see them all).
-extern "C" int s2c_parser_retain_events(s2c_parser *p) {
+static int s2c_parser_retain_events_impl(s2c_parser *p) {
     if (!p) return s2c_set_error(S2C_ERR_ARG, "parser is NULL");
     if (p->err) return s2c_set_error(p->err, p->errmsg);
     compact_reads(p, [](const Chunk &, const ReadRec &r, int64_t) { return r.nev > 0; }, true);
     return S2C_OK;
+}
+extern "C" int s2c_parser_retain_events(s2c_parser *p) {
+    return s2c_guarded([&] { return s2c_parser_retain_events_impl(p); });
 }
 
 // state[0] = 1 if a read parsed after a retain reached below its frontier; state[1..2] =
@@ -1284,7 +1448,7 @@ static void insertion_checks(const s2c_parser *p, std::vector<uint8_t> &bad_sym,
 // each read goes to the ranks whose position range it can change (read_extent, as the
 // streamed retain); a rank plans its sub-batch from the reads it receives.
 
-extern "C" int s2c_parser_pos_weights(s2c_parser *p, int64_t shift, int64_t *w, int64_t n) {
+static int s2c_parser_pos_weights_impl(s2c_parser *p, int64_t shift, int64_t *w, int64_t n) {
     if (!p || (!w && n > 0) || shift < 0 || shift > 40) return s2c_set_error(S2C_ERR_ARG, "bad argument");
     int rc = feed_flush(p);
     if (rc) return rc;
@@ -1298,8 +1462,11 @@ extern "C" int s2c_parser_pos_weights(s2c_parser *p, int64_t shift, int64_t *w, 
         }
     return S2C_OK;
 }
+extern "C" int s2c_parser_pos_weights(s2c_parser *p, int64_t shift, int64_t *w, int64_t n) {
+    return s2c_guarded([&] { return s2c_parser_pos_weights_impl(p, shift, w, n); });
+}
 
-extern "C" int s2c_parser_checks(s2c_parser *p, uint8_t *bad, int64_t n_refs) {
+static int s2c_parser_checks_impl(s2c_parser *p, uint8_t *bad, int64_t n_refs) {
     if (!p || (!bad && n_refs > 0)) return s2c_set_error(S2C_ERR_ARG, "bad argument");
     if (n_refs != (int64_t)p->ref_names.size()) return s2c_set_error(S2C_ERR_ARG, "n_refs differs from the header's");
     int rc = feed_flush(p);
@@ -1311,6 +1478,9 @@ extern "C" int s2c_parser_checks(s2c_parser *p, uint8_t *bad, int64_t n_refs) {
         bad[2 * r + 1] = bk[r];
     }
     return S2C_OK;
+}
+extern "C" int s2c_parser_checks(s2c_parser *p, uint8_t *bad, int64_t n_refs) {
+    return s2c_guarded([&] { return s2c_parser_checks_impl(p, bad, n_refs); });
 }
 
 extern "C" int s2c_parser_counters(s2c_parser *p, int64_t *out) {
@@ -1335,7 +1505,7 @@ struct BlobHdr {
 constexpr uint32_t BLOB_MAGIC = 0x42433253u;   // "S2CB"
 }  // namespace
 
-extern "C" int s2c_parser_pack(s2c_parser *p, int64_t g0, int64_t g1, size_t *len) {
+static int s2c_parser_pack_impl(s2c_parser *p, int64_t g0, int64_t g1, size_t *len) {
     if (!p || !len) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
     int rc = feed_flush(p);
     if (rc) return rc;
@@ -1364,6 +1534,9 @@ extern "C" int s2c_parser_pack(s2c_parser *p, int64_t g0, int64_t g1, size_t *le
     *len = bytes;
     return S2C_OK;
 }
+extern "C" int s2c_parser_pack(s2c_parser *p, int64_t g0, int64_t g1, size_t *len) {
+    return s2c_guarded([&] { return s2c_parser_pack_impl(p, g0, g1, len); });
+}
 
 extern "C" int s2c_parser_blob_copy(const s2c_parser *p, void *dst, size_t cap) {
     if (!p || (!dst && !p->blob.empty())) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
@@ -1372,7 +1545,7 @@ extern "C" int s2c_parser_blob_copy(const s2c_parser *p, void *dst, size_t cap) 
     return S2C_OK;
 }
 
-extern "C" int s2c_parser_unpack(s2c_parser *p, const void *blob, size_t len) {
+static int s2c_parser_unpack_impl(s2c_parser *p, const void *blob, size_t len) {
     if (!p || (!blob && len)) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
     if (p->err) return s2c_set_error(p->err, p->errmsg);
     int rc = feed_flush(p);
@@ -1412,6 +1585,9 @@ extern "C" int s2c_parser_unpack(s2c_parser *p, const void *blob, size_t len) {
     p->chunks.push_back(std::move(c));
     p->chunks.emplace_back(new Chunk());   // the sequential feed appends here
     return S2C_OK;
+}
+extern "C" int s2c_parser_unpack(s2c_parser *p, const void *blob, size_t len) {
+    return s2c_guarded([&] { return s2c_parser_unpack_impl(p, blob, len); });
 }
 
 static int build_batch(s2c_parser *p, s2c_batch **out) {
@@ -1741,7 +1917,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
         int64_t maxc = 0;
         for (int64_t W = w0; W < w1; W++)
             maxc = std::max<int64_t>(maxc, (int64_t)b->rs[W + 1] - (int64_t)b->rs[std::max<int64_t>(W - K, 0)] + nlg);
-        const int64_t nl = plan_layers(b, PB, K, (uint64_t)T.a, (uint64_t)T.b, G);
+        int64_t nl = plan_layers(b, PB, K, (uint64_t)T.a, (uint64_t)T.b, G);
         if (nl <= 0) return s2c_set_error(S2C_ERR_LIMIT, "a read whose SEQ or CIGAR exceeds k_tile's LDS chunk");
         const int64_t nch = plan_items(b, K, (uint64_t)T.a, (uint64_t)T.b, nl);
         I.chunk = std::max<int64_t>(I.chunk, nl);
@@ -1785,6 +1961,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     I.n_lng = (int64_t)loff;
     I.n_cols = (int64_t)coff;
     I.runs_max = runs_max;
+    build_layers(b, PB, G);
     mark_runs(b);
     *out = guard.release();
     return S2C_OK;
@@ -1798,7 +1975,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
 // global coordinates; words outside the shard map to no tile (k_reads drops events keyed
 // there).  Counts of a position depend only on the runs covering it, so every shard's
 // tiles get exactly the unsharded counts — no exchange of counts is needed.
-extern "C" int s2c_batch_shard(const s2c_batch *b, int64_t t0, int64_t t1, s2c_batch **out) {
+static int s2c_batch_shard_impl(const s2c_batch *b, int64_t t0, int64_t t1, s2c_batch **out) {
     if (!b || !out) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
     const s2c_batch_info &I = b->info;
     if (t0 < 0 || t1 > I.n_tiles || t0 > t1) return s2c_set_error(S2C_ERR_ARG, "bad tile range");
@@ -1956,11 +2133,21 @@ extern "C" int s2c_batch_shard(const s2c_batch *b, int64_t t0, int64_t t1, s2c_b
         if (!dense_fits(tw, K)) return s2c_set_error(S2C_ERR_LIMIT, "shard window beyond the dense kernel's LDS");
         J.dense_lds = std::max<int64_t>(J.dense_lds, dense_bytes(tw, K));
     }
+    {   // the shard's own layered windows (its pieces are re-laid)
+        int64_t nwp = 8;
+        while (nwp * 32 < J.tile_max) nwp *= 2;
+        PieceBlocks PB;
+        piece_blocks(s.get(), PB);
+        build_layers(s.get(), PB, 256 / nwp);
+    }
     mark_runs(s.get());
     // the shard's share of the workload's aligned bases (by its positions; for reporting)
     J.aligned_bases = I.total_len ? (int64_t)((double)I.aligned_bases * (double)aligned / (double)I.total_len) : 0;
     *out = s.release();
     return S2C_OK;
+}
+extern "C" int s2c_batch_shard(const s2c_batch *b, int64_t t0, int64_t t1, s2c_batch **out) {
+    return s2c_guarded([&] { return s2c_batch_shard_impl(b, t0, t1, out); });
 }
 
 extern "C" int s2c_batch_info_get(const s2c_batch *b, s2c_batch_info *out) {
@@ -1987,6 +2174,11 @@ extern "C" int s2c_batch_arrays_get(const s2c_batch *b, s2c_batch_arrays *o) {
     o->wtile = b->wtile.data();
     o->rlist = b->rlist.data();
     o->ps = b->ps.data();
+    o->lly = b->lly.data();
+    o->lpc = b->lpc.data();
+    o->lops = b->lops.data();
+    o->lbq = b->lbq.data();
+    o->lbx = b->lbx.data();
     return S2C_OK;
 }
 
@@ -1998,7 +2190,7 @@ extern "C" const char *s2c_batch_ref_name(const s2c_batch *b, int64_t i) {
 extern "C" void s2c_batch_free(s2c_batch *b) { delete b; }
 
 // ------------------------------------------------------------------ parsecigar (:46-82)
-extern "C" int s2c_parsecigar(const char *cigar, size_t cigar_len, const char *seq, size_t seq_len,
+static int s2c_parsecigar_impl(const char *cigar, size_t cigar_len, const char *seq, size_t seq_len,
                               int64_t pos_ref, char *seqout, size_t cap, size_t *seqout_len,
                               int64_t *ins, size_t max_ins, size_t *n_ins) {
     std::vector<uint32_t> toks;
@@ -2043,6 +2235,11 @@ extern "C" int s2c_parsecigar(const char *cigar, size_t cigar_len, const char *s
     *seqout_len = o;
     *n_ins = ni;
     return ni > max_ins ? s2c_set_error(S2C_ERR_ARG, "insertion buffer too small") : S2C_OK;
+}
+extern "C" int s2c_parsecigar(const char *cigar, size_t cigar_len, const char *seq, size_t seq_len,
+                              int64_t pos_ref, char *seqout, size_t cap, size_t *seqout_len,
+                              int64_t *ins, size_t max_ins, size_t *n_ins) {
+    return s2c_guarded([&] { return s2c_parsecigar_impl(cigar, cigar_len, seq, seq_len, pos_ref, seqout, cap, seqout_len, ins, max_ins, n_ins); });
 }
 
 // ------------------------------------------------------------------ ABI layout self-check

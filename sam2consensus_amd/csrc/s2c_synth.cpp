@@ -9,6 +9,22 @@
 #include <thread>
 #include "../../include/s2c.h"
 
+#include <new>
+#include <stdexcept>
+#include <string>
+
+int s2c_set_error(int code, const std::string &msg);
+template <class F>
+static int s2c_guarded(F &&f) {   // (as in s2c_host.cpp: no exception crosses the C-ABI)
+    try {
+        return f();
+    } catch (const std::bad_alloc &) {
+        return s2c_set_error(S2C_ERR_LIMIT, "out of host memory");
+    } catch (const std::exception &e) {
+        return s2c_set_error(S2C_ERR_IO, std::string("host exception: ") + e.what());
+    }
+}
+
 #include <zlib.h>
 
 #include <algorithm>
@@ -194,12 +210,15 @@ int generate(const s2c_synth_spec &sp, const Sink &sink, int64_t *n_out) {
 }
 }  // namespace
 
-extern "C" int s2c_synth_feed(const s2c_synth_spec *spec, s2c_parser *p, int64_t *n_reads_out) {
+static int s2c_synth_feed_impl(const s2c_synth_spec *spec, s2c_parser *p, int64_t *n_reads_out) {
     if (!spec || !p) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
     return generate(*spec, [p](const char *b, size_t n) { return s2c_parser_feed(p, b, n); }, n_reads_out);
 }
+extern "C" int s2c_synth_feed(const s2c_synth_spec *spec, s2c_parser *p, int64_t *n_reads_out) {
+    return s2c_guarded([&] { return s2c_synth_feed_impl(spec, p, n_reads_out); });
+}
 
-extern "C" int s2c_synth_write(const s2c_synth_spec *spec, const char *path, int64_t *n_reads_out) {
+static int s2c_synth_write_impl(const s2c_synth_spec *spec, const char *path, int64_t *n_reads_out) {
     if (!spec || !path) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
     size_t n = strlen(path);
     if (n >= 3 && strcmp(path + n - 3, ".gz") == 0) {
@@ -278,4 +297,7 @@ extern "C" int s2c_synth_write(const s2c_synth_spec *spec, const char *path, int
     }, n_reads_out);
     fclose(f);
     return rc;
+}
+extern "C" int s2c_synth_write(const s2c_synth_spec *spec, const char *path, int64_t *n_reads_out) {
+    return s2c_guarded([&] { return s2c_synth_write_impl(spec, path, n_reads_out); });
 }

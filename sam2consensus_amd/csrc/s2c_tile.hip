@@ -78,7 +78,9 @@ constexpr uint32_t MODE_RUN = 0, MODE_STORE = 1, MODE_ADD = 2, MODE_ADD_KEEP = 3
 
 struct TileArgs {
     const uint32_t *rs, *runs, *bq, *bx, *tiles, *lp, *pc, *ops, *ps;
-    const void *bq_end, *bx_end, *ops_end, *pc_end;   // ends of the DMA sources (buffer ranges)
+    const uint32_t *lly, *lpc, *lops, *lbq, *lbx;
+    const void *bq_end, *bx_end, *ops_end, *pc_end;      // ends of the DMA sources (buffer ranges)
+    const void *lbq_end, *lbx_end, *lops_end, *lpc_end;
     uint32_t maxdel_active, maxdel;
     uint32_t *ibkt, *ilong, *ilong_n;
     const double *thresholds;
@@ -654,22 +656,60 @@ constexpr uint32_t SL_SDC = 0, SL_SD = 1, SL_X = 2, SL_Y = 3, SL_N = 4, SL_Z = 5
 // still leaves room for the loads' immediate offsets: the hardware returns zeros.
 constexpr uint32_t OOR = 0xF0000000u;
 
-// A chunk in LDS: per chunk piece (segment-major, thread t stages and walks piece t) its
-// 16-byte blocks of base planes (pl, block 0 a pad so plane word −1 is readable), of
-// non-ACGT words (xl) and of op words (ol), at the block-scan offsets of the pieces before
-// it; its run records runl[recPre[t] + j − opoff] for op words j.  Segment σ (start word
-// S0 + σ) holds chunk pieces [segP[σ], segP[σ+1]) and records [segR[σ], segR[σ+1]).
+// A chunk in LDS: one layer of the tile's window, DMA'd as four contiguous ranges — its
+// piece records (into runl, read before the walk writes run records there), op words (ol),
+// base planes (pl; a 16-byte pad first, so plane word −1 is readable) and non-ACGT words
+// (xl), each landing at its source's 16-byte phase.  segR[σ]: the first run record of the
+// layer's pieces starting in word S0 + σ (pieces are in start-word order).
 struct ChunkLds {
-    uint32_t ps[CSEG + 1];                  // first piece of each start word of the window (tile-constant)
-    uint32_t segP[2][CSEG + 1];             // by layer parity: the next layer's table is built during this one
     uint32_t segR[CSEG + 1];
-    uint32_t recPre[S2C_CHUNK_PIECES + 1];
-    uint32_t wsumA[2][4], wsumB[2][4];      // block scans: wave totals
-    alignas(16) uint4 pl[1 + S2C_CHUNK_PBLK + 1];
-    alignas(16) uint4 xl[S2C_CHUNK_XBLK];
-    alignas(16) uint4 ol[S2C_CHUNK_OBLK];
-    uint2 runl[S2C_CHUNK_RECS + RPAD];
+    alignas(16) uint8_t pl[16 + S2C_CHUNK_QBYTES + 16];
+    alignas(16) uint8_t xl[S2C_CHUNK_XBYTES + 16];
+    alignas(16) uint8_t ol[S2C_CHUNK_OBYTES + 16];
+    alignas(16) uint2 runl[S2C_CHUNK_RECS + RPAD];
 };
+static_assert(S2C_CHUNK_PIECES * 16 <= (S2C_CHUNK_RECS + RPAD) * 8, "piece records fit the run-record region");
+
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t lds_byte_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+// A DMA source array: its buffer descriptor (base = the array's 16-byte aligned start, range
+// through its end rounded up to 16 bytes, < 4 GB: s2c_pileup checks), built once per kernel.
+struct DmaSrc {
+    v4i_t r;
+    uintptr_t base;
+};
+__device__ __forceinline__ DmaSrc dma_src(const void *p, const void *end) {
+    DmaSrc S;
+    S.base = (uintptr_t)p & ~(uintptr_t)15;
+    const uintptr_t eal = ((uintptr_t)end + 15) & ~(uintptr_t)15;
+    S.r.x = (int)uni((uint32_t)S.base);
+    S.r.y = (int)uni((uint32_t)(S.base >> 32) & 0xFFFFu);
+    S.r.z = (int)uni((uint32_t)min((uint64_t)(eal - S.base), (uint64_t)0xFFFFFFF0u));
+    S.r.w = 0x00020000;
+    return S;
+}
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"   // m0 (reserved) is set and clobbered by the DMA
+// n dwords src[0..n) of source array S → the 16-byte aligned LDS region dst by 16-byte
+// LDS-DMA, the 1 KB blocks split between the workgroup's waves (offsets in SGPRs); the copy
+// starts at the 16-byte boundary below src, so the dwords land at dst + (src & 15).
+// Arguments workgroup-uniform.  Completion: s_waitcnt vmcnt(0) (the compiler does not count
+// these loads), then a barrier.
+__device__ __forceinline__ void dma16_wg(uint8_t *dst, const DmaSrc &S, const uint32_t *src, uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
+    const uintptr_t sal = (uintptr_t)src & ~(uintptr_t)15;
+    const uint32_t nbytes = uni((uint32_t)((uintptr_t)src - sal) + 4 * n);
+    const uint32_t soff = uni((uint32_t)(sal - S.base)), m0 = uni(lds_byte_addr(dst));
+    for (uint32_t base = 1024 * wv; base < nbytes; base += 1024 * (WG / 64)) {
+        if (base + 16 * lane < nbytes)
+            asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                         :: "s"(m0 + base), "v"(16 * lane), "s"(S.r), "s"(soff + base) : "memory", "m0");
+    }
+}
+#pragma clang diagnostic pop
+
 template <uint32_t ICOL>
 struct EpiLds {
     FastLds<ICOL> L;
@@ -683,29 +723,50 @@ union TileLds {
 
 // The N / '-' chars of SEQ among LDS plane bases [q, q + l), whose first lies at
 // tile-relative position r0: 'N' (counted as A by the planes) into SL_N; '-' (counted as C)
-// into SL_SD and, unless the read's '-' are maxdel-dropped (:210), SL_SDC.
+// into SL_SD and, unless the read's '-' are maxdel-dropped (:210), SL_SDC.  Runs of up to
+// six plane words take an unrolled pass (their non-ACGT words read together, the rare set
+// bits handled one by one); longer ones a loop.
+template <int NWP>
+__device__ __forceinline__ void x_bits(uint32_t xm, uint32_t p0, int32_t b0, uint32_t r0, bool drop, uint32_t *hist) {
+    using H = Hist<NWP>;
+    while (xm) {
+        const uint32_t bit = (uint32_t)__builtin_ctz(xm);
+        xm &= xm - 1;
+        const uint32_t p = r0 + (uint32_t)(b0 + (int32_t)bit);
+        if ((p0 >> bit) & 1u) {
+            H::add1(hist, SL_SD, p, 1u);
+            if (!drop) H::add1(hist, SL_SDC, p, 1u);
+        } else {
+            H::add1(hist, SL_N, p, 1u);
+        }
+    }
+}
 template <int NWP>
 __device__ void x_fix(const uint2 *bql, const uint32_t *xl, uint32_t xd, uint32_t q, uint32_t l, uint32_t r0, bool drop,
                       uint32_t *hist) {
-    using H = Hist<NWP>;
-    for (uint32_t v = q >> 5; v <= (q + l - 1) >> 5; v++) {
+    const uint32_t v0 = q >> 5, v1 = (q + l - 1) >> 5;
+    if (v1 - v0 < 6) {
+        uint32_t xs[6];
+#pragma unroll
+        for (uint32_t u = 0; u < 6; u++) {
+            const uint32_t v = v0 + u;
+            uint32_t m = v <= v1 ? xl[v + xd] : 0u;
+            if (u == 0) m &= 0xFFFFFFFFu << (q & 31u);
+            if (v == v1) m &= 0xFFFFFFFFu >> (31u - ((q + l - 1) & 31u));
+            xs[u] = m;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 6; u++)
+            if (xs[u]) x_bits<NWP>(xs[u], bql[v0 + u].x, (int32_t)(32 * (v0 + u)) - (int32_t)q, r0, drop, hist);
+        return;
+    }
+    for (uint32_t v = v0; v <= v1; v++) {
         uint32_t xm = xl[v + xd];
         if (!xm) continue;
         const int32_t b0 = (int32_t)(32 * v) - (int32_t)q;   // run offset of the word's bit 0
         if (b0 < 0) xm &= 0xFFFFFFFFu << (uint32_t)(-b0);
         if (b0 + 32 > (int32_t)l) xm &= 0xFFFFFFFFu >> (uint32_t)(b0 + 32 - (int32_t)l);
-        const uint32_t p0 = bql[v].x;
-        while (xm) {
-            const uint32_t bit = (uint32_t)__builtin_ctz(xm);
-            xm &= xm - 1;
-            const uint32_t p = r0 + (uint32_t)(b0 + (int32_t)bit);
-            if ((p0 >> bit) & 1u) {
-                H::add1(hist, SL_SD, p, 1u);
-                if (!drop) H::add1(hist, SL_SDC, p, 1u);
-            } else {
-                H::add1(hist, SL_N, p, 1u);
-            }
-        }
+        x_bits<NWP>(xm, bql[v].x, b0, r0, drop, hist);
     }
 }
 
@@ -793,31 +854,6 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
     }
 }
 
-// Exclusive scans of x and y over the workgroup (every thread calls: one barrier); tx / ty:
-// the totals.  wsum: this scan's own wave-total slots.
-__device__ __forceinline__ void scan256x2(uint32_t x, uint32_t y, uint32_t (*wsum)[4], uint32_t &ex, uint32_t &ey,
-                                          uint32_t &tx, uint32_t &ty) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const uint32_t ix = __ockl_wfscan_add_u32(x, true), iy = __ockl_wfscan_add_u32(y, true);
-    if (lane == 63) {
-        wsum[0][wv] = ix;
-        wsum[1][wv] = iy;
-    }
-    lds_sync();
-    uint32_t ox = 0, oy = 0;
-    tx = ty = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < WG / 64; k++) {
-        const uint32_t vx = wsum[0][k], vy = wsum[1][k];
-        ox += k < wv ? vx : 0u;
-        oy += k < wv ? vy : 0u;
-        tx += vx;
-        ty += vy;
-    }
-    ex = ox + ix - x;
-    ey = oy + iy - y;
-}
-
 #ifndef S2C_TILE_XCD
 #define S2C_TILE_XCD 1
 #endif
@@ -866,7 +902,6 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
         dV[i] = 0;
         dD[i] = 0;
     }
-    for (uint32_t i = tid; i <= NS; i += WG) C.ps[i] = d.ps[S0 + i];
     if (counts_only && d.mode != MODE_ADD_KEEP && T.nev > 0 && chunk == 0) {   // no vote: leave the tile's tables zero for the next run
         for (uint32_t e = tid; e < T.bcap; e += WG) ((uint4 *)d.ibkt)[T.boff + e] = make_uint4(0, 0, 0, 0);
         if (tid == 0) d.ilong_n[tile] = 0;
@@ -919,7 +954,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
 
     // this lane's word reads the records of segments [sa, sb] (start words W - K .. W)
     const uint32_t sa = active ? (W >= S0 + K ? W - K : S0) - S0 : 1u, sb = active ? W - S0 : 0u;
-    const uint2 *bql = (const uint2 *)(C.pl + 1);
+    const uint2 *bql = (const uint2 *)(C.pl + 16);
     const int32_t W32 = (int32_t)(32 * W);
     // one group's records → carry-save trees of X, Y, Z; NR = 8: weight-8 carries in t8o,
     // NR = 4 (a tail group): weight-4 carries
@@ -980,134 +1015,89 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     using Full = std::integral_constant<int, 8>;
     using Half = std::integral_constant<int, 4>;
 
-    // ---- layer tables: segment σ's layer-ly pieces [lo, hi) by arithmetic on the window's
-    //      piece CSR; their prefix (a block scan) into segP[ly & 1]; thread t's piece
-    auto seg_range = [&](uint32_t sg, uint32_t ly, uint32_t &lo, uint32_t &hi) {
-        const uint32_t p0 = C.ps[sg], cnt = C.ps[sg + 1] - p0;
-        lo = p0 + (uint32_t)(((uint64_t)cnt * ly) / nl);
-        hi = p0 + (uint32_t)(((uint64_t)cnt * (ly + 1)) / nl);
-    };
-    auto layer_table = [&](uint32_t ly) -> uint32_t {   // (ends with the scan's barrier, not after the writes)
-        uint32_t np = 0;
-        if (tid < NS) {
-            uint32_t lo, hi;
-            seg_range(tid, ly, lo, hi);
-            np = hi - lo;
-        }
-        uint32_t ex, ey, tot, toty;
-        scan256x2(np, 0u, C.wsumB, ex, ey, tot, toty);
-        if (tid < NS) C.segP[ly & 1][tid] = ex;
-        if (tid == 0) C.segP[ly & 1][NS] = tot;
-        return uni(tot);
-    };
-    auto piece_of = [&](uint32_t t, uint32_t ly) -> uint32_t {   // largest σ with segP[σ] ≤ t
-        const uint32_t *sp = C.segP[ly & 1];
-        uint32_t lo2 = 0, hi2 = NS;
-        while (hi2 - lo2 > 1) {
-            const uint32_t m = (lo2 + hi2) >> 1;
-            if (sp[m] <= t) lo2 = m; else hi2 = m;
-        }
-        uint32_t lo, hi;
-        seg_range(lo2, ly, lo, hi);
-        return lo + (t - sp[lo2]);
-    };
-    const uint4 *const pc4 = (const uint4 *)d.pc;
-    const uint4 *const bq4 = (const uint4 *)d.bq;
-    const uint4 *const bx4 = (const uint4 *)d.bx;
-    const uint4 *const op4 = (const uint4 *)d.ops;
+    // ---- the layers: in place (one layer: the window of the sorted arrays) or the tile's
+    //      copies in the layered arrays
+    const uint32_t ly0 = uni(d.tiles[(size_t)tile * S2C_TILE_WORDS + 20]);
+    const bool inplace = ly0 == S2C_LY_MAIN;
+    const uint32_t *const spc = inplace ? d.pc : d.lpc, *const sops = inplace ? d.ops : d.lops;
+    const uint32_t *const sbq = inplace ? d.bq : d.lbq, *const sbx = inplace ? d.bx : d.lbx;
+    const DmaSrc Dpc = dma_src(spc, inplace ? d.pc_end : d.lpc_end), Dops = dma_src(sops, inplace ? d.ops_end : d.lops_end);
+    const DmaSrc Dbq = dma_src(sbq, inplace ? d.bq_end : d.lbq_end), Dbx = dma_src(sbx, inplace ? d.bx_end : d.lbx_end);
     const uint32_t *const xl = (const uint32_t *)C.xl;
     const uint32_t *const opl = (const uint32_t *)C.ol;
-    constexpr uint32_t PBF = 5, XBF = 3;   // blocks staged through registers at once (more: a serial tail)
-    uint4 P = make_uint4(0u, 0u, 0u, 0u);
-    uint32_t oe = 0, npc = 0;
-    if (l0 < l1) {
-        npc = layer_table(l0);
-        lds_sync();
-        if (tid < npc) {
-            const uint32_t k = piece_of(tid, l0);
-            P = pc4[k];
-            oe = d.pc[4 * (size_t)k + 6];
-        }
-    }
+    const uint4 *const pcr = (const uint4 *)C.runl;
     for (uint32_t ly = l0; ly < l1; ly++) {
-        // ---- 1. this thread's piece: its blocks of planes / non-ACGT words / op words and
-        //      its run records; block scans → its LDS offsets
-        const bool valid = tid < npc;
-        const uint32_t fl = P.w >> 24, len = P.w & 0xFFFFFFu;
-        const bool simple = (fl & S2C_PF_SIMPLE) != 0, lng = (fl & S2C_PF_LONG) != 0;
-        const uint32_t gw0 = P.y >> 1;                                 // plane word of SEQ[0]
-        const uint32_t nw = ((16u * (P.y & 1u) + len + 31u) >> 5) + 1u;   // through the word after the last base
-        const uint32_t pb0 = gw0 >> 1, xb0 = gw0 >> 2, ob0 = P.z >> 2;
-        const uint32_t pb = (valid && !lng) ? ((gw0 + nw + 1u) >> 1) - pb0 : 0u;
-        const uint32_t xb = (valid && !lng && (fl & S2C_PF_X)) ? ((gw0 + nw + 3u) >> 2) - xb0 : 0u;
-        const uint32_t ob = (valid && !lng && !simple) ? ((oe + 3u) >> 2) - ob0 : 0u;
-        const uint32_t nr = valid ? oe - P.z : 0u;
-        uint32_t exA, exB, totA, totB;
-        scan256x2(pb | xb << 16, ob | nr << 16, C.wsumA, exA, exB, totA, totB);
-        TPROF_MARK(2);
-        const uint32_t pbPre = exA & 0xFFFFu, xbPre = exA >> 16, obPre = exB & 0xFFFFu, rPre = exB >> 16;
-        const uint32_t NR = uni(totB >> 16);
-        if (valid) C.recPre[tid] = rPre;
-        if (tid == 0) C.recPre[npc] = NR;
-        // the blocks: loads now, LDS writes after the next layer's table is built
-        uint4 pv[PBF], xv[XBF];
-#pragma unroll
-        for (uint32_t m = 0; m < PBF; m++) pv[m] = m < pb ? bq4[pb0 + m] : make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-        for (uint32_t m = 0; m < XBF; m++) xv[m] = m < xb ? bx4[xb0 + m] : make_uint4(0u, 0u, 0u, 0u);
-        // ---- 2. the next layer's table and piece records (in flight through this layer's walk
-        //      and count)
-        uint4 Pn = make_uint4(0u, 0u, 0u, 0u);
-        uint32_t oen = 0, npcn = 0;
-        if (ly + 1 < l1) {
-            npcn = layer_table(ly + 1);
-            lds_sync();
-            if (tid < npcn) {
-                const uint32_t k = piece_of(tid, ly + 1);
-                Pn = pc4[k];
-                oen = d.pc[4 * (size_t)k + 6];
-            }
+        // ---- 1. the layer: pieces [P0, P1), op words [O0, O1), plane words [qa, qb)
+        uint32_t P0, P1, O0, O1, qa, qb;
+        if (inplace) {
+            const uint32_t *tw = d.tiles + (size_t)tile * S2C_TILE_WORDS;
+            P0 = uni(tw[13]); P1 = uni(tw[14]); O0 = uni(tw[15]); O1 = uni(tw[16]); qa = uni(tw[17]); qb = uni(tw[18]);
         } else {
-            lds_sync();
+            const uint4 A = ((const uint4 *)d.lly)[ly0 + ly], B = ((const uint4 *)d.lly)[ly0 + ly + 1];
+            P0 = uni(A.x); P1 = uni(B.x); O0 = uni(A.y); O1 = uni(B.y);
+            qa = uni(A.z) >> 1;
+            qb = ((uni(B.z) + 1u) >> 1) + 1u;   // through the word after the last base (funnel)
         }
-        TPROF_MARK(3);
-#pragma unroll
-        for (uint32_t m = 0; m < PBF; m++)
-            if (m < pb) C.pl[1 + pbPre + m] = pv[m];
-#pragma unroll
-        for (uint32_t m = 0; m < XBF; m++)
-            if (m < xb) C.xl[xbPre + m] = xv[m];
-        for (uint32_t m = PBF; m < pb; m++) C.pl[1 + pbPre + m] = bq4[pb0 + m];   // (long SEQ: serial)
-        for (uint32_t m = XBF; m < xb; m++) C.xl[xbPre + m] = bx4[xb0 + m];
-        for (uint32_t m = 0; m < ob; m++) C.ol[obPre + m] = op4[ob0 + m];
-        if (tid <= NS) C.segR[tid] = C.recPre[C.segP[ly & 1][tid]];
-        for (uint32_t i = tid; i < RPAD; i += WG) C.runl[NR + i] = make_uint2(0u, 0u);
+        const uint32_t NPc = P1 - P0, NR = O1 - O0;
+        dma16_wg((uint8_t *)C.runl, Dpc, spc + 4 * (size_t)P0, 4 * NPc);
+        dma16_wg(C.ol, Dops, sops + O0, NR);
+        dma16_wg(C.pl + 16, Dbq, sbq + 2 * (size_t)qa, 2 * (qb - qa));
+        dma16_wg(C.xl, Dbx, sbx + qa, qb - qa);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_sync();
-        TPROF_MARK(4);
-        // ---- 3. walk this thread's piece (from registers and LDS)
-        if (valid) {
-            // LDS plane base of SEQ[0]; non-ACGT word of LDS plane word v: xl[v + xd]; op word j:
-            // opl[j + od]; its records runl[j + rd]
-            const uint32_t ql = 64u * pbPre + 32u * (gw0 & 1u) + 16u * (P.y & 1u);
-            const uint32_t xd = 4u * xbPre - 4u * xb0 - (2u * pbPre - 2u * pb0);
-            if (simple) {   // one run of SEQ[0:take] (:64-69)
+        TPROF_MARK(2);
+        // ---- 2. walk: thread per piece (records to registers first: their region becomes
+        //      the run records); the per-word record ranges from the pieces' start words
+        const uint32_t od = (O0 & 3u) - O0;                     // op word j at opl[j + od]
+        const uint32_t qadj = 32u * (qa & 1u) - 32u * qa;       // SEQ[0] at LDS plane base 16·qh + qadj
+        const uint32_t xd = (qa & 3u) - (qa & 1u);              // non-ACGT word of LDS plane word v: xl[v + xd]
+        uint4 Pw[2];
+        uint32_t oe[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const uint32_t i = tid + WG * u;
+            Pw[u] = make_uint4(0u, 0u, 0u, 0u);
+            oe[u] = 0;
+            if (i < NPc) {
+                Pw[u] = pcr[i];
+                oe[u] = i + 1 < NPc ? pcr[i + 1].z : O1;
+                const int32_t sw = (int32_t)(Pw[u].x >> 5) - (int32_t)S0;
+                const int32_t pw = i > 0 ? (int32_t)(pcr[i - 1].x >> 5) - (int32_t)S0 : -1;
+                for (int32_t sg = pw + 1; sg <= sw; sg++) C.segR[sg] = Pw[u].z - O0;
+                if (i + 1 == NPc)
+                    for (uint32_t sg = (uint32_t)(sw + 1); sg <= NS; sg++) C.segR[sg] = NR;
+            }
+        }
+        if (NPc == 0)
+            for (uint32_t sg = tid; sg <= NS; sg += WG) C.segR[sg] = 0;
+        lds_sync();
+        for (uint32_t i = tid; i < RPAD; i += WG) C.runl[NR + i] = make_uint2(0u, 0u);
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            if (tid + WG * u >= NPc) continue;
+            const uint4 P = Pw[u];
+            const uint32_t fl = P.w >> 24, len = P.w & 0xFFFFFFu, rPre = P.z - O0;
+            const uint32_t ql = 16u * P.y + qadj;
+            if (fl & S2C_PF_SIMPLE) {   // one run of SEQ[0:take] (:64-69)
                 const uint32_t c0 = max(P.x, a), c1 = min(P.x + len, a + n);
                 C.runl[rPre] = len ? make_uint2(P.x, (ql << 11) | len) : make_uint2(0u, 0u);
                 if (c1 > c0) {
                     atomicAdd(&dV[c0 - a], 1);
                     atomicSub(&dV[c1 - a], 1);
+#ifndef S2C_ABL_X
                     if (fl & S2C_PF_X) x_fix<NWP>(bql, xl, xd, ql + (c0 - P.x), c1 - c0, c0 - a, false, hist);
+#endif
                 }
-            } else if (lng) {   // (its runs come through the tile long lists)
-                for (uint32_t j = 0; j < nr; j++) C.runl[rPre + j] = make_uint2(0u, 0u);
+            } else if (fl & S2C_PF_LONG) {   // (its runs come through the tile long lists)
+                for (uint32_t j = P.z; j < oe[u]; j++) C.runl[j - O0] = make_uint2(0u, 0u);
             } else {
-                walk_chunk_piece<NWP>(P, oe, opl, 4u * obPre - 4u * ob0, C.runl, rPre - P.z, bql, xl, xd, ql - 16u * P.y,
-                                      d.maxdel_active != 0, (uint32_t)d.maxdel, a, n, hist, dV, dD);
+                walk_chunk_piece<NWP>(P, oe[u], opl, od, C.runl, 0u - O0, bql, xl, xd, qadj, d.maxdel_active != 0,
+                                      (uint32_t)d.maxdel, a, n, hist, dV, dD);
             }
         }
         lds_sync();
-        TPROF_MARK(5);
-        // ---- 4. count this lane's records cw0 + g + G·m < cw1 (reads past them: records of
+        TPROF_MARK(3);
+        // ---- 3. count this lane's records cw0 + g + G·m < cw1 (reads past them: records of
         //      pieces starting after W, or the zero pad — they cover nothing of W)
         const uint32_t cw0 = C.segR[sa], cw1 = C.segR[sb + 1];
         const uint32_t nrec = cw0 + g < cw1 ? (cw1 - cw0 - g + G - 1) / G : 0u;
@@ -1150,10 +1140,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
             close4(Z, t4[2]);
         }
         lds_sync();   // the chunk's LDS is rewritten by the next layer
-        TPROF_MARK(6);
-        P = Pn;
-        oe = oen;
-        npc = npcn;
+        TPROF_MARK(4);
     }
 
     // ---- long-piece records (rare; k_reads' run records through the tile's long list,
@@ -1202,7 +1189,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     }
     if (acc) flush();
     lds_sync();
-    TPROF_MARK(7);
+    TPROF_MARK(5);
     // ---- difference arrays → coverage and '-' per position (inclusive scans, thread blocks
     //      of NPOS / WG positions)
     {
@@ -1260,7 +1247,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
         for (uint32_t c = 0; c < NSYM; c++) hist[c * HP + hs] = outw[c];
     }
     lds_sync();
-    TPROF_MARK(8);
+    TPROF_MARK(6);
     if (finish) {
         // the epilogue's LDS (aliases the chunk): layout arrays zeroed, tables, fill
         FastLds<ICOL> &L = U.e.L;
@@ -1295,7 +1282,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
                 }
             }
     }
-    TPROF_MARK(9);
+    TPROF_MARK(7);
 #ifdef S2C_PROF
     if (threadIdx.x == 0 && (blockIdx.x & 15) == 0) {
         atomicAdd(&g_tprof[15], 1ull);
@@ -1503,6 +1490,9 @@ TileArgs tile_args(const s2c_dev &d) {
     p.rs = d.rs; p.runs = d.runs; p.bq = d.bq; p.bx = d.bx; p.tiles = d.tiles; p.lp = d.lp;
     p.pc = d.pc; p.ops = d.ops; p.ps = d.ps; p.bq_end = d.bq + 2 * d.n_qwords; p.bx_end = d.bx + d.n_qwords;
     p.ops_end = d.ops + std::max<int64_t>(d.n_ops, 1); p.pc_end = d.pc + 4 * (d.n_pieces + 1);
+    p.lly = d.lly; p.lpc = d.lpc; p.lops = d.lops; p.lbq = d.lbq; p.lbx = d.lbx;
+    p.lbq_end = d.lbq + 2 * d.n_lqwords; p.lbx_end = d.lbx + d.n_lqwords;
+    p.lops_end = d.lops + std::max<int64_t>(d.n_lops, 4); p.lpc_end = d.lpc + 4 * (d.n_lpieces + 1);
     p.maxdel_active = d.maxdel_active ? 1u : 0u;
     p.maxdel = d.maxdel < 0 ? 0u : (uint32_t)d.maxdel;
     p.ibkt = d.ibkt; p.ilong = d.ilong; p.ilong_n = d.ilong_n;
@@ -1562,8 +1552,11 @@ static int check_dev(const s2c_dev *d) {
     if (d->padded_len <= 0 || d->padded_len >= ((int64_t)1 << 32)) return s2c_set_error(S2C_ERR_ARG, "bad padded_len");
     if (d->n_tiles >= ((int64_t)1 << 31) || (int64_t)d->n_thr * d->n_tiles >= ((int64_t)1 << 40))
         return s2c_set_error(S2C_ERR_LIMIT, "too many (threshold, tile) blocks");
-    if (16 * d->n_ops >= 0xE0000000ll || 8 * d->n_qwords >= 0xE0000000ll)   // 32-bit buffer offsets below OOR
-        return s2c_set_error(S2C_ERR_LIMIT, "run records or base planes beyond 3.5 GB (split the input)");
+    if (16 * d->n_ops >= 0xE0000000ll || 8 * d->n_qwords >= 0xE0000000ll || 16 * d->n_pieces >= 0xE0000000ll ||
+        8 * d->n_lqwords >= 0xE0000000ll || 16 * d->n_lpieces >= 0xE0000000ll || 4 * d->n_lops >= 0xE0000000ll)
+        return s2c_set_error(S2C_ERR_LIMIT, "run records, pieces or base planes beyond 3.5 GB (split the input)");   // 32-bit buffer offsets
+    if (d->n_layers > 0 && (!d->lly || !d->lpc || !d->lops || !d->lbq || !d->lbx))
+        return s2c_set_error(S2C_ERR_ARG, "missing layered windows");
     if (d->n_pieces > 0 && (!d->pc || !d->ops || !d->bq || !d->bx || !d->runs))
         return s2c_set_error(S2C_ERR_ARG, "missing piece buffers");
     if (d->n_tiles > 0 && (!d->tiles || !d->rs || !d->wtile || !d->tile_stats || !d->blk_len || !d->out))

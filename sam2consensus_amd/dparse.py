@@ -75,6 +75,12 @@ class BlockParser(Parser):
     def set_tile_width(self, w):
         L.check(L.lib.s2c_parser_set_tile_width(self._p, int(w)))
 
+    def feed_header(self, header):
+        """The file's header lines, then the end of the header: a block from the middle of the
+        file may start with an '@' line, which the read pass skips (:195) as a body line."""
+        self.feed(header)
+        L.check(L.lib.s2c_parser_end_header(self._p))
+
 
 def split_header(head: bytes):
     """(header bytes, offset of the first record line) of a file's leading bytes; the header
@@ -199,11 +205,18 @@ def bgzf_index(mm):
 
 
 def _inflate(mm, blocks):
+    """The blocks' text; each checked against its CRC32 and ISIZE trailer as gzip does
+    (the reference reads with gzip.open, :111).  A mismatch raises IOError."""
+    import struct
     import zlib
     out = []
     for off, size in blocks:
         xlen = mm[off + 10] | (mm[off + 11] << 8)
-        out.append(zlib.decompress(mm[off + 12 + xlen:off + size - 8], -15))
+        data = zlib.decompress(mm[off + 12 + xlen:off + size - 8], -15)
+        crc, isize = struct.unpack("<II", mm[off + size - 8:off + size])
+        if zlib.crc32(data) != crc or len(data) & 0xFFFFFFFF != isize:
+            raise IOError("CRC check failed in BGZF block at byte %d" % off)
+        out.append(data)
     return b"".join(out)
 
 
@@ -227,12 +240,20 @@ def bgzf_text(filename, rank, world, group=None):
                 return None
             C = idx[-1][0] + idx[-1][1]
             mine = [b for b in idx if rank * C // world <= b[0] < (rank + 1) * C // world]
-            text = _inflate(mm, mine)
-            head = b""
-            for k in range(0, len(idx), 64):   # the header: the file's first blocks until a record line
-                head += _inflate(mm, idx[k:k + 64])
-                if split_header(head) is not None:
-                    break
+            bad = ""
+            try:
+                text = _inflate(mm, mine)
+                head = b""
+                for k in range(0, len(idx), 64):   # the header: the file's first blocks until a record line
+                    head += _inflate(mm, idx[k:k + 64])
+                    if split_header(head) is not None:
+                        break
+            except (IOError, OSError, __import__("zlib").error) as e:
+                bad = str(e) or "corrupt BGZF block"
+            errs = [None] * world   # a corrupt block fails every rank alike (no rank left waiting)
+            dist.all_gather_object(errs, bad, group=group)
+            if any(errs):
+                raise IOError(next(e for e in errs if e))
         finally:
             mm.close()
     header, H = split_header(head) or (head, len(head))
@@ -358,7 +379,7 @@ def parse_distributed(filename, rank, world, maxdel_active=True, group=None, blo
     for k, data in blocks:
         p = BlockParser(maxdel_active, 150)
         try:
-            p.feed(header)
+            p.feed_header(header)
             p.feed(data)
             c = p.counters()
         except Exception as e:  # noqa: BLE001 - re-raised on every rank below

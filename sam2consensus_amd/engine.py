@@ -44,7 +44,8 @@ def _ptr(t):
 class DeviceBatch:
     """The packed batch resident in HBM (inputs of every launch)."""
 
-    ARRAYS = ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile", "rlist", "ps")
+    ARRAYS = ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile", "rlist", "ps",
+              "lly", "lpc", "lops", "lbq", "lbx")
 
     def __init__(self, hb, device=None):
         self.device = _dev(device)
@@ -103,6 +104,7 @@ class Workspace:
         d.padded_len, d.chunk, d.kwin, d.tile_max = i.padded_len, i.chunk, i.kwin, i.tile_max
         d.dense_lds = i.dense_lds
         d.n_rlist = i.n_rlist
+        d.n_layers, d.n_lpieces, d.n_lops, d.n_lqwords = i.n_layers, i.n_lpieces, i.n_lops, i.n_lqwords
         # the maxdel rule (:210) runs on the device: the parser's setting unless overridden
         if maxdel_active is None:
             maxdel_active = getattr(db.hb, "maxdel_active", True)

@@ -89,9 +89,10 @@ def _tensor_device(group):
 
 
 def gather_results(fetched, sub, rank, world, T, group=None):
-    """Merge every rank's (stats, offs, out) on rank 0 with tensor collectives: an all-reduce
-    of the stats, an all-gather of (tile range, sizes), then of the padded offsets and body
-    bytes.  Returns the whole batch's (stats, offs, out) on rank 0, None elsewhere."""
+    """Merge every rank's (stats, offs, out) on rank 0 with tensor collectives: a reduce of
+    the stats, an all-gather of (tile range, sizes) (four numbers per rank), then a gather of
+    the padded offsets and body bytes to rank 0 only (no other rank holds every body).
+    Returns the whole batch's (stats, offs, out) on rank 0, None elsewhere."""
     import torch
     import torch.distributed as dist
 
@@ -99,7 +100,7 @@ def gather_results(fetched, sub, rank, world, T, group=None):
     dev = _tensor_device(group)
     st = torch.from_numpy(np.ascontiguousarray(stats).view(np.int64).copy()).to(dev)
     if world > 1:
-        dist.all_reduce(st, op=dist.ReduceOp.SUM, group=group)   # record stats of cut references
+        dist.reduce(st, dst=0, op=dist.ReduceOp.SUM, group=group)   # record stats of cut references
     offs = np.asarray(offs, dtype=np.uint64)
     meta = torch.tensor([sub.t0, sub.t1, len(offs), len(out)], dtype=torch.int64, device=dev)
     metas = [torch.empty_like(meta) for _ in range(world)]
@@ -113,10 +114,10 @@ def gather_results(fetched, sub, rank, world, T, group=None):
     if len(out):
         b_t[: len(out)] = torch.from_numpy(np.frombuffer(out, dtype=np.uint8).copy()).to(dev)
     if world > 1:
-        os_ = [torch.empty_like(o_t) for _ in range(world)]
-        bs_ = [torch.empty_like(b_t) for _ in range(world)]
-        dist.all_gather(os_, o_t, group=group)
-        dist.all_gather(bs_, b_t, group=group)
+        os_ = [torch.empty_like(o_t) for _ in range(world)] if rank == 0 else None
+        bs_ = [torch.empty_like(b_t) for _ in range(world)] if rank == 0 else None
+        dist.gather(o_t, os_, dst=0, group=group)
+        dist.gather(b_t, bs_, dst=0, group=group)
     else:
         os_, bs_ = [o_t], [b_t]
     if rank != 0:

@@ -6,7 +6,7 @@ rc=$?; tail -2 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || { grep -E "Error|erro
 for wl in ${WLS:-c5}; do
 for tp in ${TPS:-0}; do
   if [ "$tp" = 0 ]; then unset S2C_TILE_POS; else export S2C_TILE_POS=$tp; fi
-  timeout -k 10 300 python -u bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/q_$wl.json 2> gpurun_out/q_$wl.err || { tail -5 gpurun_out/q_$wl.err; exit 1; }
+  timeout -k 10 300 python -u bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline --no-file-parse > gpurun_out/q_$wl.json 2> gpurun_out/q_$wl.err || { tail -5 gpurun_out/q_$wl.err; exit 1; }
   python -c "import json;d=json.load(open('gpurun_out/q_$wl.json'));print('$wl tp $tp step', round(d['ms_per_step'],4), {k: round(v,4) for k,v in d['kernels_ms'].items()}, d['parity'])"
 done
 done

@@ -9,7 +9,7 @@ fi
 for wl in ${WLS:-c5}; do
 for v in base ${VARS}; do
   if [ "$v" = base ]; then unset S2C_LIB; else export S2C_LIB=libs2c_$v.so; fi
-  timeout -k 10 300 python -u bench.py --workload $wl --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/v_${wl}_$v.json 2> gpurun_out/v_${wl}_$v.err || { tail -5 gpurun_out/v_${wl}_$v.err; exit 1; }
+  timeout -k 10 300 python -u bench.py --workload $wl --steps 20 --warmup 3 --no-cpu-baseline --no-file-parse > gpurun_out/v_${wl}_$v.json 2> gpurun_out/v_${wl}_$v.err || { tail -5 gpurun_out/v_${wl}_$v.err; exit 1; }
   python -c "import json;d=json.load(open('gpurun_out/v_${wl}_$v.json'));print('$wl $v step', round(d['ms_per_step'],4), {k: round(v,4) for k,v in d['kernels_ms'].items()}, d['parity'])"
 done
 done

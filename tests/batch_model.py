@@ -217,7 +217,8 @@ def check_plan(hb):
     assert set(hb.rlist.tolist()) == set(np.nonzero(((fl & 16) != 0) | ((fl & PF_INS) != 0))[0].tolist())
 
 
-CHUNK_PIECES, CHUNK_PBLK, CHUNK_XBLK, CHUNK_OBLK, CHUNK_RECS = 256, 1280, 256, 128, 768   # include/s2c.h
+CHUNK_PIECES, CHUNK_QBYTES, CHUNK_XBYTES, CHUNK_OBYTES, CHUNK_RECS = 512, 16384, 8192, 4096, 768   # include/s2c.h
+LY_MAIN = 0xFFFFFFFF
 CHUNK_LANE_RECS, ITEM_RECS = 248, 60000
 
 
@@ -234,28 +235,17 @@ def layer_ranges(hb, t, nl=None):
     return S0, W0, W1, [(p0 + cnt * l // nl, p0 + cnt * (l + 1) // nl) for l in range(nl)]
 
 
-def piece_blocks(hb):
-    """Per piece the 16-byte blocks k_tile stages (s2c_tile.hip, thread per piece): base
-    planes through the word after its last base, non-ACGT words (PF_X), op words (not
-    PF_SIMPLE); none for long pieces."""
-    pc = hb.pc.astype(np.int64)
-    NP = hb.info.n_pieces
-    qh, oz, w3 = pc[:NP, 1], pc[:NP, 2], pc[:NP, 3]
-    oe = pc[1:NP + 1, 2]
-    fl, ln = w3 >> 24, w3 & 0xFFFFFF
-    gw0 = qh >> 1
-    nw = ((16 * (qh & 1) + ln + 31) >> 5) + 1
-    lng = (fl & PF_LONG) != 0
-    pb = np.where(lng, 0, ((gw0 + nw + 1) >> 1) - (gw0 >> 1))
-    xb = np.where(lng | ((fl & PF_X) == 0), 0, ((gw0 + nw + 3) >> 2) - (gw0 >> 2))
-    ob = np.where(lng | ((fl & PF_SIMPLE) != 0), 0, ((oe + 3) >> 2) - (oz >> 2))
-    return pb, xb, ob
+def _region(nbytes, phase):
+    """LDS bytes of a 16-byte LDS-DMA copy of nbytes starting at source phase `phase`."""
+    return (phase + nbytes + 15) & ~15
 
 
 def check_layers(hb):
-    """Every layer of every tile fits k_tile's LDS chunk exactly as the kernel lays it out
-    (this batch's own 16-byte alignments); records per word and counting lane; every item's
-    records per word fit its u16 histogram."""
+    """k_tile's layers: a tile read in place has one layer whose window fits the chunk at its
+    arrays' own 16-byte phases; every other tile's layers are exact copies, in start-word
+    order, of the short pieces of its proportional per-start-word slices (records, op words,
+    the planes of SEQ[0:len]), 16-byte aligned, within the chunk's caps; records per word
+    and counting lane; every item's records per word fit its u16 histogram."""
     i = hb.info
     pc = hb.pc.astype(np.int64)
     nwp = 8
@@ -263,18 +253,48 @@ def check_layers(hb):
         nwp *= 2
     G = 256 // nwp
     K = i.kwin
-    pb, xb, ob = (np.concatenate([[0], np.cumsum(v)]) for v in piece_blocks(hb))
+    lly, lpc = hb.lly.astype(np.int64), hb.lpc.astype(np.int64)
+    T = hb.tiles.astype(np.int64)
     for t in range(i.n_tiles):
+        row = T[t]
         S0, W0, W1, lays = layer_ranges(hb, t)
         assert W1 - S0 <= 128
-        for lo, hi in lays:
-            recs = pc[hi, 2] - pc[lo, 2]
-            assert (hi - lo).sum() <= CHUNK_PIECES and recs.sum() <= CHUNK_RECS
-            assert (pb[hi] - pb[lo]).sum() <= CHUNK_PBLK and (xb[hi] - xb[lo]).sum() <= CHUNK_XBLK
-            assert (ob[hi] - ob[lo]).sum() <= CHUNK_OBLK
+        if row[20] == LY_MAIN:
+            assert row[19] == 1
+            np_, no, nq = row[14] - row[13], row[16] - row[15], row[18] - row[17]
+            assert np_ <= CHUNK_PIECES and no <= CHUNK_RECS and _region(4 * no, 4 * (row[15] & 3)) <= CHUNK_OBYTES
+            assert _region(8 * nq, 8 * (row[17] & 1)) <= CHUNK_QBYTES and _region(4 * nq, 4 * (row[17] & 3)) <= CHUNK_XBYTES
+            rs = hb.rs.astype(np.int64)
             for W in range(W0, W1):
-                a = max(W - K, S0) - S0
-                assert recs[a:W - S0 + 1].sum() <= CHUNK_LANE_RECS * G
+                assert rs[W + 1] - rs[max(W - K, 0)] <= CHUNK_LANE_RECS * G
+        else:
+            for l, (lo, hi) in enumerate(lays):
+                L = row[20] + l
+                want = [k for s_lo, s_hi in zip(lo, hi) for k in range(s_lo, s_hi) if not (pc[k, 3] >> 24) & PF_LONG]
+                p0, p1 = lly[L, 0], lly[L + 1, 0]
+                o0, o1, h0, h1 = lly[L, 1], lly[L + 1, 1], lly[L, 2], lly[L + 1, 2]
+                assert p1 - p0 == len(want)
+                for j, k in enumerate(want):
+                    c = lpc[p0 + j]
+                    assert c[0] == pc[k, 0] and c[3] == pc[k, 3]
+                    ne = (lpc[p0 + j + 1, 2] if j + 1 < len(want) else o1) - c[2]
+                    assert ne == pc[k + 1, 2] - pc[k, 2]
+                    assert (hb.lops[c[2]:c[2] + ne] == hb.ops[pc[k, 2]:pc[k + 1, 2]]).all()
+                    ln = int(c[3] & 0xFFFFFF)
+                    if ln:
+                        a = _codes(hb.bq, hb.bx, 16 * int(pc[k, 1]), ln)
+                        b = _codes(hb.lbq, hb.lbx, 16 * int(c[1]), ln)
+                        assert (a == b).all()
+                recs = np.zeros(len(lo), dtype=np.int64)
+                for s_i, (s_lo, s_hi) in enumerate(zip(lo, hi)):
+                    recs[s_i] = sum(pc[k + 1, 2] - pc[k, 2] for k in range(s_lo, s_hi) if not (pc[k, 3] >> 24) & PF_LONG)
+                qa, nq = h0 >> 1, ((h1 + 1) >> 1) + 1 - (h0 >> 1)
+                assert p1 - p0 <= CHUNK_PIECES and o1 - o0 == recs.sum() <= CHUNK_RECS
+                assert _region(4 * (o1 - o0), 4 * (o0 & 3)) <= CHUNK_OBYTES
+                assert _region(8 * nq, 8 * (qa & 1)) <= CHUNK_QBYTES and _region(4 * nq, 4 * (qa & 3)) <= CHUNK_XBYTES
+                for W in range(W0, W1):
+                    a = max(W - K, S0) - S0
+                    assert recs[a:W - S0 + 1].sum() <= CHUNK_LANE_RECS * G
         items = [it for it in hb.items.astype(np.int64) if it[0] == t]
         for _, _, l0, l1 in items:
             lo0, _ = lays[l0]
@@ -283,6 +303,12 @@ def check_layers(hb):
             for W in range(W0, W1):
                 a = max(W - K, S0) - S0
                 assert rec[a:W - S0 + 1].sum() <= ITEM_RECS
+
+
+def _codes(bq, bx, q, n):
+    idx = np.arange(q, q + n, dtype=np.int64)
+    w, sh = idx >> 5, (idx & 31).astype(np.uint32)
+    return ((bx[w] >> sh) & 1) << 2 | ((bq[w, 1] >> sh) & 1) << 1 | ((bq[w, 0] >> sh) & 1)
 
 
 def check_plan_shard(sub):

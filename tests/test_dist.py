@@ -177,6 +177,17 @@ def test_distributed_parse_matches_reference(world, block, tmp_path):
     cases += [(big, a) for a in ([], ["-c", "0.25,0.75"], ["-d", "9"])]
     want = [(c["status"], c["files"]) for c in kat]
     want += [("ok", o.run_case(big, a)["files"]) for a in ([], ["-c", "0.25,0.75"], ["-d", "9"])]
+    # '@' lines in the body (skipped by the read pass, :195; never references): every block
+    # boundary of the small block size falls on one of them somewhere
+    body = []
+    for k in range(40):
+        body.append("r%d\t0\tg1\t%d\t60\t6M\t*\t0\t0\tACGTAC\t*\n" % (k, 1 + k % 20))
+        if k % 3 == 1:
+            body.append("@SQ\tSN:zz%d\tLN:9\n" % k if k % 2 else "@CO\tcomment %d\n" % k)
+    at_body = "@HD\tVN:1.0\n@SQ\tSN:g1\tLN:30\n" + "".join(body)
+    cases.append((at_body, []))
+    ref = o.run_case(at_body, [])
+    want.append((ref["status"], ref["files"]))
     paths = []
     for ext in (".sam", ".sam.gz"):   # (.sam.gz: BGZF, each rank inflates its own blocks)
         p = str(tmp_path / ("c2s" + ext))

@@ -118,6 +118,32 @@ def test_config_fasta_byte_identical_to_reference(name):
             assert tot < hb.info.aligned_bases
 
 
+def test_c3_samgz_bgzf_reduced_matches_oracle(tmp_path):
+    """C3's record order and compression at 1/20 scale (250 kb x 1000x, 1.67 M reads): the
+    .sam.gz is BGZF, so the CLI's parser inflates it block-parallel; the FASTA equals the C
+    restatement's on the same file (the full-size golden: test_config_fasta_..., c3)."""
+    import subprocess
+    from sam2consensus_amd import configs
+    from sam2consensus_amd.cli import main
+    gz = str(tmp_path / "c3r.sam.gz")
+    configs.synth_write("c3", gz, scale=0.05)
+    with open(gz, "rb") as fh:
+        h = fh.read(18)
+    assert h[:4] == b"\x1f\x8b\x08\x04" and h[12:14] == b"BC", "expected a BGZF member"
+    args = configs.cli_args("c3")
+    out = tmp_path / "out"
+    assert main(["-i", gz, "-o", str(out), "-p", "c3r"] + args) == 0
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-s", "-C", os.path.join(root, "oracle")], check=True)
+    ref = tmp_path / "ref"
+    r = subprocess.run([os.path.join(root, "oracle", "build", "s2c_oracle_mc"), "16", "-i", gz, "-o", str(ref),
+                        "-p", "c3r"] + args, capture_output=True, text=True, timeout=300)
+    assert "status: ok" in r.stdout, r.stdout[-500:]
+    assert sorted(os.listdir(out)) == sorted(os.listdir(ref))
+    for fn in os.listdir(ref):
+        assert open(os.path.join(out, fn), "rb").read() == open(os.path.join(ref, fn), "rb").read()
+
+
 def test_cli_end_to_end_c1(tmp_path):
     from sam2consensus_amd import configs
     from sam2consensus_amd.cli import main
@@ -201,9 +227,11 @@ def test_repeated_runs_identical():
         assert (a[0] == b[0]).all() and (a[1] == b[1]).all() and a[2] == b[2]
 
 
-@pytest.mark.parametrize("name,world", [("c1", 4), ("c2", 3), ("c5", 2)])
+@pytest.mark.parametrize("name,world", [("c1", 4), ("c2", 3), ("c5", 2), ("c3", 8), ("c4", 8)])
 def test_sharded_on_device_matches_golden(name, world):
-    """Tile-range shards (s2c_batch_shard) run through libs2c.so, merged == the reference."""
+    """Tile-range shards (s2c_batch_shard) run through libs2c.so, merged == the reference.
+    C3 and C4 split 8 ways as BASELINE.json runs them: deep and layered tiles cut by shard
+    boundaries (each shard re-lays its pieces and layered windows)."""
     from sam2consensus_amd import configs, shard
     from sam2consensus_amd.engine import DeviceBatch, Workspace
     g = CONFIGS[name]
@@ -357,8 +385,14 @@ def test_device_pipeline_equals_batch_model(name, over, thr, md, fill):
         assert (st == want[0]).all()
         assert (offs == want[1]).all()
         assert out == want[2], _first_diff(out, want[2])
-    if ref["status"] == "ok" and fill:
-        from sam2consensus_amd.records import build_records, render
+    # the reference's files, or its exception class (:367 KeyError for thresholds that select
+    # no symbol or ACGNT, :395 ZeroDivisionError for an empty record)
+    import builtins
+    from sam2consensus_amd.records import build_records, render
+    if ref["status"] == "ok":
         recs = build_records(hb, thr, "case", st, offs, out)
         got = {n + "__case.fasta": render(r, 0).decode("latin-1") for n, r in recs.items()}
         assert got == ref["files"]
+    else:
+        with pytest.raises(getattr(builtins, ref["status"])):
+            build_records(hb, thr, "case", st, offs, out)
