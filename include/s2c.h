@@ -288,6 +288,10 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
     const uint32_t *lbx;       /* [n_lqwords] */
 } s2c_batch_arrays;
 
+/* Build the batch's layered windows (s2c_batch_arrays lly .. lbx, tile word 20) if not yet
+ * built: required before a batch's arrays go to the device; snapshots that are only cut into
+ * shards never pay for them (each shard builds its own). */
+int  s2c_batch_layers(s2c_batch *b);
 int  s2c_batch_info_get(const s2c_batch *b, s2c_batch_info *out);
 int  s2c_batch_arrays_get(const s2c_batch *b, s2c_batch_arrays *out);
 /* The sub-batch of tiles [t0, t1) for one GPU of a multi-GPU run (positions keep their

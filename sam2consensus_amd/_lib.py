@@ -109,7 +109,7 @@ EXPORTS = [
     "s2c_parser_retain_events", "s2c_accumulate",
     "s2c_parser_pos_weights", "s2c_parser_checks", "s2c_parser_counters", "s2c_parser_pack",
     "s2c_parser_blob_copy", "s2c_parser_unpack",
-    "s2c_batch_info_get", "s2c_batch_arrays_get", "s2c_batch_ref_name", "s2c_batch_free", "s2c_batch_shard",
+    "s2c_batch_layers", "s2c_batch_info_get", "s2c_batch_arrays_get", "s2c_batch_ref_name", "s2c_batch_free", "s2c_batch_shard",
     "s2c_parsecigar", "s2c_synth_feed", "s2c_synth_write",
     "s2c_workspace_sizes", "s2c_reads", "s2c_pileup", "s2c_consensus", "s2c_run", "s2c_pileup_counts",
 ]
@@ -147,6 +147,7 @@ def _load():
         "s2c_parser_pack": (C.c_int, [_VP, C.c_int64, C.c_int64, C.POINTER(C.c_size_t)]),
         "s2c_parser_blob_copy": (C.c_int, [_VP, _VP, C.c_size_t]),
         "s2c_parser_unpack": (C.c_int, [_VP, _VP, C.c_size_t]),
+        "s2c_batch_layers": (C.c_int, [_VP]),
         "s2c_batch_info_get": (C.c_int, [_VP, C.POINTER(BatchInfo)]),
         "s2c_batch_arrays_get": (C.c_int, [_VP, C.POINTER(BatchArrays)]),
         "s2c_batch_ref_name": (C.c_char_p, [_VP, C.c_int64]),

@@ -77,12 +77,7 @@ class HostBatch:
         self.bx = _view(a.bx, i.n_qwords, np.uint32)
         self.rs = _view(a.rs, i.n_words + 1, np.uint32)
         self.ps = _view(a.ps, i.n_words + 1, np.uint32)
-        # layered windows of the tiles k_tile does not read in place
-        self.lly = _view(a.lly, 4 * (i.n_layers + 1), np.uint32).reshape(-1, 4)
-        self.lpc = _view(a.lpc, 4 * (i.n_lpieces + 1), np.uint32).reshape(-1, 4)
-        self.lops = _view(a.lops, max(i.n_lops, 4), np.uint32)
-        self.lbq = _view(a.lbq, 2 * i.n_lqwords, np.uint32).reshape(-1, 2)
-        self.lbx = _view(a.lbx, i.n_lqwords, np.uint32)
+        self._layers = False
         # tile plan
         self.tiles = _view(a.tiles, i.n_tiles * L.S2C_TILE_WORDS, np.uint32).reshape(-1, L.S2C_TILE_WORDS)
         self.items = _view(a.items, i.n_items * L.S2C_ITEM_WORDS, np.uint32).reshape(-1, L.S2C_ITEM_WORDS)
@@ -97,6 +92,24 @@ class HostBatch:
             np.zeros(i.n_refs, dtype=np.int64)
         self.ref_nblocks = nb.astype(np.int64)
         self.ref_first_block = (np.cumsum(nb) - nb).astype(np.int64)
+
+    def ensure_layers(self):
+        """Build the layered windows of the tiles k_tile does not read in place
+        (s2c_batch_layers; before the arrays go to the device) and view them."""
+        if self._layers:
+            return self
+        L.check(lib.s2c_batch_layers(self._b))
+        L.check(lib.s2c_batch_info_get(self._b, C.byref(self.info)))
+        a = L.BatchArrays()
+        L.check(lib.s2c_batch_arrays_get(self._b, C.byref(a)))
+        i = self.info
+        self.lly = _view(a.lly, 4 * (i.n_layers + 1), np.uint32).reshape(-1, 4)
+        self.lpc = _view(a.lpc, 4 * (i.n_lpieces + 1), np.uint32).reshape(-1, 4)
+        self.lops = _view(a.lops, max(i.n_lops, 4), np.uint32)
+        self.lbq = _view(a.lbq, 2 * i.n_lqwords, np.uint32).reshape(-1, 2)
+        self.lbx = _view(a.lbx, i.n_lqwords, np.uint32)
+        self._layers = True
+        return self
 
     @property
     def blocks(self):

@@ -228,6 +228,7 @@ struct s2c_batch {
     std::vector<int64_t> ref_len, ref_off, ref_reads;
     std::vector<uint32_t> pc, ops, bq, bx, rs, tiles, items, dense, deep, lp, wtile, rlist, ps;
     std::vector<uint32_t> lly, lpc, lops, lbq, lbx;   // layered windows of the non-dense tiles
+    bool layers = false;                               // built (s2c_batch_layers)
     std::vector<uint32_t> kmin, kmax;   // host only: global key range of each piece's insertion events
 };
 
@@ -1961,7 +1962,6 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     I.n_lng = (int64_t)loff;
     I.n_cols = (int64_t)coff;
     I.runs_max = runs_max;
-    build_layers(b, PB, G);
     mark_runs(b);
     *out = guard.release();
     return S2C_OK;
@@ -2133,13 +2133,8 @@ static int s2c_batch_shard_impl(const s2c_batch *b, int64_t t0, int64_t t1, s2c_
         if (!dense_fits(tw, K)) return s2c_set_error(S2C_ERR_LIMIT, "shard window beyond the dense kernel's LDS");
         J.dense_lds = std::max<int64_t>(J.dense_lds, dense_bytes(tw, K));
     }
-    {   // the shard's own layered windows (its pieces are re-laid)
-        int64_t nwp = 8;
-        while (nwp * 32 < J.tile_max) nwp *= 2;
-        PieceBlocks PB;
-        piece_blocks(s.get(), PB);
-        build_layers(s.get(), PB, 256 / nwp);
-    }
+    // (the shard's own layered windows are built on first use: s2c_batch_layers)
+    J.n_layers = J.n_lpieces = J.n_lops = J.n_lqwords = 0;
     mark_runs(s.get());
     // the shard's share of the workload's aligned bases (by its positions; for reporting)
     J.aligned_bases = I.total_len ? (int64_t)((double)I.aligned_bases * (double)aligned / (double)I.total_len) : 0;
@@ -2148,6 +2143,21 @@ static int s2c_batch_shard_impl(const s2c_batch *b, int64_t t0, int64_t t1, s2c_
 }
 extern "C" int s2c_batch_shard(const s2c_batch *b, int64_t t0, int64_t t1, s2c_batch **out) {
     return s2c_guarded([&] { return s2c_batch_shard_impl(b, t0, t1, out); });
+}
+
+static int s2c_batch_layers_impl(s2c_batch *b) {
+    if (!b) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
+    if (b->layers) return S2C_OK;
+    int64_t nwp = 8;
+    while (nwp * 32 < b->info.tile_max) nwp *= 2;
+    PieceBlocks PB;
+    piece_blocks(b, PB);
+    build_layers(b, PB, 256 / nwp);
+    b->layers = true;
+    return S2C_OK;
+}
+extern "C" int s2c_batch_layers(s2c_batch *b) {
+    return s2c_guarded([&] { return s2c_batch_layers_impl(b); });
 }
 
 extern "C" int s2c_batch_info_get(const s2c_batch *b, s2c_batch_info *out) {

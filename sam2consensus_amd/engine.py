@@ -49,7 +49,7 @@ class DeviceBatch:
 
     def __init__(self, hb, device=None):
         self.device = _dev(device)
-        self.hb = hb
+        self.hb = hb.ensure_layers()
         self.info = hb.info
         for name in self.ARRAYS:
             setattr(self, name, _up(np.asarray(getattr(hb, name)).reshape(-1), self.device))
