@@ -306,15 +306,17 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms,
             "higher_is_better": True,
-            "scaling": "strong" if sharded else "weak",
+            "scaling": "weak" if args.independent else "strong",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic",
             "config": {"workload": WORKLOADS[wl], "aligned_bases_per_gpu": info.aligned_bases,
                        "reads_per_gpu": info.reads_mapped, "positions_per_gpu": info.total_len,
                        "thresholds": thresholds,
-                       "parallelism": ("one workload split into contiguous tile ranges per GPU" if sharded else
-                                       "one batch per GPU, independent workloads (no collective on the data path)")},
+                       "parallelism": ("one batch per GPU, independent workloads (no collective on the data path)"
+                                       if args.independent else
+                                       "one workload split into contiguous tile ranges per GPU (N=1: the whole "
+                                       "workload); shard bodies and stats gathered to rank 0")},
         }
         if kern:
             tile_ms = kern["k_tile"]
@@ -327,6 +329,7 @@ def main():
             line["roofline"] = {
                 "bound": bound.get("bound", "hbm"), "bound_evidence": bound.get("evidence"), "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic.get("bytes") if traffic else None,
+                "traffic_range": traffic.get("range") if traffic else None,
                 "traffic_frac": (traffic["bytes"] / (tile_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS) if traffic else None,
                 "kernel": "s2c_pileup = k_tile_dense + k_tile (CIGAR walk of dense tiles, pileup, insertion "
                           "columns, vote, FASTA bytes); time from HIP events around the stage in every timed step",
@@ -403,7 +406,8 @@ def traffic_from_profile(wl):
             t = json.load(fh)
         b = t.get("tile_hbm_bytes_per_launch")
         if b:
-            return {"bytes": b, "source": "profiles/traffic_%s.json (%s)" % (wl, t.get("round", ""))}
+            return {"bytes": b, "range": t.get("tile_hbm_bytes_range"),
+                    "source": "profiles/traffic_%s.json (%s)" % (wl, t.get("round", ""))}
     return None
 
 

@@ -39,13 +39,21 @@ def main():
         kernels[k] = {"fetch_kib_raw": f_raw, "write_kib_raw": w_raw,
                       "hbm_bytes_per_launch": (2.0 * f_raw + w_raw) * 1024.0}
     # the pileup stage of one step: k_tile_dense + k_tile (+ k_prep), summed per launch
-    pile = sum(v["hbm_bytes_per_launch"] for k, v in kernels.items()
-               if k.split("<")[0] in ("s2c::k_tile_dense", "s2c::k_tile", "s2c::k_prep"))
+    tile = [v for k, v in kernels.items() if k.split("<")[0] in ("s2c::k_tile_dense", "s2c::k_tile", "s2c::k_prep")]
+    pile = sum(v["hbm_bytes_per_launch"] for v in tile)
+    # the ×2 holds for wide (16 B/lane) streaming reads only: the tile kernels read their
+    # windows with buffer_load_dwordx4 … lds (wide) but their descriptors, piece lists and
+    # HBM count rows with narrower loads, so the true bytes lie between the raw counter
+    # (all reads narrow) and the doubled one (all reads wide); the doubled one is reported
+    lo = sum((v["fetch_kib_raw"] + v["write_kib_raw"]) * 1024.0 for v in tile)
     out = {"workload": wl, "round": tag, "kernels": kernels,
            "tile_hbm_bytes_per_launch": pile or None,
+           "tile_hbm_bytes_range": [lo, pile] if pile else None,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (scripts/pmc.sh); "
                      "bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 per dispatch, averaged; the x2 is the gfx950 "
-                     "read correction of MI355X_MICROARCH.md; WRITE_SIZE is uncalibrated for byte stores/atomics. "
+                     "read correction of MI355X_MICROARCH.md for wide 16-B/lane reads (the window DMAs); "
+                     "the tile kernels' narrower reads (descriptors, piece lists, count rows) make the "
+                     "true figure lie in tile_hbm_bytes_range = [raw, doubled]; WRITE_SIZE is uncalibrated for byte stores/atomics. "
                      "Infinity Cache hits are included (a batch below 256 MiB, e.g. C2, is largely served from it)."}
     dst = os.path.join(ROOT, "profiles", "traffic_%s.json" % wl)
     with open(dst, "w") as fh:
