@@ -467,8 +467,9 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         const uint32_t fl = P.w >> 24, slen = P.w & 0xFFFFFFu, j = P.z - o0;
         const uint32_t op = w0 & 15u, l = w0 >> 4;
         const bool xf = (fl & S2C_PF_X) != 0;
-        // (no maxdel count to take: the rule is off, or SEQ holds no '-')
-        const bool plain = in && (fl & ~(uint32_t)(S2C_PF_X | S2C_PF_DASH)) == 0u && op_bases(op) &&
+        // (no maxdel count to take: the rule is off, or SEQ holds no '-'; S2C_PF_SIMPLE marks the
+        // one-token pieces, whose length field already holds take)
+        const bool plain = in && (fl & ~(uint32_t)(S2C_PF_X | S2C_PF_DASH | S2C_PF_SIMPLE)) == 0u && op_bases(op) &&
                            !((fl & S2C_PF_DASH) && mda);
         const uint32_t nops = oend - P.z;
         // one M / = / X token and nothing else: seqout = SEQ[0 : min(l, len(SEQ))] (:64-69)
