@@ -17,10 +17,12 @@
 // needs the seqout length, the '-' count and the counted range) and to size the plan.
 #include "../../include/s2c.h"
 
+#include <sys/mman.h>
 #include <zlib.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -140,7 +142,8 @@ inline bool op_dash(uint32_t op) { return op == S2C_OP_D || op == S2C_OP_N || op
 // re.findall(r"(\d+)([MIDNSHPX=]{1})", cigar) (:58): a match is a maximal digit run
 // immediately followed by an op letter; everything else is skipped.  Appends token words
 // (len << 4 | opcode).
-int tokenize_cigar(const char *s, size_t n, std::vector<uint32_t> &out, uint32_t *ntok) {
+template <class V>
+int tokenize_cigar(const char *s, size_t n, V &out, uint32_t *ntok) {
     size_t i = 0;
     uint32_t k = 0;
     while (i < n) {
@@ -170,6 +173,49 @@ int tokenize_cigar(const char *s, size_t n, std::vector<uint32_t> &out, uint32_t
 }
 }  // namespace
 
+// Allocator of the parser's and the batch's big arrays: default-initialising (resize() leaves
+// the elements unwritten, so they are first touched by the threads that fill them, not by a
+// serial zero-fill) and, from 4 MB on, backed by 2 MB-aligned anonymous mappings advised
+// as transparent huge pages (512x fewer page faults for the GB-sized arrays of a batch).
+constexpr size_t HUGE_MIN = (size_t)4 << 20, HUGE_PAGE = (size_t)2 << 20;
+inline bool huge_pages() {   // S2C_HUGEPAGES=0 turns the advice off
+    static const bool on = [] { const char *e = getenv("S2C_HUGEPAGES"); return !e || atoi(e) != 0; }();
+    return on;
+}
+template <class T>
+struct uninit_alloc {
+    using value_type = T;
+    template <class U> struct rebind { using other = uninit_alloc<U>; };
+    uninit_alloc() = default;
+    template <class U> uninit_alloc(const uninit_alloc<U> &) {}
+    static size_t map_len(size_t bytes) { return (bytes + HUGE_PAGE - 1) & ~(HUGE_PAGE - 1); }
+    T *allocate(size_t n) {
+        const size_t bytes = n * sizeof(T);
+        if (bytes < HUGE_MIN) {
+            void *q = ::operator new(bytes);
+            return (T *)q;
+        }
+        const size_t len = map_len(bytes);
+        void *raw = mmap(nullptr, len + HUGE_PAGE, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (raw == MAP_FAILED) throw std::bad_alloc();
+        const uintptr_t r = (uintptr_t)raw, a = (r + HUGE_PAGE - 1) & ~(uintptr_t)(HUGE_PAGE - 1);
+        if (a > r) munmap(raw, a - r);                                      // the unaligned head
+        if (r + len + HUGE_PAGE > a + len) munmap((void *)(a + len), r + len + HUGE_PAGE - (a + len));   // and tail
+        if (huge_pages()) madvise((void *)a, len, MADV_HUGEPAGE);
+        return (T *)a;
+    }
+    void deallocate(T *q, size_t n) {
+        const size_t bytes = n * sizeof(T);
+        if (bytes < HUGE_MIN) ::operator delete((void *)q);
+        else munmap((void *)q, map_len(bytes));
+    }
+    template <class U> void construct(U *q) noexcept { ::new ((void *)q) U; }
+    template <class U, class... A> void construct(U *q, A &&...a) { ::new ((void *)q) U(std::forward<A>(a)...); }
+    template <class U> bool operator==(const uninit_alloc<U> &) const { return true; }
+    template <class U> bool operator!=(const uninit_alloc<U> &) const { return false; }
+};
+using u32buf = std::vector<uint32_t, uninit_alloc<uint32_t>>;
+
 // ------------------------------------------------------------------ parser state
 // One mapped read as the parser keeps it (file order).  Its tokens, base planes and
 // insertion events live in the parse chunk that read it.
@@ -188,13 +234,13 @@ struct Event {              // insertion with a non-empty motif (:73-75), file o
     uint32_t ref, len, read;
 };
 struct Chunk {
-    std::vector<ReadRec> reads;
-    std::vector<uint32_t> toks;
-    std::vector<uint32_t> bq, bx;   // planes [k][2] and [k]; bases [0, nq)
+    std::vector<ReadRec, uninit_alloc<ReadRec>> reads;
+    u32buf toks;
+    u32buf bq, bx;   // planes [k][2] and [k]; bases [0, nq)
     uint64_t nq = 0;
     std::vector<Event> ev;
     int64_t lines_total = 0, reads_mapped = 0, aligned = 0, qbases = 0, ntokens = 0;
-    std::vector<uint8_t> scratch;   // SEQ codes of the current read
+    std::vector<uint32_t> sp;       // the current read's SEQ planes (seq_planes: 4 words per 32 chars)
 };
 
 struct s2c_parser {
@@ -226,10 +272,11 @@ struct s2c_batch {
     s2c_batch_info info{};
     std::vector<std::string> names;
     std::vector<int64_t> ref_len, ref_off, ref_reads;
-    std::vector<uint32_t> pc, ops, bq, bx, rs, tiles, items, dense, deep, lp, wtile, rlist, ps;
+    u32buf pc, ops, bq, bx;   // filled entirely by the emitters (resize: no zero-fill)
+    std::vector<uint32_t> rs, tiles, items, dense, deep, lp, wtile, rlist, ps;
     std::vector<uint32_t> lly, lpc, lops, lbq, lbx;   // layered windows of the non-dense tiles
     bool layers = false;                               // built (s2c_batch_layers)
-    std::vector<uint32_t> kmin, kmax;   // host only: global key range of each piece's insertion events
+    u32buf kmin, kmax;   // host only: global key range of each piece's insertion events
 };
 
 static int perr(s2c_parser *p, int code, const std::string &msg) {
@@ -283,9 +330,74 @@ struct RefView {
     int64_t maxdel;
 };
 
-// SEQ → planes at a 16-base boundary of the chunk; returns the first base index.
-// *has_x: bit 0 = a non-ACGT char, bit 1 = a '-' char (x = 1, p1 = 0, p0 = 1)
-static uint64_t pack_seq(Chunk &c, const char *seq, size_t slen, uint8_t *has_x) {
+// SEQ → bit planes, 32 chars per word group {p0, p1, x, bad} (bit j = char 32·w + j; the QL
+// code's bits x·4 + p1·2 + p0, and bad = a char outside "-ACGNT"); bits past slen are zero.
+static void seq_planes_scalar(const char *seq, size_t slen, uint32_t *o) {
+    for (size_t w = 0; w * 32 < slen; w++) {
+        const size_t m = std::min<size_t>(slen - 32 * w, 32);
+        uint32_t p0 = 0, p1 = 0, x = 0, bad = 0;
+        for (size_t j = 0; j < m; j++) {
+            const uint32_t v = QL.v[(uint8_t)seq[32 * w + j]];
+            p0 |= (v & 1u) << j;
+            p1 |= ((v >> 1) & 1u) << j;
+            x |= ((v >> 2) & 1u) << j;
+            bad |= (v == Q_BAD ? 1u : 0u) << j;
+        }
+        o[4 * w] = p0; o[4 * w + 1] = p1; o[4 * w + 2] = x; o[4 * w + 3] = bad;
+    }
+}
+#if defined(__x86_64__)
+#include <immintrin.h>
+__attribute__((target("avx2"))) static void seq_planes_avx2(const char *seq, size_t slen, uint32_t *o) {
+    const __m256i A = _mm256_set1_epi8('A'), Cc = _mm256_set1_epi8('C'), Gg = _mm256_set1_epi8('G');
+    const __m256i Tt = _mm256_set1_epi8('T'), Nn = _mm256_set1_epi8('N'), Dd = _mm256_set1_epi8('-');
+    size_t w = 0;
+    for (; 32 * w + 32 <= slen; w++) {
+        const __m256i v = _mm256_loadu_si256((const __m256i *)(seq + 32 * w));
+        const uint32_t a = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, A));
+        const uint32_t c = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, Cc));
+        const uint32_t g = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, Gg));
+        const uint32_t t = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, Tt));
+        const uint32_t n = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, Nn));
+        const uint32_t d = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, Dd));
+        const uint32_t bad = ~(a | c | g | t | n | d);
+        o[4 * w] = c | t | d | bad;
+        o[4 * w + 1] = g | t | bad;
+        o[4 * w + 2] = n | d | bad;
+        o[4 * w + 3] = bad;
+    }
+    if (32 * w < slen) seq_planes_scalar(seq + 32 * w, slen - 32 * w, o + 4 * w);
+}
+static const bool HAVE_AVX2 = __builtin_cpu_supports("avx2");
+#endif
+static void seq_planes(const char *seq, size_t slen, uint32_t *o) {
+#if defined(__x86_64__)
+    if (HAVE_AVX2) return seq_planes_avx2(seq, slen, o);
+#endif
+    seq_planes_scalar(seq, slen, o);
+}
+// the set bits of plane word group k (0 p0, 1 p1, 2 x, 3 bad) in chars [a, b)
+static inline uint32_t plane_bits(const uint32_t *sp, int k, size_t a, size_t b, bool any) {
+    uint32_t tot = 0;
+    for (size_t w = a >> 5; w < ((b + 31) >> 5); w++) {
+        uint32_t m = k == 4 ? sp[4 * w + 2] & sp[4 * w] & ~sp[4 * w + 1] : sp[4 * w + k];   // 4: '-' chars
+        if (w == (a >> 5)) m &= ~0u << (a & 31);
+        if (w == ((b - 1) >> 5) && (b & 31)) m &= ~0u >> (32 - (b & 31));
+        if (any && m) return 1;
+        tot += (uint32_t)__builtin_popcount(m);
+    }
+    return tot;
+}
+// QL code of char i from the planes
+static inline uint8_t plane_code(const uint32_t *sp, size_t i) {
+    const size_t w = i >> 5, j = i & 31;
+    if ((sp[4 * w + 3] >> j) & 1u) return Q_BAD;
+    return (uint8_t)(((sp[4 * w] >> j) & 1u) | (((sp[4 * w + 1] >> j) & 1u) << 1) | (((sp[4 * w + 2] >> j) & 1u) << 2));
+}
+
+// The read's planes (seq_planes) → the chunk's planes at a 16-base boundary; returns the
+// first base index.  *has_x: bit 0 = a non-ACGT char, bit 1 = a '-' char (x = 1, p1 = 0, p0 = 1)
+static uint64_t pack_seq(Chunk &c, const uint32_t *sp, size_t slen, uint8_t *has_x) {
     const uint64_t q0 = (c.nq + 15) & ~(uint64_t)15;
     const uint64_t q1 = q0 + slen;
     const size_t need = (size_t)((q1 + 31) >> 5) + 1;
@@ -295,25 +407,20 @@ static uint64_t pack_seq(Chunk &c, const char *seq, size_t slen, uint8_t *has_x)
         c.bx.resize(cap, 0u);
     }
     uint8_t anyx = 0;
-    uint64_t b = q0;
-    size_t i = 0;
-    while (i < slen) {   // 32-base words (the first may start at bit 16)
-        const uint32_t sh = (uint32_t)(b & 31);
-        const size_t m = std::min<size_t>(slen - i, 32 - sh);
-        uint32_t p0 = 0, p1 = 0, x = 0;
-        for (size_t j = 0; j < m; j++) {
-            const uint32_t v = QL.v[(uint8_t)seq[i + j]];
-            p0 |= (v & 1u) << j;
-            p1 |= ((v >> 1) & 1u) << j;
-            x |= ((v >> 2) & 1u) << j;
-        }
-        const uint64_t w = b >> 5;
-        c.bq[2 * w] |= p0 << sh;
-        c.bq[2 * w + 1] |= p1 << sh;
-        c.bx[w] |= x << sh;
+    const uint32_t sh = (uint32_t)(q0 & 31);   // 0 or 16
+    const uint64_t w0 = q0 >> 5;
+    const size_t nw = (slen + 31) / 32;
+    for (size_t w = 0; w < nw; w++) {
+        const uint32_t p0 = sp[4 * w], p1 = sp[4 * w + 1], x = sp[4 * w + 2];
         anyx |= (x != 0 ? 1 : 0) | ((x & p0 & ~p1) != 0 ? 2 : 0);
-        b += m;
-        i += m;
+        c.bq[2 * (w0 + w)] |= p0 << sh;
+        c.bq[2 * (w0 + w) + 1] |= p1 << sh;
+        c.bx[w0 + w] |= x << sh;
+        if (sh) {
+            c.bq[2 * (w0 + w + 1)] |= p0 >> (32 - sh);
+            c.bq[2 * (w0 + w + 1) + 1] |= p1 >> (32 - sh);
+            c.bx[w0 + w + 1] |= x >> (32 - sh);
+        }
     }
     c.nq = q1;
     *has_x = anyx;
@@ -371,9 +478,9 @@ static int process_record(Chunk &c, const RefView &rv, std::string &last_name, i
 
     // ---- the token walk of parsecigar (:64-81): seqout length, its '-' count, the codes of
     //      the bases it takes (validated below), insertion events with non-empty motifs ----
-    std::vector<uint8_t> &codes = c.scratch;   // codes of SEQ chars (query order)
-    codes.resize((size_t)slen);
-    for (int64_t j = 0; j < slen; j++) codes[j] = QL.v[(uint8_t)seq[j]];
+    std::vector<uint32_t> &sp = c.sp;   // SEQ planes (query order)
+    if (sp.size() < 4 * (size_t)((slen + 31) / 32)) sp.resize(4 * (size_t)((slen + 31) / 32) + 64);
+    seq_planes(seq, (size_t)slen, sp.data());
     int64_t start = 0, start_ref = pos0, klen = 0, dashes = 0, mb = 0;
     bool any_bad = false;
     const uint32_t ev0 = (uint32_t)c.ev.size();
@@ -383,9 +490,9 @@ static int process_record(Chunk &c, const RefView &rv, std::string &last_name, i
         const int64_t l = (int64_t)(w >> 4);
         if (op_bases(op)) {
             const int64_t take = start < slen ? std::min(l, slen - start) : 0;
-            for (int64_t j = start; j < start + take; j++) {
-                dashes += codes[j] == Q_DASH;
-                any_bad |= codes[j] == Q_BAD;
+            if (take > 0) {
+                dashes += plane_bits(sp.data(), 4, (size_t)start, (size_t)(start + take), false);
+                any_bad |= plane_bits(sp.data(), 3, (size_t)start, (size_t)(start + take), true) != 0;
             }
             klen += take;
             mb += take;
@@ -429,7 +536,7 @@ static int process_record(Chunk &c, const RefView &rv, std::string &last_name, i
             if (op_bases(op)) { take = st < slen ? std::min(l, slen - st) : 0; bases = true; }
             else if (op_dash(op)) take = l;
             for (int64_t j = 0; j < take; j++, k++) {
-                const uint8_t cd = bases ? codes[st + j] : Q_DASH;
+                const uint8_t cd = bases ? plane_code(sp.data(), (size_t)(st + j)) : Q_DASH;
                 if (drop && cd == Q_DASH) continue;            // '-' skipped (:216)
                 const int64_t pp = pos0 + k;
                 if (pp < -L || pp >= L) return fail(S2C_ERR_INDEX, "IndexError: list index out of range (:212)");
@@ -457,7 +564,7 @@ static int process_record(Chunk &c, const RefView &rv, std::string &last_name, i
     r.nev = nev;
     r.drop = drop;
     if (kc0 >= 0 || nev > 0) {
-        r.q = pack_seq(c, seq, (size_t)slen, &r.has_x);
+        r.q = pack_seq(c, sp.data(), (size_t)slen, &r.has_x);
         for (uint32_t e = ev0; e < ev0 + nev; e++) c.ev[e].q += r.q;
     } else {
         r.q = 0;
@@ -604,8 +711,10 @@ int parse_window(s2c_parser *p, const char *s, size_t n) {
         int64_t last_ref = -1;
         const char *b = s + cut[k];
         const size_t m = cut[k + 1] - cut[k];
-        c.reads.reserve(m / 256);
-        c.toks.reserve(m / 200);
+        c.reads.reserve(m / 150 + 16);   // (SAM lines of ≥ 150 bytes: no regrowth for typical reads)
+        c.toks.reserve(m / 100 + 16);
+        c.bx.resize(m / 32 + 64, 0u);     // SEQ bytes ≤ m: planes of ≤ m bases, 16-base aligned reads
+        c.bq.resize(2 * c.bx.size(), 0u);
         size_t j = 0;
         while (j < m) {
             const char *nl = (const char *)memchr(b + j, '\n', m - j);
@@ -951,7 +1060,26 @@ struct Piece {
     uint8_t range, ins, lng;
     uint32_t nslots;        // prefix words + tokens
     uint32_t kmin, kmax;    // global keys of the insertion events it emits (ins)
+    uint32_t qlen;          // plane bases: len(SEQ) rounded up to 16
+    uint32_t ref;           // reference index
 };
+
+// Host threads of the plan: the parse's (≤ 16, S2C_PARSE_THREADS), at most n / grain.
+static int plan_threads(int64_t n, int64_t grain) {
+    unsigned hw = std::thread::hardware_concurrency();
+    int nt = (int)std::min<unsigned>(hw ? hw : 1, 16);
+    if (const char *e = getenv("S2C_PARSE_THREADS")) nt = std::max(1, std::min(64, atoi(e)));
+    return (int)std::max<int64_t>(1, std::min<int64_t>(nt, n / std::max<int64_t>(grain, 1)));
+}
+// f(t, i0, i1) on nt contiguous ranges of [0, n), thread t on range t
+template <class F>
+static void par_ranges(int nt, int64_t n, F &&f) {
+    if (nt <= 1) { f(0, (int64_t)0, n); return; }
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; t++) th.emplace_back([&f, t, nt, n] { f(t, n * t / nt, n * (t + 1) / nt); });
+    f(0, (int64_t)0, n / nt);
+    for (auto &x : th) x.join();
+}
 }  // namespace
 
 // The window of tile [a, b): the short pieces starting in words [a/32 - K, ceil(b/32)) — a
@@ -960,6 +1088,7 @@ struct Piece {
 static void tile_window(const s2c_batch *b, int64_t K, uint64_t a, uint64_t e, uint32_t *tw) {
     const int64_t NP = b->info.n_pieces;
     auto piece_at_word = [&](int64_t w) {   // first piece with start word >= w
+        if ((int64_t)b->ps.size() == b->info.n_words + 1 && w <= b->info.n_words) return (int64_t)b->ps[w];
         int64_t lo = 0, hi = NP;
         while (lo < hi) {
             const int64_t m = (lo + hi) / 2;
@@ -1002,12 +1131,17 @@ static void mark_runs(s2c_batch *b) {
         need[lo] = 1;
     }
     b->rlist.clear();
-    for (int64_t k = 0; k < NP; k++) {
-        uint32_t &w3 = b->pc[4 * k + 3];
-        if (need[k]) w3 |= (uint32_t)S2C_PF_RUNS << 24;
-        else w3 &= ~((uint32_t)S2C_PF_RUNS << 24);
-        if (need[k] || ((w3 >> 24) & S2C_PF_INS)) b->rlist.push_back((uint32_t)k);
-    }
+    const int nt = plan_threads(NP, 1 << 18);
+    std::vector<std::vector<uint32_t>> rl(nt);
+    par_ranges(nt, NP, [&](int t, int64_t k0, int64_t k1) {
+        for (int64_t k = k0; k < k1; k++) {
+            uint32_t &w3 = b->pc[4 * k + 3];
+            if (need[k]) w3 |= (uint32_t)S2C_PF_RUNS << 24;
+            else w3 &= ~((uint32_t)S2C_PF_RUNS << 24);
+            if (need[k] || ((w3 >> 24) & S2C_PF_INS)) rl[t].push_back((uint32_t)k);
+        }
+    });
+    for (int t = 0; t < nt; t++) b->rlist.insert(b->rlist.end(), rl[t].begin(), rl[t].end());
     b->info.n_rlist = (int64_t)b->rlist.size();
     if (b->rlist.empty()) b->rlist.push_back(0);
 }
@@ -1026,16 +1160,28 @@ struct PieceBlocks {          // prefix sums over the sorted pieces (mod 2^32: d
 static inline uint32_t piece_half_words(uint32_t w3) { return ((w3 & 0xFFFFFFu) + 15u) / 16u; }
 static void piece_blocks(const s2c_batch *b, PieceBlocks &B) {
     const int64_t NP = b->info.n_pieces;
-    B.n.assign(NP + 1, 0);
-    B.h.assign(NP + 1, 0);
-    B.o.assign(NP + 1, 0);
-    for (int64_t k = 0; k < NP; k++) {
-        const uint32_t w3 = b->pc[4 * k + 3];
-        const bool sh = !((w3 >> 24) & S2C_PF_LONG);
-        B.n[k + 1] = B.n[k] + (sh ? 1u : 0u);
-        B.h[k + 1] = B.h[k] + (sh ? piece_half_words(w3) : 0u);
-        B.o[k + 1] = B.o[k] + (sh ? b->pc[4 * k + 6] - b->pc[4 * k + 2] : 0u);
-    }
+    B.n.resize(NP + 1);
+    B.h.resize(NP + 1);
+    B.o.resize(NP + 1);
+    B.n[0] = B.h[0] = B.o[0] = 0;
+    const int nt = plan_threads(NP, 1 << 18);
+    std::vector<uint32_t> sn(nt + 1, 0), sh(nt + 1, 0), so(nt + 1, 0);
+    par_ranges(nt, NP, [&](int t, int64_t k0, int64_t k1) {   // range sums (mod 2^32) ...
+        uint32_t n = 0, h = 0, o = 0;
+        for (int64_t k = k0; k < k1; k++) {
+            const uint32_t w3 = b->pc[4 * k + 3];
+            const bool s = !((w3 >> 24) & S2C_PF_LONG);
+            n += s ? 1u : 0u;
+            h += s ? piece_half_words(w3) : 0u;
+            o += s ? b->pc[4 * k + 6] - b->pc[4 * k + 2] : 0u;
+            B.n[k + 1] = n; B.h[k + 1] = h; B.o[k + 1] = o;
+        }
+        sn[t + 1] = n; sh[t + 1] = h; so[t + 1] = o;
+    });
+    for (int t = 0; t < nt; t++) { sn[t + 1] += sn[t]; sh[t + 1] += sh[t]; so[t + 1] += so[t]; }
+    par_ranges(nt, NP, [&](int t, int64_t k0, int64_t k1) {   // ... then each range from its base
+        for (int64_t k = k0; k < k1; k++) { B.n[k + 1] += sn[t]; B.h[k + 1] += sh[t]; B.o[k + 1] += so[t]; }
+    });
 }
 
 struct LayerSeg { uint64_t p0, n; };
@@ -1591,7 +1737,20 @@ extern "C" int s2c_parser_unpack(s2c_parser *p, const void *blob, size_t len) {
     return s2c_guarded([&] { return s2c_parser_unpack_impl(p, blob, len); });
 }
 
+// Opt-in phase clock of the host plan (S2C_HOST_TIMING=1: one line per phase on stderr).
+struct PhaseClock {
+    bool on = getenv("S2C_HOST_TIMING") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(const char *what) {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        fprintf(stderr, "[s2c host] %-18s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+        t = n;
+    }
+};
+
 static int build_batch(s2c_parser *p, s2c_batch **out) {
+    PhaseClock clk;
     const int64_t R = (int64_t)p->ref_names.size();
     auto &CH = p->chunks;
 
@@ -1606,6 +1765,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
         }
     }
 
+    clk.mark("checks");
     s2c_batch *b = new s2c_batch();
     std::unique_ptr<s2c_batch> guard(b);
     s2c_batch_info &I = b->info;
@@ -1635,44 +1795,85 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     }
 
     // ---- pieces: the counted range of each read, split at the POS<=0 wrap (:212), plus a
-    //      zero-span piece for a read whose insertion events have nothing counted ----
-    std::vector<Piece> pcs;
-    std::vector<int64_t> ref_span(R, 0);
-    for (uint32_t ci = 0; ci < (uint32_t)CH.size(); ci++) {
+    //      zero-span piece for a read whose insertion events have nothing counted; in file
+    //      order (chunk by chunk), counted and then written by the host threads ----
+    const int64_t NC = (int64_t)CH.size();
+    // the pieces of read ri of chunk ci into dst (nullptr: count only); returns how many
+    auto read_pieces = [&](uint32_t ci, uint32_t ri, Piece *dst, int64_t *span, int64_t *nrd) -> int {
         const Chunk &c = *CH[ci];
-        for (uint32_t ri = 0; ri < (uint32_t)c.reads.size(); ri++) {
-            const ReadRec &r = c.reads[ri];
-            const int64_t L = p->ref_len[r.ref], off = b->ref_off[r.ref];
-            bool any_key = false;   // an event the consensus can emit (key >= 0)
-            uint64_t kmin = ~0ull, kmax = 0;
-            for (uint32_t e = r.ev0; e < r.ev0 + r.nev; e++)
-                if (c.ev[e].key >= 0) {
-                    any_key = true;
-                    kmin = std::min<uint64_t>(kmin, (uint64_t)(off + c.ev[e].key));
-                    kmax = std::max<uint64_t>(kmax, (uint64_t)(off + c.ev[e].key));
-                }
-            const size_t first = pcs.size();
-            if (r.kc0 >= 0) {
-                const int64_t pa = r.pos0 + r.kc0;
-                if (pa < 0) {
-                    const int64_t kb = std::min(r.kc1, -r.pos0);
-                    pcs.push_back({(uint64_t)(off + L + pa), r.kc0, kb, ci, ri, 1, 0, 0, 0, 0, 0});
-                    if (r.kc1 > -r.pos0) pcs.push_back({(uint64_t)off, -r.pos0, r.kc1, ci, ri, 1, 0, 0, 0, 0, 0});
-                } else {
-                    const bool whole = r.kc0 == 0 && r.kc1 == r.klen;
-                    pcs.push_back({(uint64_t)(off + pa), r.kc0, r.kc1, ci, ri, (uint8_t)!whole, 0, 0, 0, 0, 0});
-                }
-                b->ref_reads[r.ref] += (int64_t)(pcs.size() - first);
+        const ReadRec &r = c.reads[ri];
+        const int64_t L = p->ref_len[r.ref], off = b->ref_off[r.ref];
+        bool any_key = false;   // an event the consensus can emit (key >= 0)
+        uint64_t kmin = ~0ull, kmax = 0;
+        for (uint32_t e = r.ev0; e < r.ev0 + r.nev; e++)
+            if (c.ev[e].key >= 0) {
+                any_key = true;
+                kmin = std::min<uint64_t>(kmin, (uint64_t)(off + c.ev[e].key));
+                kmax = std::max<uint64_t>(kmax, (uint64_t)(off + c.ev[e].key));
             }
-            if (any_key) {   // (a read with events but nothing counted: a zero-span piece at its first key)
-                if (pcs.size() == first) pcs.push_back({kmin, 0, 0, ci, ri, 1, 0, 0, 0, 0, 0});
-                pcs[first].ins = 1;
-                pcs[first].kmin = (uint32_t)kmin;
-                pcs[first].kmax = (uint32_t)kmax;
+        Piece tmp[2];
+        int n = 0;
+        if (r.kc0 >= 0) {
+            const int64_t pa = r.pos0 + r.kc0;
+            if (pa < 0) {
+                const int64_t kb = std::min(r.kc1, -r.pos0);
+                tmp[n++] = {(uint64_t)(off + L + pa), r.kc0, kb, ci, ri, 1, 0, 0, 0, 0, 0, 0};
+                if (r.kc1 > -r.pos0) tmp[n++] = {(uint64_t)off, -r.pos0, r.kc1, ci, ri, 1, 0, 0, 0, 0, 0, 0};
+            } else {
+                const bool whole = r.kc0 == 0 && r.kc1 == r.klen;
+                tmp[n++] = {(uint64_t)(off + pa), r.kc0, r.kc1, ci, ri, (uint8_t)!whole, 0, 0, 0, 0, 0, 0};
             }
-            for (size_t k = first; k < pcs.size(); k++) ref_span[r.ref] += pcs[k].kb - pcs[k].ka;
+            nrd[r.ref] += n;
         }
+        if (any_key) {   // (a read with events but nothing counted: a zero-span piece at its first key)
+            if (n == 0) tmp[n++] = {kmin, 0, 0, ci, ri, 1, 0, 0, 0, 0, 0, 0};
+            tmp[0].ins = 1;
+            tmp[0].kmin = (uint32_t)kmin;
+            tmp[0].kmax = (uint32_t)kmax;
+        }
+        for (int k = 0; k < n; k++) {
+            span[r.ref] += tmp[k].kb - tmp[k].ka;
+            tmp[k].nslots = r.ntok + (tmp[k].range ? 2u : 0u) + (tmp[k].ins ? 3u : 0u);
+            tmp[k].qlen = (uint32_t)align_up(r.slen, 16);
+            tmp[k].ref = r.ref;
+            if (dst) dst[k] = tmp[k];
+        }
+        return n;
+    };
+    std::vector<int64_t> chof(NC + 1, 0);
+    const int ntp = plan_threads(NC, 1);
+    std::vector<std::vector<int64_t>> tspan(ntp, std::vector<int64_t>(R, 0)), treads(ntp, std::vector<int64_t>(R, 0));
+    {
+        std::atomic<int64_t> nextc{0};
+        par_ranges(ntp, ntp, [&](int t, int64_t, int64_t) {   // pass 1: pieces per chunk
+            std::vector<int64_t> sp(R, 0), rd(R, 0);
+            for (int64_t ci; (ci = nextc++) < NC;) {
+                int64_t n = 0;
+                for (uint32_t ri = 0; ri < (uint32_t)CH[ci]->reads.size(); ri++) n += read_pieces((uint32_t)ci, ri, nullptr, sp.data(), rd.data());
+                chof[ci + 1] = n;
+            }
+            (void)t;
+        });
     }
+    for (int64_t ci = 0; ci < NC; ci++) chof[ci + 1] += chof[ci];
+    std::vector<Piece, uninit_alloc<Piece>> pcs((size_t)chof[NC]);
+    {
+        std::atomic<int64_t> nextc{0};
+        par_ranges(ntp, ntp, [&](int t, int64_t, int64_t) {   // pass 2: written in place
+            for (int64_t ci; (ci = nextc++) < NC;) {
+                Piece *dst = pcs.data() + chof[ci];
+                for (uint32_t ri = 0; ri < (uint32_t)CH[ci]->reads.size(); ri++)
+                    dst += read_pieces((uint32_t)ci, ri, dst, tspan[t].data(), treads[t].data());
+            }
+        });
+    }
+    std::vector<int64_t> ref_span(R, 0);
+    for (int t = 0; t < ntp; t++)
+        for (int64_t r = 0; r < R; r++) {
+            ref_span[r] += tspan[t][r];
+            b->ref_reads[r] += treads[t][r];
+        }
+    clk.mark("pieces");
     const int64_t NP = (int64_t)pcs.size();
     if (NP >= ((int64_t)1 << 32) - 2) return s2c_set_error(S2C_ERR_LIMIT, "more than 2^32 pieces (split the input)");
     I.n_pieces = NP;
@@ -1680,9 +1881,15 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     // ---- window: pieces up to S positions are short (reached from the run-slot CSR of the
     //      kwin + 1 words before a word); the rare longer ones go to the tile long lists ----
     int64_t S = 64;
+    const int ntw = plan_threads(NP, 1 << 18);
     {
+        std::vector<std::vector<int64_t>> th(ntw, std::vector<int64_t>(4097, 0));
+        par_ranges(ntw, NP, [&](int t, int64_t k0, int64_t k1) {
+            for (int64_t k = k0; k < k1; k++) th[t][std::min<int64_t>(pcs[k].kb - pcs[k].ka, 4096)]++;
+        });
         std::vector<int64_t> hist(4097, 0);
-        for (const Piece &q : pcs) hist[std::min<int64_t>(q.kb - q.ka, 4096)]++;
+        for (int t = 0; t < ntw; t++)
+            for (int s = 0; s <= 4096; s++) hist[s] += th[t][s];
         int64_t above = NP, lim = NP / 1000;
         for (int64_t s = 0; s <= 4096; s++) {
             above -= hist[s];
@@ -1691,47 +1898,118 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
         S = std::min<int64_t>(S, 1024);
     }
     int64_t K = 0;
-    for (Piece &q : pcs) {
-        const int64_t span = q.kb - q.ka;
-        q.lng = span > S;
-        if (!q.lng && span > 0) K = std::max<int64_t>(K, (int64_t)(((q.gpos + span - 1) >> 5) - (q.gpos >> 5)));
-        const ReadRec &r = CH[q.chunk]->reads[q.read];
-        q.nslots = r.ntok + (q.range ? 2u : 0u) + (q.ins ? 3u : 0u);
+    {
+        std::vector<int64_t> tk(ntw, 0);
+        par_ranges(ntw, NP, [&](int t, int64_t k0, int64_t k1) {
+            int64_t kk = 0;
+            for (int64_t k = k0; k < k1; k++) {
+                Piece &q = pcs[k];
+                const int64_t span = q.kb - q.ka;
+                q.lng = span > S;
+                if (!q.lng && span > 0) kk = std::max<int64_t>(kk, (int64_t)(((q.gpos + span - 1) >> 5) - (q.gpos >> 5)));
+            }
+            tk[t] = kk;
+        });
+        for (int t = 0; t < ntw; t++) K = std::max(K, tk[t]);
     }
     I.kwin = K;
 
+    clk.mark("window");
     // ---- bucket the pieces by start word (counting sort, stable in file order) ----
-    std::vector<uint32_t> order(NP);
-    b->rs.assign(NW + 1, 0);
+    std::vector<uint32_t, uninit_alloc<uint32_t>> order(NP);
     {
-        std::vector<uint64_t> cnt(NW + 1, 0);
-        for (const Piece &q : pcs) cnt[(q.gpos >> 5) + 1]++;
-        for (int64_t w = 0; w < NW; w++) cnt[w + 1] += cnt[w];
-        for (int64_t i = 0; i < NP; i++) order[cnt[pcs[i].gpos >> 5]++] = (uint32_t)i;
+        std::atomic<bool> sorted{true};   // (coordinate-sorted input: already in word order)
+        par_ranges(ntw, NP, [&](int, int64_t k0, int64_t k1) {
+            for (int64_t k = std::max<int64_t>(k0, 1); k < k1 && sorted; k++)
+                if ((pcs[k].gpos >> 5) < (pcs[k - 1].gpos >> 5)) sorted = false;
+        });
+        if (sorted) {
+            par_ranges(ntw, NP, [&](int, int64_t k0, int64_t k1) {
+                for (int64_t k = k0; k < k1; k++) order[k] = (uint32_t)k;
+            });
+        } else if ((uint64_t)(NW + 1) * (uint64_t)ntw <= ((uint64_t)1 << 27)) {
+            // per-range histograms, word-major offsets, stable scatter (ranges in file order)
+            std::vector<std::vector<uint32_t>> cnt(ntw);
+            par_ranges(ntw, NP, [&](int t, int64_t k0, int64_t k1) {
+                cnt[t].assign(NW + 1, 0u);
+                for (int64_t k = k0; k < k1; k++) cnt[t][pcs[k].gpos >> 5]++;
+            });
+            uint64_t run = 0;
+            for (int64_t w = 0; w <= NW; w++)
+                for (int t = 0; t < ntw; t++) {
+                    const uint32_t c = cnt[t][w];
+                    cnt[t][w] = (uint32_t)run;
+                    run += c;
+                }
+            par_ranges(ntw, NP, [&](int t, int64_t k0, int64_t k1) {
+                for (int64_t k = k0; k < k1; k++) order[cnt[t][pcs[k].gpos >> 5]++] = (uint32_t)k;
+            });
+        } else {
+            std::vector<uint64_t> cnt(NW + 1, 0);
+            for (int64_t i = 0; i < NP; i++) cnt[(pcs[i].gpos >> 5) + 1]++;
+            for (int64_t w = 0; w < NW; w++) cnt[w + 1] += cnt[w];
+            for (int64_t i = 0; i < NP; i++) order[cnt[pcs[i].gpos >> 5]++] = (uint32_t)i;
+        }
     }
+    // piece CSR by start word: ps[w] = the first sorted piece starting in word ≥ w
+    b->ps.resize(NW + 1);
+    par_ranges(ntw, NP, [&](int, int64_t k0, int64_t k1) {
+        for (int64_t k = k0; k < k1; k++) {
+            const int64_t wk = (int64_t)(pcs[order[k]].gpos >> 5), wp = k ? (int64_t)(pcs[order[k - 1]].gpos >> 5) : -1;
+            for (int64_t w = wp + 1; w <= wk; w++) b->ps[w] = (uint32_t)k;
+        }
+    });
+    for (int64_t w = NP ? (int64_t)(pcs[order[NP - 1]].gpos >> 5) + 1 : 0; w <= NW; w++) b->ps[w] = (uint32_t)NP;
+    clk.mark("bucket");
     // output offsets (ops, bases) in sorted order
-    std::vector<uint64_t> ooff(NP + 1, 0), qoff(NP + 1, 0);
-    for (int64_t k = 0; k < NP; k++) {
-        const Piece &q = pcs[order[k]];
-        const ReadRec &r = CH[q.chunk]->reads[q.read];
-        ooff[k + 1] = ooff[k] + q.nslots;
-        qoff[k + 1] = qoff[k] + (uint64_t)align_up(r.slen, 16);
+    std::vector<uint64_t, uninit_alloc<uint64_t>> ooff(NP + 1), qoff(NP + 1);
+    ooff[0] = qoff[0] = 0;
+    {   // (range sums, then each range's prefix from its base)
+        std::vector<uint64_t> so(ntw + 1, 0), sq(ntw + 1, 0);
+        par_ranges(ntw, NP, [&](int t, int64_t k0, int64_t k1) {
+            uint64_t a = 0, q = 0;
+            for (int64_t k = k0; k < k1; k++) {
+                const Piece &pc = pcs[order[k]];
+                a += pc.nslots;
+                q += pc.qlen;
+                ooff[k + 1] = a;
+                qoff[k + 1] = q;
+            }
+            so[t + 1] = a;
+            sq[t + 1] = q;
+        });
+        for (int t = 0; t < ntw; t++) { so[t + 1] += so[t]; sq[t + 1] += sq[t]; }
+        par_ranges(ntw, NP, [&](int t, int64_t k0, int64_t k1) {
+            for (int64_t k = k0; k < k1; k++) { ooff[k + 1] += so[t]; qoff[k + 1] += sq[t]; }
+        });
     }
+    clk.mark("offsets");
     const uint64_t NOPS = ooff[NP], NQ = qoff[NP];
     // the kernels address run records and base planes with 32-bit buffer offsets (< 3.5 GB)
     if (16 * NOPS >= 0xE0000000ull) return s2c_set_error(S2C_ERR_LIMIT, "more than 2^28 op words (split the input)");
     if (NQ / 4 >= 0xE0000000ull) return s2c_set_error(S2C_ERR_LIMIT, "more than 14 G query bases (split the input)");
     I.n_ops = (int64_t)NOPS;
     I.n_qwords = (int64_t)((NQ + 31) / 32) + 2;
-    b->pc.assign(4 * (size_t)(NP + 1), 0u);
-    b->kmin.assign(NP, 0xFFFFFFFFu);
-    b->kmax.assign(NP, 0u);
+    b->pc.resize(4 * (size_t)(NP + 1));
+    b->kmin.resize(NP);
+    b->kmax.resize(NP);
     b->ops.resize(std::max<uint64_t>(NOPS, 1));
-    b->bq.assign(2 * (size_t)I.n_qwords, 0u);
-    b->bx.assign((size_t)I.n_qwords, 0u);
-    {   // emit in parallel over ranges of sorted pieces
-        unsigned hw = std::thread::hardware_concurrency();
-        const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(std::min<unsigned>(hw ? hw : 1, 16), NP / 65536));
+    b->bq.resize(2 * (size_t)I.n_qwords);
+    b->bx.resize((size_t)I.n_qwords);
+    {   // the words the pieces do not cover: from the half-word after the last piece's bases on
+        const uint64_t h0 = NQ / 16, nh = 2 * (uint64_t)I.n_qwords;
+        uint16_t *dq = (uint16_t *)b->bq.data(), *dx = (uint16_t *)b->bx.data();
+        for (uint64_t d = h0; d < nh; d++) {
+            dq[(d >> 1) * 4 + (d & 1)] = 0;
+            dq[(d >> 1) * 4 + 2 + (d & 1)] = 0;
+            dx[d] = 0;
+        }
+        b->ops[0] = 0;
+        for (int j = 0; j < 4; j++) b->pc[4 * (size_t)NP + j] = 0;
+    }
+    clk.mark("alloc");
+    {   // emit in parallel over ranges of sorted pieces (each thread first-touches its range)
+        const int nt = plan_threads(NP, 65536);
         auto emit = [&](int64_t k0, int64_t k1) {
             uint16_t *dq = (uint16_t *)b->bq.data();   // half-words: [k][plane][2 halves]
             uint16_t *dx = (uint16_t *)b->bx.data();
@@ -1742,6 +2020,8 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
                 uint32_t *o = &b->ops[ooff[k]];
                 uint32_t fl = (r.has_x ? S2C_PF_X : 0u) | ((r.has_x & 2) ? S2C_PF_DASH : 0u);
                 if (q.range) { fl |= S2C_PF_RANGE; *o++ = (uint32_t)q.ka; *o++ = (uint32_t)q.kb; }
+                b->kmin[k] = 0xFFFFFFFFu;
+                b->kmax[k] = 0u;
                 if (q.ins) {
                     fl |= S2C_PF_INS;
                     b->kmin[k] = q.kmin;
@@ -1780,21 +2060,18 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
             for (int t = 0; t < nt; t++) th.emplace_back(emit, NP * t / nt, NP * (t + 1) / nt);
             for (auto &t : th) t.join();
         }
+    clk.mark("emit threads");
         uint32_t *pr = &b->pc[4 * (size_t)NP];   // sentinel
         pr[1] = (uint32_t)(NQ / 16);
         pr[2] = (uint32_t)NOPS;
-        // run-slot and piece CSRs by start word
-        b->ps.assign(NW + 1, 0);
-        for (int64_t k = 0; k < NP; k++) {
-            b->rs[(pcs[order[k]].gpos >> 5) + 1] += pcs[order[k]].nslots;
-            b->ps[(pcs[order[k]].gpos >> 5) + 1]++;
-        }
-        for (int64_t w = 0; w < NW; w++) {
-            b->rs[w + 1] += b->rs[w];
-            b->ps[w + 1] += b->ps[w];
-        }
+        // run-slot CSR by start word: the op slots before the first piece of word w
+        b->rs.resize(NW + 1);
+        par_ranges(plan_threads(NW + 1, 1 << 16), NW + 1, [&](int, int64_t w0, int64_t w1) {
+            for (int64_t w = w0; w < w1; w++) b->rs[w] = (uint32_t)ooff[b->ps[w]];
+        });
     }
 
+    clk.mark("emit");
     // ---- tiles: width from depth; a shallow tile keeps its window's runs in LDS ----
     struct Tile { int64_t a, b, ref; };
     std::vector<Tile> tiles;
@@ -1805,12 +2082,28 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
         tile_force = align_up(std::min<int64_t>(std::max<int64_t>(atoll(e), 64), TP_MAX), S2C_POS_ALIGN);
     if (p->tile_width > 0) tile_force = p->tile_width;   // streamed batches: the same tiles every time
     std::vector<int64_t> ref_slots(R, 0), ref_np(R, 0), ref_qw(R, 0);
-    for (int64_t k = 0; k < NP; k++) {
-        const Piece &q = pcs[order[k]];
-        const ReadRec &rr = CH[q.chunk]->reads[q.read];
-        ref_slots[rr.ref] += q.nslots;
-        ref_np[rr.ref]++;
-        ref_qw[rr.ref] += (int64_t)align_up(rr.slen, 16);
+    std::vector<int64_t> longs;   // sorted indices of the long pieces
+    {
+        std::vector<std::vector<int64_t>> ts(ntw, std::vector<int64_t>(3 * R, 0)), tl(ntw);
+        par_ranges(ntw, NP, [&](int t, int64_t k0, int64_t k1) {
+            int64_t *a = ts[t].data();
+            for (int64_t k = k0; k < k1; k++) {   // (a piece's reference from its start position)
+                const Piece &q = pcs[order[k]];
+                const uint32_t ref = q.ref;
+                a[3 * ref] += q.nslots;
+                a[3 * ref + 1]++;
+                a[3 * ref + 2] += q.qlen;
+                if (q.lng) tl[t].push_back(k);
+            }
+        });
+        for (int t = 0; t < ntw; t++) {
+            for (int64_t r = 0; r < R; r++) {
+                ref_slots[r] += ts[t][3 * r];
+                ref_np[r] += ts[t][3 * r + 1];
+                ref_qw[r] += ts[t][3 * r + 2];
+            }
+            longs.insert(longs.end(), tl[t].begin(), tl[t].end());
+        }
     }
     for (int64_t r = 0; r < R; r++) {
         const int64_t L = p->ref_len[r], off = b->ref_off[r];
@@ -1845,12 +2138,12 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     for (int64_t t = 0; t < NT; t++)
         for (int64_t W = tiles[t].a >> 5; W < (tiles[t].b + 31) >> 5; W++) b->wtile[W] = (uint32_t)t;
 
+    clk.mark("tiles");
     // ---- long lists: run slots of long pieces per tile they overlap ----
     std::vector<uint32_t> lcnt(NT + 1, 0);
     auto for_long = [&](auto fn) {
-        for (int64_t k = 0; k < NP; k++) {
+        for (const int64_t k : longs) {
             const Piece &q = pcs[order[k]];
-            if (!q.lng) continue;
             const uint32_t t0 = b->wtile[q.gpos >> 5], t1 = b->wtile[(q.gpos + (q.kb - q.ka) - 1) >> 5];
             for (uint32_t t = t0; t <= t1; t++) fn(t, k);
         }
@@ -1866,6 +2159,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     }
     I.n_long = lcnt[NT];
 
+    clk.mark("long lists");
     // ---- insertion plan: per tile its events' hash-table capacity, long-motif slots and an
     //      upper bound of its columns (Σ motif lengths ≥ Σ over keys of the longest, :278-281)
     std::vector<uint32_t> nshort(NT, 0), nlong(NT, 0), nev(NT, 0);
@@ -1882,6 +2176,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
             I.n_ins_bases += e.len;
         }
 
+    clk.mark("ins plan");
     // ---- work items: per tile its layers (k_tile's LDS chunks; lane groups of G = 256 / nwp
     //      lanes per word) split into items ----
     int64_t nwp = 8;
@@ -1899,33 +2194,51 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     // that lets 8 two-wave tiles reside (4 waves per SIMD, the kernel's register budget),
     // the rest are not dense (k_tile runs them).
     int64_t dense_cap = S2C_DENSE_LDS;
+    // per tile (host threads): its window, the most candidate runs of a word, layers, items
+    std::vector<int64_t> t_nl(NT), t_nch(NT), t_maxc(NT), t_wruns(NT);
+    std::atomic<bool> too_big{false};
+    par_ranges(plan_threads(NT, 64), NT, [&](int, int64_t ta, int64_t tb) {
+        for (int64_t t = ta; t < tb; t++) {
+            const Tile &T = tiles[t];
+            const int64_t w0 = T.a >> 5, w1 = (T.b + 31) >> 5;
+            const int64_t nlg = lcnt[t + 1] - lcnt[t];
+            int64_t maxc = 0;
+            for (int64_t W = w0; W < w1; W++)
+                maxc = std::max<int64_t>(maxc, (int64_t)b->rs[W + 1] - (int64_t)b->rs[std::max<int64_t>(W - K, 0)] + nlg);
+            t_maxc[t] = maxc;
+            const int64_t nl = plan_layers(b, PB, K, (uint64_t)T.a, (uint64_t)T.b, G);
+            t_nl[t] = nl;
+            if (nl <= 0) { too_big = true; continue; }
+            t_nch[t] = plan_items(b, K, (uint64_t)T.a, (uint64_t)T.b, nl);
+            t_wruns[t] = (int64_t)b->rs[w1] - (int64_t)b->rs[std::max<int64_t>(w0 - K, 0)];
+            tile_window(b, K, T.a, T.b, &b->tiles[(size_t)t * S2C_TILE_WORDS]);
+        }
+    });
+    if (too_big) return s2c_set_error(S2C_ERR_LIMIT, "a read whose SEQ or CIGAR exceeds k_tile's LDS chunk");
+    // Launch LDS of k_tile_dense = the largest dense window, so one outlier window sets every
+    // tile's occupancy: when all but ≤ 0.2 % of the windows fit the share of a CU's 160 KB
+    // that lets 8 two-wave tiles reside (4 waves per SIMD, the kernel's register budget),
+    // the rest are not dense (k_tile runs them).
     {
         const int64_t nwp = tile_max <= 512 ? 16 : tile_max <= 1024 ? 32 : 64;
         const int64_t cap8 = 163840 / 8 - (96 * nwp + 128);   // (the kernel's static LDS)
-        std::vector<int64_t> db;
-        uint32_t tw[S2C_TILE_WORDS];
+        int64_t nfit = 0, over = 0;
         for (int64_t t = 0; t < NT; t++) {
-            tile_window(b, K, tiles[t].a, tiles[t].b, tw);
-            if (dense_fits(tw, K)) db.push_back(dense_bytes(tw, K));
+            const uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
+            if (dense_fits(tw, K)) {
+                nfit++;
+                over += dense_bytes(tw, K) > cap8;
+            }
         }
-        const int64_t over = (int64_t)std::count_if(db.begin(), db.end(), [&](int64_t x) { return x > cap8; });
-        if (over > 0 && over * 500 <= (int64_t)db.size()) dense_cap = cap8;
+        if (over > 0 && over * 500 <= nfit) dense_cap = cap8;
     }
     for (int64_t t = 0; t < NT; t++) {
         const Tile &T = tiles[t];
-        const int64_t w0 = T.a >> 5, w1 = (T.b + 31) >> 5;
         const int64_t nlg = lcnt[t + 1] - lcnt[t];
-        int64_t maxc = 0;
-        for (int64_t W = w0; W < w1; W++)
-            maxc = std::max<int64_t>(maxc, (int64_t)b->rs[W + 1] - (int64_t)b->rs[std::max<int64_t>(W - K, 0)] + nlg);
-        int64_t nl = plan_layers(b, PB, K, (uint64_t)T.a, (uint64_t)T.b, G);
-        if (nl <= 0) return s2c_set_error(S2C_ERR_LIMIT, "a read whose SEQ or CIGAR exceeds k_tile's LDS chunk");
-        const int64_t nch = plan_items(b, K, (uint64_t)T.a, (uint64_t)T.b, nl);
+        const int64_t maxc = t_maxc[t], nl = t_nl[t], nch = t_nch[t];
         I.chunk = std::max<int64_t>(I.chunk, nl);
-        const int64_t wruns = (int64_t)b->rs[w1] - (int64_t)b->rs[std::max<int64_t>(w0 - K, 0)];
-        runs_max = std::max(runs_max, wruns);
+        runs_max = std::max(runs_max, t_wruns[t]);
         uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
-        tile_window(b, K, T.a, T.b, tw);
         uint32_t fl = nch > 1 ? S2C_TILE_DEEP : 0u;
         if (nev[t] > S2C_EPI_KEYS || (int64_t)ccap[t] > lcols) fl |= S2C_TILE_GENERAL;
         if (fl == 0 && nev[t] == 0 && nlg == 0 && maxc <= 255 && !no_dense && dense_fits(tw, K) &&
@@ -1953,6 +2266,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
         }
         if (fl & (S2C_TILE_DEEP | S2C_TILE_GENERAL)) b->deep.push_back((uint32_t)t);
     }
+    clk.mark("items");
     if (boff >= (1ull << 32) || loff >= (1ull << 32) || coff >= (1ull << 31))
         return s2c_set_error(S2C_ERR_LIMIT, "insertion tables exceed 2^32 slots (split the input)");
     I.n_items = (int64_t)(b->items.size() / S2C_ITEM_WORDS);
@@ -1963,6 +2277,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     I.n_cols = (int64_t)coff;
     I.runs_max = runs_max;
     mark_runs(b);
+    clk.mark("mark_runs");
     *out = guard.release();
     return S2C_OK;
 }
@@ -1993,6 +2308,7 @@ static int s2c_batch_shard_impl(const s2c_batch *b, int64_t t0, int64_t t1, s2c_
     // ---- pieces: the window range, long pieces listed by the tiles, event pieces keyed inside
     std::vector<uint8_t> take(NP, 0);
     auto piece_at_word = [&](int64_t w) {   // first piece with start word >= w
+        if ((int64_t)b->ps.size() == b->info.n_words + 1 && w <= b->info.n_words) return (int64_t)b->ps[w];
         int64_t lo = 0, hi = NP;
         while (lo < hi) {
             const int64_t m = (lo + hi) / 2;
@@ -2032,7 +2348,7 @@ static int s2c_batch_shard_impl(const s2c_batch *b, int64_t t0, int64_t t1, s2c_
     J.n_ops = (int64_t)ooff[NS];
     J.n_qwords = (int64_t)((qoff[NS] + 31) / 32) + 2;
     s->pc.assign(4 * (size_t)(NS + 1), 0u);
-    s->ops.resize(std::max<uint64_t>(ooff[NS], 1));
+    s->ops.assign(std::max<uint64_t>(ooff[NS], 1), 0u);
     s->bq.assign(2 * (size_t)J.n_qwords, 0u);
     s->bx.assign((size_t)J.n_qwords, 0u);
     s->kmin.assign(NS, 0xFFFFFFFFu);
