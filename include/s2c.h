@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define S2C_ABI_VERSION 7
+#define S2C_ABI_VERSION 8
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define S2C_OK            0
@@ -99,7 +99,9 @@ int s2c_layout(int64_t *out, int n);
                                 seqout is SEQ[0:take] (:64-69) and slen holds take = min(l, len(SEQ))
                                 (every consumer's min(l, slen) is then take) */
 
-/* run record (device-written by k_reads, parallel to ops[]): {gpos, len | kind << 24, qlo, qhi} */
+/* run record (device-written by k_reads, parallel to ops[]): {gpos, len | kind << 27, qlo, qhi};
+   a run (and a read's seqout) is < 2^27 positions: N skips of up to 134 Mb */
+#define S2C_RUN_KSHIFT 27
 #define S2C_RUN_EMPTY   0u
 #define S2C_RUN_BASES   1u   /* seqout [gpos, gpos+len) = query bases [q, q+len) (q = qhi:qlo) */
 #define S2C_RUN_DASH    2u   /* seqout '-' (D/N/P, counted: not maxdel-dropped) */
@@ -121,7 +123,7 @@ int s2c_layout(int64_t *out, int n);
 #define S2C_LY_MAIN 0xFFFFFFFFu
 #define S2C_TILE_DEEP     1  /* several work items: counts summed in HBM, voted by k_consensus */
 #define S2C_TILE_GENERAL  2  /* insertion layout beyond k_tile's LDS: voted by k_consensus */
-#define S2C_TILE_DENSE    4  /* routed to k_tile_dense (one item, no insertion keys, no long pieces) */
+#define S2C_TILE_DENSE    4  /* routed to k_tile_dense (one item, no insertion keys; long pieces through its long list) */
 #define S2C_ITEM_WORDS    4  /* work item {tile, chunk, l0, l1}: the tile's layers [l0, l1) */
 #define S2C_EPI_KEYS    256  /* insertion keys per tile k_tile's epilogue holds in LDS */
 /* insertion columns per tile k_tile's epilogue holds in LDS, by words per tile */
@@ -134,17 +136,17 @@ int s2c_layout(int64_t *out, int n);
    readable up to their end rounded up to 16 bytes. */
 #define S2C_DENSE_BYTES(ns, nq) (((4 * (ns) + 30) & ~15) + ((8 * (nq) + 30) & ~15) + ((12 * (ns) + 1024 + 15) & ~15))
 #define S2C_DENSE_QW   4096  /* base plane words of a dense tile's window (17-bit query offsets) */
-/* k_tile's LDS chunk: one layer of a tile window, contiguous in the layered arrays: its
+/* k_tile's LDS chunk (one per wave): one layer of a tile window, contiguous in the layered arrays: its
    piece records, op words, base planes
    {p0, p1} through the word after its last base (funnel shift) and non-ACGT words — caps
    per layer — and its run records (= op slots), per 32-position word and counting lane <=
-   S2C_CHUNK_LANE_RECS * lanes per word (8-bit counters).  A work item's run records per
+   S2C_CHUNK_LANE_RECS * lanes per word of a wave, 64 / words per tile (8-bit counters).  A work item's run records per
    word are <= S2C_ITEM_RECS (its u16 histogram). */
-#define S2C_CHUNK_PIECES     512
-#define S2C_CHUNK_QBYTES   16384
-#define S2C_CHUNK_XBYTES    8192
-#define S2C_CHUNK_OBYTES    4096
-#define S2C_CHUNK_RECS       768
+#define S2C_CHUNK_PIECES     128
+#define S2C_CHUNK_QBYTES    4096
+#define S2C_CHUNK_XBYTES    2048
+#define S2C_CHUNK_OBYTES    1024
+#define S2C_CHUNK_RECS       192
 #define S2C_CHUNK_LANE_RECS  248
 #define S2C_CHUNK_SEGS       128
 #define S2C_ITEM_RECS      60000
@@ -215,6 +217,11 @@ int  s2c_parser_retain_events(s2c_parser *p);
 int  s2c_parser_pos_weights(s2c_parser *p, int64_t shift, int64_t *w, int64_t n);
 int  s2c_parser_checks(s2c_parser *p, uint8_t *bad, int64_t n_refs);
 int  s2c_parser_counters(s2c_parser *p, int64_t *out);
+/* Where the read pass stands, also after a read-pass error (the reference prints its header
+   line and progress lines up to the failing line, :182, :224-225, before raising):
+   out[5] = {header ended (0/1), references, header lines, lines read (through the failing
+   line), error code of the read pass (0: none)}. */
+int  s2c_parser_progress(const s2c_parser *p, int64_t *out);
 int  s2c_parser_pack(s2c_parser *p, int64_t g0, int64_t g1, size_t *len);
 int  s2c_parser_blob_copy(const s2c_parser *p, void *dst, size_t cap);
 int  s2c_parser_unpack(s2c_parser *p, const void *blob, size_t len);

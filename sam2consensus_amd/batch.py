@@ -38,6 +38,19 @@ class Parser:
         hb.maxdel_active, hb.maxdel = self.maxdel_active, self.maxdel   # the device applies :210
         return hb
 
+    def progress(self):
+        """(header ended, references, header lines, lines read, read-pass error code): where
+        the read pass stands, also after it raised (s2c_parser_progress)."""
+        c = (C.c_int64 * 5)()
+        L.check(lib.s2c_parser_progress(self._p, c))
+        return tuple(int(x) for x in c)
+
+    def counters(self):
+        """(header lines, lines, mapped reads, aligned bases) of a clean read pass."""
+        c = (C.c_int64 * 4)()
+        L.check(lib.s2c_parser_counters(self._p, c))
+        return tuple(int(x) for x in c)
+
     def close(self):
         if self._p:
             lib.s2c_parser_free(self._p)

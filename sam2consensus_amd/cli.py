@@ -104,15 +104,51 @@ def _log_summary(log, info):
         str(info.reads_mapped) + " reads were mapped.\n")
 
 
+REF_ERRORS = (KeyError, IndexError, ValueError, ZeroDivisionError, OverflowError)
+
+
+class _Partial:
+    """_log_summary's fields from the parser's counters (a run that failed after the read pass)."""
+
+    def __init__(self, n_refs, counters):
+        self.n_refs = n_refs
+        self.header_lines, self.lines_total, self.reads_mapped = counters[0], counters[1], counters[2]
+
+
+def _log_failed_parse(log, parser):
+    """What the reference has printed when the read pass or its insertion checks raise: its
+    header line once the header is read (:182), the progress lines of the lines before the
+    failing one (:224-225); after a clean read pass (an insertion check failed, :284-294) the
+    whole summary (:227)."""
+    ended, n_refs, header_lines, lines, err = parser.progress()
+    if not err:
+        _log_summary(log, _Partial(n_refs, parser.counters()))
+        return
+    if not ended:
+        return   # (the header pass raised: nothing after "Processing file")
+    log("SAM header processed, " + str(n_refs) + " references found.\n")
+    for line in progress_lines(header_lines, lines - 1):
+        log(line)
+
+
 def consensus_files(filename, thresholds, prefix, min_depth=1, fill=b"-", nchar=0, maxdel_active=True,
                     device=None, log=None):
     """Run the whole pipeline on one SAM/SAM.gz file; returns a RunResult whose
     ``files`` maps ``REF__PREFIX.fasta`` → content bytes (nothing written)."""
-    from .batch import parse_file
+    from .batch import Parser
 
     t = {}
     t0 = time.perf_counter()
-    hb = parse_file(filename, maxdel_active, 150)
+    p = Parser(maxdel_active, 150)
+    try:
+        p.feed_file(filename)
+        hb = p.finish()
+    except REF_ERRORS:
+        if log:
+            _log_failed_parse(log, p)
+        raise
+    finally:
+        p.close()
     t["parse"] = time.perf_counter() - t0
     if log:
         _log_summary(log, hb.info)

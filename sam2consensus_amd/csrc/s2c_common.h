@@ -334,8 +334,8 @@ struct Run {
 __device__ __forceinline__ Run run_of(uint4 v) {
     Run r;
     r.gpos = v.x;
-    r.len = v.y & 0xFFFFFFu;
-    r.kind = v.y >> 24;
+    r.len = v.y & ((1u << S2C_RUN_KSHIFT) - 1u);
+    r.kind = v.y >> S2C_RUN_KSHIFT;
     r.q = (uint64_t)v.z | ((uint64_t)v.w << 32);
     return r;
 }
@@ -346,7 +346,7 @@ struct RecGeom {
     uint32_t valid, lo;   // covered bits, first covered bit
     uint32_t qs;          // offset into the run of position 32W + lo
 };
-// 32-bit arithmetic: positions < 2^32, a run's length < 2^24 and the runs a word looks at
+// 32-bit arithmetic: positions < 2^32, a run's length < 2^27 and the runs a word looks at
 // start within 2^31 positions of it
 __device__ __forceinline__ RecGeom rec_geom(uint32_t gpos, uint32_t len, uint32_t W) {
     RecGeom g;

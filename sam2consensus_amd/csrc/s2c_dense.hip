@@ -66,7 +66,7 @@ __constant__ uint8_t c_amb[64] = {
 };
 
 struct DenseArgs {
-    const uint32_t *rs, *pc, *ops, *bq, *bx, *tiles, *items;
+    const uint32_t *rs, *pc, *ops, *bq, *bx, *tiles, *items, *lp, *runs;
     const double *thresholds;
     uint64_t *tile_stats, *blk_len;
     uint8_t *out;
@@ -346,7 +346,7 @@ __device__ __forceinline__ uint32_t byte_bits(uint32_t m) { return ((m & 0x80808
 
 // A tile's window (uniform values from its tile record; S2C_TILE_WORDS layout)
 struct Win {
-    uint32_t tile, a, n, cb0, pf0, npc, o0, nslot, qw0, nqw, W0, nwords;
+    uint32_t tile, a, n, cb0, pf0, npc, o0, nslot, qw0, nqw, W0, nwords, lp0, nlong;
 };
 __device__ __forceinline__ Win win_of(const DenseArgs &d, uint32_t item) {
     Win v;
@@ -358,6 +358,8 @@ __device__ __forceinline__ Win win_of(const DenseArgs &d, uint32_t item) {
     asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx4 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
                  : "=s"(r), "=s"(r4) : "s"(twp) : "memory");
     v.cb0 = (uint32_t)r[8];
+    v.lp0 = (uint32_t)r[10];
+    v.nlong = (uint32_t)r[11] - v.lp0;
     v.a = (uint32_t)r[0];
     v.n = (uint32_t)r[1] - v.a;
     v.pf0 = (uint32_t)r[13];
@@ -663,6 +665,47 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         count_group(ra, t4, Half{});
 #pragma unroll
         for (int c = 0; c < 4; c++) close4(C[c], t4[c]);
+    }
+    // long pieces over the tile (rare: > window spans, C5's long deletions): k_reads' run
+    // records through the tile's long list, one per lane of the word and round — bases into
+    // the counters (planes from HBM), '-' runs and the N / '-' chars of SEQ into the byte
+    // counters (the host keeps a dense tile's candidate runs + long runs ≤ 255 per word)
+    if (v.nlong) {
+        const int32_t wr = (int32_t)(32 * w);   // tile-relative first position of the lane's word
+        const uint32_t ntr = uni(__ockl_wfred_max_u32(active && g < v.nlong ? (v.nlong - g + G - 1) / G : 0u));
+        for (uint32_t m = 0; m < ntr; m++) {
+            const uint32_t j = g + G * m;
+            if (!(active && j < v.nlong)) continue;
+            const Run r = run_of(((const uint4 *)d.runs)[d.lp[v.lp0 + j]]);
+            const RecGeom gm = rec_geom(r.gpos, r.len, W);
+            if (!gm.valid) continue;
+            const int32_t p0 = wr + (int32_t)gm.lo, p1 = p0 + __popc(gm.valid);
+            if ((r.kind & 3u) == S2C_RUN_DASH) {
+                cnt_range(dcnt, p0, p1, TL);
+            } else if ((r.kind & 3u) == S2C_RUN_BASES) {
+                const uint64_t qs = r.q + gm.qs, qw = qs >> 5;
+                const uint32_t sh = (uint32_t)(qs & 31);
+                const uint32_t mx = (funnel(d.bq[2 * qw + 2], d.bq[2 * qw], sh) << gm.lo) & gm.valid;
+                const uint32_t my = (funnel(d.bq[2 * qw + 3], d.bq[2 * qw + 1], sh) << gm.lo) & gm.valid;
+                ripple1(C[0], mx);
+                ripple1(C[1], my);
+                ripple1(C[2], mx & my);
+                ripple1(C[3], gm.valid);
+                if (r.kind & S2C_RUN_XBIT) {
+                    uint32_t xm = (funnel(d.bx[qw + 1], d.bx[qw], sh) << gm.lo) & gm.valid;
+                    while (xm) {
+                        const uint32_t bit = (uint32_t)__builtin_ctz(xm);
+                        xm &= xm - 1;
+                        if ((mx >> bit) & 1u) {   // '-' of SEQ (p0 = 1)
+                            cnt_add1(ccnt, (uint32_t)(wr + (int32_t)bit));
+                            if (!(r.kind & S2C_RUN_DROP)) cnt_add1(dcnt, (uint32_t)(wr + (int32_t)bit));
+                        } else {
+                            cnt_add1(ncnt, (uint32_t)(wr + (int32_t)bit));
+                        }
+                    }
+                }
+            }
+        }
     }
     PROF_MARK(5);
     // queued single-token runs of reads with N / '-' in SEQ (never dropped: maxdel is off)
@@ -998,7 +1041,7 @@ int s2c_launch_dense(const s2c_dev *dv, hipStream_t st) {
     if (dv->fill_len != 1) return s2c_set_error(S2C_ERR_ARG, "dense tiles need a one-char fill");
     if (dv->n_dense >= ((int64_t)1 << 31)) return s2c_set_error(S2C_ERR_LIMIT, "too many dense tiles");
     DenseArgs a;
-    a.rs = dv->rs; a.pc = dv->pc; a.ops = dv->ops; a.bq = dv->bq; a.bx = dv->bx; a.tiles = dv->tiles; a.items = dv->dense;
+    a.rs = dv->rs; a.lp = dv->lp; a.runs = dv->runs; a.pc = dv->pc; a.ops = dv->ops; a.bq = dv->bq; a.bx = dv->bx; a.tiles = dv->tiles; a.items = dv->dense;
     a.thresholds = dv->thresholds; a.tile_stats = dv->tile_stats; a.blk_len = dv->blk_len; a.out = dv->out;
     a.padded_len = (uint32_t)dv->padded_len; a.n_cols = (uint32_t)dv->n_cols; a.n_tiles = (uint32_t)dv->n_tiles;
     a.kwin = (uint32_t)dv->kwin; a.fill_nondash = (uint32_t)dv->fill_nondash;

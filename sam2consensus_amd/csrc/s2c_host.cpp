@@ -516,7 +516,7 @@ static int process_record(Chunk &c, const RefView &rv, std::string &last_name, i
         }
         if (op != S2C_OP_S && op != S2C_OP_H) c.ntokens++;
     }
-    if (klen >= ((int64_t)1 << 24)) return fail(S2C_ERR_LIMIT, "seqout of 2^24 or more positions not supported");
+    if (klen >= ((int64_t)1 << S2C_RUN_KSHIFT)) return fail(S2C_ERR_LIMIT, "seqout of 2^27 or more positions not supported");
     c.aligned += klen;
     c.qbases += mb;
     if (ref < 0) return fail(S2C_ERR_KEY, "KeyError: '" + std::string(nb, nl) + "' (:212/:221)");
@@ -1184,8 +1184,15 @@ static void piece_blocks(const s2c_batch *b, PieceBlocks &B) {
     });
 }
 
-struct LayerSeg { uint64_t p0, n; };
-static inline uint64_t layer_lo(const LayerSeg &g, uint64_t l, uint64_t nl) { return g.p0 + g.n * l / nl; }
+// Segment s's pieces [p0, p0 + n) cut into nl slices at p0 + floor((n·l + r_s) / nl), the
+// rotation r_s = (s · 2654435761) mod nl spreading the segments' rounding (a segment of fewer
+// pieces than layers puts them in different layers for different segments, not all in the
+// last one).
+struct LayerSeg { uint64_t p0, n, s; };
+static inline uint64_t layer_rot(uint64_t s, uint64_t nl) { return (s * 2654435761ull) % nl; }
+static inline uint64_t layer_lo(const LayerSeg &g, uint64_t l, uint64_t nl) {
+    return g.p0 + (g.n * l + layer_rot(g.s, nl)) / nl;
+}
 
 static bool layer_fits(const PieceBlocks &B, const std::vector<LayerSeg> &seg, int64_t S0, int64_t W0, int64_t W1,
                        int64_t K, int64_t G, uint64_t l, uint64_t nl, std::vector<int64_t> &recs) {
@@ -1217,7 +1224,7 @@ static int64_t plan_layers(const s2c_batch *b, const PieceBlocks &B, int64_t K, 
     uint64_t tp = 0, th = 0, tr = 0, maxn = 0;
     for (int64_t s = S0; s < W1; s++) {
         const uint64_t p0 = b->ps[s], n = b->ps[s + 1] - p0;
-        seg.push_back({p0, n});
+        seg.push_back({p0, n, (uint64_t)s});
         tp += (uint32_t)(B.n[p0 + n] - B.n[p0]);
         th += (uint32_t)(B.h[p0 + n] - B.h[p0]);
         tr += (uint32_t)(B.o[p0 + n] - B.o[p0]);
@@ -1227,13 +1234,15 @@ static int64_t plan_layers(const s2c_batch *b, const PieceBlocks &B, int64_t K, 
     std::vector<int64_t> recs(seg.size());
     uint64_t nl = std::max<uint64_t>({1, (tp * 10 / 9) / S2C_CHUNK_PIECES + 1, (4 * th * 10 / 9) / S2C_CHUNK_QBYTES + 1,
                                       (tr * 10 / 9) / S2C_CHUNK_RECS + 1});
-    nl = std::min(nl, maxn);
+    // (past maxn layers the rotation still spreads the segments' pieces: up to 4 per piece)
+    const uint64_t nlmax = std::max<uint64_t>(maxn, 4 * tp);
+    nl = std::min(nl, nlmax);
     for (;; nl = nl + 1 + nl / 16) {
-        if (nl > maxn) nl = maxn;
+        if (nl > nlmax) nl = nlmax;
         bool ok = true;
         for (uint64_t l = 0; l < nl && ok; l++) ok = layer_fits(B, seg, S0, W0, W1, K, G, l, nl, recs);
         if (ok) return (int64_t)nl;
-        if (nl == maxn) return 0;
+        if (nl == nlmax) return 0;
     }
 }
 
@@ -1276,7 +1285,7 @@ static void build_layers(s2c_batch *b, const PieceBlocks &B, int64_t G) {
         for (int64_t l = 0; l < nl; l++) {
             uint64_t np = 0, no = 0, nh = 0;
             for (int64_t s = S0; s < W1; s++) {
-                const LayerSeg g{b->ps[s], (uint64_t)(b->ps[s + 1] - b->ps[s])};
+                const LayerSeg g{b->ps[s], (uint64_t)(b->ps[s + 1] - b->ps[s]), (uint64_t)s};
                 const uint64_t lo = layer_lo(g, l, nl), hi = layer_lo(g, l + 1, nl);
                 np += (uint32_t)(B.n[hi] - B.n[lo]);
                 no += (uint32_t)(B.o[hi] - B.o[lo]);
@@ -1318,7 +1327,7 @@ static void build_layers(s2c_batch *b, const PieceBlocks &B, int64_t G) {
                 const int64_t L = T.ly0 + l;
                 uint64_t kp = lyp[L], ko = lyo[L], kh = lyh[L];
                 for (int64_t s = S0; s < W1; s++) {
-                    const LayerSeg g{b->ps[s], (uint64_t)(b->ps[s + 1] - b->ps[s])};
+                    const LayerSeg g{b->ps[s], (uint64_t)(b->ps[s + 1] - b->ps[s]), (uint64_t)s};
                     const uint64_t lo = layer_lo(g, l, T.nl), hi = layer_lo(g, l + 1, T.nl);
                     for (uint64_t k = lo; k < hi; k++) {
                         const uint32_t *pr = &b->pc[4 * k];
@@ -1369,7 +1378,7 @@ static int64_t plan_items(const s2c_batch *b, int64_t K, uint64_t a, uint64_t e,
             for (int64_t W = W0; W < W1 && ok; W++) {
                 int64_t r = 0;
                 for (int64_t s = std::max(W - K, S0); s <= W; s++) {
-                    const LayerSeg g{b->ps[s], (uint64_t)(b->ps[s + 1] - b->ps[s])};
+                    const LayerSeg g{b->ps[s], (uint64_t)(b->ps[s + 1] - b->ps[s]), (uint64_t)s};
                     r += b->pc[4 * layer_lo(g, l1, nl) + 2] - b->pc[4 * layer_lo(g, l0, nl) + 2];
                 }
                 ok = r <= S2C_ITEM_RECS;
@@ -1630,6 +1639,17 @@ extern "C" int s2c_parser_checks(s2c_parser *p, uint8_t *bad, int64_t n_refs) {
     return s2c_guarded([&] { return s2c_parser_checks_impl(p, bad, n_refs); });
 }
 
+extern "C" int s2c_parser_progress(const s2c_parser *p, int64_t *out) {
+    if (!p || !out) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
+    out[0] = p->in_header ? 0 : 1;
+    out[1] = (int64_t)p->ref_names.size();
+    out[2] = p->header_lines;
+    out[3] = 0;
+    for (auto &cp : p->chunks) out[3] += cp->lines_total;
+    out[4] = p->err;
+    return S2C_OK;
+}
+
 extern "C" int s2c_parser_counters(s2c_parser *p, int64_t *out) {
     if (!p || !out) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
     int rc = feed_flush(p);
@@ -1817,16 +1837,16 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
             const int64_t pa = r.pos0 + r.kc0;
             if (pa < 0) {
                 const int64_t kb = std::min(r.kc1, -r.pos0);
-                tmp[n++] = {(uint64_t)(off + L + pa), r.kc0, kb, ci, ri, 1, 0, 0, 0, 0, 0, 0};
-                if (r.kc1 > -r.pos0) tmp[n++] = {(uint64_t)off, -r.pos0, r.kc1, ci, ri, 1, 0, 0, 0, 0, 0, 0};
+                tmp[n++] = {(uint64_t)(off + L + pa), r.kc0, kb, ci, ri, 1, 0, 0, 0, 0, 0, 0, 0};
+                if (r.kc1 > -r.pos0) tmp[n++] = {(uint64_t)off, -r.pos0, r.kc1, ci, ri, 1, 0, 0, 0, 0, 0, 0, 0};
             } else {
                 const bool whole = r.kc0 == 0 && r.kc1 == r.klen;
-                tmp[n++] = {(uint64_t)(off + pa), r.kc0, r.kc1, ci, ri, (uint8_t)!whole, 0, 0, 0, 0, 0, 0};
+                tmp[n++] = {(uint64_t)(off + pa), r.kc0, r.kc1, ci, ri, (uint8_t)!whole, 0, 0, 0, 0, 0, 0, 0};
             }
             nrd[r.ref] += n;
         }
         if (any_key) {   // (a read with events but nothing counted: a zero-span piece at its first key)
-            if (n == 0) tmp[n++] = {kmin, 0, 0, ci, ri, 1, 0, 0, 0, 0, 0, 0};
+            if (n == 0) tmp[n++] = {kmin, 0, 0, ci, ri, 1, 0, 0, 0, 0, 0, 0, 0};
             tmp[0].ins = 1;
             tmp[0].kmin = (uint32_t)kmin;
             tmp[0].kmax = (uint32_t)kmax;
@@ -1905,7 +1925,9 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
             for (int64_t k = k0; k < k1; k++) {
                 Piece &q = pcs[k];
                 const int64_t span = q.kb - q.ka;
-                q.lng = span > S;
+                // long: a span past the window, or a piece too big for a quarter of k_tile's
+                // per-wave chunk (its runs then come from k_reads through the long lists)
+                q.lng = span > S || q.nslots > S2C_CHUNK_RECS / 4 || 4 * (uint64_t)(q.qlen / 16) + 32 > S2C_CHUNK_QBYTES / 4;
                 if (!q.lng && span > 0) kk = std::max<int64_t>(kk, (int64_t)(((q.gpos + span - 1) >> 5) - (q.gpos >> 5)));
             }
             tk[t] = kk;
@@ -2177,11 +2199,11 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
         }
 
     clk.mark("ins plan");
-    // ---- work items: per tile its layers (k_tile's LDS chunks; lane groups of G = 256 / nwp
+    // ---- work items: per tile its layers (k_tile's per-wave LDS chunks; lane groups of G = 64 / nwp
     //      lanes per word) split into items ----
     int64_t nwp = 8;
     while (nwp * 32 < tile_max) nwp *= 2;
-    const int64_t G = 256 / nwp;
+    const int64_t G = 64 / nwp;   // (counting lanes per word of one wave: each wave runs its own layers)
     I.chunk = 0;   // (the most layers of any tile)
     PieceBlocks PB;
     piece_blocks(b, PB);
@@ -2234,14 +2256,13 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     }
     for (int64_t t = 0; t < NT; t++) {
         const Tile &T = tiles[t];
-        const int64_t nlg = lcnt[t + 1] - lcnt[t];
         const int64_t maxc = t_maxc[t], nl = t_nl[t], nch = t_nch[t];
         I.chunk = std::max<int64_t>(I.chunk, nl);
         runs_max = std::max(runs_max, t_wruns[t]);
         uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
         uint32_t fl = nch > 1 ? S2C_TILE_DEEP : 0u;
         if (nev[t] > S2C_EPI_KEYS || (int64_t)ccap[t] > lcols) fl |= S2C_TILE_GENERAL;
-        if (fl == 0 && nev[t] == 0 && nlg == 0 && maxc <= 255 && !no_dense && dense_fits(tw, K) &&
+        if (fl == 0 && nev[t] == 0 && maxc <= 255 && !no_dense && dense_fits(tw, K) &&
             dense_bytes(tw, K) <= dense_cap)
             fl = S2C_TILE_DENSE;
         const uint32_t bcap = nshort[t] ? pow2_at_least(2 * (uint64_t)nshort[t]) : 0u;
@@ -2468,7 +2489,7 @@ static int s2c_batch_layers_impl(s2c_batch *b) {
     while (nwp * 32 < b->info.tile_max) nwp *= 2;
     PieceBlocks PB;
     piece_blocks(b, PB);
-    build_layers(b, PB, 256 / nwp);
+    build_layers(b, PB, 64 / nwp);
     b->layers = true;
     return S2C_OK;
 }

@@ -91,7 +91,7 @@ __global__ __launch_bounds__(WG) void k_reads(const ReadsArgs d) {
     uint4 *out = (uint4 *)d.runs;
     walk_piece(GlobalMem{d.ops, d.bq, d.bx}, P, oend, d.maxdel_active != 0, d.maxdel,
                [&](uint32_t j, uint32_t g, uint32_t l, uint32_t k, uint64_t q) {
-                   if (runs) out[j] = make_uint4(g, l | (k << 24), (uint32_t)q, (uint32_t)(q >> 32));
+                   if (runs) out[j] = make_uint4(g, l | (k << S2C_RUN_KSHIFT), (uint32_t)q, (uint32_t)(q >> 32));
                },
                [&](uint64_t gkey, uint64_t q, uint32_t len) { add_event(d, gkey, q, len); });
 }

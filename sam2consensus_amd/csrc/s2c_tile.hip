@@ -629,15 +629,18 @@ __device__ __forceinline__ void tile_epilogue_fast(const D &d, uint32_t tile, co
 // The tile's WINDOW — the short pieces starting in the kwin words before it and in it — is
 // cut into nl LAYERS (host plan, s2c_host.cpp plan_layers): layer ℓ takes from every start
 // word s of the window (a SEGMENT) its pieces [ps[s] + n_s·ℓ/nl, ps[s] + n_s·(ℓ+1)/nl), so
-// every layer reaches every word of the tile alike.  One layer at a time is a CHUNK in LDS:
-//   1 table  per segment its piece, op-slot and base-plane ranges and their LDS offsets
-//   2 DMA    each segment's base planes {p0, p1} into LDS (16-byte LDS-DMA, the source in
-//            SGPRs; the waves take segments round-robin)
-//   3 walk   thread per piece: the parsecigar token walk (:64-81) with the maxdel rule (:210)
-//            → one run record per op word in LDS {gpos, q << 11 | len} (q: the run's first
-//            base in the LDS planes); coverage and counted '-' runs (D/N/P) into position
-//            difference arrays; the N / '-' chars of SEQ (:212, :217) into the histogram
-//   4 count  lane (word w, g of G) takes the records of segments W-kwin .. W — one
+// every layer reaches every word of the tile alike.  Each WAVE of the workgroup takes every
+// WV-th layer of the item into its own LDS chunk and runs it start to end with no
+// workgroup barrier (the waves only meet in the shared histogram and difference arrays,
+// by atomics), so one wave's DMA wait or walk overlaps the others' counting:
+//   1 DMA    the layer's piece records, op words, base planes {p0, p1} and non-ACGT words,
+//            each one contiguous range (16-byte LDS-DMA issued by the wave, the source
+//            offset in SGPRs)
+//   2 walk   lane per piece: the parsecigar token walk (:64-81) with the maxdel rule (:210)
+//            → one run record per op word {gpos, q << 11 | len} (q: the run's first base in
+//            the LDS planes); coverage and counted '-' runs (D/N/P) into position difference
+//            arrays; the N / '-' chars of SEQ (:212, :217) into the histogram
+//   3 count  lane (word w, g of G = 64 / NWP) takes the records of segments W-kwin .. W — one
 //            contiguous LDS range — g, g + G, ..., 8 at a time: two plane words from LDS,
 //            funnel shift, masks X = p0 (C|T), Y = p1 (G|T), Z = X & Y (T) into Harley–Seal
 //            carry-save counters (8 bit-planes each)
@@ -649,18 +652,19 @@ __device__ __forceinline__ void tile_epilogue_fast(const D &d, uint32_t tile, co
 // the tile's long list.  Then the epilogue (a single-item tile) or the counts to HBM.
 constexpr int GS = 8;                 // records per counting group
 constexpr int CSEG = S2C_CHUNK_SEGS;  // segments of a window (≤ 64 words + kwin ≤ 32)
-constexpr uint32_t RPAD = 256;        // zero records after a chunk's last (a group's reads past it)
+constexpr uint32_t RPAD = 64;         // zero records after a chunk's last (a group's reads past it: ≤ 7·G ≤ 56)
+constexpr uint32_t WV = WG / 64;      // waves per workgroup (each its own chunk)
 // raw histogram slots while counting ("-ACGNT" slots after the reconstruction)
 constexpr uint32_t SL_SDC = 0, SL_SD = 1, SL_X = 2, SL_Y = 3, SL_N = 4, SL_Z = 5;
 // A buffer offset past every buffer (their sizes stay below it, checked on the host) that
 // still leaves room for the loads' immediate offsets: the hardware returns zeros.
 constexpr uint32_t OOR = 0xF0000000u;
 
-// A chunk in LDS: one layer of the tile's window, DMA'd as four contiguous ranges — its
-// piece records (into runl, read before the walk writes run records there), op words (ol),
-// base planes (pl; a 16-byte pad first, so plane word −1 is readable) and non-ACGT words
-// (xl), each landing at its source's 16-byte phase.  segR[σ]: the first run record of the
-// layer's pieces starting in word S0 + σ (pieces are in start-word order).
+// A wave's chunk in LDS: one layer of the tile's window, DMA'd as four contiguous ranges —
+// its piece records (into runl, read before the walk writes run records there), op words
+// (ol), base planes (pl; a 16-byte pad first, so plane word −1 is readable) and non-ACGT
+// words (xl), each landing at its source's 16-byte phase.  segR[σ]: the first run record of
+// the layer's pieces starting in word S0 + σ (pieces are in start-word order).
 struct ChunkLds {
     uint32_t segR[CSEG + 1];
     alignas(16) uint8_t pl[16 + S2C_CHUNK_QBYTES + 16];
@@ -693,16 +697,16 @@ __device__ __forceinline__ DmaSrc dma_src(const void *p, const void *end) {
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"   // m0 (reserved) is set and clobbered by the DMA
 // n dwords src[0..n) of source array S → the 16-byte aligned LDS region dst by 16-byte
-// LDS-DMA, the 1 KB blocks split between the workgroup's waves (offsets in SGPRs); the copy
+// LDS-DMA issued by the calling wave, 1 KB per instruction (offsets in SGPRs); the copy
 // starts at the 16-byte boundary below src, so the dwords land at dst + (src & 15).
-// Arguments workgroup-uniform.  Completion: s_waitcnt vmcnt(0) (the compiler does not count
-// these loads), then a barrier.
-__device__ __forceinline__ void dma16_wg(uint8_t *dst, const DmaSrc &S, const uint32_t *src, uint32_t n) {
-    const uint32_t lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
+// Arguments wave-uniform.  Completion: s_waitcnt vmcnt(0) (the compiler does not count these
+// loads): the wave's own LDS reads then see the data.
+__device__ __forceinline__ void dma16_wave(uint8_t *dst, const DmaSrc &S, const uint32_t *src, uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63;
     const uintptr_t sal = (uintptr_t)src & ~(uintptr_t)15;
     const uint32_t nbytes = uni((uint32_t)((uintptr_t)src - sal) + 4 * n);
     const uint32_t soff = uni((uint32_t)(sal - S.base)), m0 = uni(lds_byte_addr(dst));
-    for (uint32_t base = 1024 * wv; base < nbytes; base += 1024 * (WG / 64)) {
+    for (uint32_t base = 0; base < nbytes; base += 1024) {
         if (base + 16 * lane < nbytes)
             asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
                          :: "s"(m0 + base), "v"(16 * lane), "s"(S.r), "s"(soff + base) : "memory", "m0");
@@ -717,9 +721,12 @@ struct EpiLds {
 };
 template <uint32_t ICOL>
 union TileLds {
-    ChunkLds c;
+    ChunkLds c[WV];   // one chunk per wave
     EpiLds<ICOL> e;
 };
+// A wave's LDS hand-off between its own lanes (no other wave involved): the wave's LDS
+// operations complete in order, and the compiler keeps its memory accesses on either side.
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // The N / '-' chars of SEQ among LDS plane bases [q, q + l), whose first lies at
 // tile-relative position r0: 'N' (counted as A by the planes) into SL_N; '-' (counted as C)
@@ -859,7 +866,7 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
 #endif
 template <int NWP>
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 3 : 2))) void k_tile(const TileArgs d, const uint32_t *items) {
-    constexpr int G = WG / NWP, HP = 17 * NWP;
+    constexpr int HP = 17 * NWP;
     constexpr uint32_t NPOS = 32 * NWP;
     using H = Hist<NWP>;
     constexpr uint32_t ICOL = S2C_LDS_COLS(NWP);
@@ -868,9 +875,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     __shared__ int32_t dV[NPOS + 1], dD[NPOS + 1];
     __shared__ uint32_t wtot[2][WG / 64];
     __shared__ __attribute__((aligned(16))) TileLds<ICOL> U;
-    ChunkLds &C = U.c;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const uint32_t w = tid / G, g = tid % G;
 #ifdef S2C_PROF
     unsigned long long tprof_t = 0;
 #endif
@@ -887,8 +892,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     const TileRec T = tile_rec(d.tiles, tile);
     const uint32_t nl = uni(d.tiles[(size_t)tile * S2C_TILE_WORDS + 19]);
     const uint32_t a = T.a, n = T.b - T.a;
-    const uint32_t W0 = a >> 5, nwords = (n + 31) / 32, W = W0 + w;
-    const bool active = w < nwords;
+    const uint32_t W0 = a >> 5, nwords = (n + 31) / 32;
     const uint32_t K = d.kwin;
     const uint32_t S0 = W0 >= K ? W0 - K : 0u, NS = W0 + nwords - S0;
     const bool counts_only = d.mode != MODE_RUN;
@@ -914,26 +918,27 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     for (int b = 0; b < 8; b++) X[b] = Y[b] = Z[b] = 0;
     uint32_t acc = 0;   // records counted per lane since the last flush (wave-uniform bound)
     // flush: counters → bytes (R[r] byte j = count of position 8j + r) → u16 pairs of the
-    // histogram; the G lanes of a word pre-reduced by DPP row shifts while a byte cannot carry
-    auto flush = [&]() {
+    // histogram for the lane's word wd (lane gg of gn of the word, consecutive lanes); the
+    // gn lanes pre-reduced by DPP row shifts while a byte cannot carry
+    auto flush = [&](uint32_t wd, uint32_t gg, uint32_t gn, bool act) {
         transpose8(X);
         transpose8(Y);
         transpose8(Z);
         uint32_t red = 1;
         auto shr1 = [](uint32_t &v) { v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true); };
         auto shr2 = [](uint32_t &v) { v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true); };
-        if (acc < 128) {
+        if (acc < 128 && gn >= 2) {
             red = 2;
 #pragma unroll
             for (int r = 0; r < 8; r++) { shr1(X[r]); shr1(Y[r]); shr1(Z[r]); }
-            if (acc < 64) {
+            if (acc < 64 && gn >= 4) {
                 red = 4;
 #pragma unroll
                 for (int r = 0; r < 8; r++) { shr2(X[r]); shr2(Y[r]); shr2(Z[r]); }
             }
         }
-        if (active && (g % red) == red - 1) {
-            uint32_t *h0 = hist + 17 * w;
+        if (act && (gg % red) == red - 1) {
+            uint32_t *h0 = hist + 17 * wd;
             auto add = [&](uint32_t sym, const uint32_t (&R)[8]) {
                 uint32_t *hw = h0 + sym * HP;
 #pragma unroll
@@ -952,10 +957,15 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
         acc = 0;
     };
 
-    // this lane's word reads the records of segments [sa, sb] (start words W - K .. W)
-    const uint32_t sa = active ? (W >= S0 + K ? W - K : S0) - S0 : 1u, sb = active ? W - S0 : 0u;
+    // ---- the wave's layers: lane (word ww, ga of GW) of the wave's own chunk
+    constexpr uint32_t GW = 64 / NWP;
+    const uint32_t ww = lane / GW, ga = lane % GW, Ww = W0 + ww;
+    const bool wact = ww < nwords;
+    ChunkLds &C = U.c[wv];
+    // this lane's word reads the records of segments [sa, sb] (start words Ww - K .. Ww)
+    const uint32_t sa = wact ? (Ww >= S0 + K ? Ww - K : S0) - S0 : 1u, sb = wact ? Ww - S0 : 0u;
     const uint2 *bql = (const uint2 *)(C.pl + 16);
-    const int32_t W32 = (int32_t)(32 * W);
+    const int32_t W32 = (int32_t)(32 * Ww);
     // one group's records → carry-save trees of X, Y, Z; NR = 8: weight-8 carries in t8o,
     // NR = 4 (a tail group): weight-4 carries
     auto count_group = [&](const uint2 (&rv)[GS], uint32_t (&t8o)[3], auto nr) {
@@ -1015,8 +1025,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     using Full = std::integral_constant<int, 8>;
     using Half = std::integral_constant<int, 4>;
 
-    // ---- the layers: in place (one layer: the window of the sorted arrays) or the tile's
-    //      copies in the layered arrays
+    // the layers: in place (one layer: the window of the sorted arrays) or the tile's copies
+    // in the layered arrays
     const uint32_t ly0 = uni(d.tiles[(size_t)tile * S2C_TILE_WORDS + 20]);
     const bool inplace = ly0 == S2C_LY_MAIN;
     const uint32_t *const spc = inplace ? d.pc : d.lpc, *const sops = inplace ? d.ops : d.lops;
@@ -1026,7 +1036,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     const uint32_t *const xl = (const uint32_t *)C.xl;
     const uint32_t *const opl = (const uint32_t *)C.ol;
     const uint4 *const pcr = (const uint4 *)C.runl;
-    for (uint32_t ly = l0; ly < l1; ly++) {
+    for (uint32_t ly = l0 + wv; ly < l1; ly += WV) {
         // ---- 1. the layer: pieces [P0, P1), op words [O0, O1), plane words [qa, qb)
         uint32_t P0, P1, O0, O1, qa, qb;
         if (inplace) {
@@ -1039,15 +1049,14 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
             qb = ((uni(B.z) + 1u) >> 1) + 1u;   // through the word after the last base (funnel)
         }
         const uint32_t NPc = P1 - P0, NR = O1 - O0;
-        dma16_wg((uint8_t *)C.runl, Dpc, spc + 4 * (size_t)P0, 4 * NPc);
-        dma16_wg(C.ol, Dops, sops + O0, NR);
-        dma16_wg(C.pl + 16, Dbq, sbq + 2 * (size_t)qa, 2 * (qb - qa));
-        dma16_wg(C.xl, Dbx, sbx + qa, qb - qa);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        lds_sync();
+        dma16_wave((uint8_t *)C.runl, Dpc, spc + 4 * (size_t)P0, 4 * NPc);
+        dma16_wave(C.ol, Dops, sops + O0, NR);
+        dma16_wave(C.pl + 16, Dbq, sbq + 2 * (size_t)qa, 2 * (qb - qa));
+        dma16_wave(C.xl, Dbx, sbx + qa, qb - qa);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the wave's own DMA: its LDS reads see it)
         TPROF_MARK(2);
-        // ---- 2. walk: thread per piece (records to registers first: their region becomes
-        //      the run records); the per-word record ranges from the pieces' start words
+        // ---- 2. walk: lane per piece (records to registers first: their region becomes the
+        //      run records); the per-word record ranges from the pieces' start words
         const uint32_t od = (O0 & 3u) - O0;                     // op word j at opl[j + od]
         const uint32_t qadj = 32u * (qa & 1u) - 32u * qa;       // SEQ[0] at LDS plane base 16·qh + qadj
         const uint32_t xd = (qa & 3u) - (qa & 1u);              // non-ACGT word of LDS plane word v: xl[v + xd]
@@ -1055,7 +1064,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
         uint32_t oe[2];
 #pragma unroll
         for (int u = 0; u < 2; u++) {
-            const uint32_t i = tid + WG * u;
+            const uint32_t i = lane + 64 * u;
             Pw[u] = make_uint4(0u, 0u, 0u, 0u);
             oe[u] = 0;
             if (i < NPc) {
@@ -1069,12 +1078,12 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
             }
         }
         if (NPc == 0)
-            for (uint32_t sg = tid; sg <= NS; sg += WG) C.segR[sg] = 0;
-        lds_sync();
-        for (uint32_t i = tid; i < RPAD; i += WG) C.runl[NR + i] = make_uint2(0u, 0u);
+            for (uint32_t sg = lane; sg <= NS; sg += 64) C.segR[sg] = 0;
+        wave_lds_sync();   // (the piece records are read before run records overwrite them)
+        for (uint32_t i = lane; i < RPAD; i += 64) C.runl[NR + i] = make_uint2(0u, 0u);
 #pragma unroll
         for (int u = 0; u < 2; u++) {
-            if (tid + WG * u >= NPc) continue;
+            if (lane + 64 * u >= NPc) continue;
             const uint4 P = Pw[u];
             const uint32_t fl = P.w >> 24, len = P.w & 0xFFFFFFu, rPre = P.z - O0;
             const uint32_t ql = 16u * P.y + qadj;
@@ -1095,23 +1104,23 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
                                       (uint32_t)d.maxdel, a, n, hist, dV, dD);
             }
         }
-        lds_sync();
+        wave_lds_sync();   // every run record written
         TPROF_MARK(3);
-        // ---- 3. count this lane's records cw0 + g + G·m < cw1 (reads past them: records of
-        //      pieces starting after W, or the zero pad — they cover nothing of W)
+        // ---- 3. count this lane's records cw0 + ga + GW·m < cw1 (reads past them: records of
+        //      pieces starting after Ww, or the zero pad — they cover nothing of Ww)
         const uint32_t cw0 = C.segR[sa], cw1 = C.segR[sb + 1];
-        const uint32_t nrec = cw0 + g < cw1 ? (cw1 - cw0 - g + G - 1) / G : 0u;
+        const uint32_t nrec = cw0 + ga < cw1 ? (cw1 - cw0 - ga + GW - 1) / GW : 0u;
         const uint32_t nmx = uni(__ockl_wfred_max_u32(nrec));
         const uint32_t ngrp = nmx / GS + ((nmx % GS) > 4u ? 1u : 0u);
         const bool half = (nmx % GS) != 0u && (nmx % GS) <= 4u;
         const uint32_t add_recs = GS * ngrp + (half ? 4u : 0u);
-        if (acc + add_recs > 255u) flush();
+        if (acc + add_recs > 255u) flush(ww, ga, GW, wact);
         acc += add_recs;
         const uint32_t rend = NR;
         auto load_runs = [&](uint2 (&rv)[GS], uint32_t gi) {
-            const uint2 *rb = C.runl + min(cw0 + g + G * GS * gi, rend);
+            const uint2 *rb = C.runl + min(cw0 + ga + GW * GS * gi, rend);
 #pragma unroll
-            for (int u = 0; u < GS; u++) rv[u] = rb[G * u];
+            for (int u = 0; u < GS; u++) rv[u] = rb[GW * u];
         };
         uint2 ra[GS], rb2[GS];
         if (ngrp) load_runs(ra, 0);
@@ -1139,17 +1148,23 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
             close4(Y, t4[1]);
             close4(Z, t4[2]);
         }
-        lds_sync();   // the chunk's LDS is rewritten by the next layer
+        wave_lds_sync();   // the chunk is rewritten by the wave's next layer
         TPROF_MARK(4);
     }
+    if (acc) flush(ww, ga, GW, wact);
+    lds_sync();   // every wave's layers counted (hist, dV, dD complete but for the long pieces)
 
+    // the workgroup's lanes for the long pieces: word w, lane g of G = 256 / NWP
+    constexpr uint32_t G = WG / NWP;
+    const uint32_t w = tid / G, g = tid % G, W = W0 + w;
+    const bool active = w < nwords;
     // ---- long-piece records (rare; k_reads' run records through the tile's long list,
     //      counted once per tile: by its first item), one per lane and round
     {
         const uint32_t nlong = l0 == 0 ? T.lp1 - T.lp0 : 0u;
         const uint32_t ntr = uni(__ockl_wfred_max_u32(active && g < nlong ? (nlong - g + G - 1) / G : 0u));
         for (uint32_t m = 0; m < ntr; m++) {
-            if (acc >= 255u) flush();
+            if (acc >= 255u) flush(w, g, G, active);
             acc++;
             const uint32_t j = g + G * m;
             if (!(active && j < nlong)) continue;
@@ -1187,7 +1202,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
             }
         }
     }
-    if (acc) flush();
+    if (acc) flush(w, g, G, active);
     lds_sync();
     TPROF_MARK(5);
     // ---- difference arrays → coverage and '-' per position (inclusive scans, thread blocks

@@ -41,16 +41,76 @@ def _ptr(t):
     return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p()
 
 
+class Uploader:
+    """H2D of packed batches through pinned host staging: a ring of ``nbuf`` pinned buffers and
+    a copy stream.  ``upload(hb)`` packs the batch's arrays into the next staging buffer (after
+    that buffer's previous copy has completed), copies them to ONE device allocation on the
+    copy stream and makes the compute stream wait on the copy's event, so the host can go on
+    (parsing the next batch) while the copy and the kernels run."""
+
+    ALIGN = 256
+
+    def __init__(self, device=None, nbuf=2):
+        self.device = _dev(device)
+        self.copy_stream = torch.cuda.Stream(self.device)
+        self.slots = [None] * nbuf      # pinned uint8 tensors
+        self.events = [None] * nbuf     # the copy out of each slot
+        self.k = 0
+
+    def _layout(self, arrays):
+        offs, total = [], 0
+        for a in arrays:
+            offs.append(total)
+            total += (max(a.nbytes, 16) + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+        return offs, max(total, self.ALIGN)
+
+    def upload(self, arrays):
+        """numpy arrays → device uint8 views (each 256-byte aligned, ≥ 16 bytes, zero-padded
+        to its 16-byte end), in HBM once the compute stream reaches this point."""
+        arrays = [np.ascontiguousarray(a) for a in arrays]
+        offs, total = self._layout(arrays)
+        i = self.k % len(self.slots)
+        self.k += 1
+        if self.events[i] is not None:
+            self.events[i].synchronize()          # this slot's previous copy has left it
+        if self.slots[i] is None or self.slots[i].numel() < total:
+            self.slots[i] = torch.empty(int(total * 1.25) + (1 << 20), dtype=torch.uint8, pin_memory=True)
+        host = self.slots[i].numpy()
+        for a, o in zip(arrays, offs):
+            n = a.nbytes
+            host[o:o + n] = a.reshape(-1).view(np.uint8)
+            pad = (-n) % 16 or (16 if n == 0 else 0)
+            host[o + n:o + n + pad] = 0
+        compute = torch.cuda.current_stream(self.device)
+        dev = torch.empty(total, dtype=torch.uint8, device=self.device)   # (on the compute stream)
+        self.copy_stream.wait_stream(compute)     # the allocation is free on the compute stream
+        with torch.cuda.stream(self.copy_stream):
+            dev.copy_(self.slots[i][:total], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.copy_stream)
+        dev.record_stream(self.copy_stream)
+        self.events[i] = ev
+        compute.wait_event(ev)
+        return [dev[o:o + max(a.nbytes, 16)] for a, o in zip(arrays, offs)], dev
+
+
 class DeviceBatch:
-    """The packed batch resident in HBM (inputs of every launch)."""
+    """The packed batch resident in HBM (inputs of every launch).  With an ``Uploader`` the
+    arrays go through its pinned staging buffers and copy stream (asynchronous); without,
+    each array is copied synchronously."""
 
     ARRAYS = ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile", "rlist", "ps",
               "lly", "lpc", "lops", "lbq", "lbx")
 
-    def __init__(self, hb, device=None):
-        self.device = _dev(device)
+    def __init__(self, hb, device=None, uploader=None):
+        self.device = _dev(device) if uploader is None else uploader.device
         self.hb = hb.ensure_layers()
         self.info = hb.info
+        if uploader is not None:
+            views, self._storage = uploader.upload([np.asarray(getattr(hb, n)).reshape(-1) for n in self.ARRAYS])
+            for name, v in zip(self.ARRAYS, views):
+                setattr(self, name, v)
+            return
         for name in self.ARRAYS:
             setattr(self, name, _up(np.asarray(getattr(hb, name)).reshape(-1), self.device))
 
@@ -193,7 +253,7 @@ class Workspace:
 
         stats[r, t] = Σ over reference r's tiles of the device's per-tile statistics
         (tiles never straddle a reference; :352-397 sums)."""
-        torch.cuda.synchronize(self.db.device)
+        torch.cuda.current_stream(self.db.device).synchronize()
         i = self.db.info
         R, T, nb = i.n_refs, self.T, i.n_tiles
         stats = np.zeros((R, T, 4), dtype=np.uint64)

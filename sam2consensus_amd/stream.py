@@ -105,34 +105,63 @@ class StreamResult:
         self.held_max = held_max      # most reads the parser held at a snapshot
 
 
-def stream_batches(blocks, thresholds, runner, maxdel_active=True, tile_width=DEFAULT_TILE,
-                   batch_bytes=DEFAULT_BATCH, stats_hook=None):
-    """Run ``runner(sub) -> (stats, offs, out)`` over the streamed tile ranges of the SAM
-    text in ``blocks`` (an iterable of bytes).  Raises NotSorted for unsorted input."""
-    T = len(thresholds)
-    p = StreamParser(maxdel_active, 150, tile_width)
-    parts, stats, cov = [], None, None
-    t_done, pending, broken = 0, 0, False
-    lines = mapped = 0
-    held_max = 0
+_END = object()
 
-    def run(hb, t0, t1):
-        nonlocal stats
-        sub = _sub(hb, t0, t1)
+
+class _Producer:
+    """The parser side of a streamed run on its own host thread: it feeds the blocks, takes
+    the snapshots, cuts the sub-batches and retains, handing each item to the consumer (the
+    device side, on the calling thread) through a bounded queue — so parsing batch k + 1
+    overlaps batch k's upload, kernels and fetch.  libs2c.so's calls release the GIL (ctypes).
+    An exception ends the thread and is re-raised by the consumer in order."""
+
+    def __init__(self, gen, depth=2):
+        import queue
+        import threading
+        self.q = queue.Queue(maxsize=depth)
+        self.stop = threading.Event()
+        self.t = threading.Thread(target=self._run, args=(gen,), daemon=True)
+        self.t.start()
+
+    def _put(self, item):
+        import queue
+        while not self.stop.is_set():
+            try:
+                self.q.put(item, timeout=0.1)
+                return True
+            except queue.Full:
+                continue
+        return False
+
+    def _run(self, gen):
         try:
-            st, offs, out = runner(sub)
+            for item in gen:
+                if not self._put(("item", item)):
+                    gen.close()
+                    return
+            self._put(("end", None))
+        except BaseException as e:  # noqa: BLE001 - re-raised on the consumer thread
+            self._put(("error", e))
+
+    def __iter__(self):
+        try:
+            while True:
+                kind, v = self.q.get()
+                if kind == "end":
+                    return
+                if kind == "error":
+                    raise v
+                yield v
         finally:
-            sub.free()
-        stats = st.copy() if stats is None else stats + st
-        parts.append((t0, t1, np.asarray(offs, dtype=np.uint64), out))
+            self.stop.set()
+            self.t.join()
 
-    def absorb(hb):
-        nonlocal cov, lines, mapped
-        flag = (hb.ref_reads > 0)
-        cov = flag.copy() if cov is None else (cov | flag)
-        lines += int(hb.info.lines_total)
-        mapped += int(hb.info.reads_mapped)
 
+def _sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, state):
+    """Generator (producer thread) of the streamed run of sorted input: ("run", sub, t0, t1)
+    for every final tile range, then ("last", hb) with the final batch."""
+    p = StreamParser(maxdel_active, 150, tile_width)
+    t_done, pending, broken = 0, 0, False
     try:
         for blk in blocks:
             p.feed(blk)
@@ -147,7 +176,7 @@ def stream_batches(blocks, thresholds, runner, maxdel_active=True, tile_width=DE
                 continue
             try:
                 late, ref, pos0, held = p.state()
-                held_max = max(held_max, held)
+                state["held_max"] = max(state["held_max"], held)
                 if late:
                     raise NotSorted("a read reaches positions already emitted")
                 if ref < 0:
@@ -157,10 +186,11 @@ def stream_batches(blocks, thresholds, runner, maxdel_active=True, tile_width=DE
                 t1 = int(np.searchsorted(hb.tiles[:, 1].astype(np.int64), bound, side="right"))
                 if t1 <= t_done:
                     continue
-                run(hb, t_done, t1)
-                absorb(hb)
+                sub = _sub(hb, t_done, t1)
+                state["absorb"](hb)
                 gmin = int(hb.tiles[t1, 0]) if t1 < NT else int(hb.info.padded_len)
                 p.retain(gmin)
+                yield ("run", sub, t_done, t1)
                 t_done = t1
                 if stats_hook:
                     stats_hook(t_done, NT, held)
@@ -168,47 +198,102 @@ def stream_batches(blocks, thresholds, runner, maxdel_active=True, tile_width=DE
                 hb.free()
         hb = p.finish()
         late, _, _, held = p.state()
-        held_max = max(held_max, held)
+        state["held_max"] = max(state["held_max"], held)
         if late:
             hb.free()
             raise NotSorted("a read reaches positions already emitted")
         NT = int(hb.info.n_tiles)
         if t_done < NT:
-            run(hb, t_done, NT)
-        absorb(hb)
+            yield ("run", _sub(hb, t_done, NT), t_done, NT)
+        state["absorb"](hb)
+        yield ("last", hb)
     finally:
         p.close()
-    hb.ref_reads = cov.astype(np.int64)          # Σcoverage > 0 in any batch (:334-341)
+
+
+def stream_batches(blocks, thresholds, runner, maxdel_active=True, tile_width=DEFAULT_TILE,
+                   batch_bytes=DEFAULT_BATCH, stats_hook=None):
+    """Run ``runner`` over the streamed tile ranges of the SAM text in ``blocks`` (an
+    iterable of bytes): ``runner(sub) -> (stats, offs, out)``, or, if it has a ``launch``
+    method, ``runner.launch(sub) -> handle`` with ``handle.result() -> (stats, offs, out)``
+    collected one batch later (batch k's results are fetched after batch k + 1 is launched).
+    The parse runs on a producer thread (``_Producer``).  Raises NotSorted for unsorted input."""
+    T = len(thresholds)
+    parts = []
+    stats = None
+    state = {"held_max": 0, "cov": None, "lines": 0, "mapped": 0}
+
+    def absorb(hb):
+        flag = (hb.ref_reads > 0)
+        state["cov"] = flag.copy() if state["cov"] is None else (state["cov"] | flag)
+        state["lines"] += int(hb.info.lines_total)
+        state["mapped"] += int(hb.info.reads_mapped)
+    state["absorb"] = absorb
+
+    launch = getattr(runner, "launch", None)
+    pend = []            # (t0, t1, handle) launched, not yet collected
+
+    def collect(entry):
+        nonlocal stats
+        t0, t1, h, sub = entry
+        try:
+            st, offs, out = h.result() if launch else h
+        finally:
+            sub.free()             # (the fetch reads the sub-batch's tile table)
+        stats = st.copy() if stats is None else stats + st
+        parts.append((t0, t1, np.asarray(offs, dtype=np.uint64), out))
+
+    hb = None
+    for item in _Producer(_sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, state)):
+        if item[0] == "last":
+            hb = item[1]
+            break
+        _, sub, t0, t1 = item
+        sub.t0, sub.t1 = t0, t1
+        try:
+            h = launch(sub) if launch else runner(sub)
+        except BaseException:
+            sub.free()
+            raise
+        pend.append((t0, t1, h, sub))
+        while len(pend) > 1:
+            collect(pend.pop(0))
+    while pend:
+        collect(pend.pop(0))
+    hb.ref_reads = state["cov"].astype(np.int64)          # Σcoverage > 0 in any batch (:334-341)
     offs, out = _merge(parts, T)
     if stats is None:
         stats = np.zeros((hb.info.n_refs, T, 4), np.uint64)
-    return StreamResult(hb, stats, offs, out, int(hb.info.header_lines), lines, mapped,
-                        [(a, b) for a, b, _, _ in parts], held_max)
+    return StreamResult(hb, stats, offs, out, int(hb.info.header_lines), state["lines"], state["mapped"],
+                        [(a, b) for a, b, _, _ in parts], state["held_max"])
 
 
 class DeviceAccumulator:
-    """Running totals counts[6][padded_len] u32 in HBM for unsorted input: ``add`` runs a
-    batch's pileup into them (s2c_accumulate), ``finish`` adds the last batch and votes every
-    tile from them (s2c_consensus over all tiles)."""
+    """Running totals counts[6][padded_len] u32 in HBM for unsorted input: ``add`` enqueues a
+    batch's pileup into them (s2c_accumulate; the batch goes through the pinned staging ring
+    and copy stream, nothing waits), ``finish`` adds the last batch and votes every tile from
+    them (s2c_consensus over all tiles)."""
 
     def __init__(self, thresholds, min_depth=1, fill=b"-", device=None):
         self.thresholds, self.min_depth, self.fill, self.device = thresholds, min_depth, fill, device
         self.counts = None
+        self.up = None
 
     def _ws(self, hb):
         import torch
 
-        from .engine import DeviceBatch, Workspace
-        db = DeviceBatch(hb, self.device)
+        from .engine import DeviceBatch, Uploader, Workspace
+        if self.up is None:
+            self.up = Uploader(self.device)
+        db = DeviceBatch(hb, uploader=self.up)
         if self.counts is None:
             self.counts = torch.zeros(max(6 * int(hb.info.padded_len) * 4, 16), dtype=torch.uint8, device=db.device)
         return Workspace(db, self.thresholds, self.min_depth, self.fill, counts=self.counts)
 
     def add(self, hb):
-        import torch
-        ws = self._ws(hb)
-        ws.accumulate(keep_tables=False)
-        torch.cuda.synchronize(ws.db.device)   # the batch's buffers are freed after this
+        # (the batch's device buffers are released in stream order after its kernels; the
+        # host arrays were copied into pinned staging by the upload)
+        self._ws(hb).accumulate(keep_tables=False)
 
     def finish(self, hb):
         ws = self._ws(hb)
@@ -217,25 +302,11 @@ class DeviceAccumulator:
         return ws.fetch()
 
 
-def stream_unsorted(blocks, thresholds, acc, maxdel_active=True, batch_bytes=DEFAULT_BATCH):
-    """Unsorted input in bounded host memory: every ``batch_bytes`` the reads held are
-    counted into the accumulator's running totals and dropped, except their insertion
-    events (``s2c_parser_retain_events``); the last batch holds every event of the file and
-    is voted over the totals.  Same bytes and error precedence as one batch: the read-pass
-    checks run as blocks are fed, and the last ``s2c_parser_finish`` sees every insertion
-    event for the checks of :284-294."""
+def _unsorted_items(blocks, maxdel_active, batch_bytes, state):
+    """Generator (producer thread) of the unsorted streamed run: ("add", hb) per batch, then
+    ("last", hb)."""
     p = StreamParser(maxdel_active, 150, 0)
-    cov = None
-    lines = mapped = pending = nb = held_max = 0
-    broken = False
-
-    def absorb(hb):
-        nonlocal cov, lines, mapped
-        flag = (hb.ref_reads > 0)
-        cov = flag.copy() if cov is None else (cov | flag)
-        lines += int(hb.info.lines_total)
-        mapped += int(hb.info.reads_mapped)
-
+    pending, broken = 0, False
     try:
         for blk in blocks:
             p.feed(blk)
@@ -246,28 +317,53 @@ def stream_unsorted(blocks, thresholds, acc, maxdel_active=True, batch_bytes=DEF
             _, ref, _, held = p.state()
             if ref < 0:
                 continue
-            held_max = max(held_max, held)
+            state["held_max"] = max(state["held_max"], held)
             try:
                 hb = p.snapshot()
             except (KeyError, IndexError):
                 broken = True          # raised by s2c_parser_finish once the input is read
                 continue
-            try:
-                acc.add(hb)
-                absorb(hb)
-            finally:
-                hb.free()
+            state["absorb"](hb)
             p.retain_events()
-            nb += 1
+            state["nb"] += 1
+            yield ("add", hb)
         hb = p.finish()
-        held_max = max(held_max, p.state()[3])
+        state["held_max"] = max(state["held_max"], p.state()[3])
+        yield ("last", hb)
     finally:
         p.close()
+
+
+def stream_unsorted(blocks, thresholds, acc, maxdel_active=True, batch_bytes=DEFAULT_BATCH):
+    """Unsorted input in bounded host memory: every ``batch_bytes`` the reads held are
+    counted into the accumulator's running totals and dropped, except their insertion
+    events (``s2c_parser_retain_events``); the last batch holds every event of the file and
+    is voted over the totals.  Same bytes and error precedence as one batch: the read-pass
+    checks run as blocks are fed, and the last ``s2c_parser_finish`` sees every insertion
+    event for the checks of :284-294.  The parse runs on a producer thread (``_Producer``)."""
+    state = {"held_max": 0, "cov": None, "lines": 0, "mapped": 0, "nb": 0}
+
+    def absorb(hb):
+        flag = (hb.ref_reads > 0)
+        state["cov"] = flag.copy() if state["cov"] is None else (state["cov"] | flag)
+        state["lines"] += int(hb.info.lines_total)
+        state["mapped"] += int(hb.info.reads_mapped)
+    state["absorb"] = absorb
+
+    hb = None
+    for kind, b in _Producer(_unsorted_items(blocks, maxdel_active, batch_bytes, state)):
+        if kind == "last":
+            hb = b
+            break
+        try:
+            acc.add(b)
+        finally:
+            b.free()
     stats, offs, out = acc.finish(hb)
     absorb(hb)
-    hb.ref_reads = cov.astype(np.int64)
-    return StreamResult(hb, stats, offs, out, int(hb.info.header_lines), lines, mapped,
-                        [(0, int(hb.info.n_tiles))] * (nb + 1), held_max)
+    hb.ref_reads = state["cov"].astype(np.int64)
+    return StreamResult(hb, stats, offs, out, int(hb.info.header_lines), state["lines"], state["mapped"],
+                        [(0, int(hb.info.n_tiles))] * (state["nb"] + 1), state["held_max"])
 
 
 def _merge(parts, T):
@@ -286,15 +382,40 @@ def file_blocks(filename, block=BLOCK):
             yield b
 
 
-def device_runner(thresholds, min_depth, fill, device=None):
-    """runner(sub) on the GPU: upload, s2c_run, fetch (sam2consensus_amd/engine.py)."""
-    from .engine import DeviceBatch, Workspace
+class DeviceRunner:
+    """The streamed batches' device side (sam2consensus_amd/engine.py): ``launch(sub)`` uploads
+    the sub-batch through the pinned staging ring and copy stream (``Uploader``) and enqueues
+    s2c_run on the compute stream without waiting; the handle's ``result()`` synchronises and
+    fetches.  ``runner(sub)`` does both at once."""
 
-    def runner(sub):
-        ws = Workspace(DeviceBatch(sub, device), thresholds, min_depth, fill)
+    def __init__(self, thresholds, min_depth, fill, device=None):
+        from .engine import Uploader
+        self.thresholds, self.min_depth, self.fill = thresholds, min_depth, fill
+        self.up = Uploader(device)
+
+    def launch(self, sub):
+        from .engine import DeviceBatch, Workspace
+        ws = Workspace(DeviceBatch(sub, uploader=self.up), self.thresholds, self.min_depth, self.fill)
         ws.run()
-        return ws.fetch()
-    return runner
+        return _Launched(ws)
+
+    def __call__(self, sub):
+        return self.launch(sub).result()
+
+
+class _Launched:
+    def __init__(self, ws):
+        self.ws = ws
+
+    def result(self):
+        r = self.ws.fetch()
+        self.ws = None
+        return r
+
+
+def device_runner(thresholds, min_depth, fill, device=None):
+    """The streamed runner on the GPU (``DeviceRunner``)."""
+    return DeviceRunner(thresholds, min_depth, fill, device)
 
 
 def consensus_files_streamed(filename, thresholds, prefix, min_depth=1, fill=b"-", nchar=0, maxdel_active=True,

@@ -21,6 +21,7 @@ OP_DASH = (2, 3, 6)         # D N P
 OP_I, OP_S = 1, 4
 PF_X, PF_RANGE, PF_INS, PF_LONG, PF_SIMPLE = 1, 2, 4, 8, 64
 RUN_BASES, RUN_DASH, RUN_XBIT, RUN_DROP, RUN_LONG = 1, 2, 4, 8, 16
+RUN_KSHIFT = 27   # include/s2c.h S2C_RUN_KSHIFT
 
 
 def _amb():
@@ -99,9 +100,9 @@ def model_reads(hb, maxdel_active=None, maxdel=None):
                     g = gpos + (s - ka)
                     if bases:
                         q = q0 + start + (s - k)
-                        runs[o + j] = (g, (e - s) | (bkind << 24), q & 0xFFFFFFFF, q >> 32)
+                        runs[o + j] = (g, (e - s) | (bkind << RUN_KSHIFT), q & 0xFFFFFFFF, q >> 32)
                     else:
-                        runs[o + j] = (g, (e - s) | ((RUN_DASH | lng) << 24), 0, 0)
+                        runs[o + j] = (g, (e - s) | ((RUN_DASH | lng) << RUN_KSHIFT), 0, 0)
                 k += take
                 if bases:
                     start += ln
@@ -123,8 +124,8 @@ def model_counts(hb, runs=None):
     Lp = hb.info.padded_len
     counts = np.zeros((NSYM, Lp), dtype=np.int64)
     r = runs.astype(np.int64)
-    kind = r[:, 1] >> 24
-    ln = r[:, 1] & 0xFFFFFF
+    kind = r[:, 1] >> RUN_KSHIFT
+    ln = r[:, 1] & ((1 << RUN_KSHIFT) - 1)
     for sel, is_bases in (((kind & 3) == RUN_BASES, True), ((kind & 3) == RUN_DASH, False)):
         g, n = r[sel, 0], ln[sel]
         if not len(g):
@@ -217,7 +218,7 @@ def check_plan(hb):
     assert set(hb.rlist.tolist()) == set(np.nonzero(((fl & 16) != 0) | ((fl & PF_INS) != 0))[0].tolist())
 
 
-CHUNK_PIECES, CHUNK_QBYTES, CHUNK_XBYTES, CHUNK_OBYTES, CHUNK_RECS = 512, 16384, 8192, 4096, 768   # include/s2c.h
+CHUNK_PIECES, CHUNK_QBYTES, CHUNK_XBYTES, CHUNK_OBYTES, CHUNK_RECS = 128, 4096, 2048, 1024, 192   # include/s2c.h (per wave)
 LY_MAIN = 0xFFFFFFFF
 CHUNK_LANE_RECS, ITEM_RECS = 248, 60000
 
@@ -232,7 +233,9 @@ def layer_ranges(hb, t, nl=None):
     p0 = ps[S0:W1]
     cnt = ps[S0 + 1:W1 + 1] - p0
     nl = int(row[19]) if nl is None else nl
-    return S0, W0, W1, [(p0 + cnt * l // nl, p0 + cnt * (l + 1) // nl) for l in range(nl)]
+    rot = (np.arange(S0, W1, dtype=np.uint64) * np.uint64(2654435761)) % np.uint64(nl)   # s2c_host.cpp layer_rot
+    rot = rot.astype(np.int64)
+    return S0, W0, W1, [(p0 + (cnt * l + rot) // nl, p0 + (cnt * (l + 1) + rot) // nl) for l in range(nl)]
 
 
 def _region(nbytes, phase):
@@ -252,7 +255,7 @@ def check_layers(hb):
     nwp = 8
     while nwp * 32 < i.tile_max:
         nwp *= 2
-    G = 256 // nwp
+    G = 64 // nwp   # counting lanes per word of one wave
     K = i.kwin
     lly, lpc = hb.lly.astype(np.int64), hb.lpc.astype(np.int64)
     T = hb.tiles.astype(np.int64)

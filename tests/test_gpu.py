@@ -396,3 +396,37 @@ def test_device_pipeline_equals_batch_model(name, over, thr, md, fill):
     else:
         with pytest.raises(getattr(builtins, ref["status"])):
             build_records(hb, thr, "case", st, offs, out)
+
+
+@pytest.mark.parametrize("idx", range(len(golden_io.load("stdout"))))
+def test_cli_stdout_matches_reference(idx, tmp_path, monkeypatch, capsys):
+    """The whole CLI's stdout equals the reference's own captured stdout (tests/golden/
+    stdout.json: the reference run in a scratch directory as `-i in.sam -o out`), failing
+    cases included (the same exception class, stdout up to the raise): :143, :182, :194,
+    :224-227, :420-426."""
+    from sam2consensus_amd import cli
+    from test_host import _stdout_case
+    c = golden_io.load("stdout")[idx]
+    sam, args = _stdout_case(c)
+    (tmp_path / "in.sam").write_bytes(sam.encode("latin-1"))
+    monkeypatch.chdir(tmp_path)
+    status = "ok"
+    try:
+        cli.main(["-i", "in.sam", "-o", "out"] + list(args))
+    except (KeyError, IndexError, ValueError, ZeroDivisionError, OverflowError) as e:
+        status = type(e).__name__
+    assert status == c["status"]
+    assert capsys.readouterr().out == c["stdout"]
+
+
+@pytest.mark.parametrize("idx", [0, 1])
+def test_long_skip_on_device_matches_reference(idx):
+    """A read whose seqout spans ≥ 2^24 positions (a 16.7 Mb N skip: a long piece, its runs
+    from k_reads through the tile long lists, 27-bit run lengths) on the GPU equals the
+    reference's files (tests/golden/longskip.json)."""
+    from sam2consensus_amd.cli import run_text
+    c = golden_io.load("longskip")[idx]
+    status, files = run_text(c["sam"], c["args"])
+    assert status == c["status"]
+    got = {k: hashlib.sha256(v.encode("latin-1")).hexdigest() for k, v in files.items()}
+    assert got == {k: v["sha256"] for k, v in c["files"].items()}

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
     assert declared <= exported, declared - exported
     assert declared == set(_lib.EXPORTS)
-    assert _lib.lib.s2c_abi_version() == 7
+    assert _lib.lib.s2c_abi_version() == 8
 
 
 def _model_case(sam, args):
@@ -265,3 +265,63 @@ def _ref_progress(header_lines, lines_total):
 def test_progress_lines_match_reference_counter(h, n):
     from sam2consensus_amd.cli import progress_lines
     assert progress_lines(h, n) == _ref_progress(h, n)
+
+
+# ---------------------------------------------------------------- stdout vs the reference's own
+def _stdout_case(c):
+    """(SAM text, args) of a tests/golden/stdout.json case (oracle/gen_golden_stdout.py)."""
+    if "kat" in c:
+        kat = {k["name"]: k for k in golden_io.load("kat")}
+        return kat[c["kat"]]["sam"], c["args"]
+    n = c["progress_lines"]
+    head = "@HD\tVN:1.0\tSO:unsorted\n@SQ\tSN:g\tLN:200\n"
+    mapped = "r\t0\tg\t11\t60\t20M\t*\t0\t0\t" + "ACGT" * 5 + "\t*\n"
+    unmapped = "u\t4\t*\t0\t0\t*\t*\t0\t0\tACGT\t*\n"
+    return head + "".join(mapped if k % 1000 == 0 else unmapped for k in range(n)), c["args"]
+
+
+def test_read_pass_stdout_matches_reference_capture():
+    """The lines the CLI prints from the read pass (header count, progress counter, totals:
+    :143, :182, :194, :224-227) equal the reference's captured stdout (tests/golden/stdout.json,
+    the reference run by oracle/gen_golden_stdout.py), failing read passes included (the
+    reference's lines up to the raise); the device part of the run is covered by
+    test_gpu.py::test_cli_stdout_matches_reference."""
+    from sam2consensus_amd.batch import Parser
+    from sam2consensus_amd.cli import REF_ERRORS, _log_failed_parse, _log_summary
+    for c in golden_io.load("stdout"):
+        sam, args = _stdout_case(c)
+        out = []
+        log = lambda s: out.append(s + "\n")  # noqa: E731 - print()
+        p = Parser("-d" not in args, 150)
+        failed = False
+        try:
+            p.feed(sam.encode("latin-1"))
+            hb = p.finish()
+            _log_summary(log, hb.info)
+            hb.free()
+        except REF_ERRORS:
+            _log_failed_parse(log, p)
+            failed = True
+        finally:
+            p.close()
+        want = c["stdout"][len("\nProcessing file in.sam:\n\n"):]
+        if failed:
+            assert "".join(out) == want, (c.get("kat"), "".join(out), want)
+        else:
+            assert want.startswith("".join(out)), (c.get("kat"), "".join(out), want)
+
+
+# ---------------------------------------------------------------- seqout of 2^24+ positions
+def test_long_skip_parses_into_long_pieces():
+    """A 16.7 Mb CIGAR N skip (seqout ≥ 2^24 positions, legal SAM) parses (the limit is 2^27,
+    include/s2c.h S2C_RUN_KSHIFT) into a long piece listed by every tile it spans; its device
+    run is checked against the reference's files by test_gpu.py::test_long_skip_on_device_*
+    (the numpy model takes ~40 s on it)."""
+    c = golden_io.load("longskip")[0]
+    hb = batch.parse_text(c["sam"], False, 150)
+    try:
+        bm.check_plan(hb)
+        assert hb.info.n_long > 0 and len(hb.lp) >= (1 << 24) // 2048
+        assert hb.info.total_len == (1 << 24) + 64
+    finally:
+        hb.free()
