@@ -176,6 +176,9 @@ def main():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--graph", action="store_true", help="time HIP graph replays of the step")
     ap.add_argument("--stage-events", action="store_true", help="HIP events between all stages in the timed steps")
+    ap.add_argument("--rehearse-shards", type=int, default=0, metavar="N",
+                    help="N=1 only: also run each of the N position shards of the workload alone on this GPU "
+                         "(K steps each) and report their step times (projected N-GPU strong-scaling step)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -346,6 +349,9 @@ def main():
         line["host_synth_feed_s"] = t_synth
         line["host"] = cpu_model()
         line["parity"] = parity
+        if world == 1 and args.rehearse_shards > 1:
+            line["shard_rehearsal"] = rehearse_shards(full, args.rehearse_shards, thresholds, min_depth, dev,
+                                                      args.steps, args.warmup, info.aligned_bases)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(wl, args.cpu_sample_scale)
             if not args.no_cpu_mc:
@@ -353,6 +359,36 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def rehearse_shards(full, n, thresholds, min_depth, dev, K, W, bases):
+    """One GPU: each of the n position shards (shard.sub_batch, the N>1 default) run alone,
+    W warmup + K timed steps each; the projected n-GPU step is the slowest shard's (every
+    rank runs its shard concurrently on its own GPU; the gathers after the timed loop are
+    not part of a step)."""
+    import torch
+
+    from sam2consensus_amd import shard
+    from sam2consensus_amd.engine import DeviceBatch, Workspace
+    ms = []
+    for r in range(n):
+        sub = shard.sub_batch(full, r, n)
+        ws = Workspace(DeviceBatch(sub, dev), thresholds, min_depth, b"-")
+        for _ in range(W):
+            ws.run()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(K):
+            ws.run()
+        torch.cuda.synchronize(dev)
+        ms.append((time.perf_counter() - t0) / K * 1e3)
+        del ws
+        sub.free()
+    worst = max(ms)
+    return {"shards": n, "ms_per_step": ms, "projected_ms_per_step": worst,
+            "projected_value": bases / (worst * 1e-3),
+            "what": "each shard of the %d-way position split run alone on one GPU; projected step = the slowest "
+                    "shard's (wall clock over K steps, launches included)" % n}
 
 
 def bound_from_profile(wl):

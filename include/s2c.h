@@ -222,6 +222,11 @@ int  s2c_parser_counters(s2c_parser *p, int64_t *out);
    out[5] = {header ended (0/1), references, header lines, lines read (through the failing
    line), error code of the read pass (0: none)}. */
 int  s2c_parser_progress(const s2c_parser *p, int64_t *out);
+
+/* FASTA body assembly (:394-418): dst = raw[starts[0] : +lens[0]] ++ raw[starts[1] : +lens[1]]
+   ++ ... (n blocks; dst holds their total length), copied on the host threads.  The tiles'
+   body slots after the D2H copy of the device output, in [threshold][tile] order. */
+int  s2c_gather_bodies(const uint8_t *raw, const int64_t *starts, const int64_t *lens, int64_t n, uint8_t *dst);
 int  s2c_parser_pack(s2c_parser *p, int64_t g0, int64_t g1, size_t *len);
 int  s2c_parser_blob_copy(const s2c_parser *p, void *dst, size_t cap);
 int  s2c_parser_unpack(s2c_parser *p, const void *blob, size_t len);

@@ -407,7 +407,10 @@ __device__ __forceinline__ void win_issue(const DenseArgs &d, const Win &v, uint
 // One tile of NWP words from its window in LDS, WPT waves (WT threads): a wave holds NWP / WPT
 // words, G lanes per word, RPL = 8 / G counter rows (4 positions each) voted per lane.
 // dcnt / ncnt / ccnt: zeroed byte counters; stl: the waves' partial tile statistics.
-constexpr int WPT = 2;            // waves per tile (they share the window)
+#ifndef S2C_DENSE_WPT
+#define S2C_DENSE_WPT 2
+#endif
+constexpr int WPT = S2C_DENSE_WPT;   // waves per tile (they share the window)
 constexpr int WT = WGD * WPT;     // threads per tile
 constexpr int PFN = 2;            // piece records per thread loaded with the DMA (windows of ≤ 256 pieces)
 template <int NWP>

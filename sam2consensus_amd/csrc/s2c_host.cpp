@@ -1366,11 +1366,20 @@ static void build_layers(s2c_batch *b, const PieceBlocks &B, int64_t G) {
 }
 
 // Work items of a tile of nl layers: {tile, c, l0, l1}, enough that each one's run records
-// per word stay <= S2C_ITEM_RECS (its u16 histogram) and, past 32 layers, an item takes
-// <= 16 (parallelism for the deep tiles: C4's 16.5 kb at 100,000x).
+// per word stay <= S2C_ITEM_RECS (its u16 histogram) and, past 2·IL layers, an item takes
+// <= IL (parallelism for the deep tiles: C4's 16.5 kb at 100,000x); IL = 64 per-wave layers
+// (16 per wave), S2C_ITEM_LAYERS overrides.
+static int64_t item_layers() {
+    static const int64_t il = [] {
+        const char *e = getenv("S2C_ITEM_LAYERS");
+        return e ? std::max<int64_t>(4, atoll(e)) : (int64_t)64;
+    }();
+    return il;
+}
 static int64_t plan_items(const s2c_batch *b, int64_t K, uint64_t a, uint64_t e, int64_t nl) {
     const int64_t W0 = (int64_t)(a >> 5), W1 = (int64_t)((e + 31) >> 5), S0 = std::max<int64_t>(W0 - K, 0);
-    int64_t nch = nl > 32 ? (nl + 15) / 16 : 1;
+    const int64_t IL = item_layers();
+    int64_t nch = nl > 2 * IL ? (nl + IL - 1) / IL : 1;
     for (;; nch++) {
         bool ok = true;
         for (int64_t c = 0; c < nch && ok; c++) {
@@ -1637,6 +1646,26 @@ static int s2c_parser_checks_impl(s2c_parser *p, uint8_t *bad, int64_t n_refs) {
 }
 extern "C" int s2c_parser_checks(s2c_parser *p, uint8_t *bad, int64_t n_refs) {
     return s2c_guarded([&] { return s2c_parser_checks_impl(p, bad, n_refs); });
+}
+
+// FASTA body assembly (:394-418): the tiles' body slots, concatenated in [threshold][tile]
+// order (n blocks: raw[starts[i], starts[i] + lens[i]) → dst at the running offset), on the
+// host threads for large outputs.
+static int s2c_gather_bodies_impl(const uint8_t *raw, const int64_t *starts, const int64_t *lens, int64_t n,
+                                  uint8_t *dst) {
+    if (n < 0 || (n > 0 && (!raw || !starts || !lens || !dst))) return s2c_set_error(S2C_ERR_ARG, "bad gather arguments");
+    std::vector<int64_t> off(n + 1, 0);
+    for (int64_t i = 0; i < n; i++) {
+        if (lens[i] < 0 || starts[i] < 0) return s2c_set_error(S2C_ERR_ARG, "negative block");
+        off[i + 1] = off[i] + lens[i];
+    }
+    par_ranges(plan_threads(off[n], (int64_t)1 << 22), n, [&](int, int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; i++) memcpy(dst + off[i], raw + starts[i], (size_t)lens[i]);
+    });
+    return S2C_OK;
+}
+extern "C" int s2c_gather_bodies(const uint8_t *raw, const int64_t *starts, const int64_t *lens, int64_t n, uint8_t *dst) {
+    return s2c_guarded([&] { return s2c_gather_bodies_impl(raw, starts, lens, n, dst); });
 }
 
 extern "C" int s2c_parser_progress(const s2c_parser *p, int64_t *out) {

@@ -274,6 +274,10 @@ class Workspace:
         np.cumsum(lens, out=offs[1:])
         total = int(offs[-1])
         raw = self.out[: T * self.out_stride].cpu().numpy()
-        idx = np.repeat(starts - offs[:-1], lens) + np.arange(total, dtype=np.int64)
-        out = raw[idx].tobytes()
-        return stats, offs.astype(np.uint64), out
+        starts = np.ascontiguousarray(starts, dtype=np.int64)
+        lens = np.ascontiguousarray(lens, dtype=np.int64)
+        out = bytearray(total)
+        buf = (C.c_char * max(total, 1)).from_buffer(out) if total else None
+        L.check(lib.s2c_gather_bodies(raw.ctypes.data, starts.ctypes.data, lens.ctypes.data, len(lens),
+                                      C.addressof(buf) if total else None))
+        return stats, offs.astype(np.uint64), bytes(out)

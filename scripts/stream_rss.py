@@ -39,6 +39,7 @@ def child(mode, path, name, batch_mb):
     print(json.dumps({"mode": mode, "seconds": round(dt, 3),
                       "peak_rss_mb": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0, 1),
                       "sha256": h.hexdigest(), "batches": len(getattr(r, "batches", [])) or 1,
+                      "phases_s": {k: round(v, 3) for k, v in getattr(r, "timings", {}).items()},
                       "reads_held_max": getattr(r, "held_max", None)}))
 
 
