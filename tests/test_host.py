@@ -325,3 +325,24 @@ def test_long_skip_parses_into_long_pieces():
         assert hb.info.total_len == (1 << 24) + 64
     finally:
         hb.free()
+
+
+def test_gather_bodies_concatenates_blocks():
+    """s2c_gather_bodies (FASTA body assembly, engine.Workspace.fetch): blocks of a raw
+    buffer concatenated in order, any lengths, large outputs on the host threads."""
+    import ctypes as C
+    rng = np.random.default_rng(7)
+    raw = rng.integers(0, 256, size=1 << 22, dtype=np.uint8)
+    for n in (0, 1, 7, 5000):
+        lens = rng.integers(0, 2000, size=n).astype(np.int64)
+        starts = np.array([rng.integers(0, raw.size - L) for L in lens], dtype=np.int64).reshape(-1)
+        want = b"".join(raw[s:s + L].tobytes() for s, L in zip(starts, lens))
+        out = bytearray(max(len(want), 1))
+        buf = (C.c_char * len(out)).from_buffer(out)
+        _lib.check(_lib.lib.s2c_gather_bodies(raw.ctypes.data, starts.ctypes.data, lens.ctypes.data, n,
+                                              C.addressof(buf)))
+        assert bytes(out[:len(want)]) == want
+    bad = np.array([-1], dtype=np.int64)
+    with pytest.raises(_lib.S2CError):
+        _lib.check(_lib.lib.s2c_gather_bodies(raw.ctypes.data, bad.ctypes.data, bad.ctypes.data, 1,
+                                              raw.ctypes.data))
