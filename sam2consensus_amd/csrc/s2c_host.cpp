@@ -177,7 +177,11 @@ int tokenize_cigar(const char *s, size_t n, V &out, uint32_t *ntok) {
 // the elements unwritten, so they are first touched by the threads that fill them, not by a
 // serial zero-fill) and, from 4 MB on, backed by 2 MB-aligned anonymous mappings advised
 // as transparent huge pages (512x fewer page faults for the GB-sized arrays of a batch).
-constexpr size_t HUGE_MIN = (size_t)4 << 20, HUGE_PAGE = (size_t)2 << 20;
+constexpr size_t HUGE_PAGE = (size_t)2 << 20;
+inline size_t huge_min() {   // S2C_HUGE_MIN_KB: the smallest array so mapped (default 4 MB)
+    static const size_t m = [] { const char *e = getenv("S2C_HUGE_MIN_KB"); return e ? (size_t)atoll(e) << 10 : (size_t)4 << 20; }();
+    return m;
+}
 inline bool huge_pages() {   // S2C_HUGEPAGES=0 turns the advice off
     static const bool on = [] { const char *e = getenv("S2C_HUGEPAGES"); return !e || atoi(e) != 0; }();
     return on;
@@ -191,7 +195,7 @@ struct uninit_alloc {
     static size_t map_len(size_t bytes) { return (bytes + HUGE_PAGE - 1) & ~(HUGE_PAGE - 1); }
     T *allocate(size_t n) {
         const size_t bytes = n * sizeof(T);
-        if (bytes < HUGE_MIN) {
+        if (bytes < huge_min()) {
             void *q = ::operator new(bytes);
             return (T *)q;
         }
@@ -206,7 +210,7 @@ struct uninit_alloc {
     }
     void deallocate(T *q, size_t n) {
         const size_t bytes = n * sizeof(T);
-        if (bytes < HUGE_MIN) ::operator delete((void *)q);
+        if (bytes < huge_min()) ::operator delete((void *)q);
         else munmap((void *)q, map_len(bytes));
     }
     template <class U> void construct(U *q) noexcept { ::new ((void *)q) U; }
