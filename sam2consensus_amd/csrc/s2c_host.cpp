@@ -1657,12 +1657,13 @@ extern "C" int s2c_parser_checks(s2c_parser *p, uint8_t *bad, int64_t n_refs) {
 // host threads for large outputs.
 static int s2c_gather_bodies_impl(const uint8_t *raw, const int64_t *starts, const int64_t *lens, int64_t n,
                                   uint8_t *dst) {
-    if (n < 0 || (n > 0 && (!raw || !starts || !lens || !dst))) return s2c_set_error(S2C_ERR_ARG, "bad gather arguments");
+    if (n < 0 || (n > 0 && (!starts || !lens))) return s2c_set_error(S2C_ERR_ARG, "bad gather arguments");
     std::vector<int64_t> off(n + 1, 0);
     for (int64_t i = 0; i < n; i++) {
         if (lens[i] < 0 || starts[i] < 0) return s2c_set_error(S2C_ERR_ARG, "negative block");
         off[i + 1] = off[i] + lens[i];
     }
+    if (off[n] > 0 && (!raw || !dst)) return s2c_set_error(S2C_ERR_ARG, "bad gather arguments");
     par_ranges(plan_threads(off[n], (int64_t)1 << 22), n, [&](int, int64_t i0, int64_t i1) {
         for (int64_t i = i0; i < i1; i++) memcpy(dst + off[i], raw + starts[i], (size_t)lens[i]);
     });

@@ -342,6 +342,8 @@ def test_gather_bodies_concatenates_blocks():
         _lib.check(_lib.lib.s2c_gather_bodies(raw.ctypes.data, starts.ctypes.data, lens.ctypes.data, n,
                                               C.addressof(buf)))
         assert bytes(out[:len(want)]) == want
+    zl = np.zeros(3, dtype=np.int64)   # every block empty (e.g. all of a reference's tiles filtered): no output
+    _lib.check(_lib.lib.s2c_gather_bodies(None, zl.ctypes.data, zl.ctypes.data, 3, None))
     bad = np.array([-1], dtype=np.int64)
     with pytest.raises(_lib.S2CError):
         _lib.check(_lib.lib.s2c_gather_bodies(raw.ctypes.data, bad.ctypes.data, bad.ctypes.data, 1,
