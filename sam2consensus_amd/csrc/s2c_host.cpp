@@ -2187,6 +2187,46 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
             tile_max = std::max(tile_max, tiles.back().b - a);
         }
     }
+    // Launch LDS of k_tile_dense = the largest dense window, so one outlier window sets every
+    // tile's occupancy: when all but ≤ 0.2 % of the windows fit the share of a CU's 160 KB
+    // that lets 8 two-wave tiles reside (4 waves per SIMD, the kernel's register budget), the
+    // launch is sized to that share and the few tiles over it are split in two (each half's
+    // window fits; C5: 55 of 62,934 tiles), unless the tile width is fixed (streamed batches)
+    int64_t dense_cap = S2C_DENSE_LDS;
+    {
+        const int64_t nwp = tile_max <= 512 ? 16 : tile_max <= 1024 ? 32 : 64;
+        const int64_t cap8 = 163840 / 8 - (96 * nwp + 128);   // (the kernel's static LDS)
+        const int64_t n0 = (int64_t)tiles.size();
+        std::vector<int64_t> db(n0, -1);
+        par_ranges(plan_threads(n0, 64), n0, [&](int, int64_t t0, int64_t t1) {
+            uint32_t tw[S2C_TILE_WORDS];
+            for (int64_t t = t0; t < t1; t++) {
+                tile_window(b, K, (uint64_t)tiles[t].a, (uint64_t)tiles[t].b, tw);
+                if (dense_fits(tw, K)) db[t] = dense_bytes(tw, K);
+            }
+        });
+        int64_t nfit = 0, over = 0;
+        for (const int64_t x : db)
+            if (x >= 0) { nfit++; over += x > cap8; }
+        if (over > 0 && over * 500 <= nfit) {
+            dense_cap = cap8;
+            if (tile_force == 0) {
+                std::vector<Tile> split;
+                split.reserve(n0 + over);
+                for (int64_t t = 0; t < n0; t++) {
+                    const Tile &T = tiles[t];
+                    const int64_t mid = T.a + align_up((T.b - T.a) / 2, S2C_POS_ALIGN);
+                    if (db[t] > cap8 && mid < T.b) {
+                        split.push_back({T.a, mid, T.ref});
+                        split.push_back({mid, T.b, T.ref});
+                    } else {
+                        split.push_back(T);
+                    }
+                }
+                tiles.swap(split);
+            }
+        }
+    }
     const int64_t NT = (int64_t)tiles.size();
     I.n_tiles = NT;
     I.tile_max = tile_max;
@@ -2245,11 +2285,6 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     b->tiles.assign((size_t)NT * S2C_TILE_WORDS, 0u);
     uint64_t boff = 0, loff = 0, coff = 0;
     int64_t runs_max = 0;
-    // Launch LDS of k_tile_dense = the largest dense window, so one outlier window sets every
-    // tile's occupancy: when all but ≤ 0.2 % of the windows fit the share of a CU's 160 KB
-    // that lets 8 two-wave tiles reside (4 waves per SIMD, the kernel's register budget),
-    // the rest are not dense (k_tile runs them).
-    int64_t dense_cap = S2C_DENSE_LDS;
     // per tile (host threads): its window, the most candidate runs of a word, layers, items
     std::vector<int64_t> t_nl(NT), t_nch(NT), t_maxc(NT), t_wruns(NT);
     std::atomic<bool> too_big{false};
@@ -2271,23 +2306,6 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
         }
     });
     if (too_big) return s2c_set_error(S2C_ERR_LIMIT, "a read whose SEQ or CIGAR exceeds k_tile's LDS chunk");
-    // Launch LDS of k_tile_dense = the largest dense window, so one outlier window sets every
-    // tile's occupancy: when all but ≤ 0.2 % of the windows fit the share of a CU's 160 KB
-    // that lets 8 two-wave tiles reside (4 waves per SIMD, the kernel's register budget),
-    // the rest are not dense (k_tile runs them).
-    {
-        const int64_t nwp = tile_max <= 512 ? 16 : tile_max <= 1024 ? 32 : 64;
-        const int64_t cap8 = 163840 / 8 - (96 * nwp + 128);   // (the kernel's static LDS)
-        int64_t nfit = 0, over = 0;
-        for (int64_t t = 0; t < NT; t++) {
-            const uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
-            if (dense_fits(tw, K)) {
-                nfit++;
-                over += dense_bytes(tw, K) > cap8;
-            }
-        }
-        if (over > 0 && over * 500 <= nfit) dense_cap = cap8;
-    }
     for (int64_t t = 0; t < NT; t++) {
         const Tile &T = tiles[t];
         const int64_t maxc = t_maxc[t], nl = t_nl[t], nch = t_nch[t];
