@@ -1045,6 +1045,13 @@ extern "C" int s2c_parser_feed_file(s2c_parser *p, const char *path) {
 // ------------------------------------------------------------------ finish: layout + plan
 namespace {
 constexpr int64_t TP_MIN = 256, TP_MAX = 2048;      // tile bounds (positions)
+static int64_t deep_tile_min() {   // S2C_DEEP_TILE: the narrowest deep tile (positions)
+    static const int64_t v = [] {
+        const char *e = getenv("S2C_DEEP_TILE");
+        return e ? std::min<int64_t>(std::max<int64_t>(atoll(e), 64), 2048) : (int64_t)512;
+    }();
+    return v;
+}
 constexpr double E_TARGET = 262144.0;                // aligned bases per deep tile
 // LDS a shallow tile's window is planned to (one wave per tile, ~10 resident per CU; C5's
 // 30x gives 1024-position tiles — measured faster than 512, profiles/r02)
@@ -2165,7 +2172,15 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
         const int64_t L = p->ref_len[r], off = b->ref_off[r];
         if (L == 0) continue;
         const double depth = (double)ref_span[r] / (double)L, spp = (double)ref_slots[r] / (double)L;
-        int64_t tp = depth > 0 ? align_up((int64_t)std::ceil(E_TARGET / depth), S2C_POS_ALIGN) : TP_MAX;
+        // deep: ≈ E_TARGET aligned bases per tile, a power of two of words (every counting lane
+        // of k_tile's waves busy) and at least S2C_DEEP_TILE positions (default 512: measured
+        // against 256 / 320 on C3 and 256 on C4, profiles/r03/)
+        int64_t tp = TP_MAX;
+        if (depth > 0) {
+            const double want = std::max(64.0, std::ceil(E_TARGET / depth));
+            tp = (int64_t)1 << (int64_t)std::llround(std::log2(want));
+            tp = std::max<int64_t>(tp, deep_tile_min());
+        }
         const double win = 32.0 * (double)(K + 1) * spp;    // run slots per word's window
         if (win <= 200.0 && spp > 0) {
             // shallow: the widest tile whose window (12 B per op slot and 12 B per base plane word
