@@ -131,6 +131,24 @@ def _log_failed_parse(log, parser):
         log(line)
 
 
+def _warm_device(device):
+    """Start the HIP runtime and the device's context on a side thread (the first device
+    call costs tenths of a second) so it overlaps the host parse; join() before the upload.
+    A failure here is left to the upload to report."""
+    import threading
+
+    def run():
+        try:
+            from .engine import _dev
+            import torch
+            torch.empty(1, device=_dev(device))
+        except Exception:  # noqa: BLE001 - reported by DeviceBatch on the main thread
+            pass
+    th = threading.Thread(target=run, daemon=True)
+    th.start()
+    return th
+
+
 def consensus_files(filename, thresholds, prefix, min_depth=1, fill=b"-", nchar=0, maxdel_active=True,
                     device=None, log=None):
     """Run the whole pipeline on one SAM/SAM.gz file; returns a RunResult whose
@@ -139,6 +157,7 @@ def consensus_files(filename, thresholds, prefix, min_depth=1, fill=b"-", nchar=
 
     t = {}
     t0 = time.perf_counter()
+    warm = _warm_device(device)   # (the HIP context comes up while the host parses)
     p = Parser(maxdel_active, 150)
     try:
         p.feed_file(filename)
@@ -150,6 +169,7 @@ def consensus_files(filename, thresholds, prefix, min_depth=1, fill=b"-", nchar=
     finally:
         p.close()
     t["parse"] = time.perf_counter() - t0
+    warm.join()
     if log:
         _log_summary(log, hb.info)
     files = consensus_batch(hb, thresholds, prefix, min_depth, fill, nchar, device, t)

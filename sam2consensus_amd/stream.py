@@ -162,15 +162,24 @@ def _sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, st
     for every final tile range, then ("last", hb) with the final batch."""
     p = StreamParser(maxdel_active, 150, tile_width)
     t_done, pending, broken = 0, 0, False
+    tm = state.setdefault("t", {})
+    clk = time.perf_counter
+
+    def add(k, t0):
+        tm[k] = tm.get(k, 0.0) + clk() - t0
     try:
         for blk in blocks:
+            t0 = clk()
             p.feed(blk)
+            add("feed", t0)
             pending += len(blk)
             if broken or pending < batch_bytes:
                 continue
             pending = 0
             try:
+                t0 = clk()
                 hb = p.snapshot()
+                add("snapshot", t0)
             except (KeyError, IndexError):
                 broken = True          # s2c_parser_finish raises it once the input is read
                 continue
@@ -186,17 +195,23 @@ def _sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, st
                 t1 = int(np.searchsorted(hb.tiles[:, 1].astype(np.int64), bound, side="right"))
                 if t1 <= t_done:
                     continue
+                t0 = clk()
                 sub = _sub(hb, t_done, t1)
+                add("cut", t0)
                 state["absorb"](hb)
                 gmin = int(hb.tiles[t1, 0]) if t1 < NT else int(hb.info.padded_len)
+                t0 = clk()
                 p.retain(gmin)
+                add("retain", t0)
                 yield ("run", sub, t_done, t1)
                 t_done = t1
                 if stats_hook:
                     stats_hook(t_done, NT, held)
             finally:
                 hb.free()
+        t0 = clk()
         hb = p.finish()
+        add("finish", t0)
         late, _, _, held = p.state()
         state["held_max"] = max(state["held_max"], held)
         if late:
@@ -244,28 +259,42 @@ def stream_batches(blocks, thresholds, runner, maxdel_active=True, tile_width=DE
         parts.append((t0, t1, np.asarray(offs, dtype=np.uint64), out))
 
     hb = None
+    ct = {"launch": 0.0, "collect": 0.0, "wait": 0.0}
+    clk = time.perf_counter
+    tw = clk()
     for item in _Producer(_sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, state)):
+        ct["wait"] += clk() - tw
         if item[0] == "last":
             hb = item[1]
             break
         _, sub, t0, t1 = item
         sub.t0, sub.t1 = t0, t1
+        tl = clk()
         try:
             h = launch(sub) if launch else runner(sub)
         except BaseException:
             sub.free()
             raise
+        ct["launch"] += clk() - tl
         pend.append((t0, t1, h, sub))
+        tl = clk()
         while len(pend) > 1:
             collect(pend.pop(0))
+        ct["collect"] += clk() - tl
+        tw = clk()
+    tl = clk()
     while pend:
         collect(pend.pop(0))
+    ct["collect"] += clk() - tl
     hb.ref_reads = state["cov"].astype(np.int64)          # Σcoverage > 0 in any batch (:334-341)
     offs, out = _merge(parts, T)
     if stats is None:
         stats = np.zeros((hb.info.n_refs, T, 4), np.uint64)
-    return StreamResult(hb, stats, offs, out, int(hb.info.header_lines), state["lines"], state["mapped"],
-                        [(a, b) for a, b, _, _ in parts], state["held_max"])
+    res = StreamResult(hb, stats, offs, out, int(hb.info.header_lines), state["lines"], state["mapped"],
+                       [(a, b) for a, b, _, _ in parts], state["held_max"])
+    res.timings = {"producer_" + k: v for k, v in state.get("t", {}).items()}
+    res.timings.update({"consumer_" + k: v for k, v in ct.items()})
+    return res
 
 
 class DeviceAccumulator:
@@ -433,6 +462,7 @@ def consensus_files_streamed(filename, thresholds, prefix, min_depth=1, fill=b"-
         res = stream_unsorted(file_blocks(filename), thresholds,
                               DeviceAccumulator(thresholds, min_depth, fill, device), maxdel_active, batch_bytes)
     t["stream"] = time.perf_counter() - t0
+    t.update(getattr(res, "timings", {}))
     if log:
         _log_summary(log, res)
     t0 = time.perf_counter()
