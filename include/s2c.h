@@ -123,7 +123,8 @@ int s2c_layout(int64_t *out, int n);
 #define S2C_LY_MAIN 0xFFFFFFFFu
 #define S2C_TILE_DEEP     1  /* several work items: counts summed in HBM, voted by k_consensus */
 #define S2C_TILE_GENERAL  2  /* insertion layout beyond k_tile's LDS: voted by k_consensus */
-#define S2C_TILE_DENSE    4  /* routed to k_tile_dense (one item, no insertion keys; long pieces through its long list) */
+#define S2C_TILE_DENSE    4  /* routed to k_tile_dense (one item, no insertion keys); its long list (lp[lp0, lp1)) holds
+                                 piece indices, walked by the kernel; other tiles list run slots (k_reads) */
 #define S2C_ITEM_WORDS    4  /* work item {tile, chunk, l0, l1}: the tile's layers [l0, l1) */
 #define S2C_EPI_KEYS    256  /* insertion keys per tile k_tile's epilogue holds in LDS */
 /* insertion columns per tile k_tile's epilogue holds in LDS, by words per tile */

@@ -66,7 +66,7 @@ __constant__ uint8_t c_amb[64] = {
 };
 
 struct DenseArgs {
-    const uint32_t *rs, *pc, *ops, *bq, *bx, *tiles, *items, *lp, *runs;
+    const uint32_t *rs, *pc, *ops, *bq, *bx, *tiles, *items, *lp;
     const double *thresholds;
     uint64_t *tile_stats, *blk_len;
     uint8_t *out;
@@ -147,6 +147,15 @@ __device__ __forceinline__ void walk_window(const uint32_t *opl, const uint2 *bq
         run(j, rg, rl, rk, rq);
     }
 }
+
+// walk_piece's view of the batch in HBM (the tile's long pieces)
+struct DenseMem {
+    const uint32_t *ops, *bq, *bx;
+    __device__ __forceinline__ uint32_t op(uint32_t j) const { return ops[j]; }
+    __device__ __forceinline__ uint32_t p0(uint64_t w) const { return bq[2 * w]; }
+    __device__ __forceinline__ uint32_t p1(uint64_t w) const { return bq[2 * w + 1]; }
+    __device__ __forceinline__ uint32_t x(uint64_t w) const { return bx[w]; }
+};
 
 constexpr int WGD = 64;   // one wave per tile
 constexpr int GSD = 8;    // records per counting group (one Harley–Seal tree)
@@ -669,45 +678,55 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
 #pragma unroll
         for (int c = 0; c < 4; c++) close4(C[c], t4[c]);
     }
-    // long pieces over the tile (rare: > window spans, C5's long deletions): k_reads' run
-    // records through the tile's long list, one per lane of the word and round — bases into
-    // the counters (planes from HBM), '-' runs and the N / '-' chars of SEQ into the byte
-    // counters (the host keeps a dense tile's candidate runs + long runs ≤ 255 per word)
+    // long pieces over the tile (rare: spans past the window, C5's long deletions): the tile's
+    // long list holds their piece indices; the lanes of each word take them one per lane and
+    // round and walk each from HBM (parsecigar :64-81 + maxdel :210, walk_piece), keeping the
+    // runs' parts in the lane's word — bases into the counters (planes from HBM), '-' runs and
+    // the N / '-' chars of SEQ into the byte counters (the host keeps a dense tile's candidate
+    // runs + long runs ≤ 255 per word)
     if (v.nlong) {
         const int32_t wr = (int32_t)(32 * w);   // tile-relative first position of the lane's word
         const uint32_t ntr = uni(__ockl_wfred_max_u32(active && g < v.nlong ? (v.nlong - g + G - 1) / G : 0u));
         for (uint32_t m = 0; m < ntr; m++) {
             const uint32_t j = g + G * m;
             if (!(active && j < v.nlong)) continue;
-            const Run r = run_of(((const uint4 *)d.runs)[d.lp[v.lp0 + j]]);
-            const RecGeom gm = rec_geom(r.gpos, r.len, W);
-            if (!gm.valid) continue;
-            const int32_t p0 = wr + (int32_t)gm.lo, p1 = p0 + __popc(gm.valid);
-            if ((r.kind & 3u) == S2C_RUN_DASH) {
-                cnt_range(dcnt, p0, p1, TL);
-            } else if ((r.kind & 3u) == S2C_RUN_BASES) {
-                const uint64_t qs = r.q + gm.qs, qw = qs >> 5;
-                const uint32_t sh = (uint32_t)(qs & 31);
-                const uint32_t mx = (funnel(d.bq[2 * qw + 2], d.bq[2 * qw], sh) << gm.lo) & gm.valid;
-                const uint32_t my = (funnel(d.bq[2 * qw + 3], d.bq[2 * qw + 1], sh) << gm.lo) & gm.valid;
-                ripple1(C[0], mx);
-                ripple1(C[1], my);
-                ripple1(C[2], mx & my);
-                ripple1(C[3], gm.valid);
-                if (r.kind & S2C_RUN_XBIT) {
-                    uint32_t xm = (funnel(d.bx[qw + 1], d.bx[qw], sh) << gm.lo) & gm.valid;
-                    while (xm) {
-                        const uint32_t bit = (uint32_t)__builtin_ctz(xm);
-                        xm &= xm - 1;
-                        if ((mx >> bit) & 1u) {   // '-' of SEQ (p0 = 1)
-                            cnt_add1(ccnt, (uint32_t)(wr + (int32_t)bit));
-                            if (!(r.kind & S2C_RUN_DROP)) cnt_add1(dcnt, (uint32_t)(wr + (int32_t)bit));
-                        } else {
-                            cnt_add1(ncnt, (uint32_t)(wr + (int32_t)bit));
-                        }
-                    }
-                }
-            }
+            const uint32_t k = d.lp[v.lp0 + j];
+            const uint4 P = ((const uint4 *)d.pc)[k];
+            const uint32_t oend = d.pc[4 * (size_t)k + 6];   // next piece's op offset
+            walk_piece(DenseMem{d.ops, d.bq, d.bx}, P, oend, mda, d.maxdel,
+                       [&](uint32_t, uint32_t gp, uint32_t l, uint32_t kind, uint64_t q) {
+                           const uint32_t kd = kind & 3u;
+                           if (kd != S2C_RUN_BASES && kd != S2C_RUN_DASH) return;
+                           const RecGeom gm = rec_geom(gp, l, W);
+                           if (!gm.valid) return;
+                           const int32_t p0 = wr + (int32_t)gm.lo, p1 = p0 + __popc(gm.valid);
+                           if (kd == S2C_RUN_DASH) {
+                               cnt_range(dcnt, p0, p1, TL);
+                               return;
+                           }
+                           const uint64_t qs = q + gm.qs, qw = qs >> 5;
+                           const uint32_t sh = (uint32_t)(qs & 31);
+                           const uint32_t mx = (funnel(d.bq[2 * qw + 2], d.bq[2 * qw], sh) << gm.lo) & gm.valid;
+                           const uint32_t my = (funnel(d.bq[2 * qw + 3], d.bq[2 * qw + 1], sh) << gm.lo) & gm.valid;
+                           ripple1(C[0], mx);
+                           ripple1(C[1], my);
+                           ripple1(C[2], mx & my);
+                           ripple1(C[3], gm.valid);
+                           if (kind & S2C_RUN_XBIT) {
+                               uint32_t xm = (funnel(d.bx[qw + 1], d.bx[qw], sh) << gm.lo) & gm.valid;
+                               while (xm) {
+                                   const uint32_t bit = (uint32_t)__builtin_ctz(xm);
+                                   xm &= xm - 1;
+                                   if ((mx >> bit) & 1u) {   // '-' of SEQ (p0 = 1)
+                                       cnt_add1(ccnt, (uint32_t)(wr + (int32_t)bit));
+                                       if (!(kind & S2C_RUN_DROP)) cnt_add1(dcnt, (uint32_t)(wr + (int32_t)bit));
+                                   } else {
+                                       cnt_add1(ncnt, (uint32_t)(wr + (int32_t)bit));
+                                   }
+                               }
+                           }
+                       },
+                       [](uint64_t, uint64_t, uint32_t) {});   // (a dense tile holds no insertion keys)
         }
     }
     PROF_MARK(5);
@@ -1044,7 +1063,7 @@ int s2c_launch_dense(const s2c_dev *dv, hipStream_t st) {
     if (dv->fill_len != 1) return s2c_set_error(S2C_ERR_ARG, "dense tiles need a one-char fill");
     if (dv->n_dense >= ((int64_t)1 << 31)) return s2c_set_error(S2C_ERR_LIMIT, "too many dense tiles");
     DenseArgs a;
-    a.rs = dv->rs; a.lp = dv->lp; a.runs = dv->runs; a.pc = dv->pc; a.ops = dv->ops; a.bq = dv->bq; a.bx = dv->bx; a.tiles = dv->tiles; a.items = dv->dense;
+    a.rs = dv->rs; a.lp = dv->lp; a.pc = dv->pc; a.ops = dv->ops; a.bq = dv->bq; a.bx = dv->bx; a.tiles = dv->tiles; a.items = dv->dense;
     a.thresholds = dv->thresholds; a.tile_stats = dv->tile_stats; a.blk_len = dv->blk_len; a.out = dv->out;
     a.padded_len = (uint32_t)dv->padded_len; a.n_cols = (uint32_t)dv->n_cols; a.n_tiles = (uint32_t)dv->n_tiles;
     a.kwin = (uint32_t)dv->kwin; a.fill_nondash = (uint32_t)dv->fill_nondash;

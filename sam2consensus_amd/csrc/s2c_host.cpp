@@ -1132,14 +1132,20 @@ static bool dense_fits(const uint32_t *tw, int64_t K) {
 static void mark_runs(s2c_batch *b) {
     const int64_t NP = b->info.n_pieces;
     std::vector<uint8_t> need(NP, 0);
-    for (uint32_t slot : b->lp) {   // long pieces (listed by slot)
-        if (b->info.n_long == 0) break;
-        int64_t lo = 0, hi = NP - 1;
-        while (lo < hi) {
-            const int64_t m = (lo + hi + 1) / 2;
-            if (b->pc[4 * m + 2] <= slot) lo = m; else hi = m - 1;
+    // long pieces listed by run slot (k_tile's tiles: k_reads writes their runs); a dense
+    // tile lists its long pieces themselves (k_tile_dense walks them)
+    for (int64_t t = 0; t < b->info.n_tiles && b->info.n_long > 0; t++) {
+        const uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
+        if (tw[3] & S2C_TILE_DENSE) continue;
+        for (uint32_t e = tw[10]; e < tw[11]; e++) {
+            const uint32_t slot = b->lp[e];
+            int64_t lo = 0, hi = NP - 1;
+            while (lo < hi) {
+                const int64_t m = (lo + hi + 1) / 2;
+                if (b->pc[4 * m + 2] <= slot) lo = m; else hi = m - 1;
+            }
+            need[lo] = 1;
         }
-        need[lo] = 1;
     }
     b->rlist.clear();
     const int nt = plan_threads(NP, 1 << 18);
@@ -2355,6 +2361,26 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
         if (fl & (S2C_TILE_DEEP | S2C_TILE_GENERAL)) b->deep.push_back((uint32_t)t);
     }
     clk.mark("items");
+    // the long lists once the tiles' kinds are known: a dense tile lists its long pieces
+    // (k_tile_dense walks them itself), the others their run slots (k_reads' records)
+    if (I.n_long > 0) {
+        std::vector<uint32_t> cnt2(NT + 1, 0);
+        auto is_dense = [&](uint32_t t) { return (b->tiles[(size_t)t * S2C_TILE_WORDS + 3] & S2C_TILE_DENSE) != 0; };
+        for_long([&](uint32_t t, int64_t k) { cnt2[t + 1] += is_dense(t) ? 1u : pcs[order[k]].nslots; });
+        for (int64_t t = 0; t < NT; t++) cnt2[t + 1] += cnt2[t];
+        std::vector<uint32_t> lp2(std::max<uint32_t>(cnt2[NT], 1), 0u), at(cnt2.begin(), cnt2.end() - 1);
+        for_long([&](uint32_t t, int64_t k) {
+            if (is_dense(t)) lp2[at[t]++] = (uint32_t)k;
+            else
+                for (uint64_t sl = ooff[k]; sl < ooff[k + 1]; sl++) lp2[at[t]++] = (uint32_t)sl;
+        });
+        for (int64_t t = 0; t < NT; t++) {
+            b->tiles[(size_t)t * S2C_TILE_WORDS + 10] = cnt2[t];
+            b->tiles[(size_t)t * S2C_TILE_WORDS + 11] = cnt2[t + 1];
+        }
+        b->lp.swap(lp2);
+        I.n_long = cnt2[NT];
+    }
     if (boff >= (1ull << 32) || loff >= (1ull << 32) || coff >= (1ull << 31))
         return s2c_set_error(S2C_ERR_LIMIT, "insertion tables exceed 2^32 slots (split the input)");
     I.n_items = (int64_t)(b->items.size() / S2C_ITEM_WORDS);
@@ -2417,7 +2443,8 @@ static int s2c_batch_shard_impl(const s2c_batch *b, int64_t t0, int64_t t1, s2c_
         };
         for (int64_t t = t0; t < t1; t++) {
             const uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
-            for (uint32_t e = tw[10]; e < tw[11]; e++) take[piece_of_slot(b->lp[e])] = 1;
+            const bool dl = (tw[3] & S2C_TILE_DENSE) != 0;   // (a dense tile lists pieces, others run slots)
+            for (uint32_t e = tw[10]; e < tw[11]; e++) take[dl ? (int64_t)b->lp[e] : piece_of_slot(b->lp[e])] = 1;
         }
         for (int64_t k = 0; k < NP; k++)
             if (b->kmin[k] != 0xFFFFFFFFu && b->kmax[k] >= A && b->kmin[k] < B) take[k] = 1;
@@ -2441,8 +2468,7 @@ static int s2c_batch_shard_impl(const s2c_batch *b, int64_t t0, int64_t t1, s2c_
     s->bx.assign((size_t)J.n_qwords, 0u);
     s->kmin.assign(NS, 0xFFFFFFFFu);
     s->kmax.assign(NS, 0u);
-    std::vector<uint32_t> slot_map;   // old op index → new, for the long lists (sparse use)
-    std::unordered_map<uint32_t, uint32_t> slot_new;
+    std::unordered_map<uint32_t, uint32_t> slot_new, piece_new;   // old op slot / long piece → new
     {
         const uint16_t *sq = (const uint16_t *)b->bq.data(), *sx = (const uint16_t *)b->bx.data();
         uint16_t *dq = (uint16_t *)s->bq.data(), *dx = (uint16_t *)s->bx.data();
@@ -2455,8 +2481,10 @@ static int s2c_batch_shard_impl(const s2c_batch *b, int64_t t0, int64_t t1, s2c_
             pr[1] = (uint32_t)(qoff[i] / 16);
             pr[2] = (uint32_t)ooff[i];
             pr[3] = b->pc[4 * k + 3];
-            if (pr[3] >> 24 & S2C_PF_LONG)
+            if (pr[3] >> 24 & S2C_PF_LONG) {
                 for (uint32_t o = o0; o < o1; o++) slot_new[o] = (uint32_t)(ooff[i] + (o - o0));
+                piece_new[(uint32_t)k] = (uint32_t)i;
+            }
             s->kmin[i] = b->kmin[k];
             s->kmax[i] = b->kmax[k];
             const uint32_t slen = b->pc[4 * k + 3] & 0xFFFFFFu;
@@ -2495,7 +2523,8 @@ static int s2c_batch_shard_impl(const s2c_batch *b, int64_t t0, int64_t t1, s2c_
         nlng = std::max<int64_t>(nlng, (int64_t)tw[6] + tw[7]);
         ncol = std::max<int64_t>(ncol, (int64_t)tw[8] + tw[9]);
         const uint32_t l0 = (uint32_t)s->lp.size();
-        for (uint32_t e = tw[10]; e < tw[11]; e++) s->lp.push_back(slot_new.at(b->lp[e]));
+        const bool dl = (tw[3] & S2C_TILE_DENSE) != 0;
+        for (uint32_t e = tw[10]; e < tw[11]; e++) s->lp.push_back(dl ? piece_new.at(b->lp[e]) : slot_new.at(b->lp[e]));
         tw[10] = l0;
         tw[11] = (uint32_t)s->lp.size();
     }

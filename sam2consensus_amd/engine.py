@@ -42,18 +42,22 @@ def _ptr(t):
 
 
 class Uploader:
-    """H2D of packed batches through pinned host staging: a ring of ``nbuf`` pinned buffers and
-    a copy stream.  ``upload(hb)`` packs the batch's arrays into the next staging buffer (after
-    that buffer's previous copy has completed), copies them to ONE device allocation on the
-    copy stream and makes the compute stream wait on the copy's event, so the host can go on
-    (parsing the next batch) while the copy and the kernels run."""
+    """H2D of packed batches through pinned host staging: a ring of ``nbuf`` pinned buffers of
+    ``chunk`` bytes and a copy stream.  ``upload(arrays)`` lays the arrays out in ONE device
+    allocation and streams them through the ring: each chunk is packed into the next pinned
+    buffer (after that buffer's previous copy has completed) and copied on the copy stream, so
+    packing chunk k + 1 overlaps the DMA of chunk k; the compute stream waits on the last
+    copy's event, and the host goes on (parsing the next batch) while the copies and the
+    kernels run.  Pageable H2D of a GB-sized batch runs at ~2 GB/s on the box; this at the
+    memcpy rate."""
 
     ALIGN = 256
 
-    def __init__(self, device=None, nbuf=2):
+    def __init__(self, device=None, nbuf=4, chunk=16 << 20):
         self.device = _dev(device)
         self.copy_stream = torch.cuda.Stream(self.device)
-        self.slots = [None] * nbuf      # pinned uint8 tensors
+        self.chunk = int(chunk)
+        self.slots = [None] * nbuf      # pinned uint8 tensors of `chunk` bytes
         self.events = [None] * nbuf     # the copy out of each slot
         self.k = 0
 
@@ -64,40 +68,68 @@ class Uploader:
             total += (max(a.nbytes, 16) + self.ALIGN - 1) // self.ALIGN * self.ALIGN
         return offs, max(total, self.ALIGN)
 
-    def upload(self, arrays):
-        """numpy arrays → device uint8 views (each 256-byte aligned, ≥ 16 bytes, zero-padded
-        to its 16-byte end), in HBM once the compute stream reaches this point."""
-        arrays = [np.ascontiguousarray(a) for a in arrays]
-        offs, total = self._layout(arrays)
+    def _slot(self):
         i = self.k % len(self.slots)
         self.k += 1
         if self.events[i] is not None:
             self.events[i].synchronize()          # this slot's previous copy has left it
-        if self.slots[i] is None or self.slots[i].numel() < total:
-            self.slots[i] = torch.empty(int(total * 1.25) + (1 << 20), dtype=torch.uint8, pin_memory=True)
-        host = self.slots[i].numpy()
-        for a, o in zip(arrays, offs):
-            n = a.nbytes
-            host[o:o + n] = a.reshape(-1).view(np.uint8)
-            pad = (-n) % 16 or (16 if n == 0 else 0)
-            host[o + n:o + n + pad] = 0
+        if self.slots[i] is None:
+            self.slots[i] = torch.empty(self.chunk, dtype=torch.uint8, pin_memory=True)
+        return i
+
+    def upload(self, arrays):
+        """numpy arrays → device uint8 views (each 256-byte aligned, ≥ 16 bytes, zero-padded
+        to its 16-byte end), in HBM once the compute stream reaches this point."""
+        arrays = [np.ascontiguousarray(a).reshape(-1).view(np.uint8) for a in arrays]
+        offs, total = self._layout(arrays)
         compute = torch.cuda.current_stream(self.device)
         dev = torch.empty(total, dtype=torch.uint8, device=self.device)   # (on the compute stream)
         self.copy_stream.wait_stream(compute)     # the allocation is free on the compute stream
-        with torch.cuda.stream(self.copy_stream):
-            dev.copy_(self.slots[i][:total], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(self.copy_stream)
+        ends = [o + (max(a.nbytes, 16) + 15) // 16 * 16 for a, o in zip(arrays, offs)]   # (zero pad to 16 bytes)
+        ai = 0
+        ev = None
+        for w0 in range(0, max(ends) if ends else 0, self.chunk):
+            w1 = min(w0 + self.chunk, total)
+            i = self._slot()
+            host = self.slots[i].numpy()
+            while ai < len(arrays) and ends[ai] <= w0:
+                ai += 1
+            j = ai
+            while j < len(arrays) and offs[j] < w1:   # the arrays (and their pads) in [w0, w1)
+                a, o = arrays[j], offs[j]
+                lo, hi = max(o, w0), min(ends[j], w1)
+                n_data = max(0, min(o + a.nbytes, hi) - lo)
+                if n_data:
+                    host[lo - w0:lo - w0 + n_data] = a[lo - o:lo - o + n_data]
+                if lo + n_data < hi:
+                    host[lo - w0 + n_data:hi - w0] = 0
+                j += 1
+            with torch.cuda.stream(self.copy_stream):
+                dev[w0:w1].copy_(self.slots[i][:w1 - w0], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.copy_stream)
+            self.events[i] = ev
         dev.record_stream(self.copy_stream)
-        self.events[i] = ev
-        compute.wait_event(ev)
+        if ev is not None:
+            compute.wait_event(ev)
         return [dev[o:o + max(a.nbytes, 16)] for a, o in zip(arrays, offs)], dev
 
 
+_UPLOADERS = {}
+
+
+def default_uploader(device=None):
+    """The process's Uploader for a device (its pinned ring allocated once)."""
+    d = _dev(device)
+    if d not in _UPLOADERS:
+        _UPLOADERS[d] = Uploader(d)
+    return _UPLOADERS[d]
+
+
 class DeviceBatch:
-    """The packed batch resident in HBM (inputs of every launch).  With an ``Uploader`` the
-    arrays go through its pinned staging buffers and copy stream (asynchronous); without,
-    each array is copied synchronously."""
+    """The packed batch resident in HBM (inputs of every launch).  With an ``Uploader`` (by
+    default for batches of 64 MB or more) the arrays go through its pinned staging ring and
+    copy stream (asynchronous); otherwise each array is copied synchronously."""
 
     ARRAYS = ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile", "rlist", "ps",
               "lly", "lpc", "lops", "lbq", "lbx")
@@ -106,6 +138,8 @@ class DeviceBatch:
         self.device = _dev(device) if uploader is None else uploader.device
         self.hb = hb.ensure_layers()
         self.info = hb.info
+        if uploader is None and sum(np.asarray(getattr(hb, n)).nbytes for n in self.ARRAYS) >= (64 << 20):
+            uploader = default_uploader(self.device)   # (large batches: pinned chunks, not pageable copies)
         if uploader is not None:
             views, self._storage = uploader.upload([np.asarray(getattr(hb, n)).reshape(-1) for n in self.ARRAYS])
             for name, v in zip(self.ARRAYS, views):

@@ -198,7 +198,10 @@ def check_plan(hb):
         if fl & PF_LONG:
             for t in range(int(hb.wtile[w0]), int(hb.wtile[w1]) + 1):
                 sl = set(lp[T[t, 10]:T[t, 11]].tolist())
-                assert set(range(pc[k, 2], pc[k + 1, 2])) <= sl
+                if T[t, 3] & 4:   # a dense tile lists its long pieces (k_tile_dense walks them)
+                    assert k in sl
+                else:             # the others their run slots (k_reads' records)
+                    assert set(range(pc[k, 2], pc[k + 1, 2])) <= sl
         else:
             assert w1 - w0 <= K, "short piece beyond the window"
     assert sorted(hb.deep.tolist()) == [t for t in range(i.n_tiles) if T[t, 3] & 3]
@@ -212,9 +215,16 @@ def check_plan(hb):
         if row[3] == 4:
             ns, nq = row[16] - row[15], row[18] - row[17]
             assert 4 * ((ns + 65) & ~1) + 8 * (nq + 32) + 4 * ((nq + 65) & ~1) + 8 * ns <= S2C_DENSE_LDS and nq <= 4096
-    # k_reads' list: the long pieces (their runs feed the tile long lists) and the insertion emitters
+    # k_reads' list: the long pieces listed by non-dense tiles (their runs feed those tiles' long
+    # lists) and the insertion emitters
     fl = pc[:NP, 3] >> 24
     assert (((fl & 16) != 0) <= ((fl & PF_LONG) != 0)).all()
+    by_slot = set()
+    for t in range(i.n_tiles):
+        if not T[t, 3] & 4:
+            for e in range(T[t, 10], T[t, 11]):
+                by_slot.add(int(np.searchsorted(pc[:NP, 2], lp[e], side="right")) - 1)
+    assert set(np.nonzero((fl & 16) != 0)[0].tolist()) == by_slot
     assert set(hb.rlist.tolist()) == set(np.nonzero(((fl & 16) != 0) | ((fl & PF_INS) != 0))[0].tolist())
 
 
