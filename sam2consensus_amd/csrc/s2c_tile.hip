@@ -115,6 +115,15 @@ __device__ __forceinline__ TileRec tile_rec(const uint32_t *tiles, uint32_t t) {
             uni(v2.x), uni(v2.y), uni(v2.z), uni(v2.w), uni(v3.x)};
 }
 
+// walk_piece's view of the batch in HBM (a dense tile's long pieces in counts-only modes)
+struct TileMem {
+    const uint32_t *ops, *bq, *bx;
+    __device__ __forceinline__ uint32_t op(uint32_t j) const { return ops[j]; }
+    __device__ __forceinline__ uint32_t p0(uint64_t w) const { return bq[2 * w]; }
+    __device__ __forceinline__ uint32_t p1(uint64_t w) const { return bq[2 * w + 1]; }
+    __device__ __forceinline__ uint32_t x(uint64_t w) const { return bx[w]; }
+};
+
 // symbol code ("-ACGNT" index) of query base q
 __device__ __forceinline__ uint32_t base_code(const uint32_t *bq, const uint32_t *bx, uint64_t q) {
     const uint64_t w = q >> 5;
@@ -1158,26 +1167,20 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     constexpr uint32_t G = WG / NWP;
     const uint32_t w = tid / G, g = tid % G, W = W0 + w;
     const bool active = w < nwords;
-    // ---- long-piece records (rare; k_reads' run records through the tile's long list,
-    //      counted once per tile: by its first item), one per lane and round
+    // ---- long pieces (rare), counted once per tile (by its first item), one list entry per
+    //      lane and round: k_reads' run records through the tile's long list of run slots, or
+    //      for a dense tile (run here in counts-only modes) its long pieces themselves, walked
+    //      from HBM (walk_piece) — each run's part in the lane's word W
     {
-        const uint32_t nlong = l0 == 0 ? T.lp1 - T.lp0 : 0u;
-        const uint32_t ntr = uni(__ockl_wfred_max_u32(active && g < nlong ? (nlong - g + G - 1) / G : 0u));
-        for (uint32_t m = 0; m < ntr; m++) {
-            if (acc >= 255u) flush(w, g, G, active);
-            acc++;
-            const uint32_t j = g + G * m;
-            if (!(active && j < nlong)) continue;
-            const uint32_t slot = d.lp[T.lp0 + j];
-            const Run r = run_of(((const uint4 *)d.runs)[slot]);
-            const RecGeom gm = rec_geom(r.gpos, r.len, W);
-            if (!gm.valid) continue;
+        auto one_run = [&](uint32_t gpos, uint32_t len, uint32_t kind, uint64_t q) {
+            const RecGeom gm = rec_geom(gpos, len, W);
+            if (!gm.valid) return;
             const uint32_t p0 = 32 * w + gm.lo, p1 = p0 + (uint32_t)__popc(gm.valid);
-            if ((r.kind & 3u) == S2C_RUN_DASH) {
+            if ((kind & 3u) == S2C_RUN_DASH) {
                 atomicAdd(&dD[p0], 1);
                 atomicSub(&dD[p1], 1);
-            } else if ((r.kind & 3u) == S2C_RUN_BASES) {
-                const uint64_t qs = r.q + gm.qs, qw = qs >> 5;
+            } else if ((kind & 3u) == S2C_RUN_BASES) {
+                const uint64_t qs = q + gm.qs, qw = qs >> 5;
                 const uint32_t sh = (uint32_t)(qs & 31);
                 const uint32_t mx = (funnel(d.bq[2 * qw + 2], d.bq[2 * qw], sh) << gm.lo) & gm.valid;
                 const uint32_t my = (funnel(d.bq[2 * qw + 3], d.bq[2 * qw + 1], sh) << gm.lo) & gm.valid;
@@ -1186,19 +1189,41 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
                 ripple1(Z, mx & my);
                 atomicAdd(&dV[p0], 1);
                 atomicSub(&dV[p1], 1);
-                if (r.kind & S2C_RUN_XBIT) {
+                if (kind & S2C_RUN_XBIT) {
                     uint32_t xm = (funnel(d.bx[qw + 1], d.bx[qw], sh) << gm.lo) & gm.valid;
                     while (xm) {
                         const uint32_t bit = (uint32_t)__builtin_ctz(xm);
                         xm &= xm - 1;
                         if ((mx >> bit) & 1u) {   // '-' of SEQ (p0 = 1)
                             H::add1(hist, SL_SD, 32 * w + bit, 1u);
-                            if (!(r.kind & S2C_RUN_DROP)) H::add1(hist, SL_SDC, 32 * w + bit, 1u);
+                            if (!(kind & S2C_RUN_DROP)) H::add1(hist, SL_SDC, 32 * w + bit, 1u);
                         } else {
                             H::add1(hist, SL_N, 32 * w + bit, 1u);
                         }
                     }
                 }
+            }
+        };
+        const bool lpieces = (T.flags & S2C_TILE_DENSE) != 0;
+        const uint32_t nlong = l0 == 0 ? T.lp1 - T.lp0 : 0u;
+        const uint32_t ntr = uni(__ockl_wfred_max_u32(active && g < nlong ? (nlong - g + G - 1) / G : 0u));
+        for (uint32_t m = 0; m < ntr; m++) {
+            // (a walked piece adds at most one to a position: its runs cover disjoint positions)
+            if (acc >= 255u) flush(w, g, G, active);
+            acc++;
+            const uint32_t j = g + G * m;
+            if (!(active && j < nlong)) continue;
+            const uint32_t e = d.lp[T.lp0 + j];
+            if (lpieces) {
+                const uint4 P = ((const uint4 *)d.pc)[e];
+                walk_piece(TileMem{d.ops, d.bq, d.bx}, P, d.pc[4 * (size_t)e + 6], d.maxdel_active != 0, d.maxdel,
+                           [&](uint32_t, uint32_t gp, uint32_t l, uint32_t kind, uint64_t q) {
+                               if (kind != S2C_RUN_EMPTY) one_run(gp, l, kind, q);
+                           },
+                           [](uint64_t, uint64_t, uint32_t) {});   // (a dense tile holds no insertion keys)
+            } else {
+                const Run r = run_of(((const uint4 *)d.runs)[e]);
+                one_run(r.gpos, r.len, r.kind, r.q);
             }
         }
     }

@@ -156,10 +156,14 @@ class Workspace:
     """All scratch + output buffers for one (batch, thresholds, fill, maxdel) configuration."""
 
     def __init__(self, db: DeviceBatch, thresholds, min_depth=1, fill=b"-", keep_counts=False,
-                 maxdel_active=None, maxdel=None, counts=None):
+                 maxdel_active=None, maxdel=None, counts=None, tile_range=None):
         dev = db.device
         i = db.info
         self.db = db
+        # tile_range (t0, t1): launch only those tiles (their work items, dense and deep lists
+        # filtered) and fetch only their results — a streamed batch's final tiles without
+        # cutting a sub-batch
+        self.tile_range = tile_range
         self.T = len(thresholds)
         sz = L.WsSizes()
         L.check(lib.s2c_workspace_sizes(C.byref(i), self.T, C.byref(sz)))
@@ -195,6 +199,19 @@ class Workspace:
             setattr(d, name, _ptr(getattr(db, name)))
         d.n_pieces, d.n_ops, d.n_qwords, d.n_tiles = i.n_pieces, i.n_ops, i.n_qwords, i.n_tiles
         d.n_items, d.n_dense, d.n_deep = i.n_items, i.n_dense, i.n_deep
+        if tile_range is not None:
+            t0, t1 = tile_range
+            hb = db.hb
+            keep = lambda a, col: a[(a[:, col] >= t0) & (a[:, col] < t1)] if len(a) else a  # noqa: E731
+            self._sel = {"items": keep(hb.items, 0), "dense": keep(hb.dense, 0),
+                         "deep": hb.deep[(hb.deep >= t0) & (hb.deep < t1)]}
+            for name, a in self._sel.items():
+                t = _up(np.ascontiguousarray(a).reshape(-1), dev)
+                self._sel[name] = t
+                setattr(d, name, _ptr(t))
+            d.n_items = int(len(keep(hb.items, 0)))
+            d.n_dense = int(len(keep(hb.dense, 0)))
+            d.n_deep = int(((hb.deep >= t0) & (hb.deep < t1)).sum())
         d.padded_len, d.chunk, d.kwin, d.tile_max = i.padded_len, i.chunk, i.kwin, i.tile_max
         d.dense_lds = i.dense_lds
         d.n_rlist = i.n_rlist
@@ -290,21 +307,24 @@ class Workspace:
         torch.cuda.current_stream(self.db.device).synchronize()
         i = self.db.info
         R, T, nb = i.n_refs, self.T, i.n_tiles
+        t0, t1 = self.tile_range if self.tile_range is not None else (0, nb)
         stats = np.zeros((R, T, 4), dtype=np.uint64)
-        if nb:
+        if t1 > t0:
             ts = self.tile_stats[: T * nb * 32].view(torch.int64).cpu().numpy().view(np.uint64).reshape(T, nb, 4)
-            ref = self.db.hb.tiles[:, 2].astype(np.int64)
+            ref = self.db.hb.tiles[t0:t1, 2].astype(np.int64)
             for t in range(T):
-                np.add.at(stats[:, t, :], ref, ts[t])
-        if T * nb == 0:
+                np.add.at(stats[:, t, :], ref, ts[t, t0:t1])
+        nr = t1 - t0
+        if T * nr == 0:
             return stats, np.zeros(1, dtype=np.uint64), b""
         # each tile wrote its body into its slot; the references' bodies are their tiles'
-        # pieces in order: gather them into [t][tile] order (one vectorised index)
-        lens = self.blk_len[: T * nb * 8].view(torch.int64).cpu().numpy().astype(np.int64)
-        blocks = self.db.hb.tiles.astype(np.int64)
+        # pieces in order: gather them into [t][tile] order (host threads, s2c_gather_bodies)
+        lens = self.blk_len[: T * nb * 8].view(torch.int64).cpu().numpy().astype(np.int64).reshape(T, nb)
+        lens = np.ascontiguousarray(lens[:, t0:t1]).reshape(-1)
+        blocks = self.db.hb.tiles[t0:t1].astype(np.int64)
         slot = self.fill_w * blocks[:, 0] + blocks[:, 8]                     # F·a + cb0
         starts = (np.arange(T, dtype=np.int64)[:, None] * self.out_stride + slot[None, :]).reshape(-1)
-        offs = np.zeros(T * nb + 1, dtype=np.int64)
+        offs = np.zeros(T * nr + 1, dtype=np.int64)
         np.cumsum(lens, out=offs[1:])
         total = int(offs[-1])
         raw = self.out[: T * self.out_stride].cpu().numpy()

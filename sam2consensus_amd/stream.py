@@ -157,9 +157,10 @@ class _Producer:
             self.t.join()
 
 
-def _sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, state):
+def _sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, state, ranged=False):
     """Generator (producer thread) of the streamed run of sorted input: ("run", sub, t0, t1)
-    for every final tile range, then ("last", hb) with the final batch."""
+    for every final tile range — a cut sub-batch, or with ``ranged`` the snapshot itself
+    (the device side runs its tiles [t0, t1)) — then ("last", hb) with the final batch."""
     p = StreamParser(maxdel_active, 150, tile_width)
     t_done, pending, broken = 0, 0, False
     tm = state.setdefault("t", {})
@@ -195,11 +196,15 @@ def _sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, st
                 t1 = int(np.searchsorted(hb.tiles[:, 1].astype(np.int64), bound, side="right"))
                 if t1 <= t_done:
                     continue
-                t0 = clk()
-                sub = _sub(hb, t_done, t1)
-                add("cut", t0)
-                state["absorb"](hb)
                 gmin = int(hb.tiles[t1, 0]) if t1 < NT else int(hb.info.padded_len)
+                state["absorb"](hb)
+                t0 = clk()
+                if ranged:            # the device runs the snapshot's tiles [t_done, t1) itself
+                    sub, hb = hb, None
+                    sub.t0_range = t_done
+                else:
+                    sub = _sub(hb, t_done, t1)
+                add("cut", t0)
                 t0 = clk()
                 p.retain(gmin)
                 add("retain", t0)
@@ -208,7 +213,8 @@ def _sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, st
                 if stats_hook:
                     stats_hook(t_done, NT, held)
             finally:
-                hb.free()
+                if hb is not None:
+                    hb.free()
         t0 = clk()
         hb = p.finish()
         add("finish", t0)
@@ -218,9 +224,9 @@ def _sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, st
             hb.free()
             raise NotSorted("a read reaches positions already emitted")
         NT = int(hb.info.n_tiles)
+        state["absorb"](hb)
         if t_done < NT:
             yield ("run", _sub(hb, t_done, NT), t_done, NT)
-        state["absorb"](hb)
         yield ("last", hb)
     finally:
         p.close()
@@ -262,16 +268,21 @@ def stream_batches(blocks, thresholds, runner, maxdel_active=True, tile_width=DE
     ct = {"launch": 0.0, "collect": 0.0, "wait": 0.0}
     clk = time.perf_counter
     tw = clk()
-    for item in _Producer(_sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, state)):
+    ranged = getattr(runner, "launch_range", None)
+    for item in _Producer(_sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, state,
+                                        ranged is not None)):
         ct["wait"] += clk() - tw
         if item[0] == "last":
             hb = item[1]
             break
         _, sub, t0, t1 = item
-        sub.t0, sub.t1 = t0, t1
         tl = clk()
         try:
-            h = launch(sub) if launch else runner(sub)
+            if ranged is not None and getattr(sub, "t0_range", None) is not None:
+                h = ranged(sub, t0, t1)
+            else:
+                sub.t0, sub.t1 = t0, t1
+                h = launch(sub) if launch else runner(sub)
         except BaseException:
             sub.free()
             raise
@@ -425,6 +436,14 @@ class DeviceRunner:
     def launch(self, sub):
         from .engine import DeviceBatch, Workspace
         ws = Workspace(DeviceBatch(sub, uploader=self.up), self.thresholds, self.min_depth, self.fill)
+        ws.run()
+        return _Launched(ws)
+
+    def launch_range(self, hb, t0, t1):
+        """The tiles [t0, t1) of a snapshot, without cutting a sub-batch (Workspace tile_range)."""
+        from .engine import DeviceBatch, Workspace
+        ws = Workspace(DeviceBatch(hb, uploader=self.up), self.thresholds, self.min_depth, self.fill,
+                       tile_range=(t0, t1))
         ws.run()
         return _Launched(ws)
 

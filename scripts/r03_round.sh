@@ -15,8 +15,6 @@ if [ -z "$NOHOST" ]; then
   cat gpurun_out/stream_rss_c5_$T.json; echo
 fi
 if [ -n "$EXP" ]; then
-  S2C_TILE_POS=2048 timeout -k 10 300 python -u bench.py --workload c5 --steps 10 --warmup 2 --no-cpu-baseline --no-file-parse > gpurun_out/${T}_c5_tp2048.json 2> gpurun_out/${T}_c5_tp2048.err || { tail -5 gpurun_out/${T}_c5_tp2048.err; exit 1; }
-  python -c "import json;d=json.load(open('gpurun_out/${T}_c5_tp2048.json'));print('c5 tp2048 step', round(d['ms_per_step'],4), {k: round(v,4) for k,v in d['kernels_ms'].items()}, d['parity'])"
   timeout -k 10 300 python -u scripts/prof_dense.py c5 0 > gpurun_out/${T}_prof_dense.txt 2>&1 || { tail -5 gpurun_out/${T}_prof_dense.txt; exit 1; }
   cat gpurun_out/${T}_prof_dense.txt
   timeout -k 10 400 python -u bench.py --workload c5 --steps 10 --warmup 2 --no-cpu-baseline --no-file-parse --rehearse-shards 8 > gpurun_out/${T}_c5_shards8.json 2> gpurun_out/${T}_c5_shards8.err || { tail -5 gpurun_out/${T}_c5_shards8.err; exit 1; }
