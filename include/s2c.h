@@ -228,6 +228,8 @@ int  s2c_parser_progress(const s2c_parser *p, int64_t *out);
    ++ ... (n blocks; dst holds their total length), copied on the host threads.  The tiles'
    body slots after the D2H copy of the device output, in [threshold][tile] order. */
 int  s2c_gather_bodies(const uint8_t *raw, const int64_t *starts, const int64_t *lens, int64_t n, uint8_t *dst);
+/* n bytes src → dst on the host threads (the host side of a batch's H2D staging). */
+int  s2c_copy_bytes(void *dst, const void *src, int64_t n);
 int  s2c_parser_pack(s2c_parser *p, int64_t g0, int64_t g1, size_t *len);
 int  s2c_parser_blob_copy(const s2c_parser *p, void *dst, size_t cap);
 int  s2c_parser_unpack(s2c_parser *p, const void *blob, size_t len);

@@ -1686,6 +1686,21 @@ extern "C" int s2c_gather_bodies(const uint8_t *raw, const int64_t *starts, cons
     return s2c_guarded([&] { return s2c_gather_bodies_impl(raw, starts, lens, n, dst); });
 }
 
+// n bytes src → dst on the host threads (staging a batch into pinned buffers for its H2D:
+// one thread's memcpy runs at a fraction of the memory bandwidth)
+static int s2c_copy_bytes_impl(void *dst, const void *src, int64_t n) {
+    if (n < 0 || (n > 0 && (!dst || !src))) return s2c_set_error(S2C_ERR_ARG, "bad copy arguments");
+    const int64_t pieces = std::max<int64_t>(1, n >> 20);   // 1 MB pieces
+    par_ranges(plan_threads(n, (int64_t)1 << 21), pieces, [&](int, int64_t i0, int64_t i1) {
+        const int64_t a = n * i0 / pieces, b = n * i1 / pieces;
+        memcpy((char *)dst + a, (const char *)src + a, (size_t)(b - a));
+    });
+    return S2C_OK;
+}
+extern "C" int s2c_copy_bytes(void *dst, const void *src, int64_t n) {
+    return s2c_guarded([&] { return s2c_copy_bytes_impl(dst, src, n); });
+}
+
 extern "C" int s2c_parser_progress(const s2c_parser *p, int64_t *out) {
     if (!p || !out) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
     out[0] = p->in_header ? 0 : 1;

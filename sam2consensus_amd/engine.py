@@ -53,7 +53,7 @@ class Uploader:
 
     ALIGN = 256
 
-    def __init__(self, device=None, nbuf=4, chunk=16 << 20):
+    def __init__(self, device=None, nbuf=4, chunk=32 << 20):
         self.device = _dev(device)
         self.copy_stream = torch.cuda.Stream(self.device)
         self.chunk = int(chunk)
@@ -99,7 +99,9 @@ class Uploader:
                 a, o = arrays[j], offs[j]
                 lo, hi = max(o, w0), min(ends[j], w1)
                 n_data = max(0, min(o + a.nbytes, hi) - lo)
-                if n_data:
+                if n_data >= (1 << 20):   # (large pieces on the host threads)
+                    L.check(lib.s2c_copy_bytes(host.ctypes.data + (lo - w0), a.ctypes.data + (lo - o), n_data))
+                elif n_data:
                     host[lo - w0:lo - w0 + n_data] = a[lo - o:lo - o + n_data]
                 if lo + n_data < hi:
                     host[lo - w0 + n_data:hi - w0] = 0

@@ -348,3 +348,17 @@ def test_gather_bodies_concatenates_blocks():
     with pytest.raises(_lib.S2CError):
         _lib.check(_lib.lib.s2c_gather_bodies(raw.ctypes.data, bad.ctypes.data, bad.ctypes.data, 1,
                                               raw.ctypes.data))
+
+
+def test_copy_bytes_matches_memcpy():
+    """s2c_copy_bytes (engine.Uploader's staging copy into its pinned ring): any length, any
+    alignment, split over the host threads, byte-identical to a plain copy."""
+    rng = np.random.default_rng(11)
+    src = rng.integers(0, 256, size=(1 << 23) + 77, dtype=np.uint8)
+    for n, a, b in ((0, 0, 0), (1, 3, 5), (4097, 1, 0), ((1 << 21) + 13, 7, 3), (src.size - 9, 9, 0)):
+        dst = np.zeros(n + 16, dtype=np.uint8)
+        _lib.check(_lib.lib.s2c_copy_bytes(dst.ctypes.data + b, src.ctypes.data + a, n))
+        assert np.array_equal(dst[b:b + n], src[a:a + n])
+        assert not dst[:b].any() and not dst[b + n:].any()
+    with pytest.raises(_lib.S2CError):
+        _lib.check(_lib.lib.s2c_copy_bytes(None, src.ctypes.data, 5))
