@@ -38,7 +38,8 @@
 // phase clocks (diagnostic build `make prof`, scripts/prof_dense.py): Σ over sampled waves
 // (one tile in 64) of the s_memtime deltas of each phase
 __device__ unsigned long long g_prof[16];
-__device__ uint32_t g_abl;   // ablation bits (timing only; results wrong): 1 events, 2 count, 4 walk, 8 vote
+__device__ uint32_t g_abl;   // ablation bits (timing only; results wrong): 1 events, 2 count, 4 walk, 8 vote,
+                             // 16 queued walk, 32 N / '-' events
 #define ABL(b) ((g_abl & (b)) != 0)
 #define PROF_MARK(i)                                                                               \
     do {                                                                                           \
@@ -530,7 +531,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     for (int u = 0; u < 8; u++) xs[u] = xin ? bxl[min(xwa + u, (xq0 + xl - 1) >> 5)] : 0u;
     // queued pieces: the general walk; '-' runs and SEQ N / '-' straight into the byte counters.
     // A queued piece's record comes from the lane that loaded it (ds_bpermute, all lanes on).
-    for (uint32_t base = 0; base < nslow; base += WGD) {
+    for (uint32_t base = 0; base < (ABL(16) ? 0u : nslow); base += WGD) {
         const uint32_t i = base + lane;
         const uint32_t qe = i < nslow ? queue[i] : 0u;
         if (i < nslow && (qe >> 31)) cnt_range(dcnt, (int32_t)((qe >> 12) & 0xFFFu), (int32_t)(qe & 0xFFFu), TL);
@@ -731,13 +732,13 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     }
     PROF_MARK(5);
     // queued single-token runs of reads with N / '-' in SEQ (never dropped: maxdel is off)
-    if (xin) {
+    if (xin && !ABL(32)) {
         uint2 xp[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) xp[u] = bql[min(xwa + u, (xq0 + xl - 1) >> 5)];
         x_events_pre(bxl, bql, xs, xp, xq0, xl, (int32_t)xrv.x - T0, TL, false, dcnt, ncnt, ccnt);
     }
-    for (uint32_t i = lane + WGD; i < nx; i += WGD) {
+    for (uint32_t i = lane + WGD; i < (ABL(32) ? 0u : nx); i += WGD) {
         const uint2 rv = runl[queue[qcap - 1u - i]];
         x_events(bxl, bql, rv.y >> 15, (rv.y >> 4) & 0x7FFu, (int32_t)rv.x - T0, TL, false, dcnt, ncnt, ccnt);
     }

@@ -42,7 +42,7 @@ for bits in bits_list:
     f(buf, 0)
     waves = max(buf[8], 1)
     tot = sum(buf[i] for i in range(len(names)))
-    print("ablate %d (1 events, 2 count, 4 walk, 8 vote): step %.3f ms" % (bits, ev0.elapsed_time(ev1) / N))
+    print("ablate %d (1 events, 2 count, 4 walk, 8 vote, 16 queued walk, 32 N/- events): step %.3f ms" % (bits, ev0.elapsed_time(ev1) / N))
     for i, nm in enumerate(names):
         print("  %-18s %9.0f cyc/wave  %5.1f%%" % (nm, buf[i] / waves, 100.0 * buf[i] / max(tot, 1)))
     print("  groups/wave %.1f pieces/wave %.1f staged dwords/wave %.0f slow/wave %.2f xq/wave %.2f" % (

@@ -15,7 +15,7 @@ if [ -z "$NOHOST" ]; then
   cat gpurun_out/stream_rss_c5_$T.json; echo
 fi
 if [ -n "$EXP" ]; then
-  timeout -k 10 300 python -u scripts/prof_dense.py c5 0 > gpurun_out/${T}_prof_dense.txt 2>&1 || { tail -5 gpurun_out/${T}_prof_dense.txt; exit 1; }
+  timeout -k 10 300 python -u scripts/prof_dense.py c5 ${ABL:-0} > gpurun_out/${T}_prof_dense.txt 2>&1 || { tail -5 gpurun_out/${T}_prof_dense.txt; exit 1; }
   cat gpurun_out/${T}_prof_dense.txt
   timeout -k 10 400 python -u bench.py --workload c5 --steps 10 --warmup 2 --no-cpu-baseline --no-file-parse --rehearse-shards 8 > gpurun_out/${T}_c5_shards8.json 2> gpurun_out/${T}_c5_shards8.err || { tail -5 gpurun_out/${T}_c5_shards8.err; exit 1; }
   python -c "import json;d=json.load(open('gpurun_out/${T}_c5_shards8.json'));print('c5 shards8', d['shard_rehearsal'])"
