@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define S2C_ABI_VERSION 8
+#define S2C_ABI_VERSION 9
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define S2C_OK            0
@@ -121,6 +121,7 @@ int s2c_layout(int64_t *out, int n);
                                  k_tile (S2C_CHUNK_*); ly0 = S2C_LY_MAIN: one layer, the window read in
                                  place from the sorted arrays (pf0 .. qw1) */
 #define S2C_LY_MAIN 0xFFFFFFFFu
+#define S2C_LY_NONE 0xFFFFFFFEu   /* a dense tile whose layered windows were not built (s2c_batch_layers_mode) */
 #define S2C_TILE_DEEP     1  /* several work items: counts summed in HBM, voted by k_consensus */
 #define S2C_TILE_GENERAL  2  /* insertion layout beyond k_tile's LDS: voted by k_consensus */
 #define S2C_TILE_DENSE    4  /* routed to k_tile_dense (one item, no insertion keys); its long list (lp[lp0, lp1)) holds
@@ -268,6 +269,7 @@ typedef struct {
     int64_t n_lpieces;         /* pieces of the layered arrays (lpc) */
     int64_t n_lops;            /* op words of the layered arrays (lops) */
     int64_t n_lqwords;         /* plane words of the layered arrays (lbq, lbx) */
+    int64_t layers_dense;      /* 1: the dense tiles' layered windows are built too (counts-only modes) */
 } s2c_batch_info;
 
 typedef struct {               /* host pointers into the batch (valid until s2c_batch_free) */
@@ -305,8 +307,12 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
 
 /* Build the batch's layered windows (s2c_batch_arrays lly .. lbx, tile word 20) if not yet
  * built: required before a batch's arrays go to the device; snapshots that are only cut into
- * shards never pay for them (each shard builds its own). */
+ * shards never pay for them (each shard builds its own).  s2c_batch_layers builds them for
+ * every tile; s2c_batch_layers_mode(b, 0) skips the dense tiles (k_tile_dense reads their
+ * windows in place; tile word 20 = S2C_LY_NONE), which s2c_run needs and the counts-only
+ * modes refuse — (b, 1) afterwards rebuilds them all. */
 int  s2c_batch_layers(s2c_batch *b);
+int  s2c_batch_layers_mode(s2c_batch *b, int with_dense);
 int  s2c_batch_info_get(const s2c_batch *b, s2c_batch_info *out);
 int  s2c_batch_arrays_get(const s2c_batch *b, s2c_batch_arrays *out);
 /* The sub-batch of tiles [t0, t1) for one GPU of a multi-GPU run (positions keep their
@@ -392,6 +398,8 @@ typedef struct {
                                   blk_len bytes each.  A reference's body for threshold t is its
                                   tiles' pieces in order. */
     int64_t   out_cap;         /* ≥ T·(F·padded_len + n_cols) */
+    int64_t   layers_dense;    /* the batch's info.layers_dense: s2c_pileup_counts and s2c_accumulate
+                                  run dense tiles through k_tile and refuse a batch without them */
 } s2c_dev;
 
 /* Sizes (bytes) of every workspace / output buffer for a batch and T thresholds. */

@@ -55,7 +55,7 @@ class BatchInfo(C.Structure):
         "aligned_bases", "query_bases", "n_pieces", "n_ops", "n_tokens", "n_qwords", "n_words",
         "n_tiles", "n_items", "n_dense", "n_deep", "n_long", "n_rlist", "kwin", "tile_max", "chunk",
         "n_ins", "n_ins_bases", "n_bkt", "n_lng", "n_cols", "runs_max", "dense_lds", "n_layers", "n_lpieces", "n_lops",
-        "n_lqwords")]
+        "n_lqwords", "layers_dense")]
 
 
 _P64 = C.POINTER(C.c_int64)
@@ -92,7 +92,7 @@ class Dev(C.Structure):
         ("fill_len", C.c_int32), ("fill_nondash", C.c_int32), ("fill", _VP),
         ("runs", _VP), ("ibkt", _VP), ("ilong", _VP), ("ilong_n", _VP), ("counts", _VP),
         ("ins_cols", _VP), ("ins_chr", _VP), ("n_cols", C.c_int64),
-        ("tile_stats", _VP), ("blk_len", _VP), ("out", _VP), ("out_cap", C.c_int64)]
+        ("tile_stats", _VP), ("blk_len", _VP), ("out", _VP), ("out_cap", C.c_int64), ("layers_dense", C.c_int64)]
 
 
 class WsSizes(C.Structure):
@@ -109,7 +109,7 @@ EXPORTS = [
     "s2c_parser_retain_events", "s2c_accumulate",
     "s2c_parser_pos_weights", "s2c_parser_checks", "s2c_parser_counters", "s2c_parser_progress", "s2c_gather_bodies", "s2c_copy_bytes", "s2c_parser_pack",
     "s2c_parser_blob_copy", "s2c_parser_unpack",
-    "s2c_batch_layers", "s2c_batch_info_get", "s2c_batch_arrays_get", "s2c_batch_ref_name", "s2c_batch_free", "s2c_batch_shard",
+    "s2c_batch_layers", "s2c_batch_layers_mode", "s2c_batch_info_get", "s2c_batch_arrays_get", "s2c_batch_ref_name", "s2c_batch_free", "s2c_batch_shard",
     "s2c_parsecigar", "s2c_synth_feed", "s2c_synth_write",
     "s2c_workspace_sizes", "s2c_reads", "s2c_pileup", "s2c_consensus", "s2c_run", "s2c_pileup_counts",
 ]
@@ -151,6 +151,7 @@ def _load():
         "s2c_parser_blob_copy": (C.c_int, [_VP, _VP, C.c_size_t]),
         "s2c_parser_unpack": (C.c_int, [_VP, _VP, C.c_size_t]),
         "s2c_batch_layers": (C.c_int, [_VP]),
+        "s2c_batch_layers_mode": (C.c_int, [_VP, C.c_int]),
         "s2c_batch_info_get": (C.c_int, [_VP, C.POINTER(BatchInfo)]),
         "s2c_batch_arrays_get": (C.c_int, [_VP, C.POINTER(BatchArrays)]),
         "s2c_batch_ref_name": (C.c_char_p, [_VP, C.c_int64]),

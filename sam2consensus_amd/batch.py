@@ -106,12 +106,14 @@ class HostBatch:
         self.ref_nblocks = nb.astype(np.int64)
         self.ref_first_block = (np.cumsum(nb) - nb).astype(np.int64)
 
-    def ensure_layers(self):
+    def ensure_layers(self, dense=False):
         """Build the layered windows of the tiles k_tile does not read in place
-        (s2c_batch_layers; before the arrays go to the device) and view them."""
-        if self._layers:
+        (s2c_batch_layers_mode; before the arrays go to the device) and view them.  The dense
+        tiles' are built only with ``dense`` (the counts-only modes run them through k_tile;
+        the pileup reads their windows in place); a later ``dense=True`` rebuilds them all."""
+        if self._layers and (self.info.layers_dense or not dense):
             return self
-        L.check(lib.s2c_batch_layers(self._b))
+        L.check(lib.s2c_batch_layers_mode(self._b, 1 if dense else 0))
         L.check(lib.s2c_batch_info_get(self._b, C.byref(self.info)))
         a = L.BatchArrays()
         L.check(lib.s2c_batch_arrays_get(self._b, C.byref(a)))

@@ -57,7 +57,7 @@ __device__ uint32_t g_abl;   // ablation bits (timing only; results wrong): 1 ev
 namespace s2c {
 namespace {
 
-__constant__ uint8_t c_amb[64] = {
+__constant__ __attribute__((aligned(16))) uint8_t c_amb[64] = {
 #define E(i) AMB.v[i]
     E(0), E(1), E(2), E(3), E(4), E(5), E(6), E(7), E(8), E(9), E(10), E(11), E(12), E(13), E(14), E(15),
     E(16), E(17), E(18), E(19), E(20), E(21), E(22), E(23), E(24), E(25), E(26), E(27), E(28), E(29), E(30), E(31),
@@ -491,33 +491,53 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         const bool fast = plain && nops == 1u;
         const uint32_t take = min(l, slen), q = 16u * (P.y - 2u * qw0);
         if (fast) runl[j] = make_uint2(P.x, (q << 15) | (take << 4) | S2C_RUN_BASES | (xf ? S2C_RUN_XBIT : 0u));
-        // bases, D / N / P, bases (the deletion reads; no N / '-' in SEQ): two base runs here
-        // (:64-72: k = take, then l1 '-', then SEQ[l : l + min(l2, len(SEQ) − l)]), the '-' run
-        // queued for the byte counters unless maxdel drops it (:210: l1 dashes)
+        // bases, D / N / P, bases (the deletion reads): two base runs here (:64-72: k = take,
+        // then l1 '-', then SEQ[l : l + min(l2, len(SEQ) − l)]), the '-' run queued for the byte
+        // counters unless maxdel drops it (:210: l1 dashes); with N / '-' in SEQ (no maxdel
+        // count to take: `plain`) both base runs go to the X-run queue
         bool fdel = false, fdash = false;
-        uint32_t da = 0, db = 0;   // the '-' run's tile-relative range, clipped to the tile
-        if (plain && nops == 3u && !xf) {
+        uint32_t da = 0, db = 0, t2 = 0;   // the '-' run's tile-relative range, clipped to the tile
+        if (plain && nops == 3u) {
             const uint32_t w1 = opl[j + 1], w2 = opl[j + 2];
             if (op_dash(w1 & 15u) && op_bases(w2 & 15u)) {
-                const uint32_t l1 = w1 >> 4, t2 = l < slen ? min(w2 >> 4, slen - l) : 0u;
+                const uint32_t l1 = w1 >> 4, xb = xf ? S2C_RUN_XBIT : 0u;
+                t2 = l < slen ? min(w2 >> 4, slen - l) : 0u;
                 const int32_t r0 = (int32_t)(P.x + take) - T0;
                 da = (uint32_t)min(max(r0, 0), TL);
                 db = (uint32_t)min(max(r0 + (int32_t)l1, 0), TL);
                 fdel = true;
                 fdash = db > da && !(mda && l1 > d.maxdel);
-                runl[j] = make_uint2(P.x, (q << 15) | (take << 4) | S2C_RUN_BASES);
+                runl[j] = make_uint2(P.x, (q << 15) | (take << 4) | S2C_RUN_BASES | xb);
                 runl[j + 1] = make_uint2(0u, 0u);
-                runl[j + 2] = make_uint2(P.x + take + l1, ((q + l) << 15) | (t2 << 4) | S2C_RUN_BASES);
+                runl[j + 2] = make_uint2(P.x + take + l1, ((q + l) << 15) | (t2 << 4) | S2C_RUN_BASES | xb);
             }
         }
-        // queue: pieces for the general walk (their index), and the '-' runs of the deletion
-        // reads (1 << 31 | begin << 12 | end, tile-relative: TL ≤ 2048)
-        const bool qd = (in && !fast && !fdel) || fdash;
-        const uint64_t bs = __ballot(qd), bxm = __ballot(fast && xf);
+        // queue: pieces for the general walk (their index) and the '-' runs of the deletion
+        // reads (1 << 31 | begin << 12 | end, tile-relative: TL ≤ 2048) from the front; the X
+        // runs' slots from the back.  A lane adds ≤ 3 entries (an X deletion read), so while
+        // that could overrun the wave's queue (64 entries kept per walk iteration left) such
+        // reads take the general walk instead (≤ 1 entry per lane)
+        bool x1 = (fast || fdel) && xf, x2 = fdel && xf && t2 > 0u;
+        bool qd = (in && !fast && !fdel) || fdash;
+        uint64_t bs = __ballot(qd), bxm = __ballot(x1), bx2 = __ballot(x2);
+        if (nslow + nx + (uint32_t)(__popcll(bs) + __popcll(bxm) + __popcll(bx2)) > qcap - WGD * (nitw - 1u - it)) {
+            if (fdel && xf) {
+                fdel = false;
+                fdash = false;
+            }
+            x1 = fast && xf;
+            x2 = false;
+            qd = (in && !fast && !fdel) || fdash;
+            bs = __ballot(qd);
+            bxm = __ballot(x1);
+            bx2 = 0;
+        }
         if (qd) queue[nslow + mbcnt(bs)] = fdel ? 0x80000000u | (da << 12) | db : k;
-        if (fast && xf) queue[qcap - 1u - nx - mbcnt(bxm)] = j;
-        nslow += (uint32_t)__popcll(bs);
+        if (x1) queue[qcap - 1u - nx - mbcnt(bxm)] = j;
         nx += (uint32_t)__popcll(bxm);
+        if (x2) queue[qcap - 1u - nx - mbcnt(bx2)] = j + 2u;
+        nx += (uint32_t)__popcll(bx2);
+        nslow += (uint32_t)__popcll(bs);
     }
     lds_sync();
     PROF_MARK(2);
@@ -987,7 +1007,7 @@ __global__ __launch_bounds__(WT) S2C_DENSE_OCC void k_tile_dense(const DenseArgs
     // one byte per position (row layout): '-' (D/N/P runs, '-' of SEQ unless maxdel drops
     // the read's), 'N' of SEQ, '-' of SEQ (all: the planes count them as C, and 'N' as A)
     __shared__ __attribute__((aligned(16))) uint32_t dcnt[8 * NWP], ncnt[8 * NWP], ccnt[8 * NWP];
-    __shared__ uint8_t amb[64];
+    __shared__ __attribute__((aligned(16))) uint8_t amb[64];
     __shared__ uint32_t stl[2][WPT][4];
 #ifdef S2C_PROF
     const unsigned long long t_entry = __builtin_amdgcn_s_memtime();
@@ -1018,18 +1038,30 @@ __global__ __launch_bounds__(WT) S2C_DENSE_OCC void k_tile_dense(const DenseArgs
     }
     const uint32_t w = (tid >> 6) * (NWP / WPT) + (tid & 63) / G, W = v.W0 + w, K = d.kwin;
     uint32_t cw0 = 0, cw1 = 0;
-    if (w < v.nwords) {
-        cw0 = d.rs[W >= K ? W - K : 0u] - v.o0;
-        cw1 = d.rs[W + 1] - v.o0;
+    if (w < v.nwords) {   // (window-relative after the wait below: no early wait on the DMA)
+        cw0 = d.rs[W >= K ? W - K : 0u];
+        cw1 = d.rs[W + 1];
     }
-    if (tid < 64) amb[tid] = c_amb[tid];
-    const uint32_t fill0 = uni((uint32_t)d.fill[0]);
+    // the ambiguity table and the fill char by scalar loads (a vector load's wait here would
+    // also wait for the window DMA issued before it)
+    {
+        v16i r;
+        asm volatile("s_load_dwordx16 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(uni_ptr((const uint32_t *)c_amb)) : "memory");
+        if (tid == 0) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) ((uint32_t *)amb)[i] = (uint32_t)r[i];
+        }
+    }
+    const uintptr_t fa = (uintptr_t)d.fill;
+    const uint32_t fill0 = (sload1((const uint32_t *)(fa & ~(uintptr_t)3)) >> (8 * (uint32_t)(fa & 3))) & 0xFFu;
     for (uint32_t k = tid; k < 8 * NWP; k += WT) {
         dcnt[k] = 0;
         ncnt[k] = 0;
         ccnt[k] = 0;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the window landed
+    cw0 -= v.o0;
+    cw1 -= v.o0;
     lds_sync();
     dense_tile<NWP>(d, v, wl, dcnt, ncnt, ccnt, amb, fill0, Pp, oe, cw0, cw1, t_entry, stl);
 }

@@ -1283,7 +1283,7 @@ static bool main_window_fits(const s2c_batch *b, const uint32_t *tw, int64_t K, 
 // place, its nl layers in order, each a copy of its short pieces (records with re-based qh /
 // opoff, op words, base planes and non-ACGT words of SEQ[0:len], len the record's length
 // field), contiguous (the kernel's DMA takes each array's 16-byte phase).
-static void build_layers(s2c_batch *b, const PieceBlocks &B, int64_t G) {
+static void build_layers(s2c_batch *b, int64_t G, bool with_dense) {
     s2c_batch_info &I = b->info;
     const int64_t NT = I.n_tiles, K = I.kwin;
     std::vector<uint64_t> lyp, lyo, lyh;   // layer starts: pieces, op words, plane half-words
@@ -1292,13 +1292,23 @@ static void build_layers(s2c_batch *b, const PieceBlocks &B, int64_t G) {
     std::vector<TL> tl;
     for (int64_t t = 0; t < NT; t++) {
         uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
+        if (!with_dense && (tw[3] & S2C_TILE_DENSE)) {   // (k_tile_dense reads its window in place)
+            tw[20] = S2C_LY_NONE;
+            continue;
+        }
         if (tw[19] == 1 && main_window_fits(b, tw, K, G)) {
             tw[20] = S2C_LY_MAIN;
             continue;
         }
-        const int64_t nl = tw[19], W0 = tw[0] >> 5, W1 = (tw[1] + 31) >> 5, S0 = std::max<int64_t>(W0 - K, 0);
-        tw[20] = (uint32_t)(lyp.size() - 1);
-        tl.push_back({t, (int64_t)lyp.size() - 1, nl});
+        tl.push_back({t, 0, (int64_t)tw[19]});
+    }
+    PieceBlocks B;
+    if (!tl.empty()) piece_blocks(b, B);
+    for (TL &T : tl) {
+        uint32_t *tw = &b->tiles[(size_t)T.t * S2C_TILE_WORDS];
+        const int64_t nl = T.nl, W0 = tw[0] >> 5, W1 = (tw[1] + 31) >> 5, S0 = std::max<int64_t>(W0 - K, 0);
+        T.ly0 = (int64_t)lyp.size() - 1;
+        tw[20] = (uint32_t)T.ly0;
         for (int64_t l = 0; l < nl; l++) {
             uint64_t np = 0, no = 0, nh = 0;
             for (int64_t s = S0; s < W1; s++) {
@@ -1315,6 +1325,7 @@ static void build_layers(s2c_batch *b, const PieceBlocks &B, int64_t G) {
     }
     const int64_t NL = (int64_t)lyp.size() - 1;
     I.n_layers = NL;
+    I.layers_dense = with_dense ? 1 : 0;
     I.n_lpieces = (int64_t)lyp.back();
     I.n_lops = (int64_t)lyo.back();
     I.n_lqwords = (int64_t)(lyh.back() / 2) + 2;   // (+ the funnel word after the last)
@@ -2593,19 +2604,20 @@ extern "C" int s2c_batch_shard(const s2c_batch *b, int64_t t0, int64_t t1, s2c_b
     return s2c_guarded([&] { return s2c_batch_shard_impl(b, t0, t1, out); });
 }
 
-static int s2c_batch_layers_impl(s2c_batch *b) {
+static int s2c_batch_layers_impl(s2c_batch *b, bool with_dense) {
     if (!b) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
-    if (b->layers) return S2C_OK;
+    if (b->layers && (b->info.layers_dense || !with_dense)) return S2C_OK;
     int64_t nwp = 8;
     while (nwp * 32 < b->info.tile_max) nwp *= 2;
-    PieceBlocks PB;
-    piece_blocks(b, PB);
-    build_layers(b, PB, 64 / nwp);
+    build_layers(b, 64 / nwp, with_dense);
     b->layers = true;
     return S2C_OK;
 }
 extern "C" int s2c_batch_layers(s2c_batch *b) {
-    return s2c_guarded([&] { return s2c_batch_layers_impl(b); });
+    return s2c_guarded([&] { return s2c_batch_layers_impl(b, true); });
+}
+extern "C" int s2c_batch_layers_mode(s2c_batch *b, int with_dense) {
+    return s2c_guarded([&] { return s2c_batch_layers_impl(b, with_dense != 0); });
 }
 
 extern "C" int s2c_batch_info_get(const s2c_batch *b, s2c_batch_info *out) {

@@ -1665,6 +1665,8 @@ extern "C" int s2c_pileup_counts(const s2c_dev *d, void *stream) {
     int rc = check_dev(d);
     if (rc) return rc;
     if (!d->counts) return s2c_set_error(S2C_ERR_ARG, "counts buffer required");
+    if (d->n_dense > 0 && !d->layers_dense)   // (k_tile takes the dense tiles here: their layers)
+        return s2c_set_error(S2C_ERR_ARG, "counts-only modes need the dense tiles' layered windows (s2c_batch_layers_mode(b, 1))");
     hipStream_t s = (hipStream_t)stream;
     if ((rc = s2c_launch_reads(d, s, true))) return rc;   // run records of every piece (compared by the tests)
     TileArgs a = tile_args(*d);
@@ -1681,6 +1683,8 @@ extern "C" int s2c_accumulate(const s2c_dev *d, int keep_tables, void *stream) {
     int rc = check_dev(d);
     if (rc) return rc;
     if (!d->counts) return s2c_set_error(S2C_ERR_ARG, "counts buffer required");
+    if (d->n_dense > 0 && !d->layers_dense)   // (k_tile takes the dense tiles here: their layers)
+        return s2c_set_error(S2C_ERR_ARG, "counts-only modes need the dense tiles' layered windows (s2c_batch_layers_mode(b, 1))");
     hipStream_t s = (hipStream_t)stream;
     if ((rc = s2c_launch_reads(d, s, false))) return rc;   // events hashed, long pieces' runs
     TileArgs a = tile_args(*d);

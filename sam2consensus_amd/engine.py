@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import time
 
 import numpy as np
 import torch
@@ -60,6 +61,7 @@ class Uploader:
         self.slots = [None] * nbuf      # pinned uint8 tensors of `chunk` bytes
         self.events = [None] * nbuf     # the copy out of each slot
         self.k = 0
+        self.timing = {"alloc": 0.0, "wait": 0.0, "pack": 0.0, "issue": 0.0}   # host seconds, cumulative
 
     def _layout(self, arrays):
         offs, total = [], 0
@@ -71,10 +73,14 @@ class Uploader:
     def _slot(self):
         i = self.k % len(self.slots)
         self.k += 1
+        t0 = time.perf_counter()
         if self.events[i] is not None:
             self.events[i].synchronize()          # this slot's previous copy has left it
+        t1 = time.perf_counter()
         if self.slots[i] is None:
             self.slots[i] = torch.empty(self.chunk, dtype=torch.uint8, pin_memory=True)
+        self.timing["wait"] += t1 - t0
+        self.timing["alloc"] += time.perf_counter() - t1
         return i
 
     def upload(self, arrays):
@@ -83,7 +89,9 @@ class Uploader:
         arrays = [np.ascontiguousarray(a).reshape(-1).view(np.uint8) for a in arrays]
         offs, total = self._layout(arrays)
         compute = torch.cuda.current_stream(self.device)
+        t0 = time.perf_counter()
         dev = torch.empty(total, dtype=torch.uint8, device=self.device)   # (on the compute stream)
+        self.timing["alloc"] += time.perf_counter() - t0
         self.copy_stream.wait_stream(compute)     # the allocation is free on the compute stream
         ends = [o + (max(a.nbytes, 16) + 15) // 16 * 16 for a, o in zip(arrays, offs)]   # (zero pad to 16 bytes)
         ai = 0
@@ -92,6 +100,7 @@ class Uploader:
             w1 = min(w0 + self.chunk, total)
             i = self._slot()
             host = self.slots[i].numpy()
+            t0 = time.perf_counter()
             while ai < len(arrays) and ends[ai] <= w0:
                 ai += 1
             j = ai
@@ -106,11 +115,14 @@ class Uploader:
                 if lo + n_data < hi:
                     host[lo - w0 + n_data:hi - w0] = 0
                 j += 1
+            t1 = time.perf_counter()
             with torch.cuda.stream(self.copy_stream):
                 dev[w0:w1].copy_(self.slots[i][:w1 - w0], non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(self.copy_stream)
             self.events[i] = ev
+            self.timing["pack"] += t1 - t0
+            self.timing["issue"] += time.perf_counter() - t1
         dev.record_stream(self.copy_stream)
         if ev is not None:
             compute.wait_event(ev)
@@ -136,10 +148,12 @@ class DeviceBatch:
     ARRAYS = ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile", "rlist", "ps",
               "lly", "lpc", "lops", "lbq", "lbx")
 
-    def __init__(self, hb, device=None, uploader=None):
+    def __init__(self, hb, device=None, uploader=None, dense_layers=False):
         self.device = _dev(device) if uploader is None else uploader.device
-        self.hb = hb.ensure_layers()
-        self.info = hb.info
+        # dense_layers: the dense tiles' layered windows too (Workspace's counts-only modes run
+        # them through k_tile); the pileup reads them in place, so by default they are not built
+        self.hb = hb.ensure_layers(dense_layers)
+        self.info = type(hb.info).from_buffer_copy(hb.info)   # (the arrays as uploaded)
         if uploader is None and sum(np.asarray(getattr(hb, n)).nbytes for n in self.ARRAYS) >= (64 << 20):
             uploader = default_uploader(self.device)   # (large batches: pinned chunks, not pageable copies)
         if uploader is not None:
@@ -166,6 +180,8 @@ class Workspace:
         # filtered) and fetch only their results — a streamed batch's final tiles without
         # cutting a sub-batch
         self.tile_range = tile_range
+        if (keep_counts or counts is not None) and i.n_dense > 0 and not i.layers_dense:
+            raise ValueError("counts-only modes run the dense tiles through k_tile: DeviceBatch(..., dense_layers=True)")
         self.T = len(thresholds)
         sz = L.WsSizes()
         L.check(lib.s2c_workspace_sizes(C.byref(i), self.T, C.byref(sz)))
@@ -218,6 +234,7 @@ class Workspace:
         d.dense_lds = i.dense_lds
         d.n_rlist = i.n_rlist
         d.n_layers, d.n_lpieces, d.n_lops, d.n_lqwords = i.n_layers, i.n_lpieces, i.n_lops, i.n_lqwords
+        d.layers_dense = i.layers_dense
         # the maxdel rule (:210) runs on the device: the parser's setting unless overridden
         if maxdel_active is None:
             maxdel_active = getattr(db.hb, "maxdel_active", True)

@@ -325,7 +325,7 @@ class DeviceAccumulator:
         from .engine import DeviceBatch, Uploader, Workspace
         if self.up is None:
             self.up = Uploader(self.device)
-        db = DeviceBatch(hb, uploader=self.up)
+        db = DeviceBatch(hb, uploader=self.up, dense_layers=True)   # (s2c_accumulate: k_tile takes the dense tiles)
         if self.counts is None:
             self.counts = torch.zeros(max(6 * int(hb.info.padded_len) * 4, 16), dtype=torch.uint8, device=db.device)
         return Workspace(db, self.thresholds, self.min_depth, self.fill, counts=self.counts)

@@ -21,7 +21,7 @@ def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else "c2"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     hb = configs.synth_batch(wl)
-    ws = Workspace(DeviceBatch(hb), [0.25, 0.5, 0.75], keep_counts=True)   # mode 4 stores all counts
+    ws = Workspace(DeviceBatch(hb, dense_layers=True), [0.25, 0.5, 0.75], keep_counts=True)   # mode 4 stores all counts
     times = {m: [] for m in MODES}
     for _ in range(reps):
         for m in MODES:

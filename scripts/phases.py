@@ -22,7 +22,7 @@ def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else "c2"
     extra = int(sys.argv[2], 0) if len(sys.argv) > 2 else 0
     hb = configs.synth_batch(wl)
-    ws = Workspace(DeviceBatch(hb), [0.25, 0.5, 0.75], keep_counts=True)
+    ws = Workspace(DeviceBatch(hb, dense_layers=True), [0.25, 0.5, 0.75], keep_counts=True)
     ni = hb.info.n_items
     for _ in range(3):
         ws.run()

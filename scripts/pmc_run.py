@@ -22,7 +22,7 @@ def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else "c2"
     mask = int(sys.argv[2], 0) if len(sys.argv) > 2 else 0
     hb = configs.synth_batch(wl)
-    ws = Workspace(DeviceBatch(hb), configs_thresholds(wl), keep_counts=True)
+    ws = Workspace(DeviceBatch(hb, dense_layers=True), configs_thresholds(wl), keep_counts=True)
     ws.dev.ablate = mask
     for _ in range(3):
         ws.pileup()

@@ -259,7 +259,7 @@ def check_layers(hb):
     order, of the short pieces of its proportional per-start-word slices (records, op words,
     the planes of SEQ[0:len]), 16-byte aligned, within the chunk's caps; records per word
     and counting lane; every item's records per word fit its u16 histogram."""
-    hb.ensure_layers()
+    hb.ensure_layers(dense=True)
     i = hb.info
     pc = hb.pc.astype(np.int64)
     nwp = 8

@@ -37,7 +37,7 @@ def test_hip_path_matches_reference(case):
 
 def _ws(hb, thresholds, min_depth=1, fill=b"-", keep_counts=False):
     from sam2consensus_amd.engine import DeviceBatch, Workspace
-    db = DeviceBatch(hb)
+    db = DeviceBatch(hb, dense_layers=keep_counts)
     return Workspace(db, thresholds, min_depth, fill, keep_counts)
 
 

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
     assert declared <= exported, declared - exported
     assert declared == set(_lib.EXPORTS)
-    assert _lib.lib.s2c_abi_version() == 8
+    assert _lib.lib.s2c_abi_version() == 9
 
 
 def _model_case(sam, args):
@@ -362,3 +362,34 @@ def test_copy_bytes_matches_memcpy():
         assert not dst[:b].any() and not dst[b + n:].any()
     with pytest.raises(_lib.S2CError):
         _lib.check(_lib.lib.s2c_copy_bytes(None, src.ctypes.data, 5))
+
+
+def test_layers_without_dense_tiles():
+    """s2c_batch_layers_mode(b, 0) (DeviceBatch's default: the pileup reads dense windows in
+    place): dense tiles get S2C_LY_NONE and no layered copies, every other tile the layers of
+    the full build; mode 1 afterwards rebuilds them all (batch_model.check_layers)."""
+    import batch_model
+    from sam2consensus_amd import configs
+    LY_NONE = 0xFFFFFFFE
+    full = configs.synth_batch("c5", ref_len=200_000, ins_frac=0.01)
+    full.ensure_layers(dense=True)
+    hb = configs.synth_batch("c5", ref_len=200_000, ins_frac=0.01)
+    hb.ensure_layers()
+    i = hb.info
+    dense = (hb.tiles[:, 3] & 4) != 0
+    assert 0 < dense.sum() < i.n_tiles and i.layers_dense == 0
+    assert (hb.tiles[dense, 20] == LY_NONE).all() and not (hb.tiles[~dense, 20] == LY_NONE).any()
+    assert i.n_lpieces < full.info.n_lpieces
+    for t in np.nonzero(~dense)[0]:   # the same layers, renumbered past the dense tiles'
+        r, f = hb.tiles[t], full.tiles[t]
+        if f[20] == 0xFFFFFFFF:
+            assert r[20] == f[20]
+            continue
+        for l in range(int(f[19])):
+            a, b = hb.lly[r[20] + l:r[20] + l + 2, 0], full.lly[f[20] + l:f[20] + l + 2, 0]
+            assert a[1] - a[0] == b[1] - b[0]
+            assert (hb.lpc[a[0]:a[1], [0, 3]] == full.lpc[b[0]:b[1], [0, 3]]).all()
+    hb.ensure_layers(dense=True)
+    assert hb.info.layers_dense == 1 and hb.info.n_lpieces == full.info.n_lpieces
+    assert (hb.tiles[:, 20] == full.tiles[:, 20]).all()
+    batch_model.check_layers(hb)
