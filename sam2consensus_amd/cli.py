@@ -59,12 +59,12 @@ def consensus_batch(hb, thresholds, prefix, min_depth=1, fill=b"-", nchar=0, dev
     """Device pipeline on a parsed HostBatch → {``REF__PREFIX.fasta``: bytes}."""
     import torch
 
-    from .engine import DeviceBatch, Workspace
+    from .engine import DeviceBatch, Workspace, needs_dense_layers
     from .records import build_records, render
 
     t = timings if timings is not None else {}
     t0 = time.perf_counter()
-    db = DeviceBatch(hb, device)
+    db = DeviceBatch(hb, device, dense_layers=needs_dense_layers(fill))
     ws = Workspace(db, thresholds, min_depth, fill)
     torch.cuda.synchronize(db.device)
     t["h2d"] = time.perf_counter() - t0
@@ -216,7 +216,7 @@ def consensus_files_sharded(filename, thresholds, prefix, min_depth, fill, nchar
     import torch.distributed as dist
 
     from .dparse import parse_distributed
-    from .engine import DeviceBatch, Workspace
+    from .engine import DeviceBatch, Workspace, needs_dense_layers
     from .records import build_records, render
     from .shard import gather_results
 
@@ -234,7 +234,8 @@ def consensus_files_sharded(filename, thresholds, prefix, min_depth, fill, nchar
     P = parse_distributed(filename, rank, world, maxdel_active)
     if log and rank == 0:
         _log_summary(log, _Counters(P.hb.info.n_refs, P))
-    ws = Workspace(DeviceBatch(P.sub, "cuda:%d" % local), thresholds, min_depth, fill)
+    ws = Workspace(DeviceBatch(P.sub, "cuda:%d" % local, dense_layers=needs_dense_layers(fill)), thresholds,
+                   min_depth, fill)
     ws.run()
     res = gather_results(ws.fetch(), P.sub, rank, world, len(thresholds))
     if rank != 0:

@@ -1638,6 +1638,10 @@ extern "C" int s2c_pileup(const s2c_dev *d, void *stream) {
     }
     if (d->n_dense > 0) {
         // dense tiles emit exactly one char per position: len(fill) must be 1, else k_tile
+        // (which reads their layered windows)
+        if (d->fill_len != 1 && !d->layers_dense)
+            return s2c_set_error(S2C_ERR_ARG, "a fill of length != 1 runs the dense tiles through k_tile: their layered "
+                                              "windows are needed (s2c_batch_layers_mode(b, 1))");
         rc = d->fill_len == 1 ? s2c_launch_dense(d, s) : launch_tiles(a, d->tile_max, d->dense, d->n_dense, s);
         if (rc) return rc;
     }

@@ -140,6 +140,13 @@ def default_uploader(device=None):
     return _UPLOADERS[d]
 
 
+def needs_dense_layers(fill=b"-", counts=False):
+    """Whether a Workspace runs the dense tiles through k_tile (so its DeviceBatch needs
+    ``dense_layers=True``): the counts-only modes, and a fill of length != 1 (k_tile_dense
+    emits one char per position)."""
+    return bool(counts) or len(fill.encode("latin-1") if isinstance(fill, str) else bytes(fill)) != 1
+
+
 class DeviceBatch:
     """The packed batch resident in HBM (inputs of every launch).  With an ``Uploader`` (by
     default for batches of 64 MB or more) the arrays go through its pinned staging ring and
@@ -180,8 +187,9 @@ class Workspace:
         # filtered) and fetch only their results — a streamed batch's final tiles without
         # cutting a sub-batch
         self.tile_range = tile_range
-        if (keep_counts or counts is not None) and i.n_dense > 0 and not i.layers_dense:
-            raise ValueError("counts-only modes run the dense tiles through k_tile: DeviceBatch(..., dense_layers=True)")
+        if needs_dense_layers(fill, keep_counts or counts is not None) and i.n_dense > 0 and not i.layers_dense:
+            raise ValueError("counts-only modes and a fill of length != 1 run the dense tiles through k_tile: "
+                             "DeviceBatch(..., dense_layers=True)")
         self.T = len(thresholds)
         sz = L.WsSizes()
         L.check(lib.s2c_workspace_sizes(C.byref(i), self.T, C.byref(sz)))

@@ -169,7 +169,13 @@ def _sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, st
     def add(k, t0):
         tm[k] = tm.get(k, 0.0) + clk() - t0
     try:
-        for blk in blocks:
+        it = iter(blocks)
+        while True:
+            t0 = clk()
+            blk = next(it, None)   # (the input's next block: file read / inflate)
+            add("read", t0)
+            if blk is None:
+                break
             t0 = clk()
             p.feed(blk)
             add("feed", t0)
@@ -197,7 +203,9 @@ def _sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, st
                 if t1 <= t_done:
                     continue
                 gmin = int(hb.tiles[t1, 0]) if t1 < NT else int(hb.info.padded_len)
+                t0 = clk()
                 state["absorb"](hb)
+                add("absorb", t0)
                 t0 = clk()
                 if ranged:            # the device runs the snapshot's tiles [t_done, t1) itself
                     sub, hb = hb, None
@@ -434,15 +442,17 @@ class DeviceRunner:
         self.up = Uploader(device)
 
     def launch(self, sub):
-        from .engine import DeviceBatch, Workspace
-        ws = Workspace(DeviceBatch(sub, uploader=self.up), self.thresholds, self.min_depth, self.fill)
+        from .engine import DeviceBatch, Workspace, needs_dense_layers
+        ws = Workspace(DeviceBatch(sub, uploader=self.up, dense_layers=needs_dense_layers(self.fill)), self.thresholds,
+                       self.min_depth, self.fill)
         ws.run()
         return _Launched(ws)
 
     def launch_range(self, hb, t0, t1):
         """The tiles [t0, t1) of a snapshot, without cutting a sub-batch (Workspace tile_range)."""
-        from .engine import DeviceBatch, Workspace
-        ws = Workspace(DeviceBatch(hb, uploader=self.up), self.thresholds, self.min_depth, self.fill,
+        from .engine import DeviceBatch, Workspace, needs_dense_layers
+        ws = Workspace(DeviceBatch(hb, uploader=self.up, dense_layers=needs_dense_layers(self.fill)), self.thresholds,
+                       self.min_depth, self.fill,
                        tile_range=(t0, t1))
         ws.run()
         return _Launched(ws)

@@ -36,8 +36,8 @@ def test_hip_path_matches_reference(case):
 
 
 def _ws(hb, thresholds, min_depth=1, fill=b"-", keep_counts=False):
-    from sam2consensus_amd.engine import DeviceBatch, Workspace
-    db = DeviceBatch(hb, dense_layers=keep_counts)
+    from sam2consensus_amd.engine import DeviceBatch, Workspace, needs_dense_layers
+    db = DeviceBatch(hb, dense_layers=needs_dense_layers(fill, keep_counts))
     return Workspace(db, thresholds, min_depth, fill, keep_counts)
 
 
@@ -233,14 +233,15 @@ def test_sharded_on_device_matches_golden(name, world):
     C3 and C4 split 8 ways as BASELINE.json runs them: deep and layered tiles cut by shard
     boundaries (each shard re-lays its pieces and layered windows)."""
     from sam2consensus_amd import configs, shard
-    from sam2consensus_amd.engine import DeviceBatch, Workspace
+    from sam2consensus_amd.engine import DeviceBatch, Workspace, needs_dense_layers
     g = CONFIGS[name]
     opt = o.parse_argv(["-i", g["sam_file"]] + g["args"])
     hb = configs.synth_batch(name)
     parts, stats = [], None
     for rank in range(world):
         sub = shard.sub_batch(hb, rank, world)
-        ws = Workspace(DeviceBatch(sub), opt.thresholds, opt.min_depth, opt.fill.encode())
+        ws = Workspace(DeviceBatch(sub, dense_layers=needs_dense_layers(opt.fill.encode())), opt.thresholds,
+                       opt.min_depth, opt.fill.encode())
         ws.run()
         st, offs, out = ws.fetch()
         stats = st if stats is None else stats + st
