@@ -25,7 +25,14 @@ class Parser:
         self._p = C.c_void_p()
         L.check(lib.s2c_parser_new(1 if maxdel_active else 0, int(maxdel), C.byref(self._p)))
 
-    def feed(self, data: bytes):
+    def feed(self, data):
+        """bytes, or a writable buffer (bytearray / its memoryview: read in place)."""
+        if isinstance(data, (bytearray, memoryview)):
+            mv = memoryview(data).cast("B")
+            if mv.nbytes == 0:
+                return
+            L.check(lib.s2c_parser_feed(self._p, (C.c_char * mv.nbytes).from_buffer(mv), mv.nbytes))
+            return
         L.check(lib.s2c_parser_feed(self._p, data, len(data)))
 
     def feed_file(self, path: str):

@@ -420,14 +420,24 @@ def _merge(parts, T):
 
 
 def file_blocks(filename, block=BLOCK):
-    """The file's bytes in blocks (".gz" → gzip, :111-114)."""
-    op = gzip.open if filename.endswith(".gz") else open
-    with op(filename, "rb") as fh:
+    """The file's bytes in blocks (".gz" → gzip, :111-114).  A plain file is read into one
+    reused buffer (each block is a view of it, valid until the next is read: the parser
+    copies what it keeps), so no block pays for fresh pages."""
+    if filename.endswith(".gz"):
+        with gzip.open(filename, "rb") as fh:
+            while True:
+                b = fh.read(block)
+                if not b:
+                    return
+                yield b
+        return
+    buf = bytearray(block)
+    with open(filename, "rb", buffering=0) as fh:
         while True:
-            b = fh.read(block)
-            if not b:
+            n = fh.readinto(buf)
+            if not n:
                 return
-            yield b
+            yield memoryview(buf)[:n]
 
 
 class DeviceRunner:
