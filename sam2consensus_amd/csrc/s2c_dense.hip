@@ -546,9 +546,42 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     const bool xin = lane < nx;
     const uint2 xrv = xin ? runl[queue[qcap - 1u - lane]] : make_uint2(0u, 0u);
     const uint32_t xq0 = xrv.y >> 15, xl = (xrv.y >> 4) & 0x7FFu, xwa = xq0 >> 5;
+#ifdef S2C_XPAIRS
+    // the (run, plane word) pairs of the first 64 X runs, flattened over the lanes: run r (lane
+    // r) owns pairs [xoff, xoff + xnw); a lane finds its pair's run by binary search over the
+    // runs' offsets (ds_bpermute, all lanes on) and requests its one non-ACGT word now
+    const uint32_t xnw = xin ? ((xq0 + xl - 1u) >> 5) - xwa + 1u : 0u;
+    uint32_t xinc = xnw;
+#pragma unroll
+    for (uint32_t dd = 1; dd < 64; dd <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)xinc, dd, 64);
+        xinc += lane >= dd ? t : 0u;
+    }
+    const uint32_t xoff = xinc - xnw, nrun = min(nx, 64u);
+    const uint32_t npair = uni((uint32_t)__shfl((int)xinc, 63, 64));
+    // pair p → its run's first query base q0, length l, tile-relative position r0 of q0, word qw
+    auto pair_of = [&](uint32_t p, uint32_t &q0, uint32_t &l, int32_t &r0, uint32_t &qw) {
+        uint32_t r = 0;
+#pragma unroll
+        for (uint32_t st = 32; st; st >>= 1) {
+            const uint32_t c = r + st;
+            const uint32_t oc = (uint32_t)__shfl((int)xoff, (int)min(c, 63u), 64);
+            r = (c < nrun && oc <= p) ? c : r;
+        }
+        q0 = (uint32_t)__shfl((int)xq0, (int)r, 64);
+        l = (uint32_t)__shfl((int)xl, (int)r, 64);
+        r0 = __shfl((int)xrv.x, (int)r, 64) - T0;
+        qw = (q0 >> 5) + (p - (uint32_t)__shfl((int)xoff, (int)r, 64));
+    };
+    uint32_t pq0, pl, pqw;
+    int32_t pr0;
+    pair_of(lane, pq0, pl, pr0, pqw);
+    const uint32_t pxw = lane < npair ? bxl[pqw] : 0u;
+#else
     uint32_t xs[8];
 #pragma unroll
     for (int u = 0; u < 8; u++) xs[u] = xin ? bxl[min(xwa + u, (xq0 + xl - 1) >> 5)] : 0u;
+#endif
     // queued pieces: the general walk; '-' runs and SEQ N / '-' straight into the byte counters.
     // A queued piece's record comes from the lane that loaded it (ds_bpermute, all lanes on).
     for (uint32_t base = 0; base < (ABL(16) ? 0u : nslow); base += WGD) {
@@ -752,12 +785,46 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     }
     PROF_MARK(5);
     // queued single-token runs of reads with N / '-' in SEQ (never dropped: maxdel is off)
+#ifdef S2C_XPAIRS
+    // one plane word per lane and round: its bits inside the run, 'N' / '-' by the base plane
+    auto pair_events = [&](uint32_t xw, uint32_t q0, uint32_t l, int32_t r0, uint32_t qw) {
+        const int32_t b0 = (int32_t)(32 * qw) - (int32_t)q0;   // run offset of the word's bit 0
+        uint32_t xm = xw;
+        if (b0 < 0) xm &= 0xFFFFFFFFu << (uint32_t)(-b0);
+        if (b0 + 32 > (int32_t)l) xm &= 0xFFFFFFFFu >> (uint32_t)(b0 + 32 - (int32_t)l);
+        if (!xm) return;
+        const uint2 ps = bql[qw];
+        xm &= ~ps.y;   // (p1 = 0 for every non-ACGT char)
+        while (xm) {
+            const uint32_t bit = (uint32_t)__builtin_ctz(xm);
+            xm &= xm - 1;
+            const int32_t r = r0 + b0 + (int32_t)bit;
+            if (r < 0 || r >= TL) continue;
+            if ((ps.x >> bit) & 1u) {
+                cnt_add1(ccnt, (uint32_t)r);
+                cnt_add1(dcnt, (uint32_t)r);
+            } else {
+                cnt_add1(ncnt, (uint32_t)r);
+            }
+        }
+    };
+    for (uint32_t rb = 0; rb < (ABL(32) ? 0u : npair); rb += WGD) {   // (uniform rounds)
+        uint32_t q0 = pq0, l = pl, qw = pqw, xw = pxw;
+        int32_t r0 = pr0;
+        if (rb) {
+            pair_of(rb + lane, q0, l, r0, qw);
+            xw = rb + lane < npair ? bxl[qw] : 0u;
+        }
+        if (rb + lane < npair) pair_events(xw, q0, l, r0, qw);
+    }
+#else
     if (xin && !ABL(32)) {
         uint2 xp[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) xp[u] = bql[min(xwa + u, (xq0 + xl - 1) >> 5)];
         x_events_pre(bxl, bql, xs, xp, xq0, xl, (int32_t)xrv.x - T0, TL, false, dcnt, ncnt, ccnt);
     }
+#endif
     for (uint32_t i = lane + WGD; i < (ABL(32) ? 0u : nx); i += WGD) {
         const uint2 rv = runl[queue[qcap - 1u - i]];
         x_events(bxl, bql, rv.y >> 15, (rv.y >> 4) & 0x7FFu, (int32_t)rv.x - T0, TL, false, dcnt, ncnt, ccnt);
