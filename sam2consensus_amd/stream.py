@@ -431,13 +431,58 @@ def file_blocks(filename, block=BLOCK):
                     return
                 yield b
         return
-    buf = bytearray(block)
-    with open(filename, "rb", buffering=0) as fh:
+    yield from _read_ahead(filename, block)
+
+
+def _read_ahead(filename, block, nbuf=3):
+    """A plain file's blocks read ahead on a thread (file reads release the GIL) into a ring of
+    ``nbuf`` reused buffers: block k + 1 is read while the caller parses block k.  With a
+    hand-off queue of depth 1 the reader fills at most two buffers ahead, so the buffer it
+    refills is one the caller has moved past (a block is valid until the next one is taken)."""
+    import queue
+    import threading
+    bufs = [bytearray(block) for _ in range(nbuf)]
+    q = queue.Queue(maxsize=1)
+    stop = threading.Event()
+
+    def reader():
+        try:
+            with open(filename, "rb", buffering=0) as fh:
+                k = 0
+                while not stop.is_set():
+                    b = bufs[k % nbuf]
+                    n = fh.readinto(b)
+                    item = ("blk", memoryview(b)[:n]) if n else ("end", None)
+                    while not stop.is_set():
+                        try:
+                            q.put(item, timeout=0.1)
+                            break
+                        except queue.Full:
+                            continue
+                    if not n:
+                        return
+                    k += 1
+        except BaseException as e:  # noqa: BLE001 - re-raised by the caller
+            q.put(("err", e))
+
+    t = threading.Thread(target=reader, daemon=True)
+    t.start()
+    try:
         while True:
-            n = fh.readinto(buf)
-            if not n:
+            kind, v = q.get()
+            if kind == "end":
                 return
-            yield memoryview(buf)[:n]
+            if kind == "err":
+                raise v
+            yield v
+    finally:
+        stop.set()
+        while t.is_alive():   # (unblock a reader waiting to hand over a block)
+            try:
+                q.get_nowait()
+            except queue.Empty:
+                pass
+            t.join(timeout=0.05)
 
 
 class DeviceRunner:

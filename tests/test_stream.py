@@ -216,3 +216,22 @@ def test_unsorted_accumulation_shuffled_config(tmp_path):
     assert len(res.batches) >= 6
     want, _ = o.run_path(path, ["-m", "10"])
     assert _files(res, opt) == want
+
+
+def test_file_blocks_read_ahead(tmp_path):
+    """stream.file_blocks on a plain file: the blocks (views of a reader thread's reused
+    buffers, each consumed before the next is taken) concatenate to the file; an empty file
+    gives none; closing the generator early stops the reader."""
+    data = bytes(np.random.default_rng(5).integers(0, 256, size=300_001, dtype=np.uint8))
+    path = str(tmp_path / "x.sam")
+    with open(path, "wb") as fh:
+        fh.write(data)
+    for block in (7, 4096, 65536, 1 << 20):
+        got = b"".join(bytes(b) for b in stream.file_blocks(path, block))
+        assert got == data
+    empty = str(tmp_path / "e.sam")
+    open(empty, "wb").close()
+    assert list(stream.file_blocks(empty, 4096)) == []
+    g = stream.file_blocks(path, 1024)
+    assert bytes(next(g)) == data[:1024]
+    g.close()
