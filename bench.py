@@ -53,17 +53,16 @@ def b_alg(info, T):
     step    = 0.5·Q + 16·N + 4·K + (48+T)·L + Σ_ins(8 + 0.5·len)  (SURVEY's formula: 4-bit
               query bases, 16 B per read, 4 B per CIGAR op, the count tensor written + read
               once, T vote bytes per position, the insertion events)
-    pileup  = step − 48·L, less 16·N + 4·K when no tile is dense: the tile kernels keep the
-              counts in registers / LDS (never the count tensor); the dense kernel walks its
-              pieces' records and CIGAR ops itself (k_reads then only walks the pieces of
-              non-dense tiles: C5 0.2 %), otherwise k_reads walks every piece
-    reads   = the rest of the step (16·N + 4·K without dense tiles, else ≈ 0)"""
+    pileup  = step − 48·L: the tile kernels keep the counts in registers / LDS (never the
+              count tensor), and both k_tile_dense and k_tile walk their own window's piece
+              records and CIGAR ops (16·N + 4·K are theirs; C3 / C4 / C5 launch no k_reads)
+    reads   = Σ_ins(8 + 0.5·len): k_reads walks only the pieces emitting insertion events
+              (C2) and the long pieces of k_tile's tiles, re-reading records the pileup's
+              figure already holds; priced by the events it hashes, never added to a total"""
     Q, N, K, L = info.query_bases, info.reads_mapped, info.n_tokens, info.total_len
     ins = 8 * info.n_ins + 0.5 * info.n_ins_bases
     step = 0.5 * Q + 16 * N + 4 * K + (48 + T) * L + ins
-    walk = 16 * N + 4 * K
-    pile = step - 48 * L - (0 if info.n_dense > 0 else walk)
-    return step, step - 48 * L - pile, pile
+    return step, ins, step - 48 * L
 
 def cpu_baseline(workload, scale):
     """Time the oracle (pure-Python restatement of the reference, 1 core) on a bounded sample."""

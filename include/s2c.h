@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define S2C_ABI_VERSION 9
+#define S2C_ABI_VERSION 10
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define S2C_OK            0
@@ -98,6 +98,10 @@ int s2c_layout(int64_t *out, int n);
 #define S2C_PF_SIMPLE 0x40   /* one M / = / X token, no prefix words, not long, no '-' in SEQ: its
                                 seqout is SEQ[0:take] (:64-69) and slen holds take = min(l, len(SEQ))
                                 (every consumer's min(l, slen) is then take) */
+#define S2C_PF_XFEW   0x80   /* (with S2C_PF_X) SEQ's non-ACGT chars are at most two 'N' (no '-'), at
+                                SEQ offsets < 0xFFFF listed in px[piece] = off0 | off1 << 16 (0xFFFF:
+                                none): the kernels take them from there instead of scanning the
+                                non-ACGT plane */
 
 /* run record (device-written by k_reads, parallel to ops[]): {gpos, len | kind << 27, qlo, qhi};
    a run (and a read's seqout) is < 2^27 positions: N skips of up to 134 Mb */
@@ -303,6 +307,7 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
     const uint32_t *lops;      /* [n_lops] */
     const uint32_t *lbq;       /* [n_lqwords][2] */
     const uint32_t *lbx;       /* [n_lqwords] */
+    const uint32_t *px;        /* [n_pieces] the non-ACGT SEQ offsets of S2C_PF_XFEW pieces (else 0xFFFFFFFF) */
 } s2c_batch_arrays;
 
 /* Build the batch's layered windows (s2c_batch_arrays lly .. lbx, tile word 20) if not yet
@@ -400,6 +405,7 @@ typedef struct {
     int64_t   out_cap;         /* ≥ T·(F·padded_len + n_cols) */
     int64_t   layers_dense;    /* the batch's info.layers_dense: s2c_pileup_counts and s2c_accumulate
                                   run dense tiles through k_tile and refuse a batch without them */
+    const uint32_t *px;        /* [n_pieces] s2c_batch_arrays.px (ABI 10) */
 } s2c_dev;
 
 /* Sizes (bytes) of every workspace / output buffer for a batch and T thresholds. */

@@ -32,6 +32,7 @@ S2C_CODE_FILL = 0
 S2C_SHORT_MOTIF = 16
 S2C_TILE_DEEP, S2C_TILE_GENERAL, S2C_TILE_DENSE = 1, 2, 4
 S2C_PF_X, S2C_PF_RANGE, S2C_PF_INS, S2C_PF_LONG, S2C_PF_RUNS, S2C_PF_DASH = 1, 2, 4, 8, 16, 32
+S2C_PF_SIMPLE, S2C_PF_XFEW = 64, 128
 S2C_RUN_EMPTY, S2C_RUN_BASES, S2C_RUN_DASH = 0, 1, 2
 S2C_RUN_XBIT, S2C_RUN_DROP, S2C_RUN_LONG = 4, 8, 16
 OPS = "MIDNSHP=X"   # opcode order of the token words (len << 4 | opcode)
@@ -65,7 +66,7 @@ _P32 = C.POINTER(C.c_uint32)
 class BatchArrays(C.Structure):
     _fields_ = [("ref_len", _P64), ("ref_off", _P64), ("ref_cov_reads", _P64)] + \
         [(n, _P32) for n in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "rlist", "lp", "wtile",
-                             "ps", "lly", "lpc", "lops", "lbq", "lbx")]
+                             "ps", "lly", "lpc", "lops", "lbq", "lbx", "px")]
 
 
 class SynthSpec(C.Structure):
@@ -92,7 +93,8 @@ class Dev(C.Structure):
         ("fill_len", C.c_int32), ("fill_nondash", C.c_int32), ("fill", _VP),
         ("runs", _VP), ("ibkt", _VP), ("ilong", _VP), ("ilong_n", _VP), ("counts", _VP),
         ("ins_cols", _VP), ("ins_chr", _VP), ("n_cols", C.c_int64),
-        ("tile_stats", _VP), ("blk_len", _VP), ("out", _VP), ("out_cap", C.c_int64), ("layers_dense", C.c_int64)]
+        ("tile_stats", _VP), ("blk_len", _VP), ("out", _VP), ("out_cap", C.c_int64), ("layers_dense", C.c_int64),
+        ("px", _VP)]
 
 
 class WsSizes(C.Structure):

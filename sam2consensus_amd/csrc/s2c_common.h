@@ -302,28 +302,26 @@ __device__ __forceinline__ void ripple_dec(uint32_t (&C)[8], uint32_t m) {
     }
 }
 
+// One butterfly of the transpose: the bits of a under m << s and of b under m trade places
+// (two shifts and two bit-field inserts, v_bfi_b32).
+template <int S, uint32_t M>
+__device__ __forceinline__ void tswap(uint32_t &a, uint32_t &b) {
+    const uint32_t na = ((b << S) & (M << S)) | (a & ~(M << S));
+    b = ((a >> S) & M) | (b & ~M);
+    a = na;
+}
 // 8 bit-planes of one counter → R[r] byte j = count of position 8j + r (8×8 bit transposes
 // on 4 byte lanes at once).
 __device__ __forceinline__ void transpose8(uint32_t (&R)[8]) {
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const uint32_t t = ((R[r] >> 4) ^ R[r + 4]) & 0x0F0F0F0Fu;
-        R[r + 4] ^= t;
-        R[r] ^= t << 4;
-    }
+    for (int r = 0; r < 4; r++) tswap<4, 0x0F0F0F0Fu>(R[r], R[r + 4]);
 #pragma unroll
     for (int r = 0; r < 8; r++) {
         if (r & 2) continue;
-        const uint32_t t = ((R[r] >> 2) ^ R[r + 2]) & 0x33333333u;
-        R[r + 2] ^= t;
-        R[r] ^= t << 2;
+        tswap<2, 0x33333333u>(R[r], R[r + 2]);
     }
 #pragma unroll
-    for (int r = 0; r < 8; r += 2) {
-        const uint32_t t = ((R[r] >> 1) ^ R[r + 1]) & 0x55555555u;
-        R[r + 1] ^= t;
-        R[r] ^= t << 1;
-    }
+    for (int r = 0; r < 8; r += 2) tswap<1, 0x55555555u>(R[r], R[r + 1]);
 }
 
 // ----------------------------------------------------------------- runs (k_reads output)

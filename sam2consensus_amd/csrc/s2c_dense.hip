@@ -67,7 +67,7 @@ __constant__ __attribute__((aligned(16))) uint8_t c_amb[64] = {
 };
 
 struct DenseArgs {
-    const uint32_t *rs, *pc, *ops, *bq, *bx, *tiles, *items, *lp;
+    const uint32_t *rs, *pc, *ops, *bq, *bx, *tiles, *items, *lp, *px;
     const double *thresholds;
     uint64_t *tile_stats, *blk_len;
     uint8_t *out;
@@ -226,12 +226,13 @@ __device__ __forceinline__ void dma16(uint8_t *dst, const uint32_t *src, uint32_
 // LDS bytes of a dma16 region for n dwords (16-byte phase of the source + rounding)
 __host__ __device__ constexpr uint32_t dma16_bytes(uint32_t n) { return (4 * n + 15 + 15) & ~15u; }
 
-// all-reduce of one register over the G adjacent lanes of a word
+// all-reduce of one register over the G adjacent lanes of a word (bound_ctrl on: the move
+// folds into one v_add_u32_dpp per step; every source lane of these patterns exists)
 template <int G>
 __device__ __forceinline__ uint32_t word_allreduce(uint32_t v) {
-    if constexpr (G >= 2) v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
-    if constexpr (G >= 4) v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
-    if constexpr (G >= 8) v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);   // row_half_mirror
+    if constexpr (G >= 2) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);    // quad_perm [1,0,3,2]
+    if constexpr (G >= 4) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, true);    // quad_perm [2,3,0,1]
+    if constexpr (G >= 8) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, true);   // row_half_mirror
     static_assert(G <= 8, "at most 8 lanes per word");
     return v;
 }
@@ -354,6 +355,26 @@ __device__ __forceinline__ uint32_t pk_sign(uint32_t a) {
 // bit j (j = 0..3) = top bit of byte j
 __device__ __forceinline__ uint32_t byte_bits(uint32_t m) { return ((m & 0x80808080u) * 0x00204081u) >> 28; }
 
+// A run record of the window in LDS (one per op slot, zero for none): x = rs | re << 16, the
+// run's tile-relative positions [rs, re) biased by REC_BIAS (a window starts ≤ 32·kwin ≤ 1024
+// positions before its tile and a short run ends < 2048 positions after its start, so both
+// fit 16 bits), y = q − rs with q the window-relative query base of its first position.  The
+// count takes both ends with one packed subtract and the plane word of a 32-position word W
+// from y + 32·W's biased offset; a zero record covers nothing (re = rs).
+constexpr int32_t REC_BIAS = 2048;
+__device__ __forceinline__ uint2 rec_enc(uint32_t r0, uint32_t len, uint32_t q) {   // r0: tile-relative start
+    const uint32_t rs = r0 + (uint32_t)REC_BIAS;
+    return make_uint2(rs | ((rs + len) << 16), q - rs);
+}
+struct Rec {
+    uint32_t q, l;   // first query base (window-relative), length
+    int32_t r0;      // tile-relative first position
+};
+__device__ __forceinline__ Rec rec_dec(uint2 v) {
+    const uint32_t rs = v.x & 0xFFFFu;
+    return Rec{v.y + rs, (v.x >> 16) - rs, (int32_t)rs - REC_BIAS};
+}
+
 // A tile's window (uniform values from its tile record; S2C_TILE_WORDS layout)
 struct Win {
     uint32_t tile, a, n, cb0, pf0, npc, o0, nslot, qw0, nqw, W0, nwords, lp0, nlong;
@@ -426,8 +447,9 @@ constexpr int PFN = 2;            // piece records per thread loaded with the DM
 template <int NWP>
 __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, const WinLds &L, uint32_t *dcnt,
                                            uint32_t *ncnt, uint32_t *ccnt, const uint8_t *amb, uint32_t fill0,
-                                           const uint4 (&Pp)[PFN], const uint32_t (&oe)[PFN], uint32_t cw0, uint32_t cw1,
-                                           unsigned long long t_entry, uint32_t (*stl)[WPT][4]) {
+                                           const uint4 (&Pp)[PFN], const uint32_t (&oe)[PFN], const uint32_t (&pxr)[PFN],
+                                           uint32_t cw0, uint32_t cw1, unsigned long long t_entry,
+                                           uint32_t (*stl)[WPT][4]) {
     constexpr int NWPW = NWP / WPT, G = WGD / NWPW, RPL = 8 / G;
 #ifdef S2C_PROF
     unsigned long long prof_t = t_entry;
@@ -463,7 +485,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     for (uint32_t it = 0; it < nit; it++) {
         const uint32_t k = tid + WT * it;
         uint4 P = Pp[0];
-        uint32_t oend = oe[0], w0 = opw[0];
+        uint32_t oend = oe[0], w0 = opw[0], pxv = pxr[0];
 #pragma unroll
         for (int u = 1; u < PFN; u++) {   // (the loaded records by a select chain)
             P.x = it == (uint32_t)u ? Pp[u].x : P.x;
@@ -472,44 +494,46 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             P.w = it == (uint32_t)u ? Pp[u].w : P.w;
             oend = it == (uint32_t)u ? oe[u] : oend;
             w0 = it == (uint32_t)u ? opw[u] : w0;
+            pxv = it == (uint32_t)u ? pxr[u] : pxv;
         }
         const bool in = k < npc;
         if (it >= (uint32_t)PFN && in) {   // (windows of more than WT·PFN pieces)
             P = ((const uint4 *)d.pc)[pf0 + k];
             oend = d.pc[4 * (size_t)(pf0 + k + 1) + 2];
             w0 = opl[P.z - o0];
+            pxv = d.px[pf0 + k];
         }
         const uint32_t fl = P.w >> 24, slen = P.w & 0xFFFFFFu, j = P.z - o0;
         const uint32_t op = w0 & 15u, l = w0 >> 4;
         const bool xf = (fl & S2C_PF_X) != 0;
         // (no maxdel count to take: the rule is off, or SEQ holds no '-'; S2C_PF_SIMPLE marks the
         // one-token pieces, whose length field already holds take)
-        const bool plain = in && (fl & ~(uint32_t)(S2C_PF_X | S2C_PF_DASH | S2C_PF_SIMPLE)) == 0u && op_bases(op) &&
+        const bool plain = in && (fl & ~(uint32_t)(S2C_PF_X | S2C_PF_DASH | S2C_PF_SIMPLE | S2C_PF_XFEW)) == 0u && op_bases(op) &&
                            !((fl & S2C_PF_DASH) && mda);
         const uint32_t nops = oend - P.z;
         // one M / = / X token and nothing else: seqout = SEQ[0 : min(l, len(SEQ))] (:64-69)
         const bool fast = plain && nops == 1u;
         const uint32_t take = min(l, slen), q = 16u * (P.y - 2u * qw0);
-        if (fast) runl[j] = make_uint2(P.x, (q << 15) | (take << 4) | S2C_RUN_BASES | (xf ? S2C_RUN_XBIT : 0u));
+        if (fast) runl[j] = rec_enc(P.x - (uint32_t)T0, take, q);
         // bases, D / N / P, bases (the deletion reads): two base runs here (:64-72: k = take,
         // then l1 '-', then SEQ[l : l + min(l2, len(SEQ) − l)]), the '-' run queued for the byte
         // counters unless maxdel drops it (:210: l1 dashes); with N / '-' in SEQ (no maxdel
         // count to take: `plain`) both base runs go to the X-run queue
         bool fdel = false, fdash = false;
-        uint32_t da = 0, db = 0, t2 = 0;   // the '-' run's tile-relative range, clipped to the tile
+        uint32_t da = 0, db = 0, t2 = 0, l1 = 0;   // the '-' run's tile-relative range, clipped to the tile
         if (plain && nops == 3u) {
             const uint32_t w1 = opl[j + 1], w2 = opl[j + 2];
             if (op_dash(w1 & 15u) && op_bases(w2 & 15u)) {
-                const uint32_t l1 = w1 >> 4, xb = xf ? S2C_RUN_XBIT : 0u;
+                l1 = w1 >> 4;
                 t2 = l < slen ? min(w2 >> 4, slen - l) : 0u;
                 const int32_t r0 = (int32_t)(P.x + take) - T0;
                 da = (uint32_t)min(max(r0, 0), TL);
                 db = (uint32_t)min(max(r0 + (int32_t)l1, 0), TL);
                 fdel = true;
                 fdash = db > da && !(mda && l1 > d.maxdel);
-                runl[j] = make_uint2(P.x, (q << 15) | (take << 4) | S2C_RUN_BASES | xb);
+                runl[j] = rec_enc(P.x - (uint32_t)T0, take, q);
                 runl[j + 1] = make_uint2(0u, 0u);
-                runl[j + 2] = make_uint2(P.x + take + l1, ((q + l) << 15) | (t2 << 4) | S2C_RUN_BASES | xb);
+                runl[j + 2] = rec_enc(P.x + take + l1 - (uint32_t)T0, t2, q + l);
             }
         }
         // queue: pieces for the general walk (their index) and the '-' runs of the deletion
@@ -517,15 +541,30 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         // runs' slots from the back.  A lane adds ≤ 3 entries (an X deletion read), so while
         // that could overrun the wave's queue (64 entries kept per walk iteration left) such
         // reads take the general walk instead (≤ 1 entry per lane)
-        bool x1 = (fast || fdel) && xf, x2 = fdel && xf && t2 > 0u;
+        // the 'N' chars of a read whose SEQ holds at most two (S2C_PF_XFEW: their SEQ offsets in
+        // px) straight into the 'N' counters through its runs: SEQ[0 : take) from P.x, the
+        // deletion read's SEQ[l : l + t2) from P.x + take + l1; other reads with non-ACGT chars
+        // queue their runs for the plane scan
+        const bool xfew = (fl & S2C_PF_XFEW) != 0u && (fast || fdel);
+        if (xfew) {
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const uint32_t off = (pxv >> (16 * u)) & 0xFFFFu;
+                int32_t r = -1;
+                if (off < take) r = (int32_t)(P.x + off) - T0;
+                else if (fdel && off >= l && off - l < t2) r = (int32_t)(P.x + take + l1 + (off - l)) - T0;
+                if (off != 0xFFFFu && r >= 0 && r < TL) cnt_add1(ncnt, (uint32_t)r);
+            }
+        }
+        bool x1 = (fast || fdel) && xf && !xfew, x2 = fdel && xf && !xfew && t2 > 0u;
         bool qd = (in && !fast && !fdel) || fdash;
         uint64_t bs = __ballot(qd), bxm = __ballot(x1), bx2 = __ballot(x2);
         if (nslow + nx + (uint32_t)(__popcll(bs) + __popcll(bxm) + __popcll(bx2)) > qcap - WGD * (nitw - 1u - it)) {
-            if (fdel && xf) {
+            if (fdel && xf && !xfew) {
                 fdel = false;
                 fdash = false;
             }
-            x1 = fast && xf;
+            x1 = fast && xf && !xfew;
             x2 = false;
             qd = (in && !fast && !fdel) || fdash;
             bs = __ballot(qd);
@@ -545,43 +584,12 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     // so the round trip overlaps the queued walks and the count (the X pass runs after it)
     const bool xin = lane < nx;
     const uint2 xrv = xin ? runl[queue[qcap - 1u - lane]] : make_uint2(0u, 0u);
-    const uint32_t xq0 = xrv.y >> 15, xl = (xrv.y >> 4) & 0x7FFu, xwa = xq0 >> 5;
-#ifdef S2C_XPAIRS
-    // the (run, plane word) pairs of the first 64 X runs, flattened over the lanes: run r (lane
-    // r) owns pairs [xoff, xoff + xnw); a lane finds its pair's run by binary search over the
-    // runs' offsets (ds_bpermute, all lanes on) and requests its one non-ACGT word now
-    const uint32_t xnw = xin ? ((xq0 + xl - 1u) >> 5) - xwa + 1u : 0u;
-    uint32_t xinc = xnw;
-#pragma unroll
-    for (uint32_t dd = 1; dd < 64; dd <<= 1) {
-        const uint32_t t = (uint32_t)__shfl_up((int)xinc, dd, 64);
-        xinc += lane >= dd ? t : 0u;
-    }
-    const uint32_t xoff = xinc - xnw, nrun = min(nx, 64u);
-    const uint32_t npair = uni((uint32_t)__shfl((int)xinc, 63, 64));
-    // pair p → its run's first query base q0, length l, tile-relative position r0 of q0, word qw
-    auto pair_of = [&](uint32_t p, uint32_t &q0, uint32_t &l, int32_t &r0, uint32_t &qw) {
-        uint32_t r = 0;
-#pragma unroll
-        for (uint32_t st = 32; st; st >>= 1) {
-            const uint32_t c = r + st;
-            const uint32_t oc = (uint32_t)__shfl((int)xoff, (int)min(c, 63u), 64);
-            r = (c < nrun && oc <= p) ? c : r;
-        }
-        q0 = (uint32_t)__shfl((int)xq0, (int)r, 64);
-        l = (uint32_t)__shfl((int)xl, (int)r, 64);
-        r0 = __shfl((int)xrv.x, (int)r, 64) - T0;
-        qw = (q0 >> 5) + (p - (uint32_t)__shfl((int)xoff, (int)r, 64));
-    };
-    uint32_t pq0, pl, pqw;
-    int32_t pr0;
-    pair_of(lane, pq0, pl, pr0, pqw);
-    const uint32_t pxw = lane < npair ? bxl[pqw] : 0u;
-#else
+    const Rec xrc = rec_dec(xrv);
+    const uint32_t xq0 = xrc.q, xl = xrc.l, xwa = xq0 >> 5;
+    const int32_t xr0 = xrc.r0;
     uint32_t xs[8];
 #pragma unroll
     for (int u = 0; u < 8; u++) xs[u] = xin ? bxl[min(xwa + u, (xq0 + xl - 1) >> 5)] : 0u;
-#endif
     // queued pieces: the general walk; '-' runs and SEQ N / '-' straight into the byte counters.
     // A queued piece's record comes from the lane that loaded it (ds_bpermute, all lanes on).
     for (uint32_t base = 0; base < (ABL(16) ? 0u : nslow); base += WGD) {
@@ -614,7 +622,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             walk_window(opl, bql, bxl, P, P.z - o0, oend - o0, 16u * (P.y - 2u * qw0), mda, d.maxdel,
                         [&](uint32_t j, uint32_t gp, uint32_t l, uint32_t kind, uint32_t q) {
                             const uint32_t kd = (lng || kind == S2C_RUN_EMPTY) ? 0u : (kind & 3u);
-                            runl[j] = kd == S2C_RUN_BASES ? make_uint2(gp, (q << 15) | (l << 4) | kind) : make_uint2(0u, 0u);
+                            runl[j] = kd == S2C_RUN_BASES ? rec_enc(gp - (uint32_t)T0, l, q) : make_uint2(0u, 0u);
                             const int32_t r0 = (int32_t)gp - T0;
                             if (kd == S2C_RUN_DASH) cnt_range(dcnt, r0, r0 + (int32_t)l, TL);
                             if (kd == S2C_RUN_BASES && (kind & S2C_RUN_XBIT))
@@ -644,7 +652,9 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     // The planes are aligned to the word's bit 0 (query base b of position 32·W; a record
     // outside the word reads any LDS word, masked off).
     const uint32_t rend = v.nslot;
-    const int32_t W32 = (int32_t)(32 * W);
+    const int16_t wbias = (int16_t)(32 * w + REC_BIAS);     // the word's first position, biased (rec_enc)
+    const v2s wpk = (v2s){wbias, wbias};
+    const uint2 *bqw = bql + ((32 * w + REC_BIAS) >> 5);    // plane word of query y + wbias, less y >> 5
     auto load_runs = [&](uint2 (&rv)[GSD], uint32_t gi) {
         const uint2 *rb = runl + min(cw0 + g + G * GSD * gi, rend);
 #pragma unroll
@@ -661,17 +671,22 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         uint2 pa[GSD], pb[GSD];
 #pragma unroll
         for (int u = h; u < h + CNT_PART; u++) {
-            const int32_t s0 = (int32_t)rv[u].x - W32;
-            const int32_t e0 = s0 + (int32_t)__builtin_amdgcn_ubfe(rv[u].y, 4, 11);
-            const uint32_t l0 = (uint32_t)min(max(s0, 0), 32);   // (v_med3_i32)
-            const uint32_t nb = (uint32_t)min(max(e0, 0), 32) - l0;
-            uint32_t m;
-            asm("v_bfm_b32 %0, %1, %2" : "=v"(m) : "v"(nb), "v"(l0));   // nb bits at l0 (nb < 32)
+            // both ends word-relative at once (packed 16-bit), clamped to [0, 32]
+            const v2s t = __builtin_elementwise_min(
+                __builtin_elementwise_max(__builtin_bit_cast(v2s, rv[u].x) - wpk, (v2s){0, 0}), (v2s){32, 32});
+            const uint32_t tc = __builtin_bit_cast(uint32_t, t);
+            uint32_t nb;   // e - l0 (one SDWA subtract of the halves)
+            asm("v_sub_u32_sdwa %0, %1, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0"
+                : "=v"(nb) : "v"(tc));
+            uint32_t m;   // nb bits at l0 (nb < 32; v_bfm_b32 reads the offset's low 5 bits: l0 of tc, and
+                          // l0 = 32 only with nb = 0)
+            asm("v_bfm_b32 %0, %1, %2" : "=v"(m) : "v"(nb), "v"(tc));
             bm[u] = m;
             fx[u] = (uint32_t)__builtin_amdgcn_sbfe((int32_t)nb, 5, 1);    // all ones iff nb = 32
-            const int32_t b = (int32_t)(rv[u].y >> 15) - s0;
-            sh[u] = (uint32_t)b;
-            const uint2 *pw = bql + (b >> 5);
+            // query base of the word's bit 0 = y + (biased word start): word offset y >> 5 from
+            // the lane's base, bit offset y mod 32 (the funnel shift takes the low 5 bits)
+            sh[u] = rv[u].y;
+            const uint2 *pw = bqw + ((int32_t)rv[u].y >> 5);
             pa[u] = pw[0];
             pb[u] = pw[1];
         }
@@ -785,49 +800,15 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     }
     PROF_MARK(5);
     // queued single-token runs of reads with N / '-' in SEQ (never dropped: maxdel is off)
-#ifdef S2C_XPAIRS
-    // one plane word per lane and round: its bits inside the run, 'N' / '-' by the base plane
-    auto pair_events = [&](uint32_t xw, uint32_t q0, uint32_t l, int32_t r0, uint32_t qw) {
-        const int32_t b0 = (int32_t)(32 * qw) - (int32_t)q0;   // run offset of the word's bit 0
-        uint32_t xm = xw;
-        if (b0 < 0) xm &= 0xFFFFFFFFu << (uint32_t)(-b0);
-        if (b0 + 32 > (int32_t)l) xm &= 0xFFFFFFFFu >> (uint32_t)(b0 + 32 - (int32_t)l);
-        if (!xm) return;
-        const uint2 ps = bql[qw];
-        xm &= ~ps.y;   // (p1 = 0 for every non-ACGT char)
-        while (xm) {
-            const uint32_t bit = (uint32_t)__builtin_ctz(xm);
-            xm &= xm - 1;
-            const int32_t r = r0 + b0 + (int32_t)bit;
-            if (r < 0 || r >= TL) continue;
-            if ((ps.x >> bit) & 1u) {
-                cnt_add1(ccnt, (uint32_t)r);
-                cnt_add1(dcnt, (uint32_t)r);
-            } else {
-                cnt_add1(ncnt, (uint32_t)r);
-            }
-        }
-    };
-    for (uint32_t rb = 0; rb < (ABL(32) ? 0u : npair); rb += WGD) {   // (uniform rounds)
-        uint32_t q0 = pq0, l = pl, qw = pqw, xw = pxw;
-        int32_t r0 = pr0;
-        if (rb) {
-            pair_of(rb + lane, q0, l, r0, qw);
-            xw = rb + lane < npair ? bxl[qw] : 0u;
-        }
-        if (rb + lane < npair) pair_events(xw, q0, l, r0, qw);
-    }
-#else
     if (xin && !ABL(32)) {
         uint2 xp[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) xp[u] = bql[min(xwa + u, (xq0 + xl - 1) >> 5)];
-        x_events_pre(bxl, bql, xs, xp, xq0, xl, (int32_t)xrv.x - T0, TL, false, dcnt, ncnt, ccnt);
+        x_events_pre(bxl, bql, xs, xp, xq0, xl, xr0, TL, false, dcnt, ncnt, ccnt);
     }
-#endif
     for (uint32_t i = lane + WGD; i < (ABL(32) ? 0u : nx); i += WGD) {
-        const uint2 rv = runl[queue[qcap - 1u - i]];
-        x_events(bxl, bql, rv.y >> 15, (rv.y >> 4) & 0x7FFu, (int32_t)rv.x - T0, TL, false, dcnt, ncnt, ccnt);
+        const Rec rc = rec_dec(runl[queue[qcap - 1u - i]]);
+        x_events(bxl, bql, rc.q, rc.l, rc.r0, TL, false, dcnt, ncnt, ccnt);
     }
     lds_sync();   // the byte counters are final
     PROF_MARK(4);
@@ -1092,15 +1073,17 @@ __global__ __launch_bounds__(WT) S2C_DENSE_OCC void k_tile_dense(const DenseArgs
     // with the DMA: the thread's piece records and its word's run-slot range
     constexpr int G = WGD / (NWP / WPT);
     uint4 Pp[PFN];
-    uint32_t oe[PFN];
+    uint32_t oe[PFN], pxr[PFN];
 #pragma unroll
     for (int i = 0; i < PFN; i++) {
         const uint32_t k = tid + WT * i;
         Pp[i] = make_uint4(0u, 0u, 0u, 0u);
         oe[i] = 0;
+        pxr[i] = 0xFFFFFFFFu;
         if (k < v.npc) {
             Pp[i] = ((const uint4 *)d.pc)[v.pf0 + k];
             oe[i] = d.pc[4 * (size_t)(v.pf0 + k + 1) + 2];
+            pxr[i] = d.px[v.pf0 + k];
         }
     }
     const uint32_t w = (tid >> 6) * (NWP / WPT) + (tid & 63) / G, W = v.W0 + w, K = d.kwin;
@@ -1130,7 +1113,7 @@ __global__ __launch_bounds__(WT) S2C_DENSE_OCC void k_tile_dense(const DenseArgs
     cw0 -= v.o0;
     cw1 -= v.o0;
     lds_sync();
-    dense_tile<NWP>(d, v, wl, dcnt, ncnt, ccnt, amb, fill0, Pp, oe, cw0, cw1, t_entry, stl);
+    dense_tile<NWP>(d, v, wl, dcnt, ncnt, ccnt, amb, fill0, Pp, oe, pxr, cw0, cw1, t_entry, stl);
 }
 
 template <int NWP>
@@ -1163,7 +1146,7 @@ int s2c_launch_dense(const s2c_dev *dv, hipStream_t st) {
     if (dv->fill_len != 1) return s2c_set_error(S2C_ERR_ARG, "dense tiles need a one-char fill");
     if (dv->n_dense >= ((int64_t)1 << 31)) return s2c_set_error(S2C_ERR_LIMIT, "too many dense tiles");
     DenseArgs a;
-    a.rs = dv->rs; a.lp = dv->lp; a.pc = dv->pc; a.ops = dv->ops; a.bq = dv->bq; a.bx = dv->bx; a.tiles = dv->tiles; a.items = dv->dense;
+    a.rs = dv->rs; a.lp = dv->lp; a.pc = dv->pc; a.px = dv->px; a.ops = dv->ops; a.bq = dv->bq; a.bx = dv->bx; a.tiles = dv->tiles; a.items = dv->dense;
     a.thresholds = dv->thresholds; a.tile_stats = dv->tile_stats; a.blk_len = dv->blk_len; a.out = dv->out;
     a.padded_len = (uint32_t)dv->padded_len; a.n_cols = (uint32_t)dv->n_cols; a.n_tiles = (uint32_t)dv->n_tiles;
     a.kwin = (uint32_t)dv->kwin; a.fill_nondash = (uint32_t)dv->fill_nondash;

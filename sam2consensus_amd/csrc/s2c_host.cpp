@@ -281,6 +281,7 @@ struct s2c_batch {
     std::vector<uint32_t> lly, lpc, lops, lbq, lbx;   // layered windows of the non-dense tiles
     bool layers = false;                               // built (s2c_batch_layers)
     u32buf kmin, kmax;   // host only: global key range of each piece's insertion events
+    u32buf px;           // [pieces] the non-ACGT SEQ offsets of S2C_PF_XFEW pieces (s2c.h)
 };
 
 static int perr(s2c_parser *p, int code, const std::string &msg) {
@@ -1842,6 +1843,28 @@ struct PhaseClock {
     }
 };
 
+// px of a piece of read r (s2c.h S2C_PF_XFEW): the SEQ offsets of its first two non-ACGT
+// chars when they are all 'N' (no '-': the maxdel rule never needs the plane scan), at most
+// two and below 0xFFFF; sets S2C_PF_XFEW in fl.  0xFFFFFFFF otherwise.
+static uint32_t xfew_offsets(const Chunk &c, const ReadRec &r, uint32_t &fl) {
+    if (!(r.has_x & 1) || (r.has_x & 2)) return 0xFFFFFFFFu;
+    const uint16_t *sx = (const uint16_t *)c.bx.data();
+    uint32_t off[2] = {0xFFFFu, 0xFFFFu}, nf = 0;
+    for (uint64_t h = 0; h < ((uint64_t)r.slen + 15) / 16; h++) {
+        uint32_t m = sx[r.q / 16 + h];
+        while (m) {
+            const uint64_t o = 16 * h + (uint64_t)__builtin_ctz(m);
+            m &= m - 1;
+            if (o >= r.slen) break;
+            if (nf == 2 || o >= 0xFFFFu) return 0xFFFFFFFFu;
+            off[nf++] = (uint32_t)o;
+        }
+    }
+    if (nf == 0) return 0xFFFFFFFFu;
+    fl |= S2C_PF_XFEW;
+    return off[0] | off[1] << 16;
+}
+
 static int build_batch(s2c_parser *p, s2c_batch **out) {
     PhaseClock clk;
     const int64_t R = (int64_t)p->ref_names.size();
@@ -2088,6 +2111,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     b->pc.resize(4 * (size_t)(NP + 1));
     b->kmin.resize(NP);
     b->kmax.resize(NP);
+    b->px.resize(std::max<int64_t>(NP, 1));
     b->ops.resize(std::max<uint64_t>(NOPS, 1));
     b->bq.resize(2 * (size_t)I.n_qwords);
     b->bx.resize((size_t)I.n_qwords);
@@ -2128,6 +2152,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
                 }
                 if (q.lng) fl |= S2C_PF_LONG;
                 memcpy(o, &c.toks[r.tok], 4 * (size_t)r.ntok);
+                b->px[k] = xfew_offsets(c, r, fl);
                 uint32_t slen = r.slen;
                 if (!q.range && !q.ins && !q.lng && r.ntok == 1 && op_bases(c.toks[r.tok] & 15u) && !(fl & S2C_PF_DASH)) {
                     fl |= S2C_PF_SIMPLE;   // seqout = SEQ[0:take]: the field holds take (s2c.h)
@@ -2494,6 +2519,7 @@ static int s2c_batch_shard_impl(const s2c_batch *b, int64_t t0, int64_t t1, s2c_
     s->bx.assign((size_t)J.n_qwords, 0u);
     s->kmin.assign(NS, 0xFFFFFFFFu);
     s->kmax.assign(NS, 0u);
+    s->px.assign(std::max<int64_t>(NS, 1), 0xFFFFFFFFu);
     std::unordered_map<uint32_t, uint32_t> slot_new, piece_new;   // old op slot / long piece → new
     {
         const uint16_t *sq = (const uint16_t *)b->bq.data(), *sx = (const uint16_t *)b->bx.data();
@@ -2513,6 +2539,7 @@ static int s2c_batch_shard_impl(const s2c_batch *b, int64_t t0, int64_t t1, s2c_
             }
             s->kmin[i] = b->kmin[k];
             s->kmax[i] = b->kmax[k];
+            s->px[i] = b->px[k];
             const uint32_t slen = b->pc[4 * k + 3] & 0xFFFFFFu;
             for (uint64_t h = 0; h < (slen + 15) / 16; h++) {
                 const uint64_t a = (uint64_t)b->pc[4 * k + 1] + h, d = qoff[i] / 16 + h;
@@ -2643,6 +2670,7 @@ extern "C" int s2c_batch_arrays_get(const s2c_batch *b, s2c_batch_arrays *o) {
     o->lp = b->lp.data();
     o->wtile = b->wtile.data();
     o->rlist = b->rlist.data();
+    o->px = b->px.data();
     o->ps = b->ps.data();
     o->lly = b->lly.data();
     o->lpc = b->lpc.data();

@@ -1597,7 +1597,7 @@ static int check_dev(const s2c_dev *d) {
         return s2c_set_error(S2C_ERR_LIMIT, "run records, pieces or base planes beyond 3.5 GB (split the input)");   // 32-bit buffer offsets
     if (d->n_layers > 0 && (!d->lly || !d->lpc || !d->lops || !d->lbq || !d->lbx))
         return s2c_set_error(S2C_ERR_ARG, "missing layered windows");
-    if (d->n_pieces > 0 && (!d->pc || !d->ops || !d->bq || !d->bx || !d->runs))
+    if (d->n_pieces > 0 && (!d->pc || !d->ops || !d->bq || !d->bx || !d->runs || !d->px))
         return s2c_set_error(S2C_ERR_ARG, "missing piece buffers");
     if (d->n_tiles > 0 && (!d->tiles || !d->rs || !d->wtile || !d->tile_stats || !d->blk_len || !d->out))
         return s2c_set_error(S2C_ERR_ARG, "missing tile / output buffers");

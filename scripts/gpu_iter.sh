@@ -16,3 +16,12 @@ if [ -n "$PROF" ]; then
   bash scripts/pmc_ablate_dense.sh > /dev/null 2>&1 || { echo "pmc failed"; exit 1; }
   echo PMC_OK
 fi
+if [ -n "$PMC" ]; then   # VALU / LDS instructions and LDS conflicts of the workload's tile kernels
+  cd /tmp
+  timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
+      SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/pmc_it_${WL:-c5} -o run \
+      -- python3 $GRAFT_REPO_ROOT/bench.py --workload ${WL:-c5} --steps 3 --warmup 1 --no-cpu-baseline --no-parity --no-file-parse \
+      > $GRAFT_REPO_ROOT/gpurun_out/pmc_it.log 2>&1 || { echo "pmc failed"; tail -5 $GRAFT_REPO_ROOT/gpurun_out/pmc_it.log; exit 1; }
+  cd $GRAFT_REPO_ROOT
+  python3 scripts/pmc_summary.py gpurun_out/pmc_it_${WL:-c5} k_tile | grep -E "VALU|LDS|WAVES|duration"
+fi

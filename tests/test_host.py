@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
     assert declared <= exported, declared - exported
     assert declared == set(_lib.EXPORTS)
-    assert _lib.lib.s2c_abi_version() == 9
+    assert _lib.lib.s2c_abi_version() == 10
 
 
 def _model_case(sam, args):
