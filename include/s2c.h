@@ -182,6 +182,13 @@ int  s2c_parser_feed(s2c_parser *p, const char *buf, size_t len);
 int  s2c_parser_end_header(s2c_parser *p);
 /* Parse a whole file; ".gz" suffix → zlib (:111-114).  Read in bounded windows. */
 int  s2c_parser_feed_file(s2c_parser *p, const char *path);
+/* The same byte source as a stream, for callers that feed blocks (streamed batches): plain,
+ * gzip, or BGZF inflated block-parallel on the host threads (:111-114).  read fills dst up to
+ * cap bytes (fewer only at the end; *n = 0 once the stream is over). */
+typedef struct s2c_reader s2c_reader;
+int  s2c_reader_open(const char *path, s2c_reader **out);
+int  s2c_reader_read(s2c_reader *r, void *dst, size_t cap, size_t *n);
+void s2c_reader_free(s2c_reader *r);
 /* End of input: reformat-phase checks (:284-294), global layout, bucketing, tile plan. */
 int  s2c_parser_finish(s2c_parser *p, s2c_batch **out);
 void s2c_parser_free(s2c_parser *p);
@@ -274,6 +281,8 @@ typedef struct {
     int64_t n_lops;            /* op words of the layered arrays (lops) */
     int64_t n_lqwords;         /* plane words of the layered arrays (lbq, lbx) */
     int64_t layers_dense;      /* 1: the dense tiles' layered windows are built too (counts-only modes) */
+    int64_t layers_built;      /* 1: the layered windows (lly ..., tile word 20) are built (s2c_batch_layers*);
+                                  0 for a fresh snapshot or shard */
 } s2c_batch_info;
 
 typedef struct {               /* host pointers into the batch (valid until s2c_batch_free) */
@@ -406,6 +415,7 @@ typedef struct {
     int64_t   layers_dense;    /* the batch's info.layers_dense: s2c_pileup_counts and s2c_accumulate
                                   run dense tiles through k_tile and refuse a batch without them */
     const uint32_t *px;        /* [n_pieces] s2c_batch_arrays.px (ABI 10) */
+    int64_t   layers_built;    /* the batch's info.layers_built: every launch with work items refuses 0 */
 } s2c_dev;
 
 /* Sizes (bytes) of every workspace / output buffer for a batch and T thresholds. */

@@ -17,7 +17,6 @@ namespace s2c {
 constexpr int WG = 256;
 constexpr uint32_t NSYM = S2C_NSYM;
 constexpr int VT_TMAX = 4;        // thresholds per epilogue pass (one vote-char word per column)
-constexpr int THR_MAX = 256;      // -c values supported
 constexpr int FILL_LDS = 64;      // -f bytes staged in LDS (longer fills read HBM)
 constexpr uint32_t FLUSH_RECS = 248;   // records per lane between counter flushes (8-bit counters)
 

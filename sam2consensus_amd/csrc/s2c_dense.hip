@@ -443,7 +443,10 @@ __device__ __forceinline__ void win_issue(const DenseArgs &d, const Win &v, uint
 #endif
 constexpr int WPT = S2C_DENSE_WPT;   // waves per tile (they share the window)
 constexpr int WT = WGD * WPT;     // threads per tile
-constexpr int PFN = 2;            // piece records per thread loaded with the DMA (windows of ≤ 256 pieces)
+#ifndef S2C_DENSE_PFN
+#define S2C_DENSE_PFN 2
+#endif
+constexpr int PFN = S2C_DENSE_PFN;   // piece records per thread loaded with the DMA (windows of ≤ PFN·WT pieces)
 template <int NWP>
 __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, const WinLds &L, uint32_t *dcnt,
                                            uint32_t *ncnt, uint32_t *ccnt, const uint8_t *amb, uint32_t fill0,
@@ -656,9 +659,14 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     const v2s wpk = (v2s){wbias, wbias};
     const uint2 *bqw = bql + ((32 * w + REC_BIAS) >> 5);    // plane word of query y + wbias, less y >> 5
     auto load_runs = [&](uint2 (&rv)[GSD], uint32_t gi) {
-        const uint2 *rb = runl + min(cw0 + g + G * GSD * gi, rend);
+        // (64-bit loads: two records per ds_read2_b64)
+        const unsigned long long *rb = (const unsigned long long *)(runl + min(cw0 + g + G * GSD * gi, rend));
 #pragma unroll
-        for (int u = 0; u < GSD; u++) rv[u] = rb[G * u];
+        for (int u = 0; u < GSD; u++) {
+            unsigned long long r = rb[G * u];
+            asm("" : "+v"(r));   // (kept one 64-bit load: its halves are used as different types)
+            rv[u] = make_uint2((uint32_t)r, (uint32_t)(r >> 32));
+        }
     };
     // one group's 8 records → Harley–Seal tree of each plane; returns the weight-8 carries
     // NR = 8: returns the weight-8 carries in t8o; NR = 4 (a tail group): the weight-4 carries

@@ -934,11 +934,9 @@ struct Reader {   // plain, gzip or BGZF (:111-114) byte source
 };
 }  // namespace
 
-static int s2c_parser_feed_file_impl(s2c_parser *p, const char *path) {
-    if (!p || !path) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
-    if (p->err) return s2c_set_error(p->err, p->errmsg);
+// Open path as the reference reads it (:111-114): ".gz" → gzip (BGZF block-parallel), else plain.
+static int reader_open(Reader &rd, const char *path) {
     const size_t n = strlen(path);
-    Reader rd;
     if (n >= 3 && strcmp(path + n - 3, ".gz") == 0) {   // :111
         unsigned char h[18];
         size_t bs = 0, hn = 0;
@@ -961,6 +959,14 @@ static int s2c_parser_feed_file_impl(s2c_parser *p, const char *path) {
         rd.f = fopen(path, "rb");
         if (!rd.f) return s2c_set_error(S2C_ERR_IO, std::string("cannot open ") + path);
     }
+    return S2C_OK;
+}
+
+static int s2c_parser_feed_file_impl(s2c_parser *p, const char *path) {
+    if (!p || !path) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
+    if (p->err) return s2c_set_error(p->err, p->errmsg);
+    Reader rd;
+    if (const int rc = reader_open(rd, path)) return rc;
     // A reader thread inflates / reads window k + 1 while the workers parse window k (two
     // buffers).  The reader cuts each window after its last '\n' and carries the partial
     // line into the next one.
@@ -1042,6 +1048,36 @@ static int s2c_parser_feed_file_impl(s2c_parser *p, const char *path) {
 extern "C" int s2c_parser_feed_file(s2c_parser *p, const char *path) {
     return s2c_guarded([&] { return s2c_parser_feed_file_impl(p, path); });
 }
+
+// The byte source of s2c_parser_feed_file as a stream (streamed batches, stream.py): the
+// same plain / gzip / block-parallel BGZF reader, read in caller-sized pieces.
+struct s2c_reader {
+    Reader rd;
+};
+extern "C" int s2c_reader_open(const char *path, s2c_reader **out) {
+    return s2c_guarded([&] {
+        if (!path || !out) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
+        std::unique_ptr<s2c_reader> r(new s2c_reader());
+        if (const int rc = reader_open(r->rd, path)) return rc;
+        *out = r.release();
+        return S2C_OK;
+    });
+}
+extern "C" int s2c_reader_read(s2c_reader *r, void *dst, size_t cap, size_t *n) {
+    return s2c_guarded([&] {
+        if (!r || !n || (cap && !dst)) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
+        size_t tot = 0;
+        while (tot < cap) {   // (a full buffer unless the stream ends)
+            const long k = r->rd.read((char *)dst + tot, cap - tot);
+            if (k < 0) return s2c_set_error(S2C_ERR_IO, "gzip read error");
+            if (k == 0) break;
+            tot += (size_t)k;
+        }
+        *n = tot;
+        return S2C_OK;
+    });
+}
+extern "C" void s2c_reader_free(s2c_reader *r) { delete r; }
 
 // ------------------------------------------------------------------ finish: layout + plan
 namespace {
@@ -2619,8 +2655,11 @@ static int s2c_batch_shard_impl(const s2c_batch *b, int64_t t0, int64_t t1, s2c_
         if (!dense_fits(tw, K)) return s2c_set_error(S2C_ERR_LIMIT, "shard window beyond the dense kernel's LDS");
         J.dense_lds = std::max<int64_t>(J.dense_lds, dense_bytes(tw, K));
     }
-    // (the shard's own layered windows are built on first use: s2c_batch_layers)
+    // (the shard's own layered windows are built on first use: s2c_batch_layers; until then
+    // no tile word 20 names a layer of the parent's and launches with work items refuse it)
     J.n_layers = J.n_lpieces = J.n_lops = J.n_lqwords = 0;
+    J.layers_dense = J.layers_built = 0;
+    for (int64_t t = 0; t < NT; t++) s->tiles[(size_t)t * S2C_TILE_WORDS + 20] = S2C_LY_NONE;
     mark_runs(s.get());
     // the shard's share of the workload's aligned bases (by its positions; for reporting)
     J.aligned_bases = I.total_len ? (int64_t)((double)I.aligned_bases * (double)aligned / (double)I.total_len) : 0;
@@ -2638,6 +2677,7 @@ static int s2c_batch_layers_impl(s2c_batch *b, bool with_dense) {
     while (nwp * 32 < b->info.tile_max) nwp *= 2;
     build_layers(b, 64 / nwp, with_dense);
     b->layers = true;
+    b->info.layers_built = 1;
     return S2C_OK;
 }
 extern "C" int s2c_batch_layers(s2c_batch *b) {

@@ -1349,7 +1349,6 @@ struct ConsLds {
     uint4 key[KMAX];
     uint32_t klen[KMAX];               // layout build; then per key its coverage if called, else 0
     uint16_t kem[VT_TMAX][KMAX];       // chars emitted per key (this pass)
-    double thr[THR_MAX];
     unsigned long long acc[VT_ACC];
     uint64_t wsum[VT_TMAX][WG / 64];
     uint32_t scan[12];
@@ -1368,7 +1367,6 @@ __global__ __launch_bounds__(WG) void k_consensus(const TileArgs d, const uint32
     if (tid < 64) L.amb[tid] = c_amb[tid];
     for (uint32_t i = tid; i < KMAX; i += WG) L.klen[i] = 0;
     if (tid < TILE_WORDS) L.bits[tid] = 0;
-    for (uint32_t i = tid; i < (uint32_t)d.n_thr; i += WG) L.thr[i] = d.thresholds[i];
     if (tid < (uint32_t)min(d.fill_len, FILL_LDS)) L.fill[tid] = d.fill[tid];
     __syncthreads();
     uint32_t *cols = d.ins_cols + (size_t)T.cb0 * NSYM;
@@ -1404,7 +1402,7 @@ __global__ __launch_bounds__(WG) void k_consensus(const TileArgs d, const uint32
                     uint32_t v[NSYM];
 #pragma unroll
                     for (uint32_t j = 0; j < NSYM; j++) v[j] = cols[(size_t)(kr.y + c) * NSYM + j];
-                    const uint8_t ic = L.amb[column_masks(v, cov, &L.thr[t], 1) & 63u];
+                    const uint8_t ic = L.amb[column_masks(v, cov, d.thresholds + t, 1) & 63u];
                     em += (ic != '-' && ic != 0xFF) ? 1u : 0u;
                     ne += ic == 0xFF ? 1u : 0u;
                     chr[(size_t)t * d.n_cols + T.cb0 + kr.y + c] = ic;
@@ -1449,7 +1447,7 @@ __global__ __launch_bounds__(WG) void k_consensus(const TileArgs d, const uint32
             for (int u = 0; u < VT_TMAX; u++) {
                 my[u] = 0;
                 if (u >= tn) continue;
-                const double th = L.thr[t0 + u];
+                const double th = d.thresholds[t0 + u];
                 uint32_t nd = 0, ne = 0;
 #pragma unroll
                 for (int v = 0; v < 2; v++) {
@@ -1587,7 +1585,6 @@ extern "C" int s2c_workspace_sizes(const s2c_batch_info *info, int32_t n_thr, s2
 static int check_dev(const s2c_dev *d) {
     if (!d) return s2c_set_error(S2C_ERR_ARG, "s2c_dev is NULL");
     if (d->n_thr <= 0) return s2c_set_error(S2C_ERR_ARG, "no thresholds");
-    if (d->n_thr > THR_MAX) return s2c_set_error(S2C_ERR_LIMIT, "more than 256 thresholds (-c values)");
     if (d->tile_max <= 0 || d->tile_max > S2C_TILE_MAX) return s2c_set_error(S2C_ERR_ARG, "tile_max out of range");
     if (d->padded_len <= 0 || d->padded_len >= ((int64_t)1 << 32)) return s2c_set_error(S2C_ERR_ARG, "bad padded_len");
     if (d->n_tiles >= ((int64_t)1 << 31) || (int64_t)d->n_thr * d->n_tiles >= ((int64_t)1 << 40))
@@ -1597,6 +1594,10 @@ static int check_dev(const s2c_dev *d) {
         return s2c_set_error(S2C_ERR_LIMIT, "run records, pieces or base planes beyond 3.5 GB (split the input)");   // 32-bit buffer offsets
     if (d->n_layers > 0 && (!d->lly || !d->lpc || !d->lops || !d->lbq || !d->lbx))
         return s2c_set_error(S2C_ERR_ARG, "missing layered windows");
+    // k_tile reads every work item's tile through its layered windows (tile word 20): a batch
+    // whose layers were never built (e.g. a fresh s2c_batch_shard) holds no valid ones
+    if (d->n_items > 0 && !d->layers_built)
+        return s2c_set_error(S2C_ERR_ARG, "the batch's layered windows are not built (s2c_batch_layers before upload)");
     if (d->n_pieces > 0 && (!d->pc || !d->ops || !d->bq || !d->bx || !d->runs || !d->px))
         return s2c_set_error(S2C_ERR_ARG, "missing piece buffers");
     if (d->n_tiles > 0 && (!d->tiles || !d->rs || !d->wtile || !d->tile_stats || !d->blk_len || !d->out))
@@ -1630,6 +1631,11 @@ extern "C" int s2c_reads(const s2c_dev *d, void *stream) {
 extern "C" int s2c_pileup(const s2c_dev *d, void *stream) {
     int rc = check_dev(d);
     if (rc) return rc;
+    // dense tiles emit exactly one char per position: len(fill) must be 1, else k_tile (which
+    // reads their layered windows) — refused before anything is launched
+    if (d->n_dense > 0 && d->fill_len != 1 && !d->layers_dense)
+        return s2c_set_error(S2C_ERR_ARG, "a fill of length != 1 runs the dense tiles through k_tile: their layered "
+                                          "windows are needed (s2c_batch_layers_mode(b, 1))");
     hipStream_t s = (hipStream_t)stream;
     const TileArgs a = tile_args(*d);
     if (d->n_deep > 0) {
@@ -1637,11 +1643,6 @@ extern "C" int s2c_pileup(const s2c_dev *d, void *stream) {
         if ((rc = hip_check(hipGetLastError(), "k_prep"))) return rc;
     }
     if (d->n_dense > 0) {
-        // dense tiles emit exactly one char per position: len(fill) must be 1, else k_tile
-        // (which reads their layered windows)
-        if (d->fill_len != 1 && !d->layers_dense)
-            return s2c_set_error(S2C_ERR_ARG, "a fill of length != 1 runs the dense tiles through k_tile: their layered "
-                                              "windows are needed (s2c_batch_layers_mode(b, 1))");
         rc = d->fill_len == 1 ? s2c_launch_dense(d, s) : launch_tiles(a, d->tile_max, d->dense, d->n_dense, s);
         if (rc) return rc;
     }

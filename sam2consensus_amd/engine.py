@@ -242,7 +242,7 @@ class Workspace:
         d.dense_lds = i.dense_lds
         d.n_rlist = i.n_rlist
         d.n_layers, d.n_lpieces, d.n_lops, d.n_lqwords = i.n_layers, i.n_lpieces, i.n_lops, i.n_lqwords
-        d.layers_dense = i.layers_dense
+        d.layers_dense, d.layers_built = i.layers_dense, i.layers_built
         # the maxdel rule (:210) runs on the device: the parser's setting unless overridden
         if maxdel_active is None:
             maxdel_active = getattr(db.hb, "maxdel_active", True)

@@ -35,7 +35,6 @@ reference's is by its count tables (:206-221).
 from __future__ import annotations
 
 import ctypes as C
-import gzip
 import os
 import time
 
@@ -420,22 +419,45 @@ def _merge(parts, T):
 
 
 def file_blocks(filename, block=BLOCK):
-    """The file's bytes in blocks (".gz" → gzip, :111-114).  A plain file is read into one
-    reused buffer (each block is a view of it, valid until the next is read: the parser
-    copies what it keeps), so no block pays for fresh pages."""
+    """The file's bytes in blocks, read ahead on a thread into reused buffers (each block is a
+    view, valid until the next is taken: the parser copies what it keeps).  A plain file by
+    reads; a ".gz" (:111-114) through libs2c.so's reader — the one s2c_parser_feed_file uses:
+    BGZF (bgzip / samtools) inflated block-parallel on the host threads, other gzip
+    sequentially."""
     if filename.endswith(".gz"):
-        with gzip.open(filename, "rb") as fh:
-            while True:
-                b = fh.read(block)
-                if not b:
-                    return
-                yield b
+        yield from _read_ahead(filename, block, _native_source)
         return
     yield from _read_ahead(filename, block)
 
 
-def _read_ahead(filename, block, nbuf=3):
-    """A plain file's blocks read ahead on a thread (file reads release the GIL) into a ring of
+class _native_source:
+    """libs2c.so's byte source (s2c_reader_*) with a file's readinto interface."""
+
+    def __init__(self, filename):
+        self._r = C.c_void_p()
+        L.check(L.lib.s2c_reader_open(os.fsencode(filename), C.byref(self._r)))
+
+    def readinto(self, b):
+        n = C.c_size_t()
+        mv = memoryview(b).cast("B")
+        L.check(L.lib.s2c_reader_read(self._r, (C.c_char * mv.nbytes).from_buffer(mv), mv.nbytes, C.byref(n)))
+        return n.value
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        if self._r:
+            L.lib.s2c_reader_free(self._r)
+            self._r = C.c_void_p()
+
+
+def _plain_source(filename):
+    return open(filename, "rb", buffering=0)
+
+
+def _read_ahead(filename, block, source=_plain_source, nbuf=3):
+    """A file's blocks read ahead on a thread (reads and inflates release the GIL) into a ring of
     ``nbuf`` reused buffers: block k + 1 is read while the caller parses block k.  With a
     hand-off queue of depth 1 the reader fills at most two buffers ahead, so the buffer it
     refills is one the caller has moved past (a block is valid until the next one is taken)."""
@@ -447,7 +469,7 @@ def _read_ahead(filename, block, nbuf=3):
 
     def reader():
         try:
-            with open(filename, "rb", buffering=0) as fh:
+            with source(filename) as fh:
                 k = 0
                 while not stop.is_set():
                     b = bufs[k % nbuf]

@@ -11,4 +11,4 @@ for k in 1 2; do
     python -c "import json;d=json.load(open('gpurun_out/${T}_${lib}_$k.json'));print('$lib', $k, round(d['ms_per_step'],4), round(d['kernels_ms']['step_gpu'],4), round(d['roofline']['frac'],3), d['parity'])"
   done
 done
-echo R03_AB_DONE
+echo AB_DONE

@@ -431,3 +431,16 @@ def test_long_skip_on_device_matches_reference(idx):
     assert status == c["status"]
     got = {k: hashlib.sha256(v.encode("latin-1")).hexdigest() for k, v in files.items()}
     assert got == {k: v["sha256"] for k, v in c["files"].items()}
+
+
+@pytest.mark.parametrize("idx", [0, 1])
+def test_many_thresholds_on_device_match_reference(idx):
+    """300 thresholds (more than round 3's 256-threshold limit): dense tiles loop the vote over
+    them, k_tile's epilogue passes of 4, k_consensus reads them from HBM; the FASTA equals the
+    reference's files (tests/golden/limits.json)."""
+    from sam2consensus_amd.cli import run_text
+    c = golden_io.load("limits")[idx]
+    status, files = run_text(c["sam"], c["args"])
+    assert status == c["status"]
+    got = {k: hashlib.sha256(v.encode("latin-1")).hexdigest() for k, v in files.items()}
+    assert got == {k: v["sha256"] for k, v in c["files"].items()}

@@ -393,3 +393,100 @@ def test_layers_without_dense_tiles():
     assert hb.info.layers_dense == 1 and hb.info.n_lpieces == full.info.n_lpieces
     assert (hb.tiles[:, 20] == full.tiles[:, 20]).all()
     batch_model.check_layers(hb)
+
+
+def test_xfew_lists_the_n_offsets():
+    """S2C_PF_XFEW + px (ABI 10): a read whose SEQ holds one or two 'N' (and no '-') lists their
+    SEQ offsets, so the dense kernel adds its 'N' counts through the runs without scanning the
+    non-ACGT plane; three non-ACGT chars, or any '-', leave the flag off (the plane scan)."""
+    from sam2consensus_amd import _lib as L
+    seqs = ["ACGTACGTAC", "ACGNACGTAC", "NCGTACGTAN", "NCGNACGTAN", "AC-TACGTAC", "NC-TACGTAC"]
+    long_n = "A" * 70 + "N" + "C" * 59   # an 'N' past the first 64 bases
+    sam = "@SQ\tSN:g\tLN:400\n" + "".join(
+        "r%d\t0\tg\t%d\t60\t%dM\t*\t0\t0\t%s\t*\n" % (i, 1 + i, len(s), s) for i, s in enumerate(seqs + [long_n]))
+    hb = batch.parse_text(sam, True, 150)
+    try:
+        fl = (hb.pc[:-1, 3] >> 24).astype(np.int64)
+        order = np.argsort(hb.pc[:-1, 0], kind="stable")   # pieces by start position = read order here
+        want = {0: None, 1: (3,), 2: (0, 9), 3: None, 4: None, 5: None, 6: (70,)}
+        for r, k in enumerate(order):
+            if want[r] is None:
+                assert not fl[k] & L.S2C_PF_XFEW, (r, fl[k])
+                continue
+            assert fl[k] & L.S2C_PF_XFEW and fl[k] & L.S2C_PF_X
+            px = int(hb.px[k])
+            offs = tuple(o for o in (px & 0xFFFF, px >> 16) if o != 0xFFFF)
+            assert offs == want[r], (r, hex(px))
+    finally:
+        hb.free()
+
+
+def _host_dev(hb, fill=b"-", counts=False):
+    """An s2c_dev over host pointers (never dereferenced: the calls below must return before
+    any launch) with the batch's shapes, as a caller of the C-ABI would fill it."""
+    import ctypes as C
+    L = _lib
+    i = hb.info
+    scratch = (C.c_uint8 * 4096)()
+    p = C.addressof(scratch)
+    d = L.Dev()
+    for name in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile", "rlist", "ps", "px"):
+        setattr(d, name, p)
+    d.n_pieces, d.n_ops, d.n_qwords, d.n_tiles = i.n_pieces, i.n_ops, i.n_qwords, i.n_tiles
+    d.n_items, d.n_dense, d.n_deep = i.n_items, i.n_dense, i.n_deep
+    d.padded_len, d.chunk, d.kwin, d.tile_max = i.padded_len, i.chunk, i.kwin, i.tile_max
+    d.dense_lds, d.n_rlist = i.dense_lds, i.n_rlist
+    d.layers_dense, d.layers_built = i.layers_dense, i.layers_built
+    d.maxdel_active, d.maxdel = 1, 150
+    d.thresholds, d.n_thr, d.min_depth = p, 1, 1
+    d.fill_len, d.fill_nondash, d.fill = len(fill), sum(c != ord("-") for c in fill), p
+    for name in ("runs", "ibkt", "ilong", "ilong_n", "ins_cols", "ins_chr", "tile_stats", "blk_len", "out"):
+        setattr(d, name, p)
+    d.counts = p if counts else None
+    d.n_cols = i.n_cols
+    d.out_cap = 1 << 40
+    return d, scratch
+
+
+def test_device_stages_refuse_unbuilt_layers_before_launch():
+    """The guards added after round 3's GPU fault: s2c_pileup with a fill of length != 1, and
+    the counts-only stages (s2c_pileup_counts, s2c_accumulate), refuse a batch whose dense
+    tiles' layered windows are not built (S2C_ERR_ARG, before anything is launched — this runs
+    without a GPU); so does any stage with work items on a batch whose layers were never built
+    (a fresh shard: tile word 20 reset to S2C_LY_NONE, not the parent's layer numbers)."""
+    import ctypes as C
+    L = _lib
+    sam = ("@SQ\tSN:g1\tLN:300\n@SQ\tSN:g2\tLN:300\n"
+           + "".join("a%d\t0\tg1\t%d\t60\t50M\t*\t0\t0\t%s\t*\n" % (k, 1 + 5 * k, "ACGTA" * 10) for k in range(40))
+           + "".join("b%d\t0\tg2\t%d\t60\t20M2I20M\t*\t0\t0\t%s\t*\n" % (k, 1 + 5 * k, "ACGTG" * 8 + "AC")
+                     for k in range(40)))
+    hb = batch.parse_text(sam, True, 150)
+    try:
+        hb.ensure_layers()   # DeviceBatch's default: no dense layers
+        i = hb.info
+        assert i.n_dense > 0 and i.n_items > 0 and i.layers_built == 1 and i.layers_dense == 0
+        d, keep = _host_dev(hb, fill=b"NN")
+        assert L.lib.s2c_pileup(C.byref(d), None) == L.S2C_ERR_ARG
+        assert "layered" in L.last_error()
+        d, keep = _host_dev(hb, counts=True)
+        assert L.lib.s2c_pileup_counts(C.byref(d), None) == L.S2C_ERR_ARG
+        assert L.lib.s2c_accumulate(C.byref(d), 0, None) == L.S2C_ERR_ARG
+        d, keep = _host_dev(hb)
+        d.layers_built = 0
+        for f in (L.lib.s2c_pileup, L.lib.s2c_run):
+            assert f(C.byref(d), None) == L.S2C_ERR_ARG
+            assert "not built" in L.last_error()
+        sh = C.c_void_p()
+        L.check(L.lib.s2c_batch_shard(hb._b, 0, i.n_tiles, C.byref(sh)))
+        sb = batch.HostBatch(sh)
+        try:
+            assert sb.info.layers_built == 0 and sb.info.layers_dense == 0
+            assert (sb.tiles[:, 20] == 0xFFFFFFFE).all()
+            d, keep = _host_dev(sb)
+            assert L.lib.s2c_run(C.byref(d), None) == L.S2C_ERR_ARG
+            sb.ensure_layers()
+            assert sb.info.layers_built == 1
+        finally:
+            sb.free()
+    finally:
+        hb.free()

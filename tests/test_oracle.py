@@ -121,3 +121,15 @@ def test_c_oracle_matches_python_oracle_on_configs(mc_bin, wl):
     got = run_mc(mc_bin, text, args, 4, name=name + ".sam")
     assert got["status"] == want["status"] == "ok"
     assert got["files"] == want["files"]
+
+
+@pytest.mark.parametrize("idx", [0, 1])
+def test_oracle_many_thresholds_matches_reference(idx):
+    """300 thresholds (-c; the reference takes any number, sam2consensus.py:117-118): the
+    oracle equals the reference's files (tests/golden/limits.json, oracle/gen_golden_limits.py)."""
+    import hashlib
+    c = golden_io.load("limits")[idx]
+    r = o.run_case(c["sam"], c["args"])
+    assert r["status"] == c["status"]
+    got = {k: hashlib.sha256(v.encode("latin-1")).hexdigest() for k, v in r["files"].items()}
+    assert got == {k: v["sha256"] for k, v in c["files"].items()}
