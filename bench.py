@@ -82,10 +82,23 @@ def cpu_baseline(workload, scale):
         s2c_oracle.run_path(p, configs.cli_args(workload))
         dt = time.perf_counter() - t0
     sp = configs.spec(workload, scale=scale)
-    return {"value": a / dt, "unit": "aligned bases/s", "cores": 1, "kind": "port",
+    line = {"value": a / dt, "unit": "aligned bases/s", "cores": 1, "kind": "port",
             "sample": "%s at scale %g: %d refs x %d bp (%d aligned bases, %.1f s): oracle/s2c_oracle.py, the "
                       "pure-Python restatement of sam2consensus.py, parse+pileup+vote+format, 1 thread; %s"
                       % (workload, scale, sp.n_refs, sp.ref_len, a, dt, cpu_model())}
+    # calibration against the reference itself: oracle/calibrate_cpu.py ran the
+    # reference's main() and the restatement on the same files in the build container
+    cal = os.path.join(ROOT, "profiles", "r04", "cpu_calibration.json")
+    if os.path.exists(cal):
+        rows = {r["workload"]: r for r in json.load(open(cal))["rows"]}
+        r = rows.get(workload)
+        if r:
+            line["calibration"] = {"oracle_over_reference": r["oracle_over_reference"], "sample": "%s at scale %g"
+                                   % (workload, r["scale"]), "source": "profiles/r04/cpu_calibration.json"}
+            line["reference_equivalent_value"] = line["value"] / r["oracle_over_reference"]
+            line["sample"] += ("; the reference's own main() runs the same %s sample %.2fx slower than this "
+                               "restatement (calibration, build container)" % (workload, r["oracle_over_reference"]))
+    return line
 
 
 def cpu_threads():
@@ -291,11 +304,37 @@ def main():
         total_bases = float(info.aligned_bases)
 
     parity = None
-    if not args.no_parity:
-        if sharded:
-            parity = check_parity_sharded(wl, full, hb, ws, thresholds, rank, world)
-        elif rank == 0:
-            parity = check_parity(wl, hb, ws, thresholds)
+    exchange = None
+    if sharded:
+        # the exchange after the steps, on the record: fetch (D2H + body gather on the host),
+        # stats reduce, meta all-gather, body gather to rank 0 (RCCL), merge on rank 0; every
+        # rank's times synchronised, the max over ranks reported; and the read duplication the
+        # position split costs (each rank's pieces and batch bytes summed over the ranks)
+        dist.barrier()
+        t0 = time.perf_counter()
+        fetched = ws.fetch()
+        tim = {"fetch_s": time.perf_counter() - t0}
+        res = shard.gather_results(fetched, hb, rank, world, T, timing=tim)
+        dist.barrier()
+        tim["exchange_s"] = time.perf_counter() - t0
+        keys = ["fetch_s", "stats_reduce_s", "meta_s", "body_gather_s", "merge_s", "exchange_s"]
+        v = torch.tensor([tim.get(k, 0.0) for k in keys], dtype=torch.float64, device=dev)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        dv = torch.tensor([float(hb.info.n_pieces), float(shard.batch_bytes(hb)), float(tim.get("body_gather_bytes", 0))],
+                          dtype=torch.float64, device=dev)
+        dist.all_reduce(dv, op=dist.ReduceOp.SUM)
+        exchange = {k.replace("_s", "_ms"): float(x) * 1e3 for k, x in zip(keys, v.tolist())}
+        exchange.update({"pieces_over_ranks": int(dv[0].item()), "pieces_total": int(full.info.n_pieces),
+                         "dup_frac": float(dv[0].item()) / max(int(full.info.n_pieces), 1),
+                         "batch_bytes_over_ranks": int(dv[1].item()), "batch_bytes_total": shard.batch_bytes(full),
+                         "body_gather_bytes": int(dv[2].item()),
+                         "what": "after the K steps, once: ws.fetch + shard.gather_results (RCCL reduce / "
+                                 "all_gather / gather to rank 0), max over ranks; dup_frac = pieces summed over the "
+                                 "ranks' shards / the workload's"})
+        if not args.no_parity and rank == 0:
+            parity = check_parity_result(wl, full, res, thresholds, world)
+    elif not args.no_parity and rank == 0:
+        parity = check_parity(wl, hb, ws, thresholds)
 
     if rank == 0:
         ms = elapsed / K * 1e3
@@ -352,6 +391,10 @@ def main():
         line["host_synth_feed_s"] = t_synth
         line["host"] = cpu_model()
         line["parity"] = parity
+        if exchange is not None:
+            exchange["value_with_exchange"] = total_bases * K / (elapsed + K * exchange["exchange_ms"] * 1e-3)
+            exchange["value_with_exchange_what"] = "aligned bases/s if every step's output were gathered: K steps + K exchanges"
+            line["exchange"] = exchange
         if world == 1 and args.rehearse_shards > 1:
             line["shard_rehearsal"] = rehearse_shards(full, args.rehearse_shards, thresholds, min_depth, dev,
                                                       args.steps, args.warmup, info.aligned_bases)
@@ -373,7 +416,7 @@ def rehearse_shards(full, n, thresholds, min_depth, dev, K, W, bases):
 
     from sam2consensus_amd import shard
     from sam2consensus_amd.engine import DeviceBatch, Workspace
-    ms = []
+    ms, fetch_ms, parts, subs_info = [], [], [], []
     for r in range(n):
         sub = shard.sub_batch(full, r, n)
         ws = Workspace(DeviceBatch(sub, dev), thresholds, min_depth, b"-")
@@ -385,13 +428,33 @@ def rehearse_shards(full, n, thresholds, min_depth, dev, K, W, bases):
             ws.run()
         torch.cuda.synchronize(dev)
         ms.append((time.perf_counter() - t0) / K * 1e3)
+        t0 = time.perf_counter()
+        st, offs, out = ws.fetch()   # (a rank's exchange starts with its fetch: D2H + body gather)
+        fetch_ms.append((time.perf_counter() - t0) * 1e3)
+        parts.append((sub.t0, sub.t1, offs, out))
+        subs_info.append(sub)
         del ws
+    vol = shard.exchange_volumes(full, subs_info)
+    for sub in subs_info:
         sub.free()
+    t0 = time.perf_counter()
+    shard.merge_outputs(parts, len(thresholds))   # rank 0's merge of the gathered bodies
+    merge_ms = (time.perf_counter() - t0) * 1e3
+    body = sum(len(p[3]) + 8 * len(p[2]) for p in parts)
+    # rank 0 receives every other rank's bodies over its own xGMI link (≈153 GB/s per link,
+    # 7 per GPU: priced at half of that, one direction): the largest rank's share over one link
+    link_ms = max(len(p[3]) + 8 * len(p[2]) for p in parts) / 76.5e9 * 1e3
+    gather_ms = max(fetch_ms) + link_ms + merge_ms
     worst = max(ms)
     return {"shards": n, "ms_per_step": ms, "projected_ms_per_step": worst,
             "projected_value": bases / (worst * 1e-3),
+            "fetch_ms": fetch_ms, "merge_ms": merge_ms, "body_bytes": body, "gather_link_ms_est": link_ms,
+            "gather_ms": gather_ms, "dup_frac": vol["dup_frac"], "exchange_volumes": vol,
+            "projected_value_with_gather": bases / ((worst + gather_ms) * 1e-3),
             "what": "each shard of the %d-way position split run alone on one GPU; projected step = the slowest "
-                    "shard's (wall clock over K steps, launches included)" % n}
+                    "shard's (wall clock over K steps, launches included); gather_ms = the slowest shard's fetch "
+                    "(D2H + host body gather) + its bodies over one xGMI link at 76.5 GB/s (estimated) + rank 0's "
+                    "merge (measured), once per job: projected_value_with_gather charges it to every step" % n}
 
 
 def bound_from_profile(wl):
@@ -478,12 +541,8 @@ def check_parity(wl, hb, ws, thresholds):
     return "byte-identical to reference (%d files)" % len(want) if got == want else "MISMATCH"
 
 
-def check_parity_sharded(wl, full, hb, ws, thresholds, rank, world):
-    """Every rank's shard result is gathered (RCCL) and merged on rank 0, then compared."""
-    from sam2consensus_amd import shard
-    res = shard.gather_results(ws.fetch(), hb, rank, world, len(thresholds))
-    if rank != 0:
-        return None
+def check_parity_result(wl, full, res, thresholds, world):
+    """Rank 0: the shards' results gathered (RCCL) and merged, compared with the golden."""
     g = _golden(wl)
     if not g:
         return None

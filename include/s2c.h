@@ -131,6 +131,9 @@ int s2c_layout(int64_t *out, int n);
 #define S2C_TILE_DENSE    4  /* routed to k_tile_dense (one item, no insertion keys); its long list (lp[lp0, lp1)) holds
                                  piece indices, walked by the kernel; other tiles list run slots (k_reads) */
 #define S2C_ITEM_WORDS    4  /* work item {tile, chunk, l0, l1}: the tile's layers [l0, l1) */
+#define S2C_DWIN_WORDS   16  /* dense item's window {tile, a, b, cb0, lp0, lp1, pf0, pf1, o0, o1, qw0, qw1, 0, 0, 0, 0}:
+                                the words of its tile record k_tile_dense needs, in item order (one
+                                16-dword scalar load per tile instead of item → tile → record) */
 #define S2C_EPI_KEYS    256  /* insertion keys per tile k_tile's epilogue holds in LDS */
 /* insertion columns per tile k_tile's epilogue holds in LDS, by words per tile */
 #define S2C_LDS_COLS(nwp) ((nwp) <= 16 ? 640 : ((nwp) == 32 ? 448 : 192))
@@ -238,8 +241,10 @@ int  s2c_parser_progress(const s2c_parser *p, int64_t *out);
 
 /* FASTA body assembly (:394-418): dst = raw[starts[0] : +lens[0]] ++ raw[starts[1] : +lens[1]]
    ++ ... (n blocks; dst holds their total length), copied on the host threads.  The tiles'
-   body slots after the D2H copy of the device output, in [threshold][tile] order. */
-int  s2c_gather_bodies(const uint8_t *raw, const int64_t *starts, const int64_t *lens, int64_t n, uint8_t *dst);
+   body slots after the D2H copy of the device output, in [threshold][tile] order.  A block
+   outside raw's raw_len bytes is refused (S2C_ERR_ARG) before anything is copied. */
+int  s2c_gather_bodies(const uint8_t *raw, int64_t raw_len, const int64_t *starts, const int64_t *lens, int64_t n,
+                       uint8_t *dst);
 /* n bytes src → dst on the host threads (the host side of a batch's H2D staging). */
 int  s2c_copy_bytes(void *dst, const void *src, int64_t n);
 int  s2c_parser_pack(s2c_parser *p, int64_t g0, int64_t g1, size_t *len);
@@ -317,6 +322,7 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
     const uint32_t *lbq;       /* [n_lqwords][2] */
     const uint32_t *lbx;       /* [n_lqwords] */
     const uint32_t *px;        /* [n_pieces] the non-ACGT SEQ offsets of S2C_PF_XFEW pieces (else 0xFFFFFFFF) */
+    const uint32_t *dwin;      /* [n_dense][S2C_DWIN_WORDS] the dense items' windows */
 } s2c_batch_arrays;
 
 /* Build the batch's layered windows (s2c_batch_arrays lly .. lbx, tile word 20) if not yet
@@ -416,6 +422,7 @@ typedef struct {
                                   run dense tiles through k_tile and refuse a batch without them */
     const uint32_t *px;        /* [n_pieces] s2c_batch_arrays.px (ABI 10) */
     int64_t   layers_built;    /* the batch's info.layers_built: every launch with work items refuses 0 */
+    const uint32_t *dwin;      /* [n_dense][S2C_DWIN_WORDS] s2c_batch_arrays.dwin, filtered like dense */
 } s2c_dev;
 
 /* Sizes (bytes) of every workspace / output buffer for a batch and T thresholds. */

@@ -28,6 +28,7 @@ S2C_POS_ALIGN = 64
 S2C_TILE_WORDS = 24
 S2C_LY_MAIN = 0xFFFFFFFF
 S2C_ITEM_WORDS = 4
+S2C_DWIN_WORDS = 16
 S2C_CODE_FILL = 0
 S2C_SHORT_MOTIF = 16
 S2C_TILE_DEEP, S2C_TILE_GENERAL, S2C_TILE_DENSE = 1, 2, 4
@@ -66,7 +67,7 @@ _P32 = C.POINTER(C.c_uint32)
 class BatchArrays(C.Structure):
     _fields_ = [("ref_len", _P64), ("ref_off", _P64), ("ref_cov_reads", _P64)] + \
         [(n, _P32) for n in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "rlist", "lp", "wtile",
-                             "ps", "lly", "lpc", "lops", "lbq", "lbx", "px")]
+                             "ps", "lly", "lpc", "lops", "lbq", "lbx", "px", "dwin")]
 
 
 class SynthSpec(C.Structure):
@@ -94,7 +95,7 @@ class Dev(C.Structure):
         ("runs", _VP), ("ibkt", _VP), ("ilong", _VP), ("ilong_n", _VP), ("counts", _VP),
         ("ins_cols", _VP), ("ins_chr", _VP), ("n_cols", C.c_int64),
         ("tile_stats", _VP), ("blk_len", _VP), ("out", _VP), ("out_cap", C.c_int64), ("layers_dense", C.c_int64),
-        ("px", _VP), ("layers_built", C.c_int64)]
+        ("px", _VP), ("layers_built", C.c_int64), ("dwin", _VP)]
 
 
 class WsSizes(C.Structure):
@@ -151,7 +152,7 @@ def _load():
         "s2c_parser_checks": (C.c_int, [_VP, C.POINTER(C.c_uint8), C.c_int64]),
         "s2c_parser_counters": (C.c_int, [_VP, C.POINTER(C.c_int64)]),
         "s2c_parser_progress": (C.c_int, [_VP, C.POINTER(C.c_int64)]),
-        "s2c_gather_bodies": (C.c_int, [_VP, _VP, _VP, C.c_int64, _VP]),
+        "s2c_gather_bodies": (C.c_int, [_VP, C.c_int64, _VP, _VP, C.c_int64, _VP]),
         "s2c_copy_bytes": (C.c_int, [_VP, _VP, C.c_int64]),
         "s2c_parser_pack": (C.c_int, [_VP, C.c_int64, C.c_int64, C.POINTER(C.c_size_t)]),
         "s2c_parser_blob_copy": (C.c_int, [_VP, _VP, C.c_size_t]),

@@ -229,15 +229,20 @@ def consensus_files_sharded(filename, thresholds, prefix, min_depth, fill, nchar
                                "(S2C_DIST_BACKEND=gloo lets ranks share a device)" % (local, ndev))
         local %= ndev   # (ranks sharing a device: gloo tests on one GPU)
     torch.cuda.set_device(local)
-    if not dist.is_initialized():
+    owned = not dist.is_initialized()   # (this call's process group: destroyed on the way out)
+    if owned:
         dist.init_process_group(backend, device_id=torch.device("cuda", local) if backend == "nccl" else None)
-    P = parse_distributed(filename, rank, world, maxdel_active)
-    if log and rank == 0:
-        _log_summary(log, _Counters(P.hb.info.n_refs, P))
-    ws = Workspace(DeviceBatch(P.sub, "cuda:%d" % local, dense_layers=needs_dense_layers(fill)), thresholds,
-                   min_depth, fill)
-    ws.run()
-    res = gather_results(ws.fetch(), P.sub, rank, world, len(thresholds))
+    try:
+        P = parse_distributed(filename, rank, world, maxdel_active)
+        if log and rank == 0:
+            _log_summary(log, _Counters(P.hb.info.n_refs, P))
+        ws = Workspace(DeviceBatch(P.sub, "cuda:%d" % local, dense_layers=needs_dense_layers(fill)), thresholds,
+                       min_depth, fill)
+        ws.run()
+        res = gather_results(ws.fetch(), P.sub, rank, world, len(thresholds))
+    finally:
+        if owned and dist.is_initialized():
+            dist.destroy_process_group()
     if rank != 0:
         return None
     P.hb.ref_reads = P.ref_flags   # Σcoverage > 0 over every rank's reads (:334-341)

@@ -359,5 +359,42 @@ __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh
     return __builtin_amdgcn_alignbit(hi, lo, sh);
 }
 
+// A run record in LDS (k_tile_dense's window, k_tile's chunks; one per op slot, zero for
+// none): x = rs | re << 16, the run's positions [rs, re) relative to its tile's first word,
+// biased by REC_BIAS (a window starts ≤ 32·kwin ≤ 1024 positions before its tile and a short
+// run ends < 2048 positions after its start, so both fit 16 bits), y = q − rs with q the LDS
+// query base (planes) of its first position.  The count takes both ends with one packed
+// subtract and the plane word of a 32-position word from y + its biased first position; a
+// zero record covers nothing (re = rs).
+constexpr int32_t REC_BIAS = 2048;
+__device__ __forceinline__ uint2 rec_enc(uint32_t r0, uint32_t len, uint32_t q) {   // r0: tile-relative start
+    const uint32_t rs = r0 + (uint32_t)REC_BIAS;
+    return make_uint2(rs | ((rs + len) << 16), q - rs);
+}
+struct Rec {
+    uint32_t q, l;   // first query base (window-relative), length
+    int32_t r0;      // tile-relative first position
+};
+__device__ __forceinline__ Rec rec_dec(uint2 v) {
+    const uint32_t rs = v.x & 0xFFFFu;
+    return Rec{v.y + rs, (v.x >> 16) - rs, (int32_t)rs - REC_BIAS};
+}
+
+typedef short v2s __attribute__((ext_vector_type(2)));
+// The 32-position word at biased tile-relative position wpk (both halves) of record x: the
+// covered bits' mask (nb bits from l0) and fx = all ones iff all 32 are covered (v_bfm_b32
+// takes widths below 32), from both ends clamped to [0, 32] at once (packed 16-bit).
+__device__ __forceinline__ void rec_mask(uint32_t x, v2s wpk, uint32_t &m, uint32_t &fx) {
+    const v2s t = __builtin_elementwise_min(__builtin_elementwise_max(__builtin_bit_cast(v2s, x) - wpk, (v2s){0, 0}),
+                                            (v2s){32, 32});
+    const uint32_t tc = __builtin_bit_cast(uint32_t, t);
+    uint32_t nb;   // e - l0 (one SDWA subtract of the halves)
+    asm("v_sub_u32_sdwa %0, %1, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0"
+        : "=v"(nb) : "v"(tc));
+    // nb bits at l0 (v_bfm_b32 reads the offset's low 5 bits: l0 of tc; l0 = 32 only with nb = 0)
+    asm("v_bfm_b32 %0, %1, %2" : "=v"(m) : "v"(nb), "v"(tc));
+    fx = (uint32_t)__builtin_amdgcn_sbfe((int32_t)nb, 5, 1);
+}
+
 
 }  // namespace s2c

@@ -67,7 +67,7 @@ __constant__ __attribute__((aligned(16))) uint8_t c_amb[64] = {
 };
 
 struct DenseArgs {
-    const uint32_t *rs, *pc, *ops, *bq, *bx, *tiles, *items, *lp, *px;
+    const uint32_t *rs, *pc, *ops, *bq, *bx, *tiles, *items, *lp, *px, *dwin;
     const double *thresholds;
     uint64_t *tile_stats, *blk_len;
     uint8_t *out;
@@ -237,6 +237,31 @@ __device__ __forceinline__ uint32_t word_allreduce(uint32_t v) {
     return v;
 }
 
+// Reduce-scatter of the 8 transposed counter rows of 4 counters over the G adjacent lanes of a
+// word: lane g ends with rows g·(8/G) .. g·(8/G) + 8/G − 1 (in R[c][0 ..]) summed over the G
+// lanes.  Step h pairs lanes across bit h of g (G = 8: the first pairing is row_half_mirror,
+// lane i with 7 − i, which flips that bit too); each lane keeps the half of its remaining
+// rows holding its own and adds the partner's copy (v_add_u32_dpp).
+template <int BIT, int N>   // one step: pair across bit BIT of g, N rows held → N / 2
+__device__ __forceinline__ void rs_step(uint32_t (&R)[4][8], uint32_t g) {
+    constexpr int ctrl = BIT == 4 ? 0x141 : (BIT == 2 ? 0x4E : 0xB1);   // row_half_mirror, quad_perm [2,3,0,1] / [1,0,3,2]
+    const bool up = (g & (uint32_t)BIT) != 0;   // keep the upper half of the rows held
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+#pragma unroll
+        for (int r = 0; r < N / 2; r++) {
+            const uint32_t keep = up ? R[c][r + N / 2] : R[c][r], send = up ? R[c][r] : R[c][r + N / 2];
+            R[c][r] = keep + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)send, ctrl, 0xF, 0xF, true);
+        }
+}
+template <int G>
+__device__ __forceinline__ void reduce_scatter_rows(uint32_t (&R)[4][8], uint32_t g) {
+    static_assert(G == 1 || G == 2 || G == 4 || G == 8, "lanes per word");
+    if constexpr (G == 8) rs_step<4, 8>(R, g);
+    if constexpr (G >= 4) rs_step<2, (G == 8 ? 4 : 8)>(R, g);
+    if constexpr (G >= 2) rs_step<1, 16 / G>(R, g);
+}
+
 // Per-position byte counters in the ROW layout of the transposed counters: tile-relative
 // position p = 32w + 8j + r is byte j of dword 8w + r.
 __device__ __forceinline__ void cnt_add1(uint32_t *cnt, uint32_t p) {
@@ -340,7 +365,6 @@ __device__ __forceinline__ uint32_t lo16(uint32_t v) { return v & 0x00FF00FFu; }
 __device__ __forceinline__ uint32_t hi16(uint32_t v) { return (v >> 8) & 0x00FF00FFu; }
 // the low bytes of the halves of e (j = 0, 2) and o (j = 1, 3) back into j order
 __device__ __forceinline__ uint32_t merge16(uint32_t o, uint32_t e) { return __builtin_amdgcn_perm(o, e, 0x06020400u); }
-typedef short v2s __attribute__((ext_vector_type(2)));
 typedef unsigned short v2u __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(v2u, a), __builtin_bit_cast(v2u, b)));
@@ -355,50 +379,29 @@ __device__ __forceinline__ uint32_t pk_sign(uint32_t a) {
 // bit j (j = 0..3) = top bit of byte j
 __device__ __forceinline__ uint32_t byte_bits(uint32_t m) { return ((m & 0x80808080u) * 0x00204081u) >> 28; }
 
-// A run record of the window in LDS (one per op slot, zero for none): x = rs | re << 16, the
-// run's tile-relative positions [rs, re) biased by REC_BIAS (a window starts ≤ 32·kwin ≤ 1024
-// positions before its tile and a short run ends < 2048 positions after its start, so both
-// fit 16 bits), y = q − rs with q the window-relative query base of its first position.  The
-// count takes both ends with one packed subtract and the plane word of a 32-position word W
-// from y + 32·W's biased offset; a zero record covers nothing (re = rs).
-constexpr int32_t REC_BIAS = 2048;
-__device__ __forceinline__ uint2 rec_enc(uint32_t r0, uint32_t len, uint32_t q) {   // r0: tile-relative start
-    const uint32_t rs = r0 + (uint32_t)REC_BIAS;
-    return make_uint2(rs | ((rs + len) << 16), q - rs);
-}
-struct Rec {
-    uint32_t q, l;   // first query base (window-relative), length
-    int32_t r0;      // tile-relative first position
-};
-__device__ __forceinline__ Rec rec_dec(uint2 v) {
-    const uint32_t rs = v.x & 0xFFFFu;
-    return Rec{v.y + rs, (v.x >> 16) - rs, (int32_t)rs - REC_BIAS};
-}
-
 // A tile's window (uniform values from its tile record; S2C_TILE_WORDS layout)
 struct Win {
     uint32_t tile, a, n, cb0, pf0, npc, o0, nslot, qw0, nqw, W0, nwords, lp0, nlong;
 };
 __device__ __forceinline__ Win win_of(const DenseArgs &d, uint32_t item) {
     Win v;
-    v.tile = sload1(d.items + 4 * (size_t)item);
-    // the whole 20-word tile record in one scalar round trip
-    const uint32_t *twp = uni_ptr(d.tiles + (size_t)v.tile * S2C_TILE_WORDS);
+    // the item's window (S2C_DWIN_WORDS, built by the host from the tile record) in one
+    // scalar round trip
     v16i r;
-    v4i r4;
-    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx4 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
-                 : "=s"(r), "=s"(r4) : "s"(twp) : "memory");
-    v.cb0 = (uint32_t)r[8];
-    v.lp0 = (uint32_t)r[10];
-    v.nlong = (uint32_t)r[11] - v.lp0;
-    v.a = (uint32_t)r[0];
-    v.n = (uint32_t)r[1] - v.a;
-    v.pf0 = (uint32_t)r[13];
-    v.npc = (uint32_t)r[14] - v.pf0;
-    v.o0 = (uint32_t)r[15];
-    v.nslot = (uint32_t)r4.x - v.o0;
-    v.qw0 = (uint32_t)r4.y;
-    v.nqw = (uint32_t)r4.z - v.qw0;
+    asm volatile("s_load_dwordx16 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)"
+                 : "=s"(r) : "s"(uni_ptr(d.dwin + (size_t)item * S2C_DWIN_WORDS)) : "memory");
+    v.tile = (uint32_t)r[0];
+    v.a = (uint32_t)r[1];
+    v.n = (uint32_t)r[2] - v.a;
+    v.cb0 = (uint32_t)r[3];
+    v.lp0 = (uint32_t)r[4];
+    v.nlong = (uint32_t)r[5] - v.lp0;
+    v.pf0 = (uint32_t)r[6];
+    v.npc = (uint32_t)r[7] - v.pf0;
+    v.o0 = (uint32_t)r[8];
+    v.nslot = (uint32_t)r[9] - v.o0;
+    v.qw0 = (uint32_t)r[10];
+    v.nqw = (uint32_t)r[11] - v.qw0;
     v.W0 = v.a >> 5;
     v.nwords = (v.n + 31) / 32;
     return v;
@@ -447,12 +450,56 @@ constexpr int WT = WGD * WPT;     // threads per tile
 #define S2C_DENSE_PFN 2
 #endif
 constexpr int PFN = S2C_DENSE_PFN;   // piece records per thread loaded with the DMA (windows of ≤ PFN·WT pieces)
+#ifndef S2C_DENSE_PERSIST
+#define S2C_DENSE_PERSIST 0   // 1: persistent workgroups (the next tile's window DMA under this tile's vote)
+#endif
+// A tile's FASTA bytes and statistics held in registers until the persistent loop has issued
+// the next tile's loads (one threshold, whole words): stored then, so the loop's wait for
+// those loads is not also a wait for stores issued just before it.
 template <int NWP>
+struct Deferred {
+    static constexpr int RPL = 8 / (WGD / (NWP / WPT));
+    uint32_t body[RPL == 8 ? 8 : (RPL == 4 ? 4 : (RPL == 2 ? 2 : 1))];   // the lane's row bytes, packed
+    uint64_t boff;   // out byte offset of the lane's first byte (its word's row base)
+    bool pend;       // the lane holds body bytes to store
+    // tile statistics (uniform; stored by thread 0)
+    uint32_t tile, sc, nd, ne, n;
+    bool spend;
+};
+template <int NWP>
+__device__ __forceinline__ void flush_deferred(const DenseArgs &d, Deferred<NWP> &f) {
+    constexpr int RPL = Deferred<NWP>::RPL;
+    if (f.pend) {
+        uint8_t *dst = d.out + f.boff;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if constexpr (RPL == 8) *(uint2 *)(dst + 8 * j) = make_uint2(f.body[j], f.body[4 + j]);
+            else if constexpr (RPL == 4) *(uint32_t *)(dst + 8 * j) = f.body[j];
+            else if constexpr (RPL == 2) *(uint16_t *)(dst + 8 * j) = (uint16_t)(f.body[j >> 1] >> (16 * (j & 1)));
+            else dst[8 * j] = (uint8_t)(f.body[0] >> (8 * j));
+        }
+        f.pend = false;
+    }
+    if (f.spend) {
+        if (threadIdx.x == 0) {
+            uint64_t *st = d.tile_stats + (size_t)f.tile * 4;
+            st[0] = f.sc;
+            st[1] = f.n;
+            st[2] = f.nd;
+            st[3] = f.ne;
+            d.blk_len[f.tile] = f.n;
+        }
+        f.spend = false;
+    }
+}
+
+template <int NWP, class OnFree>
 __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, const WinLds &L, uint32_t *dcnt,
                                            uint32_t *ncnt, uint32_t *ccnt, const uint8_t *amb, uint32_t fill0,
                                            const uint4 (&Pp)[PFN], const uint32_t (&oe)[PFN], const uint32_t (&pxr)[PFN],
                                            uint32_t cw0, uint32_t cw1, unsigned long long t_entry,
-                                           uint32_t (*stl)[WPT][4]) {
+                                           uint32_t (*stl)[WPT][4], OnFree &&on_free, Deferred<NWP> &dfr, bool defer,
+                                           uint32_t tid) {
     constexpr int NWPW = NWP / WPT, G = WGD / NWPW, RPL = 8 / G;
 #ifdef S2C_PROF
     unsigned long long prof_t = t_entry;
@@ -460,7 +507,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     (void)t_entry;
 #endif
     PROF_MARK(1);   // phase 0: entry → window landed (scalar tile loads, DMA, piece records)
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t lane = tid & 63, wv = tid >> 6;
     const uint32_t w = wv * NWPW + lane / G, g = lane % G;   // tile-relative word of this lane
     const uint32_t tile = v.tile, a = v.a, n = v.n, cb0 = v.cb0, npc = v.npc, o0 = v.o0, qw0 = v.qw0;
     const uint32_t W0 = v.W0, nwords = v.nwords, W = W0 + w;
@@ -679,18 +726,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         uint2 pa[GSD], pb[GSD];
 #pragma unroll
         for (int u = h; u < h + CNT_PART; u++) {
-            // both ends word-relative at once (packed 16-bit), clamped to [0, 32]
-            const v2s t = __builtin_elementwise_min(
-                __builtin_elementwise_max(__builtin_bit_cast(v2s, rv[u].x) - wpk, (v2s){0, 0}), (v2s){32, 32});
-            const uint32_t tc = __builtin_bit_cast(uint32_t, t);
-            uint32_t nb;   // e - l0 (one SDWA subtract of the halves)
-            asm("v_sub_u32_sdwa %0, %1, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0"
-                : "=v"(nb) : "v"(tc));
-            uint32_t m;   // nb bits at l0 (nb < 32; v_bfm_b32 reads the offset's low 5 bits: l0 of tc, and
-                          // l0 = 32 only with nb = 0)
-            asm("v_bfm_b32 %0, %1, %2" : "=v"(m) : "v"(nb), "v"(tc));
-            bm[u] = m;
-            fx[u] = (uint32_t)__builtin_amdgcn_sbfe((int32_t)nb, 5, 1);    // all ones iff nb = 32
+            rec_mask(rv[u].x, wpk, bm[u], fx[u]);   // the word's covered bits (rec_enc)
             // query base of the word's bit 0 = y + (biased word start): word offset y >> 5 from
             // the lane's base, bit offset y mod 32 (the funnel shift takes the low 5 bits)
             sh[u] = rv[u].y;
@@ -818,7 +854,8 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         const Rec rc = rec_dec(runl[queue[qcap - 1u - i]]);
         x_events(bxl, bql, rc.q, rc.l, rc.r0, TL, false, dcnt, ncnt, ccnt);
     }
-    lds_sync();   // the byte counters are final
+    lds_sync();   // the byte counters are final; the window's LDS is free
+    on_free();    // (persistent: the next tile's window DMA, under this tile's vote)
     PROF_MARK(4);
     // the byte counters of this lane's rows: read now, used by the vote
     const uint32_t rbase = 8 * w + g * RPL;   // the rows' dword index in the byte counters
@@ -829,39 +866,36 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         rN[rr] = active ? ncnt[rbase + rr] : 0u;
         rX[rr] = active ? ccnt[rbase + rr] : 0u;
     }
+    if (S2C_DENSE_PERSIST && active) {   // (zero again for the next tile: a wave's lanes hold all rows of its words)
+#pragma unroll
+        for (int rr = 0; rr < RPL; rr++) {
+            dcnt[rbase + rr] = 0u;
+            ncnt[rbase + rr] = 0u;
+            ccnt[rbase + rr] = 0u;
+        }
+    }
     // ---- counters → byte counts: R[r] byte j = count of position 8j + r
 #pragma unroll
     for (int c = 0; c < 4; c++) transpose8(C[c]);
+    // this lane's rows g·RPL .. g·RPL + RPL − 1 summed over the word's G lanes by a
+    // reduce-scatter: each step pairs lanes across the top remaining bit of g, each keeps the
+    // half of its rows that holds its own and adds the partner's copy of them (the rows sent
+    // are the other half, selected into the same register first: a DPP source is the same
+    // register in the partner lane)
+    uint32_t R[4][8];
 #pragma unroll
-    for (int r = 0; r < 8; r++) {
-        const uint32_t x = C[0][r], y = C[1][r], z = C[2][r], v = C[3][r];
-        C[3][r] = v - x - y + z;   // A
-        C[0][r] = x - z;           // C
-        C[1][r] = y - z;           // G
-    }
-    // this lane's rows g·RPL .. g·RPL + RPL − 1, all-reduced over the word's G lanes
-    // (DPP needs the same register in every lane: all 8 rows reduced, then this lane's selected)
-    if constexpr (G > 1) {
+    for (int c = 0; c < 4; c++)
 #pragma unroll
-        for (int c = 0; c < 4; c++)
-#pragma unroll
-            for (int r = 0; r < 8; r++) C[c][r] = word_allreduce<G>(C[c][r]);
-    }
+        for (int r = 0; r < 8; r++) R[c][r] = C[c][r];
+    reduce_scatter_rows<G>(R, g);
     uint32_t rA[RPL], rC[RPL], rG[RPL], rT[RPL];
 #pragma unroll
-    for (int rr = 0; rr < RPL; rr++) {
-        rA[rr] = C[3][rr];
-        rC[rr] = C[0][rr];
-        rG[rr] = C[1][rr];
-        rT[rr] = C[2][rr];
-#pragma unroll
-        for (int k = 1; k < G; k++) {
-            const bool mine = g == (uint32_t)k;
-            rA[rr] = mine ? C[3][k * RPL + rr] : rA[rr];
-            rC[rr] = mine ? C[0][k * RPL + rr] : rC[rr];
-            rG[rr] = mine ? C[1][k * RPL + rr] : rG[rr];
-            rT[rr] = mine ? C[2][k * RPL + rr] : rT[rr];
-        }
+    for (int rr = 0; rr < RPL; rr++) {   // counts from the planes' sums: X = C|T, Y = G|T, Z = T, V = covered
+        const uint32_t x = R[0][rr], y = R[1][rr], z = R[2][rr], v = R[3][rr];
+        rA[rr] = v - x - y + z;
+        rC[rr] = x - z;
+        rG[rr] = y - z;
+        rT[rr] = z;
     }
     PROF_MARK(6);
 
@@ -877,10 +911,9 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         const uint32_t cA = rA[rr] - rN[rr], cC = rC[rr] - rX[rr];   // 'N' counted as A, SEQ '-' as C
         const uint32_t cv = cA + cC + rG[rr] + rT[rr] + rD[rr] + rN[rr];   // ≤ 255 per byte
         // in-tile positions: p = 32w + 8j + r < n
-        const uint32_t pr = 32 * w + g * RPL + rr;
-        uint32_t im = 0;
-#pragma unroll
-        for (int j = 0; j < 4; j++) im |= (active && pr + 8 * j < n) ? (0xFFu << (8 * j)) : 0u;
+        // (bytes j < ⌈(n − pr) / 8⌉, at most 4)
+        const int32_t nj = min(max(((int32_t)n - (int32_t)(32 * w + g * RPL + rr) + 7) >> 3, 0), 4);
+        const uint32_t im = (active && nj) ? 0xFFFFFFFFu >> (32 - 8 * nj) : 0u;
         inb[rr] = im;
         cvb[rr] = cv;
         sc = __builtin_amdgcn_udot4(cv & im, 0x01010101u, sc, false);   // Σ cov over the tile (:357)
@@ -979,11 +1012,19 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             o[2] = __builtin_amdgcn_perm(t3, t1, 0x05040100u);
             o[3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
         };
+        if (defer) dfr.boff = (uint64_t)(dst - d.out);
         if constexpr (RPL == 8) {
             uint32_t c2[4];
             tr4(ow[0], ow[1], ow[2], ow[3], cj);
             tr4(ow[4 % RPL], ow[5 % RPL], ow[6 % RPL], ow[7 % RPL], c2);
-            if (full) {
+            if (defer && full) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    dfr.body[j % (sizeof(dfr.body) / 4)] = cj[j];
+                    dfr.body[(4 + j) % (sizeof(dfr.body) / 4)] = c2[j];
+                }
+                dfr.pend = true;
+            } else if (full) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) *(uint2 *)(dst + 8 * j) = make_uint2(cj[j], c2[j]);
             } else if (active) {
@@ -995,7 +1036,20 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             }
         } else {
             tr4(ow[0], RPL > 1 ? ow[1 % RPL] : 0u, RPL > 2 ? ow[2 % RPL] : 0u, RPL > 3 ? ow[3 % RPL] : 0u, cj);
-            if (full) {
+            if (defer && full) {
+                constexpr int NB = sizeof(dfr.body) / 4;
+                if constexpr (RPL == 4) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) dfr.body[j % NB] = cj[j];
+                } else if constexpr (RPL == 2) {
+                    dfr.body[0] = (cj[0] & 0xFFFFu) | (cj[1] << 16);
+                    dfr.body[1 % NB] = (cj[2] & 0xFFFFu) | (cj[3] << 16);
+                } else {
+                    dfr.body[0] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(cj[3], cj[2], 0x0C0C0400u),
+                                                        __builtin_amdgcn_perm(cj[1], cj[0], 0x0C0C0400u), 0x05040100u);
+                }
+                dfr.pend = true;
+            } else if (full) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     if constexpr (RPL == 4) *(uint32_t *)(dst + 8 * j) = cj[j];
@@ -1011,15 +1065,29 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             }
         }
         if (t == 0) sc = wave_sum(sc);
-        nd = wave_sum(nd);
-        ne = wave_sum(ne);
+        // non-'-' and vote-error counts of the wave (≤ 512 each) in one reduction
+        const uint32_t nde = wave_sum(nd | (ne << 16));
         if (lane == 0) {   // this wave's share (by threshold parity: one barrier per threshold)
             stl[t & 1][wv][0] = sc;
-            stl[t & 1][wv][1] = nd;
-            stl[t & 1][wv][2] = ne;
+            stl[t & 1][wv][1] = nde & 0xFFFFu;
+            stl[t & 1][wv][2] = nde >> 16;
         }
         lds_sync();
-        if (tid == 0) {   // tile statistics (:352-397); ≤ 2048 positions: u32 partial sums
+        if (defer) {   // (one threshold: held for flush_deferred; uniform sums)
+            uint32_t s0 = 0, s2 = 0, s3 = 0;
+#pragma unroll
+            for (int k = 0; k < WPT; k++) {
+                s0 += stl[0][k][0];
+                s2 += stl[0][k][1];
+                s3 += stl[0][k][2];
+            }
+            dfr.tile = tile;
+            dfr.sc = uni(s0);
+            dfr.nd = uni(s2);
+            dfr.ne = uni(s3);
+            dfr.n = n;
+            dfr.spend = true;
+        } else if (tid == 0) {   // tile statistics (:352-397); ≤ 2048 positions: u32 partial sums
             uint64_t s0 = 0, s2 = 0, s3 = 0;
 #pragma unroll
             for (int k = 0; k < WPT; k++) {
@@ -1057,6 +1125,127 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
 // One wave per tile (block b → item, XCD-major: the blocks of one XCD, b ≡ x mod 8, take a
 // contiguous range of items, so neighbouring windows meet in that XCD's L2).  Everything the
 // tile needs arrives by one LDS-DMA round trip after the scalar loads of its tile record.
+#if S2C_DENSE_PERSIST
+// A persistent workgroup (WPT waves) per tile slot of a CU: XCD x (blocks b ≡ x mod 8) takes
+// the contiguous items [x0, x1) and its nbx blocks take every nbx-th of them, so the tiles in
+// flight on one XCD are neighbours.  Each tile after the first needs one round trip at its
+// top (piece records, run-slot range, the next item's window): its own window was DMA'd during
+// the previous tile's vote, once the count had freed the LDS; with one threshold the previous
+// tile's body bytes and statistics are stored after that round trip is issued (Deferred).
+__device__ __forceinline__ Win win_vrec(uint32_t rec) {   // lane k of rec: word k of the item's dwin row
+    auto wd = [&](int k) { return (uint32_t)__builtin_amdgcn_readlane((int)rec, k); };
+    Win v;
+    v.tile = wd(0);
+    v.a = wd(1);
+    v.n = wd(2) - v.a;
+    v.cb0 = wd(3);
+    v.lp0 = wd(4);
+    v.nlong = wd(5) - v.lp0;
+    v.pf0 = wd(6);
+    v.npc = wd(7) - v.pf0;
+    v.o0 = wd(8);
+    v.nslot = wd(9) - v.o0;
+    v.qw0 = wd(10);
+    v.nqw = wd(11) - v.qw0;
+    v.W0 = v.a >> 5;
+    v.nwords = (v.n + 31) / 32;
+    return v;
+}
+
+template <int NWP>
+__global__ __launch_bounds__(WT) S2C_DENSE_OCC void k_tile_dense(const DenseArgs d) {
+    extern __shared__ uint4 arena[];   // the window (S2C_DENSE_BYTES layout)
+    __shared__ __attribute__((aligned(16))) uint32_t dcnt[8 * NWP], ncnt[8 * NWP], ccnt[8 * NWP];
+    __shared__ __attribute__((aligned(16))) uint8_t amb[64];
+    __shared__ uint32_t stl[2][WPT][4];
+    const uint32_t b = blockIdx.x;
+    const uint32_t x = b & 7u, per = d.n_items >> 3, rem = d.n_items & 7u;
+    const uint32_t x0 = x * per + min(x, rem), x1 = x0 + per + (x < rem ? 1u : 0u);
+    const uint32_t nbx = (gridDim.x >> 3) + ((gridDim.x & 7u) > x ? 1u : 0u);
+    uint32_t item = x0 + (b >> 3);
+    if (item >= x1) return;   // (uniform: every wave of the block leaves)
+    Win v = win_of(d, item);
+    uint8_t *const buf = (uint8_t *)arena;
+    win_issue<WPT>(d, v, buf);
+    {
+        v16i r;
+        asm volatile("s_load_dwordx16 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(uni_ptr((const uint32_t *)c_amb)) : "memory");
+        if (threadIdx.x == 0) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) ((uint32_t *)amb)[i] = (uint32_t)r[i];
+        }
+    }
+    const uintptr_t fa = (uintptr_t)d.fill;
+    const uint32_t fill0 = (sload1((const uint32_t *)(fa & ~(uintptr_t)3)) >> (8 * (uint32_t)(fa & 3))) & 0xFFu;
+    for (uint32_t k = threadIdx.x; k < 8 * NWP; k += WT) {   // (each vote zeroes its rows again)
+        dcnt[k] = 0;
+        ncnt[k] = 0;
+        ccnt[k] = 0;
+    }
+    constexpr int G = WGD / (NWP / WPT);
+    const uint32_t K = d.kwin;
+    Deferred<NWP> def;
+    def.pend = false;
+    def.spend = false;
+    const bool defer = d.n_thr == 1;
+    for (;;) {
+#ifdef S2C_PROF
+        const unsigned long long t_entry = __builtin_amdgcn_s_memtime();
+#else
+        const unsigned long long t_entry = 0;
+#endif
+        // (the lane's indices re-derived each tile: nothing lane-dependent is hoisted out of
+        // the loop and held in registers through it)
+        uint32_t tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const uint32_t lane = tid & 63, w = (tid >> 6) * (NWP / WPT) + lane / G;
+        const WinLds wl = win_lds(d, v, buf);
+        if (tid < RUN_PAD) wl.runl[v.nslot + tid] = make_uint2(0u, 0u);   // (the DMA does not write there)
+        uint4 Pp[PFN];
+        uint32_t oe[PFN], pxr[PFN];
+#pragma unroll
+        for (int i = 0; i < PFN; i++) {
+            const uint32_t k = tid + WT * i;
+            Pp[i] = make_uint4(0u, 0u, 0u, 0u);
+            oe[i] = 0;
+            pxr[i] = 0xFFFFFFFFu;
+            if (k < v.npc) {
+                Pp[i] = ((const uint4 *)d.pc)[v.pf0 + k];
+                oe[i] = d.pc[4 * (size_t)(v.pf0 + k + 1) + 2];
+                pxr[i] = d.px[v.pf0 + k];
+            }
+        }
+        const uint32_t W = v.W0 + w;
+        uint32_t cw0 = 0, cw1 = 0;
+        if (w < v.nwords) {
+            cw0 = d.rs[W >= K ? W - K : 0u];
+            cw1 = d.rs[W + 1];
+        }
+        const uint32_t nitem = item + nbx;
+        const bool more = nitem < x1;
+        uint32_t nrec = 0;   // the next item's window row (lane k: word k; waited for where it is issued)
+        if (more) nrec = d.dwin[(size_t)nitem * S2C_DWIN_WORDS + (lane & 15u)];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the window landed; records, range, next row
+        flush_deferred<NWP>(d, def);   // the previous tile's bytes and statistics
+        cw0 -= v.o0;
+        cw1 -= v.o0;
+        lds_sync();
+        Win vn = v;
+        dense_tile<NWP>(d, v, wl, dcnt, ncnt, ccnt, amb, fill0, Pp, oe, pxr, cw0, cw1, t_entry, stl,
+                        [&]() {
+                            if (more) {
+                                vn = win_vrec(nrec);
+                                win_issue<WPT>(d, vn, buf);
+                            }
+                        },
+                        def, defer, tid);
+        if (!more) break;
+        item = nitem;
+        v = vn;
+    }
+    flush_deferred<NWP>(d, def);
+}
+#else
 template <int NWP>
 __global__ __launch_bounds__(WT) S2C_DENSE_OCC void k_tile_dense(const DenseArgs d) {
     extern __shared__ uint4 arena[];   // the window (S2C_DENSE_BYTES layout)
@@ -1121,12 +1310,29 @@ __global__ __launch_bounds__(WT) S2C_DENSE_OCC void k_tile_dense(const DenseArgs
     cw0 -= v.o0;
     cw1 -= v.o0;
     lds_sync();
-    dense_tile<NWP>(d, v, wl, dcnt, ncnt, ccnt, amb, fill0, Pp, oe, pxr, cw0, cw1, t_entry, stl);
+    Deferred<NWP> dfr;
+    dense_tile<NWP>(d, v, wl, dcnt, ncnt, ccnt, amb, fill0, Pp, oe, pxr, cw0, cw1, t_entry, stl, []() {}, dfr, false,
+                    threadIdx.x);
 }
+
+#endif
 
 template <int NWP>
 int launch(const DenseArgs &a, int64_t n, hipStream_t s) {
-    k_tile_dense<NWP><<<(unsigned)n, WT, a.buf_bytes, s>>>(a);
+    int64_t grid = n;
+#if S2C_DENSE_PERSIST
+    {   // the workgroups the device holds at once (occupancy × CUs, a multiple of the 8 XCDs)
+        int dev = 0, per_cu = 0, ncu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(&k_tile_dense<NWP>), WT,
+                                                         a.buf_bytes) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return s2c_set_error(S2C_ERR_HIP, "k_tile_dense occupancy query");
+        const int64_t full = std::max<int64_t>((int64_t)per_cu * ncu, 8) & ~(int64_t)7;
+        grid = std::min<int64_t>(n, full);
+    }
+#endif
+    k_tile_dense<NWP><<<(unsigned)grid, WT, a.buf_bytes, s>>>(a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? S2C_OK : s2c_set_error(S2C_ERR_HIP, std::string("k_tile_dense: ") + hipGetErrorString(e));
 }
@@ -1154,7 +1360,7 @@ int s2c_launch_dense(const s2c_dev *dv, hipStream_t st) {
     if (dv->fill_len != 1) return s2c_set_error(S2C_ERR_ARG, "dense tiles need a one-char fill");
     if (dv->n_dense >= ((int64_t)1 << 31)) return s2c_set_error(S2C_ERR_LIMIT, "too many dense tiles");
     DenseArgs a;
-    a.rs = dv->rs; a.lp = dv->lp; a.pc = dv->pc; a.px = dv->px; a.ops = dv->ops; a.bq = dv->bq; a.bx = dv->bx; a.tiles = dv->tiles; a.items = dv->dense;
+    a.rs = dv->rs; a.lp = dv->lp; a.pc = dv->pc; a.px = dv->px; a.dwin = dv->dwin; a.ops = dv->ops; a.bq = dv->bq; a.bx = dv->bx; a.tiles = dv->tiles; a.items = dv->dense;
     a.thresholds = dv->thresholds; a.tile_stats = dv->tile_stats; a.blk_len = dv->blk_len; a.out = dv->out;
     a.padded_len = (uint32_t)dv->padded_len; a.n_cols = (uint32_t)dv->n_cols; a.n_tiles = (uint32_t)dv->n_tiles;
     a.kwin = (uint32_t)dv->kwin; a.fill_nondash = (uint32_t)dv->fill_nondash;

@@ -282,7 +282,21 @@ struct s2c_batch {
     bool layers = false;                               // built (s2c_batch_layers)
     u32buf kmin, kmax;   // host only: global key range of each piece's insertion events
     u32buf px;           // [pieces] the non-ACGT SEQ offsets of S2C_PF_XFEW pieces (s2c.h)
+    std::vector<uint32_t> dwin;   // [dense][S2C_DWIN_WORDS] the dense items' windows (s2c.h)
 };
+
+// The dense items' windows (S2C_DWIN_WORDS) from the final tile records.
+static void build_dwin(s2c_batch *b) {
+    const size_t nd = b->dense.size() / S2C_ITEM_WORDS;
+    b->dwin.assign(std::max<size_t>(nd, 1) * S2C_DWIN_WORDS, 0u);
+    for (size_t i = 0; i < nd; i++) {
+        const uint32_t t = b->dense[i * S2C_ITEM_WORDS];
+        const uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
+        uint32_t *o = &b->dwin[i * S2C_DWIN_WORDS];
+        const uint32_t v[12] = {t, tw[0], tw[1], tw[8], tw[10], tw[11], tw[13], tw[14], tw[15], tw[16], tw[17], tw[18]};
+        for (int k = 0; k < 12; k++) o[k] = v[k];
+    }
+}
 
 static int perr(s2c_parser *p, int code, const std::string &msg) {
     p->err = code;
@@ -1715,13 +1729,16 @@ extern "C" int s2c_parser_checks(s2c_parser *p, uint8_t *bad, int64_t n_refs) {
 
 // FASTA body assembly (:394-418): the tiles' body slots, concatenated in [threshold][tile]
 // order (n blocks: raw[starts[i], starts[i] + lens[i]) → dst at the running offset), on the
-// host threads for large outputs.
-static int s2c_gather_bodies_impl(const uint8_t *raw, const int64_t *starts, const int64_t *lens, int64_t n,
-                                  uint8_t *dst) {
-    if (n < 0 || (n > 0 && (!starts || !lens))) return s2c_set_error(S2C_ERR_ARG, "bad gather arguments");
+// host threads for large outputs.  Every block must lie inside raw's raw_len bytes (the
+// lengths come from the device: a block past the end is refused, never read).
+static int s2c_gather_bodies_impl(const uint8_t *raw, int64_t raw_len, const int64_t *starts, const int64_t *lens,
+                                  int64_t n, uint8_t *dst) {
+    if (n < 0 || raw_len < 0 || (n > 0 && (!starts || !lens))) return s2c_set_error(S2C_ERR_ARG, "bad gather arguments");
     std::vector<int64_t> off(n + 1, 0);
     for (int64_t i = 0; i < n; i++) {
         if (lens[i] < 0 || starts[i] < 0) return s2c_set_error(S2C_ERR_ARG, "negative block");
+        if (lens[i] > raw_len || starts[i] > raw_len - lens[i])
+            return s2c_set_error(S2C_ERR_ARG, "body block past the end of the device output");
         off[i + 1] = off[i] + lens[i];
     }
     if (off[n] > 0 && (!raw || !dst)) return s2c_set_error(S2C_ERR_ARG, "bad gather arguments");
@@ -1730,8 +1747,9 @@ static int s2c_gather_bodies_impl(const uint8_t *raw, const int64_t *starts, con
     });
     return S2C_OK;
 }
-extern "C" int s2c_gather_bodies(const uint8_t *raw, const int64_t *starts, const int64_t *lens, int64_t n, uint8_t *dst) {
-    return s2c_guarded([&] { return s2c_gather_bodies_impl(raw, starts, lens, n, dst); });
+extern "C" int s2c_gather_bodies(const uint8_t *raw, int64_t raw_len, const int64_t *starts, const int64_t *lens,
+                                 int64_t n, uint8_t *dst) {
+    return s2c_guarded([&] { return s2c_gather_bodies_impl(raw, raw_len, starts, lens, n, dst); });
 }
 
 // n bytes src → dst on the host threads (staging a batch into pinned buffers for its H2D:
@@ -2478,6 +2496,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     I.n_cols = (int64_t)coff;
     I.runs_max = runs_max;
     mark_runs(b);
+    build_dwin(b);
     clk.mark("mark_runs");
     *out = guard.release();
     return S2C_OK;
@@ -2661,6 +2680,7 @@ static int s2c_batch_shard_impl(const s2c_batch *b, int64_t t0, int64_t t1, s2c_
     J.layers_dense = J.layers_built = 0;
     for (int64_t t = 0; t < NT; t++) s->tiles[(size_t)t * S2C_TILE_WORDS + 20] = S2C_LY_NONE;
     mark_runs(s.get());
+    build_dwin(s.get());
     // the shard's share of the workload's aligned bases (by its positions; for reporting)
     J.aligned_bases = I.total_len ? (int64_t)((double)I.aligned_bases * (double)aligned / (double)I.total_len) : 0;
     *out = s.release();
@@ -2711,6 +2731,7 @@ extern "C" int s2c_batch_arrays_get(const s2c_batch *b, s2c_batch_arrays *o) {
     o->wtile = b->wtile.data();
     o->rlist = b->rlist.data();
     o->px = b->px.data();
+    o->dwin = b->dwin.data();
     o->ps = b->ps.data();
     o->lly = b->lly.data();
     o->lpc = b->lpc.data();

@@ -646,7 +646,7 @@ __device__ __forceinline__ void tile_epilogue_fast(const D &d, uint32_t tile, co
 //            each one contiguous range (16-byte LDS-DMA issued by the wave, the source
 //            offset in SGPRs)
 //   2 walk   lane per piece: the parsecigar token walk (:64-81) with the maxdel rule (:210)
-//            → one run record per op word {gpos, q << 11 | len} (q: the run's first base in
+//            → one run record per op word (rec_enc: packed ends, q − start; q: the run's first base in
 //            the LDS planes); coverage and counted '-' runs (D/N/P) into position difference
 //            arrays; the N / '-' chars of SEQ (:212, :217) into the histogram
 //   3 count  lane (word w, g of G = 64 / NWP) takes the records of segments W-kwin .. W — one
@@ -788,7 +788,7 @@ __device__ void x_fix(const uint2 *bql, const uint32_t *xl, uint32_t xd, uint32_
 
 // One piece of a chunk (record P, op words [P.z, oend) in LDS at opl[j + od], its SEQ[0] at
 // LDS plane base 16·P.y + qadj): parsecigar (:64-81) + maxdel (:210) → run records
-// runl[j + rd] (bases: {gpos, q << 11 | len}; others zero); coverage / counted '-' of the
+// runl[j + rd] (bases: rec_enc records; others zero); coverage / counted '-' of the
 // tile part into dV / dD; N / '-' of SEQ via x_fix.  Everything from LDS.
 template <int NWP>
 __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *opl, uint32_t od, uint2 *runl, uint32_t rd,
@@ -852,7 +852,7 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
                 const uint32_t c0 = max(gp, a), c1 = min(gp + len, e_tile);   // the tile's part
                 if (bases) {
                     const uint32_t q = ql + start + (s - kk);
-                    r = make_uint2(gp, (q << 11) | len);
+                    r = rec_enc(gp - (a & ~31u), len, q);
                     if (c1 > c0) {
                         atomicAdd(&dV[c0 - a], 1);
                         atomicSub(&dV[c1 - a], 1);
@@ -974,7 +974,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     // this lane's word reads the records of segments [sa, sb] (start words Ww - K .. Ww)
     const uint32_t sa = wact ? (Ww >= S0 + K ? Ww - K : S0) - S0 : 1u, sb = wact ? Ww - S0 : 0u;
     const uint2 *bql = (const uint2 *)(C.pl + 16);
-    const int32_t W32 = (int32_t)(32 * Ww);
+    const int16_t wbias = (int16_t)(32 * ww + REC_BIAS);     // the word's first position, biased (rec_enc)
+    const v2s wpk = (v2s){wbias, wbias};
+    const uint2 *bqw = bql + ((32 * ww + REC_BIAS) >> 5);    // plane word of query y + wbias, less y >> 5
     // one group's records → carry-save trees of X, Y, Z; NR = 8: weight-8 carries in t8o,
     // NR = 4 (a tail group): weight-4 carries
     auto count_group = [&](const uint2 (&rv)[GS], uint32_t (&t8o)[3], auto nr) {
@@ -986,17 +988,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
             uint2 pa[GS], pb[GS];
 #pragma unroll
             for (int u = h; u < h + 2; u++) {
-                const int32_t s0 = (int32_t)rv[u].x - W32;
-                const int32_t e0 = s0 + (int32_t)(rv[u].y & 0x7FFu);
-                const uint32_t lo = (uint32_t)min(max(s0, 0), 32);
-                const uint32_t nb = (uint32_t)min(max(e0, 0), 32) - lo;
-                uint32_t m;
-                asm("v_bfm_b32 %0, %1, %2" : "=v"(m) : "v"(nb), "v"(lo));   // nb bits at lo (nb < 32)
-                bm[u] = m;
-                fx[u] = (uint32_t)__builtin_amdgcn_sbfe((int32_t)nb, 5, 1);   // all ones iff nb = 32
-                const int32_t b = (int32_t)(rv[u].y >> 11) - s0;
-                sh[u] = (uint32_t)b;
-                const uint2 *pw = bql + (b >> 5);
+                rec_mask(rv[u].x, wpk, bm[u], fx[u]);   // the word's covered bits (rec_enc)
+                sh[u] = rv[u].y;                       // (the funnel shift takes the low 5 bits)
+                const uint2 *pw = bqw + ((int32_t)rv[u].y >> 5);
                 pa[u] = pw[0];
                 pb[u] = pw[1];
             }
@@ -1098,7 +1092,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
             const uint32_t ql = 16u * P.y + qadj;
             if (fl & S2C_PF_SIMPLE) {   // one run of SEQ[0:take] (:64-69)
                 const uint32_t c0 = max(P.x, a), c1 = min(P.x + len, a + n);
-                C.runl[rPre] = len ? make_uint2(P.x, (ql << 11) | len) : make_uint2(0u, 0u);
+                C.runl[rPre] = len ? rec_enc(P.x - 32u * W0, len, ql) : make_uint2(0u, 0u);
                 if (c1 > c0) {
                     atomicAdd(&dV[c0 - a], 1);
                     atomicSub(&dV[c1 - a], 1);
@@ -1126,10 +1120,14 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
         if (acc + add_recs > 255u) flush(ww, ga, GW, wact);
         acc += add_recs;
         const uint32_t rend = NR;
-        auto load_runs = [&](uint2 (&rv)[GS], uint32_t gi) {
-            const uint2 *rb = C.runl + min(cw0 + ga + GW * GS * gi, rend);
+        auto load_runs = [&](uint2 (&rv)[GS], uint32_t gi) {   // (64-bit loads: two records per ds_read2_b64)
+            const unsigned long long *rb = (const unsigned long long *)(C.runl + min(cw0 + ga + GW * GS * gi, rend));
 #pragma unroll
-            for (int u = 0; u < GS; u++) rv[u] = rb[GW * u];
+            for (int u = 0; u < GS; u++) {
+                unsigned long long r = rb[GW * u];
+                asm("" : "+v"(r));   // (kept one 64-bit load: its halves are used as different types)
+                rv[u] = make_uint2((uint32_t)r, (uint32_t)(r >> 32));
+            }
         };
         uint2 ra[GS], rb2[GS];
         if (ngrp) load_runs(ra, 0);
@@ -1602,7 +1600,8 @@ static int check_dev(const s2c_dev *d) {
         return s2c_set_error(S2C_ERR_ARG, "missing piece buffers");
     if (d->n_tiles > 0 && (!d->tiles || !d->rs || !d->wtile || !d->tile_stats || !d->blk_len || !d->out))
         return s2c_set_error(S2C_ERR_ARG, "missing tile / output buffers");
-    if ((d->n_items > 0 && !d->items) || (d->n_dense > 0 && !d->dense)) return s2c_set_error(S2C_ERR_ARG, "missing items");
+    if ((d->n_items > 0 && !d->items) || (d->n_dense > 0 && (!d->dense || !d->dwin)))
+        return s2c_set_error(S2C_ERR_ARG, "missing items");
     if (!d->ibkt || !d->ilong || !d->ilong_n) return s2c_set_error(S2C_ERR_ARG, "missing insertion tables");
     if (d->n_tiles > 0 && !d->ps) return s2c_set_error(S2C_ERR_ARG, "missing piece CSR (ps)");
     {   // k_tile's segments: a window of ≤ 64 words and kwin start words before it

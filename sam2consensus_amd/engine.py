@@ -90,9 +90,11 @@ class Uploader:
         offs, total = self._layout(arrays)
         compute = torch.cuda.current_stream(self.device)
         t0 = time.perf_counter()
-        dev = torch.empty(total, dtype=torch.uint8, device=self.device)   # (on the compute stream)
+        # the allocation on the copy stream (free there in its order: no wait for the compute
+        # stream's queued kernels); the compute stream's use is recorded below
+        with torch.cuda.stream(self.copy_stream):
+            dev = torch.empty(total, dtype=torch.uint8, device=self.device)
         self.timing["alloc"] += time.perf_counter() - t0
-        self.copy_stream.wait_stream(compute)     # the allocation is free on the compute stream
         ends = [o + (max(a.nbytes, 16) + 15) // 16 * 16 for a, o in zip(arrays, offs)]   # (zero pad to 16 bytes)
         ai = 0
         ev = None
@@ -123,13 +125,21 @@ class Uploader:
             self.events[i] = ev
             self.timing["pack"] += t1 - t0
             self.timing["issue"] += time.perf_counter() - t1
-        dev.record_stream(self.copy_stream)
+        dev.record_stream(compute)   # (the kernels read it: not reused before they are done)
         if ev is not None:
             compute.wait_event(ev)
         return [dev[o:o + max(a.nbytes, 16)] for a, o in zip(arrays, offs)], dev
 
 
 _UPLOADERS = {}
+_SIDE = {}
+
+
+def _side_stream(device):
+    """A stream for result copies beside the compute stream (one per device)."""
+    if device not in _SIDE:
+        _SIDE[device] = torch.cuda.Stream(device)
+    return _SIDE[device]
 
 
 def default_uploader(device=None):
@@ -153,7 +163,7 @@ class DeviceBatch:
     copy stream (asynchronous); otherwise each array is copied synchronously."""
 
     ARRAYS = ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile", "rlist", "ps",
-              "lly", "lpc", "lops", "lbq", "lbx", "px")
+              "lly", "lpc", "lops", "lbq", "lbx", "px", "dwin")
 
     def __init__(self, hb, device=None, uploader=None, dense_layers=False):
         self.device = _dev(device) if uploader is None else uploader.device
@@ -229,7 +239,7 @@ class Workspace:
             t0, t1 = tile_range
             hb = db.hb
             keep = lambda a, col: a[(a[:, col] >= t0) & (a[:, col] < t1)] if len(a) else a  # noqa: E731
-            self._sel = {"items": keep(hb.items, 0), "dense": keep(hb.dense, 0),
+            self._sel = {"items": keep(hb.items, 0), "dense": keep(hb.dense, 0), "dwin": keep(hb.dwin, 0),
                          "deep": hb.deep[(hb.deep >= t0) & (hb.deep < t1)]}
             for name, a in self._sel.items():
                 t = _up(np.ascontiguousarray(a).reshape(-1), dev)
@@ -277,6 +287,13 @@ class Workspace:
     def run(self):
         """reads → pileup (+ insertion columns, vote, FASTA bodies) → deep tiles (no host sync)."""
         L.check(lib.s2c_run(C.byref(self.dev), self.stream_handle()))
+
+    def record_done(self):
+        """An event after this workspace's launches so far on the compute stream: ``fetch(done)``
+        then waits for these kernels only, not for later batches queued behind them."""
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.db.device))
+        return ev
 
     # ---- HIP graph of one run (the stage launches replayed without host launch overhead)
     def capture(self):
@@ -326,12 +343,22 @@ class Workspace:
         Lp = self.db.info.padded_len
         return self.counts[: 6 * Lp * 4].view(torch.int32).cpu().numpy().view(np.uint32).reshape(6, Lp)
 
-    def fetch(self):
+    def fetch(self, done=None):
         """Synchronise and copy results: (stats[R,T,4] u64, offs[T*nb+1] u64, out bytes).
+        ``done`` (record_done): wait for that event only and copy on a side stream, so later
+        batches' kernels on the compute stream neither delay nor are delayed by the copies.
 
         stats[r, t] = Σ over reference r's tiles of the device's per-tile statistics
         (tiles never straddle a reference; :352-397 sums)."""
-        torch.cuda.current_stream(self.db.device).synchronize()
+        if done is None:
+            torch.cuda.current_stream(self.db.device).synchronize()
+            return self._fetch()
+        side = _side_stream(self.db.device)
+        side.wait_event(done)
+        with torch.cuda.stream(side):
+            return self._fetch()
+
+    def _fetch(self):
         i = self.db.info
         R, T, nb = i.n_refs, self.T, i.n_tiles
         t0, t1 = self.tile_range if self.tile_range is not None else (0, nb)
@@ -359,6 +386,6 @@ class Workspace:
         lens = np.ascontiguousarray(lens, dtype=np.int64)
         out = bytearray(total)
         buf = (C.c_char * max(total, 1)).from_buffer(out) if total else None
-        L.check(lib.s2c_gather_bodies(raw.ctypes.data, starts.ctypes.data, lens.ctypes.data, len(lens),
+        L.check(lib.s2c_gather_bodies(raw.ctypes.data, raw.nbytes, starts.ctypes.data, lens.ctypes.data, len(lens),
                                       C.addressof(buf) if total else None))
         return stats, offs.astype(np.uint64), bytes(out)

@@ -88,24 +88,43 @@ def _tensor_device(group):
     return torch.device("cpu")
 
 
-def gather_results(fetched, sub, rank, world, T, group=None):
+def gather_results(fetched, sub, rank, world, T, group=None, timing=None):
     """Merge every rank's (stats, offs, out) on rank 0 with tensor collectives: a reduce of
     the stats, an all-gather of (tile range, sizes) (four numbers per rank), then a gather of
     the padded offsets and body bytes to rank 0 only (no other rank holds every body).
-    Returns the whole batch's (stats, offs, out) on rank 0, None elsewhere."""
+    Returns the whole batch's (stats, offs, out) on rank 0, None elsewhere.  ``timing``: a dict
+    that gets this rank's seconds per exchange step (stats_reduce, meta, body_gather, merge;
+    device work synchronised) and the bytes each step moved from this rank."""
+    import time
+
     import torch
     import torch.distributed as dist
 
     stats, offs, out = fetched
     dev = _tensor_device(group)
+
+    def mark(name, t0, nbytes=None):
+        if timing is None:
+            return time.perf_counter()
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        timing[name + "_s"] = timing.get(name + "_s", 0.0) + (t1 - t0)
+        if nbytes is not None:
+            timing[name + "_bytes"] = int(nbytes)
+        return t1
+
+    t0 = mark("start", time.perf_counter())
     st = torch.from_numpy(np.ascontiguousarray(stats).view(np.int64).copy()).to(dev)
     if world > 1:
         dist.reduce(st, dst=0, op=dist.ReduceOp.SUM, group=group)   # record stats of cut references
+    t0 = mark("stats_reduce", t0, st.numel() * 8)
     offs = np.asarray(offs, dtype=np.uint64)
     meta = torch.tensor([sub.t0, sub.t1, len(offs), len(out)], dtype=torch.int64, device=dev)
     metas = [torch.empty_like(meta) for _ in range(world)]
     dist.all_gather(metas, meta, group=group) if world > 1 else metas.__setitem__(0, meta)
     metas = [m.cpu().tolist() for m in metas]
+    t0 = mark("meta", t0, 32)
     mo = max(m[2] for m in metas)
     mb = max(max(m[3] for m in metas), 1)
     o_t = torch.zeros(mo, dtype=torch.int64, device=dev)
@@ -120,13 +139,42 @@ def gather_results(fetched, sub, rank, world, T, group=None):
         dist.gather(b_t, bs_, dst=0, group=group)
     else:
         os_, bs_ = [o_t], [b_t]
+    t0 = mark("body_gather", t0, o_t.numel() * 8 + b_t.numel())
     if rank != 0:
         return None
     parts = []
     for m, o, b in zip(metas, os_, bs_):
         parts.append((m[0], m[1], o[: m[2]].cpu().numpy().view(np.uint64), b[: m[3]].cpu().numpy().tobytes()))
     full_offs, full_out = merge_outputs(parts, T)
-    return st.cpu().numpy().view(np.uint64).reshape(stats.shape), full_offs, full_out
+    res = st.cpu().numpy().view(np.uint64).reshape(stats.shape), full_offs, full_out
+    mark("merge", t0)
+    return res
+
+
+def batch_bytes(hb):
+    """Bytes of a packed batch's device arrays (what its rank uploads to HBM)."""
+    return int(sum(np.asarray(getattr(hb, n)).nbytes for n in
+                   ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile", "rlist", "ps", "px",
+                    "dwin")))
+
+
+def exchange_volumes(full, subs):
+    """What the position split costs in data, from the shards themselves:
+    duplicated pieces / bytes (a read whose runs reach across a cut is in both shards' batches)
+    against what north_star's count-tensor merge would move instead — a reduce-scatter of the
+    u32 counts [6] of the positions that straddling reads cover past each cut (kwin + 1 words
+    on either side: 24 B per position)."""
+    np_full = int(full.info.n_pieces)
+    np_sum = sum(int(s.info.n_pieces) for s in subs)
+    b_full = batch_bytes(full)
+    b_sum = sum(batch_bytes(s) for s in subs)
+    cuts = sum(1 for s in subs[:-1] if s.t1 < full.info.n_tiles)
+    seam_pos = 2 * (int(full.info.kwin) + 1) * 32
+    return {"pieces_total": np_full, "pieces_over_shards": np_sum,
+            "dup_frac": (np_sum / np_full) if np_full else 1.0,
+            "batch_bytes_total": b_full, "batch_bytes_over_shards": b_sum,
+            "dup_bytes": b_sum - b_full,
+            "cuts": cuts, "count_merge_bytes": cuts * seam_pos * 24}
 
 
 def run_sharded(hb, rank, world, thresholds, runner, group=None):

@@ -276,30 +276,38 @@ def stream_batches(blocks, thresholds, runner, maxdel_active=True, tile_width=DE
     clk = time.perf_counter
     tw = clk()
     ranged = getattr(runner, "launch_range", None)
-    for item in _Producer(_sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, state,
-                                        ranged is not None)):
-        ct["wait"] += clk() - tw
-        if item[0] == "last":
-            hb = item[1]
-            break
-        _, sub, t0, t1 = item
-        tl = clk()
-        try:
-            if ranged is not None and getattr(sub, "t0_range", None) is not None:
-                h = ranged(sub, t0, t1)
-            else:
-                sub.t0, sub.t1 = t0, t1
-                h = launch(sub) if launch else runner(sub)
-        except BaseException:
+    try:
+        for item in _Producer(_sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, state,
+                                            ranged is not None)):
+            ct["wait"] += clk() - tw
+            if item[0] == "last":
+                hb = item[1]
+                break
+            _, sub, t0, t1 = item
+            tl = clk()
+            try:
+                if ranged is not None and getattr(sub, "t0_range", None) is not None:
+                    h = ranged(sub, t0, t1)
+                else:
+                    sub.t0, sub.t1 = t0, t1
+                    h = launch(sub) if launch else runner(sub)
+            except BaseException:
+                sub.free()
+                raise
+            ct["launch"] += clk() - tl
+            pend.append((t0, t1, h, sub))
+            tl = clk()
+            while len(pend) > 1:
+                collect(pend.pop(0))
+            ct["collect"] += clk() - tl
+            tw = clk()
+    except BaseException:
+        # (NotSorted, or a reference error: the launched-but-uncollected batches' device
+        # buffers and host snapshots go now, not with the traceback that holds this frame)
+        for _, _, _, sub in pend:
             sub.free()
-            raise
-        ct["launch"] += clk() - tl
-        pend.append((t0, t1, h, sub))
-        tl = clk()
-        while len(pend) > 1:
-            collect(pend.pop(0))
-        ct["collect"] += clk() - tl
-        tw = clk()
+        pend.clear()
+        raise
     tl = clk()
     while pend:
         collect(pend.pop(0))
@@ -523,7 +531,7 @@ class DeviceRunner:
         ws = Workspace(DeviceBatch(sub, uploader=self.up, dense_layers=needs_dense_layers(self.fill)), self.thresholds,
                        self.min_depth, self.fill)
         ws.run()
-        return _Launched(ws)
+        return _Launched(ws, ws.record_done())
 
     def launch_range(self, hb, t0, t1):
         """The tiles [t0, t1) of a snapshot, without cutting a sub-batch (Workspace tile_range)."""
@@ -532,19 +540,22 @@ class DeviceRunner:
                        self.min_depth, self.fill,
                        tile_range=(t0, t1))
         ws.run()
-        return _Launched(ws)
+        return _Launched(ws, ws.record_done())
 
     def __call__(self, sub):
         return self.launch(sub).result()
 
 
 class _Launched:
-    def __init__(self, ws):
-        self.ws = ws
+    """A launched batch: ``result()`` waits for its own kernels (the event recorded after
+    them) and copies its results on a side stream while later batches run."""
+
+    def __init__(self, ws, done=None):
+        self.ws, self.done = ws, done
 
     def result(self):
-        r = self.ws.fetch()
-        self.ws = None
+        r = self.ws.fetch(self.done)
+        self.ws = self.done = None
         return r
 
 
@@ -564,7 +575,9 @@ def consensus_files_streamed(filename, thresholds, prefix, min_depth=1, fill=b"-
     try:
         res = stream_batches(file_blocks(filename), thresholds, device_runner(thresholds, min_depth, fill, device),
                              maxdel_active, tile_width, batch_bytes)
-    except NotSorted:   # counts added batch by batch into running totals in HBM
+    except NotSorted:
+        res = None   # (the second pass runs after the except block: no live traceback of the first)
+    if res is None:   # counts added batch by batch into running totals in HBM
         res = stream_unsorted(file_blocks(filename), thresholds,
                               DeviceAccumulator(thresholds, min_depth, fill, device), maxdel_active, batch_bytes)
     t["stream"] = time.perf_counter() - t0

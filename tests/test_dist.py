@@ -76,6 +76,23 @@ def test_split_is_balanced_and_contiguous():
         assert max(loads) < 1.3 * (sum(loads) / world)
 
 
+def test_exchange_volumes_count_the_duplicated_reads():
+    """shard.exchange_volumes (bench.py's dup_frac): the pieces summed over the
+    shards are at least the workload's and exceed it by the reads reaching across a cut."""
+    hb = configs.synth_batch("c2", n_refs=12)
+    for world in (1, 2, 4):
+        subs = [shard.sub_batch(hb, r, world) for r in range(world)]
+        v = shard.exchange_volumes(hb, subs)
+        assert v["pieces_total"] == hb.info.n_pieces
+        assert v["pieces_over_shards"] >= v["pieces_total"]
+        if world == 1:
+            assert v["dup_frac"] == 1.0 and v["cuts"] == 0 and v["count_merge_bytes"] == 0
+        else:
+            assert 1.0 < v["dup_frac"] < 1.5 and v["cuts"] == world - 1 and v["dup_bytes"] > 0
+        for s_ in subs:
+            s_.free()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -92,9 +109,14 @@ def _worker(rank, world, port, sam, args, q):
     try:
         opt = o.parse_argv(["-i", "in.sam"] + args)
         hb = batch.parse_text(sam, opt.maxdel_active, 150)
-        res = shard.run_sharded(hb, rank, world, opt.thresholds,
-                                lambda sub: bm.model_pipeline(sub, opt.thresholds, opt.min_depth,
-                                                              opt.fill.encode("latin-1")))
+        sub = shard.sub_batch(hb, rank, world)
+        tim = {}
+        res = shard.gather_results(bm.model_pipeline(sub, opt.thresholds, opt.min_depth, opt.fill.encode("latin-1")),
+                                   sub, rank, world, len(opt.thresholds), timing=tim)
+        # every exchange step timed on every rank (bench.py's "exchange" record), merge on rank 0
+        steps = ("stats_reduce", "meta", "body_gather") + (("merge",) if rank == 0 else ())
+        assert all(tim[k + "_s"] >= 0 for k in steps), tim
+        assert tim["body_gather_bytes"] >= 8 and tim["stats_reduce_bytes"] > 0
         if rank == 0:
             q.put(_files(hb, opt, *res))
     finally:

@@ -177,12 +177,26 @@ def test_cli_torchrun_distributed_parse(tmp_path):
     env = dict(os.environ, S2C_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
 
     def torchrun(inp, out, args):
+        # every rank's stdout / stderr kept in its own file (--log-dir, --redirects 3): a failing
+        # rank's traceback is in the assertion, not only the launcher's summary
+        logs = tmp_path / ("logs_" + os.path.basename(str(out)))
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+               "--log-dir", str(logs), "--redirects", "3",
                os.path.join(root, "sam2consensus.py"), "-i", inp, "-o", str(out)] + args
         r = subprocess.run(cmd, env=env, capture_output=True, timeout=240)
-        assert r.returncode == 0, r.stderr.decode()[-2000:]
-        return r.stdout.decode()
+        ranks = {}
+        for dp, _, fns in os.walk(logs):
+            for fn in fns:
+                if fn in ("stdout.log", "stderr.log"):
+                    rank = os.path.basename(dp)
+                    ranks.setdefault(rank, {})[fn] = open(os.path.join(dp, fn), errors="replace").read()
+        if r.returncode != 0:
+            detail = "\n".join("rank %s %s:\n%s" % (k, f, v[-3000:]) for k, d in sorted(ranks.items())
+                               for f, v in sorted(d.items()) if v.strip())
+            raise AssertionError("torchrun exit %d\n%s\nlauncher:\n%s" % (r.returncode, detail,
+                                                                           r.stderr.decode()[-1500:]))
+        return "".join(d.get("stdout.log", "") for _, d in sorted(ranks.items())) + r.stdout.decode()
 
     g = CONFIGS["c1"]
     sam = str(tmp_path / "c1.sam")

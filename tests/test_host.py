@@ -339,15 +339,21 @@ def test_gather_bodies_concatenates_blocks():
         want = b"".join(raw[s:s + L].tobytes() for s, L in zip(starts, lens))
         out = bytearray(max(len(want), 1))
         buf = (C.c_char * len(out)).from_buffer(out)
-        _lib.check(_lib.lib.s2c_gather_bodies(raw.ctypes.data, starts.ctypes.data, lens.ctypes.data, n,
+        _lib.check(_lib.lib.s2c_gather_bodies(raw.ctypes.data, raw.nbytes, starts.ctypes.data, lens.ctypes.data, n,
                                               C.addressof(buf)))
         assert bytes(out[:len(want)]) == want
     zl = np.zeros(3, dtype=np.int64)   # every block empty (e.g. all of a reference's tiles filtered): no output
-    _lib.check(_lib.lib.s2c_gather_bodies(None, zl.ctypes.data, zl.ctypes.data, 3, None))
+    _lib.check(_lib.lib.s2c_gather_bodies(None, 0, zl.ctypes.data, zl.ctypes.data, 3, None))
     bad = np.array([-1], dtype=np.int64)
     with pytest.raises(_lib.S2CError):
-        _lib.check(_lib.lib.s2c_gather_bodies(raw.ctypes.data, bad.ctypes.data, bad.ctypes.data, 1,
+        _lib.check(_lib.lib.s2c_gather_bodies(raw.ctypes.data, raw.nbytes, bad.ctypes.data, bad.ctypes.data, 1,
                                               raw.ctypes.data))
+    # a block past the end of the device output (a length from a faulty kernel): refused
+    st, ln = np.array([raw.size - 10], dtype=np.int64), np.array([11], dtype=np.int64)
+    dst = np.zeros(16, dtype=np.uint8)
+    with pytest.raises(_lib.S2CError):
+        _lib.check(_lib.lib.s2c_gather_bodies(raw.ctypes.data, raw.nbytes, st.ctypes.data, ln.ctypes.data, 1,
+                                              dst.ctypes.data))
 
 
 def test_copy_bytes_matches_memcpy():
@@ -430,7 +436,8 @@ def _host_dev(hb, fill=b"-", counts=False):
     scratch = (C.c_uint8 * 4096)()
     p = C.addressof(scratch)
     d = L.Dev()
-    for name in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile", "rlist", "ps", "px"):
+    for name in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile", "rlist", "ps", "px",
+                 "dwin"):
         setattr(d, name, p)
     d.n_pieces, d.n_ops, d.n_qwords, d.n_tiles = i.n_pieces, i.n_ops, i.n_qwords, i.n_tiles
     d.n_items, d.n_dense, d.n_deep = i.n_items, i.n_dense, i.n_deep
@@ -488,5 +495,24 @@ def test_device_stages_refuse_unbuilt_layers_before_launch():
             assert sb.info.layers_built == 1
         finally:
             sb.free()
+    finally:
+        hb.free()
+
+
+def test_dense_windows_mirror_tile_records():
+    """s2c_batch_arrays.dwin (ABI 10): each dense item's window words are its tile record's
+    (k_tile_dense's one scalar load per tile), in a batch and in its shards."""
+    from sam2consensus_amd import shard
+    hb = configs.synth_batch("c5", ref_len=200_000, ins_frac=0.01)
+    try:
+        for b in [hb] + [shard.sub_batch(hb, r, 3) for r in range(3)]:
+            i = b.info
+            assert b.dwin.shape == (i.n_dense, 16) and i.n_dense > 0
+            t = b.dense[:, 0].astype(np.int64)
+            assert (b.dwin[:, 0] == t).all()
+            assert (b.dwin[:, 1:12] == b.tiles[t][:, [0, 1, 8, 10, 11, 13, 14, 15, 16, 17, 18]]).all()
+            assert not b.dwin[:, 12:].any()
+            if b is not hb:
+                b.free()
     finally:
         hb.free()
