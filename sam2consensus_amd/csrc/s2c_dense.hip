@@ -362,15 +362,25 @@ __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
 
 // 16-bit halves (positions j = 0, 2 / j = 1, 3) of a register of 4 byte counts
 __device__ __forceinline__ uint32_t lo16(uint32_t v) { return v & 0x00FF00FFu; }
-__device__ __forceinline__ uint32_t hi16(uint32_t v) { return (v >> 8) & 0x00FF00FFu; }
+__device__ __forceinline__ uint32_t hi16(uint32_t v) { return __builtin_amdgcn_perm(0u, v, 0x0C030C01u); }
 // the low bytes of the halves of e (j = 0, 2) and o (j = 1, 3) back into j order
 __device__ __forceinline__ uint32_t merge16(uint32_t o, uint32_t e) { return __builtin_amdgcn_perm(o, e, 0x06020400u); }
+// ... and their high bytes
+__device__ __forceinline__ uint32_t merge16h(uint32_t o, uint32_t e) { return __builtin_amdgcn_perm(o, e, 0x07030501u); }
+// vote keys count << 8 | symbol in the 16-bit halves of byte counts c (one byte permute each;
+// sb = symbol · 0x01010101): e = positions j = 0, 2, o = j = 1, 3
+__device__ __forceinline__ uint32_t key_e(uint32_t c, uint32_t sb) { return __builtin_amdgcn_perm(sb, c, 0x02040004u); }
+__device__ __forceinline__ uint32_t key_o(uint32_t c, uint32_t sb) { return __builtin_amdgcn_perm(sb, c, 0x03040104u); }
 typedef unsigned short v2u __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(v2u, a), __builtin_bit_cast(v2u, b)));
 }
 __device__ __forceinline__ uint32_t pk_sub(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2u, a) - __builtin_bit_cast(v2u, b));
+}
+template <int S>
+__device__ __forceinline__ uint32_t pk_shr(uint32_t a) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2u, a) >> (v2u){S, S});
 }
 // 0xFFFF in each half whose bit 15 is set
 __device__ __forceinline__ uint32_t pk_sign(uint32_t a) {
@@ -917,24 +927,26 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         inb[rr] = im;
         cvb[rr] = cv;
         sc = __builtin_amdgcn_udot4(cv & im, 0x01010101u, sc, false);   // Σ cov over the tile (:357)
-        // keys count << 3 | symbol ("-ACGNT" index), halves e (j = 0, 2) and o (j = 1, 3)
+        // keys count << 8 | symbol ("-ACGNT" index), halves e (j = 0, 2) and o (j = 1, 3); the
+        // largest key's symbol is the char wherever the count is a strict majority (elsewhere
+        // the tie order does not matter: fill, or the closed form below)
         const uint32_t cnt[NSYM] = {rD[rr], cA, cC, rG[rr], rN[rr], rT[rr]};
-        uint32_t ke = 0, ko = 0;
+        uint32_t ke = key_e(cnt[0], 0u), ko = key_o(cnt[0], 0u);
 #pragma unroll
-        for (uint32_t s = 0; s < NSYM; s++) {
-            ke = pk_max(ke, (lo16(cnt[s]) << 3) | (s * 0x00010001u));
-            ko = pk_max(ko, (hi16(cnt[s]) << 3) | (s * 0x00010001u));
+        for (uint32_t s = 1; s < NSYM; s++) {
+            ke = pk_max(ke, key_e(cnt[s], s * 0x01010101u));
+            ko = pk_max(ko, key_o(cnt[s], s * 0x01010101u));
         }
         const uint32_t ce = lo16(cv), co = hi16(cv);
-        // strict majority 2·m1 > cov ⟺ 8·m1 − 4·cov > 0: the half's bit 15 of 4·cov − 8·m1
-        const uint32_t mje = pk_sign(pk_sub(ce << 2, ke & 0xFFF8FFF8u)), mjo = pk_sign(pk_sub(co << 2, ko & 0xFFF8FFF8u));
+        // strict majority 2·m1 > cov: the half's bit 15 of cov − 2·m1 (key >> 7 = 2·m1)
+        const uint32_t mje = pk_sign(pk_sub(ce, pk_shr<7>(ke))), mjo = pk_sign(pk_sub(co, pk_shr<7>(ko)));
         // not called: cov < md
         const uint32_t nce = pk_sign(pk_sub(ce, md16)), nco = pk_sign(pk_sub(co, md16));
-        const uint32_t sym = merge16(ko & 0x00070007u, ke & 0x00070007u);
+        const uint32_t sym = merge16(ko, ke);
         chr[rr] = __builtin_amdgcn_perm(0x0000544Eu, 0x4743412Du, sym);   // "-ACGNT"[sym]
         fmk[rr] = merge16(mjo, mje);
         ncm[rr] = merge16(nco, nce) | ~im;
-        m1b[rr] = merge16(ko >> 3, ke >> 3);
+        m1b[rr] = merge16h(ko, ke);
     }
     const uint32_t fill4 = fill0 * 0x01010101u;
     const uint64_t ostride = (uint64_t)d.padded_len + d.n_cols;   // max(1, len(fill)) = 1
@@ -960,10 +972,11 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         for (int rr = 0; rr < RPL; rr++) {
             uint32_t fm = (clsA || clsB) ? fmk[rr] & ~ncm[rr] : 0u;
             if (clsB) {   // m1·2^15 ≥ uq·cov per position (m1, cov ≤ 255: 32-bit products)
-                uint32_t ok = 0;
+                uint32_t ok = 0, mb = m1b[rr], cb = cvb[rr];
+                asm volatile("" : "+v"(mb), "+v"(cb));   // (kept here: not hoisted for every class)
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    const uint32_t m1 = (m1b[rr] >> (8 * j)) & 0xFFu, cv = (cvb[rr] >> (8 * j)) & 0xFFu;
+                    const uint32_t m1 = (mb >> (8 * j)) & 0xFFu, cv = (cb >> (8 * j)) & 0xFFu;
                     ok |= (m1 << 15) >= uq * cv ? (0xFFu << (8 * j)) : 0u;
                 }
                 fm &= ok;
@@ -1027,12 +1040,14 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             } else if (full) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) *(uint2 *)(dst + 8 * j) = make_uint2(cj[j], c2[j]);
-            } else if (active) {
+            } else if (active) {   // (the tile's last word; bounds kept here, not hoisted)
+                uint32_t nn = n - 32 * w;
+                asm volatile("" : "+v"(nn));
 #pragma unroll
                 for (int j = 0; j < 4; j++)
 #pragma unroll
                     for (int b = 0; b < 8; b++)
-                        if (32 * w + 8 * j + b < n) dst[8 * j + b] = (uint8_t)((b < 4 ? cj[j] : c2[j]) >> (8 * (b & 3)));
+                        if (8 * j + b < nn) dst[8 * j + b] = (uint8_t)((b < 4 ? cj[j] : c2[j]) >> (8 * (b & 3)));
             }
         } else {
             tr4(ow[0], RPL > 1 ? ow[1 % RPL] : 0u, RPL > 2 ? ow[2 % RPL] : 0u, RPL > 3 ? ow[3 % RPL] : 0u, cj);
@@ -1056,12 +1071,14 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
                     else if constexpr (RPL == 2) *(uint16_t *)(dst + 8 * j) = (uint16_t)cj[j];
                     else dst[8 * j] = (uint8_t)cj[j];
                 }
-            } else if (active) {
+            } else if (active) {   // (the tile's last word; bounds kept here, not hoisted)
+                uint32_t nn = n - 32 * w - g * RPL;
+                asm volatile("" : "+v"(nn));
 #pragma unroll
                 for (int j = 0; j < 4; j++)
 #pragma unroll
                     for (int b = 0; b < RPL; b++)
-                        if (32 * w + 8 * j + g * RPL + b < n) dst[8 * j + b] = (uint8_t)(cj[j] >> (8 * b));
+                        if ((int32_t)(8 * j + b) < (int32_t)nn) dst[8 * j + b] = (uint8_t)(cj[j] >> (8 * b));
             }
         }
         if (t == 0) sc = wave_sum(sc);

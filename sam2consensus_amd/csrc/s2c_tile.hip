@@ -32,6 +32,8 @@ int s2c_launch_dense(const s2c_dev *d, hipStream_t s);
 // phase clocks of k_tile (diagnostic build `make prof`, scripts/prof_tile.py): Σ over sampled
 // workgroups (one in 16, wave 0) of the s_memtime deltas of each phase; [15] = workgroups
 __device__ unsigned long long g_tprof[16];
+__device__ uint32_t g_tabl;   // ablation bits (timing only; results wrong): 1 walk, 2 count, 4 flush atomics
+#define TABL(b) ((g_tabl & (b)) != 0)
 #define TPROF_MARK(i)                                                                                 \
     do {                                                                                              \
         const unsigned long long _t = __builtin_amdgcn_s_memtime();                                   \
@@ -46,7 +48,11 @@ extern "C" int s2c_prof_tile(unsigned long long *out, int reset) {
     }
     return 0;
 }
+extern "C" int s2c_prof_tile_ablate(uint32_t bits) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_tabl), &bits, sizeof(bits)) == hipSuccess ? 0 : -1;
+}
 #else
+#define TABL(b) false
 #define TPROF_MARK(i) \
     do {              \
     } while (0)
@@ -946,7 +952,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
                 for (int r = 0; r < 8; r++) { shr2(X[r]); shr2(Y[r]); shr2(Z[r]); }
             }
         }
-        if (act && (gg % red) == red - 1) {
+        if (act && (gg % red) == red - 1 && !TABL(4)) {
             uint32_t *h0 = hist + 17 * wd;
             auto add = [&](uint32_t sym, const uint32_t (&R)[8]) {
                 uint32_t *hw = h0 + sym * HP;
@@ -1084,9 +1090,11 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
             for (uint32_t sg = lane; sg <= NS; sg += 64) C.segR[sg] = 0;
         wave_lds_sync();   // (the piece records are read before run records overwrite them)
         for (uint32_t i = lane; i < RPAD; i += 64) C.runl[NR + i] = make_uint2(0u, 0u);
+        if (TABL(1))   // (ablated walk: zero records)
+            for (uint32_t i = lane; i < NR; i += 64) C.runl[i] = make_uint2(0u, 0u);
 #pragma unroll
         for (int u = 0; u < 2; u++) {
-            if (lane + 64 * u >= NPc) continue;
+            if (lane + 64 * u >= NPc || TABL(1)) continue;
             const uint4 P = Pw[u];
             const uint32_t fl = P.w >> 24, len = P.w & 0xFFFFFFu, rPre = P.z - O0;
             const uint32_t ql = 16u * P.y + qadj;
@@ -1113,7 +1121,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
         //      pieces starting after Ww, or the zero pad — they cover nothing of Ww)
         const uint32_t cw0 = C.segR[sa], cw1 = C.segR[sb + 1];
         const uint32_t nrec = cw0 + ga < cw1 ? (cw1 - cw0 - ga + GW - 1) / GW : 0u;
-        const uint32_t nmx = uni(__ockl_wfred_max_u32(nrec));
+        const uint32_t nmx = TABL(2) ? 0u : uni(__ockl_wfred_max_u32(nrec));
         const uint32_t ngrp = nmx / GS + ((nmx % GS) > 4u ? 1u : 0u);
         const bool half = (nmx % GS) != 0u && (nmx % GS) <= 4u;
         const uint32_t add_recs = GS * ngrp + (half ? 4u : 0u);

@@ -24,6 +24,9 @@ thr = [float(x) for x in args[args.index("-c") + 1].split(",")] if "-c" in args 
 ws = Workspace(DeviceBatch(hb), thr, int(args[args.index("-m") + 1]) if "-m" in args else 1, b"-")
 f = _lib.lib.s2c_prof_tile
 f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+abl = _lib.lib.s2c_prof_tile_ablate   # (1 walk, 2 count, 4 flush atomics; timing only)
+abl.argtypes = [C.c_uint32]
+abl(int(sys.argv[2]) if len(sys.argv) > 2 else 0)
 buf = (C.c_ulonglong * 16)()
 ws.run()
 torch.cuda.synchronize()
