@@ -779,20 +779,26 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     // two groups per trip (ping-pong record buffers; the next group's records are read while
     // this group's plane words are in flight), their weight-8 carries closed together
     uint2 ra[GSD], rb2[GSD];
-    if (ngrp) load_runs(ra, 0);
-    for (uint32_t gi = 0; gi < ngrp; gi += 2) {
+    auto trip = [&](uint32_t gi) -> bool {   // groups gi, gi + 1; false: the last group counted
         uint32_t t8a[4], t8b[4];
         if (gi + 1 < ngrp) load_runs(rb2, gi + 1);
         count_group(ra, t8a, Full{});
         if (gi + 1 >= ngrp) {
 #pragma unroll
             for (int c = 0; c < 4; c++) close8(C[c], t8a[c]);
-            break;
+            return false;
         }
         if (gi + 2 < ngrp) load_runs(ra, gi + 2);
         count_group(rb2, t8b, Full{});
 #pragma unroll
         for (int c = 0; c < 4; c++) close16(C[c], t8a[c], t8b[c]);
+        return true;
+    };
+    if (ngrp) {   // the first trip peeled: its counters start at zero (folded, no initialising moves)
+        load_runs(ra, 0);
+        if (trip(0))
+            for (uint32_t gi = 2; gi < ngrp; gi += 2)
+                if (!trip(gi)) break;
     }
     if (half) {   // records 8·ngrp .. 8·ngrp + 3 of each lane
         uint32_t t4[4];
