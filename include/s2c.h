@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define S2C_ABI_VERSION 10
+#define S2C_ABI_VERSION 11
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define S2C_OK            0
@@ -323,6 +323,8 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
     const uint32_t *lbx;       /* [n_lqwords] */
     const uint32_t *px;        /* [n_pieces] the non-ACGT SEQ offsets of S2C_PF_XFEW pieces (else 0xFFFFFFFF) */
     const uint32_t *dwin;      /* [n_dense][S2C_DWIN_WORDS] the dense items' windows */
+    const uint32_t *lpx;       /* [n_lpieces] px of the layered pieces (ABI 11: k_tile takes the 'N' of
+                                  S2C_PF_XFEW pieces from here instead of scanning the non-ACGT plane) */
 } s2c_batch_arrays;
 
 /* Build the batch's layered windows (s2c_batch_arrays lly .. lbx, tile word 20) if not yet
@@ -423,6 +425,7 @@ typedef struct {
     const uint32_t *px;        /* [n_pieces] s2c_batch_arrays.px (ABI 10) */
     int64_t   layers_built;    /* the batch's info.layers_built: every launch with work items refuses 0 */
     const uint32_t *dwin;      /* [n_dense][S2C_DWIN_WORDS] s2c_batch_arrays.dwin, filtered like dense */
+    const uint32_t *lpx;       /* [n_lpieces] s2c_batch_arrays.lpx (ABI 11; required with n_layers > 0) */
 } s2c_dev;
 
 /* Sizes (bytes) of every workspace / output buffer for a batch and T thresholds. */

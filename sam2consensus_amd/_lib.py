@@ -67,7 +67,7 @@ _P32 = C.POINTER(C.c_uint32)
 class BatchArrays(C.Structure):
     _fields_ = [("ref_len", _P64), ("ref_off", _P64), ("ref_cov_reads", _P64)] + \
         [(n, _P32) for n in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "rlist", "lp", "wtile",
-                             "ps", "lly", "lpc", "lops", "lbq", "lbx", "px", "dwin")]
+                             "ps", "lly", "lpc", "lops", "lbq", "lbx", "px", "dwin", "lpx")]
 
 
 class SynthSpec(C.Structure):
@@ -95,7 +95,7 @@ class Dev(C.Structure):
         ("runs", _VP), ("ibkt", _VP), ("ilong", _VP), ("ilong_n", _VP), ("counts", _VP),
         ("ins_cols", _VP), ("ins_chr", _VP), ("n_cols", C.c_int64),
         ("tile_stats", _VP), ("blk_len", _VP), ("out", _VP), ("out_cap", C.c_int64), ("layers_dense", C.c_int64),
-        ("px", _VP), ("layers_built", C.c_int64), ("dwin", _VP)]
+        ("px", _VP), ("layers_built", C.c_int64), ("dwin", _VP), ("lpx", _VP)]
 
 
 class WsSizes(C.Structure):

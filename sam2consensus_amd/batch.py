@@ -132,6 +132,7 @@ class HostBatch:
         self.lops = _view(a.lops, max(i.n_lops, 4), np.uint32)
         self.lbq = _view(a.lbq, 2 * i.n_lqwords, np.uint32).reshape(-1, 2)
         self.lbx = _view(a.lbx, i.n_lqwords, np.uint32)
+        self.lpx = _view(a.lpx, max(i.n_lpieces, 1), np.uint32)   # px of the layered pieces
         self._layers = True
         return self
 

@@ -279,6 +279,7 @@ struct s2c_batch {
     u32buf pc, ops, bq, bx;   // filled entirely by the emitters (resize: no zero-fill)
     std::vector<uint32_t> rs, tiles, items, dense, deep, lp, wtile, rlist, ps;
     std::vector<uint32_t> lly, lpc, lops, lbq, lbx;   // layered windows of the non-dense tiles
+    std::vector<uint32_t> lpx;                        // [n_lpieces] px of the layered pieces
     bool layers = false;                               // built (s2c_batch_layers)
     u32buf kmin, kmax;   // host only: global key range of each piece's insertion events
     u32buf px;           // [pieces] the non-ACGT SEQ offsets of S2C_PF_XFEW pieces (s2c.h)
@@ -1390,6 +1391,7 @@ static void build_layers(s2c_batch *b, int64_t G, bool with_dense) {
     b->lops.assign(std::max<int64_t>(I.n_lops, 4), 0u);
     b->lbq.assign(2 * (size_t)I.n_lqwords, 0u);
     b->lbx.assign((size_t)I.n_lqwords, 0u);
+    b->lpx.assign(std::max<int64_t>(I.n_lpieces, 1), 0xFFFFFFFFu);
     {
         uint32_t *sp = &b->lpc[4 * (size_t)I.n_lpieces];   // sentinel
         sp[1] = (uint32_t)lyh.back();
@@ -1417,6 +1419,7 @@ static void build_layers(s2c_batch *b, int64_t G, bool with_dense) {
                         dp[1] = (uint32_t)kh;
                         dp[2] = (uint32_t)ko;
                         dp[3] = pr[3];
+                        b->lpx[kp] = b->px[k];
                         memcpy(&b->lops[ko], &b->ops[pr[2]], 4 * (size_t)no);
                         for (uint32_t h = 0; h < nh; h++) {
                             const uint64_t a = (uint64_t)pr[1] + h, d = kh + h;
@@ -2738,6 +2741,7 @@ extern "C" int s2c_batch_arrays_get(const s2c_batch *b, s2c_batch_arrays *o) {
     o->lops = b->lops.data();
     o->lbq = b->lbq.data();
     o->lbx = b->lbx.data();
+    o->lpx = b->lpx.empty() ? nullptr : b->lpx.data();
     return S2C_OK;
 }
 

@@ -33,7 +33,7 @@ int s2c_launch_dense(const s2c_dev *d, hipStream_t s);
 // workgroups (one in 16, wave 0) of the s_memtime deltas of each phase; [15] = workgroups
 __device__ unsigned long long g_tprof[16];
 __device__ uint32_t g_tabl;   // ablation bits (timing only; results wrong): 1 walk, 2 count, 4 flush atomics
-#define TABL(b) ((g_tabl & (b)) != 0)
+#define TABL(b) ((tabl & (b)) != 0)   // (tabl: g_tabl read once per workgroup)
 #define TPROF_MARK(i)                                                                                 \
     do {                                                                                              \
         const unsigned long long _t = __builtin_amdgcn_s_memtime();                                   \
@@ -85,6 +85,7 @@ constexpr uint32_t MODE_RUN = 0, MODE_STORE = 1, MODE_ADD = 2, MODE_ADD_KEEP = 3
 struct TileArgs {
     const uint32_t *rs, *runs, *bq, *bx, *tiles, *lp, *pc, *ops, *ps;
     const uint32_t *lly, *lpc, *lops, *lbq, *lbx;
+    const uint32_t *px, *lpx;   // S2C_PF_XFEW offsets of the pieces / of the layered pieces
     const void *bq_end, *bx_end, *ops_end, *pc_end;      // ends of the DMA sources (buffer ranges)
     const void *lbq_end, *lbx_end, *lops_end, *lpc_end;
     uint32_t maxdel_active, maxdel;
@@ -892,6 +893,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     __shared__ __attribute__((aligned(16))) TileLds<ICOL> U;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
 #ifdef S2C_PROF
+    const uint32_t tabl = uni(*(volatile uint32_t *)&g_tabl);
+#endif
+#ifdef S2C_PROF
     unsigned long long tprof_t = 0;
 #endif
     TPROF_MARK(0);
@@ -1040,6 +1044,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     const bool inplace = ly0 == S2C_LY_MAIN;
     const uint32_t *const spc = inplace ? d.pc : d.lpc, *const sops = inplace ? d.ops : d.lops;
     const uint32_t *const sbq = inplace ? d.bq : d.lbq, *const sbx = inplace ? d.bx : d.lbx;
+    const uint32_t *const spx = inplace ? d.px : d.lpx;
     const DmaSrc Dpc = dma_src(spc, inplace ? d.pc_end : d.lpc_end), Dops = dma_src(sops, inplace ? d.ops_end : d.lops_end);
     const DmaSrc Dbq = dma_src(sbq, inplace ? d.bq_end : d.lbq_end), Dbx = dma_src(sbx, inplace ? d.bx_end : d.lbx_end);
     const uint32_t *const xl = (const uint32_t *)C.xl;
@@ -1062,6 +1067,10 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
         dma16_wave(C.ol, Dops, sops + O0, NR);
         dma16_wave(C.pl + 16, Dbq, sbq + 2 * (size_t)qa, 2 * (qb - qa));
         dma16_wave(C.xl, Dbx, sbx + qa, qb - qa);
+        // the lane's pieces' 'N' offsets (S2C_PF_XFEW), with the DMA
+        uint32_t pxr[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) pxr[u] = lane + 64 * u < NPc ? spx[P0 + lane + 64 * u] : 0xFFFFFFFFu;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the wave's own DMA: its LDS reads see it)
         TPROF_MARK(2);
         // ---- 2. walk: lane per piece (records to registers first: their region becomes the
@@ -1102,10 +1111,20 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
                 const uint32_t c0 = max(P.x, a), c1 = min(P.x + len, a + n);
                 C.runl[rPre] = len ? rec_enc(P.x - 32u * W0, len, ql) : make_uint2(0u, 0u);
                 if (c1 > c0) {
+#ifndef S2C_ABL_DV   // (timing-only variant: no coverage difference updates)
                     atomicAdd(&dV[c0 - a], 1);
                     atomicSub(&dV[c1 - a], 1);
+#endif
 #ifndef S2C_ABL_X
-                    if (fl & S2C_PF_X) x_fix<NWP>(bql, xl, xd, ql + (c0 - P.x), c1 - c0, c0 - a, false, hist);
+                    if (fl & S2C_PF_XFEW) {   // ≤ 2 'N' at SEQ offsets px (host-listed): no plane scan
+#pragma unroll
+                        for (int h = 0; h < 2; h++) {
+                            const uint32_t off = (pxr[u] >> (16 * h)) & 0xFFFFu, p = P.x + off;   // (0xFFFF: none)
+                            if (off != 0xFFFFu && p >= c0 && p < c1) H::add1(hist, SL_N, p - a, 1u);
+                        }
+                    } else if (fl & S2C_PF_X) {
+                        x_fix<NWP>(bql, xl, xd, ql + (c0 - P.x), c1 - c0, c0 - a, false, hist);
+                    }
 #endif
                 }
             } else if (fl & S2C_PF_LONG) {   // (its runs come through the tile long lists)
@@ -1535,6 +1554,7 @@ TileArgs tile_args(const s2c_dev &d) {
     p.pc = d.pc; p.ops = d.ops; p.ps = d.ps; p.bq_end = d.bq + 2 * d.n_qwords; p.bx_end = d.bx + d.n_qwords;
     p.ops_end = d.ops + std::max<int64_t>(d.n_ops, 1); p.pc_end = d.pc + 4 * (d.n_pieces + 1);
     p.lly = d.lly; p.lpc = d.lpc; p.lops = d.lops; p.lbq = d.lbq; p.lbx = d.lbx;
+    p.px = d.px; p.lpx = d.lpx;
     p.lbq_end = d.lbq + 2 * d.n_lqwords; p.lbx_end = d.lbx + d.n_lqwords;
     p.lops_end = d.lops + std::max<int64_t>(d.n_lops, 4); p.lpc_end = d.lpc + 4 * (d.n_lpieces + 1);
     p.maxdel_active = d.maxdel_active ? 1u : 0u;
@@ -1598,7 +1618,7 @@ static int check_dev(const s2c_dev *d) {
     if (16 * d->n_ops >= 0xE0000000ll || 8 * d->n_qwords >= 0xE0000000ll || 16 * d->n_pieces >= 0xE0000000ll ||
         8 * d->n_lqwords >= 0xE0000000ll || 16 * d->n_lpieces >= 0xE0000000ll || 4 * d->n_lops >= 0xE0000000ll)
         return s2c_set_error(S2C_ERR_LIMIT, "run records, pieces or base planes beyond 3.5 GB (split the input)");   // 32-bit buffer offsets
-    if (d->n_layers > 0 && (!d->lly || !d->lpc || !d->lops || !d->lbq || !d->lbx))
+    if (d->n_layers > 0 && (!d->lly || !d->lpc || !d->lops || !d->lbq || !d->lbx || !d->lpx))
         return s2c_set_error(S2C_ERR_ARG, "missing layered windows");
     // k_tile reads every work item's tile through its layered windows (tile word 20): a batch
     // whose layers were never built (e.g. a fresh s2c_batch_shard) holds no valid ones

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
     assert declared <= exported, declared - exported
     assert declared == set(_lib.EXPORTS)
-    assert _lib.lib.s2c_abi_version() == 10
+    assert _lib.lib.s2c_abi_version() == 11
 
 
 def _model_case(sam, args):
@@ -402,7 +402,7 @@ def test_layers_without_dense_tiles():
 
 
 def test_xfew_lists_the_n_offsets():
-    """S2C_PF_XFEW + px (ABI 10): a read whose SEQ holds one or two 'N' (and no '-') lists their
+    """S2C_PF_XFEW + px (ABI 10; the layered copies carry it too, ABI 11): a read whose SEQ holds one or two 'N' (and no '-') lists their
     SEQ offsets, so the dense kernel adds its 'N' counts through the runs without scanning the
     non-ACGT plane; three non-ACGT chars, or any '-', leave the flag off (the plane scan)."""
     from sam2consensus_amd import _lib as L
@@ -427,6 +427,28 @@ def test_xfew_lists_the_n_offsets():
         hb.free()
 
 
+def test_layered_pieces_carry_their_px():
+    """s2c_batch_arrays.lpx (ABI 11): every layered copy of a piece carries the piece's px, so
+    k_tile adds the 'N' of S2C_PF_XFEW pieces from the listed offsets (no plane scan): a copy's
+    (gpos, flags | len, px) is one of the originals', and px is 0xFFFFFFFF exactly when the copy
+    is not flagged."""
+    from sam2consensus_amd import _lib as L
+    hb = configs.synth_batch("c2", scale=0.05)
+    try:
+        hb.ensure_layers(False)
+        assert hb.info.n_lpieces > 0
+        n = int(hb.info.n_lpieces)
+        lp = hb.lpc[:n]
+        lpx = hb.lpx[:n]
+        flagged = ((lp[:, 3] >> 24) & L.S2C_PF_XFEW) != 0
+        assert flagged.any() and (~flagged).any()
+        assert (lpx[~flagged] == 0xFFFFFFFF).all() and (lpx[flagged] != 0xFFFFFFFF).all()
+        orig = set(zip(hb.pc[:-1, 0].tolist(), hb.pc[:-1, 3].tolist(), hb.px[: int(hb.info.n_pieces)].tolist()))
+        assert set(zip(lp[:, 0].tolist(), lp[:, 3].tolist(), lpx.tolist())) <= orig
+    finally:
+        hb.free()
+
+
 def _host_dev(hb, fill=b"-", counts=False):
     """An s2c_dev over host pointers (never dereferenced: the calls below must return before
     any launch) with the batch's shapes, as a caller of the C-ABI would fill it."""
@@ -437,7 +459,7 @@ def _host_dev(hb, fill=b"-", counts=False):
     p = C.addressof(scratch)
     d = L.Dev()
     for name in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile", "rlist", "ps", "px",
-                 "dwin"):
+                 "dwin", "lly", "lpc", "lops", "lbq", "lbx", "lpx"):
         setattr(d, name, p)
     d.n_pieces, d.n_ops, d.n_qwords, d.n_tiles = i.n_pieces, i.n_ops, i.n_qwords, i.n_tiles
     d.n_items, d.n_dense, d.n_deep = i.n_items, i.n_dense, i.n_deep
