@@ -260,11 +260,11 @@ def main(argv=None):
     else:
         prefix = args.prefix
     outfolder = args.outfolder.rstrip("/")                                       # :127-130
-    if not os.path.exists(outfolder):
+    world, rank, _ = _dist_env()
+    if rank == 0 and not os.path.exists(outfolder):   # (one process creates it: rank 0 writes the files)
         os.makedirs(outfolder)
     outfolder += "/"
     maxdel_active = not isinstance(args.maxdel, str)
-    world, rank, _ = _dist_env()
     if rank == 0:
         print("\nProcessing file " + filename + ":\n")
     if world > 1:

@@ -1458,9 +1458,8 @@ static int64_t item_layers() {
     }();
     return il;
 }
-static int64_t plan_items(const s2c_batch *b, int64_t K, uint64_t a, uint64_t e, int64_t nl) {
+static int64_t plan_items(const s2c_batch *b, int64_t K, uint64_t a, uint64_t e, int64_t nl, int64_t IL) {
     const int64_t W0 = (int64_t)(a >> 5), W1 = (int64_t)((e + 31) >> 5), S0 = std::max<int64_t>(W0 - K, 0);
-    const int64_t IL = item_layers();
     int64_t nch = nl > 2 * IL ? (nl + IL - 1) / IL : 1;
     for (;; nch++) {
         bool ok = true;
@@ -1518,20 +1517,38 @@ static bool read_extent(const Chunk &c, const ReadRec &r, int64_t off, int64_t L
 
 static int build_batch(s2c_parser *p, s2c_batch **out);
 
+// pred(chunk, read, ref_off) of every read held in chunks [c0, end), on the host threads (the
+// streamed batches' per-read tests: a few ms per million reads instead of tens): flags in
+// chunk-then-read order
+template <class Pred>
+static std::vector<uint8_t> read_flags(const s2c_parser *p, size_t c0, const std::vector<int64_t> &off, Pred &&pred) {
+    const size_t nc = p->chunks.size() > c0 ? p->chunks.size() - c0 : 0;
+    std::vector<int64_t> base(nc + 1, 0);
+    for (size_t i = 0; i < nc; i++) base[i + 1] = base[i] + (int64_t)p->chunks[c0 + i]->reads.size();
+    const int64_t n = base[nc];
+    std::vector<uint8_t> f((size_t)n, 0);
+    par_ranges(plan_threads(n, 1 << 15), n, [&](int, int64_t i0, int64_t i1) {
+        if (i0 >= i1) return;
+        size_t ci = (size_t)(std::upper_bound(base.begin(), base.end(), i0) - base.begin()) - 1;
+        for (int64_t i = i0; i < i1; i++) {
+            while (i >= base[ci + 1]) ci++;
+            const Chunk &c = *p->chunks[c0 + ci];
+            const ReadRec &r = c.reads[(size_t)(i - base[ci])];
+            f[(size_t)i] = pred(c, r, off[r.ref]) ? 1 : 0;
+        }
+    });
+    return f;
+}
+
 // Whether a read parsed since the last retain reaches below its frontier.
 static void check_late(s2c_parser *p) {
     if (p->frontier <= 0 || p->late) return;
     const std::vector<int64_t> off = ref_offsets(p, nullptr);
-    for (size_t ci = p->n_kept; ci < p->chunks.size(); ci++) {
-        const Chunk &c = *p->chunks[ci];
-        for (const ReadRec &r : c.reads) {
-            int64_t lo, hi;
-            if (read_extent(c, r, off[r.ref], p->ref_len[r.ref], &lo, &hi) && lo < p->frontier) {
-                p->late = true;
-                return;
-            }
-        }
-    }
+    const std::vector<uint8_t> f = read_flags(p, p->n_kept, off, [&](const Chunk &c, const ReadRec &r, int64_t o) {
+        int64_t lo, hi;
+        return read_extent(c, r, o, p->ref_len[r.ref], &lo, &hi) && lo < p->frontier;
+    });
+    p->late = std::find(f.begin(), f.end(), (uint8_t)1) != f.end();
 }
 
 static int s2c_parser_finish_impl(s2c_parser *p, s2c_batch **out) {
@@ -1612,10 +1629,12 @@ static void append_read(Chunk &d, const Chunk &c, const ReadRec &r, bool events_
 template <class Keep>
 static void compact_reads(s2c_parser *p, Keep keep, bool events_only) {
     const std::vector<int64_t> off = ref_offsets(p, nullptr);
+    const std::vector<uint8_t> f = read_flags(p, 0, off, keep);   // (the tests in parallel, the copies in order)
     std::unique_ptr<Chunk> k(new Chunk());
+    size_t i = 0;
     for (auto &cp : p->chunks)
         for (const ReadRec &r : cp->reads)
-            if (keep(*cp, r, off[r.ref])) append_read(*k, *cp, r, events_only);
+            if (f[i++]) append_read(*k, *cp, r, events_only);
     p->chunks.clear();
     p->chunks.push_back(std::move(k));
     p->chunks.emplace_back(new Chunk());   // the sequential feed appends here
@@ -2429,12 +2448,51 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
             const int64_t nl = plan_layers(b, PB, K, (uint64_t)T.a, (uint64_t)T.b, G);
             t_nl[t] = nl;
             if (nl <= 0) { too_big = true; continue; }
-            t_nch[t] = plan_items(b, K, (uint64_t)T.a, (uint64_t)T.b, nl);
+            t_nch[t] = plan_items(b, K, (uint64_t)T.a, (uint64_t)T.b, nl, item_layers());
             t_wruns[t] = (int64_t)b->rs[w1] - (int64_t)b->rs[std::max<int64_t>(w0 - K, 0)];
             tile_window(b, K, T.a, T.b, &b->tiles[(size_t)t * S2C_TILE_WORDS]);
         }
     });
     if (too_big) return s2c_set_error(S2C_ERR_LIMIT, "a read whose SEQ or CIGAR exceeds k_tile's LDS chunk");
+    // the dense class, as the loop below decides it (only single-item tiles can be dense)
+    auto dense_tile = [&](int64_t t) {
+        const uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
+        return t_nch[t] == 1 && nev[t] == 0 && (int64_t)ccap[t] <= lcols && t_maxc[t] <= 255 && !no_dense &&
+               dense_fits(tw, K) && dense_bytes(tw, K) <= dense_cap;
+    };
+    // Grid shaping for k_tile: work items run in rounds of `slots` workgroups (the device's CUs
+    // × k_tile's workgroups per CU); the last round of a launch whose items all take about as
+    // long keeps the rest of the device idle.  The multi-item (deep) tiles' items are made
+    // smaller (down to half of IL layers) until the launch fills its last round: C4's 2,487
+    // items of ≤ 64 layers (3.24 rounds of 768) become 3,0xx of ≤ 52.
+    {
+        int64_t n_single = 0, n_multi = 0;
+        for (int64_t t = 0; t < NT; t++) {
+            if (t_nch[t] > 1) n_multi += t_nch[t];
+            else if (!dense_tile(t)) n_single++;
+        }
+        int64_t slots = 256 * (nwp <= 16 ? 3 : 2);   // MI355X: 256 CUs; k_tile<16>: 3 workgroups per CU by LDS
+        if (const char *e = getenv("S2C_ITEM_SLOTS")) slots = std::max<int64_t>(0, atoll(e));
+        const int64_t IL = item_layers();
+        if (n_multi > 0 && slots > 0) {
+            const int64_t rounds = (n_single + n_multi + slots - 1) / slots;
+            int64_t best = IL;
+            for (int64_t il = IL - 1; il >= std::max<int64_t>(4, IL / 2); il--) {
+                int64_t n = n_single;
+                for (int64_t t = 0; t < NT; t++)
+                    if (t_nch[t] > 1) n += std::max<int64_t>(t_nch[t], (t_nl[t] + il - 1) / il);
+                if (n > rounds * slots) break;
+                best = il;
+            }
+            if (best < IL)
+                par_ranges(plan_threads(NT, 64), NT, [&](int, int64_t ta, int64_t tb) {
+                    for (int64_t t = ta; t < tb; t++)
+                        if (t_nch[t] > 1)
+                            t_nch[t] = std::max<int64_t>(t_nch[t], plan_items(b, K, (uint64_t)tiles[t].a, (uint64_t)tiles[t].b,
+                                                                              t_nl[t], best));
+                });
+        }
+    }
     for (int64_t t = 0; t < NT; t++) {
         const Tile &T = tiles[t];
         const int64_t maxc = t_maxc[t], nl = t_nl[t], nch = t_nch[t];
