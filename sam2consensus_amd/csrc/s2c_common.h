@@ -46,6 +46,24 @@ struct AmbTable {
 constexpr AmbTable AMB{};
 
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+// Scalar loads of uniform read-only words (tile records, layer bounds): s_load through the
+// scalar cache, waited here on lgkmcnt — a vector load's wait (vmcnt) would also wait for
+// the kernels' own LDS-DMA loads in flight, which the compiler does not see.
+__device__ __forceinline__ const uint32_t *uni_ptr(const uint32_t *p) {
+    const uint64_t v = (uint64_t)(uintptr_t)p;
+    return (const uint32_t *)(uintptr_t)((uint64_t)uni((uint32_t)v) | ((uint64_t)uni((uint32_t)(v >> 32)) << 32));
+}
+__device__ __forceinline__ uint32_t sload1(const uint32_t *p) {
+    uint32_t r;
+    asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(uni_ptr(p)) : "memory");
+    return r;
+}
+__device__ __forceinline__ uint4 sload4(const uint32_t *p) {
+    typedef int v4s __attribute__((ext_vector_type(4)));
+    v4s r;
+    asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(uni_ptr(p)) : "memory");
+    return make_uint4((uint32_t)r.x, (uint32_t)r.y, (uint32_t)r.z, (uint32_t)r.w);
+}
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for
 // its global stores (__syncthreads also drains vmcnt, i.e. waits for every outstanding

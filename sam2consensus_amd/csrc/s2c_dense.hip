@@ -174,24 +174,10 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 // Scalar loads of uniform read-only words (tile records, items): s_load through the scalar
 // cache, waited here — the compiler would otherwise emit vector loads (the kernel stores to
 // global memory) and wait on vmcnt, i.e. on the window DMA in flight.
-__device__ __forceinline__ const uint32_t *uni_ptr(const uint32_t *p) {
-    const uint64_t v = (uint64_t)(uintptr_t)p;
-    return (const uint32_t *)(uintptr_t)((uint64_t)uni((uint32_t)v) | ((uint64_t)uni((uint32_t)(v >> 32)) << 32));
-}
-__device__ __forceinline__ uint32_t sload1(const uint32_t *p) {
-    uint32_t r;
-    asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(uni_ptr(p)) : "memory");
-    return r;
-}
 __device__ __forceinline__ double sload_f64(const double *p) {
     uint64_t r;
     asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(uni_ptr((const uint32_t *)p)) : "memory");
     return __builtin_bit_cast(double, r);
-}
-__device__ __forceinline__ uint4 sload4(const uint32_t *p) {
-    v4i r;
-    asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(uni_ptr(p)) : "memory");
-    return make_uint4((uint32_t)r.x, (uint32_t)r.y, (uint32_t)r.z, (uint32_t)r.w);
 }
 
 #pragma clang diagnostic push

@@ -245,6 +245,20 @@ struct Chunk {
     std::vector<Event> ev;
     int64_t lines_total = 0, reads_mapped = 0, aligned = 0, qbases = 0, ntokens = 0;
     std::vector<uint32_t> sp;       // the current read's SEQ planes (seq_planes: 4 words per 32 chars)
+    // an upper bound of its reads' extents (read_extent's hi): reference hb_ref, position
+    // hb_pos in it (a read of an earlier reference ends below that reference's offset);
+    // hb_pos < 0: no read
+    uint32_t hb_ref = 0;
+    int64_t hb_pos = -1;
+    void bound(uint32_t ref, int64_t pos0, int64_t klen, int64_t L) {
+        const int64_t b = pos0 < 0 ? L : pos0 + klen;   // (a POS <= 0 wrap reaches the reference's end)
+        if (hb_pos < 0 || ref > hb_ref) {
+            hb_ref = ref;
+            hb_pos = b;
+        } else if (ref == hb_ref) {
+            hb_pos = std::max(hb_pos, b);
+        }
+    }
 };
 
 struct s2c_parser {
@@ -593,6 +607,7 @@ static int process_record(Chunk &c, const RefView &rv, std::string &last_name, i
         r.ntok = 0;
     }
     c.reads.push_back(r);
+    c.bound((uint32_t)ref, pos0, klen, L);
     return S2C_OK;
 }
 
@@ -1515,18 +1530,35 @@ static bool read_extent(const Chunk &c, const ReadRec &r, int64_t off, int64_t L
     return a <= b;
 }
 
+// host phase times on stderr (S2C_HOST_TIMING=1)
+struct PhaseClock {
+    bool on = getenv("S2C_HOST_TIMING") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(const char *what) {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        fprintf(stderr, "[s2c host] %-18s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+        t = n;
+    }
+};
+
 static int build_batch(s2c_parser *p, s2c_batch **out);
 
 // pred(chunk, read, ref_off) of every read held in chunks [c0, end), on the host threads (the
 // streamed batches' per-read tests: a few ms per million reads instead of tens): flags in
 // chunk-then-read order
-template <class Pred>
-static std::vector<uint8_t> read_flags(const s2c_parser *p, size_t c0, const std::vector<int64_t> &off, Pred &&pred) {
+template <class Pred, class ChunkPred>
+static std::vector<uint8_t> read_flags(const s2c_parser *p, size_t c0, const std::vector<int64_t> &off, Pred &&pred,
+                                       ChunkPred &&chunk_may) {
     const size_t nc = p->chunks.size() > c0 ? p->chunks.size() - c0 : 0;
     std::vector<int64_t> base(nc + 1, 0);
-    for (size_t i = 0; i < nc; i++) base[i + 1] = base[i] + (int64_t)p->chunks[c0 + i]->reads.size();
+    std::vector<uint8_t> may(nc, 1);   // (chunk_may false: every flag of the chunk is 0, no read looked at)
+    for (size_t i = 0; i < nc; i++) {
+        may[i] = chunk_may(*p->chunks[c0 + i]) ? 1 : 0;
+        base[i + 1] = base[i] + (may[i] ? (int64_t)p->chunks[c0 + i]->reads.size() : 0);
+    }
     const int64_t n = base[nc];
-    std::vector<uint8_t> f((size_t)n, 0);
+    std::vector<uint8_t> g((size_t)n, 0);
     par_ranges(plan_threads(n, 1 << 15), n, [&](int, int64_t i0, int64_t i1) {
         if (i0 >= i1) return;
         size_t ci = (size_t)(std::upper_bound(base.begin(), base.end(), i0) - base.begin()) - 1;
@@ -1534,9 +1566,16 @@ static std::vector<uint8_t> read_flags(const s2c_parser *p, size_t c0, const std
             while (i >= base[ci + 1]) ci++;
             const Chunk &c = *p->chunks[c0 + ci];
             const ReadRec &r = c.reads[(size_t)(i - base[ci])];
-            f[(size_t)i] = pred(c, r, off[r.ref]) ? 1 : 0;
+            g[(size_t)i] = pred(c, r, off[r.ref]) ? 1 : 0;
         }
     });
+    // the flags of every read, chunk by chunk (0 for the chunks skipped)
+    std::vector<uint8_t> f;
+    f.reserve(n);
+    for (size_t i = 0; i < nc; i++) {
+        if (may[i]) f.insert(f.end(), g.begin() + base[i], g.begin() + base[i + 1]);
+        else f.insert(f.end(), p->chunks[c0 + i]->reads.size(), (uint8_t)0);
+    }
     return f;
 }
 
@@ -1547,7 +1586,7 @@ static void check_late(s2c_parser *p) {
     const std::vector<uint8_t> f = read_flags(p, p->n_kept, off, [&](const Chunk &c, const ReadRec &r, int64_t o) {
         int64_t lo, hi;
         return read_extent(c, r, o, p->ref_len[r.ref], &lo, &hi) && lo < p->frontier;
-    });
+    }, [](const Chunk &) { return true; });
     p->late = std::find(f.begin(), f.end(), (uint8_t)1) != f.end();
 }
 
@@ -1626,16 +1665,27 @@ static void append_read(Chunk &d, const Chunk &c, const ReadRec &r, bool events_
 
 // Move the reads `keep` selects into one chunk; with events_only they keep only their
 // insertion events (their counts are already in the running totals).
-template <class Keep>
-static void compact_reads(s2c_parser *p, Keep keep, bool events_only) {
+template <class Keep, class ChunkMay>
+static void compact_reads(s2c_parser *p, Keep keep, ChunkMay chunk_may, bool events_only) {
+    PhaseClock clk;
     const std::vector<int64_t> off = ref_offsets(p, nullptr);
-    const std::vector<uint8_t> f = read_flags(p, 0, off, keep);   // (the tests in parallel, the copies in order)
+    // (the tests in parallel — skipping the chunks chunk_may rules out — the copies in order)
+    const std::vector<uint8_t> f = read_flags(p, 0, off, keep, [&](const Chunk &c) { return chunk_may(c, off); });
+    clk.mark("retain tests");
     std::unique_ptr<Chunk> k(new Chunk());
     size_t i = 0;
     for (auto &cp : p->chunks)
         for (const ReadRec &r : cp->reads)
-            if (f[i++]) append_read(*k, *cp, r, events_only);
-    p->chunks.clear();
+            if (f[i++]) {
+                append_read(*k, *cp, r, events_only);
+                k->bound(r.ref, r.pos0, r.klen, p->ref_len[r.ref]);
+            }
+    clk.mark("retain copies");
+    // the dropped chunks' memory goes back on a thread of its own (hundreds of MB of reads:
+    // tens of ms of page unmapping off the producer's path)
+    std::thread([](std::vector<std::unique_ptr<Chunk>> v) { v.clear(); }, std::move(p->chunks)).detach();
+    p->chunks = std::vector<std::unique_ptr<Chunk>>();
+    clk.mark("retain free");
     p->chunks.push_back(std::move(k));
     p->chunks.emplace_back(new Chunk());   // the sequential feed appends here
     p->n_kept = 1;
@@ -1650,6 +1700,8 @@ static int s2c_parser_retain_impl(s2c_parser *p, int64_t gmin) {
     compact_reads(p, [&](const Chunk &c, const ReadRec &r, int64_t off) {
         int64_t lo, hi;
         return read_extent(c, r, off, p->ref_len[r.ref], &lo, &hi) && hi >= gmin;
+    }, [&](const Chunk &c, const std::vector<int64_t> &off) {   // (no read of c can reach gmin)
+        return c.hb_pos >= 0 && off[c.hb_ref] + c.hb_pos >= gmin;
     }, false);
     p->frontier = gmin;
     return S2C_OK;
@@ -1664,7 +1716,8 @@ extern "C" int s2c_parser_retain(s2c_parser *p, int64_t gmin) {
 static int s2c_parser_retain_events_impl(s2c_parser *p) {
     if (!p) return s2c_set_error(S2C_ERR_ARG, "parser is NULL");
     if (p->err) return s2c_set_error(p->err, p->errmsg);
-    compact_reads(p, [](const Chunk &, const ReadRec &r, int64_t) { return r.nev > 0; }, true);
+    compact_reads(p, [](const Chunk &, const ReadRec &r, int64_t) { return r.nev > 0; },
+                  [](const Chunk &c, const std::vector<int64_t> &) { return !c.ev.empty(); }, true);
     return S2C_OK;
 }
 extern "C" int s2c_parser_retain_events(s2c_parser *p) {
@@ -1908,16 +1961,6 @@ extern "C" int s2c_parser_unpack(s2c_parser *p, const void *blob, size_t len) {
 }
 
 // Opt-in phase clock of the host plan (S2C_HOST_TIMING=1: one line per phase on stderr).
-struct PhaseClock {
-    bool on = getenv("S2C_HOST_TIMING") != nullptr;
-    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
-    void mark(const char *what) {
-        if (!on) return;
-        const auto n = std::chrono::steady_clock::now();
-        fprintf(stderr, "[s2c host] %-18s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
-        t = n;
-    }
-};
 
 // px of a piece of read r (s2c.h S2C_PF_XFEW): the SEQ offsets of its first two non-ACGT
 // chars when they are all 'N' (no '-': the maxdel rule never needs the plane scan), at most

@@ -676,19 +676,21 @@ constexpr uint32_t SL_SDC = 0, SL_SD = 1, SL_X = 2, SL_Y = 3, SL_N = 4, SL_Z = 5
 // still leaves room for the loads' immediate offsets: the hardware returns zeros.
 constexpr uint32_t OOR = 0xF0000000u;
 
-// A wave's chunk in LDS: one layer of the tile's window, DMA'd as four contiguous ranges —
-// its piece records (into runl, read before the walk writes run records there), op words
-// (ol), base planes (pl; a 16-byte pad first, so plane word −1 is readable) and non-ACGT
-// words (xl), each landing at its source's 16-byte phase.  segR[σ]: the first run record of
-// the layer's pieces starting in word S0 + σ (pieces are in start-word order).
+// A wave's chunk in LDS: one layer of the tile's window, DMA'd as three contiguous ranges,
+// each landing at its source's 16-byte phase — its piece records (pcb) and op words (ol) one
+// layer AHEAD, during the previous layer's count (both are read by the walk only), and its
+// base planes (pl;
+// a 16-byte pad first, so plane word −1 is readable) at the top of its own, under its walk.
+// The non-ACGT words stay in HBM (the few pieces that need them: S2C_PF_XFEW pieces take their
+// 'N' from px).  runl: the run records; segR[σ]: the first run record of the layer's pieces
+// starting in word S0 + σ (pieces are in start-word order).
 struct ChunkLds {
     uint32_t segR[CSEG + 1];
     alignas(16) uint8_t pl[16 + S2C_CHUNK_QBYTES + 16];
-    alignas(16) uint8_t xl[S2C_CHUNK_XBYTES + 16];
+    alignas(16) uint4 pcb[S2C_CHUNK_PIECES];
     alignas(16) uint8_t ol[S2C_CHUNK_OBYTES + 16];
     alignas(16) uint2 runl[S2C_CHUNK_RECS + RPAD];
 };
-static_assert(S2C_CHUNK_PIECES * 16 <= (S2C_CHUNK_RECS + RPAD) * 8, "piece records fit the run-record region");
 
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint32_t lds_byte_addr(const void *p) {
@@ -717,18 +719,33 @@ __device__ __forceinline__ DmaSrc dma_src(const void *p, const void *end) {
 // starts at the 16-byte boundary below src, so the dwords land at dst + (src & 15).
 // Arguments wave-uniform.  Completion: s_waitcnt vmcnt(0) (the compiler does not count these
 // loads): the wave's own LDS reads then see the data.
-__device__ __forceinline__ void dma16_wave(uint8_t *dst, const DmaSrc &S, const uint32_t *src, uint32_t n) {
+// Returns the number of DMA instructions issued (each one vmcnt event).
+__device__ __forceinline__ uint32_t dma16_wave(uint8_t *dst, const DmaSrc &S, const uint32_t *src, uint32_t n) {
     const uint32_t lane = threadIdx.x & 63;
     const uintptr_t sal = (uintptr_t)src & ~(uintptr_t)15;
     const uint32_t nbytes = uni((uint32_t)((uintptr_t)src - sal) + 4 * n);
     const uint32_t soff = uni((uint32_t)(sal - S.base)), m0 = uni(lds_byte_addr(dst));
-    for (uint32_t base = 0; base < nbytes; base += 1024) {
+    uint32_t k = 0;
+    for (uint32_t base = 0; base < nbytes; base += 1024, k++) {
         if (base + 16 * lane < nbytes)
             asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
                          :: "s"(m0 + base), "v"(16 * lane), "s"(S.r), "s"(soff + base) : "memory", "m0");
     }
+    return k;
 }
 #pragma clang diagnostic pop
+// s_waitcnt vmcnt(k) for a wave-uniform k (≤ 15 instructions younger than the ones waited
+// for; more: all): the VMEM loads complete in order, so this waits for every load issued
+// before the k youngest — the kernels' LDS-DMA loads, which the compiler does not count.
+__device__ __forceinline__ void wait_vm(uint32_t k) {
+    switch (uni(k)) {
+#define S2C_WV(i) case i: asm volatile("s_waitcnt vmcnt(" #i ")" ::: "memory"); break;
+        S2C_WV(1) S2C_WV(2) S2C_WV(3) S2C_WV(4) S2C_WV(5) S2C_WV(6) S2C_WV(7) S2C_WV(8)
+        S2C_WV(9) S2C_WV(10) S2C_WV(11) S2C_WV(12) S2C_WV(13) S2C_WV(14) S2C_WV(15)
+#undef S2C_WV
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+}
 
 template <uint32_t ICOL>
 struct EpiLds {
@@ -740,6 +757,10 @@ union TileLds {
     ChunkLds c[WV];   // one chunk per wave
     EpiLds<ICOL> e;
 };
+// the non-ACGT words in HBM, as a global-address-space pointer (a uniform base + 32-bit lane
+// offsets: global_load with an SGPR base, not flat loads with 64-bit lane addresses)
+typedef const __attribute__((address_space(1))) uint32_t *gptr_u32;
+
 // A wave's LDS hand-off between its own lanes (no other wave involved): the wave's LDS
 // operations complete in order, and the compiler keeps its memory accesses on either side.
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -765,31 +786,25 @@ __device__ __forceinline__ void x_bits(uint32_t xm, uint32_t p0, int32_t b0, uin
     }
 }
 template <int NWP>
-__device__ void x_fix(const uint2 *bql, const uint32_t *xl, uint32_t xd, uint32_t q, uint32_t l, uint32_t r0, bool drop,
+__device__ void x_fix(const uint2 *bql, gptr_u32 xl, uint32_t xd, uint32_t q, uint32_t l, uint32_t r0, bool drop,
                       uint32_t *hist) {
     const uint32_t v0 = q >> 5, v1 = (q + l - 1) >> 5;
-    if (v1 - v0 < 6) {
-        uint32_t xs[6];
+    for (uint32_t vb = v0; vb <= v1; vb += 4) {   // four HBM words per round trip, then one at a time
+        uint32_t xs[4];
 #pragma unroll
-        for (uint32_t u = 0; u < 6; u++) {
-            const uint32_t v = v0 + u;
-            uint32_t m = v <= v1 ? xl[v + xd] : 0u;
-            if (u == 0) m &= 0xFFFFFFFFu << (q & 31u);
-            if (v == v1) m &= 0xFFFFFFFFu >> (31u - ((q + l - 1) & 31u));
-            xs[u] = m;
+        for (uint32_t u = 0; u < 4; u++) xs[u] = vb + u <= v1 ? xl[vb + u + xd] : 0u;
+#pragma unroll 1
+        for (uint32_t v = vb; v < vb + 4; v++) {
+            uint32_t xm = xs[0];
+            xs[0] = xs[1];   // (shifted, not indexed: registers)
+            xs[1] = xs[2];
+            xs[2] = xs[3];
+            if (!xm) continue;
+            const int32_t b0 = (int32_t)(32 * v) - (int32_t)q;   // run offset of the word's bit 0
+            if (b0 < 0) xm &= 0xFFFFFFFFu << (uint32_t)(-b0);
+            if (b0 + 32 > (int32_t)l) xm &= 0xFFFFFFFFu >> (uint32_t)(b0 + 32 - (int32_t)l);
+            x_bits<NWP>(xm, bql[v].x, b0, r0, drop, hist);
         }
-#pragma unroll
-        for (uint32_t u = 0; u < 6; u++)
-            if (xs[u]) x_bits<NWP>(xs[u], bql[v0 + u].x, (int32_t)(32 * (v0 + u)) - (int32_t)q, r0, drop, hist);
-        return;
-    }
-    for (uint32_t v = v0; v <= v1; v++) {
-        uint32_t xm = xl[v + xd];
-        if (!xm) continue;
-        const int32_t b0 = (int32_t)(32 * v) - (int32_t)q;   // run offset of the word's bit 0
-        if (b0 < 0) xm &= 0xFFFFFFFFu << (uint32_t)(-b0);
-        if (b0 + 32 > (int32_t)l) xm &= 0xFFFFFFFFu >> (uint32_t)(b0 + 32 - (int32_t)l);
-        x_bits<NWP>(xm, bql[v].x, b0, r0, drop, hist);
     }
 }
 
@@ -799,7 +814,7 @@ __device__ void x_fix(const uint2 *bql, const uint32_t *xl, uint32_t xd, uint32_
 // tile part into dV / dD; N / '-' of SEQ via x_fix.  Everything from LDS.
 template <int NWP>
 __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *opl, uint32_t od, uint2 *runl, uint32_t rd,
-                                 const uint2 *bql, const uint32_t *xl, uint32_t xd, uint32_t qadj, bool maxdel_active,
+                                 const uint2 *bql, gptr_u32 xl, uint32_t xd, uint32_t qadj, bool maxdel_active,
                                  uint32_t maxdel, uint32_t a, uint32_t n, uint32_t *hist, int32_t *dV, int32_t *dD) {
     const uint32_t fl = P.w >> 24, slen = P.w & 0xFFFFFFu;
     uint32_t j = P.z;
@@ -1040,46 +1055,66 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
 
     // the layers: in place (one layer: the window of the sorted arrays) or the tile's copies
     // in the layered arrays
-    const uint32_t ly0 = uni(d.tiles[(size_t)tile * S2C_TILE_WORDS + 20]);
+    const uint32_t ly0 = sload1(d.tiles + (size_t)tile * S2C_TILE_WORDS + 20);
     const bool inplace = ly0 == S2C_LY_MAIN;
     const uint32_t *const spc = inplace ? d.pc : d.lpc, *const sops = inplace ? d.ops : d.lops;
     const uint32_t *const sbq = inplace ? d.bq : d.lbq, *const sbx = inplace ? d.bx : d.lbx;
     const uint32_t *const spx = inplace ? d.px : d.lpx;
     const DmaSrc Dpc = dma_src(spc, inplace ? d.pc_end : d.lpc_end), Dops = dma_src(sops, inplace ? d.ops_end : d.lops_end);
-    const DmaSrc Dbq = dma_src(sbq, inplace ? d.bq_end : d.lbq_end), Dbx = dma_src(sbx, inplace ? d.bx_end : d.lbx_end);
-    const uint32_t *const xl = (const uint32_t *)C.xl;
-    const uint32_t *const opl = (const uint32_t *)C.ol;
-    const uint4 *const pcr = (const uint4 *)C.runl;
-    for (uint32_t ly = l0 + wv; ly < l1; ly += WV) {
-        // ---- 1. the layer: pieces [P0, P1), op words [O0, O1), plane words [qa, qb)
+    const DmaSrc Dbq = dma_src(sbq, inplace ? d.bq_end : d.lbq_end);
+    const uint4 *const pcr = C.pcb;
+    // a layer's bounds: pieces [P0, P1), op words [O0, O1), plane words [qa, qb) (scalar loads)
+    struct Lay {
         uint32_t P0, P1, O0, O1, qa, qb;
+    };
+    auto layer_of = [&](uint32_t ly) {
+        Lay L;
         if (inplace) {
             const uint32_t *tw = d.tiles + (size_t)tile * S2C_TILE_WORDS;
-            P0 = uni(tw[13]); P1 = uni(tw[14]); O0 = uni(tw[15]); O1 = uni(tw[16]); qa = uni(tw[17]); qb = uni(tw[18]);
+            const uint4 A = sload4(tw + 12), B = sload4(tw + 16);   // words 13-18
+            L.P0 = A.y; L.P1 = A.z; L.O0 = A.w; L.O1 = B.x; L.qa = B.y; L.qb = B.z;
         } else {
-            const uint4 A = ((const uint4 *)d.lly)[ly0 + ly], B = ((const uint4 *)d.lly)[ly0 + ly + 1];
-            P0 = uni(A.x); P1 = uni(B.x); O0 = uni(A.y); O1 = uni(B.y);
-            qa = uni(A.z) >> 1;
-            qb = ((uni(B.z) + 1u) >> 1) + 1u;   // through the word after the last base (funnel)
+            const uint4 A = sload4(d.lly + 4 * (size_t)(ly0 + ly)), B = sload4(d.lly + 4 * (size_t)(ly0 + ly + 1));
+            L.P0 = A.x; L.P1 = B.x; L.O0 = A.y; L.O1 = B.y;
+            L.qa = A.z >> 1;
+            L.qb = ((B.z + 1u) >> 1) + 1u;   // through the word after the last base (funnel)
         }
-        const uint32_t NPc = P1 - P0, NR = O1 - O0;
-        dma16_wave((uint8_t *)C.runl, Dpc, spc + 4 * (size_t)P0, 4 * NPc);
-        dma16_wave(C.ol, Dops, sops + O0, NR);
-        dma16_wave(C.pl + 16, Dbq, sbq + 2 * (size_t)qa, 2 * (qb - qa));
-        dma16_wave(C.xl, Dbx, sbx + qa, qb - qa);
-        // the lane's pieces' 'N' offsets (S2C_PF_XFEW), with the DMA
+        return L;
+    };
+    // the ahead part of layer ly: its piece records and op words; returns the vmcnt events
+    // issued
+    auto issue_ahead = [&](const Lay &L) -> uint32_t {
+        const uint32_t k = dma16_wave((uint8_t *)C.pcb, Dpc, spc + 4 * (size_t)L.P0, 4 * (L.P1 - L.P0));
+        return k + dma16_wave(C.ol, Dops, sops + L.O0, L.O1 - L.O0);
+    };
+    uint32_t ly = l0 + wv;
+    Lay cur = {0, 0, 0, 0, 0, 0};
+    if (ly < l1) {
+        cur = layer_of(ly);
+        issue_ahead(cur);
+    }
+    for (; ly < l1; ly += WV) {
+        // ---- 1. the lane's pieces' 'N' offsets (S2C_PF_XFEW; read after the walk), the layer's
+        //      planes (their buffer is free: the previous count is done), then the wait for
+        //      what was issued ahead (older: everything but the planes)
+        const uint32_t P0 = cur.P0, O0 = cur.O0, O1 = cur.O1, qa = cur.qa;
+        const uint32_t NPc = cur.P1 - cur.P0, NR = O1 - O0;
         uint32_t pxr[2];
 #pragma unroll
-        for (int u = 0; u < 2; u++) pxr[u] = lane + 64 * u < NPc ? spx[P0 + lane + 64 * u] : 0xFFFFFFFFu;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the wave's own DMA: its LDS reads see it)
+        for (int u = 0; u < 2; u++) pxr[u] = spx[lane + 64 * u < NPc ? P0 + lane + 64 * u : (NPc ? P0 : 0u)];   // (in bounds)
+        asm volatile("" ::: "memory");   // (the loads stay ahead of the planes' DMA)
+        const uint32_t nq = dma16_wave(C.pl + 16, Dbq, sbq + 2 * (size_t)qa, 2 * (cur.qb - qa));
+        wait_vm(nq);
         TPROF_MARK(2);
-        // ---- 2. walk: lane per piece (records to registers first: their region becomes the
-        //      run records); the per-word record ranges from the pieces' start words
+        const uint32_t *const opl = (const uint32_t *)C.ol;
+        // ---- 2. walk: lane per piece (records to registers first); the per-word record
+        //      ranges from the pieces' start words
         const uint32_t od = (O0 & 3u) - O0;                     // op word j at opl[j + od]
         const uint32_t qadj = 32u * (qa & 1u) - 32u * qa;       // SEQ[0] at LDS plane base 16·qh + qadj
-        const uint32_t xd = (qa & 3u) - (qa & 1u);              // non-ACGT word of LDS plane word v: xl[v + xd]
+        const gptr_u32 xg = (gptr_u32)(sbx + (qa - (qa & 1u)));   // non-ACGT word of LDS plane word v: xg[v] (HBM)
         uint4 Pw[2];
         uint32_t oe[2];
+        bool planes = false;   // a piece of the lane reads the planes in its walk
 #pragma unroll
         for (int u = 0; u < 2; u++) {
             const uint32_t i = lane + 64 * u;
@@ -1093,11 +1128,13 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
                 for (int32_t sg = pw + 1; sg <= sw; sg++) C.segR[sg] = Pw[u].z - O0;
                 if (i + 1 == NPc)
                     for (uint32_t sg = (uint32_t)(sw + 1); sg <= NS; sg++) C.segR[sg] = NR;
+                const uint32_t f = Pw[u].w >> 24;
+                planes |= (f & S2C_PF_SIMPLE) ? ((f & S2C_PF_X) && !(f & S2C_PF_XFEW)) : !(f & S2C_PF_LONG);
             }
         }
         if (NPc == 0)
             for (uint32_t sg = lane; sg <= NS; sg += 64) C.segR[sg] = 0;
-        wave_lds_sync();   // (the piece records are read before run records overwrite them)
+        if (__ballot(planes)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the planes, for those walks)
         for (uint32_t i = lane; i < RPAD; i += 64) C.runl[NR + i] = make_uint2(0u, 0u);
         if (TABL(1))   // (ablated walk: zero records)
             for (uint32_t i = lane; i < NR; i += 64) C.runl[i] = make_uint2(0u, 0u);
@@ -1116,27 +1153,42 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
                     atomicSub(&dV[c1 - a], 1);
 #endif
 #ifndef S2C_ABL_X
-                    if (fl & S2C_PF_XFEW) {   // ≤ 2 'N' at SEQ offsets px (host-listed): no plane scan
-#pragma unroll
-                        for (int h = 0; h < 2; h++) {
-                            const uint32_t off = (pxr[u] >> (16 * h)) & 0xFFFFu, p = P.x + off;   // (0xFFFF: none)
-                            if (off != 0xFFFFu && p >= c0 && p < c1) H::add1(hist, SL_N, p - a, 1u);
-                        }
-                    } else if (fl & S2C_PF_X) {
-                        x_fix<NWP>(bql, xl, xd, ql + (c0 - P.x), c1 - c0, c0 - a, false, hist);
-                    }
+                    if ((fl & S2C_PF_X) && !(fl & S2C_PF_XFEW))   // (S2C_PF_XFEW: after the walk)
+                        x_fix<NWP>(bql, xg, 0u, ql + (c0 - P.x), c1 - c0, c0 - a, false, hist);
 #endif
                 }
             } else if (fl & S2C_PF_LONG) {   // (its runs come through the tile long lists)
                 for (uint32_t j = P.z; j < oe[u]; j++) C.runl[j - O0] = make_uint2(0u, 0u);
             } else {
-                walk_chunk_piece<NWP>(P, oe[u], opl, od, C.runl, 0u - O0, bql, xl, xd, qadj, d.maxdel_active != 0,
+                walk_chunk_piece<NWP>(P, oe[u], opl, od, C.runl, 0u - O0, bql, xg, 0u, qadj, d.maxdel_active != 0,
                                       (uint32_t)d.maxdel, a, n, hist, dV, dD);
             }
         }
-        wave_lds_sync();   // every run record written
+        wave_lds_sync();   // every run record written; the piece records and op words read
+        // this layer's planes (and 'N' offsets) have landed from here on
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifndef S2C_ABL_X
+#pragma unroll
+        for (int u = 0; u < 2; u++) {   // ≤ 2 'N' of an S2C_PF_XFEW piece at its SEQ offsets px: no plane scan
+            const uint4 P = Pw[u];
+            const uint32_t fl = P.w >> 24;
+            if (lane + 64 * u >= NPc || TABL(1) || (fl & (S2C_PF_SIMPLE | S2C_PF_XFEW)) != (S2C_PF_SIMPLE | S2C_PF_XFEW))
+                continue;
+            const uint32_t c0 = max(P.x, a), c1 = min(P.x + (P.w & 0xFFFFFFu), a + n);
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint32_t off = (pxr[u] >> (16 * h)) & 0xFFFFu, p = P.x + off;   // (0xFFFF: none)
+                if (off != 0xFFFFu && p >= c0 && p < c1) H::add1(hist, SL_N, p - a, 1u);
+            }
+        }
+#endif
         TPROF_MARK(3);
-        // ---- 3. count this lane's records cw0 + ga + GW·m < cw1 (reads past them: records of
+        // ---- 3. the next layer's piece records and op words, under this layer's count
+        if (ly + WV < l1) {
+            cur = layer_of(ly + WV);
+            issue_ahead(cur);
+        }
+        // ---- 4. count this lane's records cw0 + ga + GW·m < cw1 (reads past them: records of
         //      pieces starting after Ww, or the zero pad — they cover nothing of Ww)
         const uint32_t cw0 = C.segR[sa], cw1 = C.segR[sb + 1];
         const uint32_t nrec = cw0 + ga < cw1 ? (cw1 - cw0 - ga + GW - 1) / GW : 0u;
@@ -1182,9 +1234,10 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
             close4(Y, t4[1]);
             close4(Z, t4[2]);
         }
-        wave_lds_sync();   // the chunk is rewritten by the wave's next layer
+        wave_lds_sync();   // the planes and run records are rewritten by the wave's next layer
         TPROF_MARK(4);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (nothing of this wave's in flight past here)
     if (acc) flush(ww, ga, GW, wact);
     lds_sync();   // every wave's layers counted (hist, dV, dD complete but for the long pieces)
 
