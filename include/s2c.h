@@ -212,6 +212,13 @@ int  s2c_parser_set_tile_width(s2c_parser *p, int64_t width);
 int  s2c_parser_snapshot(s2c_parser *p, s2c_batch **out);
 int  s2c_parser_retain(s2c_parser *p, int64_t gmin);
 int  s2c_parser_stream_state(const s2c_parser *p, int64_t *state);
+/* Pipelined snapshots: detach moves every read held into a new parser *out (the reference
+ * table, settings and stream state copied; the partial last line stays in p), so one thread
+ * can snapshot / retain *out while another goes on feeding p; attach then puts out's reads
+ * (the retained ones) back in front of the reads fed since, takes its stream state and
+ * frees it.  Between the two, p and out share no data. */
+int  s2c_parser_detach(s2c_parser *p, s2c_parser **out);
+int  s2c_parser_attach(s2c_parser *p, s2c_parser *det);
 /* Unsorted input (counts added to running totals batch by batch, s2c_accumulate): keep
  * only the reads with insertion events, their counted ranges cleared; the last batch
  * (s2c_parser_finish) then holds every insertion event of the file. */

@@ -110,7 +110,7 @@ EXPORTS = [
     "s2c_parser_new", "s2c_parser_feed", "s2c_parser_end_header", "s2c_parser_feed_file", "s2c_parser_finish", "s2c_parser_free",
     "s2c_reader_open", "s2c_reader_read", "s2c_reader_free",
     "s2c_parser_set_tile_width", "s2c_parser_snapshot", "s2c_parser_retain", "s2c_parser_stream_state",
-    "s2c_parser_retain_events", "s2c_accumulate",
+    "s2c_parser_retain_events", "s2c_parser_detach", "s2c_parser_attach", "s2c_accumulate",
     "s2c_parser_pos_weights", "s2c_parser_checks", "s2c_parser_counters", "s2c_parser_progress", "s2c_gather_bodies", "s2c_copy_bytes", "s2c_parser_pack",
     "s2c_parser_blob_copy", "s2c_parser_unpack",
     "s2c_batch_layers", "s2c_batch_layers_mode", "s2c_batch_info_get", "s2c_batch_arrays_get", "s2c_batch_ref_name", "s2c_batch_free", "s2c_batch_shard",
@@ -147,6 +147,8 @@ def _load():
         "s2c_parser_retain": (C.c_int, [_VP, C.c_int64]),
         "s2c_parser_stream_state": (C.c_int, [_VP, C.POINTER(C.c_int64)]),
         "s2c_parser_retain_events": (C.c_int, [_VP]),
+        "s2c_parser_detach": (C.c_int, [_VP, pp]),
+        "s2c_parser_attach": (C.c_int, [_VP, _VP]),
         "s2c_accumulate": (C.c_int, [C.POINTER(Dev), C.c_int, _VP]),
         "s2c_parser_pos_weights": (C.c_int, [_VP, C.c_int64, C.POINTER(C.c_int64), C.c_int64]),
         "s2c_parser_checks": (C.c_int, [_VP, C.POINTER(C.c_uint8), C.c_int64]),

@@ -1724,6 +1724,56 @@ extern "C" int s2c_parser_retain_events(s2c_parser *p) {
     return s2c_guarded([&] { return s2c_parser_retain_events_impl(p); });
 }
 
+// Pipelined snapshots (s2c.h): the reads held move to a new parser with the same reference
+// table and stream state; the feeding parser keeps its partial line and starts a new chunk.
+static int s2c_parser_detach_impl(s2c_parser *p, s2c_parser **out) {
+    if (!p || !out) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
+    if (p->err) return s2c_set_error(p->err, p->errmsg);
+    std::unique_ptr<s2c_parser> d(new s2c_parser());
+    d->maxdel_active = p->maxdel_active;
+    d->maxdel = p->maxdel;
+    d->in_header = p->in_header;
+    d->header_lines = p->header_lines;
+    d->ref_names = p->ref_names;
+    d->ref_len = p->ref_len;
+    d->ref_idx = p->ref_idx;
+    d->last_name = p->last_name;
+    d->last_ref = p->last_ref;
+    d->tile_width = p->tile_width;
+    d->frontier = p->frontier;
+    d->n_kept = p->n_kept;
+    d->late = p->late;
+    d->chunks = std::move(p->chunks);
+    p->chunks.clear();
+    p->chunks.emplace_back(new Chunk());   // the sequential feed appends here
+    p->n_kept = 0;
+    *out = d.release();
+    return S2C_OK;
+}
+extern "C" int s2c_parser_detach(s2c_parser *p, s2c_parser **out) {
+    return s2c_guarded([&] { return s2c_parser_detach_impl(p, out); });
+}
+static int s2c_parser_attach_impl(s2c_parser *p, s2c_parser *det) {
+    if (!p || !det) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
+    std::unique_ptr<s2c_parser> d(det);
+    if (d->err && !p->err) {   // (an error of the detached reads comes first in file order)
+        p->err = d->err;
+        p->errmsg = d->errmsg;
+    }
+    std::vector<std::unique_ptr<Chunk>> cs = std::move(d->chunks);
+    const size_t kept = cs.size();
+    for (auto &c : p->chunks) cs.push_back(std::move(c));
+    p->chunks = std::move(cs);
+    // the detached parser's retained chunks are the kept ones; the reads fed since follow
+    p->n_kept = kept;
+    p->frontier = std::max(p->frontier, d->frontier);
+    p->late = p->late || d->late;
+    return S2C_OK;
+}
+extern "C" int s2c_parser_attach(s2c_parser *p, s2c_parser *det) {
+    return s2c_guarded([&] { return s2c_parser_attach_impl(p, det); });
+}
+
 // state[0] = 1 if a read parsed after a retain reached below its frontier; state[1..2] =
 // (reference index, POS - 1) of the last mapped read in file order (-1, 0: none yet);
 // state[3] = reads held.

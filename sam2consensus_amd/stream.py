@@ -81,6 +81,20 @@ class StreamParser(Parser):
         L.check(L.lib.s2c_parser_stream_state(self._p, s))
         return bool(s[0]), int(s[1]), int(s[2]), int(s[3])
 
+    def detach(self) -> "StreamParser":
+        """The reads held move to a new parser (s2c_parser_detach): it can be snapshot and
+        retained on another thread while this one goes on feeding; ``attach`` it back."""
+        d = StreamParser.__new__(StreamParser)
+        d.maxdel_active, d.maxdel = self.maxdel_active, self.maxdel
+        d._p = C.c_void_p()
+        L.check(L.lib.s2c_parser_detach(self._p, C.byref(d._p)))
+        return d
+
+    def attach(self, d: "StreamParser"):
+        """Put ``d``'s reads back in front of the ones fed since (``d`` is consumed)."""
+        h, d._p = d._p, C.c_void_p()
+        L.check(L.lib.s2c_parser_attach(self._p, h))
+
 
 def _sub(hb, t0, t1):
     h = C.c_void_p()
@@ -159,14 +173,94 @@ class _Producer:
 def _sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, state, ranged=False):
     """Generator (producer thread) of the streamed run of sorted input: ("run", sub, t0, t1)
     for every final tile range — a cut sub-batch, or with ``ranged`` the snapshot itself
-    (the device side runs its tiles [t0, t1)) — then ("last", hb) with the final batch."""
+    (the device side runs its tiles [t0, t1)) — then ("last", hb) with the final batch.
+
+    Pipelined (the default; S2C_STREAM_PIPE=0 turns it off): at each batch the reads held
+    are detached into a parser of their own, whose snapshot, cut and retain run on a helper
+    thread while this one goes on reading and feeding the next blocks; the retained reads
+    are attached back in front of the new ones before the next batch is detached.  So the
+    producer's time per batch is max(read + feed, snapshot + cut + retain), not their sum."""
     p = StreamParser(maxdel_active, 150, tile_width)
     t_done, pending, broken = 0, 0, False
     tm = state.setdefault("t", {})
     clk = time.perf_counter
+    pipe = os.environ.get("S2C_STREAM_PIPE", "1").strip() != "0"
 
     def add(k, t0):
         tm[k] = tm.get(k, 0.0) + clk() - t0
+
+    def stage(q, t_lo):
+        """Snapshot / cut / retain of the reads ``q`` holds: ("broken",), ("skip", held) or
+        ("run", sub, t_lo, t1, NT, held)."""
+        try:
+            t0 = clk()
+            hb = q.snapshot()
+            add("snapshot", t0)
+        except (KeyError, IndexError):
+            return ("broken",)       # s2c_parser_finish raises it once the input is read
+        try:
+            late, ref, pos0, held = q.state()
+            if late:
+                raise NotSorted("a read reaches positions already emitted")
+            if ref < 0:
+                return ("skip", held)
+            bound = int(hb.ref_off[ref]) + max(pos0, 0)
+            NT = int(hb.info.n_tiles)
+            t1 = int(np.searchsorted(hb.tiles[:, 1].astype(np.int64), bound, side="right"))
+            if t1 <= t_lo:
+                return ("skip", held)
+            gmin = int(hb.tiles[t1, 0]) if t1 < NT else int(hb.info.padded_len)
+            t0 = clk()
+            state["absorb"](hb)
+            add("absorb", t0)
+            t0 = clk()
+            if ranged:                # the device runs the snapshot's tiles [t_lo, t1) itself
+                sub, hb = hb, None
+                sub.t0_range = t_lo
+            else:
+                sub = _sub(hb, t_lo, t1)
+            add("cut", t0)
+            t0 = clk()
+            q.retain(gmin)
+            add("retain", t0)
+            return ("run", sub, t_lo, t1, NT, held)
+        finally:
+            if hb is not None:
+                hb.free()
+
+    ex = None
+    if pipe:
+        from concurrent.futures import ThreadPoolExecutor
+        ex = ThreadPoolExecutor(max_workers=1, thread_name_prefix="s2c-stage")
+    run = None                       # (future, detached parser) of the stage in flight
+
+    def join():
+        """Wait for the stage in flight and attach its parser back; its outcome."""
+        nonlocal run
+        f, d = run
+        run = None
+        t0 = clk()
+        try:
+            return f.result()
+        finally:
+            p.attach(d)
+            add("join", t0)
+
+    def outcome(o):
+        """The item to yield for a stage's outcome (None: nothing to run)."""
+        nonlocal broken, t_done
+        if o[0] == "broken":
+            broken = True
+            return None
+        state["held_max"] = max(state["held_max"], o[-1])
+        if o[0] == "skip":
+            return None
+        _, sub, t_lo, t1, NT, held = o
+        t_done = t1
+        if stats_hook:
+            stats_hook(t_done, NT, held)
+        return ("run", sub, t_lo, t1)
+
     try:
         it = iter(blocks)
         while True:
@@ -179,49 +273,24 @@ def _sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, st
             p.feed(blk)
             add("feed", t0)
             pending += len(blk)
+            if run is not None and (run[0].done() or (not broken and pending >= batch_bytes)):
+                item = outcome(join())
+                if item is not None:
+                    yield item
             if broken or pending < batch_bytes:
                 continue
             pending = 0
-            try:
-                t0 = clk()
-                hb = p.snapshot()
-                add("snapshot", t0)
-            except (KeyError, IndexError):
-                broken = True          # s2c_parser_finish raises it once the input is read
+            if ex is None:
+                item = outcome(stage(p, t_done))
+                if item is not None:
+                    yield item
                 continue
-            try:
-                late, ref, pos0, held = p.state()
-                state["held_max"] = max(state["held_max"], held)
-                if late:
-                    raise NotSorted("a read reaches positions already emitted")
-                if ref < 0:
-                    continue
-                bound = int(hb.ref_off[ref]) + max(pos0, 0)
-                NT = int(hb.info.n_tiles)
-                t1 = int(np.searchsorted(hb.tiles[:, 1].astype(np.int64), bound, side="right"))
-                if t1 <= t_done:
-                    continue
-                gmin = int(hb.tiles[t1, 0]) if t1 < NT else int(hb.info.padded_len)
-                t0 = clk()
-                state["absorb"](hb)
-                add("absorb", t0)
-                t0 = clk()
-                if ranged:            # the device runs the snapshot's tiles [t_done, t1) itself
-                    sub, hb = hb, None
-                    sub.t0_range = t_done
-                else:
-                    sub = _sub(hb, t_done, t1)
-                add("cut", t0)
-                t0 = clk()
-                p.retain(gmin)
-                add("retain", t0)
-                yield ("run", sub, t_done, t1)
-                t_done = t1
-                if stats_hook:
-                    stats_hook(t_done, NT, held)
-            finally:
-                if hb is not None:
-                    hb.free()
+            d = p.detach()
+            run = (ex.submit(stage, d, t_done), d)
+        if run is not None:
+            item = outcome(join())
+            if item is not None:
+                yield item
         t0 = clk()
         hb = p.finish()
         add("finish", t0)
@@ -236,6 +305,17 @@ def _sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, st
             yield ("run", _sub(hb, t_done, NT), t_done, NT)
         yield ("last", hb)
     finally:
+        if run is not None:          # (closed or raised with a stage in flight)
+            f, d = run
+            try:
+                o = f.result()
+                if o[0] == "run":
+                    o[1].free()
+            except BaseException:  # noqa: BLE001 - the first error is the one raised
+                pass
+            d.close()
+        if ex is not None:
+            ex.shutdown(wait=True)
         p.close()
 
 

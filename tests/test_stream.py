@@ -80,6 +80,41 @@ def test_block_and_batch_sizes(block, batch_bytes, tile):
     assert files == o.run_case(sam, ["-c", "0.5"])["files"]
 
 
+@pytest.mark.parametrize("pipe", ["0", "1"])
+def test_pipelined_and_serial_snapshots_agree(monkeypatch, pipe):
+    """S2C_STREAM_PIPE=1 (default): each batch's reads are detached and snapshot / retained
+    on a helper thread while the feed goes on, then attached back (s2c_parser_detach /
+    _attach); =0 does it in line.  Same bytes, counters and retained-read bound."""
+    monkeypatch.setenv("S2C_STREAM_PIPE", pipe)
+    sam = _sorted_case()
+    for block, batch_bytes in ((97, 300), (1, 50), (4096, 2048)):
+        res, files = _stream(sam, ["-c", "0.25,0.75"], block, batch_bytes)
+        assert files == o.run_case(sam, ["-c", "0.25,0.75"])["files"]
+        hb = batch.parse_text(sam)
+        assert (res.header_lines, res.lines_total, res.reads_mapped) == \
+            (hb.info.header_lines, hb.info.lines_total, hb.info.reads_mapped)
+        assert len(res.batches) > 1 or batch_bytes > len(sam)
+        assert [b[1] for b in res.batches] == sorted(b[1] for b in res.batches)
+
+
+def test_detach_attach_round_trip():
+    """Detached reads come back in front of the reads fed since; the batch equals one parse."""
+    sam = _sorted_case().encode("latin-1")
+    p = stream.StreamParser(True, 150, 64)
+    cut = len(sam) // 2
+    p.feed(sam[:cut])
+    d = p.detach()
+    p.feed(sam[cut:])
+    p.attach(d)
+    assert not d._p
+    hb = p.finish()
+    ref = batch.parse_text(sam.decode("latin-1"))
+    assert (hb.info.lines_total, hb.info.reads_mapped) == (ref.info.lines_total, ref.info.reads_mapped)
+    assert np.array_equal(np.asarray(hb.ref_reads), np.asarray(ref.ref_reads))
+    hb.free()
+    p.close()
+
+
 def test_golden_cases_stream_or_detect_unsorted():
     """Every KAT case: byte-identical when streamed, or NotSorted (then the CLI runs one batch)."""
     n_streamed = 0
