@@ -242,6 +242,7 @@ struct Chunk {
     u32buf toks;
     u32buf bq, bx;   // planes [k][2] and [k]; bases [0, nq)
     uint64_t nq = 0;
+    uint64_t nz = 0;   // plane words [0, nz) initialised (pack_seq zeroes the words it reaches)
     std::vector<Event> ev;
     int64_t lines_total = 0, reads_mapped = 0, aligned = 0, qbases = 0, ntokens = 0;
     std::vector<uint32_t> sp;       // the current read's SEQ planes (seq_planes: 4 words per 32 chars)
@@ -400,7 +401,23 @@ __attribute__((target("avx2"))) static void seq_planes_avx2(const char *seq, siz
         o[4 * w + 2] = n | d | bad;
         o[4 * w + 3] = bad;
     }
-    if (32 * w < slen) seq_planes_scalar(seq + 32 * w, slen - 32 * w, o + 4 * w);
+    if (32 * w < slen) {   // the tail through a 32-byte copy padded with 'A' (all planes 0)
+        alignas(32) char t[32];
+        memset(t, 'A', sizeof(t));
+        memcpy(t, seq + 32 * w, slen - 32 * w);
+        const __m256i v = _mm256_load_si256((const __m256i *)t);
+        const uint32_t a = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, A));
+        const uint32_t c = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, Cc));
+        const uint32_t g = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, Gg));
+        const uint32_t tt = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, Tt));
+        const uint32_t n = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, Nn));
+        const uint32_t d = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, Dd));
+        const uint32_t bad = ~(a | c | g | tt | n | d);
+        o[4 * w] = c | tt | d | bad;
+        o[4 * w + 1] = g | tt | bad;
+        o[4 * w + 2] = n | d | bad;
+        o[4 * w + 3] = bad;
+    }
 }
 static const bool HAVE_AVX2 = __builtin_cpu_supports("avx2");
 #endif
@@ -435,10 +452,15 @@ static uint64_t pack_seq(Chunk &c, const uint32_t *sp, size_t slen, uint8_t *has
     const uint64_t q0 = (c.nq + 15) & ~(uint64_t)15;
     const uint64_t q1 = q0 + slen;
     const size_t need = (size_t)((q1 + 31) >> 5) + 1;
-    if (c.bx.size() < need) {
+    if (c.bx.size() < need) {   // (grown without a fill: the words are zeroed as reached, below)
         size_t cap = std::max(need, c.bx.size() * 2);
-        c.bq.resize(2 * cap, 0u);
-        c.bx.resize(cap, 0u);
+        c.bq.resize(2 * cap);
+        c.bx.resize(cap);
+    }
+    if (c.nz < need) {   // the words first reached by this read (and the funnel word after it)
+        memset(&c.bq[2 * c.nz], 0, 8 * (need - c.nz));
+        memset(&c.bx[c.nz], 0, 4 * (need - c.nz));
+        c.nz = need;
     }
     uint8_t anyx = 0;
     const uint32_t sh = (uint32_t)(q0 & 31);   // 0 or 16
@@ -748,8 +770,8 @@ int parse_window(s2c_parser *p, const char *s, size_t n) {
         const size_t m = cut[k + 1] - cut[k];
         c.reads.reserve(m / 150 + 16);   // (SAM lines of ≥ 150 bytes: no regrowth for typical reads)
         c.toks.reserve(m / 100 + 16);
-        c.bx.resize(m / 32 + 64, 0u);     // SEQ bytes ≤ m: planes of ≤ m bases, 16-base aligned reads
-        c.bq.resize(2 * c.bx.size(), 0u);
+        c.bx.resize(m / 32 + 64);     // SEQ bytes ≤ m: planes of ≤ m bases, 16-base aligned reads
+        c.bq.resize(2 * c.bx.size());  // (no fill: pack_seq zeroes the words it reaches)
         size_t j = 0;
         while (j < m) {
             const char *nl = (const char *)memchr(b + j, '\n', m - j);
@@ -1239,7 +1261,7 @@ static void mark_runs(s2c_batch *b) {
 // the chunk (S2C_CHUNK_*): pieces, plane / non-ACGT / op bytes, run records, and per word
 // <= S2C_CHUNK_LANE_RECS records per counting lane.
 struct PieceBlocks {          // prefix sums over the sorted pieces (mod 2^32: differences exact)
-    std::vector<uint32_t> n, h, o;   // short pieces, their plane half-words, their op words
+    u32buf n, h, o;   // short pieces, their plane half-words, their op words (filled by the threads: no zero-fill)
 };
 static inline uint32_t piece_half_words(uint32_t w3) { return ((w3 & 0xFFFFFFu) + 15u) / 16u; }
 static void piece_blocks(const s2c_batch *b, PieceBlocks &B) {
@@ -1277,13 +1299,29 @@ static inline uint64_t layer_rot(uint64_t s, uint64_t nl) { return (s * 26544357
 static inline uint64_t layer_lo(const LayerSeg &g, uint64_t l, uint64_t nl) {
     return g.p0 + (g.n * l + layer_rot(g.s, nl)) / nl;
 }
+// c[l] = layer_lo(g, l, nl) for l = 0..nl with one division (floor((n·l + r) / nl) stepped:
+// the remainder grows by n mod nl < nl per layer, so at most one carry per step)
+static inline void layer_cuts(const LayerSeg &g, uint64_t nl, uint64_t *c) {
+    const uint64_t qn = g.n / nl, rn = g.n % nl;
+    uint64_t q = 0, rem = layer_rot(g.s, nl);
+    for (uint64_t l = 0; l <= nl; l++) {
+        c[l] = g.p0 + q;
+        q += qn;
+        rem += rn;
+        if (rem >= nl) { rem -= nl; q++; }
+    }
+}
+// the cut points of every segment of a tile (segment i's at cuts[i·(nl+1) ..])
+static void tile_cuts(const std::vector<LayerSeg> &seg, uint64_t nl, std::vector<uint64_t> &cuts) {
+    cuts.resize(seg.size() * (nl + 1));
+    for (size_t i = 0; i < seg.size(); i++) layer_cuts(seg[i], nl, &cuts[i * (nl + 1)]);
+}
 
-static bool layer_fits(const PieceBlocks &B, const std::vector<LayerSeg> &seg, int64_t S0, int64_t W0, int64_t W1,
-                       int64_t K, int64_t G, uint64_t l, uint64_t nl, std::vector<int64_t> &recs) {
-    const size_t NS = seg.size();
+static bool layer_fits(const PieceBlocks &B, size_t NS, const std::vector<uint64_t> &cuts, int64_t S0, int64_t W0,
+                       int64_t W1, int64_t K, int64_t G, uint64_t l, uint64_t nl, std::vector<int64_t> &recs) {
     uint64_t np = 0, nh = 0, rc = 0;
     for (size_t i = 0; i < NS; i++) {
-        const uint64_t lo = layer_lo(seg[i], l, nl), hi = layer_lo(seg[i], l + 1, nl);
+        const uint64_t lo = cuts[i * (nl + 1) + l], hi = cuts[i * (nl + 1) + l + 1];
         recs[i] = (int64_t)(uint32_t)(B.o[hi] - B.o[lo]);
         np += (uint32_t)(B.n[hi] - B.n[lo]);
         nh += (uint32_t)(B.h[hi] - B.h[lo]);
@@ -1316,6 +1354,7 @@ static int64_t plan_layers(const s2c_batch *b, const PieceBlocks &B, int64_t K, 
     }
     if (maxn == 0) return 1;
     std::vector<int64_t> recs(seg.size());
+    std::vector<uint64_t> cuts;
     uint64_t nl = std::max<uint64_t>({1, (tp * 10 / 9) / S2C_CHUNK_PIECES + 1, (4 * th * 10 / 9) / S2C_CHUNK_QBYTES + 1,
                                       (tr * 10 / 9) / S2C_CHUNK_RECS + 1});
     // (past maxn layers the rotation still spreads the segments' pieces: up to 4 per piece)
@@ -1323,8 +1362,9 @@ static int64_t plan_layers(const s2c_batch *b, const PieceBlocks &B, int64_t K, 
     nl = std::min(nl, nlmax);
     for (;; nl = nl + 1 + nl / 16) {
         if (nl > nlmax) nl = nlmax;
+        tile_cuts(seg, nl, cuts);
         bool ok = true;
-        for (uint64_t l = 0; l < nl && ok; l++) ok = layer_fits(B, seg, S0, W0, W1, K, G, l, nl, recs);
+        for (uint64_t l = 0; l < nl && ok; l++) ok = layer_fits(B, seg.size(), cuts, S0, W0, W1, K, G, l, nl, recs);
         if (ok) return (int64_t)nl;
         if (nl == nlmax) return 0;
     }
@@ -1376,11 +1416,14 @@ static void build_layers(s2c_batch *b, int64_t G, bool with_dense) {
         const int64_t nl = T.nl, W0 = tw[0] >> 5, W1 = (tw[1] + 31) >> 5, S0 = std::max<int64_t>(W0 - K, 0);
         T.ly0 = (int64_t)lyp.size() - 1;
         tw[20] = (uint32_t)T.ly0;
+        std::vector<LayerSeg> seg;
+        for (int64_t s = S0; s < W1; s++) seg.push_back({b->ps[s], (uint64_t)(b->ps[s + 1] - b->ps[s]), (uint64_t)s});
+        std::vector<uint64_t> cuts;
+        tile_cuts(seg, (uint64_t)nl, cuts);
         for (int64_t l = 0; l < nl; l++) {
             uint64_t np = 0, no = 0, nh = 0;
-            for (int64_t s = S0; s < W1; s++) {
-                const LayerSeg g{b->ps[s], (uint64_t)(b->ps[s + 1] - b->ps[s]), (uint64_t)s};
-                const uint64_t lo = layer_lo(g, l, nl), hi = layer_lo(g, l + 1, nl);
+            for (size_t i = 0; i < seg.size(); i++) {
+                const uint64_t lo = cuts[i * (nl + 1) + l], hi = cuts[i * (nl + 1) + l + 1];
                 np += (uint32_t)(B.n[hi] - B.n[lo]);
                 no += (uint32_t)(B.o[hi] - B.o[lo]);
                 nh += (uint32_t)(B.h[hi] - B.h[lo]);
@@ -1419,12 +1462,15 @@ static void build_layers(s2c_batch *b, int64_t G, bool with_dense) {
             const TL &T = tl[i];
             const uint32_t *tw = &b->tiles[(size_t)T.t * S2C_TILE_WORDS];
             const int64_t W0 = tw[0] >> 5, W1 = (tw[1] + 31) >> 5, S0 = std::max<int64_t>(W0 - K, 0);
+            std::vector<LayerSeg> seg;
+            for (int64_t s = S0; s < W1; s++) seg.push_back({b->ps[s], (uint64_t)(b->ps[s + 1] - b->ps[s]), (uint64_t)s});
+            std::vector<uint64_t> cuts;
+            tile_cuts(seg, (uint64_t)T.nl, cuts);
             for (int64_t l = 0; l < T.nl; l++) {
                 const int64_t L = T.ly0 + l;
                 uint64_t kp = lyp[L], ko = lyo[L], kh = lyh[L];
-                for (int64_t s = S0; s < W1; s++) {
-                    const LayerSeg g{b->ps[s], (uint64_t)(b->ps[s + 1] - b->ps[s]), (uint64_t)s};
-                    const uint64_t lo = layer_lo(g, l, T.nl), hi = layer_lo(g, l + 1, T.nl);
+                for (size_t i = 0; i < seg.size(); i++) {
+                    const uint64_t lo = cuts[i * (T.nl + 1) + l], hi = cuts[i * (T.nl + 1) + l + 1];
                     for (uint64_t k = lo; k < hi; k++) {
                         const uint32_t *pr = &b->pc[4 * k];
                         if ((pr[3] >> 24) & S2C_PF_LONG) continue;
@@ -1474,7 +1520,15 @@ static int64_t item_layers() {
     return il;
 }
 static int64_t plan_items(const s2c_batch *b, int64_t K, uint64_t a, uint64_t e, int64_t nl, int64_t IL) {
+    if (nl <= 1) return 1;   // (one layer: one item whatever its records)
     const int64_t W0 = (int64_t)(a >> 5), W1 = (int64_t)((e + 31) >> 5), S0 = std::max<int64_t>(W0 - K, 0);
+    std::vector<LayerSeg> seg;
+    for (int64_t s = S0; s < W1; s++) seg.push_back({b->ps[s], (uint64_t)(b->ps[s + 1] - b->ps[s]), (uint64_t)s});
+    std::vector<uint64_t> cuts;
+    tile_cuts(seg, (uint64_t)nl, cuts);
+    // op slot of each cut (the records between two cuts: their difference)
+    for (uint64_t &c : cuts) c = b->pc[4 * c + 2];
+    const uint64_t stride = (uint64_t)nl + 1;
     int64_t nch = nl > 2 * IL ? (nl + IL - 1) / IL : 1;
     for (;; nch++) {
         bool ok = true;
@@ -1483,8 +1537,8 @@ static int64_t plan_items(const s2c_batch *b, int64_t K, uint64_t a, uint64_t e,
             for (int64_t W = W0; W < W1 && ok; W++) {
                 int64_t r = 0;
                 for (int64_t s = std::max(W - K, S0); s <= W; s++) {
-                    const LayerSeg g{b->ps[s], (uint64_t)(b->ps[s + 1] - b->ps[s]), (uint64_t)s};
-                    r += b->pc[4 * layer_lo(g, l1, nl) + 2] - b->pc[4 * layer_lo(g, l0, nl) + 2];
+                    const uint64_t *cs = &cuts[(uint64_t)(s - S0) * stride];
+                    r += (uint32_t)(cs[l1] - cs[l0]);
                 }
                 ok = r <= S2C_ITEM_RECS;
             }
@@ -1642,6 +1696,7 @@ static void append_read(Chunk &d, const Chunk &c, const ReadRec &r, bool events_
             const size_t cap = std::max(need, d.bx.size() * 2);
             d.bq.resize(2 * cap, 0u);
             d.bx.resize(cap, 0u);
+            d.nz = cap;   // (zero-filled)
         }
         const uint16_t *sq = (const uint16_t *)c.bq.data(), *sx = (const uint16_t *)c.bx.data();
         uint16_t *dq = (uint16_t *)d.bq.data(), *dx = (uint16_t *)d.bx.data();
@@ -1994,6 +2049,7 @@ static int s2c_parser_unpack_impl(s2c_parser *p, const void *blob, size_t len) {
     get(c->bx, h.n_qw);
     get(c->ev, h.n_ev);
     c->nq = h.nq;
+    c->nz = h.n_qw;
     const size_t R = p->ref_names.size();
     for (const ReadRec &r : c->reads)   // indices into this chunk and the header's references
         if (r.ref >= R || r.tok + r.ntok > h.n_toks || (uint64_t)r.ev0 + r.nev > h.n_ev ||
@@ -2522,6 +2578,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     I.chunk = 0;   // (the most layers of any tile)
     PieceBlocks PB;
     piece_blocks(b, PB);
+    clk.mark("piece blocks");
     const int64_t lcols = S2C_LDS_COLS(nwp);
     b->tiles.assign((size_t)NT * S2C_TILE_WORDS, 0u);
     uint64_t boff = 0, loff = 0, coff = 0;
@@ -2546,6 +2603,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
             tile_window(b, K, T.a, T.b, &b->tiles[(size_t)t * S2C_TILE_WORDS]);
         }
     });
+    clk.mark("tile plans");
     if (too_big) return s2c_set_error(S2C_ERR_LIMIT, "a read whose SEQ or CIGAR exceeds k_tile's LDS chunk");
     // the dense class, as the loop below decides it (only single-item tiles can be dense)
     auto dense_tile = [&](int64_t t) {
