@@ -38,7 +38,7 @@
 // phase clocks (diagnostic build `make prof`, scripts/prof_dense.py): Σ over sampled waves
 // (one tile in 64) of the s_memtime deltas of each phase
 __device__ unsigned long long g_prof[16];
-__device__ uint32_t g_abl;   // ablation bits (timing only; results wrong): 1 events, 2 count, 4 walk, 8 vote,
+__device__ uint32_t g_abl;   // ablation bits (timing only; results wrong): 1 events, 2 count, 4 walk, 8 vote, 64 slow votes,
                              // 16 queued walk, 32 N / '-' events
 #define ABL(b) ((g_abl & (b)) != 0)
 #define PROF_MARK(i)                                                                               \
@@ -446,56 +446,12 @@ constexpr int WT = WGD * WPT;     // threads per tile
 #define S2C_DENSE_PFN 2
 #endif
 constexpr int PFN = S2C_DENSE_PFN;   // piece records per thread loaded with the DMA (windows of ≤ PFN·WT pieces)
-#ifndef S2C_DENSE_PERSIST
-#define S2C_DENSE_PERSIST 0   // 1: persistent workgroups (the next tile's window DMA under this tile's vote)
-#endif
-// A tile's FASTA bytes and statistics held in registers until the persistent loop has issued
-// the next tile's loads (one threshold, whole words): stored then, so the loop's wait for
-// those loads is not also a wait for stores issued just before it.
 template <int NWP>
-struct Deferred {
-    static constexpr int RPL = 8 / (WGD / (NWP / WPT));
-    uint32_t body[RPL == 8 ? 8 : (RPL == 4 ? 4 : (RPL == 2 ? 2 : 1))];   // the lane's row bytes, packed
-    uint64_t boff;   // out byte offset of the lane's first byte (its word's row base)
-    bool pend;       // the lane holds body bytes to store
-    // tile statistics (uniform; stored by thread 0)
-    uint32_t tile, sc, nd, ne, n;
-    bool spend;
-};
-template <int NWP>
-__device__ __forceinline__ void flush_deferred(const DenseArgs &d, Deferred<NWP> &f) {
-    constexpr int RPL = Deferred<NWP>::RPL;
-    if (f.pend) {
-        uint8_t *dst = d.out + f.boff;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            if constexpr (RPL == 8) *(uint2 *)(dst + 8 * j) = make_uint2(f.body[j], f.body[4 + j]);
-            else if constexpr (RPL == 4) *(uint32_t *)(dst + 8 * j) = f.body[j];
-            else if constexpr (RPL == 2) *(uint16_t *)(dst + 8 * j) = (uint16_t)(f.body[j >> 1] >> (16 * (j & 1)));
-            else dst[8 * j] = (uint8_t)(f.body[0] >> (8 * j));
-        }
-        f.pend = false;
-    }
-    if (f.spend) {
-        if (threadIdx.x == 0) {
-            uint64_t *st = d.tile_stats + (size_t)f.tile * 4;
-            st[0] = f.sc;
-            st[1] = f.n;
-            st[2] = f.nd;
-            st[3] = f.ne;
-            d.blk_len[f.tile] = f.n;
-        }
-        f.spend = false;
-    }
-}
-
-template <int NWP, class OnFree>
 __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, const WinLds &L, uint32_t *dcnt,
                                            uint32_t *ncnt, uint32_t *ccnt, const uint8_t *amb, uint32_t fill0,
                                            const uint4 (&Pp)[PFN], const uint32_t (&oe)[PFN], const uint32_t (&pxr)[PFN],
                                            uint32_t cw0, uint32_t cw1, unsigned long long t_entry,
-                                           uint32_t (*stl)[WPT][4], OnFree &&on_free, Deferred<NWP> &dfr, bool defer,
-                                           uint32_t tid) {
+                                           uint32_t (*stl)[WPT][4], uint32_t tid) {
     constexpr int NWPW = NWP / WPT, G = WGD / NWPW, RPL = 8 / G;
 #ifdef S2C_PROF
     unsigned long long prof_t = t_entry;
@@ -856,8 +812,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         const Rec rc = rec_dec(runl[queue[qcap - 1u - i]]);
         x_events(bxl, bql, rc.q, rc.l, rc.r0, TL, false, dcnt, ncnt, ccnt);
     }
-    lds_sync();   // the byte counters are final; the window's LDS is free
-    on_free();    // (persistent: the next tile's window DMA, under this tile's vote)
+    lds_sync();   // the byte counters are final
     PROF_MARK(4);
     // the byte counters of this lane's rows: read now, used by the vote
     const uint32_t rbase = 8 * w + g * RPL;   // the rows' dword index in the byte counters
@@ -867,14 +822,6 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         rD[rr] = active ? dcnt[rbase + rr] : 0u;
         rN[rr] = active ? ncnt[rbase + rr] : 0u;
         rX[rr] = active ? ccnt[rbase + rr] : 0u;
-    }
-    if (S2C_DENSE_PERSIST && active) {   // (zero again for the next tile: a wave's lanes hold all rows of its words)
-#pragma unroll
-        for (int rr = 0; rr < RPL; rr++) {
-            dcnt[rbase + rr] = 0u;
-            ncnt[rbase + rr] = 0u;
-            ccnt[rbase + rr] = 0u;
-        }
     }
     // ---- counters → byte counts: R[r] byte j = count of position 8j + r
 #pragma unroll
@@ -981,6 +928,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             nd += (uint32_t)__popc(nzb) + d.fill_nondash * (uint32_t)__popc(ncm[rr] & inb[rr] & 0x01010101u);
         }
         // the other called positions: closed form of the group-sort vote (:241-251, :359-366)
+        if (ABL(64)) slow = 0;
         while (slow) {
             const uint32_t i = (uint32_t)__builtin_ctz(slow);
             slow &= slow - 1;
@@ -1017,19 +965,11 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             o[2] = __builtin_amdgcn_perm(t3, t1, 0x05040100u);
             o[3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
         };
-        if (defer) dfr.boff = (uint64_t)(dst - d.out);
         if constexpr (RPL == 8) {
             uint32_t c2[4];
             tr4(ow[0], ow[1], ow[2], ow[3], cj);
             tr4(ow[4 % RPL], ow[5 % RPL], ow[6 % RPL], ow[7 % RPL], c2);
-            if (defer && full) {
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    dfr.body[j % (sizeof(dfr.body) / 4)] = cj[j];
-                    dfr.body[(4 + j) % (sizeof(dfr.body) / 4)] = c2[j];
-                }
-                dfr.pend = true;
-            } else if (full) {
+            if (full) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) *(uint2 *)(dst + 8 * j) = make_uint2(cj[j], c2[j]);
             } else if (active) {   // (the tile's last word; bounds kept here, not hoisted)
@@ -1043,20 +983,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             }
         } else {
             tr4(ow[0], RPL > 1 ? ow[1 % RPL] : 0u, RPL > 2 ? ow[2 % RPL] : 0u, RPL > 3 ? ow[3 % RPL] : 0u, cj);
-            if (defer && full) {
-                constexpr int NB = sizeof(dfr.body) / 4;
-                if constexpr (RPL == 4) {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) dfr.body[j % NB] = cj[j];
-                } else if constexpr (RPL == 2) {
-                    dfr.body[0] = (cj[0] & 0xFFFFu) | (cj[1] << 16);
-                    dfr.body[1 % NB] = (cj[2] & 0xFFFFu) | (cj[3] << 16);
-                } else {
-                    dfr.body[0] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(cj[3], cj[2], 0x0C0C0400u),
-                                                        __builtin_amdgcn_perm(cj[1], cj[0], 0x0C0C0400u), 0x05040100u);
-                }
-                dfr.pend = true;
-            } else if (full) {
+            if (full) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     if constexpr (RPL == 4) *(uint32_t *)(dst + 8 * j) = cj[j];
@@ -1082,21 +1009,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             stl[t & 1][wv][2] = nde >> 16;
         }
         lds_sync();
-        if (defer) {   // (one threshold: held for flush_deferred; uniform sums)
-            uint32_t s0 = 0, s2 = 0, s3 = 0;
-#pragma unroll
-            for (int k = 0; k < WPT; k++) {
-                s0 += stl[0][k][0];
-                s2 += stl[0][k][1];
-                s3 += stl[0][k][2];
-            }
-            dfr.tile = tile;
-            dfr.sc = uni(s0);
-            dfr.nd = uni(s2);
-            dfr.ne = uni(s3);
-            dfr.n = n;
-            dfr.spend = true;
-        } else if (tid == 0) {   // tile statistics (:352-397); ≤ 2048 positions: u32 partial sums
+        if (tid == 0) {   // tile statistics (:352-397); ≤ 2048 positions: u32 partial sums
             uint64_t s0 = 0, s2 = 0, s3 = 0;
 #pragma unroll
             for (int k = 0; k < WPT; k++) {
@@ -1134,127 +1047,6 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
 // One wave per tile (block b → item, XCD-major: the blocks of one XCD, b ≡ x mod 8, take a
 // contiguous range of items, so neighbouring windows meet in that XCD's L2).  Everything the
 // tile needs arrives by one LDS-DMA round trip after the scalar loads of its tile record.
-#if S2C_DENSE_PERSIST
-// A persistent workgroup (WPT waves) per tile slot of a CU: XCD x (blocks b ≡ x mod 8) takes
-// the contiguous items [x0, x1) and its nbx blocks take every nbx-th of them, so the tiles in
-// flight on one XCD are neighbours.  Each tile after the first needs one round trip at its
-// top (piece records, run-slot range, the next item's window): its own window was DMA'd during
-// the previous tile's vote, once the count had freed the LDS; with one threshold the previous
-// tile's body bytes and statistics are stored after that round trip is issued (Deferred).
-__device__ __forceinline__ Win win_vrec(uint32_t rec) {   // lane k of rec: word k of the item's dwin row
-    auto wd = [&](int k) { return (uint32_t)__builtin_amdgcn_readlane((int)rec, k); };
-    Win v;
-    v.tile = wd(0);
-    v.a = wd(1);
-    v.n = wd(2) - v.a;
-    v.cb0 = wd(3);
-    v.lp0 = wd(4);
-    v.nlong = wd(5) - v.lp0;
-    v.pf0 = wd(6);
-    v.npc = wd(7) - v.pf0;
-    v.o0 = wd(8);
-    v.nslot = wd(9) - v.o0;
-    v.qw0 = wd(10);
-    v.nqw = wd(11) - v.qw0;
-    v.W0 = v.a >> 5;
-    v.nwords = (v.n + 31) / 32;
-    return v;
-}
-
-template <int NWP>
-__global__ __launch_bounds__(WT) S2C_DENSE_OCC void k_tile_dense(const DenseArgs d) {
-    extern __shared__ uint4 arena[];   // the window (S2C_DENSE_BYTES layout)
-    __shared__ __attribute__((aligned(16))) uint32_t dcnt[8 * NWP], ncnt[8 * NWP], ccnt[8 * NWP];
-    __shared__ __attribute__((aligned(16))) uint8_t amb[64];
-    __shared__ uint32_t stl[2][WPT][4];
-    const uint32_t b = blockIdx.x;
-    const uint32_t x = b & 7u, per = d.n_items >> 3, rem = d.n_items & 7u;
-    const uint32_t x0 = x * per + min(x, rem), x1 = x0 + per + (x < rem ? 1u : 0u);
-    const uint32_t nbx = (gridDim.x >> 3) + ((gridDim.x & 7u) > x ? 1u : 0u);
-    uint32_t item = x0 + (b >> 3);
-    if (item >= x1) return;   // (uniform: every wave of the block leaves)
-    Win v = win_of(d, item);
-    uint8_t *const buf = (uint8_t *)arena;
-    win_issue<WPT>(d, v, buf);
-    {
-        v16i r;
-        asm volatile("s_load_dwordx16 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(uni_ptr((const uint32_t *)c_amb)) : "memory");
-        if (threadIdx.x == 0) {
-#pragma unroll
-            for (int i = 0; i < 16; i++) ((uint32_t *)amb)[i] = (uint32_t)r[i];
-        }
-    }
-    const uintptr_t fa = (uintptr_t)d.fill;
-    const uint32_t fill0 = (sload1((const uint32_t *)(fa & ~(uintptr_t)3)) >> (8 * (uint32_t)(fa & 3))) & 0xFFu;
-    for (uint32_t k = threadIdx.x; k < 8 * NWP; k += WT) {   // (each vote zeroes its rows again)
-        dcnt[k] = 0;
-        ncnt[k] = 0;
-        ccnt[k] = 0;
-    }
-    constexpr int G = WGD / (NWP / WPT);
-    const uint32_t K = d.kwin;
-    Deferred<NWP> def;
-    def.pend = false;
-    def.spend = false;
-    const bool defer = d.n_thr == 1;
-    for (;;) {
-#ifdef S2C_PROF
-        const unsigned long long t_entry = __builtin_amdgcn_s_memtime();
-#else
-        const unsigned long long t_entry = 0;
-#endif
-        // (the lane's indices re-derived each tile: nothing lane-dependent is hoisted out of
-        // the loop and held in registers through it)
-        uint32_t tid = threadIdx.x;
-        asm volatile("" : "+v"(tid));
-        const uint32_t lane = tid & 63, w = (tid >> 6) * (NWP / WPT) + lane / G;
-        const WinLds wl = win_lds(d, v, buf);
-        if (tid < RUN_PAD) wl.runl[v.nslot + tid] = make_uint2(0u, 0u);   // (the DMA does not write there)
-        uint4 Pp[PFN];
-        uint32_t oe[PFN], pxr[PFN];
-#pragma unroll
-        for (int i = 0; i < PFN; i++) {
-            const uint32_t k = tid + WT * i;
-            Pp[i] = make_uint4(0u, 0u, 0u, 0u);
-            oe[i] = 0;
-            pxr[i] = 0xFFFFFFFFu;
-            if (k < v.npc) {
-                Pp[i] = ((const uint4 *)d.pc)[v.pf0 + k];
-                oe[i] = d.pc[4 * (size_t)(v.pf0 + k + 1) + 2];
-                pxr[i] = d.px[v.pf0 + k];
-            }
-        }
-        const uint32_t W = v.W0 + w;
-        uint32_t cw0 = 0, cw1 = 0;
-        if (w < v.nwords) {
-            cw0 = d.rs[W >= K ? W - K : 0u];
-            cw1 = d.rs[W + 1];
-        }
-        const uint32_t nitem = item + nbx;
-        const bool more = nitem < x1;
-        uint32_t nrec = 0;   // the next item's window row (lane k: word k; waited for where it is issued)
-        if (more) nrec = d.dwin[(size_t)nitem * S2C_DWIN_WORDS + (lane & 15u)];
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the window landed; records, range, next row
-        flush_deferred<NWP>(d, def);   // the previous tile's bytes and statistics
-        cw0 -= v.o0;
-        cw1 -= v.o0;
-        lds_sync();
-        Win vn = v;
-        dense_tile<NWP>(d, v, wl, dcnt, ncnt, ccnt, amb, fill0, Pp, oe, pxr, cw0, cw1, t_entry, stl,
-                        [&]() {
-                            if (more) {
-                                vn = win_vrec(nrec);
-                                win_issue<WPT>(d, vn, buf);
-                            }
-                        },
-                        def, defer, tid);
-        if (!more) break;
-        item = nitem;
-        v = vn;
-    }
-    flush_deferred<NWP>(d, def);
-}
-#else
 template <int NWP>
 __global__ __launch_bounds__(WT) S2C_DENSE_OCC void k_tile_dense(const DenseArgs d) {
     extern __shared__ uint4 arena[];   // the window (S2C_DENSE_BYTES layout)
@@ -1319,29 +1111,13 @@ __global__ __launch_bounds__(WT) S2C_DENSE_OCC void k_tile_dense(const DenseArgs
     cw0 -= v.o0;
     cw1 -= v.o0;
     lds_sync();
-    Deferred<NWP> dfr;
-    dense_tile<NWP>(d, v, wl, dcnt, ncnt, ccnt, amb, fill0, Pp, oe, pxr, cw0, cw1, t_entry, stl, []() {}, dfr, false,
-                    threadIdx.x);
+    dense_tile<NWP>(d, v, wl, dcnt, ncnt, ccnt, amb, fill0, Pp, oe, pxr, cw0, cw1, t_entry, stl, threadIdx.x);
 }
 
-#endif
 
 template <int NWP>
 int launch(const DenseArgs &a, int64_t n, hipStream_t s) {
-    int64_t grid = n;
-#if S2C_DENSE_PERSIST
-    {   // the workgroups the device holds at once (occupancy × CUs, a multiple of the 8 XCDs)
-        int dev = 0, per_cu = 0, ncu = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(&k_tile_dense<NWP>), WT,
-                                                         a.buf_bytes) != hipSuccess ||
-            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return s2c_set_error(S2C_ERR_HIP, "k_tile_dense occupancy query");
-        const int64_t full = std::max<int64_t>((int64_t)per_cu * ncu, 8) & ~(int64_t)7;
-        grid = std::min<int64_t>(n, full);
-    }
-#endif
-    k_tile_dense<NWP><<<(unsigned)grid, WT, a.buf_bytes, s>>>(a);
+    k_tile_dense<NWP><<<(unsigned)n, WT, a.buf_bytes, s>>>(a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? S2C_OK : s2c_set_error(S2C_ERR_HIP, std::string("k_tile_dense: ") + hipGetErrorString(e));
 }
