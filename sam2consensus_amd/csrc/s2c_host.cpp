@@ -483,22 +483,83 @@ static uint64_t pack_seq(Chunk &c, const uint32_t *sp, size_t slen, uint8_t *has
     return q0;
 }
 
-// One SAM record line (not a header line), n includes the trailing '\n' when present.
-static int process_record(Chunk &c, const RefView &rv, std::string &last_name, int64_t &last_ref,
-                          const char *s, size_t n, std::string &emsg) {
-    c.lines_total++;
-    if (s[0] == '@') return S2C_OK;                                   // :195
-    const char *f[10];
-    size_t fl[10];
+// The first ten tab-separated fields of line [s, end) (end after its '\n' when present: the
+// last field split keeps it, as line.split('\t') does, :191); returns how many.
+static int split_fields(const char *s, const char *end, const char **f, size_t *fl, int maxf = 10) {
     int nf = 0;
-    const char *cur = s, *end = s + n;
-    while (nf < 10) {
+    const char *cur = s;
+    while (nf < maxf) {
         const char *t = (const char *)memchr(cur, '\t', end - cur);
         f[nf] = cur;
         if (!t) { fl[nf++] = end - cur; break; }
         fl[nf++] = t - cur;
         cur = t + 1;
     }
+    return nf;
+}
+
+// One line of a parse piece [s, lim): its end (after its '\n', else lim) and split_fields of
+// it, in one pass — 32 bytes per step compared against '\t' and '\n' at once.
+#if defined(__x86_64__)
+__attribute__((target("avx2,bmi"))) static const char *scan_line_avx2(const char *s, const char *lim, const char **f,
+                                                                     size_t *fl, int *nfo) {
+    const __m256i T = _mm256_set1_epi8('\t'), N = _mm256_set1_epi8('\n');
+    int nf = 0;
+    const char *cur = s, *p = s;
+    for (; p + 32 <= lim; p += 32) {
+        const __m256i v = _mm256_loadu_si256((const __m256i *)p);
+        const uint32_t mn = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, N));
+        uint32_t mt = nf < 10 ? (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, T)) : 0u;
+        if (mn) mt &= (mn & (0u - mn)) - 1u;   // (the tabs before the line's '\n')
+        while (mt && nf < 10) {
+            const uint32_t i = (uint32_t)__builtin_ctz(mt);
+            mt &= mt - 1;
+            f[nf] = cur;
+            fl[nf++] = (size_t)(p + i - cur);
+            cur = p + i + 1;
+        }
+        if (mn) {
+            const char *e = p + __builtin_ctz(mn) + 1;
+            if (nf < 10) {
+                f[nf] = cur;
+                fl[nf++] = (size_t)(e - cur);
+            }
+            *nfo = nf;
+            return e;
+        }
+    }
+    const char *nl = (const char *)memchr(p, '\n', lim - p);   // (the piece's last < 32 bytes)
+    const char *e = nl ? nl + 1 : lim;
+    if (nf < 10) nf += split_fields(cur, e, f + nf, fl + nf, 10 - nf);
+    *nfo = nf;
+    return e;
+}
+#endif
+static const char *scan_line(const char *s, const char *lim, const char **f, size_t *fl, int *nfo) {
+#if defined(__x86_64__)
+    if (HAVE_AVX2) return scan_line_avx2(s, lim, f, fl, nfo);
+#endif
+    const char *nl = (const char *)memchr(s, '\n', lim - s);
+    const char *e = nl ? nl + 1 : lim;
+    *nfo = split_fields(s, e, f, fl);
+    return e;
+}
+
+static int process_fields(Chunk &c, const RefView &rv, std::string &last_name, int64_t &last_ref, const char **f,
+                          const size_t *fl, int nf, std::string &emsg);
+// One SAM record line (not a header line), n includes the trailing '\n' when present.
+static int process_record(Chunk &c, const RefView &rv, std::string &last_name, int64_t &last_ref,
+                          const char *s, size_t n, std::string &emsg) {
+    const char *f[10];
+    size_t fl[10];
+    const int nf = s[0] == '@' ? 0 : split_fields(s, s + n, f, fl);
+    return process_fields(c, rv, last_name, last_ref, s[0] == '@' ? nullptr : f, fl, nf, emsg);
+}
+// The record of fields f (nullptr: a line starting with '@' inside the records, :195).
+static int process_fields(Chunk &c, const RefView &rv, std::string &last_name, int64_t &last_ref, const char **f,
+                          const size_t *fl, int nf, std::string &emsg) {
+    c.lines_total++;
+    if (!f) return S2C_OK;                                             // :195
     auto fail = [&](int code, const std::string &m) { emsg = m; return code; };
     if (nf < 6) return fail(S2C_ERR_INDEX, "IndexError: record with < 6 fields (:195)");
     if (fl[5] == 1 && f[5][0] == '*') return S2C_OK;                  // unmapped (:195)
@@ -773,10 +834,12 @@ int parse_window(s2c_parser *p, const char *s, size_t n) {
         c.bx.resize(m / 32 + 64);     // SEQ bytes ≤ m: planes of ≤ m bases, 16-base aligned reads
         c.bq.resize(2 * c.bx.size());  // (no fill: pack_seq zeroes the words it reaches)
         size_t j = 0;
-        while (j < m) {
-            const char *nl = (const char *)memchr(b + j, '\n', m - j);
-            const size_t e = nl ? (size_t)(nl - b) + 1 : m;   // a last line without '\n' counts (Py2)
-            rcs[k] = process_record(c, rv, last_name, last_ref, b + j, e - j, msgs[k]);
+        while (j < m) {   // (a last line without '\n' counts, Py2)
+            const char *f[10];
+            size_t fl[10];
+            int nf;
+            const size_t e = (size_t)(scan_line(b + j, b + m, f, fl, &nf) - b);
+            rcs[k] = process_fields(c, rv, last_name, last_ref, b[j] == '@' ? nullptr : f, fl, nf, msgs[k]);
             if (rcs[k]) return;
             j = e;
         }

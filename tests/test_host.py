@@ -225,6 +225,51 @@ def _batch_digest(path, maxdel_active):
     return h.hexdigest()
 
 
+def _text_digest(text, maxdel_active):
+    try:
+        hb = batch.parse_text(text, maxdel_active, 150)   # (< 4 MB: line by line, split_fields)
+    except (KeyError, IndexError, ValueError, ZeroDivisionError, OverflowError) as e:
+        return type(e).__name__
+    h = hashlib.sha256()
+    for n in ARRAYS:
+        h.update(np.ascontiguousarray(getattr(hb, n)).tobytes())
+    i = hb.info
+    h.update(repr((i.lines_total, i.reads_mapped, i.aligned_bases, i.query_bases, i.header_lines)).encode())
+    return h.hexdigest()
+
+
+def _scan_cases():
+    """Lines whose tabs and newlines fall on and around the file scanner's 32-byte steps."""
+    head = "@SQ\tSN:g\tLN:400\n@SQ\tSN:h\tLN:90\n"
+    out = []
+    for pad in range(0, 40):
+        name = "r" * (1 + pad)
+        rows = [
+            "%s\t0\tg\t%d\t60\t%dM\t*\t0\t0\t%s\t*\n" % (name, 1 + pad, 12 + pad, ("ACGT" * 20)[:12 + pad]),
+            "%s\t0\th\t3\t60\t4M2I3M\t*\t0\t0\tACGTTTACG\tIIIIIIIII\textra\tfields\n" % name,
+            "%s\t4\t*\t0\t0\t*\t*\t0\t0\tACGT\n" % name,                   # unmapped, 10 fields
+            "@CO\tinside the records\n",
+            "%s\t0\tg\t%d\t60\t%dM\t*\t0\t0\t%s" % (name, 5, 7, "NACGT-A"),   # last line, no '\n'
+        ]
+        out.append(head + "".join(rows))
+        out.append(head + rows[0] + "%s\t0\tg\t1\t60\t3M\n" % name + rows[2])   # < 10 fields: IndexError
+    return out
+
+
+def test_file_scanner_splits_like_the_line_parser(tmp_path):
+    """The file parse splits each line in one 32-byte-step pass (scan_line); the sequential
+    feed splits it field by field (split_fields): same batch, same error, on every fuzz / KAT
+    case and on lines whose tabs and newlines sit at every offset of the 32-byte steps."""
+    p = tmp_path / "in.sam"
+    for case in CASES[:200]:
+        opt = o.parse_argv(["-i", "in.sam"] + list(case["args"]))
+        p.write_bytes(case["sam"].encode("latin-1"))
+        assert _batch_digest(str(p), opt.maxdel_active) == _text_digest(case["sam"], opt.maxdel_active), case["name"]
+    for text in _scan_cases():
+        p.write_bytes(text.encode("latin-1"))
+        assert _batch_digest(str(p), True) == _text_digest(text, True), text[:80]
+
+
 def test_parallel_file_parse_equals_sequential(tmp_path, monkeypatch):
     """The threaded file parse (record lines cut into chunks, merged in file order) builds
     the same batch as one thread, and raises the first error in file order."""
