@@ -216,7 +216,8 @@ int  s2c_parser_stream_state(const s2c_parser *p, int64_t *state);
  * table, settings and stream state copied; the partial last line stays in p), so one thread
  * can snapshot / retain *out while another goes on feeding p; attach then puts out's reads
  * (the retained ones) back in front of the reads fed since, takes its stream state and
- * frees it.  Between the two, p and out share no data. */
+ * frees it.  Between the two, p and out share no data.  *out takes no input (feed /
+ * feed_file / end_header: S2C_ERR_ARG). */
 int  s2c_parser_detach(s2c_parser *p, s2c_parser **out);
 int  s2c_parser_attach(s2c_parser *p, s2c_parser *det);
 /* Unsorted input (counts added to running totals batch by batch, s2c_accumulate): keep

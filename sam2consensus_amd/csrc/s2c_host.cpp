@@ -285,6 +285,7 @@ struct s2c_parser {
     int64_t frontier = 0;
     size_t n_kept = 0;
     bool late = false;
+    bool detached = false;   // made by s2c_parser_detach: snapshot / retain / attach only, no input
     std::vector<uint8_t> blob;   // s2c_parser_pack's output
     s2c_parser() { chunks.emplace_back(new Chunk()); }
 };
@@ -734,6 +735,7 @@ int parse_window(s2c_parser *p, const char *s, size_t n);
 
 static int s2c_parser_feed_impl(s2c_parser *p, const char *buf, size_t len) {
     if (!p) return s2c_set_error(S2C_ERR_ARG, "parser is NULL");
+    if (p->detached) return s2c_set_error(S2C_ERR_ARG, "a detached parser takes no input");
     if (p->err) return s2c_set_error(p->err, p->errmsg);
     const char *s = buf, *end = buf + len;
     if (!p->carry.empty()) {
@@ -771,6 +773,7 @@ extern "C" int s2c_parser_feed(s2c_parser *p, const char *buf, size_t len) {
 
 extern "C" int s2c_parser_end_header(s2c_parser *p) {
     if (!p) return s2c_set_error(S2C_ERR_ARG, "parser is NULL");
+    if (p->detached) return s2c_set_error(S2C_ERR_ARG, "a detached parser takes no input");
     if (p->err) return s2c_set_error(p->err, p->errmsg);
     if (!p->carry.empty()) return s2c_set_error(S2C_ERR_ARG, "header does not end with a newline");
     p->in_header = false;
@@ -1120,6 +1123,7 @@ static int reader_open(Reader &rd, const char *path) {
 
 static int s2c_parser_feed_file_impl(s2c_parser *p, const char *path) {
     if (!p || !path) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
+    if (p->detached) return s2c_set_error(S2C_ERR_ARG, "a detached parser takes no input");
     if (p->err) return s2c_set_error(p->err, p->errmsg);
     Reader rd;
     if (const int rc = reader_open(rd, path)) return rc;
@@ -1893,9 +1897,9 @@ static int s2c_parser_detach_impl(s2c_parser *p, s2c_parser **out) {
     d->maxdel = p->maxdel;
     d->in_header = p->in_header;
     d->header_lines = p->header_lines;
-    d->ref_names = p->ref_names;
+    d->ref_names = p->ref_names;   // (the name index stays behind: d parses nothing)
     d->ref_len = p->ref_len;
-    d->ref_idx = p->ref_idx;
+    d->detached = true;
     d->last_name = p->last_name;
     d->last_ref = p->last_ref;
     d->tile_width = p->tile_width;

@@ -104,6 +104,8 @@ def test_detach_attach_round_trip():
     cut = len(sam) // 2
     p.feed(sam[:cut])
     d = p.detach()
+    with pytest.raises(Exception, match="detached parser takes no input"):
+        d.feed(sam[cut:])
     p.feed(sam[cut:])
     p.attach(d)
     assert not d._p
