@@ -253,18 +253,18 @@ __device__ __forceinline__ void reduce_scatter_rows(uint32_t (&R)[4][8], uint32_
 __device__ __forceinline__ void cnt_add1(uint32_t *cnt, uint32_t p) {
     atomicAdd(&cnt[((p >> 5) << 3) | (p & 7u)], 1u << (8 * ((p >> 3) & 3u)));
 }
-// +1 at the tile-relative positions [r0, r1) clipped to [0, lim): whole words 8 dwords at once
+// +1 at the tile-relative positions [r0, r1) clipped to [0, lim), a word at a time: the
+// word's covered positions m add (m >> r) & 0x01010101 to its row dword r (byte j of row r
+// is position 8j + r), at most 8 atomics per word instead of one per position at its ends
 __device__ __forceinline__ void cnt_range(uint32_t *cnt, int32_t r0, int32_t r1, int32_t lim) {
-    int32_t p = max(r0, 0);
-    const int32_t e = max(min(r1, lim), 0);
-    while (p < e) {
-        if ((p & 31) == 0 && p + 32 <= e) {
+    const int32_t p0 = max(r0, 0), e = max(min(r1, lim), 0);
+    for (int32_t wd = p0 >> 5; p0 < e && wd <= (e - 1) >> 5; wd++) {
+        const int32_t lo = max(p0 - 32 * wd, 0), hi = min(e - 32 * wd, 32);
+        const uint32_t m = (hi - lo >= 32 ? 0xFFFFFFFFu : ((1u << (hi - lo)) - 1u)) << lo;
 #pragma unroll
-            for (int r = 0; r < 8; r++) atomicAdd(&cnt[((uint32_t)p >> 2) + r], 0x01010101u);
-            p += 32;
-        } else {
-            cnt_add1(cnt, (uint32_t)p);
-            p++;
+        for (int r = 0; r < 8; r++) {
+            const uint32_t inc = (m >> r) & 0x01010101u;
+            if (inc) atomicAdd(&cnt[((uint32_t)wd << 3) + r], inc);
         }
     }
 }
