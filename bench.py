@@ -482,22 +482,25 @@ def time_file_parse(wl, ref_hb):
         configs.synth_write(wl, path)
         tw = time.perf_counter() - t0
         size = os.path.getsize(path)
-        t0 = time.perf_counter()
-        hb = parse_file(path, configs.maxdel_active(configs.cli_args(wl)), 150)
-        tp = time.perf_counter() - t0
-        same = (hb.info.reads_mapped == ref_hb.info.reads_mapped and hb.info.aligned_bases == ref_hb.info.aligned_bases
-                and hb.info.n_tiles == ref_hb.info.n_tiles)
-        hb.free()
+        runs, same = [], True
+        for _ in range(2):   # (the first right after the write, while its pages are flushed)
+            t0 = time.perf_counter()
+            hb = parse_file(path, configs.maxdel_active(configs.cli_args(wl)), 150)
+            runs.append(time.perf_counter() - t0)
+            same = same and (hb.info.reads_mapped == ref_hb.info.reads_mapped and hb.info.aligned_bases == ref_hb.info.aligned_bases
+                             and hb.info.n_tiles == ref_hb.info.n_tiles)
+            hb.free()
+        tp = min(runs)
     finally:
         try:
             os.remove(path)
             os.rmdir(td)
         except OSError:
             pass
-    return {"parse_s": tp, "file_bytes": size, "file_mb_per_s": size / tp / 1e6, "threads": cpu_threads(),
+    return {"parse_s": tp, "runs_s": runs, "file_bytes": size, "file_mb_per_s": size / tp / 1e6, "threads": cpu_threads(),
             "write_s": tw, "same_batch": same,
-            "what": "libs2c.so s2c_parser_feed_file of the workload's .sam (read, parse, pack, plan) on %d threads"
-                    % cpu_threads()}
+            "what": "libs2c.so s2c_parser_feed_file of the workload's .sam (read, parse, pack, plan) on %d threads, "
+                    "best of %d runs (runs_s)" % (cpu_threads(), len(runs))}
 
 
 def traffic_from_profile(wl):
