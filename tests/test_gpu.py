@@ -144,6 +144,46 @@ def test_c3_samgz_bgzf_reduced_matches_oracle(tmp_path):
         assert open(os.path.join(out, fn), "rb").read() == open(os.path.join(ref, fn), "rb").read()
 
 
+@pytest.mark.parametrize("wl,scale,args", [
+    ("c5", 0.05, ["-c", "0.1,0.5,0.9"]),
+    ("c5", 0.05, ["-c", "0.25", "-m", "5", "-f", "N", "-n", "60"]),
+    ("c5", 0.05, ["-c", "0.75", "-d", "3"]),
+    ("c4", 0.02, ["-c", "0.2,0.6", "-m", "20"]),
+    ("c5", 0.05, ["-c", "0.5"]),
+    ("c2", 0.1, ["-c", "0.3,0.51,0.99", "-n", "70"]),
+    ("c2", 0.1, ["-c", "0.3,0.51", "-n", "70"]),
+], ids=["c5-3thr", "c5-m5-fN-n60", "c5-d3", "c4-m20", "c5-c50", "c2-3thr-n70", "c2-2thr-n70"])
+def test_cli_options_match_c_restatement(tmp_path, wl, scale, args):
+    """The CLI (HIP path) on reduced BASELINE configs under option sets their goldens do not
+    use, against the C restatement (oracle/s2c_oracle_mc.c, itself pinned to the reference's
+    outputs in test_oracle.py) on the same file: every FASTA byte-identical, or the same error
+    (C5 with a 0.1 threshold reaches base sets the reference's IUPAC table lacks: KeyError)."""
+    import subprocess
+    from sam2consensus_amd import configs
+    from sam2consensus_amd.cli import main
+    sam = str(tmp_path / ("%s.sam" % wl))
+    configs.synth_write(wl, sam, scale=scale)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-s", "-C", os.path.join(root, "oracle")], check=True)
+    ref = tmp_path / "ref"
+    r = subprocess.run([os.path.join(root, "oracle", "build", "s2c_oracle_mc"), "16", "-i", sam, "-o", str(ref),
+                        "-p", wl] + args, capture_output=True, text=True, timeout=300)
+    status = [ln for ln in r.stdout.splitlines() if ln.startswith("status: ")][-1][len("status: "):]
+    out = tmp_path / "out"
+    try:
+        rc = main(["-i", sam, "-o", str(out), "-p", wl] + args)
+        got = "ok" if rc == 0 else "rc %d" % rc
+    except (KeyError, IndexError, ValueError, ZeroDivisionError, OverflowError) as e:
+        got = type(e).__name__
+    assert got == status, (got, status)   # (the reference's error where it raises one)
+    if status != "ok":
+        return
+    assert sorted(os.listdir(out)) == sorted(os.listdir(ref)) and os.listdir(ref)
+    for fn in os.listdir(ref):
+        a, b = open(os.path.join(out, fn), "rb").read(), open(os.path.join(ref, fn), "rb").read()
+        assert a == b, (fn, _first_diff(a, b))
+
+
 def test_cli_end_to_end_c1(tmp_path):
     from sam2consensus_amd import configs
     from sam2consensus_amd.cli import main
