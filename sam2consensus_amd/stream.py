@@ -644,6 +644,24 @@ def device_runner(thresholds, min_depth, fill, device=None):
     return DeviceRunner(thresholds, min_depth, fill, device)
 
 
+def header_sort_order(filename):
+    """The SO tag of the file's @HD line (plain or gzip, as the reference opens it, :111-114),
+    or None without one."""
+    import gzip
+    opener = gzip.open if filename.endswith(".gz") else open
+    try:
+        with opener(filename, "rb") as fh:
+            line = fh.readline(1 << 16)
+    except (OSError, EOFError):
+        return None
+    if not line.startswith(b"@HD"):
+        return None
+    for tag in line.rstrip(b"\r\n").split(b"\t")[1:]:
+        if tag.startswith(b"SO:"):
+            return tag[3:].decode("latin-1")
+    return None
+
+
 def consensus_files_streamed(filename, thresholds, prefix, min_depth=1, fill=b"-", nchar=0, maxdel_active=True,
                              device=None, log=None, batch_bytes=DEFAULT_BATCH, tile_width=DEFAULT_TILE):
     """``cli.consensus_files`` in streamed batches (unsorted input: counts accumulated)."""
@@ -652,11 +670,16 @@ def consensus_files_streamed(filename, thresholds, prefix, min_depth=1, fill=b"-
 
     t = {}
     t0 = time.perf_counter()
-    try:
-        res = stream_batches(file_blocks(filename), thresholds, device_runner(thresholds, min_depth, fill, device),
-                             maxdel_active, tile_width, batch_bytes)
-    except NotSorted:
-        res = None   # (the second pass runs after the except block: no live traceback of the first)
+    res = None
+    # a header that declares the records unsorted goes straight to accumulation (the sorted
+    # pass would stop at its second snapshot and start over); any other runs the sorted pass,
+    # which falls back when a read reaches below an emitted tile
+    if header_sort_order(filename) not in ("unsorted", "queryname"):
+        try:
+            res = stream_batches(file_blocks(filename), thresholds, device_runner(thresholds, min_depth, fill, device),
+                                 maxdel_active, tile_width, batch_bytes)
+        except NotSorted:
+            res = None   # (the second pass runs after the except block: no live traceback of the first)
     if res is None:   # counts added batch by batch into running totals in HBM
         res = stream_unsorted(file_blocks(filename), thresholds,
                               DeviceAccumulator(thresholds, min_depth, fill, device), maxdel_active, batch_bytes)

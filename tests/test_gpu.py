@@ -329,8 +329,10 @@ def test_streamed_batches_on_device_match_golden(tmp_path, name, nbatch):
 
 
 def test_cli_streamed_and_unsorted_fallback(tmp_path, monkeypatch):
-    """S2C_STREAM turns on streamed batches in the CLI: C1 (sorted) streams, a shuffled
-    .sam.gz (C3's record order, reduced) falls back to one batch; both == the oracle."""
+    """S2C_STREAM turns on streamed batches in the CLI: C1 (sorted) streams; a shuffled
+    .sam.gz (C3's record order, reduced, SO:unsorted) accumulates counts batch by batch, and so
+    does the same text under a header claiming SO:coordinate, after the sorted pass detects it;
+    all == the oracle."""
     from sam2consensus_amd import configs
     from sam2consensus_amd.cli import main
     monkeypatch.setenv("S2C_STREAM", "64K")
@@ -347,6 +349,17 @@ def test_cli_streamed_and_unsorted_fallback(tmp_path, monkeypatch):
     assert main(["-i", gz, "-o", str(out2), "-m", "10", "-p", "c3s"]) == 0
     want, _ = o.run_path(gz, ["-m", "10", "-p", "c3s"])
     got = {fn: open(os.path.join(out2, fn), "rb").read().decode("latin-1") for fn in os.listdir(out2)}
+    assert got == want
+    # the same records under a header claiming SO:coordinate: the sorted pass runs, detects the
+    # first read below an emitted tile (NotSorted) and the file is re-read in accumulation mode
+    import gzip
+    text = gzip.decompress(open(gz, "rb").read())
+    assert text.startswith(b"@HD\tVN:1.6\tSO:unsorted\n")
+    lie = str(tmp_path / "c3s_lie.sam")
+    open(lie, "wb").write(text.replace(b"SO:unsorted", b"SO:coordinate", 1))
+    out3 = tmp_path / "out3"
+    assert main(["-i", lie, "-o", str(out3), "-m", "10", "-p", "c3s"]) == 0
+    got = {fn: open(os.path.join(out3, fn), "rb").read().decode("latin-1") for fn in os.listdir(out3)}
     assert got == want
 
 

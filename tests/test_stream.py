@@ -272,3 +272,20 @@ def test_file_blocks_read_ahead(tmp_path):
     g = stream.file_blocks(path, 1024)
     assert bytes(next(g)) == data[:1024]
     g.close()
+
+
+def test_header_sort_order(tmp_path):
+    """The streamed CLI reads the @HD SO tag (plain or gzip) to skip the sorted pass of input
+    declared unsorted; no @HD line, or one without SO: None (the sorted pass runs)."""
+    import gzip
+    cases = {"a.sam": (b"@HD\tVN:1.6\tSO:coordinate\n@SQ\tSN:g\tLN:9\n", "coordinate"),
+             "b.sam.gz": (b"@HD\tVN:1.6\tSO:unsorted\n", "unsorted"),
+             "c.sam": (b"@SQ\tSN:g\tLN:9\n@HD\tSO:unsorted\n", None),
+             "d.sam": (b"@HD\tVN:1.6\r\n", None),
+             "e.sam": (b"", None)}
+    for name, (data, want) in cases.items():
+        p = tmp_path / name
+        p.write_bytes(gzip.compress(data) if name.endswith(".gz") else data)
+        assert stream.header_sort_order(str(p)) == want, name
+    assert stream.header_sort_order(str(tmp_path / "missing.sam")) is None
+
