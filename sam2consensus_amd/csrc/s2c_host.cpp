@@ -1151,7 +1151,7 @@ static int s2c_parser_feed_file_impl(s2c_parser *p, const char *path) {
             }
             std::vector<char> &buf = sl.buf;
             if (buf.size() < tail.size() + WIN) buf.resize(tail.size() + WIN + (1 << 20));
-            memcpy(buf.data(), tail.data(), tail.size());
+            if (!tail.empty()) memcpy(buf.data(), tail.data(), tail.size());
             size_t have = tail.size(), cut = 0;
             bool eof = false, err = false;
             for (;;) {
