@@ -583,3 +583,36 @@ def test_dense_windows_mirror_tile_records():
                 b.free()
     finally:
         hb.free()
+
+
+def test_host_code_under_sanitizers(tmp_path):
+    """The host library's parse / plan / streaming paths (s2c_host.cpp) built with AddressSanitizer
+    and UndefinedBehaviorSanitizer (host code only: no GPU code is sanitized) and driven by
+    tests/native/*_drive.cpp over plain and BGZF inputs, 1 and 4 parse threads: clean."""
+    import shutil
+    if not shutil.which("g++"):
+        pytest.skip("g++ not found")
+    src = os.path.join(ROOT, "sam2consensus_amd", "csrc", "s2c_host.cpp")
+    san = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"]
+    obj = str(tmp_path / "host.o")
+    subprocess.run(["g++", "-O1", "-g", "-std=c++17", "-I" + os.path.join(ROOT, "include")] + san + ["-c", src, "-o", obj],
+                   check=True, timeout=600)
+    exe = {}
+    for name in ("parse_drive", "stream_drive"):
+        exe[name] = str(tmp_path / name)
+        subprocess.run(["g++", "-O1", "-g", "-std=c++17", "-I" + os.path.join(ROOT, "include")] + san +
+                       [os.path.join(ROOT, "tests", "native", name + ".cpp"), obj, "-o", exe[name], "-lz", "-lpthread"],
+                       check=True, timeout=300)
+    inputs = {"c2": str(tmp_path / "c2.sam"), "c3": str(tmp_path / "c3.sam.gz"), "c5": str(tmp_path / "c5.sam")}
+    configs.synth_write("c2", inputs["c2"], scale=0.05)
+    configs.synth_write("c3", inputs["c3"], scale=0.005)
+    configs.synth_write("c5", inputs["c5"], scale=0.01)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    runs = [("parse_drive", inputs[w], t) for w in inputs for t in ("1", "4")] + [("stream_drive", inputs["c5"], "4")]
+    for name, path, threads in runs:
+        r = subprocess.run([exe[name], path], capture_output=True, text=True, timeout=600,
+                           env=dict(env, S2C_PARSE_THREADS=threads))
+        out = r.stdout + r.stderr
+        assert r.returncode == 0 and "rc 0" in r.stdout, (name, path, threads, out[-3000:])
+        assert "runtime error" not in out and "AddressSanitizer" not in out, out[-3000:]
