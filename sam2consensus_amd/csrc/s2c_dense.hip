@@ -580,7 +580,10 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         nx += (uint32_t)__popcll(bx2);
         nslow += (uint32_t)__popcll(bs);
     }
-    lds_sync();
+    // (the queued work below is this wave's own — its queue, its pieces' run records, atomic
+    // byte-counter adds — so its LDS writes completing is enough: the other wave's records are
+    // needed only by the count, after the barrier that ends the queued walks)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     PROF_MARK(2);
     // the first 64 queued X runs: their run records now, and their non-ACGT words from HBM,
     // so the round trip overlaps the queued walks and the count (the X pass runs after it)
