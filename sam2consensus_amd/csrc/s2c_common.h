@@ -340,6 +340,47 @@ __device__ __forceinline__ void transpose8(uint32_t (&R)[8]) {
 #pragma unroll
     for (int r = 0; r < 8; r += 2) tswap<1, 0x55555555u>(R[r], R[r + 1]);
 }
+// v_bfi_b32: (m & x) | (~m & y), the mask in an SGPR
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t x, uint32_t y) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(m), "v"(x), "v"(y));
+    return r;
+}
+// tswap with explicit bit-field inserts (two per butterfly), a / b known zero when AZ / BZ
+template <int S, uint32_t M, bool AZ, bool BZ>
+__device__ __forceinline__ void tswapz(uint32_t &a, uint32_t &b) {
+    if constexpr (AZ && BZ) {
+        a = 0u;
+        b = 0u;
+    } else if constexpr (BZ) {
+        b = (a >> S) & M;
+        a &= ~(M << S);
+    } else if constexpr (AZ) {
+        a = (b << S) & (M << S);
+        b &= ~M;
+    } else {
+        const uint32_t na = bfi(M << S, b << S, a);
+        b = bfi(M, a >> S, b);
+        a = na;
+    }
+}
+// transpose8 of planes whose planes NZ .. 7 are zero
+template <int NZ>
+__device__ __forceinline__ void transpose8z(uint32_t (&R)[8]) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        if (r >= NZ) R[r] = R[r + 4] = 0u;
+        else if (r + 4 >= NZ) tswapz<4, 0x0F0F0F0Fu, false, true>(R[r], R[r + 4]);
+        else tswapz<4, 0x0F0F0F0Fu, false, false>(R[r], R[r + 4]);
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        if (r & 2) continue;
+        tswapz<2, 0x33333333u, false, false>(R[r], R[r + 2]);
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r += 2) tswapz<1, 0x55555555u, false, false>(R[r], R[r + 1]);
+}
 
 // ----------------------------------------------------------------- runs (k_reads output)
 struct Run {

@@ -212,41 +212,95 @@ __device__ __forceinline__ void dma16(uint8_t *dst, const uint32_t *src, uint32_
 // LDS bytes of a dma16 region for n dwords (16-byte phase of the source + rounding)
 __host__ __device__ constexpr uint32_t dma16_bytes(uint32_t n) { return (4 * n + 15 + 15) & ~15u; }
 
-// all-reduce of one register over the G adjacent lanes of a word (bound_ctrl on: the move
-// folds into one v_add_u32_dpp per step; every source lane of these patterns exists)
-template <int G>
-__device__ __forceinline__ uint32_t word_allreduce(uint32_t v) {
-    if constexpr (G >= 2) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);    // quad_perm [1,0,3,2]
-    if constexpr (G >= 4) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, true);    // quad_perm [2,3,0,1]
-    if constexpr (G >= 8) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, true);   // row_half_mirror
-    static_assert(G <= 8, "at most 8 lanes per word");
-    return v;
+// Sum of N bit-sliced counters (mod 256: a word's counts are ≤ 255) whose planes NP .. 7 are
+// zero, into 8 planes.  N = 4: two carry-save layers (a + b + c → s + 2k; s + d + 2k → s2 +
+// 2k2), then one ripple s2 + 2k2; one v_bitop3 per full-adder output (xor3 0x96, majority
+// 0xE8), the known-zero inputs folded at compile time.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe8" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// a + b + c with zero-ness known at compile time (za / zb / zc): sum and carry bits
+template <bool ZA, bool ZB, bool ZC>
+__device__ __forceinline__ void fadd(uint32_t a, uint32_t b, uint32_t c, uint32_t &s, uint32_t &k) {
+    constexpr int nz = (ZA ? 0 : 1) + (ZB ? 0 : 1) + (ZC ? 0 : 1);
+    if constexpr (nz == 3) {
+        s = xor3(a, b, c);
+        k = maj3(a, b, c);
+    } else if constexpr (nz == 0) {
+        s = 0u;
+        k = 0u;
+    } else if constexpr (nz == 1) {
+        s = ZA ? (ZB ? c : b) : a;
+        k = 0u;
+    } else {   // two live inputs
+        const uint32_t x = ZA ? b : a, y = ZC ? b : c;
+        s = x ^ y;
+        k = x & y;
+    }
+}
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+template <int N, int NP>
+__device__ __forceinline__ void bsum(const uint32_t (&in)[N][8], uint32_t (&o)[8]) {
+    static_assert(N == 1 || N == 2 || N == 4, "counters summed");
+    if constexpr (N == 1) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) o[i] = in[0][i];
+    } else if constexpr (N == 2) {   // ripple a + b: the carry into plane i is live for 1 ≤ i ≤ NP
+        uint32_t cy = 0;
+        static_for<0, 8>([&](auto ic) {
+            constexpr int I = decltype(ic)::value;
+            uint32_t k;
+            fadd<(I >= NP), (I >= NP), (I == 0 || I > NP)>(in[0][I], in[1][I], cy, o[I], k);
+            cy = k;
+        });
+    } else {
+        // s / k live for planes < NP; s2 for planes ≤ NP, k2 for planes < NP; the ripple's carry
+        // into plane i is live for 2 ≤ i ≤ NP + 1
+        uint32_t s[8], k[8], s2[8], k2[8], cy = 0;
+        static_for<0, 8>([&](auto ic) {
+            constexpr int I = decltype(ic)::value;
+            fadd<(I >= NP), (I >= NP), (I >= NP)>(in[0][I], in[1][I], in[2][I], s[I], k[I]);
+        });
+        static_for<0, 8>([&](auto ic) {
+            constexpr int I = decltype(ic)::value;
+            fadd<(I >= NP), (I >= NP), (I == 0 || I > NP)>(s[I], in[3][I], I ? k[(I + 7) % 8] : 0u, s2[I], k2[I]);
+        });
+        static_for<0, 8>([&](auto ic) {
+            constexpr int I = decltype(ic)::value;
+            uint32_t c2;
+            fadd<(I > NP), (I == 0 || I > NP), (I < 2 || I > NP + 1)>(s2[I], I ? k2[(I + 7) % 8] : 0u, cy, o[I], c2);
+            cy = c2;
+        });
+    }
 }
 
-// Reduce-scatter of the 8 transposed counter rows of 4 counters over the G adjacent lanes of a
-// word: lane g ends with rows g·(8/G) .. g·(8/G) + 8/G − 1 (in R[c][0 ..]) summed over the G
-// lanes.  Step h pairs lanes across bit h of g (G = 8: the first pairing is row_half_mirror,
-// lane i with 7 − i, which flips that bit too); each lane keeps the half of its remaining
-// rows holding its own and adds the partner's copy (v_add_u32_dpp).
-template <int BIT, int N>   // one step: pair across bit BIT of g, N rows held → N / 2
-__device__ __forceinline__ void rs_step(uint32_t (&R)[4][8], uint32_t g) {
-    constexpr int ctrl = BIT == 4 ? 0x141 : (BIT == 2 ? 0x4E : 0xB1);   // row_half_mirror, quad_perm [2,3,0,1] / [1,0,3,2]
-    const bool up = (g & (uint32_t)BIT) != 0;   // keep the upper half of the rows held
-#pragma unroll
-    for (int c = 0; c < 4; c++)
-#pragma unroll
-        for (int r = 0; r < N / 2; r++) {
-            const uint32_t keep = up ? R[c][r + N / 2] : R[c][r], send = up ? R[c][r] : R[c][r + N / 2];
-            R[c][r] = keep + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)send, ctrl, 0xF, 0xF, true);
-        }
+// LDS hand-off between the lanes of one wave (its LDS operations execute in order: no wait)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-template <int G>
-__device__ __forceinline__ void reduce_scatter_rows(uint32_t (&R)[4][8], uint32_t g) {
-    static_assert(G == 1 || G == 2 || G == 4 || G == 8, "lanes per word");
-    if constexpr (G == 8) rs_step<4, 8>(R, g);
-    if constexpr (G >= 4) rs_step<2, (G == 8 ? 4 : 8)>(R, g);
-    if constexpr (G >= 2) rs_step<1, 16 / G>(R, g);
-}
+
+// The counters' exchange in the window's LDS once the count is done (k_tile_dense, after the
+// barrier that ends the count): per wave, plane pairs [4][4 counters][XCH_STRIDE lanes] of
+// uint2 (a padded lane stride: the lanes of a word read different counters on distinct
+// banks), then aliased by the summed rows [word][4 counters][8 rows] at XCH_VROW dwords a word
+constexpr uint32_t XCH_STRIDE = 65;
+constexpr uint32_t XCH_WAVE_BYTES = 4 * 4 * XCH_STRIDE * 8;   // 8,320
+constexpr uint32_t XCH_VROW = 40;                              // 32 row dwords + 8 (conflict-free b64 reads)
 
 // Per-position byte counters in the ROW layout of the transposed counters: tile-relative
 // position p = 32w + 8j + r is byte j of dword 8w + r.
@@ -451,7 +505,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
                                            uint32_t *ncnt, uint32_t *ccnt, const uint8_t *amb, uint32_t fill0,
                                            const uint4 (&Pp)[PFN], const uint32_t (&oe)[PFN], const uint32_t (&pxr)[PFN],
                                            uint32_t cw0, uint32_t cw1, unsigned long long t_entry,
-                                           uint32_t (*stl)[WPT][4], uint32_t tid) {
+                                           uint32_t (*stl)[WPT][4], uint32_t tid, uint8_t *scratch) {
     constexpr int NWPW = NWP / WPT, G = WGD / NWPW, RPL = 8 / G;
 #ifdef S2C_PROF
     unsigned long long prof_t = t_entry;
@@ -758,9 +812,10 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     // runs' parts in the lane's word — bases into the counters (planes from HBM), '-' runs and
     // the N / '-' chars of SEQ into the byte counters (the host keeps a dense tile's candidate
     // runs + long runs ≤ 255 per word)
+    uint32_t ntr = 0;   // long-piece rounds (each adds ≤ 1 per position to a lane's counters)
     if (v.nlong) {
         const int32_t wr = (int32_t)(32 * w);   // tile-relative first position of the lane's word
-        const uint32_t ntr = uni(__ockl_wfred_max_u32(active && g < v.nlong ? (v.nlong - g + G - 1) / G : 0u));
+        ntr = uni(__ockl_wfred_max_u32(active && g < v.nlong ? (v.nlong - g + G - 1) / G : 0u));
         for (uint32_t m = 0; m < ntr; m++) {
             const uint32_t j = g + G * m;
             if (!(active && j < v.nlong)) continue;
@@ -815,7 +870,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         const Rec rc = rec_dec(runl[queue[qcap - 1u - i]]);
         x_events(bxl, bql, rc.q, rc.l, rc.r0, TL, false, dcnt, ncnt, ccnt);
     }
-    lds_sync();   // the byte counters are final
+    lds_sync();   // the byte counters are final, and every wave's count is done: the window's LDS is scratch
     PROF_MARK(4);
     // the byte counters of this lane's rows: read now, used by the vote
     const uint32_t rbase = 8 * w + g * RPL;   // the rows' dword index in the byte counters
@@ -826,28 +881,83 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         rN[rr] = active ? ncnt[rbase + rr] : 0u;
         rX[rr] = active ? ccnt[rbase + rr] : 0u;
     }
-    // ---- counters → byte counts: R[r] byte j = count of position 8j + r
-#pragma unroll
-    for (int c = 0; c < 4; c++) transpose8(C[c]);
-    // this lane's rows g·RPL .. g·RPL + RPL − 1 summed over the word's G lanes by a
-    // reduce-scatter: each step pairs lanes across the top remaining bit of g, each keeps the
-    // half of its rows that holds its own and adds the partner's copy of them (the rows sent
-    // are the other half, selected into the same register first: a DPP source is the same
-    // register in the partner lane)
-    uint32_t R[4][8];
-#pragma unroll
-    for (int c = 0; c < 4; c++)
-#pragma unroll
-        for (int r = 0; r < 8; r++) R[c][r] = C[c][r];
-    reduce_scatter_rows<G>(R, g);
+    // ---- counters → byte counts of this lane's rows g·RPL .. g·RPL + RPL − 1 (row r byte j =
+    //      position 8j + r), summed over the word's G lanes.  The sum is taken while the counters
+    //      are still bit-sliced: every lane puts its four counters' planes into the scratch,
+    //      then each lane adds ONE counter of its word over the SRC lanes that hold it (a
+    //      carry-save sum of bit planes, ~45 instructions) and transposes that one counter —
+    //      where each lane used to transpose all four (192 instructions) and reduce-scatter the
+    //      bytes by DPP (72).  The word's rows go back through the scratch to the lanes voting them.
     uint32_t rA[RPL], rC[RPL], rG[RPL], rT[RPL];
+    {
+        constexpr int SRC = G < 4 ? G : 4;   // lanes summed per counter
+        constexpr int CPL = 4 / SRC;         // counters each lane sums (G = 2: two)
+        constexpr int PARTS = G / SRC;       // G = 8: two half-groups of 4, added by DPP
+        const uint32_t wl = lane / G;        // the lane's word within the wave
+        // G = 8: lanes g and 7 − g (row_half_mirror partners) take the same counter, g < 4 over
+        // lanes 0-3 of the word and 7 − g over lanes 4-7
+        const uint32_t part = PARTS == 2 ? (g >= 4 ? 1u : 0u) : 0u;
+        const uint32_t cb = PARTS == 2 ? min(g, 7u - g) : (g % (uint32_t)SRC) * (uint32_t)CPL;
+        const uint32_t src0 = wl * G + part * SRC;
+        uint2 *xp = (uint2 *)(scratch + wv * XCH_WAVE_BYTES);   // this wave's scratch
+        uint32_t *vp = (uint32_t *)xp;   // the rows (aliases the planes: read before, in wave order)
+        // a lane's count ≤ its record slots + long rounds: planes 0 .. 2·NCH − 1 carry it
+        const uint32_t mxc = 8 * ngrp + (half ? 4u : 0u) + ntr;
+        const uint32_t npl = 32u - (uint32_t)__builtin_clz(mxc | 1u);
+        auto xchg = [&](auto nch_c) {
+            constexpr int NCH = decltype(nch_c)::value;   // plane pairs exchanged
 #pragma unroll
-    for (int rr = 0; rr < RPL; rr++) {   // counts from the planes' sums: X = C|T, Y = G|T, Z = T, V = covered
-        const uint32_t x = R[0][rr], y = R[1][rr], z = R[2][rr], v = R[3][rr];
-        rA[rr] = v - x - y + z;
-        rC[rr] = x - z;
-        rG[rr] = y - z;
-        rT[rr] = z;
+            for (int ch = 0; ch < NCH; ch++)
+#pragma unroll
+                for (int c = 0; c < 4; c++) xp[(ch * 4 + c) * XCH_STRIDE + lane] = make_uint2(C[c][2 * ch], C[c][2 * ch + 1]);
+            wave_lds_sync();
+            uint32_t S[CPL][8];
+#pragma unroll
+            for (int k = 0; k < CPL; k++) {
+                uint32_t in[SRC][8];
+#pragma unroll
+                for (int j = 0; j < SRC; j++) {
+#pragma unroll
+                    for (int ch = 0; ch < 4; ch++) {
+                        uint2 pv = make_uint2(0u, 0u);
+                        if (ch < NCH) pv = xp[(ch * 4 + cb + k) * XCH_STRIDE + src0 + j];
+                        in[j][2 * ch] = pv.x;
+                        in[j][2 * ch + 1] = pv.y;
+                    }
+                }
+                constexpr int NP = 2 * NCH < 8 ? 2 * NCH : 8;   // planes exchanged
+                bsum<SRC, NP>(in, S[k]);
+                // (the sum's planes: ≤ NP + 2 for four counters, NP + 1 for two)
+                transpose8z<(SRC == 4 ? (NP + 2 < 8 ? NP + 2 : 8) : SRC == 2 ? (NP + 1 < 8 ? NP + 1 : 8) : NP)>(S[k]);
+                if constexpr (PARTS == 2) {
+#pragma unroll
+                    for (int r = 0; r < 8; r++) S[k][r] += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)S[k][r], 0x141, 0xF, 0xF, true);
+                }
+            }
+            wave_lds_sync();
+            if (part == 0) {
+#pragma unroll
+                for (int k = 0; k < CPL; k++) {
+                    uint4 *dst = (uint4 *)(vp + wl * XCH_VROW + (cb + k) * 8);
+                    dst[0] = make_uint4(S[k][0], S[k][1], S[k][2], S[k][3]);
+                    dst[1] = make_uint4(S[k][4], S[k][5], S[k][6], S[k][7]);
+                }
+            }
+            wave_lds_sync();
+        };
+        if (npl <= 2) xchg(std::integral_constant<int, 1>{});
+        else if (npl <= 4) xchg(std::integral_constant<int, 2>{});
+        else if (npl <= 6) xchg(std::integral_constant<int, 3>{});
+        else xchg(std::integral_constant<int, 4>{});
+        const uint32_t *vr = vp + wl * XCH_VROW + g * RPL;
+#pragma unroll
+        for (int rr = 0; rr < RPL; rr++) {   // counts from the planes' sums: X = C|T, Y = G|T, Z = T, V = covered
+            const uint32_t x = vr[rr], y = vr[8 + rr], z = vr[16 + rr], v = vr[24 + rr];
+            rA[rr] = v - x - y + z;
+            rC[rr] = x - z;
+            rG[rr] = y - z;
+            rT[rr] = z;
+        }
     }
     PROF_MARK(6);
 
@@ -1114,7 +1224,7 @@ __global__ __launch_bounds__(WT) S2C_DENSE_OCC void k_tile_dense(const DenseArgs
     cw0 -= v.o0;
     cw1 -= v.o0;
     lds_sync();
-    dense_tile<NWP>(d, v, wl, dcnt, ncnt, ccnt, amb, fill0, Pp, oe, pxr, cw0, cw1, t_entry, stl, threadIdx.x);
+    dense_tile<NWP>(d, v, wl, dcnt, ncnt, ccnt, amb, fill0, Pp, oe, pxr, cw0, cw1, t_entry, stl, threadIdx.x, buf);
 }
 
 
@@ -1163,7 +1273,8 @@ int s2c_launch_dense(const s2c_dev *dv, hipStream_t st) {
     // LDS: the largest window of the batch (S2C_DENSE_BYTES, host plan)
     const int64_t lds = dv->dense_lds;
     if (lds <= 0 || lds > S2C_DENSE_LDS || (lds & 15)) return s2c_set_error(S2C_ERR_ARG, "dense_lds outside (0, S2C_DENSE_LDS] or not 16-byte aligned");
-    a.buf_bytes = (uint32_t)lds;
+    // (the window's LDS doubles as the counters' exchange after the count: at least WPT waves' share)
+    a.buf_bytes = (uint32_t)std::max<int64_t>(lds, (int64_t)WPT * XCH_WAVE_BYTES);
     if (dv->tile_max <= 512) return launch<16>(a, n, st);   // (two waves: ≥ 8 words per wave)
     if (dv->tile_max <= 1024) return launch<32>(a, n, st);
     return launch<64>(a, n, st);   // tile_max ≤ 2048 (host plan)
