@@ -88,13 +88,13 @@ def cpu_baseline(workload, scale):
                       % (workload, scale, sp.n_refs, sp.ref_len, a, dt, cpu_model())}
     # calibration against the reference itself: oracle/calibrate_cpu.py ran the
     # reference's main() and the restatement on the same files in the build container
-    cal = os.path.join(ROOT, "profiles", "r04", "cpu_calibration.json")
+    cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")
     if os.path.exists(cal):
         rows = {r["workload"]: r for r in json.load(open(cal))["rows"]}
         r = rows.get(workload)
         if r:
             line["calibration"] = {"oracle_over_reference": r["oracle_over_reference"], "sample": "%s at scale %g"
-                                   % (workload, r["scale"]), "source": "profiles/r04/cpu_calibration.json"}
+                                   % (workload, r["scale"]), "source": "profiles/cpu_calibration.json"}
             line["reference_equivalent_value"] = line["value"] / r["oracle_over_reference"]
             line["sample"] += ("; the reference's own main() runs the same %s sample %.2fx slower than this "
                                "restatement (calibration, build container)" % (workload, r["oracle_over_reference"]))
@@ -370,7 +370,7 @@ def main():
             traffic = traffic_from_profile(wl)
             bound = bound_from_profile(wl)
             line["roofline"] = {
-                "bound": bound.get("bound", "hbm"), "bound_evidence": bound.get("evidence"), "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "bound": bound.get("bound", "unmeasured"), "bound_evidence": bound.get("evidence"), "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic.get("bytes") if traffic else None,
                 "traffic_range": traffic.get("range") if traffic else None,
                 "traffic_frac": (traffic["bytes"] / (tile_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS) if traffic else None,
@@ -459,7 +459,8 @@ def rehearse_shards(full, n, thresholds, min_depth, dev, K, W, bases):
 
 def bound_from_profile(wl):
     """What bounds the dominant kernel, from the committed PMC summary (scripts/bound.py):
-    "valu" when its VALU instructions alone take most of its time, else "hbm"."""
+    "valu" when its VALU instructions alone take most of its time, else "hbm"; with no
+    committed summary for the workload the line says "unmeasured" (no claim without evidence)."""
     p = os.path.join(ROOT, "profiles", "bound_%s.json" % wl)
     if os.path.exists(p):
         with open(p) as fh:

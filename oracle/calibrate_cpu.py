@@ -7,7 +7,7 @@ restatement of sam2consensus.py, timed on a bounded sample on the GPU box — to
 against the reference itself.  This runs the reference's own main() (oracle/ref_harness.py)
 and the restatement on the same C1 / C2-sample SAM files, one thread each, in this
 container, and records both rates (aligned bases / s) and their ratio; bench.py's
-cpu_baseline sample cites it (profiles/r04/cpu_calibration.json).
+cpu_baseline sample cites it (profiles/cpu_calibration.json).
 """
 from __future__ import annotations
 
@@ -27,7 +27,7 @@ from sam2consensus_amd import configs  # noqa: E402
 
 
 def main():
-    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "profiles", "r04", "cpu_calibration.json")
+    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "profiles", "cpu_calibration.json")
     rows = []
     for wl, scale in (("c1", 1.0), ("c2", 0.05), ("c5", 0.016)):
         with tempfile.TemporaryDirectory() as td:

@@ -250,7 +250,7 @@ struct Chunk {
     std::vector<uint32_t> sp;       // the current read's SEQ planes (seq_planes: 4 words per 32 chars)
     // an upper bound of its reads' extents (read_extent's hi): reference hb_ref, position
     // hb_pos in it (a read of an earlier reference ends below that reference's offset);
-    // hb_pos < 0: no read
+    // hb_pos < 0: no bound (no read yet, or a chunk made by s2c_parser_unpack)
     uint32_t hb_ref = 0;
     int64_t hb_pos = -1;
     void bound(uint32_t ref, int64_t pos0, int64_t klen, int64_t L) {
@@ -287,7 +287,17 @@ struct s2c_parser {
     bool late = false;
     bool detached = false;   // made by s2c_parser_detach: snapshot / retain / attach only, no input
     std::vector<uint8_t> blob;   // s2c_parser_pack's output
+    // frees the chunks a retain dropped, off the caller's path; one at a time (the next retain
+    // joins the previous one first) and joined when the parser is freed
+    std::thread freer;
+    void free_later(std::vector<std::unique_ptr<Chunk>> v) {
+        if (freer.joinable()) freer.join();
+        freer = std::thread([](std::vector<std::unique_ptr<Chunk>> w) { w.clear(); }, std::move(v));
+    }
     s2c_parser() { chunks.emplace_back(new Chunk()); }
+    ~s2c_parser() {
+        if (freer.joinable()) freer.join();
+    }
 };
 
 struct s2c_batch {
@@ -1846,7 +1856,7 @@ static void compact_reads(s2c_parser *p, Keep keep, ChunkMay chunk_may, bool eve
     clk.mark("retain copies");
     // the dropped chunks' memory goes back on a thread of its own (hundreds of MB of reads:
     // tens of ms of page unmapping off the producer's path)
-    std::thread([](std::vector<std::unique_ptr<Chunk>> v) { v.clear(); }, std::move(p->chunks)).detach();
+    p->free_later(std::move(p->chunks));
     p->chunks = std::vector<std::unique_ptr<Chunk>>();
     clk.mark("retain free");
     p->chunks.push_back(std::move(k));
@@ -1864,7 +1874,9 @@ static int s2c_parser_retain_impl(s2c_parser *p, int64_t gmin) {
         int64_t lo, hi;
         return read_extent(c, r, off, p->ref_len[r.ref], &lo, &hi) && hi >= gmin;
     }, [&](const Chunk &c, const std::vector<int64_t> &off) {   // (no read of c can reach gmin)
-        return c.hb_pos >= 0 && off[c.hb_ref] + c.hb_pos >= gmin;
+        // (a chunk without bounds — s2c_parser_unpack's — may hold any read: test its reads)
+        if (c.hb_pos < 0) return !c.reads.empty();
+        return off[c.hb_ref] + c.hb_pos >= gmin;
     }, false);
     p->frontier = gmin;
     return S2C_OK;

@@ -80,6 +80,14 @@ def merge_outputs(parts, T):
     return full, b"".join(b"".join(chunks[t]) for t in range(T))
 
 
+def force_collectives():
+    """S2C_FORCE_COLLECTIVES=1: run the exchange collectives even at world size 1 (they are
+    skipped there otherwise) — how a one-GPU box executes the RCCL path once
+    (tests/test_gpu.py::test_rccl_exchange_at_world_one)."""
+    import os
+    return os.environ.get("S2C_FORCE_COLLECTIVES", "0") not in ("", "0")
+
+
 def _tensor_device(group):
     import torch
     import torch.distributed as dist
@@ -116,13 +124,14 @@ def gather_results(fetched, sub, rank, world, T, group=None, timing=None):
 
     t0 = mark("start", time.perf_counter())
     st = torch.from_numpy(np.ascontiguousarray(stats).view(np.int64).copy()).to(dev)
-    if world > 1:
+    coll = world > 1 or force_collectives()
+    if coll:
         dist.reduce(st, dst=0, op=dist.ReduceOp.SUM, group=group)   # record stats of cut references
     t0 = mark("stats_reduce", t0, st.numel() * 8)
     offs = np.asarray(offs, dtype=np.uint64)
     meta = torch.tensor([sub.t0, sub.t1, len(offs), len(out)], dtype=torch.int64, device=dev)
     metas = [torch.empty_like(meta) for _ in range(world)]
-    dist.all_gather(metas, meta, group=group) if world > 1 else metas.__setitem__(0, meta)
+    dist.all_gather(metas, meta, group=group) if coll else metas.__setitem__(0, meta)
     metas = [m.cpu().tolist() for m in metas]
     t0 = mark("meta", t0, 32)
     mo = max(m[2] for m in metas)
@@ -132,7 +141,7 @@ def gather_results(fetched, sub, rank, world, T, group=None, timing=None):
     b_t = torch.zeros(mb, dtype=torch.uint8, device=dev)
     if len(out):
         b_t[: len(out)] = torch.from_numpy(np.frombuffer(out, dtype=np.uint8).copy()).to(dev)
-    if world > 1:
+    if coll:
         os_ = [torch.empty_like(o_t) for _ in range(world)] if rank == 0 else None
         bs_ = [torch.empty_like(b_t) for _ in range(world)] if rank == 0 else None
         dist.gather(o_t, os_, dst=0, group=group)
@@ -175,10 +184,3 @@ def exchange_volumes(full, subs):
             "batch_bytes_total": b_full, "batch_bytes_over_shards": b_sum,
             "dup_bytes": b_sum - b_full,
             "cuts": cuts, "count_merge_bytes": cuts * seam_pos * 24}
-
-
-def run_sharded(hb, rank, world, thresholds, runner, group=None):
-    """Run this rank's shard with ``runner(sub) -> (stats, offs, out)`` and merge on rank 0.
-    Returns (stats, offs, out) of the whole batch on rank 0, None elsewhere."""
-    sub = sub_batch(hb, rank, world)
-    return gather_results(runner(sub), sub, rank, world, len(thresholds), group)

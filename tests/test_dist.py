@@ -232,3 +232,16 @@ def test_distributed_parse_matches_reference(world, block, tmp_path):
         assert g[1] == _virtual(hb, opt, 1)
         i = hb.info
         assert g[2] == (i.header_lines, i.lines_total, i.reads_mapped)
+
+
+def test_forced_collectives_at_world_one(monkeypatch):
+    """S2C_FORCE_COLLECTIVES=1 runs the exchange collectives that world size 1 skips (the
+    path tests/test_gpu.py::test_rccl_exchange_at_world_one runs over RCCL on the GPU box):
+    here over gloo, the distributed parse and the gather == the reference."""
+    monkeypatch.setenv("S2C_FORCE_COLLECTIVES", "1")
+    big = _big_case()
+    cases = [(big, []), (big, ["-c", "0.25,0.75"])]
+    got = _run_dparse(1, cases, [], 400)
+    assert [g[0] for g in got] == ["ok", "ok"]
+    for (sam, args), g in zip(cases, got):
+        assert g[1] == o.run_case(sam, args)["files"]

@@ -205,6 +205,37 @@ def _free_port():
     return p
 
 
+def test_rccl_exchange_at_world_one(tmp_path):
+    """The multi-GPU exchange over RCCL with device tensors, on this box's one GPU: a 1-rank
+    `nccl` process group with S2C_FORCE_COLLECTIVES=1, so the collectives that world size 1
+    skips run anyway — dparse's all-reduces and all_to_all of the read blobs, shard.gather_results'
+    reduce / all_gather / gather of the stats and bodies.  The merged C2 files == the reference's."""
+    import json
+    import subprocess
+    import sys
+    from sam2consensus_amd import configs
+    g = CONFIGS["c2"]
+    path = str(tmp_path / g["sam_file"])
+    configs.synth_write("c2", path)
+    opt = o.parse_argv(["-i", path] + g["args"])
+    res = tmp_path / "sha.json"
+    code = (
+        "import hashlib, json, sys\n"
+        "import torch.distributed as dist\n"
+        "from sam2consensus_amd import cli\n"
+        "files = cli.consensus_files_sharded(%r, %r, %r, %d, %r, %d, %r)\n"
+        "assert not dist.is_initialized()\n"
+        "json.dump({k.decode('latin-1'): hashlib.sha256(v).hexdigest() for k, v in files.items()}, open(%r, 'w'))\n"
+        % (path, opt.thresholds, opt.prefix.encode(), opt.min_depth, opt.fill.encode(), opt.n, opt.maxdel_active,
+           str(res)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()), S2C_FORCE_COLLECTIVES="1", S2C_DIST_BACKEND="nccl",
+               PYTHONPATH=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, timeout=240)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    assert json.load(open(res)) == {k: v["sha256"] for k, v in g["files"].items()}
+
+
 def test_cli_torchrun_distributed_parse(tmp_path):
     """The multi-GPU CLI (2 ranks under torchrun, the file parsed once across them —
     sam2consensus_amd/dparse.py — each rank's tile range on the device, bodies gathered):

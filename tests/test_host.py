@@ -128,6 +128,30 @@ def test_text_and_file_and_gzip_parse_agree():
         _same(h, hbs[0])
 
 
+def test_retain_after_unpack_keeps_reads(tmp_path):
+    """Chunks made by s2c_parser_unpack carry no extent bound; a retain after an unpack must
+    test their reads instead of dropping the chunk (advisor, round 4): retain(0) keeps every
+    read, so the batch equals the one parsed from the text."""
+    from sam2consensus_amd.dparse import BlockParser
+    p = str(tmp_path / "c.sam")
+    configs.synth_write("c2", p, scale=0.02)
+    text = open(p, "rb").read()
+    hdr = b"".join(line + b"\n" for line in text.split(b"\n") if line.startswith(b"@"))
+    src = BlockParser(False, 150)
+    src.feed(text)
+    blob = src.pack(0, 1 << 40)
+    src.close()
+    dst = BlockParser(False, 150)
+    dst.feed(hdr)
+    dst.unpack(blob)
+    _lib.check(_lib.lib.s2c_parser_retain(dst._p, 0))
+    got = dst.finish()
+    dst.close()
+    want = batch.parse_text(text.decode("latin-1"), maxdel_active=False)
+    assert len(np.asarray(want.pc)) > 1000
+    _same(got, want)
+
+
 def test_bgzf_block_parallel_inflate(tmp_path):
     """synth_write's .sam.gz is BGZF (the blocked gzip of bgzip / samtools): it reads back as
     the same text through Python's gzip, and the parser's block-parallel inflate gives the

@@ -289,3 +289,95 @@ def test_header_sort_order(tmp_path):
         assert stream.header_sort_order(str(p)) == want, name
     assert stream.header_sort_order(str(tmp_path / "missing.sam")) is None
 
+
+
+def _slow_stages(monkeypatch, log, delay=0.1):
+    """Make the pipelined stage (a detached parser's snapshot on the s2c-stage helper thread)
+    slow and record, for the feeding parser, how many bytes were fed and whether a stage was
+    in flight when the byte at ``log['mark']`` went in."""
+    import threading
+    import time
+    snap, feed = stream.StreamParser.snapshot, stream.StreamParser.feed
+
+    def slow_snapshot(self):
+        if threading.current_thread().name.startswith("s2c-stage"):
+            log["in_stage"] += 1
+            try:
+                time.sleep(delay)
+                return snap(self)
+            finally:
+                log["in_stage"] -= 1
+        return snap(self)
+
+    def logged_feed(self, data):
+        n0 = log["fed"]
+        log["fed"] += len(data)
+        if n0 <= log["mark"] < log["fed"]:
+            log["mark_in_stage"] = log["in_stage"] > 0
+        return feed(self, data)
+
+    monkeypatch.setattr(stream.StreamParser, "snapshot", slow_snapshot)
+    monkeypatch.setattr(stream.StreamParser, "feed", logged_feed)
+
+
+def _cli_like(sam, args, block, batch_bytes):
+    """The CLI's streamed driver on the CPU model: sorted batches, or on NotSorted the
+    accumulation pass over the whole input; (status, files)."""
+    try:
+        try:
+            return "ok", _stream(sam, args, block, batch_bytes)[1]
+        except stream.NotSorted:
+            return "ok", _stream_unsorted(sam, args, block, batch_bytes)[1]
+    except (KeyError, IndexError, ValueError, ZeroDivisionError, OverflowError) as e:
+        return type(e).__name__, {}
+
+
+def _with_line(sam, frac, line):
+    head = [ln for ln in sam.splitlines(True) if ln.startswith("@")]
+    body = [ln for ln in sam.splitlines(True) if not ln.startswith("@")]
+    k = int(len(body) * frac)
+    out = "".join(head + body[:k] + [line] + body[k:])
+    return out, len("".join(head + body[:k]).encode("latin-1"))
+
+
+def test_late_read_fed_while_a_stage_runs(monkeypatch):
+    """Pipelined snapshots (advisor, round 4): a read that reaches already-emitted positions,
+    fed while the previous batch's snapshot / retain runs on the helper thread, is caught
+    (NotSorted) — and the CLI's fallback gives the reference's bytes, as the serial order does."""
+    sam, at = _with_line(_sorted_case(), 0.6, "late\t0\ta\t1\t60\t30M\t*\t0\t0\t%s\t*\n" % ("C" * 30))
+    size = len(sam.encode("latin-1"))
+    log = {"fed": 0, "in_stage": 0, "mark": at, "mark_in_stage": None}
+    _slow_stages(monkeypatch, log)
+    monkeypatch.setenv("S2C_STREAM_PIPE", "1")
+    with pytest.raises(stream.NotSorted):
+        _stream(sam, [], block=97, batch_bytes=size // 3)
+    assert log["mark_in_stage"] is True   # (the late read really went in during a stage)
+    want = o.run_case(sam, [])
+    assert want["status"] == "ok"
+    for pipe in ("1", "0"):
+        monkeypatch.setenv("S2C_STREAM_PIPE", pipe)
+        assert _cli_like(sam, [], 97, size // 3) == ("ok", want["files"]), pipe
+
+
+@pytest.mark.parametrize("late_frac", [None, 0.2, 0.5])
+def test_feed_error_while_a_stage_runs(monkeypatch, late_frac):
+    """A read-pass error (bad POS, :201) fed while a stage is in flight — alone, after a late
+    read held by the in-flight stage (0.2), or after one fed during it (0.5): the pipelined and
+    the serial driver end with the reference's exception class."""
+    sam, at = _with_line(_sorted_case(), 0.6, "bad\t0\tb\tx\t60\t20M\t*\t0\t0\t%s\t*\n" % ("A" * 20))
+    if late_frac is not None:
+        sam, _ = _with_line(sam, late_frac, "late\t0\ta\t1\t60\t30M\t*\t0\t0\t%s\t*\n" % ("C" * 30))
+        at += len("late\t0\ta\t1\t60\t30M\t*\t0\t0\t\t*\n") + 30
+    size = len(sam.encode("latin-1"))
+    want = o.run_case(sam, [])
+    assert want["status"] == "ValueError"
+    log = {"fed": 0, "in_stage": 0, "mark": at, "mark_in_stage": None}
+    _slow_stages(monkeypatch, log)
+    got = {}
+    for pipe in ("1", "0"):
+        monkeypatch.setenv("S2C_STREAM_PIPE", pipe)
+        log.update(fed=0, mark_in_stage=None)
+        got[pipe] = _cli_like(sam, [], 97, size // 3)
+        if pipe == "1":
+            assert log["mark_in_stage"] is True
+    assert got["1"] == got["0"] == ("ValueError", {})
