@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define S2C_ABI_VERSION 11
+#define S2C_ABI_VERSION 12
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define S2C_OK            0
@@ -131,9 +131,19 @@ int s2c_layout(int64_t *out, int n);
 #define S2C_TILE_DENSE    4  /* routed to k_tile_dense (one item, no insertion keys); its long list (lp[lp0, lp1)) holds
                                  piece indices, walked by the kernel; other tiles list run slots (k_reads) */
 #define S2C_ITEM_WORDS    4  /* work item {tile, chunk, l0, l1}: the tile's layers [l0, l1) */
-#define S2C_DWIN_WORDS   16  /* dense item's window {tile, a, b, cb0, lp0, lp1, pf0, pf1, o0, o1, qw0, qw1, 0, 0, 0, 0}:
+#define S2C_DWIN_WORDS   16  /* dense item's window {tile, a, b, cb0, lp0, lp1, pf0, pf1, o0, o1, qw0, qw1, dpc0, 0, 0, 0}:
                                 the words of its tile record k_tile_dense needs, in item order (one
-                                16-dword scalar load per tile instead of item → tile → record) */
+                                16-dword scalar load per tile instead of item → tile → record); dpc0 (ABI 12):
+                                the first of its window's compact piece records (s2c_batch_arrays.dpc) */
+/* k_tile_dense's compact piece records (ABI 12): one per piece of each dense item's window, in
+   window order, 3 words {rs | qh' << 12 | nops << 25, oj | len(SEQ) << 13 | flags << 24, px}:
+   rs = start position − 32·(first tile word) + 2048 (12 bits), qh' = qh − 2·qw0 (13 bits),
+   nops = op slots of the piece (7 bits), oj = op slot − o0 (13 bits), len(SEQ) (11 bits), the
+   piece's flags and its px word.  A tile whose window holds a piece beyond these fields
+   (len(SEQ) > S2C_DPC_SLEN_MAX, more than S2C_DPC_NOPS_MAX op slots, kwin > 64) is not dense. */
+#define S2C_DPC_WORDS     3
+#define S2C_DPC_SLEN_MAX  2047
+#define S2C_DPC_NOPS_MAX  127
 #define S2C_EPI_KEYS    256  /* insertion keys per tile k_tile's epilogue holds in LDS */
 /* insertion columns per tile k_tile's epilogue holds in LDS, by words per tile */
 #define S2C_LDS_COLS(nwp) ((nwp) <= 16 ? 640 : ((nwp) == 32 ? 448 : 192))
@@ -296,6 +306,7 @@ typedef struct {
     int64_t layers_dense;      /* 1: the dense tiles' layered windows are built too (counts-only modes) */
     int64_t layers_built;      /* 1: the layered windows (lly ..., tile word 20) are built (s2c_batch_layers*);
                                   0 for a fresh snapshot or shard */
+    int64_t n_dpc;             /* compact piece records of the dense items' windows (ABI 12) */
 } s2c_batch_info;
 
 typedef struct {               /* host pointers into the batch (valid until s2c_batch_free) */
@@ -333,6 +344,7 @@ typedef struct {               /* host pointers into the batch (valid until s2c_
     const uint32_t *dwin;      /* [n_dense][S2C_DWIN_WORDS] the dense items' windows */
     const uint32_t *lpx;       /* [n_lpieces] px of the layered pieces (ABI 11: k_tile takes the 'N' of
                                   S2C_PF_XFEW pieces from here instead of scanning the non-ACGT plane) */
+    const uint32_t *dpc;       /* [n_dpc][S2C_DPC_WORDS] compact piece records of the dense items' windows (ABI 12) */
 } s2c_batch_arrays;
 
 /* Build the batch's layered windows (s2c_batch_arrays lly .. lbx, tile word 20) if not yet
@@ -434,6 +446,7 @@ typedef struct {
     int64_t   layers_built;    /* the batch's info.layers_built: every launch with work items refuses 0 */
     const uint32_t *dwin;      /* [n_dense][S2C_DWIN_WORDS] s2c_batch_arrays.dwin, filtered like dense */
     const uint32_t *lpx;       /* [n_lpieces] s2c_batch_arrays.lpx (ABI 11; required with n_layers > 0) */
+    const uint32_t *dpc;       /* [n_dpc][S2C_DPC_WORDS] s2c_batch_arrays.dpc (ABI 12; required with n_dense > 0) */
 } s2c_dev;
 
 /* Sizes (bytes) of every workspace / output buffer for a batch and T thresholds. */

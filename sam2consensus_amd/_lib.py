@@ -29,6 +29,7 @@ S2C_TILE_WORDS = 24
 S2C_LY_MAIN = 0xFFFFFFFF
 S2C_ITEM_WORDS = 4
 S2C_DWIN_WORDS = 16
+S2C_DPC_WORDS = 3     # compact piece records of the dense windows (ABI 12)
 S2C_CODE_FILL = 0
 S2C_SHORT_MOTIF = 16
 S2C_TILE_DEEP, S2C_TILE_GENERAL, S2C_TILE_DENSE = 1, 2, 4
@@ -57,7 +58,7 @@ class BatchInfo(C.Structure):
         "aligned_bases", "query_bases", "n_pieces", "n_ops", "n_tokens", "n_qwords", "n_words",
         "n_tiles", "n_items", "n_dense", "n_deep", "n_long", "n_rlist", "kwin", "tile_max", "chunk",
         "n_ins", "n_ins_bases", "n_bkt", "n_lng", "n_cols", "runs_max", "dense_lds", "n_layers", "n_lpieces", "n_lops",
-        "n_lqwords", "layers_dense", "layers_built")]
+        "n_lqwords", "layers_dense", "layers_built", "n_dpc")]
 
 
 _P64 = C.POINTER(C.c_int64)
@@ -67,7 +68,7 @@ _P32 = C.POINTER(C.c_uint32)
 class BatchArrays(C.Structure):
     _fields_ = [("ref_len", _P64), ("ref_off", _P64), ("ref_cov_reads", _P64)] + \
         [(n, _P32) for n in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "rlist", "lp", "wtile",
-                             "ps", "lly", "lpc", "lops", "lbq", "lbx", "px", "dwin", "lpx")]
+                             "ps", "lly", "lpc", "lops", "lbq", "lbx", "px", "dwin", "lpx", "dpc")]
 
 
 class SynthSpec(C.Structure):
@@ -95,7 +96,7 @@ class Dev(C.Structure):
         ("runs", _VP), ("ibkt", _VP), ("ilong", _VP), ("ilong_n", _VP), ("counts", _VP),
         ("ins_cols", _VP), ("ins_chr", _VP), ("n_cols", C.c_int64),
         ("tile_stats", _VP), ("blk_len", _VP), ("out", _VP), ("out_cap", C.c_int64), ("layers_dense", C.c_int64),
-        ("px", _VP), ("layers_built", C.c_int64), ("dwin", _VP), ("lpx", _VP)]
+        ("px", _VP), ("layers_built", C.c_int64), ("dwin", _VP), ("lpx", _VP), ("dpc", _VP)]
 
 
 class WsSizes(C.Structure):

@@ -106,6 +106,7 @@ class HostBatch:
         self.rlist = _view(a.rlist, i.n_rlist, np.uint32)
         self.px = _view(a.px, i.n_pieces, np.uint32)   # non-ACGT SEQ offsets of S2C_PF_XFEW pieces
         self.dwin = _view(a.dwin, i.n_dense * L.S2C_DWIN_WORDS, np.uint32).reshape(-1, L.S2C_DWIN_WORDS)
+        self.dpc = _view(a.dpc, i.n_dpc * L.S2C_DPC_WORDS, np.uint32).reshape(-1, L.S2C_DPC_WORDS)
         self.lp = _view(a.lp, i.n_long, np.uint32)
         self.wtile = _view(a.wtile, i.n_words, np.uint32)
         self.names = [lib.s2c_batch_ref_name(self._b, k).decode("latin-1") for k in range(i.n_refs)]

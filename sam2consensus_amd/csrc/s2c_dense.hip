@@ -67,7 +67,7 @@ __constant__ __attribute__((aligned(16))) uint8_t c_amb[64] = {
 };
 
 struct DenseArgs {
-    const uint32_t *rs, *pc, *ops, *bq, *bx, *tiles, *items, *lp, *px, *dwin;
+    const uint32_t *rs, *pc, *ops, *bq, *bx, *tiles, *items, *lp, *dwin, *dpc;
     const double *thresholds;
     uint64_t *tile_stats, *blk_len;
     uint8_t *out;
@@ -157,6 +157,21 @@ struct DenseMem {
     __device__ __forceinline__ uint32_t p1(uint64_t w) const { return bq[2 * w + 1]; }
     __device__ __forceinline__ uint32_t x(uint64_t w) const { return bx[w]; }
 };
+
+// A compact piece record of the item's window (s2c.h S2C_DPC_WORDS; ABI 12) decoded: rs = its
+// start relative to the tile's first word + REC_BIAS, q = query base of SEQ[0] in the window's
+// planes, its op slots [j, j + nops) in the window, len(SEQ), flags (x: word 0, y: word 1)
+struct DPiece {
+    uint32_t rs, q, nops, j, slen, fl;
+};
+__device__ __forceinline__ DPiece dpc_dec(uint32_t c0, uint32_t c1) {
+    return DPiece{c0 & 0xFFFu, 16u * ((c0 >> 12) & 0x1FFFu), c0 >> 25, c1 & 0x1FFFu, (c1 >> 13) & 0x7FFu, c1 >> 24};
+}
+__device__ __forceinline__ uint3 dpc_load(const DenseArgs &d, uint32_t i) { return ((const uint3 *)d.dpc)[i]; }
+// rec_enc from a biased start (rs = tile-relative start + REC_BIAS)
+__device__ __forceinline__ uint2 rec_enc_b(uint32_t rs, uint32_t len, uint32_t q) {
+    return make_uint2(rs | ((rs + len) << 16), q - rs);
+}
 
 constexpr int WGD = 64;   // one wave per tile
 constexpr int GSD = 8;    // records per counting group (one Harley–Seal tree)
@@ -299,7 +314,10 @@ __device__ __forceinline__ void wave_lds_sync() {
 // uint2 (a padded lane stride: the lanes of a word read different counters on distinct
 // banks), then aliased by the summed rows [word][4 counters][8 rows] at XCH_VROW dwords a word
 constexpr uint32_t XCH_STRIDE = 65;
-constexpr uint32_t XCH_WAVE_BYTES = 4 * 4 * XCH_STRIDE * 8;   // 8,320
+#ifndef S2C_XCH_NCH_MAX
+#define S2C_XCH_NCH_MAX 4
+#endif
+constexpr uint32_t XCH_WAVE_BYTES = S2C_XCH_NCH_MAX * 4 * XCH_STRIDE * 8;   // 8,320
 constexpr uint32_t XCH_VROW = 40;                              // 32 row dwords + 8 (conflict-free b64 reads)
 
 // Per-position byte counters in the ROW layout of the transposed counters: tile-relative
@@ -362,39 +380,6 @@ __device__ __forceinline__ void x_events(const uint32_t *bxl, const uint2 *bql, 
     }
 }
 
-// x_events with the first 8 words (xs: non-ACGT plane, ps: base planes, words q/32 ..) loaded
-// by the caller
-__device__ __forceinline__ void x_events_pre(const uint32_t *bxl, const uint2 *bql, const uint32_t (&xs)[8],
-                                             const uint2 (&ps)[8], uint32_t q, uint32_t l, int32_t r0, int32_t lim,
-                                             bool drop, uint32_t *dcnt, uint32_t *ncnt, uint32_t *ccnt) {
-    const uint32_t wa = q >> 5, wb = (q + l - 1) >> 5;
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-        const uint32_t qw = wa + u;
-        const int32_t b0 = (int32_t)(32 * qw) - (int32_t)q;
-        uint32_t xm = qw <= wb ? xs[u] : 0u;
-        if (b0 < 0) xm &= 0xFFFFFFFFu << (uint32_t)(-b0);
-        if (b0 + 32 > (int32_t)l) xm &= 0xFFFFFFFFu >> (uint32_t)(b0 + 32 - (int32_t)l);
-        xm &= ~ps[u].y;
-        while (xm) {
-            const uint32_t bit = (uint32_t)__builtin_ctz(xm);
-            xm &= xm - 1;
-            const int32_t r = r0 + b0 + (int32_t)bit;
-            if (r < 0 || r >= lim) continue;
-            if ((ps[u].x >> bit) & 1u) {
-                cnt_add1(ccnt, (uint32_t)r);
-                if (!drop) cnt_add1(dcnt, (uint32_t)r);
-            } else {
-                cnt_add1(ncnt, (uint32_t)r);
-            }
-        }
-    }
-    if (wb >= wa + 8) {   // (runs over more than 8 words): the rest from word wa + 8 on
-        const uint32_t q2 = 32 * (wa + 8);
-        x_events(bxl, bql, q2, q + l - q2, r0 + (int32_t)(q2 - q), lim, drop, dcnt, ncnt, ccnt);
-    }
-}
-
 // lane index among the active lanes of a ballot below this one
 __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -431,7 +416,7 @@ __device__ __forceinline__ uint32_t byte_bits(uint32_t m) { return ((m & 0x80808
 
 // A tile's window (uniform values from its tile record; S2C_TILE_WORDS layout)
 struct Win {
-    uint32_t tile, a, n, cb0, pf0, npc, o0, nslot, qw0, nqw, W0, nwords, lp0, nlong;
+    uint32_t tile, a, n, cb0, pf0, npc, o0, nslot, qw0, nqw, W0, nwords, lp0, nlong, dpc0;
 };
 __device__ __forceinline__ Win win_of(const DenseArgs &d, uint32_t item) {
     Win v;
@@ -452,6 +437,7 @@ __device__ __forceinline__ Win win_of(const DenseArgs &d, uint32_t item) {
     v.nslot = (uint32_t)r[9] - v.o0;
     v.qw0 = (uint32_t)r[10];
     v.nqw = (uint32_t)r[11] - v.qw0;
+    v.dpc0 = (uint32_t)r[12];
     v.W0 = v.a >> 5;
     v.nwords = (v.n + 31) / 32;
     return v;
@@ -503,7 +489,7 @@ constexpr int PFN = S2C_DENSE_PFN;   // piece records per thread loaded with the
 template <int NWP>
 __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, const WinLds &L, uint32_t *dcnt,
                                            uint32_t *ncnt, uint32_t *ccnt, const uint8_t *amb, uint32_t fill0,
-                                           const uint4 (&Pp)[PFN], const uint32_t (&oe)[PFN], const uint32_t (&pxr)[PFN],
+                                           const uint3 (&Pc)[PFN],
                                            uint32_t cw0, uint32_t cw1, unsigned long long t_entry,
                                            uint32_t (*stl)[WPT][4], uint32_t tid, uint8_t *scratch) {
     constexpr int NWPW = NWP / WPT, G = WGD / NWPW, RPL = 8 / G;
@@ -537,40 +523,35 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     const uint32_t nit = ABL(4) ? 0u : nitw;
     uint32_t opw[PFN];   // the pieces' first op words, read together
 #pragma unroll
-    for (int u = 0; u < PFN; u++) opw[u] = (tid + WT * u < npc) ? opl[Pp[u].z - o0] : 0u;
+    for (int u = 0; u < PFN; u++) opw[u] = (tid + WT * u < npc) ? opl[Pc[u].y & 0x1FFFu] : 0u;
     for (uint32_t it = 0; it < nit; it++) {
         const uint32_t k = tid + WT * it;
-        uint4 P = Pp[0];
-        uint32_t oend = oe[0], w0 = opw[0], pxv = pxr[0];
+        uint3 P = Pc[0];
+        uint32_t w0 = opw[0];
 #pragma unroll
         for (int u = 1; u < PFN; u++) {   // (the loaded records by a select chain)
-            P.x = it == (uint32_t)u ? Pp[u].x : P.x;
-            P.y = it == (uint32_t)u ? Pp[u].y : P.y;
-            P.z = it == (uint32_t)u ? Pp[u].z : P.z;
-            P.w = it == (uint32_t)u ? Pp[u].w : P.w;
-            oend = it == (uint32_t)u ? oe[u] : oend;
+            P.x = it == (uint32_t)u ? Pc[u].x : P.x;
+            P.y = it == (uint32_t)u ? Pc[u].y : P.y;
+            P.z = it == (uint32_t)u ? Pc[u].z : P.z;
             w0 = it == (uint32_t)u ? opw[u] : w0;
-            pxv = it == (uint32_t)u ? pxr[u] : pxv;
         }
         const bool in = k < npc;
         if (it >= (uint32_t)PFN && in) {   // (windows of more than WT·PFN pieces)
-            P = ((const uint4 *)d.pc)[pf0 + k];
-            oend = d.pc[4 * (size_t)(pf0 + k + 1) + 2];
-            w0 = opl[P.z - o0];
-            pxv = d.px[pf0 + k];
+            P = dpc_load(d, v.dpc0 + k);
+            w0 = opl[P.y & 0x1FFFu];
         }
-        const uint32_t fl = P.w >> 24, slen = P.w & 0xFFFFFFu, j = P.z - o0;
+        const DPiece D = dpc_dec(P.x, P.y);
+        const uint32_t pxv = P.z, fl = D.fl, slen = D.slen, j = D.j, nops = D.nops;
         const uint32_t op = w0 & 15u, l = w0 >> 4;
         const bool xf = (fl & S2C_PF_X) != 0;
         // (no maxdel count to take: the rule is off, or SEQ holds no '-'; S2C_PF_SIMPLE marks the
         // one-token pieces, whose length field already holds take)
         const bool plain = in && (fl & ~(uint32_t)(S2C_PF_X | S2C_PF_DASH | S2C_PF_SIMPLE | S2C_PF_XFEW)) == 0u && op_bases(op) &&
                            !((fl & S2C_PF_DASH) && mda);
-        const uint32_t nops = oend - P.z;
         // one M / = / X token and nothing else: seqout = SEQ[0 : min(l, len(SEQ))] (:64-69)
         const bool fast = plain && nops == 1u;
-        const uint32_t take = min(l, slen), q = 16u * (P.y - 2u * qw0);
-        if (fast) runl[j] = rec_enc(P.x - (uint32_t)T0, take, q);
+        const uint32_t take = min(l, slen), q = D.q;
+        if (fast) runl[j] = rec_enc_b(D.rs, take, q);
         // bases, D / N / P, bases (the deletion reads): two base runs here (:64-72: k = take,
         // then l1 '-', then SEQ[l : l + min(l2, len(SEQ) − l)]), the '-' run queued for the byte
         // counters unless maxdel drops it (:210: l1 dashes); with N / '-' in SEQ (no maxdel
@@ -582,14 +563,14 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             if (op_dash(w1 & 15u) && op_bases(w2 & 15u)) {
                 l1 = w1 >> 4;
                 t2 = l < slen ? min(w2 >> 4, slen - l) : 0u;
-                const int32_t r0 = (int32_t)(P.x + take) - T0;
+                const int32_t r0 = (int32_t)(D.rs + take) - REC_BIAS;
                 da = (uint32_t)min(max(r0, 0), TL);
                 db = (uint32_t)min(max(r0 + (int32_t)l1, 0), TL);
                 fdel = true;
                 fdash = db > da && !(mda && l1 > d.maxdel);
-                runl[j] = rec_enc(P.x - (uint32_t)T0, take, q);
+                runl[j] = rec_enc_b(D.rs, take, q);
                 runl[j + 1] = make_uint2(0u, 0u);
-                runl[j + 2] = rec_enc(P.x + take + l1 - (uint32_t)T0, t2, q + l);
+                runl[j + 2] = rec_enc_b(D.rs + take + l1, t2, q + l);
             }
         }
         // queue: pieces for the general walk (their index) and the '-' runs of the deletion
@@ -607,8 +588,8 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             for (int u = 0; u < 2; u++) {
                 const uint32_t off = (pxv >> (16 * u)) & 0xFFFFu;
                 int32_t r = -1;
-                if (off < take) r = (int32_t)(P.x + off) - T0;
-                else if (fdel && off >= l && off - l < t2) r = (int32_t)(P.x + take + l1 + (off - l)) - T0;
+                if (off < take) r = (int32_t)(D.rs + off) - REC_BIAS;
+                else if (fdel && off >= l && off - l < t2) r = (int32_t)(D.rs + take + l1 + (off - l)) - REC_BIAS;
                 if (off != 0xFFFFu && r >= 0 && r < TL) cnt_add1(ncnt, (uint32_t)r);
             }
         }
@@ -639,16 +620,6 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     // needed only by the count, after the barrier that ends the queued walks)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     PROF_MARK(2);
-    // the first 64 queued X runs: their run records now, and their non-ACGT words from HBM,
-    // so the round trip overlaps the queued walks and the count (the X pass runs after it)
-    const bool xin = lane < nx;
-    const uint2 xrv = xin ? runl[queue[qcap - 1u - lane]] : make_uint2(0u, 0u);
-    const Rec xrc = rec_dec(xrv);
-    const uint32_t xq0 = xrc.q, xl = xrc.l, xwa = xq0 >> 5;
-    const int32_t xr0 = xrc.r0;
-    uint32_t xs[8];
-#pragma unroll
-    for (int u = 0; u < 8; u++) xs[u] = xin ? bxl[min(xwa + u, (xq0 + xl - 1) >> 5)] : 0u;
     // queued pieces: the general walk; '-' runs and SEQ N / '-' straight into the byte counters.
     // A queued piece's record comes from the lane that loaded it (ds_bpermute, all lanes on).
     for (uint32_t base = 0; base < (ABL(16) ? 0u : nslow); base += WGD) {
@@ -659,26 +630,26 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         if (!__ballot(gen)) continue;   // (only '-' runs in this round)
         const uint32_t k = gen ? qe : 0u, it = k / WT;
         const int src = (int)(4 * (k % WGD));   // (k ≡ this wave's lane mod 64: WT is a multiple of 64)
-        uint4 P = make_uint4(0u, 0u, 0u, 0u);
-        uint32_t oend = 0;
+        uint32_t c0 = 0, c1 = 0;
 #pragma unroll
         for (int u = 0; u < PFN; u++) {
-            const uint32_t px = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)Pp[u].x);
-            const uint32_t py = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)Pp[u].y);
-            const uint32_t pz = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)Pp[u].z);
-            const uint32_t pw = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)Pp[u].w);
-            const uint32_t pe = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)oe[u]);
+            const uint32_t px = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)Pc[u].x);
+            const uint32_t py = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)Pc[u].y);
             const bool me = it == (uint32_t)u;
-            P = me ? make_uint4(px, py, pz, pw) : P;
-            oend = me ? pe : oend;
+            c0 = me ? px : c0;
+            c1 = me ? py : c1;
         }
         if (gen) {
             if (it >= (uint32_t)PFN) {   // (windows of more than WT·PFN pieces)
-                P = ((const uint4 *)d.pc)[pf0 + k];
-                oend = d.pc[4 * (size_t)(pf0 + k + 1) + 2];
+                const uint3 R = dpc_load(d, v.dpc0 + k);
+                c0 = R.x;
+                c1 = R.y;
             }
-            const bool lng = ((P.w >> 24) & S2C_PF_LONG) != 0;   // (a long piece starting here does not overlap the tile)
-            walk_window(opl, bql, bxl, P, P.z - o0, oend - o0, 16u * (P.y - 2u * qw0), mda, d.maxdel,
+            const DPiece D = dpc_dec(c0, c1);
+            // (walk_window's view: the global start position and len(SEQ) | flags << 24)
+            const uint4 P = make_uint4((uint32_t)T0 + D.rs - (uint32_t)REC_BIAS, 0u, 0u, D.slen | D.fl << 24);
+            const bool lng = (D.fl & S2C_PF_LONG) != 0;   // (a long piece starting here does not overlap the tile)
+            walk_window(opl, bql, bxl, P, D.j, D.j + D.nops, D.q, mda, d.maxdel,
                         [&](uint32_t j, uint32_t gp, uint32_t l, uint32_t kind, uint32_t q) {
                             const uint32_t kd = (lng || kind == S2C_RUN_EMPTY) ? 0u : (kind & 3u);
                             runl[j] = kd == S2C_RUN_BASES ? rec_enc(gp - (uint32_t)T0, l, q) : make_uint2(0u, 0u);
@@ -859,14 +830,9 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         }
     }
     PROF_MARK(5);
-    // queued single-token runs of reads with N / '-' in SEQ (never dropped: maxdel is off)
-    if (xin && !ABL(32)) {
-        uint2 xp[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) xp[u] = bql[min(xwa + u, (xq0 + xl - 1) >> 5)];
-        x_events_pre(bxl, bql, xs, xp, xq0, xl, xr0, TL, false, dcnt, ncnt, ccnt);
-    }
-    for (uint32_t i = lane + WGD; i < (ABL(32) ? 0u : nx); i += WGD) {
+    // queued single-token runs of reads with N / '-' in SEQ (never dropped: maxdel is off; 0.08
+    // per C5 wave: read here, where their registers are not live through the count)
+    for (uint32_t i = lane; i < (ABL(32) ? 0u : nx); i += WGD) {
         const Rec rc = rec_dec(runl[queue[qcap - 1u - i]]);
         x_events(bxl, bql, rc.q, rc.l, rc.r0, TL, false, dcnt, ncnt, ccnt);
     }
@@ -947,7 +913,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         };
         if (npl <= 2) xchg(std::integral_constant<int, 1>{});
         else if (npl <= 4) xchg(std::integral_constant<int, 2>{});
-        else if (npl <= 6) xchg(std::integral_constant<int, 3>{});
+        else if (npl <= 6 || S2C_XCH_NCH_MAX < 4) xchg(std::integral_constant<int, 3>{});
         else xchg(std::integral_constant<int, 4>{});
         const uint32_t *vr = vp + wl * XCH_VROW + g * RPL;
 #pragma unroll
@@ -1183,19 +1149,12 @@ __global__ __launch_bounds__(WT) S2C_DENSE_OCC void k_tile_dense(const DenseArgs
     if (tid < RUN_PAD) wl.runl[v.nslot + tid] = make_uint2(0u, 0u);   // (the DMA does not write there)
     // with the DMA: the thread's piece records and its word's run-slot range
     constexpr int G = WGD / (NWP / WPT);
-    uint4 Pp[PFN];
-    uint32_t oe[PFN], pxr[PFN];
+    uint3 Pc[PFN];   // (compact records: s2c.h S2C_DPC_WORDS)
 #pragma unroll
     for (int i = 0; i < PFN; i++) {
         const uint32_t k = tid + WT * i;
-        Pp[i] = make_uint4(0u, 0u, 0u, 0u);
-        oe[i] = 0;
-        pxr[i] = 0xFFFFFFFFu;
-        if (k < v.npc) {
-            Pp[i] = ((const uint4 *)d.pc)[v.pf0 + k];
-            oe[i] = d.pc[4 * (size_t)(v.pf0 + k + 1) + 2];
-            pxr[i] = d.px[v.pf0 + k];
-        }
+        Pc[i] = make_uint3(0u, 0u, 0u);
+        if (k < v.npc) Pc[i] = dpc_load(d, v.dpc0 + k);
     }
     const uint32_t w = (tid >> 6) * (NWP / WPT) + (tid & 63) / G, W = v.W0 + w, K = d.kwin;
     uint32_t cw0 = 0, cw1 = 0;
@@ -1224,7 +1183,7 @@ __global__ __launch_bounds__(WT) S2C_DENSE_OCC void k_tile_dense(const DenseArgs
     cw0 -= v.o0;
     cw1 -= v.o0;
     lds_sync();
-    dense_tile<NWP>(d, v, wl, dcnt, ncnt, ccnt, amb, fill0, Pp, oe, pxr, cw0, cw1, t_entry, stl, threadIdx.x, buf);
+    dense_tile<NWP>(d, v, wl, dcnt, ncnt, ccnt, amb, fill0, Pc, cw0, cw1, t_entry, stl, threadIdx.x, buf);
 }
 
 
@@ -1258,7 +1217,8 @@ int s2c_launch_dense(const s2c_dev *dv, hipStream_t st) {
     if (dv->fill_len != 1) return s2c_set_error(S2C_ERR_ARG, "dense tiles need a one-char fill");
     if (dv->n_dense >= ((int64_t)1 << 31)) return s2c_set_error(S2C_ERR_LIMIT, "too many dense tiles");
     DenseArgs a;
-    a.rs = dv->rs; a.lp = dv->lp; a.pc = dv->pc; a.px = dv->px; a.dwin = dv->dwin; a.ops = dv->ops; a.bq = dv->bq; a.bx = dv->bx; a.tiles = dv->tiles; a.items = dv->dense;
+    if (!dv->dpc || !dv->dwin) return s2c_set_error(S2C_ERR_ARG, "dense tiles need dwin and dpc (ABI 12)");
+    a.rs = dv->rs; a.lp = dv->lp; a.pc = dv->pc; a.dwin = dv->dwin; a.dpc = dv->dpc; a.ops = dv->ops; a.bq = dv->bq; a.bx = dv->bx; a.tiles = dv->tiles; a.items = dv->dense;
     a.thresholds = dv->thresholds; a.tile_stats = dv->tile_stats; a.blk_len = dv->blk_len; a.out = dv->out;
     a.padded_len = (uint32_t)dv->padded_len; a.n_cols = (uint32_t)dv->n_cols; a.n_tiles = (uint32_t)dv->n_tiles;
     a.kwin = (uint32_t)dv->kwin; a.fill_nondash = (uint32_t)dv->fill_nondash;
@@ -1274,8 +1234,11 @@ int s2c_launch_dense(const s2c_dev *dv, hipStream_t st) {
     const int64_t lds = dv->dense_lds;
     if (lds <= 0 || lds > S2C_DENSE_LDS || (lds & 15)) return s2c_set_error(S2C_ERR_ARG, "dense_lds outside (0, S2C_DENSE_LDS] or not 16-byte aligned");
     // (the window's LDS doubles as the counters' exchange after the count: at least WPT waves' share)
-    a.buf_bytes = (uint32_t)std::max<int64_t>(lds, (int64_t)WPT * XCH_WAVE_BYTES);
-    if (dv->tile_max <= 512) return launch<16>(a, n, st);   // (two waves: ≥ 8 words per wave)
+    // (WPT > 2: the waves' queues may take up to 64·WPT entries past S2C_DENSE_BYTES' share)
+    a.buf_bytes = (uint32_t)std::max<int64_t>(lds + (WPT > 2 ? 256 * WPT : 0), (int64_t)WPT * XCH_WAVE_BYTES);
+    if constexpr (WPT <= 2) {   // (≥ 8 words per wave)
+        if (dv->tile_max <= 512) return launch<16>(a, n, st);
+    }
     if (dv->tile_max <= 1024) return launch<32>(a, n, st);
     return launch<64>(a, n, st);   // tile_max ≤ 2048 (host plan)
 }

@@ -312,20 +312,8 @@ struct s2c_batch {
     u32buf kmin, kmax;   // host only: global key range of each piece's insertion events
     u32buf px;           // [pieces] the non-ACGT SEQ offsets of S2C_PF_XFEW pieces (s2c.h)
     std::vector<uint32_t> dwin;   // [dense][S2C_DWIN_WORDS] the dense items' windows (s2c.h)
+    u32buf dpc;                   // [n_dpc][S2C_DPC_WORDS] compact piece records of the dense windows (s2c.h)
 };
-
-// The dense items' windows (S2C_DWIN_WORDS) from the final tile records.
-static void build_dwin(s2c_batch *b) {
-    const size_t nd = b->dense.size() / S2C_ITEM_WORDS;
-    b->dwin.assign(std::max<size_t>(nd, 1) * S2C_DWIN_WORDS, 0u);
-    for (size_t i = 0; i < nd; i++) {
-        const uint32_t t = b->dense[i * S2C_ITEM_WORDS];
-        const uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
-        uint32_t *o = &b->dwin[i * S2C_DWIN_WORDS];
-        const uint32_t v[12] = {t, tw[0], tw[1], tw[8], tw[10], tw[11], tw[13], tw[14], tw[15], tw[16], tw[17], tw[18]};
-        for (int k = 0; k < 12; k++) o[k] = v[k];
-    }
-}
 
 static int perr(s2c_parser *p, int code, const std::string &msg) {
     p->err = code;
@@ -1299,6 +1287,70 @@ static void par_ranges(int nt, int64_t n, F &&f) {
     for (auto &x : th) x.join();
 }
 }  // namespace
+
+// The dense items' windows (S2C_DWIN_WORDS) from the final tile records, and the compact
+// piece records of every window (S2C_DPC_WORDS, in window order: a piece of two windows has
+// two records, each relative to its own window).
+static void build_dwin(s2c_batch *b) {
+    const size_t nd = b->dense.size() / S2C_ITEM_WORDS;
+    b->dwin.assign(std::max<size_t>(nd, 1) * S2C_DWIN_WORDS, 0u);
+    std::vector<uint64_t> base(nd + 1, 0);
+    for (size_t i = 0; i < nd; i++) {
+        const uint32_t t = b->dense[i * S2C_ITEM_WORDS];
+        const uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
+        uint32_t *o = &b->dwin[i * S2C_DWIN_WORDS];
+        const uint32_t v[12] = {t, tw[0], tw[1], tw[8], tw[10], tw[11], tw[13], tw[14], tw[15], tw[16], tw[17], tw[18]};
+        for (int k = 0; k < 12; k++) o[k] = v[k];
+        o[12] = (uint32_t)base[i];
+        base[i + 1] = base[i] + (tw[14] - tw[13]);
+    }
+    if (base[nd] >= ((uint64_t)1 << 32)) throw std::runtime_error("more than 2^32 dense window pieces");
+    b->info.n_dpc = (int64_t)base[nd];
+    b->dpc.resize(std::max<uint64_t>(base[nd], 1) * S2C_DPC_WORDS);
+    if (!base[nd]) b->dpc[0] = b->dpc[1] = b->dpc[2] = 0;
+    par_ranges(plan_threads((int64_t)nd, 64), (int64_t)nd, [&](int, int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; i++) {
+            const uint32_t *w = &b->dwin[(size_t)i * S2C_DWIN_WORDS];
+            const uint32_t T0 = 32 * (w[1] >> 5), o0 = w[8], qw0 = w[10];
+            uint32_t *o = &b->dpc[base[i] * S2C_DPC_WORDS];
+            for (uint32_t k = w[6]; k < w[7]; k++, o += S2C_DPC_WORDS) {
+                const uint32_t *pc = &b->pc[4 * (size_t)k];
+                const uint32_t rs = pc[0] - T0 + 2048u, qh = pc[1] - 2 * qw0, nops = pc[6] - pc[2], oj = pc[2] - o0;
+                const uint32_t slen = pc[3] & 0xFFFFFFu;
+                if (rs >= 4096u || qh >= 8192u || nops > S2C_DPC_NOPS_MAX || oj >= 8192u || slen > S2C_DPC_SLEN_MAX)
+                    throw std::runtime_error("dense window piece beyond the compact record's fields");
+                o[0] = rs | qh << 12 | nops << 25;
+                o[1] = oj | slen << 13 | (pc[3] >> 24) << 24;
+                o[2] = b->px[k];
+            }
+        }
+    });
+}
+
+// Pieces k_tile_dense's compact records cannot hold (len(SEQ) or op slots beyond their
+// fields): prefix counts over the sorted pieces, so a tile window [pf0, pf1) holds one iff
+// p[pf1] > p[pf0]; such a tile is not dense.
+static std::vector<uint32_t> dpc_bad_prefix(const s2c_batch *b) {
+    const int64_t NP = b->info.n_pieces;
+    std::vector<uint32_t> p(NP + 1, 0);
+    const int nt = plan_threads(NP, 1 << 16);
+    std::vector<uint32_t> part(nt + 1, 0);
+    auto bad = [&](int64_t k) {
+        const uint32_t *pc = &b->pc[4 * (size_t)k];
+        return (pc[3] & 0xFFFFFFu) > S2C_DPC_SLEN_MAX || pc[6] - pc[2] > S2C_DPC_NOPS_MAX;
+    };
+    par_ranges(nt, NP, [&](int t, int64_t k0, int64_t k1) {
+        uint32_t c = 0;
+        for (int64_t k = k0; k < k1; k++) c += bad(k);
+        part[t + 1] = c;
+    });
+    for (int t = 0; t < nt; t++) part[t + 1] += part[t];
+    par_ranges(nt, NP, [&](int t, int64_t k0, int64_t k1) {
+        uint32_t c = part[t];
+        for (int64_t k = k0; k < k1; k++) p[k + 1] = (c += bad(k));
+    });
+    return p;
+}
 
 // The window of tile [a, b): the short pieces starting in words [a/32 - K, ceil(b/32)) — a
 // contiguous range of the bucketed pieces — their op slots and base plane words (+1 word for
@@ -2725,11 +2777,14 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     });
     clk.mark("tile plans");
     if (too_big) return s2c_set_error(S2C_ERR_LIMIT, "a read whose SEQ or CIGAR exceeds k_tile's LDS chunk");
+    // windows k_tile_dense's compact piece records can hold (s2c.h S2C_DPC_*)
+    const std::vector<uint32_t> dbad = dpc_bad_prefix(b);
+    auto dpc_ok = [&](const uint32_t *tw) { return K <= 64 && dbad[tw[14]] == dbad[tw[13]]; };
     // the dense class, as the loop below decides it (only single-item tiles can be dense)
     auto dense_tile = [&](int64_t t) {
         const uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
         return t_nch[t] == 1 && nev[t] == 0 && (int64_t)ccap[t] <= lcols && t_maxc[t] <= 255 && !no_dense &&
-               dense_fits(tw, K) && dense_bytes(tw, K) <= dense_cap;
+               dense_fits(tw, K) && dense_bytes(tw, K) <= dense_cap && dpc_ok(tw);
     };
     // Grid shaping for k_tile: work items run in rounds of `slots` workgroups (the device's CUs
     // × k_tile's workgroups per CU); the last round of a launch whose items all take about as
@@ -2773,7 +2828,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
         uint32_t fl = nch > 1 ? S2C_TILE_DEEP : 0u;
         if (nev[t] > S2C_EPI_KEYS || (int64_t)ccap[t] > lcols) fl |= S2C_TILE_GENERAL;
         if (fl == 0 && nev[t] == 0 && maxc <= 255 && !no_dense && dense_fits(tw, K) &&
-            dense_bytes(tw, K) <= dense_cap)
+            dense_bytes(tw, K) <= dense_cap && dpc_ok(tw))
             fl = S2C_TILE_DENSE;
         const uint32_t bcap = nshort[t] ? pow2_at_least(2 * (uint64_t)nshort[t]) : 0u;
         tw[0] = (uint32_t)T.a; tw[1] = (uint32_t)T.b; tw[2] = (uint32_t)T.ref; tw[3] = fl;
@@ -3071,6 +3126,7 @@ extern "C" int s2c_batch_arrays_get(const s2c_batch *b, s2c_batch_arrays *o) {
     o->lbq = b->lbq.data();
     o->lbx = b->lbx.data();
     o->lpx = b->lpx.empty() ? nullptr : b->lpx.data();
+    o->dpc = b->dpc.data();
     return S2C_OK;
 }
 

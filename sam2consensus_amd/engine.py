@@ -163,7 +163,7 @@ class DeviceBatch:
     copy stream (asynchronous); otherwise each array is copied synchronously."""
 
     ARRAYS = ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile", "rlist", "ps",
-              "lly", "lpc", "lops", "lbq", "lbx", "px", "dwin", "lpx")
+              "lly", "lpc", "lops", "lbq", "lbx", "px", "dwin", "lpx", "dpc")
 
     def __init__(self, hb, device=None, uploader=None, dense_layers=False):
         self.device = _dev(device) if uploader is None else uploader.device

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
     assert declared <= exported, declared - exported
     assert declared == set(_lib.EXPORTS)
-    assert _lib.lib.s2c_abi_version() == 11
+    assert _lib.lib.s2c_abi_version() == 12
 
 
 def _model_case(sam, args):
@@ -528,7 +528,7 @@ def _host_dev(hb, fill=b"-", counts=False):
     p = C.addressof(scratch)
     d = L.Dev()
     for name in ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile", "rlist", "ps", "px",
-                 "dwin", "lly", "lpc", "lops", "lbq", "lbx", "lpx"):
+                 "dwin", "lly", "lpc", "lops", "lbq", "lbx", "lpx", "dpc"):
         setattr(d, name, p)
     d.n_pieces, d.n_ops, d.n_qwords, d.n_tiles = i.n_pieces, i.n_ops, i.n_qwords, i.n_tiles
     d.n_items, d.n_dense, d.n_deep = i.n_items, i.n_dense, i.n_deep
@@ -602,9 +602,51 @@ def test_dense_windows_mirror_tile_records():
             t = b.dense[:, 0].astype(np.int64)
             assert (b.dwin[:, 0] == t).all()
             assert (b.dwin[:, 1:12] == b.tiles[t][:, [0, 1, 8, 10, 11, 13, 14, 15, 16, 17, 18]]).all()
-            assert not b.dwin[:, 12:].any()
+            # word 12: the first compact record of the window (ABI 12), records in window order
+            npw = (b.dwin[:, 7] - b.dwin[:, 6]).astype(np.int64)
+            assert (b.dwin[:, 12].astype(np.int64) == np.concatenate([[0], np.cumsum(npw)[:-1]])).all()
+            assert i.n_dpc == npw.sum() and b.dpc.shape == (i.n_dpc, 3)
+            assert not b.dwin[:, 13:].any()
+            _check_dpc(b)
             if b is not hb:
                 b.free()
+    finally:
+        hb.free()
+
+
+def _check_dpc(b):
+    """Every compact piece record (s2c.h S2C_DPC_WORDS) decodes to its piece's record, px and
+    op slot count, relative to its window."""
+    pc = b.pc.astype(np.int64)
+    for w in b.dwin.astype(np.int64):
+        k = np.arange(w[6], w[7])
+        r = b.dpc[w[12]:w[12] + len(k)].astype(np.int64)
+        T0 = 32 * (w[1] >> 5)
+        assert ((r[:, 0] & 0xFFF) == pc[k, 0] - T0 + 2048).all()
+        assert (((r[:, 0] >> 12) & 0x1FFF) == pc[k, 1] - 2 * w[10]).all()
+        assert ((r[:, 0] >> 25) == pc[k + 1, 2] - pc[k, 2]).all()
+        assert ((r[:, 1] & 0x1FFF) == pc[k, 2] - w[8]).all()
+        assert (((r[:, 1] >> 13) & 0x7FF) == (pc[k, 3] & 0xFFFFFF)).all()
+        assert ((r[:, 1] >> 24) == pc[k, 3] >> 24).all()
+        assert (r[:, 2] == b.px[k]).all()
+
+
+def test_dense_needs_compact_records():
+    """A window holding a piece the compact record cannot hold (len(SEQ) > 2047) is not dense;
+    the other tiles of the batch still are."""
+    sam = "@SQ\tSN:g\tLN:20000\n"
+    for s in range(1, 19000, 5):
+        sam += "r\t0\tg\t%d\t60\t100M\t*\t0\t0\t%s\t*\n" % (s, "ACGTA" * 20)
+    sam += "x\t0\tg\t15000\t60\t3S60M\t*\t0\t0\t%s\t*\n" % ("C" * 2100)   # len(SEQ) 2100 (not one token)
+    hb = batch.parse_text(sam, False, 150)
+    try:
+        t = hb.tiles
+        dense = (t[:, 3] & 4) != 0
+        assert dense.any() and not dense.all()
+        a, e = t[:, 0].astype(np.int64), t[:, 1].astype(np.int64)
+        bad = (a <= 15000 + 32 * int(hb.info.kwin) + 32) & (e > 14999 - 32)
+        assert not (dense & bad).any()
+        _check_dpc(hb)
     finally:
         hb.free()
 
