@@ -167,7 +167,34 @@ struct DPiece {
 __device__ __forceinline__ DPiece dpc_dec(uint32_t c0, uint32_t c1) {
     return DPiece{c0 & 0xFFFu, 16u * ((c0 >> 12) & 0x1FFFu), c0 >> 25, c1 & 0x1FFFu, (c1 >> 13) & 0x7FFu, c1 >> 24};
 }
-__device__ __forceinline__ uint3 dpc_load(const DenseArgs &d, uint32_t i) { return ((const uint3 *)d.dpc)[i]; }
+// FASTA body stores (written once, fetched by the host): nontemporal (−1.2 % on C5,
+// profiles/r05/v6_nt_loads_stores_ab.txt; the same policy on the compact records' loads cost +2 %)
+#ifndef S2C_BODY_NT
+#define S2C_BODY_NT 1
+#endif
+template <class T>
+__device__ __forceinline__ void body_st(T *p, T v) {
+#if S2C_BODY_NT
+    if constexpr (std::is_same_v<T, uint2>) {
+        __builtin_nontemporal_store(v.x, (uint32_t *)p);
+        __builtin_nontemporal_store(v.y, (uint32_t *)p + 1);
+    } else {
+        __builtin_nontemporal_store(v, p);
+    }
+#else
+    *p = v;
+#endif
+}
+// (a 3-vector takes 16 bytes: the record is addressed by dwords, 3 per record, 4-byte aligned)
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3), aligned(4)));
+__device__ __forceinline__ uint3 dpc_load(const DenseArgs &d, uint32_t i) {
+#if S2C_DPC_NT
+    const u32x3 r = __builtin_nontemporal_load((const u32x3 *)(d.dpc + 3 * (size_t)i));   // (read once: streamed)
+    return make_uint3(r.x, r.y, r.z);
+#else
+    return ((const uint3 *)d.dpc)[i];
+#endif
+}
 // rec_enc from a biased start (rs = tile-relative start + REC_BIAS)
 __device__ __forceinline__ uint2 rec_enc_b(uint32_t rs, uint32_t len, uint32_t q) {
     return make_uint2(rs | ((rs + len) << 16), q - rs);
@@ -195,6 +222,21 @@ __device__ __forceinline__ double sload_f64(const double *p) {
     return __builtin_bit_cast(double, r);
 }
 
+// cache policy bits of the window DMA: nt (streamed; measured −2.5 % on C5 against the
+// default policy, profiles/r05/v5_dma_policy_ab.txt); variant builds: -DS2C_DMA_CP=0 default,
+// 2 sc1, 3 sc0
+#ifndef S2C_DMA_CP
+#define S2C_DMA_CP 1
+#endif
+#if S2C_DMA_CP == 1
+#define S2C_DMA_POLICY " nt"
+#elif S2C_DMA_CP == 2
+#define S2C_DMA_POLICY " sc1"
+#elif S2C_DMA_CP == 3
+#define S2C_DMA_POLICY " sc0"
+#else
+#define S2C_DMA_POLICY ""
+#endif
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"   // m0 (reserved) is set and clobbered by the DMA
 // n dwords src[0..n) of an array ending at `end` → LDS by 16-byte LDS-DMA (1 KB per wave
@@ -219,7 +261,7 @@ __device__ __forceinline__ void dma16(uint8_t *dst, const uint32_t *src, uint32_
     const uint32_t m0 = uni(lds_addr(dst));
     for (uint32_t base = 1024 * wv; base < nbytes; base += 1024 * WPT) {
         if (base + 16 * lane < nbytes)
-            asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+            asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen" S2C_DMA_POLICY " lds"
                          :: "s"(uni(m0 + base)), "v"(16 * lane), "s"(r), "s"(uni(base)) : "memory", "m0");
     }
 }
@@ -1050,7 +1092,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             tr4(ow[4 % RPL], ow[5 % RPL], ow[6 % RPL], ow[7 % RPL], c2);
             if (full) {
 #pragma unroll
-                for (int j = 0; j < 4; j++) *(uint2 *)(dst + 8 * j) = make_uint2(cj[j], c2[j]);
+                for (int j = 0; j < 4; j++) body_st((uint2 *)(dst + 8 * j), make_uint2(cj[j], c2[j]));
             } else if (active) {   // (the tile's last word; bounds kept here, not hoisted)
                 uint32_t nn = n - 32 * w;
                 asm volatile("" : "+v"(nn));
@@ -1065,9 +1107,9 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
             if (full) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    if constexpr (RPL == 4) *(uint32_t *)(dst + 8 * j) = cj[j];
-                    else if constexpr (RPL == 2) *(uint16_t *)(dst + 8 * j) = (uint16_t)cj[j];
-                    else dst[8 * j] = (uint8_t)cj[j];
+                    if constexpr (RPL == 4) body_st((uint32_t *)(dst + 8 * j), cj[j]);
+                    else if constexpr (RPL == 2) body_st((uint16_t *)(dst + 8 * j), (uint16_t)cj[j]);
+                    else body_st(dst + 8 * j, (uint8_t)cj[j]);
                 }
             } else if (active) {   // (the tile's last word; bounds kept here, not hoisted)
                 uint32_t nn = n - 32 * w - g * RPL;
