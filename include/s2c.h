@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define S2C_ABI_VERSION 12
+#define S2C_ABI_VERSION 13
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define S2C_OK            0
@@ -307,6 +307,10 @@ typedef struct {
     int64_t layers_built;      /* 1: the layered windows (lly ..., tile word 20) are built (s2c_batch_layers*);
                                   0 for a fresh snapshot or shard */
     int64_t n_dpc;             /* compact piece records of the dense items' windows (ABI 12) */
+    int64_t word_lo, word_hi;  /* (ABI 13) the per-word entries any launch reads: rs / ps [word_lo, word_hi],
+                                  wtile [word_lo, word_hi) — 0 and n_words for a whole batch, a shard's
+                                  own words and its windows' lookback for s2c_batch_shard; the device
+                                  copies (s2c_dev rs / ps / wtile) hold only those entries */
 } s2c_batch_info;
 
 typedef struct {               /* host pointers into the batch (valid until s2c_batch_free) */
@@ -447,6 +451,9 @@ typedef struct {
     const uint32_t *dwin;      /* [n_dense][S2C_DWIN_WORDS] s2c_batch_arrays.dwin, filtered like dense */
     const uint32_t *lpx;       /* [n_lpieces] s2c_batch_arrays.lpx (ABI 11; required with n_layers > 0) */
     const uint32_t *dpc;       /* [n_dpc][S2C_DPC_WORDS] s2c_batch_arrays.dpc (ABI 12; required with n_dense > 0) */
+    int64_t   word_lo, word_hi;   /* (ABI 13) the batch's info.word_lo / word_hi: rs and ps point at entry
+                                     word_lo of s2c_batch_arrays rs / ps ([word_lo, word_hi] copied),
+                                     wtile at entry word_lo ([word_lo, word_hi) copied) */
 } s2c_dev;
 
 /* Sizes (bytes) of every workspace / output buffer for a batch and T thresholds. */

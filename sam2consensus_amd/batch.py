@@ -137,6 +137,18 @@ class HostBatch:
         self._layers = True
         return self
 
+    def device_view(self, name):
+        """The part of array ``name`` that goes to the device: the per-word arrays only over
+        the words a launch reads (info.word_lo / word_hi, ABI 13 — a shard's own words), the
+        others whole."""
+        a = getattr(self, name)
+        lo, hi = int(self.info.word_lo), int(self.info.word_hi)
+        if name in ("rs", "ps"):
+            return a[lo:hi + 1]
+        if name == "wtile":
+            return a[lo:hi]
+        return a
+
     @property
     def blocks(self):
         return self.tiles

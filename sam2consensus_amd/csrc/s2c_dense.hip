@@ -72,6 +72,7 @@ struct DenseArgs {
     uint64_t *tile_stats, *blk_len;
     uint8_t *out;
     uint32_t padded_len, n_cols, n_tiles, kwin, fill_nondash, maxdel_active, maxdel, n_items;
+    uint32_t word_lo;               // rs holds entries word_lo .. (s2c_dev, ABI 13)
     const void *ops_end, *bq_end;   // ends of the DMA sources
     uint32_t buf_bytes;                                        // the window's LDS (16-byte multiple)
     int32_t n_thr, min_depth;
@@ -1201,8 +1202,8 @@ __global__ __launch_bounds__(WT) S2C_DENSE_OCC void k_tile_dense(const DenseArgs
     const uint32_t w = (tid >> 6) * (NWP / WPT) + (tid & 63) / G, W = v.W0 + w, K = d.kwin;
     uint32_t cw0 = 0, cw1 = 0;
     if (w < v.nwords) {   // (window-relative after the wait below: no early wait on the DMA)
-        cw0 = d.rs[W >= K ? W - K : 0u];
-        cw1 = d.rs[W + 1];
+        cw0 = d.rs[(W >= K ? W - K : 0u) - d.word_lo];   // (rs holds entries word_lo ..: s2c_dev)
+        cw1 = d.rs[W + 1 - d.word_lo];
     }
     // the ambiguity table and the fill char by scalar loads (a vector load's wait here would
     // also wait for the window DMA issued before it)
@@ -1267,6 +1268,7 @@ int s2c_launch_dense(const s2c_dev *dv, hipStream_t st) {
     a.maxdel_active = dv->maxdel_active ? 1u : 0u;
     a.maxdel = dv->maxdel < 0 ? 0u : (uint32_t)dv->maxdel;
     a.n_items = (uint32_t)dv->n_dense;
+    a.word_lo = (uint32_t)dv->word_lo;
     a.ops_end = dv->ops + dv->n_ops;
     a.bq_end = dv->bq + 2 * dv->n_qwords;
     a.n_thr = dv->n_thr; a.min_depth = dv->min_depth;

@@ -2297,6 +2297,8 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     I.n_refs = R;
     I.padded_len = Lpad;
     I.n_words = NW;
+    I.word_lo = 0;
+    I.word_hi = NW;
     for (int64_t r = 0; r < R; r++) I.total_len += p->ref_len[r];
     I.header_lines = p->header_lines;
     for (auto &cp : CH) {
@@ -3069,6 +3071,11 @@ static int s2c_batch_shard_impl(const s2c_batch *b, int64_t t0, int64_t t1, s2c_
     mark_runs(s.get());
     build_dwin(s.get());
     // the shard's share of the workload's aligned bases (by its positions; for reporting)
+    // the per-word entries the shard's launches read (s2c_batch_info word_lo / word_hi): its
+    // tiles' words, the window lookback of k_tile_dense's run-slot ranges (rs[W - kwin]) and
+    // the piece range above; k_reads drops events keyed outside
+    J.word_lo = t1 > t0 ? std::max<int64_t>(W0 - K - 1, 0) : 0;
+    J.word_hi = t1 > t0 ? std::min<int64_t>(W1, NW) : 0;
     J.aligned_bases = I.total_len ? (int64_t)((double)I.aligned_bases * (double)aligned / (double)I.total_len) : 0;
     *out = s.release();
     return S2C_OK;

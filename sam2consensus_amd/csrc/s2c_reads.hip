@@ -24,6 +24,7 @@ struct ReadsArgs {
     const uint32_t *pc, *ops, *bq, *bx, *tiles, *wtile, *rlist;
     uint32_t *runs, *ibkt, *ilong, *ilong_n;
     uint32_t n, maxdel_active, maxdel, all;   // all: every piece (else the pieces of rlist)
+    uint32_t word_lo, word_hi;                // wtile holds words [word_lo, word_hi) (s2c_dev, ABI 13)
 };
 
 struct GlobalMem {   // walk_piece's view of the batch in HBM
@@ -54,8 +55,10 @@ __device__ __forceinline__ uint64_t mix64(uint64_t k) {
 
 // One insertion event (global key gkey, motif = query bases [q, q + len)) into its tile.
 __device__ void add_event(const ReadsArgs &d, uint64_t gkey, uint64_t q, uint32_t len) {
-    const uint32_t t = d.wtile[gkey >> 5];
-    if (t == 0xFFFFFFFFu) return;   // keyed outside this batch's tiles (a multi-GPU shard)
+    const uint64_t W = gkey >> 5;
+    if (W < d.word_lo || W >= d.word_hi) return;   // keyed outside a multi-GPU shard's words
+    const uint32_t t = d.wtile[W - d.word_lo];
+    if (t == 0xFFFFFFFFu) return;   // keyed outside this batch's tiles (padding, another shard's tile)
     const uint4 tw0 = ((const uint4 *)d.tiles)[(size_t)t * (S2C_TILE_WORDS / 4)];
     const uint4 tw1 = ((const uint4 *)d.tiles)[(size_t)t * (S2C_TILE_WORDS / 4) + 1];
     const uint32_t pos = (uint32_t)(gkey - tw0.x);   // tile-relative (< 2048)
@@ -112,6 +115,8 @@ int s2c_launch_reads(const s2c_dev *dv, hipStream_t st, bool all) {
     a.maxdel_active = dv->maxdel_active ? 1u : 0u;
     a.maxdel = dv->maxdel < 0 ? 0u : (uint32_t)dv->maxdel;
     a.all = all ? 1u : 0u;
+    a.word_lo = (uint32_t)dv->word_lo;
+    a.word_hi = (uint32_t)dv->word_hi;
     k_reads<<<(unsigned)((n + WG - 1) / WG), WG, 0, st>>>(a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? S2C_OK : s2c_set_error(S2C_ERR_HIP, std::string("k_reads: ") + hipGetErrorString(e));

@@ -720,6 +720,12 @@ __device__ __forceinline__ DmaSrc dma_src(const void *p, const void *end) {
 // Arguments wave-uniform.  Completion: s_waitcnt vmcnt(0) (the compiler does not count these
 // loads): the wave's own LDS reads then see the data.
 // Returns the number of DMA instructions issued (each one vmcnt event).
+// Cache policy of the layer DMA (variant builds: -DS2C_TILE_DMA_CP=1 nontemporal).
+#if defined(S2C_TILE_DMA_CP) && S2C_TILE_DMA_CP == 1
+#define S2C_TILE_DMA_POLICY " nt"
+#else
+#define S2C_TILE_DMA_POLICY ""
+#endif
 __device__ __forceinline__ uint32_t dma16_wave(uint8_t *dst, const DmaSrc &S, const uint32_t *src, uint32_t n) {
     const uint32_t lane = threadIdx.x & 63;
     const uintptr_t sal = (uintptr_t)src & ~(uintptr_t)15;
@@ -728,7 +734,7 @@ __device__ __forceinline__ uint32_t dma16_wave(uint8_t *dst, const DmaSrc &S, co
     uint32_t k = 0;
     for (uint32_t base = 0; base < nbytes; base += 1024, k++) {
         if (base + 16 * lane < nbytes)
-            asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+            asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen" S2C_TILE_DMA_POLICY " lds"
                          :: "s"(m0 + base), "v"(16 * lane), "s"(S.r), "s"(soff + base) : "memory", "m0");
     }
     return k;
@@ -834,11 +840,39 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
         j += 3;
     }
     const uint32_t ql = 16u * P.y + qadj;     // SEQ[0] in the LDS planes
+#if S2C_WALK_BATCH
+    // the op words eight at a time into registers (independent LDS reads, one wait); a piece
+    // of at most eight ops (nearly all) is read once for both passes
+    uint32_t ob[8];
+    auto load8 = [&](uint32_t j0) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) ob[i] = opl[j0 + i + od];   // (words past oend: unused)
+    };
+    const bool one = oend - j <= 8u;
+    if (one) load8(j);
+#define S2C_OPS_BEGIN(J)                                      \
+    for (uint32_t j0 = (J); j0 < oend; j0 += 8) {             \
+        if (!one) load8(j0);                                  \
+        _Pragma("unroll") for (uint32_t i = 0; i < 8; i++) { \
+            if (j0 + i >= oend) break;                        \
+            const uint32_t jj = j0 + i, w = ob[i];
+#define S2C_OPS_END \
+        }           \
+    }
+#else
+#define S2C_OPS_BEGIN(J)                           \
+    for (uint32_t jj = (J); jj < oend; jj++) {     \
+        {                                          \
+            const uint32_t w = opl[jj + od];
+#define S2C_OPS_END \
+        }           \
+    }
+#endif
     bool drop = false;
     if (maxdel_active) {   // :210 — D/N/P lengths + '-' chars of the bases taken
         uint32_t dashes = 0, start = 0;
-        for (uint32_t i = j; i < oend; i++) {
-            const uint32_t w = opl[i + od], op = w & 15u, l = w >> 4;
+        S2C_OPS_BEGIN(j)
+            const uint32_t op = w & 15u, l = w >> 4;
             if (op_bases(op)) {
                 uint32_t take = start < slen ? min(l, slen - start) : 0u;
                 if (fl & S2C_PF_DASH) {   // '-' chars of SEQ: x = 1, p1 = 0, p0 = 1
@@ -857,13 +891,13 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
             } else if (op == S2C_OP_I || op == S2C_OP_S) {
                 start += l;
             }
-        }
+        S2C_OPS_END
         drop = dashes > maxdel;
     }
     const uint32_t e_tile = a + n;
     uint32_t kk = 0, start = 0;
-    for (; j < oend; j++) {
-        const uint32_t w = opl[j + od], op = w & 15u, l = w >> 4;
+    S2C_OPS_BEGIN(j)
+        const uint32_t op = w & 15u, l = w >> 4;
         uint2 r = make_uint2(0u, 0u);
         const bool bases = op_bases(op);
         if (bases || op_dash(op)) {
@@ -888,8 +922,10 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
             kk += take;
         }
         if (bases || op == S2C_OP_I || op == S2C_OP_S) start += l;
-        runl[j + rd] = r;
-    }
+        runl[jj + rd] = r;
+    S2C_OPS_END
+#undef S2C_OPS_BEGIN
+#undef S2C_OPS_END
 }
 
 #ifndef S2C_TILE_XCD
@@ -1129,7 +1165,11 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
                 if (i + 1 == NPc)
                     for (uint32_t sg = (uint32_t)(sw + 1); sg <= NS; sg++) C.segR[sg] = NR;
                 const uint32_t f = Pw[u].w >> 24;
+#if S2C_PLANES_NARROW   // (only x_fix and the maxdel '-' count read the planes: S2C_PF_DASH implies S2C_PF_X)
+                planes |= (f & S2C_PF_X) && ((f & S2C_PF_SIMPLE) ? !(f & S2C_PF_XFEW) : !(f & S2C_PF_LONG));
+#else
                 planes |= (f & S2C_PF_SIMPLE) ? ((f & S2C_PF_X) && !(f & S2C_PF_XFEW)) : !(f & S2C_PF_LONG);
+#endif
             }
         }
         if (NPc == 0)
@@ -1685,6 +1725,10 @@ static int check_dev(const s2c_dev *d) {
         return s2c_set_error(S2C_ERR_ARG, "missing items");
     if (!d->ibkt || !d->ilong || !d->ilong_n) return s2c_set_error(S2C_ERR_ARG, "missing insertion tables");
     if (d->n_tiles > 0 && !d->ps) return s2c_set_error(S2C_ERR_ARG, "missing piece CSR (ps)");
+    // (ABI 13) the per-word entries the device copies hold: a batch with tiles has some
+    if (d->word_lo < 0 || d->word_hi < d->word_lo || 32 * d->word_hi > d->padded_len || d->word_hi >= ((int64_t)1 << 32) ||
+        (d->n_tiles > 0 && d->word_hi == d->word_lo))
+        return s2c_set_error(S2C_ERR_ARG, "bad per-word span word_lo / word_hi (s2c_batch_info, ABI 13)");
     {   // k_tile's segments: a window of ≤ 64 words and kwin start words before it
         int64_t nwp = 8;
         while (nwp * 32 < d->tile_max) nwp *= 2;

@@ -171,15 +171,17 @@ class DeviceBatch:
         # them through k_tile); the pileup reads them in place, so by default they are not built
         self.hb = hb.ensure_layers(dense_layers)
         self.info = type(hb.info).from_buffer_copy(hb.info)   # (the arrays as uploaded)
-        if uploader is None and sum(np.asarray(getattr(hb, n)).nbytes for n in self.ARRAYS) >= (64 << 20):
+        # (the per-word arrays over the batch's word span only: HostBatch.device_view)
+        arrays = [np.asarray(hb.device_view(n)).reshape(-1) for n in self.ARRAYS]
+        if uploader is None and sum(a.nbytes for a in arrays) >= (64 << 20):
             uploader = default_uploader(self.device)   # (large batches: pinned chunks, not pageable copies)
         if uploader is not None:
-            views, self._storage = uploader.upload([np.asarray(getattr(hb, n)).reshape(-1) for n in self.ARRAYS])
+            views, self._storage = uploader.upload(arrays)
             for name, v in zip(self.ARRAYS, views):
                 setattr(self, name, v)
             return
-        for name in self.ARRAYS:
-            setattr(self, name, _up(np.asarray(getattr(hb, name)).reshape(-1), self.device))
+        for name, a in zip(self.ARRAYS, arrays):
+            setattr(self, name, _up(a, self.device))
 
     def nbytes(self):
         return sum(getattr(self, n).numel() * getattr(self, n).element_size() for n in self.ARRAYS)
@@ -253,6 +255,7 @@ class Workspace:
         d.n_rlist = i.n_rlist
         d.n_layers, d.n_lpieces, d.n_lops, d.n_lqwords = i.n_layers, i.n_lpieces, i.n_lops, i.n_lqwords
         d.layers_dense, d.layers_built = i.layers_dense, i.layers_built
+        d.word_lo, d.word_hi = i.word_lo, i.word_hi
         # the maxdel rule (:210) runs on the device: the parser's setting unless overridden
         if maxdel_active is None:
             maxdel_active = getattr(db.hb, "maxdel_active", True)

@@ -161,8 +161,9 @@ def gather_results(fetched, sub, rank, world, T, group=None, timing=None):
 
 
 def batch_bytes(hb):
-    """Bytes of a packed batch's device arrays (what its rank uploads to HBM)."""
-    return int(sum(np.asarray(getattr(hb, n)).nbytes for n in
+    """Bytes of a packed batch's device arrays (what its rank uploads to HBM; the per-word
+    arrays over its word span only)."""
+    return int(sum(np.asarray(hb.device_view(n)).nbytes for n in
                    ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile", "rlist", "ps", "px",
                     "dwin")))
 

@@ -89,6 +89,17 @@ def test_exchange_volumes_count_the_duplicated_reads():
             assert v["dup_frac"] == 1.0 and v["cuts"] == 0 and v["count_merge_bytes"] == 0
         else:
             assert 1.0 < v["dup_frac"] < 1.5 and v["cuts"] == world - 1 and v["dup_bytes"] > 0
+        # (ABI 13) each shard uploads the per-word arrays over its own words (+ the window
+        # lookback) only: together about one copy of the whole batch's, not `world` copies
+        nw = int(hb.info.n_words)
+        per_word = sum(int(s_.info.word_hi - s_.info.word_lo) for s_ in subs)
+        assert per_word <= nw + world * (int(hb.info.kwin) + 2)
+        for s_ in subs:
+            lo, hi = int(s_.info.word_lo), int(s_.info.word_hi)
+            assert 0 <= lo < hi <= nw and len(s_.device_view("rs")) == hi - lo + 1
+            assert len(s_.device_view("wtile")) == hi - lo
+            t = s_.tiles
+            assert lo <= int(t[0, 0]) >> 5 and (int(t[-1, 1]) + 31) >> 5 <= hi
         for s_ in subs:
             s_.free()
 

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
     assert declared <= exported, declared - exported
     assert declared == set(_lib.EXPORTS)
-    assert _lib.lib.s2c_abi_version() == 12
+    assert _lib.lib.s2c_abi_version() == 13
 
 
 def _model_case(sam, args):
@@ -535,6 +535,7 @@ def _host_dev(hb, fill=b"-", counts=False):
     d.padded_len, d.chunk, d.kwin, d.tile_max = i.padded_len, i.chunk, i.kwin, i.tile_max
     d.dense_lds, d.n_rlist = i.dense_lds, i.n_rlist
     d.layers_dense, d.layers_built = i.layers_dense, i.layers_built
+    d.word_lo, d.word_hi = i.word_lo, i.word_hi
     d.maxdel_active, d.maxdel = 1, 150
     d.thresholds, d.n_thr, d.min_depth = p, 1, 1
     d.fill_len, d.fill_nondash, d.fill = len(fill), sum(c != ord("-") for c in fill), p
