@@ -88,6 +88,7 @@ struct TileArgs {
     const uint32_t *px, *lpx;   // S2C_PF_XFEW offsets of the pieces / of the layered pieces
     const void *bq_end, *bx_end, *ops_end, *pc_end;      // ends of the DMA sources (buffer ranges)
     const void *lbq_end, *lbx_end, *lops_end, *lpc_end;
+    const void *px_end, *lpx_end;
     uint32_t maxdel_active, maxdel;
     uint32_t *ibkt, *ilong, *ilong_n;
     const double *thresholds;
@@ -690,6 +691,12 @@ struct ChunkLds {
     alignas(16) uint4 pcb[S2C_CHUNK_PIECES];
     alignas(16) uint8_t ol[S2C_CHUNK_OBYTES + 16];
     alignas(16) uint2 runl[S2C_CHUNK_RECS + RPAD];
+#if S2C_PX_LDS
+    alignas(16) uint32_t pxl[S2C_CHUNK_PIECES + 4];   // the pieces' px words (ahead, like pcb)
+#endif
+#if S2C_WALK_QUEUE
+    uint8_t wq[S2C_CHUNK_PIECES];   // the layer's pieces walked op by op (neither simple nor long)
+#endif
 };
 
 typedef int v4i_t __attribute__((ext_vector_type(4)));
@@ -720,8 +727,12 @@ __device__ __forceinline__ DmaSrc dma_src(const void *p, const void *end) {
 // Arguments wave-uniform.  Completion: s_waitcnt vmcnt(0) (the compiler does not count these
 // loads): the wave's own LDS reads then see the data.
 // Returns the number of DMA instructions issued (each one vmcnt event).
-// Cache policy of the layer DMA (variant builds: -DS2C_TILE_DMA_CP=1 nontemporal).
-#if defined(S2C_TILE_DMA_CP) && S2C_TILE_DMA_CP == 1
+// Cache policy of the layer DMA: nontemporal (C3 -3.5 %, profiles/r05/v7_*; variant builds:
+// -DS2C_TILE_DMA_CP=0 the default policy)
+#ifndef S2C_TILE_DMA_CP
+#define S2C_TILE_DMA_CP 1
+#endif
+#if S2C_TILE_DMA_CP == 1
 #define S2C_TILE_DMA_POLICY " nt"
 #else
 #define S2C_TILE_DMA_POLICY ""
@@ -821,7 +832,8 @@ __device__ void x_fix(const uint2 *bql, gptr_u32 xl, uint32_t xd, uint32_t q, ui
 template <int NWP>
 __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *opl, uint32_t od, uint2 *runl, uint32_t rd,
                                  const uint2 *bql, gptr_u32 xl, uint32_t xd, uint32_t qadj, bool maxdel_active,
-                                 uint32_t maxdel, uint32_t a, uint32_t n, uint32_t *hist, int32_t *dV, int32_t *dD) {
+                                 uint32_t maxdel, uint32_t a, uint32_t n, uint32_t *hist, int32_t *dV, int32_t *dD,
+                                 uint32_t pxw = 0xFFFFFFFFu) {
     const uint32_t fl = P.w >> 24, slen = P.w & 0xFFFFFFu;
     uint32_t j = P.z;
     if (fl & S2C_PF_LONG) {   // (its runs come through the tile long lists)
@@ -840,39 +852,19 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
         j += 3;
     }
     const uint32_t ql = 16u * P.y + qadj;     // SEQ[0] in the LDS planes
-#if S2C_WALK_BATCH
-    // the op words eight at a time into registers (independent LDS reads, one wait); a piece
-    // of at most eight ops (nearly all) is read once for both passes
-    uint32_t ob[8];
-    auto load8 = [&](uint32_t j0) {
-#pragma unroll
-        for (int i = 0; i < 8; i++) ob[i] = opl[j0 + i + od];   // (words past oend: unused)
-    };
-    const bool one = oend - j <= 8u;
-    if (one) load8(j);
-#define S2C_OPS_BEGIN(J)                                      \
-    for (uint32_t j0 = (J); j0 < oend; j0 += 8) {             \
-        if (!one) load8(j0);                                  \
-        _Pragma("unroll") for (uint32_t i = 0; i < 8; i++) { \
-            if (j0 + i >= oend) break;                        \
-            const uint32_t jj = j0 + i, w = ob[i];
-#define S2C_OPS_END \
-        }           \
-    }
-#else
-#define S2C_OPS_BEGIN(J)                           \
-    for (uint32_t jj = (J); jj < oend; jj++) {     \
-        {                                          \
-            const uint32_t w = opl[jj + od];
-#define S2C_OPS_END \
-        }           \
-    }
-#endif
     bool drop = false;
-    if (maxdel_active) {   // :210 — D/N/P lengths + '-' chars of the bases taken
+    // :210 — D/N/P lengths + '-' chars of the bases taken.  With '-' in SEQ a first pass over
+    // the ops; otherwise (S2C_MAXDEL_1P) the D/N/P lengths are summed by the one pass below,
+    // which holds back the first two deletion runs' '-' counts until the sum is known
+#if S2C_MAXDEL_1P
+    const bool defer = maxdel_active && !(fl & S2C_PF_DASH);
+    if (maxdel_active && (fl & S2C_PF_DASH)) {
+#else
+    if (maxdel_active) {
+#endif
         uint32_t dashes = 0, start = 0;
-        S2C_OPS_BEGIN(j)
-            const uint32_t op = w & 15u, l = w >> 4;
+        for (uint32_t jj = j; jj < oend; jj++) {
+            const uint32_t w = opl[jj + od], op = w & 15u, l = w >> 4;
             if (op_bases(op)) {
                 uint32_t take = start < slen ? min(l, slen - start) : 0u;
                 if (fl & S2C_PF_DASH) {   // '-' chars of SEQ: x = 1, p1 = 0, p0 = 1
@@ -891,13 +883,16 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
             } else if (op == S2C_OP_I || op == S2C_OP_S) {
                 start += l;
             }
-        S2C_OPS_END
+        }
         drop = dashes > maxdel;
     }
+#if S2C_MAXDEL_1P
+    uint32_t dsum = 0, nd = 0, dr0 = 0, dr1 = 0;   // (deferred: '-' runs [c0, c1) - a packed c0 | c1 << 16)
+#endif
     const uint32_t e_tile = a + n;
     uint32_t kk = 0, start = 0;
-    S2C_OPS_BEGIN(j)
-        const uint32_t op = w & 15u, l = w >> 4;
+    for (uint32_t jj = j; jj < oend; jj++) {
+        const uint32_t w = opl[jj + od], op = w & 15u, l = w >> 4;
         uint2 r = make_uint2(0u, 0u);
         const bool bases = op_bases(op);
         if (bases || op_dash(op)) {
@@ -912,8 +907,26 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
                     if (c1 > c0) {
                         atomicAdd(&dV[c0 - a], 1);
                         atomicSub(&dV[c1 - a], 1);
+#if S2C_PX_LDS
+                        if ((fl & (S2C_PF_X | S2C_PF_XFEW)) == (S2C_PF_X | S2C_PF_XFEW)) {
+                            // ≤ 2 'N' at SEQ offsets px (s2c.h S2C_PF_XFEW): the run holds SEQ [so, so + len)
+                            const uint32_t so = start + (s - kk);
+#pragma unroll
+                            for (int h = 0; h < 2; h++) {
+                                const uint32_t off = (pxw >> (16 * h)) & 0xFFFFu, p = gp + (off - so);   // (0xFFFF: none)
+                                if (off != 0xFFFFu && off - so < len && p >= c0 && p < c1) Hist<NWP>::add1(hist, SL_N, p - a, 1u);
+                            }
+                        } else
+#endif
                         if (fl & S2C_PF_X) x_fix<NWP>(bql, xl, xd, q + (c0 - gp), c1 - c0, c0 - a, drop, hist);
                     }
+#if S2C_MAXDEL_1P
+                } else if (defer && c1 > c0) {
+                    const uint32_t pk = (c0 - a) | (c1 - a) << 16;
+                    dr1 = nd == 1 ? pk : dr1;
+                    dr0 = nd == 0 ? pk : dr0;
+                    nd++;
+#endif
                 } else if (!drop && c1 > c0) {
                     atomicAdd(&dD[c0 - a], 1);
                     atomicSub(&dD[c1 - a], 1);
@@ -921,11 +934,42 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
             }
             kk += take;
         }
+#if S2C_MAXDEL_1P
+        if (op_dash(op)) dsum += l;
+#endif
         if (bases || op == S2C_OP_I || op == S2C_OP_S) start += l;
         runl[jj + rd] = r;
-    S2C_OPS_END
-#undef S2C_OPS_BEGIN
-#undef S2C_OPS_END
+    }
+#if S2C_MAXDEL_1P
+    if (nd && dsum <= maxdel) {   // (defer: the read keeps its '-')
+        atomicAdd(&dD[dr0 & 0xFFFFu], 1);
+        atomicSub(&dD[dr0 >> 16], 1);
+        if (nd > 1) {
+            atomicAdd(&dD[dr1 & 0xFFFFu], 1);
+            atomicSub(&dD[dr1 >> 16], 1);
+        }
+        if (nd > 2) {   // (rare) the third and later runs: the ops again
+            uint32_t kk2 = 0, st2 = 0, m = 0;
+            for (uint32_t jj = j; jj < oend; jj++) {
+                const uint32_t w = opl[jj + od], op = w & 15u, l = w >> 4;
+                const bool bs = op_bases(op);
+                if (bs || op_dash(op)) {
+                    const uint32_t take = bs ? (st2 < slen ? min(l, slen - st2) : 0u) : l;
+                    const uint32_t s = max(kk2, ka), e = min(kk2 + take, kb);
+                    if (!bs && e > s) {
+                        const uint32_t gp = P.x + (s - ka), c0 = max(gp, a), c1 = min(gp + (e - s), e_tile);
+                        if (c1 > c0 && m++ >= 2) {
+                            atomicAdd(&dD[c0 - a], 1);
+                            atomicSub(&dD[c1 - a], 1);
+                        }
+                    }
+                    kk2 += take;
+                }
+                if (bs || op == S2C_OP_I || op == S2C_OP_S) st2 += l;
+            }
+        }
+    }
+#endif
 }
 
 #ifndef S2C_TILE_XCD
@@ -1098,6 +1142,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     const uint32_t *const spx = inplace ? d.px : d.lpx;
     const DmaSrc Dpc = dma_src(spc, inplace ? d.pc_end : d.lpc_end), Dops = dma_src(sops, inplace ? d.ops_end : d.lops_end);
     const DmaSrc Dbq = dma_src(sbq, inplace ? d.bq_end : d.lbq_end);
+#if S2C_PX_LDS
+    const DmaSrc Dpx = dma_src(spx, inplace ? d.px_end : d.lpx_end);
+#endif
     const uint4 *const pcr = C.pcb;
     // a layer's bounds: pieces [P0, P1), op words [O0, O1), plane words [qa, qb) (scalar loads)
     struct Lay {
@@ -1120,7 +1167,10 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     // the ahead part of layer ly: its piece records and op words; returns the vmcnt events
     // issued
     auto issue_ahead = [&](const Lay &L) -> uint32_t {
-        const uint32_t k = dma16_wave((uint8_t *)C.pcb, Dpc, spc + 4 * (size_t)L.P0, 4 * (L.P1 - L.P0));
+        uint32_t k = dma16_wave((uint8_t *)C.pcb, Dpc, spc + 4 * (size_t)L.P0, 4 * (L.P1 - L.P0));
+#if S2C_PX_LDS
+        k += dma16_wave((uint8_t *)C.pxl, Dpx, spx + L.P0, L.P1 - L.P0);
+#endif
         return k + dma16_wave(C.ol, Dops, sops + L.O0, L.O1 - L.O0);
     };
     uint32_t ly = l0 + wv;
@@ -1136,9 +1186,13 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
         const uint32_t P0 = cur.P0, O0 = cur.O0, O1 = cur.O1, qa = cur.qa;
         const uint32_t NPc = cur.P1 - cur.P0, NR = O1 - O0;
         uint32_t pxr[2];
+#if S2C_PX_LDS
+        const uint32_t *const pxl = C.pxl + (P0 & 3u);   // (px of layer piece i: pxl[i], ahead with the records)
+#else
 #pragma unroll
         for (int u = 0; u < 2; u++) pxr[u] = spx[lane + 64 * u < NPc ? P0 + lane + 64 * u : (NPc ? P0 : 0u)];   // (in bounds)
         asm volatile("" ::: "memory");   // (the loads stay ahead of the planes' DMA)
+#endif
         const uint32_t nq = dma16_wave(C.pl + 16, Dbq, sbq + 2 * (size_t)qa, 2 * (cur.qb - qa));
         wait_vm(nq);
         TPROF_MARK(2);
@@ -1156,8 +1210,14 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
             const uint32_t i = lane + 64 * u;
             Pw[u] = make_uint4(0u, 0u, 0u, 0u);
             oe[u] = 0;
+#if S2C_PX_LDS
+            pxr[u] = 0xFFFFFFFFu;
+#endif
             if (i < NPc) {
                 Pw[u] = pcr[i];
+#if S2C_PX_LDS
+                pxr[u] = pxl[i];
+#endif
                 oe[u] = i + 1 < NPc ? pcr[i + 1].z : O1;
                 const int32_t sw = (int32_t)(Pw[u].x >> 5) - (int32_t)S0;
                 const int32_t pw = i > 0 ? (int32_t)(pcr[i - 1].x >> 5) - (int32_t)S0 : -1;
@@ -1165,7 +1225,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
                 if (i + 1 == NPc)
                     for (uint32_t sg = (uint32_t)(sw + 1); sg <= NS; sg++) C.segR[sg] = NR;
                 const uint32_t f = Pw[u].w >> 24;
-#if S2C_PLANES_NARROW   // (only x_fix and the maxdel '-' count read the planes: S2C_PF_DASH implies S2C_PF_X)
+#if S2C_PX_LDS   // (x_fix and the maxdel '-' count read the planes; S2C_PF_XFEW pieces take px)
+                planes |= (f & S2C_PF_X) && !(f & (S2C_PF_XFEW | S2C_PF_LONG));
+#elif S2C_PLANES_NARROW   // (only x_fix and the maxdel '-' count read the planes: S2C_PF_DASH implies S2C_PF_X)
                 planes |= (f & S2C_PF_X) && ((f & S2C_PF_SIMPLE) ? !(f & S2C_PF_XFEW) : !(f & S2C_PF_LONG));
 #else
                 planes |= (f & S2C_PF_SIMPLE) ? ((f & S2C_PF_X) && !(f & S2C_PF_XFEW)) : !(f & S2C_PF_LONG);
@@ -1178,6 +1240,25 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
         for (uint32_t i = lane; i < RPAD; i += 64) C.runl[NR + i] = make_uint2(0u, 0u);
         if (TABL(1))   // (ablated walk: zero records)
             for (uint32_t i = lane; i < NR; i += 64) C.runl[i] = make_uint2(0u, 0u);
+#if S2C_WALK_QUEUE
+        // the pieces walked op by op go to a queue, walked after the others by the wave's first
+        // lanes: one such walk per lane and layer, not one for each of a lane's two pieces
+        uint32_t nwq;
+        {
+            bool cx[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++)
+                cx[u] = lane + 64 * u < NPc && !TABL(1) && !((Pw[u].w >> 24) & (S2C_PF_SIMPLE | S2C_PF_LONG));
+            const uint64_t m0 = __ballot(cx[0]), m1 = __ballot(cx[1]);
+            const uint32_t n0 = (uint32_t)__popcll(m0);
+            auto below = [&](uint64_t m) {
+                return (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            };
+            if (cx[0]) C.wq[below(m0)] = (uint8_t)lane;
+            if (cx[1]) C.wq[n0 + below(m1)] = (uint8_t)(lane + 64);
+            nwq = uni(n0 + (uint32_t)__popcll(m1));
+        }
+#endif
 #pragma unroll
         for (int u = 0; u < 2; u++) {
             if (lane + 64 * u >= NPc || TABL(1)) continue;
@@ -1200,10 +1281,26 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
             } else if (fl & S2C_PF_LONG) {   // (its runs come through the tile long lists)
                 for (uint32_t j = P.z; j < oe[u]; j++) C.runl[j - O0] = make_uint2(0u, 0u);
             } else {
+#if !S2C_WALK_QUEUE
                 walk_chunk_piece<NWP>(P, oe[u], opl, od, C.runl, 0u - O0, bql, xg, 0u, qadj, d.maxdel_active != 0,
-                                      (uint32_t)d.maxdel, a, n, hist, dV, dD);
+                                      (uint32_t)d.maxdel, a, n, hist, dV, dD, pxr[u]);
+#endif
             }
         }
+#if S2C_WALK_QUEUE
+        wave_lds_sync();   // (the queue)
+        for (uint32_t k = lane; k < nwq; k += 64) {
+            const uint32_t i = C.wq[k];
+            const uint32_t oend = i + 1 < NPc ? pcr[i + 1].z : O1;
+#if S2C_PX_LDS
+            const uint32_t pxw = pxl[i];
+#else
+            const uint32_t pxw = 0xFFFFFFFFu;
+#endif
+            walk_chunk_piece<NWP>(pcr[i], oend, opl, od, C.runl, 0u - O0, bql, xg, 0u, qadj, d.maxdel_active != 0,
+                                  (uint32_t)d.maxdel, a, n, hist, dV, dD, pxw);
+        }
+#endif
         wave_lds_sync();   // every run record written; the piece records and op words read
         // this layer's planes (and 'N' offsets) have landed from here on
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1648,6 +1745,7 @@ TileArgs tile_args(const s2c_dev &d) {
     p.ops_end = d.ops + std::max<int64_t>(d.n_ops, 1); p.pc_end = d.pc + 4 * (d.n_pieces + 1);
     p.lly = d.lly; p.lpc = d.lpc; p.lops = d.lops; p.lbq = d.lbq; p.lbx = d.lbx;
     p.px = d.px; p.lpx = d.lpx;
+    p.px_end = d.px + std::max<int64_t>(d.n_pieces, 1); p.lpx_end = d.lpx ? d.lpx + std::max<int64_t>(d.n_lpieces, 1) : nullptr;
     p.lbq_end = d.lbq + 2 * d.n_lqwords; p.lbx_end = d.lbx + d.n_lqwords;
     p.lops_end = d.lops + std::max<int64_t>(d.n_lops, 4); p.lpc_end = d.lpc + 4 * (d.n_lpieces + 1);
     p.maxdel_active = d.maxdel_active ? 1u : 0u;
