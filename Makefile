@@ -32,8 +32,8 @@ $(BUILD):
 # diagnostic build: phase clocks of k_tile_dense (S2C_LIB=libs2c_prof.so, scripts/prof_dense.py)
 PROF_OUT = sam2consensus_amd/libs2c_prof.so
 prof: $(BUILD)/s2c_host.o $(BUILD)/s2c_synth.o $(BUILD)/s2c_reads.o $(SRC)/s2c_tile.hip $(SRC)/s2c_dense.hip $(SRC)/s2c_common.h
-	$(HIPCC) $(HIPFLAGS) -DS2C_PROF -c $(SRC)/s2c_dense.hip -o $(BUILD)/s2c_dense_prof.o
-	$(HIPCC) $(HIPFLAGS) -DS2C_PROF -c $(SRC)/s2c_tile.hip -o $(BUILD)/s2c_tile_prof.o
+	$(HIPCC) $(HIPFLAGS) $(VDEFS) -DS2C_PROF -c $(SRC)/s2c_dense.hip -o $(BUILD)/s2c_dense_prof.o
+	$(HIPCC) $(HIPFLAGS) $(VDEFS) -DS2C_PROF -c $(SRC)/s2c_tile.hip -o $(BUILD)/s2c_tile_prof.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(BUILD)/s2c_host.o $(BUILD)/s2c_synth.o $(BUILD)/s2c_reads.o \
 	  $(BUILD)/s2c_tile_prof.o $(BUILD)/s2c_dense_prof.o -lz -lpthread -o $(PROF_OUT)
 

@@ -220,6 +220,10 @@ void s2c_parser_free(s2c_parser *p);
  *                   of the last mapped read (-1 if none), [3] reads held. */
 int  s2c_parser_set_tile_width(s2c_parser *p, int64_t width);
 int  s2c_parser_snapshot(s2c_parser *p, s2c_batch **out);
+/* (ABI 13) s2c_parser_snapshot planning only the tiles from t_from (a streamed batch's first
+ * tile) through the tile of the held reads' last position (info.plan_t0 / plan_t1); the
+ * other tiles get no work items.  Needs a tile width. */
+int  s2c_parser_snapshot_from(s2c_parser *p, int64_t t_from, s2c_batch **out);
 int  s2c_parser_retain(s2c_parser *p, int64_t gmin);
 int  s2c_parser_stream_state(const s2c_parser *p, int64_t *state);
 /* Pipelined snapshots: detach moves every read held into a new parser *out (the reference
@@ -311,6 +315,10 @@ typedef struct {
                                   wtile [word_lo, word_hi) — 0 and n_words for a whole batch, a shard's
                                   own words and its windows' lookback for s2c_batch_shard; the device
                                   copies (s2c_dev rs / ps / wtile) hold only those entries */
+    int64_t n_walked;          /* (ABI 13) pieces walked op by op (neither S2C_PF_SIMPLE nor S2C_PF_LONG) */
+    int64_t plan_t0, plan_t1;  /* (ABI 13) the tiles with a window, layers and work items: [0, n_tiles), or
+                                  for s2c_parser_snapshot_from(p, t_from) [t_from, the tile of the held
+                                  reads' last position] — the others keep bounds and insertion capacities */
 } s2c_batch_info;
 
 typedef struct {               /* host pointers into the batch (valid until s2c_batch_free) */
@@ -451,6 +459,8 @@ typedef struct {
     const uint32_t *dwin;      /* [n_dense][S2C_DWIN_WORDS] s2c_batch_arrays.dwin, filtered like dense */
     const uint32_t *lpx;       /* [n_lpieces] s2c_batch_arrays.lpx (ABI 11; required with n_layers > 0) */
     const uint32_t *dpc;       /* [n_dpc][S2C_DPC_WORDS] s2c_batch_arrays.dpc (ABI 12; required with n_dense > 0) */
+    int64_t   n_walked;           /* (ABI 13) the batch's info.n_walked: with at least 1/32 of the pieces
+                                     k_tile queues them for its walk (a variant of the kernel) */
     int64_t   word_lo, word_hi;   /* (ABI 13) the batch's info.word_lo / word_hi: rs and ps point at entry
                                      word_lo of s2c_batch_arrays rs / ps ([word_lo, word_hi] copied),
                                      wtile at entry word_lo ([word_lo, word_hi) copied) */

@@ -58,7 +58,7 @@ class BatchInfo(C.Structure):
         "aligned_bases", "query_bases", "n_pieces", "n_ops", "n_tokens", "n_qwords", "n_words",
         "n_tiles", "n_items", "n_dense", "n_deep", "n_long", "n_rlist", "kwin", "tile_max", "chunk",
         "n_ins", "n_ins_bases", "n_bkt", "n_lng", "n_cols", "runs_max", "dense_lds", "n_layers", "n_lpieces", "n_lops",
-        "n_lqwords", "layers_dense", "layers_built", "n_dpc", "word_lo", "word_hi")]
+        "n_lqwords", "layers_dense", "layers_built", "n_dpc", "word_lo", "word_hi", "n_walked", "plan_t0", "plan_t1")]
 
 
 _P64 = C.POINTER(C.c_int64)
@@ -96,7 +96,8 @@ class Dev(C.Structure):
         ("runs", _VP), ("ibkt", _VP), ("ilong", _VP), ("ilong_n", _VP), ("counts", _VP),
         ("ins_cols", _VP), ("ins_chr", _VP), ("n_cols", C.c_int64),
         ("tile_stats", _VP), ("blk_len", _VP), ("out", _VP), ("out_cap", C.c_int64), ("layers_dense", C.c_int64),
-        ("px", _VP), ("layers_built", C.c_int64), ("dwin", _VP), ("lpx", _VP), ("dpc", _VP), ("word_lo", C.c_int64), ("word_hi", C.c_int64)]
+        ("px", _VP), ("layers_built", C.c_int64), ("dwin", _VP), ("lpx", _VP), ("dpc", _VP), ("n_walked", C.c_int64), ("word_lo", C.c_int64),
+        ("word_hi", C.c_int64)]
 
 
 class WsSizes(C.Structure):
@@ -110,7 +111,7 @@ EXPORTS = [
     "s2c_last_error", "s2c_abi_version", "s2c_layout",
     "s2c_parser_new", "s2c_parser_feed", "s2c_parser_end_header", "s2c_parser_feed_file", "s2c_parser_finish", "s2c_parser_free",
     "s2c_reader_open", "s2c_reader_read", "s2c_reader_free",
-    "s2c_parser_set_tile_width", "s2c_parser_snapshot", "s2c_parser_retain", "s2c_parser_stream_state",
+    "s2c_parser_set_tile_width", "s2c_parser_snapshot", "s2c_parser_snapshot_from", "s2c_parser_retain", "s2c_parser_stream_state",
     "s2c_parser_retain_events", "s2c_parser_detach", "s2c_parser_attach", "s2c_accumulate",
     "s2c_parser_pos_weights", "s2c_parser_checks", "s2c_parser_counters", "s2c_parser_progress", "s2c_gather_bodies", "s2c_copy_bytes", "s2c_parser_pack",
     "s2c_parser_blob_copy", "s2c_parser_unpack",
@@ -145,6 +146,7 @@ def _load():
         "s2c_reader_free": (None, [_VP]),
         "s2c_parser_set_tile_width": (C.c_int, [_VP, C.c_int64]),
         "s2c_parser_snapshot": (C.c_int, [_VP, pp]),
+        "s2c_parser_snapshot_from": (C.c_int, [_VP, C.c_int64, pp]),
         "s2c_parser_retain": (C.c_int, [_VP, C.c_int64]),
         "s2c_parser_stream_state": (C.c_int, [_VP, C.POINTER(C.c_int64)]),
         "s2c_parser_retain_events": (C.c_int, [_VP]),

@@ -283,6 +283,7 @@ struct s2c_parser {
     // and whether a later read reached below the frontier (input not coordinate-sorted)
     int64_t tile_width = 0;
     int64_t frontier = 0;
+    int64_t plan_from = -1;   // s2c_parser_snapshot_from: plan the tiles from here only (-1: all)
     size_t n_kept = 0;
     bool late = false;
     bool detached = false;   // made by s2c_parser_detach: snapshot / retain / attach only, no input
@@ -1569,8 +1570,8 @@ static void build_layers(s2c_batch *b, int64_t G, bool with_dense) {
     std::vector<TL> tl;
     for (int64_t t = 0; t < NT; t++) {
         uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
-        if (!with_dense && (tw[3] & S2C_TILE_DENSE)) {   // (k_tile_dense reads its window in place)
-            tw[20] = S2C_LY_NONE;
+        if ((!with_dense && (tw[3] & S2C_TILE_DENSE)) || tw[19] == 0) {   // (k_tile_dense reads its window in
+            tw[20] = S2C_LY_NONE;                                          //  place; a ranged snapshot's unplanned tile)
             continue;
         }
         if (tw[19] == 1 && main_window_fits(b, tw, K, G)) {
@@ -1837,15 +1838,24 @@ extern "C" int s2c_parser_set_tile_width(s2c_parser *p, int64_t width) {
 }
 
 // The batch of everything parsed so far (the partial last line stays unparsed); the
-// parser keeps going.
-static int s2c_parser_snapshot_impl(s2c_parser *p, s2c_batch **out) {
+// parser keeps going.  With t_from >= 0 (s2c_parser_snapshot_from) only the tiles a streamed
+// batch can run are planned: from t_from through the tile of the reads' last position.
+static int s2c_parser_snapshot_impl(s2c_parser *p, int64_t t_from, s2c_batch **out) {
     if (!p || !out) return s2c_set_error(S2C_ERR_ARG, "NULL argument");
     if (p->err) return s2c_set_error(p->err, p->errmsg);
+    if (t_from >= 0 && p->tile_width <= 0) return s2c_set_error(S2C_ERR_ARG, "a ranged snapshot needs a tile width");
     check_late(p);
-    return build_batch(p, out);
+    p->plan_from = t_from;
+    const int rc = build_batch(p, out);
+    p->plan_from = -1;
+    return rc;
 }
 extern "C" int s2c_parser_snapshot(s2c_parser *p, s2c_batch **out) {
-    return s2c_guarded([&] { return s2c_parser_snapshot_impl(p, out); });
+    return s2c_guarded([&] { return s2c_parser_snapshot_impl(p, -1, out); });
+}
+extern "C" int s2c_parser_snapshot_from(s2c_parser *p, int64_t t_from, s2c_batch **out) {
+    if (t_from < 0) return s2c_set_error(S2C_ERR_ARG, "t_from < 0");
+    return s2c_guarded([&] { return s2c_parser_snapshot_impl(p, t_from, out); });
 }
 
 // Move the reads `keep` selects into one chunk (their tokens, planes and events; no line
@@ -2590,6 +2600,15 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
         });
     }
 
+    {   // pieces walked op by op (neither one token nor long): k_tile's walk queue pays for them
+        std::atomic<int64_t> nw{0};
+        par_ranges(plan_threads(NP, 1 << 18), NP, [&](int, int64_t k0, int64_t k1) {
+            int64_t m = 0;
+            for (int64_t k = k0; k < k1; k++) m += !((b->pc[4 * k + 3] >> 24) & (S2C_PF_SIMPLE | S2C_PF_LONG));
+            nw += m;
+        });
+        I.n_walked = nw;
+    }
     clk.mark("emit");
     // ---- tiles: width from depth; a shallow tile keeps its window's runs in LDS ----
     struct Tile { int64_t a, b, ref; };
@@ -2658,6 +2677,41 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
             tile_max = std::max(tile_max, tiles.back().b - a);
         }
     }
+    // A ranged snapshot (s2c_parser_snapshot_from) plans tiles [P0, P1) only: from the first
+    // tile its streamed batch runs through the tile of the held reads' last position (the
+    // pieces' ends, the last read's POS: the stream driver's bound); the other tiles keep
+    // their bounds and insertion capacities but get no window, layers or work items
+    int64_t P0 = 0, P1 = INT64_MAX;   // (a whole batch: every tile, after any split below)
+    if (p->plan_from >= 0) {   // (a fixed tile width: no split)
+        const int64_t NT0 = (int64_t)tiles.size();
+        std::vector<int64_t> tmax(ntw, -1);
+        par_ranges(ntw, NP, [&](int t, int64_t k0, int64_t k1) {
+            int64_t m = -1;
+            for (int64_t k = k0; k < k1; k++)
+                if (pcs[k].kb > pcs[k].ka) m = std::max<int64_t>(m, (int64_t)pcs[k].gpos + (pcs[k].kb - pcs[k].ka) - 1);
+            tmax[t] = m;
+        });
+        int64_t gmax = *std::max_element(tmax.begin(), tmax.end());
+        for (auto it = p->chunks.rbegin(); it != p->chunks.rend(); ++it)
+            if (!(*it)->reads.empty()) {
+                const ReadRec &r = (*it)->reads.back();
+                const int64_t L = p->ref_len[r.ref];
+                if (L > 0) gmax = std::max<int64_t>(gmax, b->ref_off[r.ref] + std::min<int64_t>(std::max<int64_t>(r.pos0, 0), L - 1));
+                break;
+            }
+        P0 = std::min<int64_t>(p->plan_from, NT0);
+        int64_t tl = P0;   // first tile past gmax
+        if (gmax >= 0) {
+            int64_t lo = 0, hi = NT0;   // first tile with a > gmax
+            while (lo < hi) {
+                const int64_t m = (lo + hi) / 2;
+                if (tiles[m].a > gmax) hi = m; else lo = m + 1;
+            }
+            tl = lo;
+        }
+        P1 = std::min<int64_t>(std::max<int64_t>(tl, P0), NT0);
+    }
+    auto planned = [&](int64_t t) { return t >= P0 && t < P1; };
     // Launch LDS of k_tile_dense = the largest dense window, so one outlier window sets every
     // tile's occupancy: when all but ≤ 0.2 % of the windows fit the share of a CU's 160 KB
     // that lets 8 two-wave tiles reside (4 waves per SIMD, the kernel's register budget), the
@@ -2672,6 +2726,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
         par_ranges(plan_threads(n0, 64), n0, [&](int, int64_t t0, int64_t t1) {
             uint32_t tw[S2C_TILE_WORDS];
             for (int64_t t = t0; t < t1; t++) {
+                if (!planned(t)) continue;
                 tile_window(b, K, (uint64_t)tiles[t].a, (uint64_t)tiles[t].b, tw);
                 if (dense_fits(tw, K)) db[t] = dense_bytes(tw, K);
             }
@@ -2701,6 +2756,8 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     const int64_t NT = (int64_t)tiles.size();
     I.n_tiles = NT;
     I.tile_max = tile_max;
+    I.plan_t0 = P0;
+    I.plan_t1 = std::min<int64_t>(P1, NT);
     b->wtile.assign(NW, 0xFFFFFFFFu);
     for (int64_t t = 0; t < NT; t++)
         for (int64_t W = tiles[t].a >> 5; W < (tiles[t].b + 31) >> 5; W++) b->wtile[W] = (uint32_t)t;
@@ -2762,6 +2819,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     std::atomic<bool> too_big{false};
     par_ranges(plan_threads(NT, 64), NT, [&](int, int64_t ta, int64_t tb) {
         for (int64_t t = ta; t < tb; t++) {
+            if (!planned(t)) { t_nl[t] = t_nch[t] = t_maxc[t] = t_wruns[t] = 0; continue; }
             const Tile &T = tiles[t];
             const int64_t w0 = T.a >> 5, w1 = (T.b + 31) >> 5;
             const int64_t nlg = lcnt[t + 1] - lcnt[t];
@@ -2795,7 +2853,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     // items of ≤ 64 layers (3.24 rounds of 768) become 3,0xx of ≤ 52.
     {
         int64_t n_single = 0, n_multi = 0;
-        for (int64_t t = 0; t < NT; t++) {
+        for (int64_t t = P0; t < std::min<int64_t>(P1, NT); t++) {
             if (t_nch[t] > 1) n_multi += t_nch[t];
             else if (!dense_tile(t)) n_single++;
         }
@@ -2829,7 +2887,8 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
         uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
         uint32_t fl = nch > 1 ? S2C_TILE_DEEP : 0u;
         if (nev[t] > S2C_EPI_KEYS || (int64_t)ccap[t] > lcols) fl |= S2C_TILE_GENERAL;
-        if (fl == 0 && nev[t] == 0 && maxc <= 255 && !no_dense && dense_fits(tw, K) &&
+        if (!planned(t)) fl = 0;   // (a ranged snapshot's unplanned tile: no items)
+        else if (fl == 0 && nev[t] == 0 && maxc <= 255 && !no_dense && dense_fits(tw, K) &&
             dense_bytes(tw, K) <= dense_cap && dpc_ok(tw))
             fl = S2C_TILE_DENSE;
         const uint32_t bcap = nshort[t] ? pow2_at_least(2 * (uint64_t)nshort[t]) : 0u;
@@ -2841,7 +2900,8 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
         boff += bcap;
         loff += nlong[t];
         coff += ccap[t];
-        if (fl == S2C_TILE_DENSE) {
+        if (!planned(t)) {
+        } else if (fl == S2C_TILE_DENSE) {
             I.dense_lds = std::max<int64_t>(I.dense_lds, dense_bytes(tw, K));
             const uint32_t it[S2C_ITEM_WORDS] = {(uint32_t)t, 0u, 0u, (uint32_t)nl};
             b->dense.insert(b->dense.end(), it, it + S2C_ITEM_WORDS);
@@ -3074,6 +3134,8 @@ static int s2c_batch_shard_impl(const s2c_batch *b, int64_t t0, int64_t t1, s2c_
     // the per-word entries the shard's launches read (s2c_batch_info word_lo / word_hi): its
     // tiles' words, the window lookback of k_tile_dense's run-slot ranges (rs[W - kwin]) and
     // the piece range above; k_reads drops events keyed outside
+    J.plan_t0 = 0;   // (every tile of a shard has its plan: tile_window above, items copied)
+    J.plan_t1 = NT;
     J.word_lo = t1 > t0 ? std::max<int64_t>(W0 - K - 1, 0) : 0;
     J.word_hi = t1 > t0 ? std::min<int64_t>(W1, NW) : 0;
     J.aligned_bases = I.total_len ? (int64_t)((double)I.aligned_bases * (double)aligned / (double)I.total_len) : 0;

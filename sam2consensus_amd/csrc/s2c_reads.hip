@@ -17,6 +17,10 @@
 // tile's long-event list (multiplicity 1; the column sums of :284-287 are additive).
 #include "s2c_common.h"
 
+#ifndef S2C_EV_FAST   // (variant builds: 0 = every piece through walk_piece, codes base by base)
+#define S2C_EV_FAST 1
+#endif
+
 namespace s2c {
 namespace {
 
@@ -55,6 +59,19 @@ __device__ __forceinline__ uint64_t mix64(uint64_t k) {
 
 // One insertion event (global key gkey, motif = query bases [q, q + len)) into its tile.
 __device__ void add_event(const ReadsArgs &d, uint64_t gkey, uint64_t q, uint32_t len) {
+#if S2C_EV_FAST
+    // a short motif's codes from its (at most two) plane words, loaded with the tile lookup
+    uint64_t c01[3] = {0, 0, 0};   // p0, p1, x of bases q .. q + 63
+    if (len <= S2C_SHORT_MOTIF) {
+        const uint64_t wq = q >> 5;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            c01[0] |= (uint64_t)d.bq[2 * (wq + h)] << (32 * h);
+            c01[1] |= (uint64_t)d.bq[2 * (wq + h) + 1] << (32 * h);
+            c01[2] |= (uint64_t)d.bx[wq + h] << (32 * h);
+        }
+    }
+#endif
     const uint64_t W = gkey >> 5;
     if (W < d.word_lo || W >= d.word_hi) return;   // keyed outside a multi-GPU shard's words
     const uint32_t t = d.wtile[W - d.word_lo];
@@ -64,7 +81,17 @@ __device__ void add_event(const ReadsArgs &d, uint64_t gkey, uint64_t q, uint32_
     const uint32_t pos = (uint32_t)(gkey - tw0.x);   // tile-relative (< 2048)
     if (len <= S2C_SHORT_MOTIF) {
         uint64_t key = (uint64_t)pos | ((uint64_t)len << 11);
+#if S2C_EV_FAST
+        const uint32_t sh = (uint32_t)(q & 31);
+        for (uint32_t c = 0; c < len; c++) {
+            const uint32_t p0 = (uint32_t)(c01[0] >> (sh + c)) & 1u, p1 = (uint32_t)(c01[1] >> (sh + c)) & 1u,
+                           x = (uint32_t)(c01[2] >> (sh + c)) & 1u;
+            const uint32_t code = x ? (p0 ? 0u : 4u) : ((p1 << 1 | p0) == 3u ? 5u : (p1 << 1 | p0) + 1u);
+            key |= (uint64_t)code << (16 + 3 * c);
+        }
+#else
         for (uint32_t c = 0; c < len; c++) key |= (uint64_t)base_code(d, q + c) << (16 + 3 * c);
+#endif
         const uint32_t boff = tw1.x, bcap = tw1.y;
         uint32_t s = (uint32_t)mix64(key) & (bcap - 1u);
         for (uint32_t probe = 0; probe < bcap; probe++) {   // bcap ≥ 2 × the tile's short events
@@ -84,6 +111,44 @@ __device__ void add_event(const ReadsArgs &d, uint64_t gkey, uint64_t q, uint32_
     }
 }
 
+// The insertion events of a piece walked for them only (no run records; the maxdel rule does
+// not touch events): its op words read together (one round trip), the walk in registers;
+// per event the motif's plane words and the tile lookup together, then the table.  Pieces of
+// more than EV_OPS op words take walk_piece.
+constexpr uint32_t EV_OPS = 12;
+__device__ __forceinline__ bool piece_events(const ReadsArgs &d, const uint4 P, uint32_t oend) {
+    const uint32_t fl = P.w >> 24, slen = P.w & 0xFFFFFFu, nw = oend - P.z;
+    if (nw > EV_OPS || !(fl & S2C_PF_INS)) return false;
+    uint32_t w[EV_OPS];
+#pragma unroll
+    for (uint32_t i = 0; i < EV_OPS; i++) w[i] = i < nw ? d.ops[P.z + i] : 0u;
+    const bool rg = (fl & S2C_PF_RANGE) != 0;
+    const uint32_t first = rg ? 5u : 3u;   // (prefix words: {ka, kb}, then {key0 lo, key0 hi, ref_off})
+    const int64_t key0 = (int64_t)((uint64_t)(rg ? w[2] : w[0]) | ((uint64_t)(rg ? w[3] : w[1]) << 32));
+    const uint32_t roff = rg ? w[4] : w[2];
+    const uint64_t q0 = (uint64_t)P.y * 16;
+    int64_t k = 0;
+    uint32_t start = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < EV_OPS; i++) {
+        if (i < first || i >= nw) continue;
+        const uint32_t op = w[i] & 15u, l = w[i] >> 4;
+        const uint32_t take = start < slen ? min(l, slen - start) : 0u;
+        if (op_bases(op)) {
+            k += take;
+            start += l;
+        } else if (op_dash(op)) {
+            k += l;
+        } else if (op == S2C_OP_I) {
+            if (take && key0 + k >= (int64_t)roff) add_event(d, (uint64_t)(key0 + k), q0 + start, take);
+            start += l;
+        } else if (op == S2C_OP_S) {
+            start += l;
+        }
+    }
+    return true;
+}
+
 __global__ __launch_bounds__(WG) void k_reads(const ReadsArgs d) {
     const uint32_t n = blockIdx.x * WG + threadIdx.x;
     if (n >= d.n) return;
@@ -91,6 +156,9 @@ __global__ __launch_bounds__(WG) void k_reads(const ReadsArgs d) {
     const uint4 P = ((const uint4 *)d.pc)[i];
     const uint32_t oend = d.pc[4 * (size_t)i + 6];   // next piece's opoff (sentinel at the end)
     const bool runs = d.all || ((P.w >> 24) & S2C_PF_RUNS);
+#if S2C_EV_FAST
+    if (!runs && piece_events(d, P, oend)) return;
+#endif
     uint4 *out = (uint4 *)d.runs;
     walk_piece(GlobalMem{d.ops, d.bq, d.bx}, P, oend, d.maxdel_active != 0, d.maxdel,
                [&](uint32_t j, uint32_t g, uint32_t l, uint32_t k, uint64_t q) {

@@ -98,6 +98,7 @@ struct TileArgs {
     uint64_t *tile_stats, *blk_len;
     uint8_t *out;
     uint32_t padded_len, n_cols, n_tiles, kwin, chunk, n_qwords, runs_bytes, mode;   // MODE_* below
+    uint32_t walk_queue;   // (host only: which k_tile instantiation)
     int32_t n_thr, min_depth, fill_len, fill_nondash;
 };
 
@@ -667,6 +668,21 @@ __device__ __forceinline__ void tile_epilogue_fast(const D &d, uint32_t tile, co
 // word is fetched from HBM once per tile (chunks are disjoint; neighbouring tiles share kwin
 // start words).  Long pieces (span > the window) come from k_reads' run records through
 // the tile's long list.  Then the epilogue (a single-item tile) or the counts to HBM.
+// Walk options (variant builds set them to 0 for A/B; profiles/r05/v8_*):
+//   S2C_PX_LDS     the pieces' px words come with the layer's records (ahead DMA into LDS);
+//                  a walked piece with <= 2 'N' (S2C_PF_XFEW) adds them from px: no HBM scan
+//   S2C_WALK_QUEUE the pieces walked op by op are queued and walked after the others by the
+//                  wave's first lanes (one such walk per lane and layer)
+//   S2C_MAXDEL_1P  without '-' in SEQ the maxdel sum comes from the walk itself
+#ifndef S2C_PX_LDS
+#define S2C_PX_LDS 1
+#endif
+#ifndef S2C_WALK_QUEUE
+#define S2C_WALK_QUEUE 1
+#endif
+#ifndef S2C_MAXDEL_1P
+#define S2C_MAXDEL_1P 1
+#endif
 constexpr int GS = 8;                 // records per counting group
 constexpr int CSEG = S2C_CHUNK_SEGS;  // segments of a window (≤ 64 words + kwin ≤ 32)
 constexpr uint32_t RPAD = 64;         // zero records after a chunk's last (a group's reads past it: ≤ 7·G ≤ 56)
@@ -685,18 +701,21 @@ constexpr uint32_t OOR = 0xF0000000u;
 // The non-ACGT words stay in HBM (the few pieces that need them: S2C_PF_XFEW pieces take their
 // 'N' from px).  runl: the run records; segR[σ]: the first run record of the layer's pieces
 // starting in word S0 + σ (pieces are in start-word order).
-struct ChunkLds {
+// With EXT (S2C_PX_LDS / S2C_WALK_QUEUE, tiles of <= 1024 positions: the 2048-position
+// instantiation keeps 2 workgroups per CU without them) also the pieces' px words (ahead,
+// like pcb) and the queue of the pieces walked op by op.
+template <bool EXT> struct ChunkExt {};
+template <> struct ChunkExt<true> {
+    alignas(16) uint32_t pxl[S2C_CHUNK_PIECES + 4];
+    uint8_t wq[S2C_CHUNK_PIECES];
+};
+template <bool EXT>
+struct ChunkLds : ChunkExt<EXT> {
     uint32_t segR[CSEG + 1];
     alignas(16) uint8_t pl[16 + S2C_CHUNK_QBYTES + 16];
     alignas(16) uint4 pcb[S2C_CHUNK_PIECES];
     alignas(16) uint8_t ol[S2C_CHUNK_OBYTES + 16];
     alignas(16) uint2 runl[S2C_CHUNK_RECS + RPAD];
-#if S2C_PX_LDS
-    alignas(16) uint32_t pxl[S2C_CHUNK_PIECES + 4];   // the pieces' px words (ahead, like pcb)
-#endif
-#if S2C_WALK_QUEUE
-    uint8_t wq[S2C_CHUNK_PIECES];   // the layer's pieces walked op by op (neither simple nor long)
-#endif
 };
 
 typedef int v4i_t __attribute__((ext_vector_type(4)));
@@ -769,9 +788,9 @@ struct EpiLds {
     FastLds<ICOL> L;
     uint32_t cols[ICOL * NSYM];
 };
-template <uint32_t ICOL>
+template <uint32_t ICOL, bool EXT>
 union TileLds {
-    ChunkLds c[WV];   // one chunk per wave
+    ChunkLds<EXT> c[WV];   // one chunk per wave
     EpiLds<ICOL> e;
 };
 // the non-ACGT words in HBM, as a global-address-space pointer (a uniform base + 32-bit lane
@@ -802,8 +821,13 @@ __device__ __forceinline__ void x_bits(uint32_t xm, uint32_t p0, int32_t b0, uin
         }
     }
 }
+#if S2C_XFIX_NOINLINE   // (variant: the rare non-ACGT scan out of line — fewer VGPRs for the walk)
+#define S2C_XFIX_ATTR __attribute__((noinline))
+#else
+#define S2C_XFIX_ATTR
+#endif
 template <int NWP>
-__device__ void x_fix(const uint2 *bql, gptr_u32 xl, uint32_t xd, uint32_t q, uint32_t l, uint32_t r0, bool drop,
+__device__ S2C_XFIX_ATTR void x_fix(const uint2 *bql, gptr_u32 xl, uint32_t xd, uint32_t q, uint32_t l, uint32_t r0, bool drop,
                       uint32_t *hist) {
     const uint32_t v0 = q >> 5, v1 = (q + l - 1) >> 5;
     for (uint32_t vb = v0; vb <= v1; vb += 4) {   // four HBM words per round trip, then one at a time
@@ -829,7 +853,7 @@ __device__ void x_fix(const uint2 *bql, gptr_u32 xl, uint32_t xd, uint32_t q, ui
 // LDS plane base 16·P.y + qadj): parsecigar (:64-81) + maxdel (:210) → run records
 // runl[j + rd] (bases: rec_enc records; others zero); coverage / counted '-' of the
 // tile part into dV / dD; N / '-' of SEQ via x_fix.  Everything from LDS.
-template <int NWP>
+template <int NWP, bool PXL>
 __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *opl, uint32_t od, uint2 *runl, uint32_t rd,
                                  const uint2 *bql, gptr_u32 xl, uint32_t xd, uint32_t qadj, bool maxdel_active,
                                  uint32_t maxdel, uint32_t a, uint32_t n, uint32_t *hist, int32_t *dV, int32_t *dD,
@@ -907,8 +931,7 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
                     if (c1 > c0) {
                         atomicAdd(&dV[c0 - a], 1);
                         atomicSub(&dV[c1 - a], 1);
-#if S2C_PX_LDS
-                        if ((fl & (S2C_PF_X | S2C_PF_XFEW)) == (S2C_PF_X | S2C_PF_XFEW)) {
+                        if (PXL && (fl & (S2C_PF_X | S2C_PF_XFEW)) == (S2C_PF_X | S2C_PF_XFEW)) {
                             // ≤ 2 'N' at SEQ offsets px (s2c.h S2C_PF_XFEW): the run holds SEQ [so, so + len)
                             const uint32_t so = start + (s - kk);
 #pragma unroll
@@ -916,9 +939,9 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
                                 const uint32_t off = (pxw >> (16 * h)) & 0xFFFFu, p = gp + (off - so);   // (0xFFFF: none)
                                 if (off != 0xFFFFu && off - so < len && p >= c0 && p < c1) Hist<NWP>::add1(hist, SL_N, p - a, 1u);
                             }
-                        } else
-#endif
-                        if (fl & S2C_PF_X) x_fix<NWP>(bql, xl, xd, q + (c0 - gp), c1 - c0, c0 - a, drop, hist);
+                        } else if (fl & S2C_PF_X) {
+                            x_fix<NWP>(bql, xl, xd, q + (c0 - gp), c1 - c0, c0 - a, drop, hist);
+                        }
                     }
 #if S2C_MAXDEL_1P
                 } else if (defer && c1 > c0) {
@@ -975,7 +998,7 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
 #ifndef S2C_TILE_XCD
 #define S2C_TILE_XCD 1
 #endif
-template <int NWP>
+template <int NWP, bool WQB>
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 3 : 2))) void k_tile(const TileArgs d, const uint32_t *items) {
     constexpr int HP = 17 * NWP;
     constexpr uint32_t NPOS = 32 * NWP;
@@ -985,7 +1008,10 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     __shared__ __attribute__((aligned(16))) uint32_t hist[H::CS];
     __shared__ int32_t dV[NPOS + 1], dD[NPOS + 1];
     __shared__ uint32_t wtot[2][WG / 64];
-    __shared__ __attribute__((aligned(16))) TileLds<ICOL> U;
+    // WQB: the launch's batch has pieces walked op by op (s2c_dev n_walked); without them the
+    // queue's code costs C3 / C4 4 % (profiles/r05/v9_*), so it is a separate instantiation
+    constexpr bool PXL = S2C_PX_LDS && NWP <= 32, WQ = S2C_WALK_QUEUE && WQB && NWP <= 32;   // (ChunkLds' EXT)
+    __shared__ __attribute__((aligned(16))) TileLds<ICOL, PXL || WQ> U;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
 #ifdef S2C_PROF
     const uint32_t tabl = uni(*(volatile uint32_t *)&g_tabl);
@@ -1075,7 +1101,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     constexpr uint32_t GW = 64 / NWP;
     const uint32_t ww = lane / GW, ga = lane % GW, Ww = W0 + ww;
     const bool wact = ww < nwords;
-    ChunkLds &C = U.c[wv];
+    auto &C = U.c[wv];
     // this lane's word reads the records of segments [sa, sb] (start words Ww - K .. Ww)
     const uint32_t sa = wact ? (Ww >= S0 + K ? Ww - K : S0) - S0 : 1u, sb = wact ? Ww - S0 : 0u;
     const uint2 *bql = (const uint2 *)(C.pl + 16);
@@ -1142,9 +1168,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     const uint32_t *const spx = inplace ? d.px : d.lpx;
     const DmaSrc Dpc = dma_src(spc, inplace ? d.pc_end : d.lpc_end), Dops = dma_src(sops, inplace ? d.ops_end : d.lops_end);
     const DmaSrc Dbq = dma_src(sbq, inplace ? d.bq_end : d.lbq_end);
-#if S2C_PX_LDS
     const DmaSrc Dpx = dma_src(spx, inplace ? d.px_end : d.lpx_end);
-#endif
     const uint4 *const pcr = C.pcb;
     // a layer's bounds: pieces [P0, P1), op words [O0, O1), plane words [qa, qb) (scalar loads)
     struct Lay {
@@ -1168,9 +1192,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     // issued
     auto issue_ahead = [&](const Lay &L) -> uint32_t {
         uint32_t k = dma16_wave((uint8_t *)C.pcb, Dpc, spc + 4 * (size_t)L.P0, 4 * (L.P1 - L.P0));
-#if S2C_PX_LDS
-        k += dma16_wave((uint8_t *)C.pxl, Dpx, spx + L.P0, L.P1 - L.P0);
-#endif
+        if constexpr (PXL) k += dma16_wave((uint8_t *)C.pxl, Dpx, spx + L.P0, L.P1 - L.P0);
         return k + dma16_wave(C.ol, Dops, sops + L.O0, L.O1 - L.O0);
     };
     uint32_t ly = l0 + wv;
@@ -1185,14 +1207,15 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
         //      what was issued ahead (older: everything but the planes)
         const uint32_t P0 = cur.P0, O0 = cur.O0, O1 = cur.O1, qa = cur.qa;
         const uint32_t NPc = cur.P1 - cur.P0, NR = O1 - O0;
-        uint32_t pxr[2];
-#if S2C_PX_LDS
-        const uint32_t *const pxl = C.pxl + (P0 & 3u);   // (px of layer piece i: pxl[i], ahead with the records)
-#else
+        uint32_t pxr[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+        const uint32_t *pxl = nullptr;   // (PXL: px of layer piece i at pxl[i], ahead with the records)
+        if constexpr (PXL) {
+            pxl = C.pxl + (P0 & 3u);
+        } else {
 #pragma unroll
-        for (int u = 0; u < 2; u++) pxr[u] = spx[lane + 64 * u < NPc ? P0 + lane + 64 * u : (NPc ? P0 : 0u)];   // (in bounds)
-        asm volatile("" ::: "memory");   // (the loads stay ahead of the planes' DMA)
-#endif
+            for (int u = 0; u < 2; u++) pxr[u] = spx[lane + 64 * u < NPc ? P0 + lane + 64 * u : (NPc ? P0 : 0u)];   // (in bounds)
+            asm volatile("" ::: "memory");   // (the loads stay ahead of the planes' DMA)
+        }
         const uint32_t nq = dma16_wave(C.pl + 16, Dbq, sbq + 2 * (size_t)qa, 2 * (cur.qb - qa));
         wait_vm(nq);
         TPROF_MARK(2);
@@ -1210,14 +1233,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
             const uint32_t i = lane + 64 * u;
             Pw[u] = make_uint4(0u, 0u, 0u, 0u);
             oe[u] = 0;
-#if S2C_PX_LDS
-            pxr[u] = 0xFFFFFFFFu;
-#endif
             if (i < NPc) {
                 Pw[u] = pcr[i];
-#if S2C_PX_LDS
-                pxr[u] = pxl[i];
-#endif
+                if constexpr (PXL) pxr[u] = pxl[i];
                 oe[u] = i + 1 < NPc ? pcr[i + 1].z : O1;
                 const int32_t sw = (int32_t)(Pw[u].x >> 5) - (int32_t)S0;
                 const int32_t pw = i > 0 ? (int32_t)(pcr[i - 1].x >> 5) - (int32_t)S0 : -1;
@@ -1225,13 +1243,10 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
                 if (i + 1 == NPc)
                     for (uint32_t sg = (uint32_t)(sw + 1); sg <= NS; sg++) C.segR[sg] = NR;
                 const uint32_t f = Pw[u].w >> 24;
-#if S2C_PX_LDS   // (x_fix and the maxdel '-' count read the planes; S2C_PF_XFEW pieces take px)
-                planes |= (f & S2C_PF_X) && !(f & (S2C_PF_XFEW | S2C_PF_LONG));
-#elif S2C_PLANES_NARROW   // (only x_fix and the maxdel '-' count read the planes: S2C_PF_DASH implies S2C_PF_X)
-                planes |= (f & S2C_PF_X) && ((f & S2C_PF_SIMPLE) ? !(f & S2C_PF_XFEW) : !(f & S2C_PF_LONG));
-#else
-                planes |= (f & S2C_PF_SIMPLE) ? ((f & S2C_PF_X) && !(f & S2C_PF_XFEW)) : !(f & S2C_PF_LONG);
-#endif
+                if constexpr (PXL)   // (x_fix and the maxdel '-' count read the planes; S2C_PF_XFEW pieces take px)
+                    planes |= (f & S2C_PF_X) && !(f & (S2C_PF_XFEW | S2C_PF_LONG));
+                else
+                    planes |= (f & S2C_PF_SIMPLE) ? ((f & S2C_PF_X) && !(f & S2C_PF_XFEW)) : !(f & S2C_PF_LONG);
             }
         }
         if (NPc == 0)
@@ -1240,11 +1255,10 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
         for (uint32_t i = lane; i < RPAD; i += 64) C.runl[NR + i] = make_uint2(0u, 0u);
         if (TABL(1))   // (ablated walk: zero records)
             for (uint32_t i = lane; i < NR; i += 64) C.runl[i] = make_uint2(0u, 0u);
-#if S2C_WALK_QUEUE
-        // the pieces walked op by op go to a queue, walked after the others by the wave's first
-        // lanes: one such walk per lane and layer, not one for each of a lane's two pieces
-        uint32_t nwq;
-        {
+        // (WQ) the pieces walked op by op go to a queue, walked after the others by the wave's
+        // first lanes: one such walk per lane and layer, not one for each of a lane's two pieces
+        uint32_t nwq = 0;
+        if constexpr (WQ) {
             bool cx[2];
 #pragma unroll
             for (int u = 0; u < 2; u++)
@@ -1258,7 +1272,6 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
             if (cx[1]) C.wq[n0 + below(m1)] = (uint8_t)(lane + 64);
             nwq = uni(n0 + (uint32_t)__popcll(m1));
         }
-#endif
 #pragma unroll
         for (int u = 0; u < 2; u++) {
             if (lane + 64 * u >= NPc || TABL(1)) continue;
@@ -1274,39 +1287,39 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
                     atomicSub(&dV[c1 - a], 1);
 #endif
 #ifndef S2C_ABL_X
-                    if ((fl & S2C_PF_X) && !(fl & S2C_PF_XFEW))   // (S2C_PF_XFEW: after the walk)
+                    if (PXL && (fl & (S2C_PF_X | S2C_PF_XFEW)) == (S2C_PF_X | S2C_PF_XFEW)) {   // ≤ 2 'N' at SEQ offsets px
+#pragma unroll
+                        for (int h = 0; h < 2; h++) {
+                            const uint32_t off = (pxr[u] >> (16 * h)) & 0xFFFFu, p = P.x + off;   // (0xFFFF: none)
+                            if (off != 0xFFFFu && p >= c0 && p < c1) H::add1(hist, SL_N, p - a, 1u);
+                        }
+                    } else if ((fl & S2C_PF_X) && !(fl & S2C_PF_XFEW)) {   // (without PXL: S2C_PF_XFEW after the walk)
                         x_fix<NWP>(bql, xg, 0u, ql + (c0 - P.x), c1 - c0, c0 - a, false, hist);
+                    }
 #endif
                 }
             } else if (fl & S2C_PF_LONG) {   // (its runs come through the tile long lists)
                 for (uint32_t j = P.z; j < oe[u]; j++) C.runl[j - O0] = make_uint2(0u, 0u);
-            } else {
-#if !S2C_WALK_QUEUE
-                walk_chunk_piece<NWP>(P, oe[u], opl, od, C.runl, 0u - O0, bql, xg, 0u, qadj, d.maxdel_active != 0,
-                                      (uint32_t)d.maxdel, a, n, hist, dV, dD, pxr[u]);
-#endif
+            } else if constexpr (!WQ) {
+                walk_chunk_piece<NWP, PXL>(P, oe[u], opl, od, C.runl, 0u - O0, bql, xg, 0u, qadj, d.maxdel_active != 0,
+                                           (uint32_t)d.maxdel, a, n, hist, dV, dD, pxr[u]);
             }
         }
-#if S2C_WALK_QUEUE
-        wave_lds_sync();   // (the queue)
-        for (uint32_t k = lane; k < nwq; k += 64) {
-            const uint32_t i = C.wq[k];
-            const uint32_t oend = i + 1 < NPc ? pcr[i + 1].z : O1;
-#if S2C_PX_LDS
-            const uint32_t pxw = pxl[i];
-#else
-            const uint32_t pxw = 0xFFFFFFFFu;
-#endif
-            walk_chunk_piece<NWP>(pcr[i], oend, opl, od, C.runl, 0u - O0, bql, xg, 0u, qadj, d.maxdel_active != 0,
-                                  (uint32_t)d.maxdel, a, n, hist, dV, dD, pxw);
+        if constexpr (WQ) {
+            if (nwq) wave_lds_sync();   // (the queue)
+            for (uint32_t k = lane; k < nwq; k += 64) {
+                const uint32_t i = C.wq[k];
+                const uint32_t oend = i + 1 < NPc ? pcr[i + 1].z : O1;
+                walk_chunk_piece<NWP, PXL>(pcr[i], oend, opl, od, C.runl, 0u - O0, bql, xg, 0u, qadj, d.maxdel_active != 0,
+                                           (uint32_t)d.maxdel, a, n, hist, dV, dD, PXL ? pxl[i] : 0xFFFFFFFFu);
+            }
         }
-#endif
         wave_lds_sync();   // every run record written; the piece records and op words read
         // this layer's planes (and 'N' offsets) have landed from here on
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifndef S2C_ABL_X
+#if !defined(S2C_ABL_X)
 #pragma unroll
-        for (int u = 0; u < 2; u++) {   // ≤ 2 'N' of an S2C_PF_XFEW piece at its SEQ offsets px: no plane scan
+        for (int u = 0; u < 2 && !PXL; u++) {   // ≤ 2 'N' of an S2C_PF_XFEW piece at its SEQ offsets px: no plane scan
             const uint4 P = Pw[u];
             const uint32_t fl = P.w >> 24;
             if (lane + 64 * u >= NPc || TABL(1) || (fl & (S2C_PF_SIMPLE | S2C_PF_XFEW)) != (S2C_PF_SIMPLE | S2C_PF_XFEW))
@@ -1757,6 +1770,7 @@ TileArgs tile_args(const s2c_dev &d) {
     p.kwin = (uint32_t)d.kwin; p.chunk = (uint32_t)d.chunk; p.n_qwords = (uint32_t)d.n_qwords;
     p.runs_bytes = (uint32_t)std::min<int64_t>(16 * std::max<int64_t>(d.n_ops, 1), 0xFFFFFFF0ll);
     p.mode = MODE_RUN;
+    p.walk_queue = d.n_walked > 0 && 32 * d.n_walked >= d.n_pieces ? 1u : 0u;
     p.n_thr = d.n_thr; p.min_depth = d.min_depth; p.fill_len = d.fill_len; p.fill_nondash = d.fill_nondash;
     return p;
 }
@@ -1764,7 +1778,8 @@ TileArgs tile_args(const s2c_dev &d) {
 template <int NWP>
 int launch_tile(const TileArgs &a, const uint32_t *items, int64_t n, hipStream_t s) {
     if (n <= 0) return S2C_OK;
-    k_tile<NWP><<<(unsigned)n, WG, 0, s>>>(a, items);
+    if (a.walk_queue) k_tile<NWP, true><<<(unsigned)n, WG, 0, s>>>(a, items);
+    else k_tile<NWP, false><<<(unsigned)n, WG, 0, s>>>(a, items);
     return hip_check(hipGetLastError(), "k_tile");
 }
 int launch_tiles(const TileArgs &a, int32_t tile_max, const uint32_t *items, int64_t n, hipStream_t s) {

@@ -64,9 +64,14 @@ class StreamParser(Parser):
         hb.maxdel_active, hb.maxdel = self.maxdel_active, self.maxdel
         return hb
 
-    def snapshot(self) -> HostBatch:
+    def snapshot(self, t_from=None) -> HostBatch:
+        """The batch of the reads held; with ``t_from`` only tiles t_from .. the tile of the
+        reads' last position are planned (``s2c_parser_snapshot_from``: info.plan_t0 / plan_t1)."""
         h = C.c_void_p()
-        L.check(L.lib.s2c_parser_snapshot(self._p, C.byref(h)))
+        if t_from is None:
+            L.check(L.lib.s2c_parser_snapshot(self._p, C.byref(h)))
+        else:
+            L.check(L.lib.s2c_parser_snapshot_from(self._p, int(t_from), C.byref(h)))
         return self._wrap(h)
 
     def retain(self, gmin):
@@ -194,7 +199,7 @@ def _sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, st
         ("run", sub, t_lo, t1, NT, held)."""
         try:
             t0 = clk()
-            hb = q.snapshot()
+            hb = q.snapshot(t_lo)    # (planned from t_lo: tiles before it ran with an earlier batch)
             add("snapshot", t0)
         except (KeyError, IndexError):
             return ("broken",)       # s2c_parser_finish raises it once the input is read
@@ -207,6 +212,7 @@ def _sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, st
             bound = int(hb.ref_off[ref]) + max(pos0, 0)
             NT = int(hb.info.n_tiles)
             t1 = int(np.searchsorted(hb.tiles[:, 1].astype(np.int64), bound, side="right"))
+            assert t1 <= int(hb.info.plan_t1) or t1 <= t_lo, "ranged snapshot plan ends before the batch's bound"
             if t1 <= t_lo:
                 return ("skip", held)
             gmin = int(hb.tiles[t1, 0]) if t1 < NT else int(hb.info.padded_len)

@@ -14,6 +14,7 @@
 #   profdefault           rocprofv3 --kernel-trace --stats of the default bench line
 #   pmc:WL                PMC passes of WL (scripts/pmc.sh)
 #   phases:WL             phase clocks of the dense kernel (libs2c_prof.so, scripts/prof_dense.py)
+#   tphases:WL            phase clocks of k_tile (libs2c_prof.so, scripts/prof_tile.py)
 #   rehearse:N            bench --rehearse-shards N (the one-GPU rehearsal of the N-way split)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}" || exit 1
@@ -69,6 +70,10 @@ for st in "$@"; do
       S2C_LIB=libs2c_prof.so timeout -k 10 300 python -u scripts/prof_dense.py $arg 0 > gpurun_out/${T}_phases_$arg.txt 2>&1 \
         || { tail -9 gpurun_out/${T}_phases_$arg.txt; exit 1; }
       tail -12 gpurun_out/${T}_phases_$arg.txt ;;
+    tphases)
+      S2C_LIB=libs2c_prof.so timeout -k 10 300 python -u scripts/prof_tile.py $arg > gpurun_out/${T}_tphases_$arg.txt 2>&1 \
+        || { tail -9 gpurun_out/${T}_tphases_$arg.txt; exit 1; }
+      tail -12 gpurun_out/${T}_tphases_$arg.txt ;;
     rehearse)
       timeout -k 10 600 python -u bench.py --rehearse-shards $arg > gpurun_out/${T}_rehearse_$arg.json 2> gpurun_out/${T}_rehearse_$arg.err \
         || { tail -5 gpurun_out/${T}_rehearse_$arg.err; exit 1; } ;;

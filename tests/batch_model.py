@@ -177,7 +177,10 @@ def check_plan(hb):
         assert int(t) not in items and c == 0 and l0 == 0 and l1 == T[t, 19]
         items[int(t)] = [(0, 0, int(l1))]
         assert T[t, 3] == 4
-    assert sorted(items) == list(range(i.n_tiles))
+    # (a ranged snapshot, s2c_parser_snapshot_from, plans tiles [plan_t0, plan_t1) only)
+    P0, P1 = int(i.plan_t0), int(i.plan_t1)
+    assert 0 <= P0 <= P1 <= i.n_tiles
+    assert sorted(items) == list(range(P0, P1))
     for t, cs in items.items():
         cs = sorted(cs)
         assert [c for c, _, _ in cs] == list(range(len(cs)))
@@ -207,6 +210,9 @@ def check_plan(hb):
     assert sorted(hb.deep.tolist()) == [t for t in range(i.n_tiles) if T[t, 3] & 3]
     # window fields: pieces [pf0, pf1) start in words [a/32 - kwin, ceil(b/32)); slots, planes
     for t, row in enumerate(T):
+        if not P0 <= t < P1:
+            assert row[3] == 0 and row[19] == 0 and (row[13:19] == 0).all()
+            continue
         w0, w1 = max((row[0] >> 5) - K, 0), (row[1] + 31) >> 5
         pf0, pf1 = np.searchsorted(sw, [w0, w1])
         assert (row[13], row[14]) == (pf0, pf1) and (row[15], row[16]) == (pc[pf0, 2], pc[pf1, 2])
@@ -269,7 +275,7 @@ def check_layers(hb):
     K = i.kwin
     lly, lpc = hb.lly.astype(np.int64), hb.lpc.astype(np.int64)
     T = hb.tiles.astype(np.int64)
-    for t in range(i.n_tiles):
+    for t in range(int(i.plan_t0), int(i.plan_t1)):
         row = T[t]
         S0, W0, W1, lays = layer_ranges(hb, t)
         assert W1 - S0 <= 128

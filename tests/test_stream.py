@@ -299,15 +299,15 @@ def _slow_stages(monkeypatch, log, delay=0.1):
     import time
     snap, feed = stream.StreamParser.snapshot, stream.StreamParser.feed
 
-    def slow_snapshot(self):
+    def slow_snapshot(self, *a):
         if threading.current_thread().name.startswith("s2c-stage"):
             log["in_stage"] += 1
             try:
                 time.sleep(delay)
-                return snap(self)
+                return snap(self, *a)
             finally:
                 log["in_stage"] -= 1
-        return snap(self)
+        return snap(self, *a)
 
     def logged_feed(self, data):
         n0 = log["fed"]
@@ -381,3 +381,35 @@ def test_feed_error_while_a_stage_runs(monkeypatch, late_frac):
         if pipe == "1":
             assert log["mark_in_stage"] is True
     assert got["1"] == got["0"] == ("ValueError", {})
+
+
+def test_ranged_snapshot_plans_only_the_tiles_a_batch_can_run():
+    """s2c_parser_snapshot_from (ABI 13, the streamed driver's snapshots): tiles before t_from
+    and after the tile of the held reads' last position get no window, layers or items; the
+    tiles in between are planned exactly as a whole snapshot plans them."""
+    sam = _sorted_case().encode("latin-1")
+    p = stream.StreamParser(True, 150, 64)
+    p.feed(sam[: len(sam) * 2 // 3])
+    full = p.snapshot()
+    nt = int(full.info.n_tiles)
+    assert (full.info.plan_t0, full.info.plan_t1) == (0, nt)
+    for t_from in (0, 5, nt // 3):
+        part = p.snapshot(t_from)
+        try:
+            P0, P1 = int(part.info.plan_t0), int(part.info.plan_t1)
+            assert P0 == t_from and t_from < P1 < nt
+            bm.check_plan(part)
+            _, ref, pos0, _ = p.state()
+            bound = int(part.ref_off[ref]) + max(pos0, 0)
+            t1 = int(np.searchsorted(part.tiles[:, 1].astype(np.int64), bound, side="right"))
+            assert t1 <= P1                                      # every tile the batch can run is planned
+            # planned tiles: the same records (windows, capacities, layers) and items
+            assert np.array_equal(part.tiles[P0:P1, :20], full.tiles[P0:P1, :20])
+            keep = lambda a: a[(a[:, 0] >= P0) & (a[:, 0] < P1)]  # noqa: E731
+            assert np.array_equal(keep(part.items), keep(full.items)) and np.array_equal(keep(part.dense), keep(full.dense))
+            assert (part.tiles[:P0, 3] == 0).all() and (part.tiles[P1:, 19] == 0).all()
+            assert len(part.items) + len(part.dense) < len(full.items) + len(full.dense)
+        finally:
+            part.free()
+    full.free()
+    p.close()
