@@ -18,8 +18,10 @@ $(BUILD)/s2c_host.o: $(SRC)/s2c_host.cpp include/s2c.h | $(BUILD)
 $(BUILD)/s2c_synth.o: $(SRC)/s2c_synth.cpp include/s2c.h | $(BUILD)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
-$(BUILD)/%.o: $(SRC)/%.hip $(SRC)/s2c_common.h include/s2c.h | $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+# (every kernel's resource remarks checked: a spill fails the build, scripts/check_spills.py)
+$(BUILD)/%.o: $(SRC)/%.hip $(SRC)/s2c_common.h include/s2c.h scripts/check_spills.py | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage -c $< -o $@ 2> $(BUILD)/$*.usage || { cat $(BUILD)/$*.usage; exit 1; }
+	python3 scripts/check_spills.py $(BUILD)/$*.usage || { rm -f $@; exit 1; }
 
 KOBJ = $(BUILD)/s2c_reads.o $(BUILD)/s2c_tile.o $(BUILD)/s2c_dense.o
 

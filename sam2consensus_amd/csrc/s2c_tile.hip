@@ -821,13 +821,8 @@ __device__ __forceinline__ void x_bits(uint32_t xm, uint32_t p0, int32_t b0, uin
         }
     }
 }
-#if S2C_XFIX_NOINLINE   // (variant: the rare non-ACGT scan out of line — fewer VGPRs for the walk)
-#define S2C_XFIX_ATTR __attribute__((noinline))
-#else
-#define S2C_XFIX_ATTR
-#endif
 template <int NWP>
-__device__ S2C_XFIX_ATTR void x_fix(const uint2 *bql, gptr_u32 xl, uint32_t xd, uint32_t q, uint32_t l, uint32_t r0, bool drop,
+__device__ __forceinline__ void x_fix_body(const uint2 *bql, gptr_u32 xl, uint32_t xd, uint32_t q, uint32_t l, uint32_t r0, bool drop,
                       uint32_t *hist) {
     const uint32_t v0 = q >> 5, v1 = (q + l - 1) >> 5;
     for (uint32_t vb = v0; vb <= v1; vb += 4) {   // four HBM words per round trip, then one at a time
@@ -848,12 +843,29 @@ __device__ S2C_XFIX_ATTR void x_fix(const uint2 *bql, gptr_u32 xl, uint32_t xd, 
         }
     }
 }
+// x_fix in line, or (OOL) out of line: the walk-queue instantiation of k_tile spills 416
+// bytes per lane with the rare non-ACGT scan in line (C2 0.075 -> 0.095 ms, profiles/r05/v9_*),
+// the other one runs 2-4 % slower with it out of line
+template <int NWP, bool OOL>
+__device__ __forceinline__ void x_fix(const uint2 *bql, gptr_u32 xl, uint32_t xd, uint32_t q, uint32_t l, uint32_t r0, bool drop,
+                                      uint32_t *hist);
+template <int NWP>
+__device__ __attribute__((noinline)) void x_fix_ool(const uint2 *bql, gptr_u32 xl, uint32_t xd, uint32_t q, uint32_t l, uint32_t r0,
+                                                     bool drop, uint32_t *hist) {
+    x_fix_body<NWP>(bql, xl, xd, q, l, r0, drop, hist);
+}
+template <int NWP, bool OOL>
+__device__ __forceinline__ void x_fix(const uint2 *bql, gptr_u32 xl, uint32_t xd, uint32_t q, uint32_t l, uint32_t r0, bool drop,
+                                      uint32_t *hist) {
+    if constexpr (OOL) x_fix_ool<NWP>(bql, xl, xd, q, l, r0, drop, hist);
+    else x_fix_body<NWP>(bql, xl, xd, q, l, r0, drop, hist);
+}
 
 // One piece of a chunk (record P, op words [P.z, oend) in LDS at opl[j + od], its SEQ[0] at
 // LDS plane base 16·P.y + qadj): parsecigar (:64-81) + maxdel (:210) → run records
 // runl[j + rd] (bases: rec_enc records; others zero); coverage / counted '-' of the
 // tile part into dV / dD; N / '-' of SEQ via x_fix.  Everything from LDS.
-template <int NWP, bool PXL>
+template <int NWP, bool PXL, bool OOL>
 __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *opl, uint32_t od, uint2 *runl, uint32_t rd,
                                  const uint2 *bql, gptr_u32 xl, uint32_t xd, uint32_t qadj, bool maxdel_active,
                                  uint32_t maxdel, uint32_t a, uint32_t n, uint32_t *hist, int32_t *dV, int32_t *dD,
@@ -940,7 +952,7 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
                                 if (off != 0xFFFFu && off - so < len && p >= c0 && p < c1) Hist<NWP>::add1(hist, SL_N, p - a, 1u);
                             }
                         } else if (fl & S2C_PF_X) {
-                            x_fix<NWP>(bql, xl, xd, q + (c0 - gp), c1 - c0, c0 - a, drop, hist);
+                            x_fix<NWP, OOL>(bql, xl, xd, q + (c0 - gp), c1 - c0, c0 - a, drop, hist);
                         }
                     }
 #if S2C_MAXDEL_1P
@@ -1294,14 +1306,14 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
                             if (off != 0xFFFFu && p >= c0 && p < c1) H::add1(hist, SL_N, p - a, 1u);
                         }
                     } else if ((fl & S2C_PF_X) && !(fl & S2C_PF_XFEW)) {   // (without PXL: S2C_PF_XFEW after the walk)
-                        x_fix<NWP>(bql, xg, 0u, ql + (c0 - P.x), c1 - c0, c0 - a, false, hist);
+                        x_fix<NWP, WQ>(bql, xg, 0u, ql + (c0 - P.x), c1 - c0, c0 - a, false, hist);
                     }
 #endif
                 }
             } else if (fl & S2C_PF_LONG) {   // (its runs come through the tile long lists)
                 for (uint32_t j = P.z; j < oe[u]; j++) C.runl[j - O0] = make_uint2(0u, 0u);
             } else if constexpr (!WQ) {
-                walk_chunk_piece<NWP, PXL>(P, oe[u], opl, od, C.runl, 0u - O0, bql, xg, 0u, qadj, d.maxdel_active != 0,
+                walk_chunk_piece<NWP, PXL, WQ>(P, oe[u], opl, od, C.runl, 0u - O0, bql, xg, 0u, qadj, d.maxdel_active != 0,
                                            (uint32_t)d.maxdel, a, n, hist, dV, dD, pxr[u]);
             }
         }
@@ -1310,7 +1322,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
             for (uint32_t k = lane; k < nwq; k += 64) {
                 const uint32_t i = C.wq[k];
                 const uint32_t oend = i + 1 < NPc ? pcr[i + 1].z : O1;
-                walk_chunk_piece<NWP, PXL>(pcr[i], oend, opl, od, C.runl, 0u - O0, bql, xg, 0u, qadj, d.maxdel_active != 0,
+                walk_chunk_piece<NWP, PXL, WQ>(pcr[i], oend, opl, od, C.runl, 0u - O0, bql, xg, 0u, qadj, d.maxdel_active != 0,
                                            (uint32_t)d.maxdel, a, n, hist, dV, dD, PXL ? pxl[i] : 0xFFFFFFFFu);
             }
         }
