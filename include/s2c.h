@@ -292,7 +292,7 @@ typedef struct {
     int64_t n_dense;           /* dense tiles (k_tile_dense; k_tile when len(-f) != 1) */
     int64_t n_deep;            /* tiles voted by k_consensus (deep or general) */
     int64_t n_long;            /* long-list entries (tile, run slot of a long piece) */
-    int64_t n_rlist;           /* pieces k_reads walks */
+    int64_t n_rlist;           /* pieces k_reads walks (the counts-only modes) */
     int64_t kwin;              /* window: a short piece spans <= kwin + 1 words */
     int64_t tile_max;          /* max positions of any tile (<= 2048) */
     int64_t chunk;             /* candidate run slots per word per work item */
@@ -316,6 +316,12 @@ typedef struct {
                                   own words and its windows' lookback for s2c_batch_shard; the device
                                   copies (s2c_dev rs / ps / wtile) hold only those entries */
     int64_t n_walked;          /* (ABI 13) pieces walked op by op (neither S2C_PF_SIMPLE nor S2C_PF_LONG) */
+    int64_t walk_queue;        /* (ABI 13) 1: n_walked >= n_pieces / 32 and tile_max <= 1024 — k_tile queues
+                                  those pieces for its walk (a variant of the kernel) */
+    int64_t tile_events;       /* (ABI 13) 1 (with walk_queue; S2C_NO_TILE_EVENTS unset): k_tile records its
+                                  finish tiles' short-motif insertion events itself — s2c_reads leaves
+                                  them (rlist's run prefix n_rlist_run was cut for it) */
+    int64_t n_rlist_run;       /* (ABI 13) the first n_rlist_run of rlist: the pieces s2c_reads walks */
     int64_t plan_t0, plan_t1;  /* (ABI 13) the tiles with a window, layers and work items: [0, n_tiles), or
                                   for s2c_parser_snapshot_from(p, t_from) [t_from, the tile of the held
                                   reads' last position] — the others keep bounds and insertion capacities */
@@ -459,8 +465,10 @@ typedef struct {
     const uint32_t *dwin;      /* [n_dense][S2C_DWIN_WORDS] s2c_batch_arrays.dwin, filtered like dense */
     const uint32_t *lpx;       /* [n_lpieces] s2c_batch_arrays.lpx (ABI 11; required with n_layers > 0) */
     const uint32_t *dpc;       /* [n_dpc][S2C_DPC_WORDS] s2c_batch_arrays.dpc (ABI 12; required with n_dense > 0) */
-    int64_t   n_walked;           /* (ABI 13) the batch's info.n_walked: with at least 1/32 of the pieces
-                                     k_tile queues them for its walk (a variant of the kernel) */
+    int64_t   walk_queue;         /* (ABI 13) the batch's info.walk_queue (k_tile's variant) */
+    int64_t   tile_events;        /* (ABI 13) the batch's info.tile_events (who records the finish tiles'
+                                     events: must match the batch's rlist run prefix) */
+    int64_t   n_rlist_run;        /* (ABI 13) the batch's info.n_rlist_run: s2c_reads walks rlist[0, n_rlist_run) */
     int64_t   word_lo, word_hi;   /* (ABI 13) the batch's info.word_lo / word_hi: rs and ps point at entry
                                      word_lo of s2c_batch_arrays rs / ps ([word_lo, word_hi] copied),
                                      wtile at entry word_lo ([word_lo, word_hi) copied) */

@@ -58,7 +58,7 @@ class BatchInfo(C.Structure):
         "aligned_bases", "query_bases", "n_pieces", "n_ops", "n_tokens", "n_qwords", "n_words",
         "n_tiles", "n_items", "n_dense", "n_deep", "n_long", "n_rlist", "kwin", "tile_max", "chunk",
         "n_ins", "n_ins_bases", "n_bkt", "n_lng", "n_cols", "runs_max", "dense_lds", "n_layers", "n_lpieces", "n_lops",
-        "n_lqwords", "layers_dense", "layers_built", "n_dpc", "word_lo", "word_hi", "n_walked", "plan_t0", "plan_t1")]
+        "n_lqwords", "layers_dense", "layers_built", "n_dpc", "word_lo", "word_hi", "n_walked", "walk_queue", "tile_events", "n_rlist_run", "plan_t0", "plan_t1")]
 
 
 _P64 = C.POINTER(C.c_int64)
@@ -96,7 +96,7 @@ class Dev(C.Structure):
         ("runs", _VP), ("ibkt", _VP), ("ilong", _VP), ("ilong_n", _VP), ("counts", _VP),
         ("ins_cols", _VP), ("ins_chr", _VP), ("n_cols", C.c_int64),
         ("tile_stats", _VP), ("blk_len", _VP), ("out", _VP), ("out_cap", C.c_int64), ("layers_dense", C.c_int64),
-        ("px", _VP), ("layers_built", C.c_int64), ("dwin", _VP), ("lpx", _VP), ("dpc", _VP), ("n_walked", C.c_int64), ("word_lo", C.c_int64),
+        ("px", _VP), ("layers_built", C.c_int64), ("dwin", _VP), ("lpx", _VP), ("dpc", _VP), ("walk_queue", C.c_int64), ("tile_events", C.c_int64), ("n_rlist_run", C.c_int64), ("word_lo", C.c_int64),
         ("word_hi", C.c_int64)]
 
 

@@ -311,6 +311,7 @@ struct s2c_batch {
     std::vector<uint32_t> lpx;                        // [n_lpieces] px of the layered pieces
     bool layers = false;                               // built (s2c_batch_layers)
     u32buf kmin, kmax;   // host only: global key range of each piece's insertion events
+    std::vector<uint8_t> lmot;   // host only: the piece emits a motif > S2C_SHORT_MOTIF bases
     u32buf px;           // [pieces] the non-ACGT SEQ offsets of S2C_PF_XFEW pieces (s2c.h)
     std::vector<uint32_t> dwin;   // [dense][S2C_DWIN_WORDS] the dense items' windows (s2c.h)
     u32buf dpc;                   // [n_dpc][S2C_DPC_WORDS] compact piece records of the dense windows (s2c.h)
@@ -1389,8 +1390,20 @@ static bool dense_fits(const uint32_t *tw, int64_t K) {
 // PF_RUNS on the long pieces (the tile long lists read k_reads' run records of them; the
 // tile kernels walk every short piece of their windows themselves), and the list of pieces
 // k_reads walks (those, and the pieces emitting insertion events).
+// k_tile's walk-queue variant (s2c_batch_info walk_queue): at least 1/32 of the pieces walked
+// op by op, tiles of <= 1024 positions (the 2048-position instantiation has no LDS for it).
+// It also records its finish tiles' short-motif insertion events (LDS event list, s2c_tile.hip).
+static int64_t walk_queue_of(const s2c_batch_info &I) {
+    return I.n_walked > 0 && 32 * I.n_walked >= I.n_pieces && I.tile_max <= 1024 ? 1 : 0;
+}
+
+// The pieces k_reads walks (rlist): first the ones s2c_run needs (n_rlist_run) — long pieces
+// listed by non-dense tiles (k_reads writes their run records) and insertion pieces with an
+// event k_tile does not record: a motif > S2C_SHORT_MOTIF bases, a long piece, or a key in a
+// tile that is not a finish tile (deep / general: k_consensus votes it) or whose window does
+// not hold the piece — then the other insertion pieces (the counts-only modes hash every event).
 static void mark_runs(s2c_batch *b) {
-    const int64_t NP = b->info.n_pieces;
+    const int64_t NP = b->info.n_pieces, K = b->info.kwin;
     std::vector<uint8_t> need(NP, 0);
     // long pieces listed by run slot (k_tile's tiles: k_reads writes their runs); a dense
     // tile lists its long pieces themselves (k_tile_dense walks them)
@@ -1407,18 +1420,40 @@ static void mark_runs(s2c_batch *b) {
             need[lo] = 1;
         }
     }
+    b->info.walk_queue = walk_queue_of(b->info);
+    static const bool no_tile_events = getenv("S2C_NO_TILE_EVENTS") != nullptr;   // (A/B: k_reads hashes every event)
+    b->info.tile_events = b->info.walk_queue && !no_tile_events ? 1 : 0;
+    const bool rec = b->info.tile_events != 0;
+    auto tile_takes_events = [&](int64_t k) {   // every event of insertion piece k recorded by k_tile
+        const uint32_t fl = b->pc[4 * k + 3] >> 24;
+        if (!rec || (fl & S2C_PF_LONG) || ((size_t)k < b->lmot.size() && b->lmot[k]) || b->kmin[k] == 0xFFFFFFFFu) return false;
+        const uint32_t t0 = b->wtile[b->kmin[k] >> 5], t1 = b->wtile[b->kmax[k] >> 5];
+        if (t0 == 0xFFFFFFFFu || t1 == 0xFFFFFFFFu) return false;
+        const int64_t ws = (int64_t)(b->pc[4 * k] >> 5);
+        for (uint32_t t = t0; t <= t1; t++) {
+            const uint32_t *tw = &b->tiles[(size_t)t * S2C_TILE_WORDS];
+            const int64_t W0 = tw[0] >> 5, W1 = (tw[1] + 31) >> 5;
+            if ((tw[3] & (S2C_TILE_DEEP | S2C_TILE_GENERAL | S2C_TILE_DENSE)) || ws < std::max<int64_t>(W0 - K, 0) || ws >= W1)
+                return false;
+        }
+        return true;
+    };
     b->rlist.clear();
     const int nt = plan_threads(NP, 1 << 18);
-    std::vector<std::vector<uint32_t>> rl(nt);
+    std::vector<std::vector<uint32_t>> rl(nt), rx(nt);
     par_ranges(nt, NP, [&](int t, int64_t k0, int64_t k1) {
         for (int64_t k = k0; k < k1; k++) {
             uint32_t &w3 = b->pc[4 * k + 3];
             if (need[k]) w3 |= (uint32_t)S2C_PF_RUNS << 24;
             else w3 &= ~((uint32_t)S2C_PF_RUNS << 24);
-            if (need[k] || ((w3 >> 24) & S2C_PF_INS)) rl[t].push_back((uint32_t)k);
+            const bool ins = ((w3 >> 24) & S2C_PF_INS) != 0;
+            if (need[k] || (ins && !tile_takes_events(k))) rl[t].push_back((uint32_t)k);
+            else if (ins) rx[t].push_back((uint32_t)k);
         }
     });
     for (int t = 0; t < nt; t++) b->rlist.insert(b->rlist.end(), rl[t].begin(), rl[t].end());
+    b->info.n_rlist_run = (int64_t)b->rlist.size();
+    for (int t = 0; t < nt; t++) b->rlist.insert(b->rlist.end(), rx[t].begin(), rx[t].end());
     b->info.n_rlist = (int64_t)b->rlist.size();
     if (b->rlist.empty()) b->rlist.push_back(0);
 }
@@ -2520,6 +2555,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     b->pc.resize(4 * (size_t)(NP + 1));
     b->kmin.resize(NP);
     b->kmax.resize(NP);
+    b->lmot.resize(NP);
     b->px.resize(std::max<int64_t>(NP, 1));
     b->ops.resize(std::max<uint64_t>(NOPS, 1));
     b->bq.resize(2 * (size_t)I.n_qwords);
@@ -2550,10 +2586,13 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
                 if (q.range) { fl |= S2C_PF_RANGE; *o++ = (uint32_t)q.ka; *o++ = (uint32_t)q.kb; }
                 b->kmin[k] = 0xFFFFFFFFu;
                 b->kmax[k] = 0u;
+                b->lmot[k] = 0;
                 if (q.ins) {
                     fl |= S2C_PF_INS;
                     b->kmin[k] = q.kmin;
                     b->kmax[k] = q.kmax;
+                    for (uint32_t e = r.ev0; e < r.ev0 + r.nev; e++)
+                        if (c.ev[e].key >= 0 && c.ev[e].len > S2C_SHORT_MOTIF) b->lmot[k] = 1;
                     const int64_t off = b->ref_off[r.ref], key0 = off + r.pos0;
                     *o++ = (uint32_t)(uint64_t)key0;
                     *o++ = (uint32_t)((uint64_t)key0 >> 32);
@@ -3023,6 +3062,7 @@ static int s2c_batch_shard_impl(const s2c_batch *b, int64_t t0, int64_t t1, s2c_
     s->bx.assign((size_t)J.n_qwords, 0u);
     s->kmin.assign(NS, 0xFFFFFFFFu);
     s->kmax.assign(NS, 0u);
+    s->lmot.assign(NS, 0);
     s->px.assign(std::max<int64_t>(NS, 1), 0xFFFFFFFFu);
     std::unordered_map<uint32_t, uint32_t> slot_new, piece_new;   // old op slot / long piece → new
     {
@@ -3043,6 +3083,7 @@ static int s2c_batch_shard_impl(const s2c_batch *b, int64_t t0, int64_t t1, s2c_
             }
             s->kmin[i] = b->kmin[k];
             s->kmax[i] = b->kmax[k];
+            s->lmot[i] = b->lmot[k];
             s->px[i] = b->px[k];
             const uint32_t slen = b->pc[4 * k + 3] & 0xFFFFFFu;
             for (uint64_t h = 0; h < (slen + 15) / 16; h++) {
@@ -3128,6 +3169,11 @@ static int s2c_batch_shard_impl(const s2c_batch *b, int64_t t0, int64_t t1, s2c_
     J.n_layers = J.n_lpieces = J.n_lops = J.n_lqwords = 0;
     J.layers_dense = J.layers_built = 0;
     for (int64_t t = 0; t < NT; t++) s->tiles[(size_t)t * S2C_TILE_WORDS + 20] = S2C_LY_NONE;
+    {   // the shard's own pieces walked op by op (its k_tile variant: walk_queue_of, mark_runs)
+        int64_t nw = 0;
+        for (int64_t i = 0; i < NS; i++) nw += !((s->pc[4 * i + 3] >> 24) & (S2C_PF_SIMPLE | S2C_PF_LONG));
+        J.n_walked = nw;
+    }
     mark_runs(s.get());
     build_dwin(s.get());
     // the shard's share of the workload's aligned bases (by its positions; for reporting)

@@ -29,6 +29,7 @@ struct ReadsArgs {
     uint32_t *runs, *ibkt, *ilong, *ilong_n;
     uint32_t n, maxdel_active, maxdel, all;   // all: every piece (else the pieces of rlist)
     uint32_t word_lo, word_hi;                // wtile holds words [word_lo, word_hi) (s2c_dev, ABI 13)
+    uint32_t skip_fin, kwin;                  // s2c_reads: events k_tile records are left to it (below)
 };
 
 struct GlobalMem {   // walk_piece's view of the batch in HBM
@@ -57,8 +58,11 @@ __device__ __forceinline__ uint64_t mix64(uint64_t k) {
     return k;
 }
 
-// One insertion event (global key gkey, motif = query bases [q, q + len)) into its tile.
-__device__ void add_event(const ReadsArgs &d, uint64_t gkey, uint64_t q, uint32_t len) {
+// One insertion event (global key gkey, motif = query bases [q, q + len)) of the piece starting
+// in word ws into its tile.  With skip_fin (s2c_reads, k_tile recording events: the launch's
+// walk_queue) a short motif keyed in a finish tile whose window holds the piece is left
+// to that tile's k_tile walk (s2c_tile.hip, the LDS event list): exactly the events it records.
+__device__ void add_event(const ReadsArgs &d, uint64_t gkey, uint64_t q, uint32_t len, uint32_t ws, bool lng) {
 #if S2C_EV_FAST
     // a short motif's codes from its (at most two) plane words, loaded with the tile lookup
     uint64_t c01[3] = {0, 0, 0};   // p0, p1, x of bases q .. q + 63
@@ -78,6 +82,10 @@ __device__ void add_event(const ReadsArgs &d, uint64_t gkey, uint64_t q, uint32_
     if (t == 0xFFFFFFFFu) return;   // keyed outside this batch's tiles (padding, another shard's tile)
     const uint4 tw0 = ((const uint4 *)d.tiles)[(size_t)t * (S2C_TILE_WORDS / 4)];
     const uint4 tw1 = ((const uint4 *)d.tiles)[(size_t)t * (S2C_TILE_WORDS / 4) + 1];
+    if (d.skip_fin && len <= S2C_SHORT_MOTIF && !lng && !(tw0.w & (S2C_TILE_DEEP | S2C_TILE_GENERAL | S2C_TILE_DENSE))) {
+        const uint32_t W0 = tw0.x >> 5, W1 = (tw0.y + 31) >> 5;
+        if (ws + d.kwin >= W0 && ws < W1) return;   // (the window [max(W0 - kwin, 0), W1) holds the piece)
+    }
     const uint32_t pos = (uint32_t)(gkey - tw0.x);   // tile-relative (< 2048)
     if (len <= S2C_SHORT_MOTIF) {
         uint64_t key = (uint64_t)pos | ((uint64_t)len << 11);
@@ -140,7 +148,7 @@ __device__ __forceinline__ bool piece_events(const ReadsArgs &d, const uint4 P, 
         } else if (op_dash(op)) {
             k += l;
         } else if (op == S2C_OP_I) {
-            if (take && key0 + k >= (int64_t)roff) add_event(d, (uint64_t)(key0 + k), q0 + start, take);
+            if (take && key0 + k >= (int64_t)roff) add_event(d, (uint64_t)(key0 + k), q0 + start, take, P.x >> 5, false);
             start += l;
         } else if (op == S2C_OP_S) {
             start += l;
@@ -164,16 +172,21 @@ __global__ __launch_bounds__(WG) void k_reads(const ReadsArgs d) {
                [&](uint32_t j, uint32_t g, uint32_t l, uint32_t k, uint64_t q) {
                    if (runs) out[j] = make_uint4(g, l | (k << S2C_RUN_KSHIFT), (uint32_t)q, (uint32_t)(q >> 32));
                },
-               [&](uint64_t gkey, uint64_t q, uint32_t len) { add_event(d, gkey, q, len); });
+               [&](uint64_t gkey, uint64_t q, uint32_t len) {
+                   add_event(d, gkey, q, len, P.x >> 5, ((P.w >> 24) & S2C_PF_LONG) != 0);
+               });
 }
 
 }  // namespace
 }  // namespace s2c
 
 // Launcher (called by s2c_reads in s2c_tile.hip): the pieces of rlist, or all of them
-int s2c_launch_reads(const s2c_dev *dv, hipStream_t st, bool all) {
+// all: every piece (s2c_pileup_counts); run: s2c_reads (rlist's run prefix, the events k_tile
+// records skipped); neither: all of rlist (s2c_accumulate)
+int s2c_launch_reads(const s2c_dev *dv, hipStream_t st, bool all, bool run) {
     using namespace s2c;
-    const int64_t n = all ? dv->n_pieces : dv->n_rlist;
+    const bool rec = run && dv->walk_queue && dv->tile_events;   // (k_tile records its finish tiles' short-motif events)
+    const int64_t n = all ? dv->n_pieces : rec ? dv->n_rlist_run : dv->n_rlist;
     if (n == 0) return S2C_OK;
     ReadsArgs a;
     a.pc = dv->pc; a.ops = dv->ops; a.bq = dv->bq; a.bx = dv->bx; a.tiles = dv->tiles; a.wtile = dv->wtile;
@@ -185,6 +198,8 @@ int s2c_launch_reads(const s2c_dev *dv, hipStream_t st, bool all) {
     a.all = all ? 1u : 0u;
     a.word_lo = (uint32_t)dv->word_lo;
     a.word_hi = (uint32_t)dv->word_hi;
+    a.skip_fin = rec ? 1u : 0u;
+    a.kwin = (uint32_t)dv->kwin;
     k_reads<<<(unsigned)((n + WG - 1) / WG), WG, 0, st>>>(a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? S2C_OK : s2c_set_error(S2C_ERR_HIP, std::string("k_reads: ") + hipGetErrorString(e));

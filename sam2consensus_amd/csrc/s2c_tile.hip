@@ -25,7 +25,7 @@
 
 #include "s2c_common.h"
 
-int s2c_launch_reads(const s2c_dev *d, hipStream_t s, bool all);
+int s2c_launch_reads(const s2c_dev *d, hipStream_t s, bool all, bool run);
 int s2c_launch_dense(const s2c_dev *d, hipStream_t s);
 
 #ifdef S2C_PROF
@@ -99,6 +99,8 @@ struct TileArgs {
     uint8_t *out;
     uint32_t padded_len, n_cols, n_tiles, kwin, chunk, n_qwords, runs_bytes, mode;   // MODE_* below
     uint32_t walk_queue;   // (host only: which k_tile instantiation)
+    uint32_t tile_events;  // finish tiles record their short-motif insertion events (EvRec)
+    uint32_t tables_empty; // MODE_RUN with tile_events and no piece for s2c_reads: no HBM table to read
     int32_t n_thr, min_depth, fill_len, fill_nondash;
 };
 
@@ -153,21 +155,29 @@ struct InsLayout {
     uint32_t nkeys, ncol;
 };
 template <uint32_t KCAP, bool HBMCOLS, class D>
-__device__ InsLayout build_layout(const D &d, const TileRec &T, uint32_t t, uint32_t *bits, uint32_t *wrank,
-                                  uint32_t *klen, uint4 *key, uint32_t *cols, uint16_t *colkey, uint32_t *scan) {
+__device__ __forceinline__ InsLayout build_layout(   // (in line: an out-of-line call copies the kernel arguments to scratch)
+    const D &d, const TileRec &T, uint32_t t, uint32_t *bits, uint32_t *wrank,
+                                  uint32_t *klen, uint4 *key, uint32_t *cols, uint16_t *colkey, uint32_t *scan,
+                                  const uint2 *evl = nullptr, uint32_t nevl = 0, bool tables = true) {
+    // tables = false: k_reads hashed nothing this run (s2c_reads launched no piece): the tile's
+    // HBM table and long-event list are empty, the LDS event list is everything
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t nwords = (T.b - T.a + 31) / 32;
-    const uint32_t nlong = uni(d.ilong_n[t]);
+    const uint32_t nlong = tables ? uni(d.ilong_n[t]) : 0u, bcap = tables ? T.bcap : 0u;
     const uint4 *bk = (const uint4 *)d.ibkt + T.boff;
     const uint4 *lg = (const uint4 *)d.ilong + T.loff;
     // (1) key bitmap
-    for (uint32_t e = tid; e < T.bcap; e += WG) {
+    for (uint32_t e = tid; e < bcap; e += WG) {
         const uint4 v = bk[e];
         if (v.x | v.y) atomicOr(&bits[(v.x & 0x7FFu) >> 5], 1u << (v.x & 31u));
     }
     for (uint32_t e = tid; e < nlong; e += WG) {
         const uint32_t pos = lg[e].x;
         atomicOr(&bits[pos >> 5], 1u << (pos & 31u));
+    }
+    for (uint32_t e = tid; e < nevl; e += WG) {   // (the events k_tile recorded: count 1 each)
+        const uint32_t x = evl[e].x;
+        atomicOr(&bits[(x & 0x7FFu) >> 5], 1u << (x & 31u));
     }
     lds_sync();
     // (2) keys before each word
@@ -188,7 +198,7 @@ __device__ InsLayout build_layout(const D &d, const TileRec &T, uint32_t t, uint
         return wrank[pos >> 5] + (uint32_t)__popc(bits[pos >> 5] & ((1u << (pos & 31u)) - 1u));
     };
     // (3) longest motif per key
-    for (uint32_t e = tid; e < T.bcap; e += WG) {
+    for (uint32_t e = tid; e < bcap; e += WG) {
         const uint4 v = bk[e];
         if (v.x | v.y) {
             const uint32_t pos = v.x & 0x7FFu, k = rank(pos);
@@ -201,6 +211,11 @@ __device__ InsLayout build_layout(const D &d, const TileRec &T, uint32_t t, uint
         const uint32_t k = rank(v.x);
         atomicMax(&klen[k], v.y);
         key[k].x = T.a + v.x;
+    }
+    for (uint32_t e = tid; e < nevl; e += WG) {
+        const uint32_t x = evl[e].x, pos = x & 0x7FFu, k = rank(pos);
+        atomicMax(&klen[k], (x >> 11) & 31u);
+        key[k].x = T.a + pos;
     }
     lds_sync();
     // (4) column bases: exclusive scan of klen over keys (chunks of WG keys)
@@ -231,7 +246,7 @@ __device__ InsLayout build_layout(const D &d, const TileRec &T, uint32_t t, uint
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-    for (uint32_t e = tid; e < T.bcap; e += WG) {
+    for (uint32_t e = tid; e < bcap; e += WG) {
         const uint4 v = bk[e];
         if (v.x | v.y) {
             const uint32_t pos = v.x & 0x7FFu, len = (v.x >> 11) & 31u, k = rank(pos);
@@ -247,15 +262,22 @@ __device__ InsLayout build_layout(const D &d, const TileRec &T, uint32_t t, uint
         uint32_t *cc = cols + (size_t)key[k].y * NSYM;
         for (uint32_t c = 0; c < v.y; c++) atomicAdd(&cc[c * NSYM + base_code(d.bq, d.bx, q + c)], 1u);
     }
+    for (uint32_t e = tid; e < nevl; e += WG) {
+        const uint2 v = evl[e];
+        const uint32_t pos = v.x & 0x7FFu, len = (v.x >> 11) & 31u, k = rank(pos);
+        const uint64_t m = ((uint64_t)v.x | ((uint64_t)v.y << 32)) >> 16;
+        uint32_t *cc = cols + (size_t)key[k].y * NSYM;
+        for (uint32_t c = 0; c < len; c++) atomicAdd(&cc[c * NSYM + ((m >> (3 * c)) & 7u)], 1u);
+    }
     // (6) leave the table zero for the next run
-    for (uint32_t e = tid; e < T.bcap; e += WG) ((uint4 *)d.ibkt)[T.boff + e] = make_uint4(0, 0, 0, 0);
+    for (uint32_t e = tid; e < bcap; e += WG) ((uint4 *)d.ibkt)[T.boff + e] = make_uint4(0, 0, 0, 0);
     if constexpr (HBMCOLS) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // atomics done before the readers
         __syncthreads();
     } else {
         lds_sync();
     }
-    if (tid == 0) d.ilong_n[t] = 0;
+    if (tid == 0 && tables) d.ilong_n[t] = 0;
     return {nkeys, ncol};
 }
 
@@ -711,7 +733,7 @@ template <> struct ChunkExt<true> {
 };
 template <bool EXT>
 struct ChunkLds : ChunkExt<EXT> {
-    uint32_t segR[CSEG + 1];
+    uint16_t segR[CSEG + 1];   // (u16: record offsets < S2C_CHUNK_RECS + RPAD; the LDS of 3 workgroups per CU)
     alignas(16) uint8_t pl[16 + S2C_CHUNK_QBYTES + 16];
     alignas(16) uint4 pcb[S2C_CHUNK_PIECES];
     alignas(16) uint8_t ol[S2C_CHUNK_OBYTES + 16];
@@ -865,11 +887,54 @@ __device__ __forceinline__ void x_fix(const uint2 *bql, gptr_u32 xl, uint32_t xd
 // LDS plane base 16·P.y + qadj): parsecigar (:64-81) + maxdel (:210) → run records
 // runl[j + rd] (bases: rec_enc records; others zero); coverage / counted '-' of the
 // tile part into dV / dD; N / '-' of SEQ via x_fix.  Everything from LDS.
-template <int NWP, bool PXL, bool OOL>
+// A finish tile's LDS event list (k_tile records the short-motif insertion events of its
+// window's pieces keyed inside it; s2c_reads leaves exactly those to it, s2c_reads.hip
+// add_event): key = tile position | length << 11 | 3-bit codes << 16 (k_reads' table key).
+// The walking lane keeps up to two events of its piece in registers (EvOut: LDS plane base,
+// position | length << 11 | non-ACGT << 16) and keys them once the layer's planes have landed
+// (k_tile, after the planes wait), so the walk never waits for the planes; a third event of
+// one piece flushes the first two with a wait of its own.
+struct EvRec {
+    uint2 *l;
+    uint32_t *n;
+    bool on;
+};
+struct EvOut {
+    uint32_t n, q0, t0, q1, t1;
+};
+
+// One event's key: motif = LDS plane bases [q, q + take) (take <= 16), at tile position pos
+__device__ __forceinline__ uint64_t ev_key(const uint2 *bql, gptr_u32 xl, uint32_t xd, uint32_t q, uint32_t take,
+                                           uint32_t pos, bool x) {
+    const uint32_t v = q >> 5, sh = q & 31u;
+    const uint64_t p0 = (uint64_t)bql[v].x | ((uint64_t)bql[v + 1].x << 32);
+    const uint64_t p1 = (uint64_t)bql[v].y | ((uint64_t)bql[v + 1].y << 32);
+    const uint64_t px = x ? ((uint64_t)xl[v + xd] | ((uint64_t)xl[v + 1 + xd] << 32)) : 0ull;
+    uint64_t key = (uint64_t)pos | ((uint64_t)take << 11);
+    for (uint32_t c = 0; c < take; c++) {
+        const uint32_t b0 = (uint32_t)(p0 >> (sh + c)) & 1u, b1 = (uint32_t)(p1 >> (sh + c)) & 1u;
+        const uint32_t code = ((px >> (sh + c)) & 1u) ? (b0 ? 0u : 4u) : ((b1 << 1 | b0) == 3u ? 5u : (b1 << 1 | b0) + 1u);
+        key |= (uint64_t)code << (16 + 3 * c);
+    }
+    return key;
+}
+__device__ __forceinline__ void ev_append(const uint2 *bql, gptr_u32 xl, uint32_t xd, uint32_t q, uint32_t t, const EvRec &ev) {
+    const uint64_t k = ev_key(bql, xl, xd, q, (t >> 11) & 31u, t & 0x7FFu, (t >> 16) != 0);
+    const uint32_t i = atomicAdd(ev.n, 1u);
+    if (i < S2C_EPI_KEYS) ev.l[i] = make_uint2((uint32_t)k, (uint32_t)(k >> 32));
+}
+// the lane's held events keyed (the planes have landed)
+__device__ __forceinline__ void ev_flush(const uint2 *bql, gptr_u32 xl, uint32_t xd, EvOut &eo, const EvRec &ev) {
+    if (eo.n > 0) ev_append(bql, xl, xd, eo.q0, eo.t0, ev);
+    if (eo.n > 1) ev_append(bql, xl, xd, eo.q1, eo.t1, ev);
+    eo.n = 0;
+}
+
+template <int NWP, bool PXL, bool OOL, bool REC>
 __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *opl, uint32_t od, uint2 *runl, uint32_t rd,
                                  const uint2 *bql, gptr_u32 xl, uint32_t xd, uint32_t qadj, bool maxdel_active,
                                  uint32_t maxdel, uint32_t a, uint32_t n, uint32_t *hist, int32_t *dV, int32_t *dD,
-                                 uint32_t pxw = 0xFFFFFFFFu) {
+                                 uint32_t pxw, const EvRec &ev, EvOut &eo) {
     const uint32_t fl = P.w >> 24, slen = P.w & 0xFFFFFFu;
     uint32_t j = P.z;
     if (fl & S2C_PF_LONG) {   // (its runs come through the tile long lists)
@@ -883,7 +948,14 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
         runl[j + rd] = runl[j + 1 + rd] = make_uint2(0u, 0u);
         j += 2;
     }
-    if (fl & S2C_PF_INS) {   // (its events: k_reads)
+    int64_t key0 = 0;   // (:74 start_ref = POS-1 + the seqout index; events before the ref start dropped)
+    uint32_t roff = 0;
+    const bool rec = REC && ev.on && (fl & S2C_PF_INS);
+    if (fl & S2C_PF_INS) {   // (its events: the finish tiles' own, else k_reads)
+        if (rec) {
+            key0 = (int64_t)((uint64_t)opl[j + od] | ((uint64_t)opl[j + 1 + od] << 32));
+            roff = opl[j + 2 + od];
+        }
         runl[j + rd] = runl[j + 1 + rd] = runl[j + 2 + rd] = make_uint2(0u, 0u);
         j += 3;
     }
@@ -972,6 +1044,20 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
 #if S2C_MAXDEL_1P
         if (op_dash(op)) dsum += l;
 #endif
+        if (REC && rec && op == S2C_OP_I) {   // an insertion event (:73-75) keyed in the tile, motif <= 16 bases
+            const uint32_t take = start < slen ? min(l, slen - start) : 0u;
+            const int64_t gk = key0 + (int64_t)kk;
+            if (take && take <= S2C_SHORT_MOTIF && gk >= (int64_t)roff && gk >= (int64_t)a && gk < (int64_t)e_tile)
+            {
+                if (eo.n == 2) {   // (rare: a third event of the piece) the planes now
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    ev_flush(bql, xl, xd, eo, ev);
+                }
+                const uint32_t tq = (uint32_t)(gk - (int64_t)a) | take << 11 | ((fl & S2C_PF_X) ? 1u << 16 : 0u);
+                if (eo.n == 0) { eo.q0 = ql + start; eo.t0 = tq; } else { eo.q1 = ql + start; eo.t1 = tq; }
+                eo.n++;
+            }
+        }
         if (bases || op == S2C_OP_I || op == S2C_OP_S) start += l;
         runl[jj + rd] = r;
     }
@@ -1024,6 +1110,11 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     // queue's code costs C3 / C4 4 % (profiles/r05/v9_*), so it is a separate instantiation
     constexpr bool PXL = S2C_PX_LDS && NWP <= 32, WQ = S2C_WALK_QUEUE && WQB && NWP <= 32;   // (ChunkLds' EXT)
     __shared__ __attribute__((aligned(16))) TileLds<ICOL, PXL || WQ> U;
+    // a finish tile's own short-motif insertion events (EvRec; the 2048-position instantiation
+    // leaves them to k_reads: its LDS)
+    constexpr bool REC = WQB && NWP <= 32;   // (the walk-queue instantiation's LDS has room for the list)
+    __shared__ uint2 evl[REC ? S2C_EPI_KEYS : 1];
+    __shared__ uint32_t evn;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
 #ifdef S2C_PROF
     const uint32_t tabl = uni(*(volatile uint32_t *)&g_tabl);
@@ -1058,6 +1149,13 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
         dV[i] = 0;
         dD[i] = 0;
     }
+    const bool rec_ev = REC && d.tile_events && finish && T.nev > 0;   // (s2c_reads.hip add_event leaves these to the walk)
+    EvRec evr;
+    evr.l = evl;
+    evr.n = &evn;
+    evr.on = rec_ev;
+    if (tid == 0) evn = 0;
+
     if (counts_only && d.mode != MODE_ADD_KEEP && T.nev > 0 && chunk == 0) {   // no vote: leave the tile's tables zero for the next run
         for (uint32_t e = tid; e < T.bcap; e += WG) ((uint4 *)d.ibkt)[T.boff + e] = make_uint4(0, 0, 0, 0);
         if (tid == 0) d.ilong_n[tile] = 0;
@@ -1240,6 +1338,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
         uint4 Pw[2];
         uint32_t oe[2];
         bool planes = false;   // a piece of the lane reads the planes in its walk
+        EvOut eo;              // (REC: the lane's insertion events, keyed after the planes wait)
+        eo.n = 0;
 #pragma unroll
         for (int u = 0; u < 2; u++) {
             const uint32_t i = lane + 64 * u;
@@ -1251,11 +1351,12 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
                 oe[u] = i + 1 < NPc ? pcr[i + 1].z : O1;
                 const int32_t sw = (int32_t)(Pw[u].x >> 5) - (int32_t)S0;
                 const int32_t pw = i > 0 ? (int32_t)(pcr[i - 1].x >> 5) - (int32_t)S0 : -1;
-                for (int32_t sg = pw + 1; sg <= sw; sg++) C.segR[sg] = Pw[u].z - O0;
+                for (int32_t sg = pw + 1; sg <= sw; sg++) C.segR[sg] = (uint16_t)(Pw[u].z - O0);
                 if (i + 1 == NPc)
-                    for (uint32_t sg = (uint32_t)(sw + 1); sg <= NS; sg++) C.segR[sg] = NR;
+                    for (uint32_t sg = (uint32_t)(sw + 1); sg <= NS; sg++) C.segR[sg] = (uint16_t)NR;
                 const uint32_t f = Pw[u].w >> 24;
-                if constexpr (PXL)   // (x_fix and the maxdel '-' count read the planes; S2C_PF_XFEW pieces take px)
+                if constexpr (PXL)   // (x_fix and the maxdel '-' count read the planes; S2C_PF_XFEW pieces take px;
+                                     //  recorded events are keyed after the walk)
                     planes |= (f & S2C_PF_X) && !(f & (S2C_PF_XFEW | S2C_PF_LONG));
                 else
                     planes |= (f & S2C_PF_SIMPLE) ? ((f & S2C_PF_X) && !(f & S2C_PF_XFEW)) : !(f & S2C_PF_LONG);
@@ -1313,8 +1414,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
             } else if (fl & S2C_PF_LONG) {   // (its runs come through the tile long lists)
                 for (uint32_t j = P.z; j < oe[u]; j++) C.runl[j - O0] = make_uint2(0u, 0u);
             } else if constexpr (!WQ) {
-                walk_chunk_piece<NWP, PXL, WQ>(P, oe[u], opl, od, C.runl, 0u - O0, bql, xg, 0u, qadj, d.maxdel_active != 0,
-                                           (uint32_t)d.maxdel, a, n, hist, dV, dD, pxr[u]);
+                walk_chunk_piece<NWP, PXL, WQ, REC>(P, oe[u], opl, od, C.runl, 0u - O0, bql, xg, 0u, qadj, d.maxdel_active != 0,
+                                               (uint32_t)d.maxdel, a, n, hist, dV, dD, pxr[u], evr, eo);
             }
         }
         if constexpr (WQ) {
@@ -1322,13 +1423,17 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
             for (uint32_t k = lane; k < nwq; k += 64) {
                 const uint32_t i = C.wq[k];
                 const uint32_t oend = i + 1 < NPc ? pcr[i + 1].z : O1;
-                walk_chunk_piece<NWP, PXL, WQ>(pcr[i], oend, opl, od, C.runl, 0u - O0, bql, xg, 0u, qadj, d.maxdel_active != 0,
-                                           (uint32_t)d.maxdel, a, n, hist, dV, dD, PXL ? pxl[i] : 0xFFFFFFFFu);
+                walk_chunk_piece<NWP, PXL, WQ, REC>(pcr[i], oend, opl, od, C.runl, 0u - O0, bql, xg, 0u, qadj, d.maxdel_active != 0,
+                                           (uint32_t)d.maxdel, a, n, hist, dV, dD, PXL ? pxl[i] : 0xFFFFFFFFu, evr, eo);
             }
         }
         wave_lds_sync();   // every run record written; the piece records and op words read
+        TPROF_MARK(9);     // (the walk's own work; MARK(3) below: the wait for the planes)
         // this layer's planes (and 'N' offsets) have landed from here on
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (REC) {   // the lane's held events keyed from the landed planes (EvOut)
+            if (eo.n) ev_flush(bql, xg, 0u, eo, evr);
+        }
 #if !defined(S2C_ABL_X)
 #pragma unroll
         for (int u = 0; u < 2 && !PXL; u++) {   // ≤ 2 'N' of an S2C_PF_XFEW piece at its SEQ offsets px: no plane scan
@@ -1544,7 +1649,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
         if (tid < (uint32_t)min(d.fill_len, FILL_LDS)) L.fill[tid] = d.fill[tid];
         lds_sync();
         InsLayout il = {0, 0};
-        if (has_ins) il = build_layout<PF, false>(d, T, tile, L.bits, L.wrank, L.klen, L.key, cols, L.colkey, L.scan);
+        if (has_ins)
+            il = build_layout<PF, false>(d, T, tile, L.bits, L.wrank, L.klen, L.key, cols, L.colkey, L.scan, evl,
+                                         rec_ev ? min(evn, (uint32_t)S2C_EPI_KEYS) : 0u, !(rec_ev && d.tables_empty));
         tile_epilogue_fast<NWP>(d, tile, T, il, hist, cols, L);
     } else {
         // deep tile: this item's counts → HBM (symbol-major, coalesced atomics); a general
@@ -1782,7 +1889,9 @@ TileArgs tile_args(const s2c_dev &d) {
     p.kwin = (uint32_t)d.kwin; p.chunk = (uint32_t)d.chunk; p.n_qwords = (uint32_t)d.n_qwords;
     p.runs_bytes = (uint32_t)std::min<int64_t>(16 * std::max<int64_t>(d.n_ops, 1), 0xFFFFFFF0ll);
     p.mode = MODE_RUN;
-    p.walk_queue = d.n_walked > 0 && 32 * d.n_walked >= d.n_pieces ? 1u : 0u;
+    p.walk_queue = d.walk_queue ? 1u : 0u;
+    p.tile_events = d.walk_queue && d.tile_events ? 1u : 0u;
+    p.tables_empty = p.tile_events && d.n_rlist_run == 0 ? 1u : 0u;
     p.n_thr = d.n_thr; p.min_depth = d.min_depth; p.fill_len = d.fill_len; p.fill_nondash = d.fill_nondash;
     return p;
 }
@@ -1874,7 +1983,7 @@ extern "C" int s2c_reads(const s2c_dev *d, void *stream) {
     if (rc) return rc;
     // the tile kernels walk their windows' pieces themselves: k_reads takes the insertion
     // emitters and the long pieces (rlist)
-    return s2c_launch_reads(d, (hipStream_t)stream, false);
+    return s2c_launch_reads(d, (hipStream_t)stream, false, true);
 }
 
 extern "C" int s2c_pileup(const s2c_dev *d, void *stream) {
@@ -1922,7 +2031,7 @@ extern "C" int s2c_pileup_counts(const s2c_dev *d, void *stream) {
     if (d->n_dense > 0 && !d->layers_dense)   // (k_tile takes the dense tiles here: their layers)
         return s2c_set_error(S2C_ERR_ARG, "counts-only modes need the dense tiles' layered windows (s2c_batch_layers_mode(b, 1))");
     hipStream_t s = (hipStream_t)stream;
-    if ((rc = s2c_launch_reads(d, s, true))) return rc;   // run records of every piece (compared by the tests)
+    if ((rc = s2c_launch_reads(d, s, true, false))) return rc;   // run records of every piece (compared by the tests)
     TileArgs a = tile_args(*d);
     a.mode = MODE_STORE;
     if (d->n_deep > 0) {
@@ -1940,7 +2049,7 @@ extern "C" int s2c_accumulate(const s2c_dev *d, int keep_tables, void *stream) {
     if (d->n_dense > 0 && !d->layers_dense)   // (k_tile takes the dense tiles here: their layers)
         return s2c_set_error(S2C_ERR_ARG, "counts-only modes need the dense tiles' layered windows (s2c_batch_layers_mode(b, 1))");
     hipStream_t s = (hipStream_t)stream;
-    if ((rc = s2c_launch_reads(d, s, false))) return rc;   // events hashed, long pieces' runs
+    if ((rc = s2c_launch_reads(d, s, false, false))) return rc;   // every event hashed, long pieces' runs
     TileArgs a = tile_args(*d);
     a.mode = keep_tables ? MODE_ADD_KEEP : MODE_ADD;
     if ((rc = launch_tiles(a, d->tile_max, d->dense, d->n_dense, s))) return rc;

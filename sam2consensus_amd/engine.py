@@ -256,7 +256,7 @@ class Workspace:
         d.n_layers, d.n_lpieces, d.n_lops, d.n_lqwords = i.n_layers, i.n_lpieces, i.n_lops, i.n_lqwords
         d.layers_dense, d.layers_built = i.layers_dense, i.layers_built
         d.word_lo, d.word_hi = i.word_lo, i.word_hi
-        d.n_walked = i.n_walked
+        d.walk_queue, d.tile_events, d.n_rlist_run = i.walk_queue, i.tile_events, i.n_rlist_run
         # the maxdel rule (:210) runs on the device: the parser's setting unless overridden
         if maxdel_active is None:
             maxdel_active = getattr(db.hb, "maxdel_active", True)

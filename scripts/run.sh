@@ -10,6 +10,7 @@
 #   bench:WL              bench line of workload WL (device step; no CPU legs)
 #   default               the default `python bench.py` (the driver's line, CPU legs included)
 #   ab:WL                 A/B of LIBS="libs2c.so libs2c_x.so ..." on WL, two alternating rounds
+#   abenv:WL              A/B of libs2c.so without / with the environment ENVB (e.g. "S2C_NO_TILE_EVENTS=1")
 #   prof:WL               rocprofv3 --kernel-trace --stats of WL's bench line
 #   profdefault           rocprofv3 --kernel-trace --stats of the default bench line
 #   pmc:WL                PMC passes of WL (scripts/pmc.sh)
@@ -55,6 +56,15 @@ for st in "$@"; do
           S2C_LIB=$lib timeout -k 10 300 python -u bench.py --workload $arg --steps 20 --warmup 3 $NB \
             > gpurun_out/${T}_${arg}_${lib}_$k.json 2> gpurun_out/${T}_${arg}_${lib}_$k.err || { tail -5 gpurun_out/${T}_${arg}_${lib}_$k.err; exit 1; }
           line gpurun_out/${T}_${arg}_${lib}_$k.json "$arg $lib $k"
+        done
+      done ;;
+    abenv)
+      for k in 1 2; do
+        for v in base env; do
+          E=""; [ $v = env ] && E="$ENVB"
+          env $E timeout -k 10 300 python -u bench.py --workload $arg --steps 20 --warmup 3 $NB \
+            > gpurun_out/${T}_${arg}_${v}_$k.json 2> gpurun_out/${T}_${arg}_${v}_$k.err || { tail -5 gpurun_out/${T}_${arg}_${v}_$k.err; exit 1; }
+          line gpurun_out/${T}_${arg}_${v}_$k.json "$arg $v $k"
         done
       done ;;
     prof)

@@ -49,8 +49,9 @@ def plane_codes(hb, q, n):
 CODE_SYM = np.array([1, 2, 3, 5, 4, 0, -1, -1], dtype=np.int64)   # plane code → "-ACGNT" index
 
 
-def model_reads(hb, maxdel_active=None, maxdel=None):
-    """k_reads: (runs [n_ops][4] u32, events [(gkey, (sym, ...))]) from the packed batch."""
+def model_reads(hb, maxdel_active=None, maxdel=None, with_piece=False):
+    """k_reads: (runs [n_ops][4] u32, events [(gkey, (sym, ...))]) from the packed batch
+    (with_piece: events [(gkey, (sym, ...), piece)])."""
     if maxdel_active is None:
         maxdel_active = getattr(hb, "maxdel_active", True)
     if maxdel is None:
@@ -110,7 +111,7 @@ def model_reads(hb, maxdel_active=None, maxdel=None):
                 take = max(0, min(ln, slen - start))
                 if fl & PF_INS and take and key0 + k >= roff:
                     syms = tuple(int(CODE_SYM[c]) for c in plane_codes(hb, q0 + start, take))
-                    events.append((key0 + k, syms))
+                    events.append((key0 + k, syms, i) if with_piece else (key0 + k, syms))
                 start += ln
             elif op == OP_S:
                 start += ln
@@ -232,6 +233,33 @@ def check_plan(hb):
                 by_slot.add(int(np.searchsorted(pc[:NP, 2], lp[e], side="right")) - 1)
     assert set(np.nonzero((fl & 16) != 0)[0].tolist()) == by_slot
     assert set(hb.rlist.tolist()) == set(np.nonzero(((fl & 16) != 0) | ((fl & PF_INS) != 0))[0].tolist())
+    # (ABI 13) rlist's run prefix: what s2c_reads walks when k_tile's walk-queue variant records
+    # its finish tiles' short-motif events itself (s2c_host.cpp mark_runs)
+    assert bool(i.walk_queue) == (i.n_walked > 0 and 32 * i.n_walked >= i.n_pieces and i.tile_max <= 1024)
+    wq = bool(i.tile_events)
+    assert wq <= bool(i.walk_queue)
+    assert i.n_walked == int((((fl & (PF_SIMPLE | PF_LONG)) == 0)).sum())
+    nrr = int(i.n_rlist_run)
+    rl = hb.rlist[: i.n_rlist].astype(np.int64)
+    ins = set(np.nonzero((fl & PF_INS) != 0)[0].tolist())
+    ev_keys = {}
+    for g, syms, k in model_reads(hb, with_piece=True)[1]:
+        ev_keys.setdefault(k, []).append((g, len(syms)))
+
+    def tile_takes(k):
+        if not wq or fl[k] & PF_LONG or k not in ev_keys or max(n for _, n in ev_keys[k]) > 16:
+            return False
+        g0, g1 = min(g for g, _ in ev_keys[k]), max(g for g, _ in ev_keys[k])
+        t0, t1 = int(hb.wtile[g0 >> 5]), int(hb.wtile[g1 >> 5])
+        ws = int(pc[k, 0]) >> 5
+        for t in range(t0, t1 + 1):
+            w0, w1 = int(T[t, 0]) >> 5, (int(T[t, 1]) + 31) >> 5
+            if T[t, 3] & 7 or ws < max(w0 - K, 0) or ws >= w1:
+                return False
+        return True
+    want = {k for k in range(NP) if fl[k] & 16} | {k for k in ins if not tile_takes(k)}
+    assert set(rl[:nrr].tolist()) == want and set(rl[nrr:].tolist()) == ins - want
+    assert len(set(rl.tolist())) == len(rl)
 
 
 CHUNK_PIECES, CHUNK_QBYTES, CHUNK_XBYTES, CHUNK_OBYTES, CHUNK_RECS = 128, 4096, 2048, 1024, 192   # include/s2c.h (per wave)

@@ -536,7 +536,7 @@ def _host_dev(hb, fill=b"-", counts=False):
     d.dense_lds, d.n_rlist = i.dense_lds, i.n_rlist
     d.layers_dense, d.layers_built = i.layers_dense, i.layers_built
     d.word_lo, d.word_hi = i.word_lo, i.word_hi
-    d.n_walked = i.n_walked
+    d.walk_queue, d.tile_events, d.n_rlist_run = i.walk_queue, i.tile_events, i.n_rlist_run
     d.maxdel_active, d.maxdel = 1, 150
     d.thresholds, d.n_thr, d.min_depth = p, 1, 1
     d.fill_len, d.fill_nondash, d.fill = len(fill), sum(c != ord("-") for c in fill), p
