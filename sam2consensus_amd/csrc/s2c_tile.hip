@@ -705,6 +705,7 @@ __device__ __forceinline__ void tile_epilogue_fast(const D &d, uint32_t tile, co
 #ifndef S2C_MAXDEL_1P
 #define S2C_MAXDEL_1P 1
 #endif
+
 constexpr int GS = 8;                 // records per counting group
 constexpr int CSEG = S2C_CHUNK_SEGS;  // segments of a window (≤ 64 words + kwin ≤ 32)
 constexpr uint32_t RPAD = 64;         // zero records after a chunk's last (a group's reads past it: ≤ 7·G ≤ 56)
@@ -1366,6 +1367,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
             for (uint32_t sg = lane; sg <= NS; sg += 64) C.segR[sg] = 0;
         if (__ballot(planes)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the planes, for those walks)
         for (uint32_t i = lane; i < RPAD; i += 64) C.runl[NR + i] = make_uint2(0u, 0u);
+        TPROF_MARK(10);    // (the records, segments and any planes wait of the walk)
         if (TABL(1))   // (ablated walk: zero records)
             for (uint32_t i = lane; i < NR; i += 64) C.runl[i] = make_uint2(0u, 0u);
         // (WQ) the pieces walked op by op go to a queue, walked after the others by the wave's
@@ -1418,6 +1420,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
                                                (uint32_t)d.maxdel, a, n, hist, dV, dD, pxr[u], evr, eo);
             }
         }
+        TPROF_MARK(11);    // (the one-token pieces; MARK(9) below: the op walks)
         if constexpr (WQ) {
             if (nwq) wave_lds_sync();   // (the queue)
             for (uint32_t k = lane; k < nwq; k += 64) {

@@ -44,8 +44,9 @@ f(buf, 0)
 print("k_reads %.4f ms  pileup %.4f ms  consensus %.4f ms" % (ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2]),
                                                             ev[2].elapsed_time(ev[3])))
 n = max(buf[15], 1)
-names = {0: "setup (zero LDS)", 1: "layer DMA + wait", 8: "walk (work)", 2: "walk: planes wait", 3: "count",
-         4: "long pieces + flush", 5: "reconstruct counts", 6: "epilogue / store"}
+names = {0: "setup (zero LDS)", 1: "layer DMA + wait", 9: "walk: records, segments", 10: "walk: one-token pieces",
+         8: "walk: op walks", 2: "walk: planes wait", 3: "count", 4: "long pieces + flush", 5: "reconstruct counts",
+         6: "epilogue / store"}
 tot = sum(buf[k] for k in names)
 for k, nm in names.items():
     print("  %-24s %9.0f cyc/wg  %5.1f%%" % (nm, buf[k] / n, 100.0 * buf[k] / max(tot, 1)))

@@ -17,6 +17,7 @@
 #   phases:WL             phase clocks of the dense kernel (libs2c_prof.so, scripts/prof_dense.py)
 #   tphases:WL            phase clocks of k_tile (libs2c_prof.so, scripts/prof_tile.py)
 #   rehearse:N            bench --rehearse-shards N (the one-GPU rehearsal of the N-way split)
+#   streamrss:WL          whole vs streamed CLI on WL's .sam (scripts/stream_rss.py: time, peak RSS, FASTA sha)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}" || exit 1
 mkdir -p gpurun_out; export TMPDIR=/tmp
@@ -87,6 +88,10 @@ for st in "$@"; do
     rehearse)
       timeout -k 10 600 python -u bench.py --rehearse-shards $arg > gpurun_out/${T}_rehearse_$arg.json 2> gpurun_out/${T}_rehearse_$arg.err \
         || { tail -5 gpurun_out/${T}_rehearse_$arg.err; exit 1; } ;;
+    streamrss)
+      timeout -k 10 900 python -u scripts/stream_rss.py $arg > gpurun_out/${T}_stream_rss_$arg.json 2> gpurun_out/${T}_stream_rss_$arg.err \
+        || { tail -5 gpurun_out/${T}_stream_rss_$arg.err; exit 1; }
+      python -c "import json,sys;d=json.load(open(sys.argv[1]));print({k:(d[k]['seconds'],d[k]['peak_rss_mb']) for k in ('whole','stream')}, d['identical'])" gpurun_out/${T}_stream_rss_$arg.json ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
