@@ -28,6 +28,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <string>
 #include <condition_variable>
@@ -58,6 +59,83 @@ int s2c_guarded(F &&f) {
     }
 }
 extern "C" int s2c_abi_version(void) { return S2C_ABI_VERSION; }
+
+// ------------------------------------------------------------------ host worker pools
+// Persistent host threads for the parse windows and the plan's parallel loops.  A thread
+// made per window (16 per 64 MB block of a streamed file) maps its stack while the other
+// threads first-touch their chunks' buffers; those page faults and the mapping serialise on
+// the process's memory map, and the last thread of a window started 25-35 ms after the
+// first (S2C_HOST_TIMING).  A pool's threads wait on a condition variable between runs.
+// One run at a time per pool: a run asked for while the pool is busy (another thread's run,
+// or a run nested in one) gets threads of its own, as before.  A forked child makes new pools.
+namespace {
+class WorkerPool {
+  public:
+    // f(t) for t in [0, nt): t = 0 on the calling thread, the others on the pool's
+    template <class F>
+    void run(int nt, F &&f) {
+        if (nt <= 1) { f(0); return; }
+        std::unique_lock<std::mutex> rl(run_m_, std::try_to_lock);
+        if (!rl.owns_lock()) {   // busy: threads of its own
+            std::vector<std::thread> th;
+            for (int t = 1; t < nt; t++) th.emplace_back([&f, t] { f(t); });
+            f(0);
+            for (auto &x : th) x.join();
+            return;
+        }
+        const std::function<void(int)> job = [&f](int t) { f(t); };
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            while ((int)n_threads_ < nt - 1) {
+                const int t = n_threads_ + 1;
+                std::thread([this, t] { loop(t); }).detach();
+                n_threads_++;
+            }
+            job_ = &job;
+            want_ = nt;
+            left_ = nt - 1;
+            gen_++;
+        }
+        go_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [&] { return left_ == 0; });
+        job_ = nullptr;
+    }
+    // the pool of this process (pools are never destroyed: their threads may outlive main)
+    static WorkerPool &get(int which) {
+        static std::mutex gm;
+        static WorkerPool *pools[2] = {nullptr, nullptr};
+        static pid_t owner = 0;
+        std::lock_guard<std::mutex> lk(gm);
+        if (owner != getpid()) { pools[0] = pools[1] = nullptr; owner = getpid(); }
+        if (!pools[which]) pools[which] = new WorkerPool();
+        return *pools[which];
+    }
+
+  private:
+    void loop(int t) {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(m_);
+        for (;;) {
+            go_.wait(lk, [&] { return gen_ != seen; });
+            seen = gen_;
+            if (t >= want_) continue;
+            const std::function<void(int)> *j = job_;
+            lk.unlock();
+            (*j)(t);
+            lk.lock();
+            if (--left_ == 0) done_.notify_one();
+        }
+    }
+    std::mutex run_m_, m_;
+    std::condition_variable go_, done_;
+    const std::function<void(int)> *job_ = nullptr;
+    uint64_t gen_ = 0;
+    int want_ = 0, left_ = 0, n_threads_ = 0;
+};
+enum { POOL_PARSE = 0, POOL_PLAN = 1 };
+}  // namespace
 
 // ------------------------------------------------------------------ tables
 namespace {
@@ -816,16 +894,20 @@ int parse_window(s2c_parser *p, const char *s, size_t n) {
     unsigned hw = std::thread::hardware_concurrency();
     int nt = (int)std::min<size_t>(std::min<unsigned>(hw ? hw : 1, 16), std::max<size_t>(1, body >> 22));   // ≥ 4 MB each
     if (const char *e = getenv("S2C_PARSE_THREADS")) nt = std::max(1, std::min(64, atoi(e)));
-    std::vector<size_t> cut(nt + 1, n);
+    // 4 pieces per thread (≥ 1 MB each), taken in turn by the threads: a thread slowed by
+    // the others' work (a streamed snapshot planning beside the feed) holds up the window by
+    // one piece, not by its fixed share
+    const int np = nt == 1 ? 1 : (int)std::min<size_t>((size_t)nt * 4, std::max<size_t>((size_t)nt, body >> 20));
+    std::vector<size_t> cut(np + 1, n);
     cut[0] = i;
-    for (int k = 1; k < nt; k++) {   // piece k starts after the line end nearest to its share
-        size_t c = std::max(cut[k - 1], i + body * k / nt);
+    for (int k = 1; k < np; k++) {   // piece k starts after the line end nearest to its share
+        size_t c = std::max(cut[k - 1], i + body * k / np);
         const char *nl = c < n ? (const char *)memchr(s + c, '\n', n - c) : nullptr;
         cut[k] = nl ? (size_t)(nl - s) + 1 : n;
     }
-    std::vector<std::unique_ptr<Chunk>> cs(nt);
-    std::vector<int> rcs(nt, S2C_OK);
-    std::vector<std::string> msgs(nt);
+    std::vector<std::unique_ptr<Chunk>> cs(np);
+    std::vector<int> rcs(np, S2C_OK);
+    std::vector<std::string> msgs(np);
     RefView rv{&p->ref_idx, &p->ref_len, p->maxdel_active, p->maxdel};
     auto work = [&](int k) {
         cs[k].reset(new Chunk());
@@ -849,14 +931,27 @@ int parse_window(s2c_parser *p, const char *s, size_t n) {
             j = e;
         }
     };
-    if (nt == 1) {
-        work(0);
-    } else {
-        std::vector<std::thread> th;
-        for (int k = 0; k < nt; k++) th.emplace_back(work, k);
-        for (auto &t : th) t.join();
+    static const bool timing = getenv("S2C_HOST_TIMING") != nullptr;
+    std::vector<double> tw(nt, 0.0);
+    const auto t0 = std::chrono::steady_clock::now();
+    std::atomic<int> next{0};
+    std::vector<double> ts(nt, 0.0);
+    auto worker = [&](int t) {
+        const auto a = std::chrono::steady_clock::now();
+        for (int k; (k = next++) < np;) work(k);
+        tw[t] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+        ts[t] = std::chrono::duration<double, std::milli>(a - t0).count();
+    };
+    WorkerPool::get(POOL_PARSE).run(nt, worker);
+    if (timing) {   // (S2C_HOST_TIMING: the window's wall time, its threads' longest and mean)
+        double mx = 0, sm = 0;
+        for (double x : tw) { mx = std::max(mx, x); sm += x; }
+        double smax = 0;
+        for (double x : ts) smax = std::max(smax, x);
+        fprintf(stderr, "[s2c feed] %zu B %d thr %d pieces wall %.2f ms max %.2f mean %.2f last start %.2f\n", n - i, nt, np,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), mx, sm / nt, smax);
     }
-    for (int k = 0; k < nt; k++) {
+    for (int k = 0; k < np; k++) {
         if (!cs[k]->reads.empty() || cs[k]->lines_total) p->chunks.push_back(std::move(cs[k]));
         if (rcs[k]) return perr(p, rcs[k], msgs[k]);
     }
@@ -1277,16 +1372,14 @@ static int plan_threads(int64_t n, int64_t grain) {
     unsigned hw = std::thread::hardware_concurrency();
     int nt = (int)std::min<unsigned>(hw ? hw : 1, 16);
     if (const char *e = getenv("S2C_PARSE_THREADS")) nt = std::max(1, std::min(64, atoi(e)));
+    if (const char *e = getenv("S2C_PLAN_THREADS")) nt = std::max(1, std::min(64, atoi(e)));   // (the plan's own)
     return (int)std::max<int64_t>(1, std::min<int64_t>(nt, n / std::max<int64_t>(grain, 1)));
 }
 // f(t, i0, i1) on nt contiguous ranges of [0, n), thread t on range t
 template <class F>
 static void par_ranges(int nt, int64_t n, F &&f) {
     if (nt <= 1) { f(0, (int64_t)0, n); return; }
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; t++) th.emplace_back([&f, t, nt, n] { f(t, n * t / nt, n * (t + 1) / nt); });
-    f(0, (int64_t)0, n / nt);
-    for (auto &x : th) x.join();
+    WorkerPool::get(POOL_PLAN).run(nt, [&f, nt, n](int t) { f(t, n * t / nt, n * (t + 1) / nt); });
 }
 }  // namespace
 

@@ -48,6 +48,18 @@ DEFAULT_BATCH = 256 << 20         # input bytes per streamed batch
 BLOCK = 64 << 20                  # bytes per feed call (a 64 MB block parses on 16 host threads, ≥ 4 MB each)
 
 
+def _env_bytes(name, default):
+    """<bytes>[K|M|G] from the environment variable ``name`` (unset or empty: ``default``)."""
+    v = os.environ.get(name, "").strip().upper()
+    if not v:
+        return default
+    mult = {"K": 1 << 10, "M": 1 << 20, "G": 1 << 30}.get(v[-1], 1)
+    return int(float(v.rstrip("KMG")) * mult)
+
+
+BLOCK = _env_bytes("S2C_STREAM_BLOCK", BLOCK)   # (measurement knob: the feed call's size)
+
+
 class NotSorted(Exception):
     """A read changes positions already emitted: the input is not coordinate-sorted."""
 
@@ -706,8 +718,4 @@ def consensus_files_streamed(filename, thresholds, prefix, min_depth=1, fill=b"-
 
 def stream_bytes_from_env():
     """S2C_STREAM=<bytes>[K|M|G] turns on streamed batches in the CLI (0 / unset: one batch)."""
-    v = os.environ.get("S2C_STREAM", "").strip().upper()
-    if not v:
-        return 0
-    mult = {"K": 1 << 10, "M": 1 << 20, "G": 1 << 30}.get(v[-1], 1)
-    return int(float(v.rstrip("KMG")) * mult)
+    return _env_bytes("S2C_STREAM", 0)

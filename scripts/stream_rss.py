@@ -30,6 +30,7 @@ def child(mode, path, name, batch_mb):
     if mode == "whole":
         r = consensus_files(path, *common)
     else:
+        batch_mb = int(os.environ.get("STREAM_BATCH_MB", batch_mb))
         r = consensus_files_streamed(path, *common, batch_bytes=batch_mb << 20)
     dt = time.perf_counter() - t0
     h = hashlib.sha256()
@@ -57,16 +58,26 @@ def main():
         res = {"config": name, "reads": n, "sam_bytes": size, "batch_mb": batch_mb}
         sys.stderr.write("wrote %d reads, %d bytes\n" % (n, size))
         sys.stderr.flush()
-        for mode in ("whole", "stream"):
+        # STREAM_VARIANTS="A=1,B=2;A=4": more streamed runs of the same file, each with those
+        # environment settings (keys "stream:A=1,B=2", ...)
+        runs = [("whole", {}), ("stream", {})]
+        for v in filter(None, os.environ.get("STREAM_VARIANTS", "").split(";")):
+            runs.append(("stream:" + v, dict(kv.split("=", 1) for kv in v.split(","))))
+        for key, env in runs:
+            mode = key.split(":")[0]
             out = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", mode, path, name,
-                                  str(batch_mb)], capture_output=True, text=True, timeout=600)
+                                  str(batch_mb)], capture_output=True, text=True, timeout=600,
+                                 env=dict(os.environ, **env))
             if out.returncode != 0:
                 sys.stderr.write(out.stderr)
                 return out.returncode
-            res[mode] = json.loads(out.stdout.strip().splitlines()[-1])
-            sys.stderr.write(json.dumps(res[mode]) + "\n")
+            if os.environ.get("STREAM_LOG"):   # (the children's stderr, e.g. S2C_HOST_TIMING lines)
+                with open(os.environ["STREAM_LOG"], "a") as f:
+                    f.write("== %s\n%s" % (key, out.stderr))
+            res[key] = json.loads(out.stdout.strip().splitlines()[-1])
+            sys.stderr.write(key + " " + json.dumps(res[key]) + "\n")
             sys.stderr.flush()
-        res["identical"] = res["whole"]["sha256"] == res["stream"]["sha256"]
+        res["identical"] = all(res[k]["sha256"] == res["whole"]["sha256"] for k, _ in runs)
         print(json.dumps(res))
         return 0 if res["identical"] else 1
 
