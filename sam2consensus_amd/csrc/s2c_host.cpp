@@ -105,10 +105,10 @@ class WorkerPool {
     // the pool of this process (pools are never destroyed: their threads may outlive main)
     static WorkerPool &get(int which) {
         static std::mutex gm;
-        static WorkerPool *pools[2] = {nullptr, nullptr};
+        static WorkerPool *pools[3] = {nullptr, nullptr, nullptr};
         static pid_t owner = 0;
         std::lock_guard<std::mutex> lk(gm);
-        if (owner != getpid()) { pools[0] = pools[1] = nullptr; owner = getpid(); }
+        if (owner != getpid()) { pools[0] = pools[1] = pools[2] = nullptr; owner = getpid(); }
         if (!pools[which]) pools[which] = new WorkerPool();
         return *pools[which];
     }
@@ -134,7 +134,7 @@ class WorkerPool {
     uint64_t gen_ = 0;
     int want_ = 0, left_ = 0, n_threads_ = 0;
 };
-enum { POOL_PARSE = 0, POOL_PLAN = 1 };
+enum { POOL_PARSE = 0, POOL_PLAN = 1, POOL_IO = 2 };
 }  // namespace
 
 // ------------------------------------------------------------------ tables
@@ -1048,11 +1048,7 @@ struct Bgzf {
                     }
                     inflateEnd(&zz);
                 };
-                std::vector<std::thread> th;
-                const unsigned n = (unsigned)std::min<size_t>(nt, off.size());
-                for (unsigned i = 1; i < n; i++) th.emplace_back(work);
-                work();
-                for (auto &x : th) x.join();
+                WorkerPool::get(POOL_IO).run((int)std::min<size_t>(nt, off.size()), [&](int) { work(); });
                 if (bad) { err = true; return false; }
             }
             cb.erase(cb.begin(), cb.begin() + k);
@@ -1153,14 +1149,7 @@ struct Reader {   // plain, gzip or BGZF (:111-114) byte source
             }
             got[k] = h;
         };
-        if (nt == 1) {
-            piece(0);
-        } else {
-            std::vector<std::thread> th;
-            for (size_t k = 1; k < nt; k++) th.emplace_back(piece, k);
-            piece(0);
-            for (auto &x : th) x.join();
-        }
+        WorkerPool::get(POOL_IO).run((int)nt, [&](int k) { piece((size_t)k); });
         if (bad) return -1;
         size_t tot = 0;   // (pieces after a short one are empty: the file ends there)
         for (size_t k = 0; k < nt; k++) {
@@ -1798,13 +1787,7 @@ static void build_layers(s2c_batch *b, int64_t G, bool with_dense) {
     const size_t NTL = tl.size();
     unsigned hw = std::thread::hardware_concurrency();
     const int nt = (int)std::max<size_t>(1, std::min<size_t>(std::min<unsigned>(hw ? hw : 1, 16), NTL / 64));
-    if (nt <= 1) {
-        copy_tiles(0, NTL);
-    } else {
-        std::vector<std::thread> th;
-        for (int k = 0; k < nt; k++) th.emplace_back(copy_tiles, NTL * k / nt, NTL * (k + 1) / nt);
-        for (auto &x : th) x.join();
-    }
+    par_ranges(nt, (int64_t)NTL, [&](int, int64_t k0, int64_t k1) { copy_tiles((size_t)k0, (size_t)k1); });
 }
 
 // Work items of a tile of nl layers: {tile, c, l0, l1}, enough that each one's run records
@@ -2714,13 +2697,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
                 }
             }
         };
-        if (nt <= 1) {
-            emit(0, NP);
-        } else {
-            std::vector<std::thread> th;
-            for (int t = 0; t < nt; t++) th.emplace_back(emit, NP * t / nt, NP * (t + 1) / nt);
-            for (auto &t : th) t.join();
-        }
+        par_ranges(nt, NP, [&](int, int64_t k0, int64_t k1) { emit(k0, k1); });
     clk.mark("emit threads");
         uint32_t *pr = &b->pc[4 * (size_t)NP];   // sentinel
         pr[1] = (uint32_t)(NQ / 16);
@@ -2855,10 +2832,10 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
         const int64_t cap8 = 163840 / 8 - (96 * nwp + 128);   // (the kernel's static LDS)
         const int64_t n0 = (int64_t)tiles.size();
         std::vector<int64_t> db(n0, -1);
-        par_ranges(plan_threads(n0, 64), n0, [&](int, int64_t t0, int64_t t1) {
+        const int64_t q0 = std::min(P0, n0), q1 = std::min(P1, n0);   // (the planned tiles only: balanced ranges)
+        par_ranges(plan_threads(q1 - q0, 64), q1 - q0, [&](int, int64_t i0, int64_t i1) {
             uint32_t tw[S2C_TILE_WORDS];
-            for (int64_t t = t0; t < t1; t++) {
-                if (!planned(t)) continue;
+            for (int64_t t = q0 + i0; t < q0 + i1; t++) {
                 tile_window(b, K, (uint64_t)tiles[t].a, (uint64_t)tiles[t].b, tw);
                 if (dense_fits(tw, K)) db[t] = dense_bytes(tw, K);
             }
@@ -2890,9 +2867,14 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     I.tile_max = tile_max;
     I.plan_t0 = P0;
     I.plan_t1 = std::min<int64_t>(P1, NT);
-    b->wtile.assign(NW, 0xFFFFFFFFu);
-    for (int64_t t = 0; t < NT; t++)
-        for (int64_t W = tiles[t].a >> 5; W < (tiles[t].b + 31) >> 5; W++) b->wtile[W] = (uint32_t)t;
+    b->wtile.resize(NW);
+    par_ranges(plan_threads(NW, 1 << 16), NW, [&](int, int64_t w0, int64_t w1) {
+        std::fill(b->wtile.begin() + w0, b->wtile.begin() + w1, 0xFFFFFFFFu);
+    });
+    par_ranges(plan_threads(NT, 1 << 10), NT, [&](int, int64_t t0, int64_t t1) {   // (tiles hold disjoint words)
+        for (int64_t t = t0; t < t1; t++)
+            for (int64_t W = tiles[t].a >> 5; W < (tiles[t].b + 31) >> 5; W++) b->wtile[W] = (uint32_t)t;
+    });
 
     clk.mark("tiles");
     // ---- long lists: run slots of long pieces per tile they overlap ----
@@ -2947,11 +2929,11 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     uint64_t boff = 0, loff = 0, coff = 0;
     int64_t runs_max = 0;
     // per tile (host threads): its window, the most candidate runs of a word, layers, items
-    std::vector<int64_t> t_nl(NT), t_nch(NT), t_maxc(NT), t_wruns(NT);
+    std::vector<int64_t> t_nl(NT, 0), t_nch(NT, 0), t_maxc(NT, 0), t_wruns(NT, 0);   // (0: an unplanned tile)
     std::atomic<bool> too_big{false};
-    par_ranges(plan_threads(NT, 64), NT, [&](int, int64_t ta, int64_t tb) {
-        for (int64_t t = ta; t < tb; t++) {
-            if (!planned(t)) { t_nl[t] = t_nch[t] = t_maxc[t] = t_wruns[t] = 0; continue; }
+    const int64_t q0 = std::min(P0, NT), q1 = std::min(P1, NT);   // the planned tiles, in balanced ranges
+    par_ranges(plan_threads(q1 - q0, 64), q1 - q0, [&](int, int64_t i0, int64_t i1) {
+        for (int64_t t = q0 + i0; t < q0 + i1; t++) {
             const Tile &T = tiles[t];
             const int64_t w0 = T.a >> 5, w1 = (T.b + 31) >> 5;
             const int64_t nlg = lcnt[t + 1] - lcnt[t];
@@ -3003,8 +2985,8 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
                 best = il;
             }
             if (best < IL)
-                par_ranges(plan_threads(NT, 64), NT, [&](int, int64_t ta, int64_t tb) {
-                    for (int64_t t = ta; t < tb; t++)
+                par_ranges(plan_threads(q1 - q0, 64), q1 - q0, [&](int, int64_t i0, int64_t i1) {
+                    for (int64_t t = q0 + i0; t < q0 + i1; t++)
                         if (t_nch[t] > 1)
                             t_nch[t] = std::max<int64_t>(t_nch[t], plan_items(b, K, (uint64_t)tiles[t].a, (uint64_t)tiles[t].b,
                                                                               t_nl[t], best));
