@@ -318,6 +318,44 @@ def test_parallel_file_parse_equals_sequential(tmp_path, monkeypatch):
     assert got["1"] == got["5"]
 
 
+def test_worker_pools_concurrent_and_forked(tmp_path, monkeypatch):
+    """The host's persistent worker pools (s2c_host.cpp WorkerPool): parses and plans run from
+    several Python threads at once (a busy pool hands the second caller threads of its own)
+    and from a forked child after the parent used the pools — each one the same batch as a
+    serial parse."""
+    import ctypes as C
+    import multiprocessing as mp
+    import threading
+    p = tmp_path / "in.sam"
+    sp = configs.spec("c2", scale=0.05)
+    n = C.c_int64()
+    _lib.check(_lib.lib.s2c_synth_write(C.byref(sp), str(p).encode(), C.byref(n)))
+    monkeypatch.setenv("S2C_PARSE_THREADS", "4")
+    want = _batch_digest(str(p), True)
+    got, errs = [None] * 4, []
+
+    def run(k):
+        try:
+            got[k] = _batch_digest(str(p), True)
+        except BaseException as e:  # noqa: BLE001 - reported below
+            errs.append(e)
+    th = [threading.Thread(target=run, args=(k,)) for k in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errs and got == [want] * 4
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    ch = ctx.Process(target=lambda: q.put(_batch_digest(str(p), True)))
+    ch.start()
+    try:
+        assert q.get(timeout=120) == want
+    finally:
+        ch.join(timeout=30)
+    assert ch.exitcode == 0
+
+
 # ---------------------------------------------------------------- CLI progress lines
 def _ref_progress(header_lines, lines_total):
     """:182, :194, :224-225 restated line by line (the counter starts at -header_length)."""
