@@ -3059,8 +3059,9 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     I.n_cols = (int64_t)coff;
     I.runs_max = runs_max;
     mark_runs(b);
-    build_dwin(b);
     clk.mark("mark_runs");
+    build_dwin(b);
+    clk.mark("dwin");
     *out = guard.release();
     return S2C_OK;
 }
