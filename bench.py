@@ -15,11 +15,14 @@ HIP events recorded on the launch stream between the stages of every timed step,
 kernel's time is a sub-interval of the step it belongs to.
 
 N>1 (torch.distributed.run, one process per GPU):
-  default        strong scaling, the north_star position split: ONE workload split into
-                 contiguous tile ranges (sam2consensus_amd.shard.split_tiles), each rank runs
-                 its shard; the shards' FASTA bodies and statistics are gathered to rank 0
-                 (RCCL) and checked against the reference's golden;
-  --independent  weak scaling: each rank runs its own batch of the workload (seed + rank).
+  default        weak scaling (the path partitions by position: per-GPU work fixed as N
+                 grows): each rank runs its own batch of the workload (seed + rank), as the
+                 position shards of an N-times larger genome would; no collective on the
+                 data path;
+  --shard        strong scaling, the north_star position split of ONE workload: contiguous
+                 tile ranges (sam2consensus_amd.shard.split_tiles), each rank runs its shard;
+                 the shards' FASTA bodies and statistics are gathered to rank 0 (RCCL) after
+                 the timed steps and checked against the reference's golden.
 Timing: barrier + synchronize on both sides of exactly K steps, MAX over ranks; value =
 aligned bases of all ranks / that time.  Rank 0 prints ONE JSON line.
 """
@@ -177,9 +180,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="c5", choices=sorted(WORKLOADS))
-    ap.add_argument("--independent", action="store_true",
-                    help="N>1: every rank its own batch (weak scaling) instead of one workload split by position")
-    ap.add_argument("--shard", action="store_true", help="(default for N>1; kept for old command lines)")
+    ap.add_argument("--shard", action="store_true",
+                    help="N>1: one workload split by position across the ranks (strong scaling) instead of "
+                         "every rank its own batch (weak scaling, the default)")
+    ap.add_argument("--independent", action="store_true", help="(the N>1 default; kept for old command lines)")
     ap.add_argument("--no-file-parse", action="store_true", help="skip the timed SAM-file parse (host_parse_s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-scale", type=float, default=0.016)
@@ -223,7 +227,7 @@ def main():
         min_depth = int(opt_args[opt_args.index("-m") + 1])
 
     t0 = time.perf_counter()
-    sharded = world > 1 and not args.independent
+    sharded = world > 1 and args.shard
     full = configs.synth_batch(wl, seed=configs.SEED + (0 if sharded else rank))
     hb = shard.sub_batch(full, rank, world) if sharded else full
     t_synth = time.perf_counter() - t0
@@ -349,7 +353,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms,
             "higher_is_better": True,
-            "scaling": "weak" if args.independent else "strong",
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic",
@@ -357,7 +361,7 @@ def main():
                        "reads_per_gpu": info.reads_mapped, "positions_per_gpu": info.total_len,
                        "thresholds": thresholds,
                        "parallelism": ("one batch per GPU, independent workloads (no collective on the data path)"
-                                       if args.independent else
+                                       if not sharded else
                                        "one workload split into contiguous tile ranges per GPU (N=1: the whole "
                                        "workload); shard bodies and stats gathered to rank 0")},
         }
