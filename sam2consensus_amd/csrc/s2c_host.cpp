@@ -28,6 +28,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <functional>
 #include <memory>
 #include <string>
@@ -72,18 +73,30 @@ namespace {
 class WorkerPool {
   public:
     // f(t) for t in [0, nt): t = 0 on the calling thread, the others on the pool's
+    // (an exception of any f(t) is rethrown here once every thread is done with the run)
     template <class F>
     void run(int nt, F &&f) {
         if (nt <= 1) { f(0); return; }
+        std::exception_ptr err;
+        std::mutex em;
+        auto safe = [&](int t) {
+            try {
+                f(t);
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(em);
+                if (!err) err = std::current_exception();
+            }
+        };
         std::unique_lock<std::mutex> rl(run_m_, std::try_to_lock);
         if (!rl.owns_lock()) {   // busy: threads of its own
             std::vector<std::thread> th;
-            for (int t = 1; t < nt; t++) th.emplace_back([&f, t] { f(t); });
-            f(0);
+            for (int t = 1; t < nt; t++) th.emplace_back([&safe, t] { safe(t); });
+            safe(0);
             for (auto &x : th) x.join();
+            if (err) std::rethrow_exception(err);
             return;
         }
-        const std::function<void(int)> job = [&f](int t) { f(t); };
+        const std::function<void(int)> job = [&safe](int t) { safe(t); };
         {
             std::lock_guard<std::mutex> lk(m_);
             while ((int)n_threads_ < nt - 1) {
@@ -97,10 +110,13 @@ class WorkerPool {
             gen_++;
         }
         go_.notify_all();
-        f(0);
-        std::unique_lock<std::mutex> lk(m_);
-        done_.wait(lk, [&] { return left_ == 0; });
-        job_ = nullptr;
+        safe(0);
+        {
+            std::unique_lock<std::mutex> lk(m_);
+            done_.wait(lk, [&] { return left_ == 0; });
+            job_ = nullptr;
+        }
+        if (err) std::rethrow_exception(err);
     }
     // the pool of this process (pools are never destroyed: their threads may outlive main)
     static WorkerPool &get(int which) {
