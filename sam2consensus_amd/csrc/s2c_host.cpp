@@ -289,7 +289,16 @@ struct uninit_alloc {
     uninit_alloc() = default;
     template <class U> uninit_alloc(const uninit_alloc<U> &) {}
     static size_t map_len(size_t bytes) { return (bytes + HUGE_PAGE - 1) & ~(HUGE_PAGE - 1); }
+    static bool poison() {   // S2C_MAP_POISON=1 (tests): every array starts as 0xA5 bytes, not zero pages
+        static const bool on = getenv("S2C_MAP_POISON") != nullptr;
+        return on;
+    }
     T *allocate(size_t n) {
+        T *p = allocate_raw(n);
+        if (poison()) memset((void *)p, 0xA5, n * sizeof(T));
+        return p;
+    }
+    T *allocate_raw(size_t n) {
         const size_t bytes = n * sizeof(T);
         if (bytes < huge_min()) {
             void *q = ::operator new(bytes);

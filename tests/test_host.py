@@ -356,6 +356,37 @@ def test_worker_pools_concurrent_and_forked(tmp_path, monkeypatch):
     assert ch.exitcode == 0
 
 
+def test_batch_does_not_read_unwritten_memory(tmp_path):
+    """The packed batch's arrays come from an allocator that leaves them uninitialised
+    (uninit_alloc; fresh mappings happen to be zero pages).  With S2C_MAP_POISON=1 every such
+    array starts as 0xA5 bytes: the batch (every array, the plan and the layered windows) must
+    not change, i.e. no field is left unwritten and read as zero."""
+    import ctypes as C
+    import sys
+    p = tmp_path / "in.sam"
+    sp = configs.spec("c2", scale=0.05)
+    n = C.c_int64()
+    _lib.check(_lib.lib.s2c_synth_write(C.byref(sp), str(p).encode(), C.byref(n)))
+    code = ("import sys, hashlib, numpy as np; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+            "from sam2consensus_amd import batch\n"
+            "hb = batch.parse_file(%r, True, 150).ensure_layers(dense=True)\n"
+            "h = hashlib.sha256()\n"
+            "for k in sorted(vars(hb)):\n"
+            "    v = getattr(hb, k)\n"
+            "    if isinstance(v, np.ndarray): h.update(k.encode()); h.update(np.ascontiguousarray(v).tobytes())\n"
+            "print(h.hexdigest())\n") % (ROOT, os.path.join(ROOT, "tests"), str(p))
+    out = {}
+    for poison in ("0", "1"):
+        env = dict(os.environ)
+        env.pop("S2C_MAP_POISON", None)
+        if poison == "1":
+            env["S2C_MAP_POISON"] = "1"
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[poison] = r.stdout.strip().splitlines()[-1]
+    assert out["0"] == out["1"]
+
+
 # ---------------------------------------------------------------- CLI progress lines
 def _ref_progress(header_lines, lines_total):
     """:182, :194, :224-225 restated line by line (the counter starts at -header_length)."""
