@@ -25,6 +25,7 @@ S2C_ERR_LIMIT = -13
 
 S2C_NSYM = 6
 S2C_POS_ALIGN = 64
+ABI_VERSION = 13      # include/s2c.h S2C_ABI_VERSION: the structs below mirror this version
 S2C_TILE_WORDS = 24
 S2C_LY_MAIN = 0xFFFFFFFF
 S2C_ITEM_WORDS = 4
@@ -204,6 +205,8 @@ def _layout_check():
         raise ImportError("libs2c.so ABI mismatch: C %r vs ctypes %r" % (got, want))
 
 
+if lib.s2c_abi_version() != ABI_VERSION:
+    raise ImportError("libs2c.so ABI %d, these bindings ABI %d (rebuild: make)" % (lib.s2c_abi_version(), ABI_VERSION))
 _layout_check()
 
 

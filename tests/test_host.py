@@ -27,7 +27,8 @@ def test_library_exports_every_declared_symbol():
     exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
     assert declared <= exported, declared - exported
     assert declared == set(_lib.EXPORTS)
-    assert _lib.lib.s2c_abi_version() == 13
+    hv = int(re.search(r"#define S2C_ABI_VERSION (\d+)", header).group(1))
+    assert _lib.lib.s2c_abi_version() == _lib.ABI_VERSION == hv == 13
 
 
 def _model_case(sam, args):
@@ -753,3 +754,12 @@ def test_host_code_under_sanitizers(tmp_path):
         out = r.stdout + r.stderr
         assert r.returncode == 0 and "rc 0" in r.stdout, (name, path, threads, out[-3000:])
         assert "runtime error" not in out and "AddressSanitizer" not in out, out[-3000:]
+
+
+def test_graft_build_entry():
+    """__graft_entry__.build() (the driver's build check): make in-tree, import, ABI check."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("graft_entry", os.path.join(ROOT, "__graft_entry__.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    m.build()
