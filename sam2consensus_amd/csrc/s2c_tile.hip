@@ -1655,6 +1655,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
         if (has_ins)
             il = build_layout<PF, false>(d, T, tile, L.bits, L.wrank, L.klen, L.key, cols, L.colkey, L.scan, evl,
                                          rec_ev ? min(evn, (uint32_t)S2C_EPI_KEYS) : 0u, !(rec_ev && d.tables_empty));
+        TPROF_MARK(12);   // (the epilogue's LDS set up and the insertion layout; MARK(7): the votes and stores)
         tile_epilogue_fast<NWP>(d, tile, T, il, hist, cols, L);
     } else {
         // deep tile: this item's counts → HBM (symbol-major, coalesced atomics); a general

@@ -46,7 +46,7 @@ print("k_reads %.4f ms  pileup %.4f ms  consensus %.4f ms" % (ev[0].elapsed_time
 n = max(buf[15], 1)
 names = {0: "setup (zero LDS)", 1: "layer DMA + wait", 9: "walk: records, segments", 10: "walk: one-token pieces",
          8: "walk: op walks", 2: "walk: planes wait", 3: "count", 4: "long pieces + flush", 5: "reconstruct counts",
-         6: "epilogue / store"}
+         11: "epilogue: LDS + layout", 6: "epilogue: votes / store"}
 tot = sum(buf[k] for k in names)
 for k, nm in names.items():
     print("  %-24s %9.0f cyc/wg  %5.1f%%" % (nm, buf[k] / n, 100.0 * buf[k] / max(tot, 1)))
