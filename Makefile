@@ -23,7 +23,7 @@ $(BUILD)/%.o: $(SRC)/%.hip $(SRC)/s2c_common.h include/s2c.h scripts/check_spill
 	$(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage -c $< -o $@ 2> $(BUILD)/$*.usage || { cat $(BUILD)/$*.usage; exit 1; }
 	python3 scripts/check_spills.py $(BUILD)/$*.usage || { rm -f $@; exit 1; }
 
-KOBJ = $(BUILD)/s2c_reads.o $(BUILD)/s2c_tile.o $(BUILD)/s2c_dense.o
+KOBJ = $(BUILD)/s2c_reads.o $(BUILD)/s2c_tile.o $(BUILD)/s2c_dense.o $(BUILD)/s2c_bodies.o
 
 $(OUT): $(BUILD)/s2c_host.o $(BUILD)/s2c_synth.o $(KOBJ)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ -lz -lpthread -o $@
@@ -33,10 +33,10 @@ $(BUILD):
 
 # diagnostic build: phase clocks of k_tile_dense (S2C_LIB=libs2c_prof.so, scripts/prof_dense.py)
 PROF_OUT = sam2consensus_amd/libs2c_prof.so
-prof: $(BUILD)/s2c_host.o $(BUILD)/s2c_synth.o $(BUILD)/s2c_reads.o $(SRC)/s2c_tile.hip $(SRC)/s2c_dense.hip $(SRC)/s2c_common.h
+prof: $(BUILD)/s2c_host.o $(BUILD)/s2c_synth.o $(BUILD)/s2c_reads.o $(BUILD)/s2c_bodies.o $(SRC)/s2c_tile.hip $(SRC)/s2c_dense.hip $(SRC)/s2c_common.h
 	$(HIPCC) $(HIPFLAGS) $(VDEFS) -DS2C_PROF -c $(SRC)/s2c_dense.hip -o $(BUILD)/s2c_dense_prof.o
 	$(HIPCC) $(HIPFLAGS) $(VDEFS) -DS2C_PROF -c $(SRC)/s2c_tile.hip -o $(BUILD)/s2c_tile_prof.o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(BUILD)/s2c_host.o $(BUILD)/s2c_synth.o $(BUILD)/s2c_reads.o \
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(BUILD)/s2c_host.o $(BUILD)/s2c_synth.o $(BUILD)/s2c_reads.o $(BUILD)/s2c_bodies.o \
 	  $(BUILD)/s2c_tile_prof.o $(BUILD)/s2c_dense_prof.o -lz -lpthread -o $(PROF_OUT)
 
 # kernel resource usage (VGPR/SGPR/LDS/occupancy) and ISA for inspection
@@ -50,12 +50,22 @@ isa:
 clean:
 	rm -rf $(BUILD) $(OUT)
 
-.PHONY: all clean isa prof variant
+# diagnostic build: every kernel fills its workgroup's LDS with 0xA5 at entry (S2C_LIB=libs2c_poison.so;
+# the GPU suite once under it shows no kernel reads LDS it did not write in that launch)
+poison: $(BUILD)/s2c_host.o $(BUILD)/s2c_synth.o
+	$(HIPCC) $(HIPFLAGS) -DS2C_LDS_POISON -c $(SRC)/s2c_reads.hip -o $(BUILD)/s2c_reads_poison.o
+	$(HIPCC) $(HIPFLAGS) -DS2C_LDS_POISON -c $(SRC)/s2c_dense.hip -o $(BUILD)/s2c_dense_poison.o
+	$(HIPCC) $(HIPFLAGS) -DS2C_LDS_POISON -c $(SRC)/s2c_tile.hip -o $(BUILD)/s2c_tile_poison.o
+	$(HIPCC) $(HIPFLAGS) -DS2C_LDS_POISON -c $(SRC)/s2c_bodies.hip -o $(BUILD)/s2c_bodies_poison.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ $(BUILD)/s2c_reads_poison.o $(BUILD)/s2c_dense_poison.o \
+	  $(BUILD)/s2c_tile_poison.o $(BUILD)/s2c_bodies_poison.o -lz -lpthread -o sam2consensus_amd/libs2c_poison.so
+
+.PHONY: all clean isa prof variant poison
 
 # experiment build: k_reads, k_tile_dense and k_tile with extra defines (V=name VDEFS='-D...'): libs2c_$(V).so
 V ?= var
 VDEFS ?=
-variant: $(BUILD)/s2c_host.o $(BUILD)/s2c_synth.o
+variant: $(BUILD)/s2c_host.o $(BUILD)/s2c_synth.o $(BUILD)/s2c_bodies.o
 	$(HIPCC) $(HIPFLAGS) $(VDEFS) -c $(SRC)/s2c_reads.hip -o $(BUILD)/s2c_reads_$(V).o
 	$(HIPCC) $(HIPFLAGS) $(VDEFS) -c $(SRC)/s2c_dense.hip -o $(BUILD)/s2c_dense_$(V).o
 	$(HIPCC) $(HIPFLAGS) $(VDEFS) -c $(SRC)/s2c_tile.hip -o $(BUILD)/s2c_tile_$(V).o

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define S2C_ABI_VERSION 13
+#define S2C_ABI_VERSION 14
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define S2C_OK            0
@@ -260,6 +260,12 @@ int  s2c_parser_counters(s2c_parser *p, int64_t *out);
    out[5] = {header ended (0/1), references, header lines, lines read (through the failing
    line), error code of the read pass (0: none)}. */
 int  s2c_parser_progress(const s2c_parser *p, int64_t *out);
+
+/* (ABI 14) The compute units of the device the batches will run on (the grid shaping of the
+ * deep tiles' work items, s2c_parser_finish): 256 (MI355X) until set; a partitioned device
+ * mode or another part names its own.  Process-wide; it changes how work is split, never a
+ * result. */
+int  s2c_plan_set_cus(int64_t cus);
 
 /* FASTA body assembly (:394-418): dst = raw[starts[0] : +lens[0]] ++ raw[starts[1] : +lens[1]]
    ++ ... (n blocks; dst holds their total length), copied on the host threads.  The tiles'
@@ -495,6 +501,15 @@ int s2c_pileup(const s2c_dev *d, void *stream);
 int s2c_consensus(const s2c_dev *d, void *stream);
 /* all three, in order, on one stream (graph-capturable: no allocation, no sync) */
 int s2c_run(const s2c_dev *d, void *stream);
+
+/* (ABI 14) FASTA body assembly on the device (:394-418; replaces the host gather of the
+ * output's body slots, s2c_gather_bodies): dst[offs[i], offs[i+1]) = out[starts[i], +len)
+ * with len = offs[i+1] - offs[i], for n blocks in [threshold][tile] order — out = s2c_dev.out,
+ * starts[i] = the block's slot t·(F·padded_len + n_cols) + F·a + cb0, offs = the exclusive
+ * prefix sum of the blocks' blk_len (offs[0] = 0, n + 1 entries).  All pointers are device
+ * pointers (int64 arrays); a block reaching past out_len is skipped.  Asynchronous on stream. */
+int s2c_gather_bodies_dev(const uint8_t *out, int64_t out_len, const int64_t *starts, const int64_t *offs,
+                          int64_t n, uint8_t *dst, void *stream);
 
 /* Diagnostics (tests only, not part of the product path): k_reads over every piece, then
  * every tile's counts stored to d->counts ([6][padded_len] u32) and no vote. */

@@ -25,7 +25,7 @@ S2C_ERR_LIMIT = -13
 
 S2C_NSYM = 6
 S2C_POS_ALIGN = 64
-ABI_VERSION = 13      # include/s2c.h S2C_ABI_VERSION: the structs below mirror this version
+ABI_VERSION = 14      # include/s2c.h S2C_ABI_VERSION: the structs below mirror this version
 S2C_TILE_WORDS = 24
 S2C_LY_MAIN = 0xFFFFFFFF
 S2C_ITEM_WORDS = 4
@@ -119,6 +119,7 @@ EXPORTS = [
     "s2c_batch_layers", "s2c_batch_layers_mode", "s2c_batch_info_get", "s2c_batch_arrays_get", "s2c_batch_ref_name", "s2c_batch_free", "s2c_batch_shard",
     "s2c_parsecigar", "s2c_synth_feed", "s2c_synth_write",
     "s2c_workspace_sizes", "s2c_reads", "s2c_pileup", "s2c_consensus", "s2c_run", "s2c_pileup_counts",
+    "s2c_gather_bodies_dev", "s2c_plan_set_cus",
 ]
 
 
@@ -181,6 +182,8 @@ def _load():
         "s2c_pileup_counts": (C.c_int, [C.POINTER(Dev), _VP]),
         "s2c_consensus": (C.c_int, [C.POINTER(Dev), _VP]),
         "s2c_run": (C.c_int, [C.POINTER(Dev), _VP]),
+        "s2c_gather_bodies_dev": (C.c_int, [_VP, C.c_int64, _VP, _VP, C.c_int64, _VP, _VP]),
+        "s2c_plan_set_cus": (C.c_int, [C.c_int64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -208,6 +211,13 @@ def _layout_check():
 if lib.s2c_abi_version() != ABI_VERSION:
     raise ImportError("libs2c.so ABI %d, these bindings ABI %d (rebuild: make)" % (lib.s2c_abi_version(), ABI_VERSION))
 _layout_check()
+
+
+def plan_for_device(device):
+    """Plan batches for ``device``'s compute units (s2c_plan_set_cus: the deep tiles' grid
+    shaping) — the product paths call it once they hold their GPU."""
+    import torch
+    check(lib.s2c_plan_set_cus(int(torch.cuda.get_device_properties(device).multi_processor_count)))
 
 
 def last_error():

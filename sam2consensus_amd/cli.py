@@ -139,9 +139,12 @@ def _warm_device(device):
 
     def run():
         try:
+            from . import _lib
             from .engine import _dev
             import torch
-            torch.empty(1, device=_dev(device))
+            d = _dev(device)
+            torch.empty(1, device=d)
+            _lib.plan_for_device(d)   # (the plan's grid shaping: this device's CUs, once known)
         except Exception:  # noqa: BLE001 - reported by DeviceBatch on the main thread
             pass
     th = threading.Thread(target=run, daemon=True)
@@ -218,7 +221,7 @@ def consensus_files_sharded(filename, thresholds, prefix, min_depth, fill, nchar
     from .dparse import parse_distributed
     from .engine import DeviceBatch, Workspace, needs_dense_layers
     from .records import build_records, render
-    from .shard import gather_results
+    from .shard import gather_device
 
     world, rank, local = _dist_env()
     backend = os.environ.get("S2C_DIST_BACKEND", "nccl")
@@ -229,6 +232,8 @@ def consensus_files_sharded(filename, thresholds, prefix, min_depth, fill, nchar
                                "(S2C_DIST_BACKEND=gloo lets ranks share a device)" % (local, ndev))
         local %= ndev   # (ranks sharing a device: gloo tests on one GPU)
     torch.cuda.set_device(local)
+    from . import _lib
+    _lib.plan_for_device(torch.device("cuda", local))
     owned = not dist.is_initialized()   # (this call's process group: destroyed on the way out)
     if owned:
         dist.init_process_group(backend, device_id=torch.device("cuda", local) if backend == "nccl" else None)
@@ -239,7 +244,7 @@ def consensus_files_sharded(filename, thresholds, prefix, min_depth, fill, nchar
         ws = Workspace(DeviceBatch(P.sub, "cuda:%d" % local, dense_layers=needs_dense_layers(fill)), thresholds,
                        min_depth, fill)
         ws.run()
-        res = gather_results(ws.fetch(), P.sub, rank, world, len(thresholds))
+        res = gather_device(ws, P.sub, rank, world, len(thresholds))
     finally:
         if owned and dist.is_initialized():
             dist.destroy_process_group()

@@ -76,6 +76,23 @@ __device__ __forceinline__ void lds_sync() {
 // s_waitcnt vmcnt(0) as a real S_WAITCNT (the compiler's wait tracking sees it)
 __device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
+// Diagnostic build S2C_LDS_POISON (`make poison`): at entry every kernel fills all of its
+// workgroup's LDS with 0xA5 bytes (then an LDS barrier), so a read of LDS that this workgroup
+// did not write sees the same garbage every time instead of whatever an earlier workgroup
+// left on that CU — round 5's k_tile keyed stale LDS event slots that way.
+#ifdef S2C_LDS_POISON
+template <typename T>
+__device__ __forceinline__ void lds_poison(T *p, uint32_t bytes) {
+    uint32_t *q = (uint32_t *)p;
+    for (uint32_t i = threadIdx.x; i < bytes / 4; i += blockDim.x) q[i] = 0xA5A5A5A5u;
+}
+#define S2C_POISON(p, bytes) lds_poison(p, (uint32_t)(bytes))
+#define S2C_POISON_DONE() lds_sync()
+#else
+#define S2C_POISON(p, bytes) ((void)0)
+#define S2C_POISON_DONE() ((void)0)
+#endif
+
 
 // ----------------------------------------------------------------- parsecigar on the device
 __device__ __forceinline__ bool op_bases(uint32_t op) { return op == S2C_OP_M || op == S2C_OP_EQ || op == S2C_OP_X; }

@@ -170,31 +170,18 @@ __device__ __forceinline__ DPiece dpc_dec(uint32_t c0, uint32_t c1) {
 }
 // FASTA body stores (written once, fetched by the host): nontemporal (−1.2 % on C5,
 // profiles/r05/v6_nt_loads_stores_ab.txt; the same policy on the compact records' loads cost +2 %)
-#ifndef S2C_BODY_NT
-#define S2C_BODY_NT 1
-#endif
 template <class T>
 __device__ __forceinline__ void body_st(T *p, T v) {
-#if S2C_BODY_NT
     if constexpr (std::is_same_v<T, uint2>) {
         __builtin_nontemporal_store(v.x, (uint32_t *)p);
         __builtin_nontemporal_store(v.y, (uint32_t *)p + 1);
     } else {
         __builtin_nontemporal_store(v, p);
     }
-#else
-    *p = v;
-#endif
 }
 // (a 3-vector takes 16 bytes: the record is addressed by dwords, 3 per record, 4-byte aligned)
-typedef uint32_t u32x3 __attribute__((ext_vector_type(3), aligned(4)));
 __device__ __forceinline__ uint3 dpc_load(const DenseArgs &d, uint32_t i) {
-#if S2C_DPC_NT
-    const u32x3 r = __builtin_nontemporal_load((const u32x3 *)(d.dpc + 3 * (size_t)i));   // (read once: streamed)
-    return make_uint3(r.x, r.y, r.z);
-#else
     return ((const uint3 *)d.dpc)[i];
-#endif
 }
 // rec_enc from a biased start (rs = tile-relative start + REC_BIAS)
 __device__ __forceinline__ uint2 rec_enc_b(uint32_t rs, uint32_t len, uint32_t q) {
@@ -203,10 +190,7 @@ __device__ __forceinline__ uint2 rec_enc_b(uint32_t rs, uint32_t len, uint32_t q
 
 constexpr int WGD = 64;   // one wave per tile
 constexpr int GSD = 8;    // records per counting group (one Harley–Seal tree)
-#ifndef S2C_CNT_PART
-#define S2C_CNT_PART 2
-#endif
-constexpr int CNT_PART = S2C_CNT_PART;   // records whose geometry and plane words are in registers at once
+constexpr int CNT_PART = 2;   // records whose geometry and plane words are in registers at once
 
 // LDS byte address of a shared-memory pointer
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
@@ -224,20 +208,8 @@ __device__ __forceinline__ double sload_f64(const double *p) {
 }
 
 // cache policy bits of the window DMA: nt (streamed; measured −2.5 % on C5 against the
-// default policy, profiles/r05/v5_dma_policy_ab.txt); variant builds: -DS2C_DMA_CP=0 default,
-// 2 sc1, 3 sc0
-#ifndef S2C_DMA_CP
-#define S2C_DMA_CP 1
-#endif
-#if S2C_DMA_CP == 1
+// default policy and sc0 / sc1, profiles/r05/v5_dma_policy_ab.txt)
 #define S2C_DMA_POLICY " nt"
-#elif S2C_DMA_CP == 2
-#define S2C_DMA_POLICY " sc1"
-#elif S2C_DMA_CP == 3
-#define S2C_DMA_POLICY " sc0"
-#else
-#define S2C_DMA_POLICY ""
-#endif
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"   // m0 (reserved) is set and clobbered by the DMA
 // n dwords src[0..n) of an array ending at `end` → LDS by 16-byte LDS-DMA (1 KB per wave
@@ -357,10 +329,8 @@ __device__ __forceinline__ void wave_lds_sync() {
 // uint2 (a padded lane stride: the lanes of a word read different counters on distinct
 // banks), then aliased by the summed rows [word][4 counters][8 rows] at XCH_VROW dwords a word
 constexpr uint32_t XCH_STRIDE = 65;
-#ifndef S2C_XCH_NCH_MAX
-#define S2C_XCH_NCH_MAX 4
-#endif
-constexpr uint32_t XCH_WAVE_BYTES = S2C_XCH_NCH_MAX * 4 * XCH_STRIDE * 8;   // 8,320
+constexpr uint32_t XCH_NCH_MAX = 4;
+constexpr uint32_t XCH_WAVE_BYTES = XCH_NCH_MAX * 4 * XCH_STRIDE * 8;   // 8,320
 constexpr uint32_t XCH_VROW = 40;                              // 32 row dwords + 8 (conflict-free b64 reads)
 
 // Per-position byte counters in the ROW layout of the transposed counters: tile-relative
@@ -520,15 +490,9 @@ __device__ __forceinline__ void win_issue(const DenseArgs &d, const Win &v, uint
 // One tile of NWP words from its window in LDS, WPT waves (WT threads): a wave holds NWP / WPT
 // words, G lanes per word, RPL = 8 / G counter rows (4 positions each) voted per lane.
 // dcnt / ncnt / ccnt: zeroed byte counters; stl: the waves' partial tile statistics.
-#ifndef S2C_DENSE_WPT
-#define S2C_DENSE_WPT 2
-#endif
-constexpr int WPT = S2C_DENSE_WPT;   // waves per tile (they share the window)
+constexpr int WPT = 2;   // waves per tile (they share the window)
 constexpr int WT = WGD * WPT;     // threads per tile
-#ifndef S2C_DENSE_PFN
-#define S2C_DENSE_PFN 2
-#endif
-constexpr int PFN = S2C_DENSE_PFN;   // piece records per thread loaded with the DMA (windows of ≤ PFN·WT pieces)
+constexpr int PFN = 2;   // piece records per thread loaded with the DMA (windows of ≤ PFN·WT pieces)
 template <int NWP>
 __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, const WinLds &L, uint32_t *dcnt,
                                            uint32_t *ncnt, uint32_t *ccnt, const uint8_t *amb, uint32_t fill0,
@@ -956,7 +920,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         };
         if (npl <= 2) xchg(std::integral_constant<int, 1>{});
         else if (npl <= 4) xchg(std::integral_constant<int, 2>{});
-        else if (npl <= 6 || S2C_XCH_NCH_MAX < 4) xchg(std::integral_constant<int, 3>{});
+        else if (npl <= 6) xchg(std::integral_constant<int, 3>{});
         else xchg(std::integral_constant<int, 4>{});
         const uint32_t *vr = vp + wl * XCH_VROW + g * RPL;
 #pragma unroll
@@ -1161,22 +1125,24 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
 #endif
 }
 
-// waves per SIMD the register budget is cut for (variant builds: -DS2C_DENSE_OCC=...)
-#ifndef S2C_DENSE_OCC
-#define S2C_DENSE_OCC
-#endif
-
 // One wave per tile (block b → item, XCD-major: the blocks of one XCD, b ≡ x mod 8, take a
 // contiguous range of items, so neighbouring windows meet in that XCD's L2).  Everything the
 // tile needs arrives by one LDS-DMA round trip after the scalar loads of its tile record.
 template <int NWP>
-__global__ __launch_bounds__(WT) S2C_DENSE_OCC void k_tile_dense(const DenseArgs d) {
+__global__ __launch_bounds__(WT) void k_tile_dense(const DenseArgs d) {
     extern __shared__ uint4 arena[];   // the window (S2C_DENSE_BYTES layout)
     // one byte per position (row layout): '-' (D/N/P runs, '-' of SEQ unless maxdel drops
     // the read's), 'N' of SEQ, '-' of SEQ (all: the planes count them as C, and 'N' as A)
     __shared__ __attribute__((aligned(16))) uint32_t dcnt[8 * NWP], ncnt[8 * NWP], ccnt[8 * NWP];
     __shared__ __attribute__((aligned(16))) uint8_t amb[64];
     __shared__ uint32_t stl[2][WPT][4];
+    S2C_POISON(arena, d.buf_bytes);   // (before the window's DMA lands there)
+    S2C_POISON(dcnt, sizeof(dcnt));
+    S2C_POISON(ncnt, sizeof(ncnt));
+    S2C_POISON(ccnt, sizeof(ccnt));
+    S2C_POISON(amb, sizeof(amb));
+    S2C_POISON(stl, sizeof(stl));
+    S2C_POISON_DONE();
 #ifdef S2C_PROF
     const unsigned long long t_entry = __builtin_amdgcn_s_memtime();
 #else

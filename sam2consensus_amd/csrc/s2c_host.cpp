@@ -61,6 +61,23 @@ int s2c_guarded(F &&f) {
 }
 extern "C" int s2c_abi_version(void) { return S2C_ABI_VERSION; }
 
+// ------------------------------------------------------------------ plan knobs
+// Overrides of the batch plan's shape (tile widths, deep-tile items, dense / event routing)
+// are measurement tools, not options: they are read only when S2C_DEBUG_PLAN is set, so the
+// product plan is the same whatever else the environment holds.
+static const char *plan_env(const char *name) {
+    static const bool debug = getenv("S2C_DEBUG_PLAN") != nullptr;
+    return debug ? getenv(name) : nullptr;
+}
+// The device's compute units (grid shaping of k_tile's launches; s2c_plan_set_cus) — the
+// MI355X's 256 until the caller names its device's.
+static std::atomic<int64_t> g_plan_cus{256};
+extern "C" int s2c_plan_set_cus(int64_t cus) {
+    if (cus <= 0 || cus > 4096) return s2c_set_error(S2C_ERR_ARG, "compute units outside (0, 4096]");
+    g_plan_cus.store(cus);
+    return S2C_OK;
+}
+
 // ------------------------------------------------------------------ host worker pools
 // Persistent host threads for the parse windows and the plan's parallel loops.  A thread
 // made per window (16 per 64 MB block of a streamed file) maps its stack while the other
@@ -1353,7 +1370,7 @@ namespace {
 constexpr int64_t TP_MIN = 256, TP_MAX = 2048;      // tile bounds (positions)
 static int64_t deep_tile_min() {   // S2C_DEEP_TILE: the narrowest deep tile (positions)
     static const int64_t v = [] {
-        const char *e = getenv("S2C_DEEP_TILE");
+        const char *e = plan_env("S2C_DEEP_TILE");
         return e ? std::min<int64_t>(std::max<int64_t>(atoll(e), 64), 2048) : (int64_t)512;
     }();
     return v;
@@ -1528,7 +1545,7 @@ static void mark_runs(s2c_batch *b) {
         }
     }
     b->info.walk_queue = walk_queue_of(b->info);
-    static const bool no_tile_events = getenv("S2C_NO_TILE_EVENTS") != nullptr;   // (A/B: k_reads hashes every event)
+    static const bool no_tile_events = plan_env("S2C_NO_TILE_EVENTS") != nullptr;   // (A/B: k_reads hashes every event)
     b->info.tile_events = b->info.walk_queue && !no_tile_events ? 1 : 0;
     const bool rec = b->info.tile_events != 0;
     auto tile_takes_events = [&](int64_t k) {   // every event of insertion piece k recorded by k_tile
@@ -1821,7 +1838,7 @@ static void build_layers(s2c_batch *b, int64_t G, bool with_dense) {
 // (16 per wave), S2C_ITEM_LAYERS overrides.
 static int64_t item_layers() {
     static const int64_t il = [] {
-        const char *e = getenv("S2C_ITEM_LAYERS");
+        const char *e = plan_env("S2C_ITEM_LAYERS");
         return e ? std::max<int64_t>(4, atoll(e)) : (int64_t)64;
     }();
     return il;
@@ -2749,8 +2766,8 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     std::vector<Tile> tiles;
     int64_t tile_max = S2C_POS_ALIGN;
     int64_t tile_force = 0;   // diagnostic override (S2C_TILE_POS, a multiple of 64 in [64, 2048])
-    const bool no_dense = getenv("S2C_NO_DENSE") != nullptr;   // diagnostic: every tile through k_tile
-    if (const char *e = getenv("S2C_TILE_POS"))
+    const bool no_dense = plan_env("S2C_NO_DENSE") != nullptr;   // diagnostic: every tile through k_tile
+    if (const char *e = plan_env("S2C_TILE_POS"))
         tile_force = align_up(std::min<int64_t>(std::max<int64_t>(atoll(e), 64), TP_MAX), S2C_POS_ALIGN);
     if (p->tile_width > 0) tile_force = p->tile_width;   // streamed batches: the same tiles every time
     std::vector<int64_t> ref_slots(R, 0), ref_np(R, 0), ref_qw(R, 0);
@@ -2996,8 +3013,8 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
             if (t_nch[t] > 1) n_multi += t_nch[t];
             else if (!dense_tile(t)) n_single++;
         }
-        int64_t slots = 256 * (nwp <= 16 ? 3 : 2);   // MI355X: 256 CUs; k_tile<16>: 3 workgroups per CU by LDS
-        if (const char *e = getenv("S2C_ITEM_SLOTS")) slots = std::max<int64_t>(0, atoll(e));
+        int64_t slots = g_plan_cus.load() * (nwp <= 16 ? 3 : 2);   // the device's CUs × k_tile<16>'s 3 workgroups per CU by LDS
+        if (const char *e = plan_env("S2C_ITEM_SLOTS")) slots = std::max<int64_t>(0, atoll(e));
         const int64_t IL = item_layers();
         if (n_multi > 0 && slots > 0) {
             const int64_t rounds = (n_single + n_multi + slots - 1) / slots;

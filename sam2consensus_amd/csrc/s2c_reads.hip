@@ -17,10 +17,6 @@
 // tile's long-event list (multiplicity 1; the column sums of :284-287 are additive).
 #include "s2c_common.h"
 
-#ifndef S2C_EV_FAST   // (variant builds: 0 = every piece through walk_piece, codes base by base)
-#define S2C_EV_FAST 1
-#endif
-
 namespace s2c {
 namespace {
 
@@ -40,15 +36,6 @@ struct GlobalMem {   // walk_piece's view of the batch in HBM
     __device__ __forceinline__ uint32_t x(uint64_t w) const { return bx[w]; }
 };
 
-// symbol code ("-ACGNT" index) of query base q
-__device__ __forceinline__ uint32_t base_code(const ReadsArgs &d, uint64_t q) {
-    const uint64_t w = q >> 5;
-    const uint32_t sh = (uint32_t)(q & 31);
-    const uint32_t p0 = (d.bq[2 * w] >> sh) & 1u, p1 = (d.bq[2 * w + 1] >> sh) & 1u, x = (d.bx[w] >> sh) & 1u;
-    // x = 0: A C G T → 1 2 3 5;  x = 1: p0 = 0 'N' → 4, p0 = 1 '-' → 0
-    return x ? (p0 ? 0u : 4u) : ((p1 << 1 | p0) == 3u ? 5u : (p1 << 1 | p0) + 1u);
-}
-
 __device__ __forceinline__ uint64_t mix64(uint64_t k) {
     k ^= k >> 33;
     k *= 0xff51afd7ed558ccdULL;
@@ -63,7 +50,6 @@ __device__ __forceinline__ uint64_t mix64(uint64_t k) {
 // walk_queue) a short motif keyed in a finish tile whose window holds the piece is left
 // to that tile's k_tile walk (s2c_tile.hip, the LDS event list): exactly the events it records.
 __device__ void add_event(const ReadsArgs &d, uint64_t gkey, uint64_t q, uint32_t len, uint32_t ws, bool lng) {
-#if S2C_EV_FAST
     // a short motif's codes from its (at most two) plane words, loaded with the tile lookup
     uint64_t c01[3] = {0, 0, 0};   // p0, p1, x of bases q .. q + 63
     if (len <= S2C_SHORT_MOTIF) {
@@ -75,7 +61,6 @@ __device__ void add_event(const ReadsArgs &d, uint64_t gkey, uint64_t q, uint32_
             c01[2] |= (uint64_t)d.bx[wq + h] << (32 * h);
         }
     }
-#endif
     const uint64_t W = gkey >> 5;
     if (W < d.word_lo || W >= d.word_hi) return;   // keyed outside a multi-GPU shard's words
     const uint32_t t = d.wtile[W - d.word_lo];
@@ -89,7 +74,6 @@ __device__ void add_event(const ReadsArgs &d, uint64_t gkey, uint64_t q, uint32_
     const uint32_t pos = (uint32_t)(gkey - tw0.x);   // tile-relative (< 2048)
     if (len <= S2C_SHORT_MOTIF) {
         uint64_t key = (uint64_t)pos | ((uint64_t)len << 11);
-#if S2C_EV_FAST
         const uint32_t sh = (uint32_t)(q & 31);
         for (uint32_t c = 0; c < len; c++) {
             const uint32_t p0 = (uint32_t)(c01[0] >> (sh + c)) & 1u, p1 = (uint32_t)(c01[1] >> (sh + c)) & 1u,
@@ -97,9 +81,6 @@ __device__ void add_event(const ReadsArgs &d, uint64_t gkey, uint64_t q, uint32_
             const uint32_t code = x ? (p0 ? 0u : 4u) : ((p1 << 1 | p0) == 3u ? 5u : (p1 << 1 | p0) + 1u);
             key |= (uint64_t)code << (16 + 3 * c);
         }
-#else
-        for (uint32_t c = 0; c < len; c++) key |= (uint64_t)base_code(d, q + c) << (16 + 3 * c);
-#endif
         const uint32_t boff = tw1.x, bcap = tw1.y;
         uint32_t s = (uint32_t)mix64(key) & (bcap - 1u);
         for (uint32_t probe = 0; probe < bcap; probe++) {   // bcap ≥ 2 × the tile's short events
@@ -164,9 +145,7 @@ __global__ __launch_bounds__(WG) void k_reads(const ReadsArgs d) {
     const uint4 P = ((const uint4 *)d.pc)[i];
     const uint32_t oend = d.pc[4 * (size_t)i + 6];   // next piece's opoff (sentinel at the end)
     const bool runs = d.all || ((P.w >> 24) & S2C_PF_RUNS);
-#if S2C_EV_FAST
     if (!runs && piece_events(d, P, oend)) return;
-#endif
     uint4 *out = (uint4 *)d.runs;
     walk_piece(GlobalMem{d.ops, d.bq, d.bx}, P, oend, d.maxdel_active != 0, d.maxdel,
                [&](uint32_t j, uint32_t g, uint32_t l, uint32_t k, uint64_t q) {

@@ -690,21 +690,12 @@ __device__ __forceinline__ void tile_epilogue_fast(const D &d, uint32_t tile, co
 // word is fetched from HBM once per tile (chunks are disjoint; neighbouring tiles share kwin
 // start words).  Long pieces (span > the window) come from k_reads' run records through
 // the tile's long list.  Then the epilogue (a single-item tile) or the counts to HBM.
-// Walk options (variant builds set them to 0 for A/B; profiles/r05/v8_*):
-//   S2C_PX_LDS     the pieces' px words come with the layer's records (ahead DMA into LDS);
-//                  a walked piece with <= 2 'N' (S2C_PF_XFEW) adds them from px: no HBM scan
-//   S2C_WALK_QUEUE the pieces walked op by op are queued and walked after the others by the
-//                  wave's first lanes (one such walk per lane and layer)
-//   S2C_MAXDEL_1P  without '-' in SEQ the maxdel sum comes from the walk itself
-#ifndef S2C_PX_LDS
-#define S2C_PX_LDS 1
-#endif
-#ifndef S2C_WALK_QUEUE
-#define S2C_WALK_QUEUE 1
-#endif
-#ifndef S2C_MAXDEL_1P
-#define S2C_MAXDEL_1P 1
-#endif
+// The walk (each measured against its alternative in round 5, profiles/r05/v8_*): the pieces'
+// px words come with the layer's records (ahead DMA into LDS), so a walked piece with <= 2 'N'
+// (S2C_PF_XFEW) adds them from px, no HBM scan (≤ 1024-position tiles); in the walk-queue
+// instantiation the pieces walked op by op are queued and walked after the others by the
+// wave's first lanes (one such walk per lane and layer); without '-' in SEQ the maxdel sum
+// comes from the walk itself (one pass).
 
 constexpr int GS = 8;                 // records per counting group
 constexpr int CSEG = S2C_CHUNK_SEGS;  // segments of a window (≤ 64 words + kwin ≤ 32)
@@ -724,7 +715,7 @@ constexpr uint32_t OOR = 0xF0000000u;
 // The non-ACGT words stay in HBM (the few pieces that need them: S2C_PF_XFEW pieces take their
 // 'N' from px).  runl: the run records; segR[σ]: the first run record of the layer's pieces
 // starting in word S0 + σ (pieces are in start-word order).
-// With EXT (S2C_PX_LDS / S2C_WALK_QUEUE, tiles of <= 1024 positions: the 2048-position
+// With EXT (px words in LDS / the walk queue, tiles of <= 1024 positions: the 2048-position
 // instantiation keeps 2 workgroups per CU without them) also the pieces' px words (ahead,
 // like pcb) and the queue of the pieces walked op by op.
 template <bool EXT> struct ChunkExt {};
@@ -769,16 +760,9 @@ __device__ __forceinline__ DmaSrc dma_src(const void *p, const void *end) {
 // Arguments wave-uniform.  Completion: s_waitcnt vmcnt(0) (the compiler does not count these
 // loads): the wave's own LDS reads then see the data.
 // Returns the number of DMA instructions issued (each one vmcnt event).
-// Cache policy of the layer DMA: nontemporal (C3 -3.5 %, profiles/r05/v7_*; variant builds:
-// -DS2C_TILE_DMA_CP=0 the default policy)
-#ifndef S2C_TILE_DMA_CP
-#define S2C_TILE_DMA_CP 1
-#endif
-#if S2C_TILE_DMA_CP == 1
+// Cache policy of the layer DMA: nontemporal (C3 -3.5 % against the default policy,
+// profiles/r05/v7_*)
 #define S2C_TILE_DMA_POLICY " nt"
-#else
-#define S2C_TILE_DMA_POLICY ""
-#endif
 __device__ __forceinline__ uint32_t dma16_wave(uint8_t *dst, const DmaSrc &S, const uint32_t *src, uint32_t n) {
     const uint32_t lane = threadIdx.x & 63;
     const uintptr_t sal = (uintptr_t)src & ~(uintptr_t)15;
@@ -963,14 +947,10 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
     const uint32_t ql = 16u * P.y + qadj;     // SEQ[0] in the LDS planes
     bool drop = false;
     // :210 — D/N/P lengths + '-' chars of the bases taken.  With '-' in SEQ a first pass over
-    // the ops; otherwise (S2C_MAXDEL_1P) the D/N/P lengths are summed by the one pass below,
+    // the ops; otherwise the D/N/P lengths are summed by the one pass below,
     // which holds back the first two deletion runs' '-' counts until the sum is known
-#if S2C_MAXDEL_1P
     const bool defer = maxdel_active && !(fl & S2C_PF_DASH);
     if (maxdel_active && (fl & S2C_PF_DASH)) {
-#else
-    if (maxdel_active) {
-#endif
         uint32_t dashes = 0, start = 0;
         for (uint32_t jj = j; jj < oend; jj++) {
             const uint32_t w = opl[jj + od], op = w & 15u, l = w >> 4;
@@ -995,9 +975,7 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
         }
         drop = dashes > maxdel;
     }
-#if S2C_MAXDEL_1P
     uint32_t dsum = 0, nd = 0, dr0 = 0, dr1 = 0;   // (deferred: '-' runs [c0, c1) - a packed c0 | c1 << 16)
-#endif
     const uint32_t e_tile = a + n;
     uint32_t kk = 0, start = 0;
     for (uint32_t jj = j; jj < oend; jj++) {
@@ -1028,13 +1006,11 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
                             x_fix<NWP, OOL>(bql, xl, xd, q + (c0 - gp), c1 - c0, c0 - a, drop, hist);
                         }
                     }
-#if S2C_MAXDEL_1P
                 } else if (defer && c1 > c0) {
                     const uint32_t pk = (c0 - a) | (c1 - a) << 16;
                     dr1 = nd == 1 ? pk : dr1;
                     dr0 = nd == 0 ? pk : dr0;
                     nd++;
-#endif
                 } else if (!drop && c1 > c0) {
                     atomicAdd(&dD[c0 - a], 1);
                     atomicSub(&dD[c1 - a], 1);
@@ -1042,9 +1018,7 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
             }
             kk += take;
         }
-#if S2C_MAXDEL_1P
         if (op_dash(op)) dsum += l;
-#endif
         if (REC && rec && op == S2C_OP_I) {   // an insertion event (:73-75) keyed in the tile, motif <= 16 bases
             const uint32_t take = start < slen ? min(l, slen - start) : 0u;
             const int64_t gk = key0 + (int64_t)kk;
@@ -1062,7 +1036,6 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
         if (bases || op == S2C_OP_I || op == S2C_OP_S) start += l;
         runl[jj + rd] = r;
     }
-#if S2C_MAXDEL_1P
     if (nd && dsum <= maxdel) {   // (defer: the read keeps its '-')
         atomicAdd(&dD[dr0 & 0xFFFFu], 1);
         atomicSub(&dD[dr0 >> 16], 1);
@@ -1091,12 +1064,8 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
             }
         }
     }
-#endif
 }
 
-#ifndef S2C_TILE_XCD
-#define S2C_TILE_XCD 1
-#endif
 template <int NWP, bool WQB>
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 3 : 2))) void k_tile(const TileArgs d, const uint32_t *items) {
     constexpr int HP = 17 * NWP;
@@ -1109,13 +1078,21 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     __shared__ uint32_t wtot[2][WG / 64];
     // WQB: the launch's batch has pieces walked op by op (s2c_dev n_walked); without them the
     // queue's code costs C3 / C4 4 % (profiles/r05/v9_*), so it is a separate instantiation
-    constexpr bool PXL = S2C_PX_LDS && NWP <= 32, WQ = S2C_WALK_QUEUE && WQB && NWP <= 32;   // (ChunkLds' EXT)
+    constexpr bool PXL = NWP <= 32, WQ = WQB && NWP <= 32;   // (ChunkLds' EXT)
     __shared__ __attribute__((aligned(16))) TileLds<ICOL, PXL || WQ> U;
     // a finish tile's own short-motif insertion events (EvRec; the 2048-position instantiation
     // leaves them to k_reads: its LDS)
     constexpr bool REC = WQB && NWP <= 32;   // (the walk-queue instantiation's LDS has room for the list)
     __shared__ uint2 evl[REC ? S2C_EPI_KEYS : 1];
     __shared__ uint32_t evn;
+    S2C_POISON(hist, sizeof(hist));
+    S2C_POISON(dV, sizeof(dV));
+    S2C_POISON(dD, sizeof(dD));
+    S2C_POISON(wtot, sizeof(wtot));
+    S2C_POISON(&U, sizeof(U));
+    S2C_POISON(evl, sizeof(evl));
+    S2C_POISON(&evn, sizeof(evn));
+    S2C_POISON_DONE();
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
 #ifdef S2C_PROF
     const uint32_t tabl = uni(*(volatile uint32_t *)&g_tabl);
@@ -1124,14 +1101,10 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     unsigned long long tprof_t = 0;
 #endif
     TPROF_MARK(0);
-#if S2C_TILE_XCD
     // XCD-major: the blocks of one XCD (b ≡ x mod 8) take a contiguous range of items, so
     // neighbouring tiles' shared window reads meet in that XCD's L2
     const uint32_t bx8 = blockIdx.x & 7u, per = gridDim.x >> 3, rem = gridDim.x & 7u;
     const uint4 itv = ((const uint4 *)items)[bx8 * per + min(bx8, rem) + (blockIdx.x >> 3)];
-#else
-    const uint4 itv = ((const uint4 *)items)[blockIdx.x];
-#endif
     const uint32_t tile = uni(itv.x), chunk = uni(itv.y), l0 = uni(itv.z), l1 = uni(itv.w);
     const TileRec T = tile_rec(d.tiles, tile);
     const uint32_t nl = uni(d.tiles[(size_t)tile * S2C_TILE_WORDS + 19]);
@@ -1397,11 +1370,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
                 const uint32_t c0 = max(P.x, a), c1 = min(P.x + len, a + n);
                 C.runl[rPre] = len ? rec_enc(P.x - 32u * W0, len, ql) : make_uint2(0u, 0u);
                 if (c1 > c0) {
-#ifndef S2C_ABL_DV   // (timing-only variant: no coverage difference updates)
                     atomicAdd(&dV[c0 - a], 1);
                     atomicSub(&dV[c1 - a], 1);
-#endif
-#ifndef S2C_ABL_X
                     if (PXL && (fl & (S2C_PF_X | S2C_PF_XFEW)) == (S2C_PF_X | S2C_PF_XFEW)) {   // ≤ 2 'N' at SEQ offsets px
 #pragma unroll
                         for (int h = 0; h < 2; h++) {
@@ -1411,7 +1381,6 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
                     } else if ((fl & S2C_PF_X) && !(fl & S2C_PF_XFEW)) {   // (without PXL: S2C_PF_XFEW after the walk)
                         x_fix<NWP, WQ>(bql, xg, 0u, ql + (c0 - P.x), c1 - c0, c0 - a, false, hist);
                     }
-#endif
                 }
             } else if (fl & S2C_PF_LONG) {   // (its runs come through the tile long lists)
                 for (uint32_t j = P.z; j < oe[u]; j++) C.runl[j - O0] = make_uint2(0u, 0u);
@@ -1437,7 +1406,6 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
         if constexpr (REC) {   // the lane's held events keyed from the landed planes (EvOut)
             if (eo.n) ev_flush(bql, xg, 0u, eo, evr);
         }
-#if !defined(S2C_ABL_X)
 #pragma unroll
         for (int u = 0; u < 2 && !PXL; u++) {   // ≤ 2 'N' of an S2C_PF_XFEW piece at its SEQ offsets px: no plane scan
             const uint4 P = Pw[u];
@@ -1451,7 +1419,6 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
                 if (off != 0xFFFFu && p >= c0 && p < c1) H::add1(hist, SL_N, p - a, 1u);
             }
         }
-#endif
         TPROF_MARK(3);
         // ---- 3. the next layer's piece records and op words, under this layer's count
         if (ly + WV < l1) {
@@ -1711,6 +1678,8 @@ struct ConsLds {
 
 __global__ __launch_bounds__(WG) void k_consensus(const TileArgs d, const uint32_t *deep) {
     __shared__ ConsLds L;
+    S2C_POISON(&L, sizeof(L));
+    S2C_POISON_DONE();
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t tile = deep[blockIdx.x];
     const TileRec T = tile_rec(d.tiles, tile);

@@ -133,6 +133,27 @@ class Uploader:
 
 _UPLOADERS = {}
 _SIDE = {}
+_PINNED = {}
+_PINNED_LOCK = __import__("threading").Lock()
+
+
+def to_host_bytes(t):
+    """A device uint8 tensor → bytes, through a pinned staging buffer kept per device (one
+    DMA at the link's rate instead of a pageable copy; the buffer grows by doubling and is
+    reused, so only the first large fetch pays its allocation)."""
+    n = int(t.numel())
+    if n == 0:
+        return b""
+    if t.device.type != "cuda":
+        return t.numpy().tobytes()
+    with _PINNED_LOCK:
+        buf = _PINNED.get(t.device)
+        if buf is None or buf.numel() < n:
+            cap = max(n, 2 * buf.numel() if buf is not None else 0, 1 << 20)
+            buf = _PINNED[t.device] = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
+        buf[:n].copy_(t, non_blocking=True)
+        torch.cuda.current_stream(t.device).synchronize()
+        return buf[:n].numpy().tobytes()
 
 
 def _side_stream(device):
@@ -363,7 +384,32 @@ class Workspace:
             return self._fetch()
 
     def _fetch(self):
+        stats, offs, body = self.fetch_device()
+        return stats, offs, to_host_bytes(body)
+
+    def _body_starts(self):
+        """Device int64 [T·tiles]: each fetched (threshold, tile) body's slot in ``out``,
+        t·(F·padded_len + n_cols) + F·a + cb0 (s2c.h s2c_dev.out), in [t][tile] order."""
+        if getattr(self, "_starts", None) is None:
+            nb = self.db.info.n_tiles
+            t0, t1 = self.tile_range if self.tile_range is not None else (0, nb)
+            blocks = self.db.hb.tiles[t0:t1].astype(np.int64)
+            slot = self.fill_w * blocks[:, 0] + blocks[:, 8]                     # F·a + cb0
+            starts = (np.arange(self.T, dtype=np.int64)[:, None] * self.out_stride + slot[None, :]).reshape(-1)
+            self._starts = _up(starts, self.db.device)
+        return self._starts
+
+    def fetch_device(self):
+        """Results with the FASTA bodies left on the device: (stats[R,T,4] u64, offs[T*nb+1]
+        u64, body) — ``body`` a device uint8 tensor of exactly offs[-1] bytes, the fetched
+        tiles' bodies compacted in [t][tile] order by ``s2c_gather_bodies_dev`` (only the
+        statistics and the body lengths cross to the host here).  The current stream must
+        have the kernels' results (``fetch`` arranges that).
+
+        stats[r, t] = Σ over reference r's tiles of the device's per-tile statistics
+        (tiles never straddle a reference; :352-397 sums)."""
         i = self.db.info
+        dev = self.db.device
         R, T, nb = i.n_refs, self.T, i.n_tiles
         t0, t1 = self.tile_range if self.tile_range is not None else (0, nb)
         stats = np.zeros((R, T, 4), dtype=np.uint64)
@@ -374,22 +420,15 @@ class Workspace:
                 np.add.at(stats[:, t, :], ref, ts[t, t0:t1])
         nr = t1 - t0
         if T * nr == 0:
-            return stats, np.zeros(1, dtype=np.uint64), b""
-        # each tile wrote its body into its slot; the references' bodies are their tiles'
-        # pieces in order: gather them into [t][tile] order (host threads, s2c_gather_bodies)
-        lens = self.blk_len[: T * nb * 8].view(torch.int64).cpu().numpy().astype(np.int64).reshape(T, nb)
-        lens = np.ascontiguousarray(lens[:, t0:t1]).reshape(-1)
-        blocks = self.db.hb.tiles[t0:t1].astype(np.int64)
-        slot = self.fill_w * blocks[:, 0] + blocks[:, 8]                     # F·a + cb0
-        starts = (np.arange(T, dtype=np.int64)[:, None] * self.out_stride + slot[None, :]).reshape(-1)
-        offs = np.zeros(T * nr + 1, dtype=np.int64)
-        np.cumsum(lens, out=offs[1:])
+            return stats, np.zeros(1, dtype=np.uint64), torch.empty(0, dtype=torch.uint8, device=dev)
+        # each tile wrote its body into its slot; a reference's body is its tiles' pieces in
+        # order: the slots compacted into [t][tile] order on the device
+        lens = self.blk_len[: T * nb * 8].view(torch.int64).view(T, nb)[:, t0:t1].reshape(-1)
+        offs_d = torch.zeros(T * nr + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(lens, 0, out=offs_d[1:])
+        offs = offs_d.cpu().numpy()
         total = int(offs[-1])
-        raw = self.out[: T * self.out_stride].cpu().numpy()
-        starts = np.ascontiguousarray(starts, dtype=np.int64)
-        lens = np.ascontiguousarray(lens, dtype=np.int64)
-        out = bytearray(total)
-        buf = (C.c_char * max(total, 1)).from_buffer(out) if total else None
-        L.check(lib.s2c_gather_bodies(raw.ctypes.data, raw.nbytes, starts.ctypes.data, lens.ctypes.data, len(lens),
-                                      C.addressof(buf) if total else None))
-        return stats, offs.astype(np.uint64), bytes(out)
+        body = torch.empty(max(total, 16), dtype=torch.uint8, device=dev)
+        L.check(lib.s2c_gather_bodies_dev(_ptr(self.out), self.out.numel(), _ptr(self._body_starts()), _ptr(offs_d),
+                                          T * nr, _ptr(body), C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+        return stats, offs.astype(np.uint64), body[:total]

@@ -63,21 +63,30 @@ def sub_batch(hb, rank, world):
     return sub
 
 
-def merge_outputs(parts, T):
-    """Rank outputs [(t0, t1, offs, out)] → (offs, out) of the whole batch, [t][tile] order."""
-    parts = sorted(parts, key=lambda p: p[0])
+def merge_plan(parts, T):
+    """Rank results [(t0, t1, offs)] → (offs of the whole batch, segments): the merged body
+    is, in [t][tile] order, the concatenation of part k's bytes [a, b) over the segments
+    (k, a, b) — k indexes ``parts`` as given."""
+    order = sorted(range(len(parts)), key=lambda k: parts[k][0])
     nb = max(p[1] for p in parts) if parts else 0
     lens = np.zeros(T * nb, np.int64)
-    chunks = [[b""] * len(parts) for _ in range(T)]
-    for k, (t0, t1, offs, out) in enumerate(parts):
-        nbr = t1 - t0
-        for t in range(T):
+    segs = []
+    for t in range(T):
+        for k in order:
+            t0, t1, offs = parts[k][:3]
+            nbr = t1 - t0
             a, b = int(offs[t * nbr]), int(offs[t * nbr + nbr])
-            chunks[t][k] = out[a:b]
-            lens[t * nb + t0:t * nb + t1] = np.diff(offs[t * nbr:t * nbr + nbr + 1].astype(np.int64))
+            segs.append((k, a, b))
+            lens[t * nb + t0:t * nb + t1] = np.diff(np.asarray(offs[t * nbr:t * nbr + nbr + 1]).astype(np.int64))
     full = np.zeros(T * nb + 1, np.uint64)
     full[1:] = np.cumsum(lens)
-    return full, b"".join(b"".join(chunks[t]) for t in range(T))
+    return full, segs
+
+
+def merge_outputs(parts, T):
+    """Rank outputs [(t0, t1, offs, out)] → (offs, out) of the whole batch, [t][tile] order."""
+    full, segs = merge_plan(parts, T)
+    return full, b"".join(parts[k][3][a:b] for k, a, b in segs)
 
 
 def force_collectives():
@@ -157,6 +166,81 @@ def gather_results(fetched, sub, rank, world, T, group=None, timing=None):
     full_offs, full_out = merge_outputs(parts, T)
     res = st.cpu().numpy().view(np.uint64).reshape(stats.shape), full_offs, full_out
     mark("merge", t0)
+    return res
+
+
+def gather_device(ws, sub, rank, world, T, group=None, timing=None):
+    """``gather_results`` for a rank whose results are still on its GPU (``Workspace``): the
+    bodies are compacted on the device (``Workspace.fetch_device``, s2c_gather_bodies_dev) and
+    gathered to rank 0 straight from device memory — only the statistics and the body
+    lengths cross to the host before the collectives.  Rank 0 orders the shards' bodies on its
+    device and copies the merged bodies to the host once (pinned).  Collectives: a reduce of
+    the stats, an all-gather of (tile range, sizes), a gather of the padded offsets and of the
+    padded body bytes.  Returns (stats, offs, out) of the whole batch on rank 0, None
+    elsewhere.  ``timing``: this rank's seconds per step (fetch, stats_reduce, meta,
+    body_gather, merge; device work synchronised) and the bytes each step moved."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    from .engine import to_host_bytes
+
+    t0 = time.perf_counter()
+    stats, offs, body = ws.fetch_device()
+    dev = _tensor_device(group)
+
+    def mark(name, t0, nbytes=None):
+        if timing is None:
+            return time.perf_counter()
+        torch.cuda.synchronize(body.device)
+        if dev.type == "cuda" and dev != body.device:
+            torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        timing[name + "_s"] = timing.get(name + "_s", 0.0) + (t1 - t0)
+        if nbytes is not None:
+            timing[name + "_bytes"] = int(nbytes)
+        return t1
+
+    t0 = mark("fetch", t0, body.numel())
+    st = torch.from_numpy(np.ascontiguousarray(stats).view(np.int64).copy()).to(dev)
+    coll = world > 1 or force_collectives()
+    if coll:
+        dist.reduce(st, dst=0, op=dist.ReduceOp.SUM, group=group)   # record stats of cut references
+    t0 = mark("stats_reduce", t0, st.numel() * 8)
+    offs = np.asarray(offs, dtype=np.uint64)
+    meta = torch.tensor([sub.t0, sub.t1, len(offs), int(body.numel())], dtype=torch.int64, device=dev)
+    metas = [torch.empty_like(meta) for _ in range(world)]
+    dist.all_gather(metas, meta, group=group) if coll else metas.__setitem__(0, meta)
+    metas = [m.cpu().tolist() for m in metas]
+    t0 = mark("meta", t0, 32)
+    mo = max(m[2] for m in metas)
+    mb = max(max(m[3] for m in metas), 16)
+    o_t = torch.zeros(mo, dtype=torch.int64, device=dev)
+    o_t[: len(offs)] = torch.from_numpy(offs.view(np.int64).copy()).to(dev)
+    src = body if dev == body.device else body.to(dev)
+    if src.numel() == mb:
+        b_t = src
+    else:   # (the gather moves equal sizes: padded on the device)
+        b_t = torch.empty(mb, dtype=torch.uint8, device=dev)
+        b_t[: src.numel()] = src
+    if coll:
+        os_ = [torch.empty_like(o_t) for _ in range(world)] if rank == 0 else None
+        bs_ = [torch.empty_like(b_t) for _ in range(world)] if rank == 0 else None
+        dist.gather(o_t, os_, dst=0, group=group)
+        dist.gather(b_t, bs_, dst=0, group=group)
+    else:
+        os_, bs_ = [o_t], [b_t]
+    t0 = mark("body_gather", t0, o_t.numel() * 8 + b_t.numel())
+    if rank != 0:
+        return None
+    parts = [(m[0], m[1], o[: m[2]].cpu().numpy().view(np.uint64)) for m, o in zip(metas, os_)]
+    full_offs, segs = merge_plan(parts, T)
+    pieces = [bs_[k][a:b] for k, a, b in segs if b > a]
+    merged = torch.cat(pieces) if pieces else torch.empty(0, dtype=torch.uint8, device=dev)
+    full_out = to_host_bytes(merged)
+    res = st.cpu().numpy().view(np.uint64).reshape(stats.shape), full_offs, full_out
+    mark("merge", t0, len(full_out))
     return res
 
 

@@ -17,7 +17,7 @@
 #   phases:WL             phase clocks of the dense kernel (libs2c_prof.so, scripts/prof_dense.py)
 #   tphases:WL            phase clocks of k_tile (libs2c_prof.so, scripts/prof_tile.py)
 #   rehearse:N            bench --rehearse-shards N (the one-GPU rehearsal of the N-way split)
-#   bench2[:WL]           bench.py as 2 ranks sharing the GPU over gloo (weak default, then --shard)
+#   bench2[:WL]           bench.py --gpus 2 (strong split + weak run), 2 ranks sharing the GPU over gloo
 #   streamrss:WL          whole vs streamed CLI on WL's .sam (scripts/stream_rss.py: time, peak RSS, FASTA sha)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}" || exit 1
@@ -89,16 +89,11 @@ for st in "$@"; do
     rehearse)
       timeout -k 10 600 python -u bench.py --rehearse-shards $arg > gpurun_out/${T}_rehearse_$arg.json 2> gpurun_out/${T}_rehearse_$arg.err \
         || { tail -5 gpurun_out/${T}_rehearse_$arg.err; exit 1; } ;;
-    bench2)   # 2 ranks sharing the one GPU over gloo: bench.py's N > 1 paths (weak default, --shard)
-      for mode in weak shard; do
-        F=""; [ $mode = shard ] && F="--shard"
-        S2C_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-          --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 10 --warmup 3 --workload ${arg:-c5} \
-          --no-cpu-baseline $F > gpurun_out/${T}_bench_2rank_$mode.out 2> gpurun_out/${T}_bench_2rank_$mode.err \
-          || { tail -20 gpurun_out/${T}_bench_2rank_$mode.err; exit 1; }
-        grep '^{' gpurun_out/${T}_bench_2rank_$mode.out | tail -1 > gpurun_out/${T}_bench_2rank_$mode.json   # (gloo prints to stdout too)
-        line gpurun_out/${T}_bench_2rank_$mode.json "2rank-$mode"
-      done ;;
+    bench2)   # bench.py --gpus 2 as the driver runs it (torchrun started as a child), both ranks sharing the GPU over gloo
+      S2C_DIST_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --steps 10 --warmup 3 --workload ${arg:-c5} \
+        --no-cpu-baseline > gpurun_out/${T}_bench_2rank.json 2> gpurun_out/${T}_bench_2rank.err \
+        || { tail -20 gpurun_out/${T}_bench_2rank.err; exit 1; }
+      line gpurun_out/${T}_bench_2rank.json "2rank" ;;
     streamrss)
       timeout -k 10 900 python -u scripts/stream_rss.py $arg > gpurun_out/${T}_stream_rss_$arg.json 2> gpurun_out/${T}_stream_rss_$arg.err \
         || { tail -5 gpurun_out/${T}_stream_rss_$arg.err; exit 1; }

@@ -542,3 +542,80 @@ def test_many_thresholds_on_device_match_reference(idx):
     assert status == c["status"]
     got = {k: hashlib.sha256(v.encode("latin-1")).hexdigest() for k, v in files.items()}
     assert got == {k: v["sha256"] for k, v in c["files"].items()}
+
+
+@pytest.mark.timeout(600)
+def test_bench_two_ranks_strong_split_line():
+    """bench.py --gpus 2 as the driver runs it (no WORLD_SIZE: it starts torchrun as a child):
+    the line says n_gpus 2; its value is the strong position split of C5 — two tile ranges,
+    the shards' bodies gathered to rank 0 from device memory and byte-identical to the
+    reference's file — with the exchange timed; the weak run rides in the same line.  Both
+    ranks share this box's one GPU, so the collectives run over gloo."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, S2C_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--no-cpu-baseline"], env=env, capture_output=True, text=True, timeout=540)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["world_size"] == 2 and d["backend"] == "gloo"
+    assert d["scaling"] == "strong"
+    assert d["parity"] == "byte-identical to reference (1 files, 2 shards)"
+    ex = d["exchange"]
+    for k in ("fetch_ms", "stats_reduce_ms", "meta_ms", "body_gather_ms", "merge_ms", "exchange_ms"):
+        assert ex[k] >= 0.0, k
+    assert ex["body_gather_bytes"] >= 60_000_000   # (C5: 64.4 MB of bodies)
+    w = d["weak"]
+    assert w["scaling"] == "weak" and w["parity"] == "byte-identical to reference (1 files)"
+    assert d["value"] > 0 and w["value"] > 0
+
+
+@pytest.mark.parametrize("ins_frac,ins_max", [(0.05, 12), (0.01, 20)])
+def test_tile_events_and_k_reads_events_agree(tmp_path, ins_frac, ins_max):
+    """Who hashes which insertion event is decided twice — on the host (mark_runs: the
+    tile's walk records the short motifs of its finish tiles, k_reads the rest) and on the
+    device (k_reads' skip test, k_tile's record test).  An event both skipped would be lost
+    silently.  The CLI on workloads with insertions of up to 12 / 20 bases (both planned as
+    a mix: most events recorded by the tiles, some hashed by k_reads — motifs > 16 bases,
+    general tiles), N calls (S2C_PF_XFEW pieces) and events at tile edges, run with the
+    tile-recorded events (the product plan) and with every event hashed by k_reads
+    (S2C_DEBUG_PLAN=1 S2C_NO_TILE_EVENTS=1, its own process: the plan reads it once): both
+    byte-identical to the C restatement."""
+    import json
+    import subprocess
+    import sys
+    from sam2consensus_amd import configs
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sam = str(tmp_path / "ins.sam")
+    configs.synth_write("c2", sam, n_refs=24, ins_frac=ins_frac, ins_max=ins_max, n_rate=0.01)
+    args = ["-c", "0.25,0.5,0.75"]
+    subprocess.run(["make", "-s", "-C", os.path.join(root, "oracle")], check=True)
+    ref = tmp_path / "ref"
+    r = subprocess.run([os.path.join(root, "oracle", "build", "s2c_oracle_mc"), "16", "-i", sam, "-o", str(ref),
+                        "-p", "ins"] + args, capture_output=True, text=True, timeout=300)
+    assert "status: ok" in r.stdout, r.stdout[-500:]
+    want = {fn: open(os.path.join(ref, fn), "rb").read() for fn in os.listdir(ref)}
+    assert want
+    for tag, extra in (("tile", {}), ("reads", {"S2C_DEBUG_PLAN": "1", "S2C_NO_TILE_EVENTS": "1"})):
+        out = tmp_path / tag
+        code = ("import json, sys\nfrom sam2consensus_amd import cli\nfrom sam2consensus_amd.batch import parse_file\n"
+                "i = parse_file(%r, True, 150).info\n"
+                "print(json.dumps([i.tile_events, i.n_rlist, i.n_rlist_run]))\n"
+                "sys.exit(cli.main(%r))\n" % (sam, ["-i", sam, "-o", str(out), "-p", "ins"] + args))
+        env = dict(os.environ, PYTHONPATH=root, **extra)
+        rr = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+        assert rr.returncode == 0, (tag, rr.stderr[-3000:])
+        te, nr, nrun = json.loads(rr.stdout.splitlines()[0])
+        if tag == "tile":   # (a mix: the tiles record most events, k_reads hashes some)
+            assert te == 1 and 0 < nrun < nr, (te, nr, nrun)
+        else:
+            assert te == 0
+        got = {fn: open(os.path.join(out, fn), "rb").read() for fn in os.listdir(out)}
+        assert sorted(got) == sorted(want), tag
+        for fn in want:
+            assert got[fn] == want[fn], (tag, fn, _first_diff(got[fn], want[fn]))

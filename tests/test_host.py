@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     assert declared <= exported, declared - exported
     assert declared == set(_lib.EXPORTS)
     hv = int(re.search(r"#define S2C_ABI_VERSION (\d+)", header).group(1))
-    assert _lib.lib.s2c_abi_version() == _lib.ABI_VERSION == hv == 13
+    assert _lib.lib.s2c_abi_version() == _lib.ABI_VERSION == hv == 14
 
 
 def _model_case(sam, args):
@@ -763,3 +763,44 @@ def test_graft_build_entry():
     m = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(m)
     m.build()
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_bench_launches_ranks_as_child(monkeypatch, capsys):
+    """bench.py --gpus N without WORLD_SIZE (how the driver runs it): torch.distributed.run is
+    started as a child process (N ranks on 127.0.0.1), every line the ranks print goes to
+    stderr except rank 0's JSON line, which is the parent's one stdout line; the parent exits
+    with the child's status."""
+    import sys
+    m = _bench_module()
+    cmd = m.rank_command(8, ["--gpus", "8", "--steps", "3"], 29555)
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
+    assert cmd[cmd.index("--nproc-per-node") + 1] == "8" and cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "3"] and cmd[-5].endswith("bench.py")
+    script = ("import sys\nprint('rank noise')\nprint('{\"metric\": \"m\", \"value\": 1}')\n"
+              "print('more', file=sys.stderr)\nsys.exit(%d)\n")
+    for rc in (0, 3):
+        monkeypatch.setattr(m, "rank_command", lambda n, argv, port, rc=rc: [sys.executable, "-c", script % rc])
+        assert m.spawn_ranks(2, []) == rc
+        out = capsys.readouterr()
+        assert out.out == '{"metric": "m", "value": 1}\n'
+        assert "rank noise" in out.err
+    monkeypatch.setattr(m, "rank_command", lambda n, argv, port: [sys.executable, "-c", "print('no line')"])
+    assert m.spawn_ranks(2, []) == 1   # (no result line: a failure even when every rank exits 0)
+
+
+def test_bench_refuses_world_size_mismatch():
+    """--gpus N must equal the launched world size (a mismatched torchrun would otherwise
+    report the wrong n_gpus): exit 2 before anything imports torch."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True, text=True,
+                       env=dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"), timeout=60)
+    assert r.returncode == 2 and "--gpus 2 but WORLD_SIZE 1" in r.stderr
