@@ -154,6 +154,9 @@ int s2c_layout(int64_t *out, int n);
    walk iteration: ≤ pieces + 128).  Device arrays must be
    readable up to their end rounded up to 16 bytes. */
 #define S2C_DENSE_BYTES(ns, nq) (((4 * (ns) + 30) & ~15) + ((8 * (nq) + 30) & ~15) + ((12 * (ns) + 1024 + 15) & ~15))
+/* the dense kernel's dynamic LDS is at least this: after the count its two waves' counter
+   exchange (8,320 bytes each) reuses the window's LDS — the host's occupancy plan counts it */
+#define S2C_DENSE_MIN_LDS 16640
 #define S2C_DENSE_QW   4096  /* base plane words of a dense tile's window (17-bit query offsets) */
 /* k_tile's LDS chunk (one per wave): one layer of a tile window, contiguous in the layered arrays: its
    piece records, op words, base planes

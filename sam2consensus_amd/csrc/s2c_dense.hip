@@ -1245,6 +1245,7 @@ int s2c_launch_dense(const s2c_dev *dv, hipStream_t st) {
     if (lds <= 0 || lds > S2C_DENSE_LDS || (lds & 15)) return s2c_set_error(S2C_ERR_ARG, "dense_lds outside (0, S2C_DENSE_LDS] or not 16-byte aligned");
     // (the window's LDS doubles as the counters' exchange after the count: at least WPT waves' share)
     // (WPT > 2: the waves' queues may take up to 64·WPT entries past S2C_DENSE_BYTES' share)
+    static_assert(WPT * XCH_WAVE_BYTES == S2C_DENSE_MIN_LDS, "s2c.h S2C_DENSE_MIN_LDS (the host's occupancy plan)");
     a.buf_bytes = (uint32_t)std::max<int64_t>(lds + (WPT > 2 ? 256 * WPT : 0), (int64_t)WPT * XCH_WAVE_BYTES);
     if constexpr (WPT <= 2) {   // (≥ 8 words per wave)
         if (dv->tile_max <= 512) return launch<16>(a, n, st);

@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <pthread.h>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -104,7 +105,10 @@ class WorkerPool {
                 if (!err) err = std::current_exception();
             }
         };
-        std::unique_lock<std::mutex> rl(run_m_, std::try_to_lock);
+        // a run nested in this thread's own run of the pool must not try_lock the mutex it
+        // holds (undefined behaviour): it is told apart by the owner's thread id
+        std::unique_lock<std::mutex> rl;
+        if (owner_.load(std::memory_order_relaxed) != std::this_thread::get_id()) rl = std::unique_lock<std::mutex>(run_m_, std::try_to_lock);
         if (!rl.owns_lock()) {   // busy: threads of its own
             std::vector<std::thread> th;
             for (int t = 1; t < nt; t++) th.emplace_back([&safe, t] { safe(t); });
@@ -114,6 +118,11 @@ class WorkerPool {
             return;
         }
         const std::function<void(int)> job = [&safe](int t) { safe(t); };
+        owner_.store(std::this_thread::get_id(), std::memory_order_relaxed);
+        struct Release {
+            std::atomic<std::thread::id> &o;
+            ~Release() { o.store(std::thread::id(), std::memory_order_relaxed); }
+        } release{owner_};
         {
             std::lock_guard<std::mutex> lk(m_);
             while ((int)n_threads_ < nt - 1) {
@@ -135,18 +144,32 @@ class WorkerPool {
         }
         if (err) std::rethrow_exception(err);
     }
-    // the pool of this process (pools are never destroyed: their threads may outlive main)
+    // the pool of this process (pools are never destroyed: their threads may outlive main).
+    // fork: the registry's mutex is held across the fork (pthread_atfork) and a forked child
+    // forgets the parent's pools (their threads do not exist in it) and makes new ones
     static WorkerPool &get(int which) {
-        static std::mutex gm;
-        static WorkerPool *pools[3] = {nullptr, nullptr, nullptr};
-        static pid_t owner = 0;
-        std::lock_guard<std::mutex> lk(gm);
-        if (owner != getpid()) { pools[0] = pools[1] = pools[2] = nullptr; owner = getpid(); }
-        if (!pools[which]) pools[which] = new WorkerPool();
-        return *pools[which];
+        static std::once_flag once;
+        std::call_once(once, [] {
+            pthread_atfork([] { reg_m().lock(); }, [] { reg_m().unlock(); }, [] {
+                for (auto &q : reg()) q = nullptr;
+                reg_m().unlock();
+            });
+        });
+        std::lock_guard<std::mutex> lk(reg_m());
+        WorkerPool *&q = reg()[which];
+        if (!q) q = new WorkerPool();
+        return *q;
     }
 
   private:
+    static std::mutex &reg_m() {
+        static std::mutex m;
+        return m;
+    }
+    static WorkerPool *(&reg())[3] {
+        static WorkerPool *pools[3] = {nullptr, nullptr, nullptr};
+        return pools;
+    }
     void loop(int t) {
         uint64_t seen = 0;
         std::unique_lock<std::mutex> lk(m_);
@@ -162,6 +185,7 @@ class WorkerPool {
         }
     }
     std::mutex run_m_, m_;
+    std::atomic<std::thread::id> owner_{};   // the thread running the pool's current run
     std::condition_variable go_, done_;
     const std::function<void(int)> *job_ = nullptr;
     uint64_t gen_ = 0;
@@ -2871,7 +2895,10 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     int64_t dense_cap = S2C_DENSE_LDS;
     {
         const int64_t nwp = tile_max <= 512 ? 16 : tile_max <= 1024 ? 32 : 64;
-        const int64_t cap8 = 163840 / 8 - (96 * nwp + 128);   // (the kernel's static LDS)
+        // (the kernel's static LDS; its dynamic LDS is never below S2C_DENSE_MIN_LDS, so for
+        // 2048-position tiles (cap8 14,208 B) 8 tiles per CU cannot reside whatever the windows:
+        // no tile is split for it)
+        const int64_t cap8 = 163840 / 8 - (96 * nwp + 128);
         const int64_t n0 = (int64_t)tiles.size();
         std::vector<int64_t> db(n0, -1);
         const int64_t q0 = std::min(P0, n0), q1 = std::min(P1, n0);   // (the planned tiles only: balanced ranges)
@@ -2885,7 +2912,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
         int64_t nfit = 0, over = 0;
         for (const int64_t x : db)
             if (x >= 0) { nfit++; over += x > cap8; }
-        if (over > 0 && over * 500 <= nfit) {
+        if (over > 0 && over * 500 <= nfit && cap8 >= S2C_DENSE_MIN_LDS) {
             dense_cap = cap8;
             if (tile_force == 0) {
                 std::vector<Tile> split;

@@ -221,10 +221,14 @@ def _sorted_items(blocks, maxdel_active, tile_width, batch_bytes, stats_hook, st
                 raise NotSorted("a read reaches positions already emitted")
             if ref < 0:
                 return ("skip", held)
-            bound = int(hb.ref_off[ref]) + max(pos0, 0)
+            # every later read changes positions >= this bound only: POS clamped to the
+            # reference's last position as the host plan clamps it (a read with no aligned
+            # span may carry a POS past LN, and counts nothing there)
+            bound = int(hb.ref_off[ref]) + min(max(pos0, 0), max(int(hb.ref_len[ref]) - 1, 0))
             NT = int(hb.info.n_tiles)
             t1 = int(np.searchsorted(hb.tiles[:, 1].astype(np.int64), bound, side="right"))
-            assert t1 <= int(hb.info.plan_t1) or t1 <= t_lo, "ranged snapshot plan ends before the batch's bound"
+            if t1 > int(hb.info.plan_t1) and t1 > t_lo:   # (never with the clamp; a tile without a plan
+                raise NotSorted("the batch's bound lies past its snapshot's plan")   # must not run: accumulate)
             if t1 <= t_lo:
                 return ("skip", held)
             gmin = int(hb.tiles[t1, 0]) if t1 < NT else int(hb.info.padded_len)

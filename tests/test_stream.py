@@ -413,3 +413,23 @@ def test_ranged_snapshot_plans_only_the_tiles_a_batch_can_run():
             part.free()
     full.free()
     p.close()
+
+
+@pytest.mark.parametrize("pos", [900, 1000, 5000])
+def test_zero_span_read_past_the_reference_end(pos):
+    """A kept read with no aligned span (a CIGAR of S only) whose POS is past LN (and past
+    the 64-position padding) on a reference that is not the last: the reference counts
+    nothing for it (:206-218) and goes on.  A streamed snapshot taken right after it bounds
+    its final tiles like the host plan does (POS clamped to the reference's last position),
+    never into the next reference's tiles."""
+    sam = "@HD\tVN:1.6\tSO:coordinate\n@SQ\tSN:a\tLN:900\n@SQ\tSN:b\tLN:300\n"
+    rows = [("a", s, "30M", "ACGTA" * 6) for s in range(1, 860, 7)]
+    rows.append(("a", pos, "5S", "ACGTA"))
+    rows += [("b", s, "20M", "TTGCA" * 4) for s in range(1, 280, 9)]
+    for r in rows:
+        sam += "r\t0\t%s\t%d\t60\t%s\t*\t0\t0\t%s\t*\n" % r
+    want = o.run_case(sam, [])
+    assert want["status"] == "ok"
+    for block, batch_bytes in ((1, 1), (37, 64), (97, 300)):
+        res, files = _stream(sam, [], block, batch_bytes)
+        assert files == want["files"], (block, batch_bytes)
