@@ -533,7 +533,7 @@ def rehearse_shards(full, n, thresholds, min_depth, dev, K, W, bases):
     import torch
 
     from sam2consensus_amd import shard
-    from sam2consensus_amd.engine import DeviceBatch, Workspace, to_host_bytes
+    from sam2consensus_amd.engine import DeviceBatch, Workspace, to_host
     ms, fetch_ms, parts, bodies, subs_info, stats = [], [], [], [], [], None
     for r in range(n):
         sub = shard.sub_batch(full, r, n)
@@ -558,12 +558,12 @@ def rehearse_shards(full, n, thresholds, min_depth, dev, K, W, bases):
     vol = shard.exchange_volumes(full, subs_info)
     for sub in subs_info:
         sub.free()
-    to_host_bytes(torch.zeros(sum(b.numel() for b in bodies), dtype=torch.uint8, device=dev))   # (pinned buffer, once per job)
+    to_host(torch.zeros(sum(b.numel() for b in bodies), dtype=torch.uint8, device=dev))   # (pinned buffer, once per job)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     full_offs, segs = shard.merge_plan(parts, len(thresholds))   # rank 0's merge of the gathered bodies
     pieces = [bodies[k][a:b] for k, a, b in segs if b > a]
-    merged = to_host_bytes(torch.cat(pieces)) if pieces else b""
+    merged = to_host(torch.cat(pieces)) if pieces else b""
     merge_ms = (time.perf_counter() - t0) * 1e3
     body = sum(int(b.numel()) + 8 * len(p[2]) for b, p in zip(bodies, parts))
     # rank 0 receives every other rank's bodies over its own xGMI link (≈153 GB/s per link,

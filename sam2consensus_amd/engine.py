@@ -133,27 +133,23 @@ class Uploader:
 
 _UPLOADERS = {}
 _SIDE = {}
-_PINNED = {}
-_PINNED_LOCK = __import__("threading").Lock()
 
 
-def to_host_bytes(t):
-    """A device uint8 tensor → bytes, through a pinned staging buffer kept per device (one
-    DMA at the link's rate instead of a pageable copy; the buffer grows by doubling and is
-    reused, so only the first large fetch pays its allocation)."""
+def to_host(t):
+    """A device uint8 tensor → the host, as a read-only memoryview of a pinned buffer (one DMA
+    at the link's rate; no further copy: a 65 MB bytes object built from it would cost more
+    than the transfer, its fresh pages faulted in by one thread).  The buffer comes from
+    torch's caching host allocator and lives as long as the view; bytes-like everywhere
+    (slicing, ``bytes +``, ``b"".join``, ``==``)."""
     n = int(t.numel())
     if n == 0:
-        return b""
+        return memoryview(b"")
     if t.device.type != "cuda":
-        return t.numpy().tobytes()
-    with _PINNED_LOCK:
-        buf = _PINNED.get(t.device)
-        if buf is None or buf.numel() < n:
-            cap = max(n, 2 * buf.numel() if buf is not None else 0, 1 << 20)
-            buf = _PINNED[t.device] = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
-        buf[:n].copy_(t, non_blocking=True)
-        torch.cuda.current_stream(t.device).synchronize()
-        return buf[:n].numpy().tobytes()
+        return memoryview(t.contiguous().numpy()).toreadonly()
+    buf = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    buf.copy_(t, non_blocking=True)
+    torch.cuda.current_stream(t.device).synchronize()
+    return memoryview(buf.numpy()).toreadonly()
 
 
 def _side_stream(device):
@@ -385,7 +381,7 @@ class Workspace:
 
     def _fetch(self):
         stats, offs, body = self.fetch_device()
-        return stats, offs, to_host_bytes(body)
+        return stats, offs, to_host(body)
 
     def _body_starts(self):
         """Device int64 [T·tiles]: each fetched (threshold, tile) body's slot in ``out``,

@@ -184,7 +184,7 @@ def gather_device(ws, sub, rank, world, T, group=None, timing=None):
     import torch
     import torch.distributed as dist
 
-    from .engine import to_host_bytes
+    from .engine import to_host
 
     t0 = time.perf_counter()
     stats, offs, body = ws.fetch_device()
@@ -238,7 +238,7 @@ def gather_device(ws, sub, rank, world, T, group=None, timing=None):
     full_offs, segs = merge_plan(parts, T)
     pieces = [bs_[k][a:b] for k, a, b in segs if b > a]
     merged = torch.cat(pieces) if pieces else torch.empty(0, dtype=torch.uint8, device=dev)
-    full_out = to_host_bytes(merged)
+    full_out = to_host(merged)
     res = st.cpu().numpy().view(np.uint64).reshape(stats.shape), full_offs, full_out
     mark("merge", t0, len(full_out))
     return res

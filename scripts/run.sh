@@ -16,6 +16,8 @@
 #   pmc:WL                PMC passes of WL (scripts/pmc.sh)
 #   phases:WL             phase clocks of the dense kernel (libs2c_prof.so, scripts/prof_dense.py)
 #   tphases:WL            phase clocks of k_tile (libs2c_prof.so, scripts/prof_tile.py)
+#   valu:WL               VALU per phase of k_tile_dense (prof-build ablations, one PMC pass)
+#   poison                pytest -m gpu on the LDS-poison build (libs2c_poison.so)
 #   rehearse:N            bench --rehearse-shards N (the one-GPU rehearsal of the N-way split)
 #   bench2[:WL]           bench.py --gpus 2 (strong split + weak run), 2 ranks sharing the GPU over gloo
 #   streamrss:WL          whole vs streamed CLI on WL's .sam (scripts/stream_rss.py: time, peak RSS, FASTA sha)
@@ -86,6 +88,17 @@ for st in "$@"; do
       S2C_LIB=libs2c_prof.so timeout -k 10 300 python -u scripts/prof_tile.py $arg > gpurun_out/${T}_tphases_$arg.txt 2>&1 \
         || { tail -9 gpurun_out/${T}_tphases_$arg.txt; exit 1; }
       tail -12 gpurun_out/${T}_tphases_$arg.txt ;;
+    valu)     # VALU per phase of k_tile_dense: prof build ablations under one SQ_INSTS_VALU pass (scripts/valu_phases.py)
+      S2C_LIB=libs2c_prof.so timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES --output-format csv \
+        -d gpurun_out/${T}_valu_$arg -o run -- python3 scripts/prof_dense.py $arg 0,4,2,8,16,32,64 \
+        > gpurun_out/${T}_valu_$arg.log 2>&1 || { tail -9 gpurun_out/${T}_valu_$arg.log; exit 1; }
+      python scripts/valu_phases.py gpurun_out/${T}_valu_$arg 0,4,2,8,16,32,64 > gpurun_out/${T}_valu_$arg.txt 2>&1
+      cat gpurun_out/${T}_valu_$arg.txt ;;
+    poison)   # the GPU suite once on the LDS-poison build (make poison): every kernel's LDS 0xA5 at entry
+      S2C_LIB=libs2c_poison.so timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        > gpurun_out/${T}_pytest_gpu_poison.log 2>&1; rc=$?
+      tail -3 gpurun_out/${T}_pytest_gpu_poison.log
+      [ $rc -eq 0 ] || { grep -E "Error|assert|FAIL" gpurun_out/${T}_pytest_gpu_poison.log | head -30; exit $rc; } ;;
     rehearse)
       timeout -k 10 600 python -u bench.py --rehearse-shards $arg > gpurun_out/${T}_rehearse_$arg.json 2> gpurun_out/${T}_rehearse_$arg.err \
         || { tail -5 gpurun_out/${T}_rehearse_$arg.err; exit 1; } ;;
