@@ -307,15 +307,6 @@ __device__ __forceinline__ void close4(uint32_t (&C)[8], uint32_t t4) {
         t4 = t;
     }
 }
-// one weight-2 carry into plane C[1], rippled into C[2..7]
-__device__ __forceinline__ void close2(uint32_t (&C)[8], uint32_t t2) {
-#pragma unroll
-    for (int b = 1; b < 8; b++) {
-        const uint32_t t = C[b] & t2;
-        C[b] ^= t2;
-        t2 = t;
-    }
-}
 // one weight-8 carry into plane C[3], rippled into C[4..7]
 __device__ __forceinline__ void close8(uint32_t (&C)[8], uint32_t t8) {
 #pragma unroll

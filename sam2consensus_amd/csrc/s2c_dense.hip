@@ -531,9 +531,22 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     uint32_t opw[PFN];   // the pieces' first op words, read together
 #pragma unroll
     for (int u = 0; u < PFN; u++) opw[u] = (tid + WT * u < npc) ? opl[Pc[u].y & 0x1FFFu] : 0u;
-    auto walk_one = [&](uint32_t it, uint3 P, uint32_t w0) {
+    for (uint32_t it = 0; it < nit; it++) {
         const uint32_t k = tid + WT * it;
+        uint3 P = Pc[0];
+        uint32_t w0 = opw[0];
+#pragma unroll
+        for (int u = 1; u < PFN; u++) {   // (the loaded records by a select chain)
+            P.x = it == (uint32_t)u ? Pc[u].x : P.x;
+            P.y = it == (uint32_t)u ? Pc[u].y : P.y;
+            P.z = it == (uint32_t)u ? Pc[u].z : P.z;
+            w0 = it == (uint32_t)u ? opw[u] : w0;
+        }
         const bool in = k < npc;
+        if (it >= (uint32_t)PFN && in) {   // (windows of more than WT·PFN pieces)
+            P = dpc_load(d, v.dpc0 + k);
+            w0 = opl[P.y & 0x1FFFu];
+        }
         const DPiece D = dpc_dec(P.x, P.y);
         const uint32_t pxv = P.z, fl = D.fl, slen = D.slen, j = D.j, nops = D.nops;
         const uint32_t op = w0 & 15u, l = w0 >> 4;
@@ -608,42 +621,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         if (x2) queue[qcap - 1u - nx - mbcnt(bx2)] = j + 2u;
         nx += (uint32_t)__popcll(bx2);
         nslow += (uint32_t)__popcll(bs);
-    };
-#if S2C_EXP_UNROLL
-    // the records loaded with the DMA, one iteration each (compile-time indices), then windows
-    // of more than WT·PFN pieces
-#pragma unroll
-    for (int u = 0; u < PFN; u++)
-        if ((uint32_t)u < nit) walk_one((uint32_t)u, Pc[u], opw[u]);
-    for (uint32_t it = PFN; it < nit; it++) {
-        const uint32_t k = tid + WT * it;
-        uint3 P = make_uint3(0u, 0u, 0u);
-        uint32_t w0 = 0;
-        if (k < npc) {
-            P = dpc_load(d, v.dpc0 + k);
-            w0 = opl[P.y & 0x1FFFu];
-        }
-        walk_one(it, P, w0);
     }
-#else
-    for (uint32_t it = 0; it < nit; it++) {
-        const uint32_t k = tid + WT * it;
-        uint3 P = Pc[0];
-        uint32_t w0 = opw[0];
-#pragma unroll
-        for (int u = 1; u < PFN; u++) {   // (the loaded records by a select chain)
-            P.x = it == (uint32_t)u ? Pc[u].x : P.x;
-            P.y = it == (uint32_t)u ? Pc[u].y : P.y;
-            P.z = it == (uint32_t)u ? Pc[u].z : P.z;
-            w0 = it == (uint32_t)u ? opw[u] : w0;
-        }
-        if (it >= (uint32_t)PFN && k < npc) {   // (windows of more than WT·PFN pieces)
-            P = dpc_load(d, v.dpc0 + k);
-            w0 = opl[P.y & 0x1FFFu];
-        }
-        walk_one(it, P, w0);
-    }
-#endif
     // (the queued work below is this wave's own — its queue, its pieces' run records, atomic
     // byte-counter adds — so its LDS writes completing is enough: the other wave's records are
     // needed only by the count, after the barrier that ends the queued walks)
@@ -703,17 +681,8 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     const uint32_t nrec = cw0 + g < cw1 ? (cw1 - cw0 - g + G - 1) / G : 0u;
     // full groups of 8, then (when the wave's longest lane has 1-4 records left) a group of 4
     const uint32_t nmx = ABL(2) ? 0u : uni(__ockl_wfred_max_u32(nrec));
-#if S2C_EXP_TAIL
-    // full groups of 8, then the wave's last 1-6 records as a tail of 2, 4 or 6 (7: a full group)
-    const uint32_t rem8 = nmx % GSD;
-    const uint32_t ngrp = nmx / GSD + (rem8 == 7u ? 1u : 0u);
-    const uint32_t tail = rem8 == 7u ? 0u : (rem8 + 1u) & ~1u;
-    const bool half = false;
-#else
     const uint32_t ngrp = nmx / GSD + ((nmx % GSD) > 4u ? 1u : 0u);
     const bool half = (nmx % GSD) != 0u && (nmx % GSD) <= 4u;
-    const uint32_t tail = half ? 4u : 0u;
-#endif
     // Group gi reads records cw0 + g + G·(8 gi + u), u < 8, by immediate offsets from one base
     // clamped to the end of the records: every slot past this lane's candidates is a record of
     // a piece starting in a later word (or a zero pad record), so it covers nothing here.
@@ -723,12 +692,11 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     const int16_t wbias = (int16_t)(32 * w + REC_BIAS);     // the word's first position, biased (rec_enc)
     const v2s wpk = (v2s){wbias, wbias};
     const uint2 *bqw = bql + ((32 * w + REC_BIAS) >> 5);    // plane word of query y + wbias, less y >> 5
-    auto load_runs = [&](uint2 (&rv)[GSD], uint32_t gi, auto nl) {
-        constexpr int NL = decltype(nl)::value;   // records read (a tail group: its own)
+    auto load_runs = [&](uint2 (&rv)[GSD], uint32_t gi) {
         // (64-bit loads: two records per ds_read2_b64)
         const unsigned long long *rb = (const unsigned long long *)(runl + min(cw0 + g + G * GSD * gi, rend));
 #pragma unroll
-        for (int u = 0; u < NL; u++) {
+        for (int u = 0; u < GSD; u++) {
             unsigned long long r = rb[G * u];
             asm("" : "+v"(r));   // (kept one 64-bit load: its halves are used as different types)
             rv[u] = make_uint2((uint32_t)r, (uint32_t)(r >> 32));
@@ -736,9 +704,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     };
     // one group's 8 records → Harley–Seal tree of each plane; returns the weight-8 carries
     // NR = 8: returns the weight-8 carries in t8o; NR = 4 (a tail group): the weight-4 carries
-    // NR = 6: the weight-4 carries of records 0-3 in t8o, the weight-2 carries of 4-5 in t2o;
-    // NR = 2: the weight-2 carries in t2o
-    auto count_group = [&](const uint2 (&rv)[GSD], uint32_t (&t8o)[4], uint32_t (&t2o)[4], auto nr) {
+    auto count_group = [&](const uint2 (&rv)[GSD], uint32_t (&t8o)[4], auto nr) {
         constexpr int NR = decltype(nr)::value;
         uint32_t pend[4], t2a[4], t4a[4];
 #pragma unroll
@@ -771,14 +737,13 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
                 csa(t2, C[c][0], C[c][0], pend[c], mk[c]);
                 if ((u & 3) == 1) {
                     t2a[c] = t2;
-                    if constexpr (NR % 4 == 2) t2o[c] = t2;
                     continue;
                 }
                 uint32_t t4;
                 csa(t4, C[c][1], C[c][1], t2a[c], t2);
                 if ((u & 7) == 3) {
                     t4a[c] = t4;
-                    if constexpr (NR == 4 || NR == 6) t8o[c] = t4;
+                    if constexpr (NR == 4) t8o[c] = t4;
                     continue;
                 }
                 csa(t8o[c], C[c][2], C[c][2], t4a[c], t4);
@@ -788,58 +753,37 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     };
     using Full = std::integral_constant<int, 8>;
     using Half = std::integral_constant<int, 4>;
-    uint32_t t2u[4];   // (the weight-2 carries of a tail: unused by full groups)
     // two groups per trip (ping-pong record buffers; the next group's records are read while
     // this group's plane words are in flight), their weight-8 carries closed together
     uint2 ra[GSD], rb2[GSD];
     auto trip = [&](uint32_t gi) -> bool {   // groups gi, gi + 1; false: the last group counted
         uint32_t t8a[4], t8b[4];
-        if (gi + 1 < ngrp) load_runs(rb2, gi + 1, Full{});
-        count_group(ra, t8a, t2u, Full{});
+        if (gi + 1 < ngrp) load_runs(rb2, gi + 1);
+        count_group(ra, t8a, Full{});
         if (gi + 1 >= ngrp) {
 #pragma unroll
             for (int c = 0; c < 4; c++) close8(C[c], t8a[c]);
             return false;
         }
-        if (gi + 2 < ngrp) load_runs(ra, gi + 2, Full{});
-        count_group(rb2, t8b, t2u, Full{});
+        if (gi + 2 < ngrp) load_runs(ra, gi + 2);
+        count_group(rb2, t8b, Full{});
 #pragma unroll
         for (int c = 0; c < 4; c++) close16(C[c], t8a[c], t8b[c]);
         return true;
     };
     if (ngrp) {   // the first trip peeled: its counters start at zero (folded, no initialising moves)
-        load_runs(ra, 0, Full{});
+        load_runs(ra, 0);
         if (trip(0))
             for (uint32_t gi = 2; gi < ngrp; gi += 2)
                 if (!trip(gi)) break;
     }
-    if (tail == 4u) {   // records 8·ngrp .. 8·ngrp + 3 of each lane
+    if (half) {   // records 8·ngrp .. 8·ngrp + 3 of each lane
         uint32_t t4[4];
-        load_runs(ra, ngrp, Half{});
-        count_group(ra, t4, t2u, Half{});
+        load_runs(ra, ngrp);
+        count_group(ra, t4, Half{});
 #pragma unroll
         for (int c = 0; c < 4; c++) close4(C[c], t4[c]);
     }
-#if S2C_EXP_TAIL
-    else if (tail == 2u) {
-        using Two = std::integral_constant<int, 2>;
-        uint32_t t4[4], t2[4];
-        load_runs(ra, ngrp, Two{});
-        count_group(ra, t4, t2, Two{});
-#pragma unroll
-        for (int c = 0; c < 4; c++) close2(C[c], t2[c]);
-    } else if (tail == 6u) {
-        using Six = std::integral_constant<int, 6>;
-        uint32_t t4[4], t2[4];
-        load_runs(ra, ngrp, Six{});
-        count_group(ra, t4, t2, Six{});
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            close4(C[c], t4[c]);
-            close2(C[c], t2[c]);
-        }
-    }
-#endif
     // long pieces over the tile (rare: spans past the window, C5's long deletions): the tile's
     // long list holds their piece indices; the lanes of each word take them one per lane and
     // round and walk each from HBM (parsecigar :64-81 + maxdel :210, walk_piece), keeping the
@@ -931,7 +875,7 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
         uint2 *xp = (uint2 *)(scratch + wv * XCH_WAVE_BYTES);   // this wave's scratch
         uint32_t *vp = (uint32_t *)xp;   // the rows (aliases the planes: read before, in wave order)
         // a lane's count ≤ its record slots + long rounds: planes 0 .. 2·NCH − 1 carry it
-        const uint32_t mxc = 8 * ngrp + tail + ntr;
+        const uint32_t mxc = 8 * ngrp + (half ? 4u : 0u) + ntr;
         const uint32_t npl = 32u - (uint32_t)__builtin_clz(mxc | 1u);
         auto xchg = [&](auto nch_c) {
             constexpr int NCH = decltype(nch_c)::value;   // plane pairs exchanged
@@ -997,14 +941,19 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
     // and of "not called", the largest count m1 and coverage (bytes), in-tile bytes
     uint32_t chr[RPL], fmk[RPL], ncm[RPL], m1b[RPL], cvb[RPL], inb[RPL];
     uint32_t sc = 0;
+    const bool wave_full = uni(n >= 32u * (wv * NWPW + NWPW) ? 1u : 0u) != 0u;   // (uniform)
 #pragma unroll
     for (int rr = 0; rr < RPL; rr++) {
         const uint32_t cA = rA[rr] - rN[rr], cC = rC[rr] - rX[rr];   // 'N' counted as A, SEQ '-' as C
         const uint32_t cv = cA + cC + rG[rr] + rT[rr] + rD[rr] + rN[rr];   // ≤ 255 per byte
         // in-tile positions: p = 32w + 8j + r < n
         // (bytes j < ⌈(n − pr) / 8⌉, at most 4)
-        const int32_t nj = min(max(((int32_t)n - (int32_t)(32 * w + g * RPL + rr) + 7) >> 3, 0), 4);
-        const uint32_t im = (active && nj) ? 0xFFFFFFFFu >> (32 - 8 * nj) : 0u;
+        // (a wave whose words are all inside the tile — every wave of a full tile: all bytes)
+        uint32_t im = 0xFFFFFFFFu;
+        if (!wave_full) {
+            const int32_t nj = min(max(((int32_t)n - (int32_t)(32 * w + g * RPL + rr) + 7) >> 3, 0), 4);
+            im = (active && nj) ? 0xFFFFFFFFu >> (32 - 8 * nj) : 0u;
+        }
         inb[rr] = im;
         cvb[rr] = cv;
         sc = __builtin_amdgcn_udot4(cv & im, 0x01010101u, sc, false);   // Σ cov over the tile (:357)
@@ -1142,9 +1091,21 @@ __device__ __forceinline__ void dense_tile(const DenseArgs &d, const Win &v, con
                         if ((int32_t)(8 * j + b) < (int32_t)nn) dst[8 * j + b] = (uint8_t)(cj[j] >> (8 * b));
             }
         }
-        if (t == 0) sc = wave_sum(sc);
-        // non-'-' and vote-error counts of the wave (≤ 512 each) in one reduction
-        const uint32_t nde = wave_sum(nd | (ne << 16));
+        // one reduction: at t = 0 Σcov (≤ 4·RPL·255 per lane: 17 bits per wave for RPL ≤ 2, 18
+        // for 4) with the non-'-' count (≤ 256·RPL) above it; later thresholds the non-'-'
+        // count alone; the vote-error count (almost always 0 in the whole wave) only when some
+        // lane has one (round 5: two reductions per threshold)
+        uint32_t nde;
+        constexpr uint32_t SCB = RPL <= 2 ? 17u : 18u;
+        static_assert(RPL <= 4, "Σcov and the non-'-' count share 32 bits");
+        if (t == 0) {
+            const uint32_t s2 = wave_sum(sc | (nd << SCB));
+            sc = s2 & ((1u << SCB) - 1u);
+            nde = s2 >> SCB;
+        } else {
+            nde = wave_sum(nd);
+        }
+        if (__ballot(ne != 0u)) nde |= wave_sum(ne) << 16;
         if (lane == 0) {   // this wave's share (by threshold parity: one barrier per threshold)
             stl[t & 1][wv][0] = sc;
             stl[t & 1][wv][1] = nde & 0xFFFFu;

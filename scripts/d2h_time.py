@@ -58,6 +58,19 @@ def main():
     def into_touched_numpy():
         torch.from_numpy(a).copy_(t)
     res["into_touched_numpy_ms"] = best(into_touched_numpy)
+    import mmap
+
+    def into_mmap(flags, huge):
+        def f():
+            mm = mmap.mmap(-1, n, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS | flags)
+            if huge:
+                mm.madvise(mmap.MADV_HUGEPAGE)
+            torch.from_numpy(np.frombuffer(mm, dtype=np.uint8)).copy_(t)
+            return mm
+        return f
+    res["into_mmap_ms"] = best(into_mmap(0, False))
+    res["into_mmap_populate_ms"] = best(into_mmap(mmap.MAP_POPULATE, False))
+    res["into_mmap_huge_ms"] = best(into_mmap(0, True))
     res["cat8_device_ms"] = best(lambda: torch.cat([t[k * (n // 8):(k + 1) * (n // 8)] for k in range(8)]))
     print(json.dumps(res))
 
