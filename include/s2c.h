@@ -452,7 +452,10 @@ typedef struct {
                                   before the first run, left zero by every run */
     uint32_t *ilong;           /* [n_lng][4] long-motif events {pos, len, q lo, q hi} */
     uint32_t *ilong_n;         /* [n_tiles] long-motif events per tile (zero, left zero) */
-    uint32_t *counts;          /* [6][padded_len] counts of deep / general tiles (SoA by symbol) */
+    uint32_t *counts;          /* [6][padded_len] counts of deep / general tiles (SoA by symbol); zero
+                                  before the first s2c_run / s2c_pileup, left zero by s2c_consensus
+                                  (round 6: no zeroing launch per run) — s2c_pileup_counts leaves
+                                  them filled, so zero them again before the next s2c_run */
     uint32_t *ins_cols;        /* [n_cols][6] column counts of general tiles */
     uint8_t  *ins_chr;         /* [T][n_cols] column vote chars of general tiles */
     int64_t   n_cols;

@@ -15,8 +15,9 @@
 //                            hash table (:262-294), the vote for all thresholds, IUPAC,
 //                            min-depth / fill, insertion chars, tile statistics — counts
 //                            never reach HBM; deep / general tiles add / store their counts
-//   k_prep / k_consensus     deep / general tiles: zero their HBM counts, then the same
-//                            insertion layout and vote with HBM columns
+//   k_consensus              deep / general tiles: the same insertion layout and vote with HBM
+//                            columns, then their HBM counts left zero for the next run (k_prep
+//                            zeroes them before the counts-only modes)
 //
 // Everything is integer counting; the single floating-point operation is the reference's
 // `cov_nucs < t*coverage` (:362, :376), evaluated as (double)S < t * (double)cov — built
@@ -1836,6 +1837,10 @@ __global__ __launch_bounds__(WG) void k_consensus(const TileArgs d, const uint32
         }
         __syncthreads();   // acc is rezeroed by the next pass
     }
+    // the tile's HBM counts read for the last time: left zero for the next run, whose deep items
+    // add into them (s2c_dev.counts; round 6 — a k_prep launch zeroed them before every run)
+    for (uint32_t c = 0; c < NSYM; c++)
+        for (uint32_t i = tid; i < n; i += WG) d.counts[(size_t)c * d.padded_len + a + i] = 0u;
 }
 
 inline int hip_check(hipError_t e, const char *what) {
@@ -1969,10 +1974,8 @@ extern "C" int s2c_pileup(const s2c_dev *d, void *stream) {
                                           "windows are needed (s2c_batch_layers_mode(b, 1))");
     hipStream_t s = (hipStream_t)stream;
     const TileArgs a = tile_args(*d);
-    if (d->n_deep > 0) {
-        k_prep<<<(unsigned)d->n_deep, WG, 0, s>>>(a, d->deep);
-        if ((rc = hip_check(hipGetLastError(), "k_prep"))) return rc;
-    }
+    // (the deep tiles' HBM counts are zero: before the first run by the caller, after every
+    // run by s2c_consensus — s2c_dev.counts)
     if (d->n_dense > 0) {
         rc = d->fill_len == 1 ? s2c_launch_dense(d, s) : launch_tiles(a, d->tile_max, d->dense, d->n_dense, s);
         if (rc) return rc;

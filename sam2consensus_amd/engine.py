@@ -83,6 +83,14 @@ class Uploader:
         self.timing["alloc"] += time.perf_counter() - t1
         return i
 
+    def prime(self):
+        """Allocate the whole pinned ring now (the CLI does it on its warm-up thread while the
+        host parses: 4 × 32 MB of page-locked memory is milliseconds of host time each)."""
+        for i, s in enumerate(self.slots):
+            if s is None:
+                self.slots[i] = torch.empty(self.chunk, dtype=torch.uint8, pin_memory=True)
+        return self
+
     def upload(self, arrays):
         """numpy arrays → device uint8 views (each 256-byte aligned, ≥ 16 bytes, zero-padded
         to its 16-byte end), in HBM once the compute stream reaches this point."""
@@ -238,8 +246,9 @@ class Workspace:
             if counts.numel() * counts.element_size() < 6 * i.padded_len * 4:
                 raise ValueError("counts buffer smaller than 6 x padded_len u32")
             self.counts = counts
-        else:
-            self.counts = u8(6 * i.padded_len * 4 if keep_counts else sz.counts)
+        else:   # (zero before the first run; s2c_consensus leaves it zero: s2c_dev.counts)
+            self.counts = z8(6 * i.padded_len * 4 if keep_counts else sz.counts)
+        self._counts_filled = False   # s2c_pileup_counts leaves counts filled: zeroed before a run
         self.ins_cols = u8(sz.ins_cols)
         self.ins_chr = u8(sz.ins_chr)
         self.blk_len = u8(sz.blk_len)
@@ -299,7 +308,13 @@ class Workspace:
         """parsecigar + maxdel per piece → run records; insertion events → hash tables."""
         L.check(lib.s2c_reads(C.byref(self.dev), self.stream_handle()))
 
+    def _counts_ready(self):
+        if self._counts_filled:   # (after the counts-only diagnostic)
+            self.counts.zero_()
+            self._counts_filled = False
+
     def pileup(self):
+        self._counts_ready()
         L.check(lib.s2c_pileup(C.byref(self.dev), self.stream_handle()))
 
     def consensus(self):
@@ -307,6 +322,7 @@ class Workspace:
 
     def run(self):
         """reads → pileup (+ insertion columns, vote, FASTA bodies) → deep tiles (no host sync)."""
+        self._counts_ready()
         L.check(lib.s2c_run(C.byref(self.dev), self.stream_handle()))
 
     def record_done(self):
@@ -357,6 +373,7 @@ class Workspace:
         if not self.keep_counts:
             raise ValueError("pileup_counts needs Workspace(keep_counts=True)")
         L.check(lib.s2c_pileup_counts(C.byref(self.dev), self.stream_handle()))
+        self._counts_filled = True
         return self.counts_host()
 
     def counts_host(self):

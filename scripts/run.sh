@@ -110,7 +110,7 @@ for st in "$@"; do
     streamrss)
       timeout -k 10 900 python -u scripts/stream_rss.py $arg > gpurun_out/${T}_stream_rss_$arg.json 2> gpurun_out/${T}_stream_rss_$arg.err \
         || { tail -5 gpurun_out/${T}_stream_rss_$arg.err; exit 1; }
-      python -c "import json,sys;d=json.load(open(sys.argv[1]));print({k:(d[k]['seconds'],d[k]['peak_rss_mb']) for k in d if k=='whole' or k.startswith('stream')}, d['identical'])" gpurun_out/${T}_stream_rss_$arg.json ;;
+      python -c "import json,sys;d=json.load(open(sys.argv[1]));print({k:(d[k]['seconds'],d[k]['peak_rss_mb']) for k in d if k.startswith('whole') or k.startswith('stream')}, d['identical']);[print(k,d[k]['phases_s']) for k in d if k.startswith('whole')]" gpurun_out/${T}_stream_rss_$arg.json ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done

@@ -299,17 +299,26 @@ def test_cli_failure_writes_nothing(tmp_path):
     assert os.listdir(out) == []
 
 
-def test_repeated_runs_identical():
-    """Workspace reuse (bench steps) gives identical bytes every time (no stale state)."""
+@pytest.mark.parametrize("name,over", [("c2", {"scale": 0.03}), ("c4", {"ref_len": 2000, "depth": 12000.0})])
+def test_repeated_runs_identical(name, over):
+    """Workspace reuse (bench steps) gives identical bytes every time (no stale state): the
+    insertion tables and (round 6) the deep tiles' HBM counts are left zero by every run —
+    no zeroing launch before the next — also after the counts-only diagnostic filled them."""
     from sam2consensus_amd import configs
-    hb = configs.synth_batch("c2", scale=0.03)
-    ws = _ws(hb, [0.25, 0.5, 0.75])
+    hb = configs.synth_batch(name, **over)
+    if name == "c4":
+        assert hb.info.n_deep > 0, "the deep-tile path must run"
+    ws = _ws(hb, [0.25, 0.5, 0.75], keep_counts=(name == "c4"))
     ws.run()
     a = ws.fetch()
-    for _ in range(3):
+    for k in range(3):
+        if k == 1 and name == "c4":
+            ws.pileup_counts()   # (fills the counts; the next run must not add to them)
         ws.run()
         b = ws.fetch()
         assert (a[0] == b[0]).all() and (a[1] == b[1]).all() and a[2] == b[2]
+    if name == "c4":   # and the counts themselves are zero after a run
+        assert int(np.count_nonzero(ws.counts_host())) == 0
 
 
 @pytest.mark.parametrize("name,world", [("c1", 4), ("c2", 3), ("c5", 2), ("c3", 8), ("c4", 8)])
