@@ -162,6 +162,19 @@ class HostBatch:
             lib.s2c_batch_free(self._b)
             self._b = None
 
+    def free_async(self):
+        """Release the host arrays on a side thread (GBs of mappings for a large input: tens
+        of ms of munmap, overlapped with what the caller does next); returns the thread (None
+        when nothing was held).  The handle is detached first, so no second free can race it;
+        this batch's array views must not be read afterwards (as after free())."""
+        b, self._b = self._b, None
+        if not b:
+            return None
+        import threading
+        th = threading.Thread(target=lib.s2c_batch_free, args=(b,), daemon=True)
+        th.start()
+        return th
+
     def __del__(self):
         try:
             self.free()

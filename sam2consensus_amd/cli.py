@@ -49,29 +49,45 @@ def build_parser():
 
 
 class RunResult:
-    def __init__(self, files, timings, info):
+    def __init__(self, files, timings, info, pending=None):
         self.files = files          # {filename: bytes}
         self.timings = timings      # phase → seconds
         self.info = info            # s2c_batch_info
+        self.pending = pending      # the host batch's release, still running (HostBatch.free_async)
+
+    def wait(self):
+        """Join the batch's release (the CLI does, after writing its files)."""
+        if self.pending is not None:
+            self.pending.join()
+            self.pending = None
+        return self
 
 
 def consensus_batch(hb, thresholds, prefix, min_depth=1, fill=b"-", nchar=0, device=None, timings=None):
     """Device pipeline on a parsed HostBatch → {``REF__PREFIX.fasta``: bytes}."""
     import torch
 
-    from .engine import DeviceBatch, Workspace, needs_dense_layers
+    from .engine import _UPLOADERS, DeviceBatch, Workspace, needs_dense_layers
     from .records import build_records, render
 
     t = timings if timings is not None else {}
     t0 = time.perf_counter()
     db = DeviceBatch(hb, device, dense_layers=needs_dense_layers(fill))
+    t1 = time.perf_counter()
     ws = Workspace(db, thresholds, min_depth, fill)
     torch.cuda.synchronize(db.device)
     t["h2d"] = time.perf_counter() - t0
+    t["h2d_issue"] = t1 - t0   # (layers + pinned staging + copies issued; the rest: workspace + drain)
+    up = _UPLOADERS.get(db.device)
+    if up is not None:   # (the pinned ring's cumulative host seconds: alloc, wait, pack, issue)
+        t.update(("h2d_up_" + k, v) for k, v in up.timing.items())
     t0 = time.perf_counter()
     ws.run()
+    torch.cuda.synchronize(db.device)
+    t1 = time.perf_counter()
     stats, offs, out = ws.fetch()
     t["device"] = time.perf_counter() - t0
+    t["device_run"] = t1 - t0   # (the launches to completion; the rest: the results' D2H)
     t0 = time.perf_counter()
     fastas = build_records(hb, thresholds, prefix, stats, offs, out)
     pre = prefix.encode("latin-1") if isinstance(prefix, str) else prefix
@@ -131,25 +147,55 @@ def _log_failed_parse(log, parser):
         log(line)
 
 
-def _warm_device(device):
+def _warm_device(device, reserve=0, timing=None):
     """Start the HIP runtime and the device's context on a side thread (the first device
     call costs tenths of a second) so it overlaps the host parse; join() before the upload.
+    ``reserve`` > 0 (a large input): also allocate the upload's pinned staging ring and a
+    device block of ``reserve`` bytes on its copy stream, released at once into torch's
+    caching allocator, whose next allocation there (the batch's one upload buffer) is then
+    carved from it instead of a fresh hipMalloc (86-90 ms for C5's 1.06 GB on the box).
     A failure here is left to the upload to report."""
     import threading
+
+    t = timing if timing is not None else {}
 
     def run():
         try:
             from . import _lib
             from .engine import _dev
             import torch
+            t0 = time.perf_counter()
             d = _dev(device)
             torch.empty(1, device=d)
             _lib.plan_for_device(d)   # (the plan's grid shaping: this device's CUs, once known)
+            t1 = time.perf_counter()
+            t["warm_context"] = t1 - t0
+            if reserve > 0:
+                from .engine import default_uploader
+                up = default_uploader(d).prime()
+                t2 = time.perf_counter()
+                free, _ = torch.cuda.mem_get_info(d)
+                with torch.cuda.stream(up.copy_stream):
+                    torch.empty(min(int(reserve), free // 2), dtype=torch.uint8, device=d)
+                t["warm_pinned"], t["warm_reserve"] = t2 - t1, time.perf_counter() - t2
         except Exception:  # noqa: BLE001 - reported by DeviceBatch on the main thread
             pass
     th = threading.Thread(target=run, daemon=True)
     th.start()
     return th
+
+
+def upload_estimate(filename):
+    """A device block that holds the packed batch of a large input (0 below 64 MB of input):
+    the batch is ≈ 0.42 of a plain SAM file's bytes on C5 (short reads, qualities dropped,
+    bases in 2-bit planes) — 0.6 × the file (2.4 × a gzip file) leaves room for longer CIGARs."""
+    try:
+        size = os.path.getsize(filename)
+    except OSError:
+        return 0   # (the parser reports the reference's error for a missing file)
+    if size < (64 << 20):
+        return 0
+    return int(size * (2.4 if filename.endswith(".gz") else 0.6))
 
 
 def consensus_files(filename, thresholds, prefix, min_depth=1, fill=b"-", nchar=0, maxdel_active=True,
@@ -160,7 +206,7 @@ def consensus_files(filename, thresholds, prefix, min_depth=1, fill=b"-", nchar=
 
     t = {}
     t0 = time.perf_counter()
-    warm = _warm_device(device)   # (the HIP context comes up while the host parses)
+    warm = _warm_device(device, upload_estimate(filename), t)   # (the HIP context comes up while the host parses)
     p = Parser(maxdel_active, 150)
     try:
         p.feed_file(filename)
@@ -176,7 +222,9 @@ def consensus_files(filename, thresholds, prefix, min_depth=1, fill=b"-", nchar=
     if log:
         _log_summary(log, hb.info)
     files = consensus_batch(hb, thresholds, prefix, min_depth, fill, nchar, device, t)
-    return RunResult(files, t, hb.info)
+    # the batch's host arrays (GBs for a large input: ~60 ms of munmap on the box) released
+    # beside the caller's file writes
+    return RunResult(files, t, hb.info, hb.free_async())
 
 
 def run_text(sam_text, argv, device=None):
@@ -270,6 +318,7 @@ def main(argv=None):
         os.makedirs(outfolder)
     outfolder += "/"
     maxdel_active = not isinstance(args.maxdel, str)
+    res = None
     if rank == 0:
         print("\nProcessing file " + filename + ":\n")
     if world > 1:
@@ -285,8 +334,9 @@ def main(argv=None):
                                              os.fsencode(args.fill), args.n, maxdel_active, log=print,
                                              batch_bytes=sb).files
         else:
-            files = consensus_files(filename, thresholds, os.fsencode(prefix), args.min_depth,
-                                    os.fsencode(args.fill), args.n, maxdel_active, log=lambda s: print(s)).files
+            res = consensus_files(filename, thresholds, os.fsencode(prefix), args.min_depth,
+                                  os.fsencode(args.fill), args.n, maxdel_active, log=lambda s: print(s))
+            files = res.files
     for fname, body in files.items():                                             # :411-424
         path = os.fsencode(outfolder) + fname
         with open(path, "wb") as fh:
@@ -298,6 +348,8 @@ def main(argv=None):
         else:
             print("Consensus sequences at " + ",".join([str(int(i * 100)) + "%" for i in thresholds]) +
                   " saved for " + os.fsdecode(fname[: fname.rfind(b"__")]) + " in: " + shown)
+    if res is not None:
+        res.wait()
     print("Done.\n")
     return 0
 

@@ -457,12 +457,14 @@ __device__ __forceinline__ Rec rec_dec(uint2 v) {
 }
 
 typedef short v2s __attribute__((ext_vector_type(2)));
+typedef unsigned short v2u __attribute__((ext_vector_type(2)));
 // The 32-position word at biased tile-relative position wpk (both halves) of record x: the
 // covered bits' mask (nb bits from l0) and fx = all ones iff all 32 are covered (v_bfm_b32
-// takes widths below 32), from both ends clamped to [0, 32] at once (packed 16-bit).
+// takes widths below 32), from both ends clamped to [0, 32] at once (packed 16-bit: the
+// biased ends and wpk are non-negative, so one saturating unsigned subtract clamps at 0).
 __device__ __forceinline__ void rec_mask(uint32_t x, v2s wpk, uint32_t &m, uint32_t &fx) {
-    const v2s t = __builtin_elementwise_min(__builtin_elementwise_max(__builtin_bit_cast(v2s, x) - wpk, (v2s){0, 0}),
-                                            (v2s){32, 32});
+    const v2u t = __builtin_elementwise_min(
+        __builtin_elementwise_sub_sat(__builtin_bit_cast(v2u, x), __builtin_bit_cast(v2u, wpk)), (v2u){32, 32});
     const uint32_t tc = __builtin_bit_cast(uint32_t, t);
     uint32_t nb;   // e - l0 (one SDWA subtract of the halves)
     asm("v_sub_u32_sdwa %0, %1, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0"

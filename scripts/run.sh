@@ -9,7 +9,7 @@
 #   quick                 pytest -m gpu on the dense-path subset
 #   bench:WL              bench line of workload WL (device step; no CPU legs)
 #   default               the default `python bench.py` (the driver's line, CPU legs included)
-#   ab:WL                 A/B of LIBS="libs2c.so libs2c_x.so ..." on WL, two alternating rounds
+#   ab:WL                 A/B of LIBS="libs2c.so libs2c_x.so ..." on WL, two rounds (the second in reverse order)
 #   abenv:WL              A/B of libs2c.so without / with the environment ENVB (e.g. "S2C_NO_TILE_EVENTS=1")
 #   prof:WL               rocprofv3 --kernel-trace --stats of WL's bench line
 #   profdefault           rocprofv3 --kernel-trace --stats of the default bench line
@@ -56,7 +56,8 @@ for st in "$@"; do
       line gpurun_out/${T}_default_bench.json default ;;
     ab)
       for k in 1 2; do
-        for lib in ${LIBS:-libs2c.so}; do
+        L=${LIBS:-libs2c.so}; [ $k = 2 ] && L=$(echo $L | tr ' ' '\n' | tac | tr '\n' ' ')   # (second round in reverse order: the first run of a pair measured ~1-3 % faster)
+        for lib in $L; do
           S2C_LIB=$lib timeout -k 10 300 python -u bench.py --workload $arg --steps 20 --warmup 3 $NB \
             > gpurun_out/${T}_${arg}_${lib}_$k.json 2> gpurun_out/${T}_${arg}_${lib}_$k.err || { tail -5 gpurun_out/${T}_${arg}_${lib}_$k.err; exit 1; }
           line gpurun_out/${T}_${arg}_${lib}_$k.json "$arg $lib $k"
@@ -64,7 +65,8 @@ for st in "$@"; do
       done ;;
     abenv)
       for k in 1 2; do
-        for v in base env; do
+        VS="base env"; [ $k = 2 ] && VS="env base"
+        for v in $VS; do
           E=""; [ $v = env ] && E="$ENVB"
           env $E timeout -k 10 300 python -u bench.py --workload $arg --steps 20 --warmup 3 $NB \
             > gpurun_out/${T}_${arg}_${v}_$k.json 2> gpurun_out/${T}_${arg}_${v}_$k.err || { tail -5 gpurun_out/${T}_${arg}_${v}_$k.err; exit 1; }

@@ -1,6 +1,8 @@
 """Host memory of the whole-batch path vs streamed batches (stream.py) on one config's
 coordinate-sorted SAM file: each mode runs in its own child process (peak RSS from
-getrusage), and the FASTA bytes of both must agree.
+getrusage), and the FASTA bytes of both must agree.  `seconds` is the CLI's work: parse,
+device, records, the FASTA files written (round 6: the writes and the whole batch's host
+release are included; earlier rounds' figures stop before the writes).
 
     python scripts/stream_rss.py c5 [batch_MB] > gpurun_out/stream_rss_c5.json
 """
@@ -26,13 +28,26 @@ def child(mode, path, name, batch_mb):
     thr = [float(x) for x in a.thresholds.split(",")]
     prefix = os.path.basename(path).split(".")[0].encode()
     common = (thr, prefix, a.min_depth, a.fill.encode(), a.n, not isinstance(a.maxdel, str))
+    if os.environ.get("E2E_NO_RESERVE"):   # (A/B: the CLI's warm-up thread without the upload reservation)
+        import sam2consensus_amd.cli as cli
+        warm = cli._warm_device
+        cli._warm_device = lambda device, reserve=0, timing=None: warm(device, 0, timing)
     t0 = time.perf_counter()
     if mode == "whole":
         r = consensus_files(path, *common)
     else:
         batch_mb = int(os.environ.get("STREAM_BATCH_MB", batch_mb))
         r = consensus_files_streamed(path, *common, batch_bytes=batch_mb << 20)
-    dt = time.perf_counter() - t0
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as od:   # (the CLI's file writes)
+        t1 = time.perf_counter()
+        for k, body in r.files.items():
+            with open(os.path.join(os.fsencode(od), k), "wb") as fh:
+                fh.write(body)
+        r.timings["write"] = time.perf_counter() - t1
+        if hasattr(r, "wait"):
+            r.wait()   # (the whole batch's release, overlapped with the writes)
+        r.timings["write_and_free"] = time.perf_counter() - t1
+        dt = time.perf_counter() - t0
     h = hashlib.sha256()
     for k in sorted(r.files):
         h.update(k)
@@ -61,8 +76,17 @@ def main():
         # STREAM_VARIANTS="A=1,B=2;A=4": more streamed runs of the same file, each with those
         # environment settings (keys "stream:A=1,B=2", ...)
         runs = [("whole", {}), ("stream", {})]
+        if os.environ.get("STREAM_WHOLE_ONLY"):   # (the whole-file CLI only, twice: box-to-box spread)
+            runs = [("whole", {}), ("whole:E2E_NO_RESERVE=1", {"E2E_NO_RESERVE": "1"}), ("whole:again", {}),
+                    ("whole:E2E_NO_RESERVE=1,again", {"E2E_NO_RESERVE": "1"})]
         for v in filter(None, os.environ.get("STREAM_VARIANTS", "").split(";")):
             runs.append(("stream:" + v, dict(kv.split("=", 1) for kv in v.split(","))))
+        # WHOLE_VARIANTS="A=1;A=2": whole-file runs with those settings, the set twice in turn
+        # (with a plain run in each turn; keys "whole:A=1#1", ...)
+        wv = list(filter(None, os.environ.get("WHOLE_VARIANTS", "").split(";")))
+        if wv:
+            runs = [(("whole:%s#%d" % (v, k)) if v else "whole" if k == 1 else "whole:#2",
+                     dict(kv.split("=", 1) for kv in v.split(",")) if v else {}) for k in (1, 2) for v in [""] + wv]
         for key, env in runs:
             mode = key.split(":")[0]
             out = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", mode, path, name,
