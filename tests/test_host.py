@@ -765,6 +765,36 @@ def test_graft_build_entry():
     m.build()
 
 
+def test_cli_upload_reservation_estimate(tmp_path):
+    """The whole-file CLI's warm-up reservation (cli.upload_estimate): nothing below 64 MB of
+    input or for a missing file (the parser raises the reference's error), 0.6 × a plain file,
+    2.4 × a gzip one — above the packed batch of each (C5: 0.42 × its .sam)."""
+    from sam2consensus_amd import cli
+    assert cli.upload_estimate(str(tmp_path / "missing.sam")) == 0
+    small = tmp_path / "s.sam"
+    small.write_bytes(b"@HD\tVN:1.0\n")
+    assert cli.upload_estimate(str(small)) == 0
+    for name, f in (("big.sam", 0.6), ("big.sam.gz", 2.4)):
+        p = tmp_path / name
+        with open(p, "wb") as fh:
+            fh.truncate(100 << 20)   # (sparse: no 100 MB written)
+        assert cli.upload_estimate(str(p)) == int((100 << 20) * f)
+
+
+def test_host_batch_release_on_a_side_thread():
+    """HostBatch.free_async detaches the handle before its thread frees it: free() and the
+    destructor after it are no-ops (no double free), and a second call returns None."""
+    from sam2consensus_amd.batch import parse_text
+    sam = "@SQ\tSN:r\tLN:40\nq\t0\tr\t1\t60\t10M\t*\t0\t0\tACGTACGTAC\t*\n"
+    hb = parse_text(sam, True, 150)
+    th = hb.free_async()
+    assert th is not None
+    th.join()
+    assert hb.free_async() is None
+    hb.free()
+    del hb
+
+
 def _bench_module():
     import importlib.util
     spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
