@@ -130,8 +130,11 @@ __device__ __forceinline__ void walk_window(const uint32_t *opl, const uint2 *bq
     }
     const uint32_t bkind = S2C_RUN_BASES | ((fl & S2C_PF_X) ? S2C_RUN_XBIT : 0u) | (drop ? S2C_RUN_DROP : 0u);
     uint32_t k = 0, start = 0;
+    // the next op word read ahead of run()'s LDS writes (which the compiler must assume alias it)
+    uint32_t wn = j < j1 ? opl[j] : 0u;
     for (; j < j1; j++) {
-        const uint32_t w = opl[j], op = w & 15u, l = w >> 4;
+        const uint32_t w = wn, op = w & 15u, l = w >> 4;
+        wn = opl[min(j + 1u, j1 - 1u)];
         uint32_t rg = 0, rl = 0, rk = S2C_RUN_EMPTY, rq = 0;
         const bool bases = op_bases(op);
         if (bases || op_dash(op)) {

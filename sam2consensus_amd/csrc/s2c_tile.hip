@@ -979,8 +979,12 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
     uint32_t dsum = 0, nd = 0, dr0 = 0, dr1 = 0;   // (deferred: '-' runs [c0, c1) - a packed c0 | c1 << 16)
     const uint32_t e_tile = a + n;
     uint32_t kk = 0, start = 0;
+    // the next op word is read ahead of this op's LDS writes (records, atomics), which the
+    // compiler must otherwise assume may alias it: one LDS round trip per piece, not per op
+    uint32_t wn = j < oend ? opl[j + od] : 0u;
     for (uint32_t jj = j; jj < oend; jj++) {
-        const uint32_t w = opl[jj + od], op = w & 15u, l = w >> 4;
+        const uint32_t w = wn, op = w & 15u, l = w >> 4;
+        wn = opl[min(jj + 1u, oend - 1u) + od];
         uint2 r = make_uint2(0u, 0u);
         const bool bases = op_bases(op);
         if (bases || op_dash(op)) {
