@@ -1071,6 +1071,93 @@ __device__ void walk_chunk_piece(const uint4 P, uint32_t oend, const uint32_t *o
     }
 }
 
+// Exclusive prefix sum and total over the 4 lanes of a lane group (lane & 3 = sub) by DPP
+// quad permutes (no LDS round trip); every lane of the wave takes part.
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_perm(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t xscan4(uint32_t x, uint32_t sub) {
+    // (each permute taken by every lane, then selected: a permute inside the select could be
+    // predicated to the selecting lanes, leaving its source lanes off)
+    const uint32_t t1 = quad_perm<0x90>(x);   // [0,0,1,2]: lane i − 1's
+    uint32_t v = x + (sub >= 1u ? t1 : 0u);
+    const uint32_t t2 = quad_perm<0x44>(v);   // [0,1,0,1]: lane i − 2's
+    v += sub >= 2u ? t2 : 0u;
+    return v - x;
+}
+__device__ __forceinline__ uint32_t sum4(uint32_t x) {
+    x += quad_perm<0xB1>(x);      // [1,0,3,2]
+    return x + quad_perm<0x4E>(x);   // [2,3,0,1]
+}
+
+// walk_chunk_piece for a piece of at most 4 op words (after its insertion-key prefix), walked
+// by the 4 lanes of a group, one op word each (the walk-queue instantiation: C2's indel reads
+// are 3-op pieces).  The serial walk's running values come from two group scans — the query
+// offset `start` over the query-consuming ops, then the seqout offset `kk` over the taken
+// lengths, which depend on `start` (a base op takes min(l, len(SEQ) − start), :64-69) — and
+// the read's D/N/P total (:210) from a group sum, so each op's run, coverage, '-' run and
+// insertion event are the serial walk's.  No shard range (ka = 0, kb = ∞) and no '-' in SEQ
+// (drop = false; the maxdel rule then keeps the '-' runs iff their total ≤ maxdel, as the
+// serial walk's deferred runs do).  `mine`: this lane holds op word jj of such a piece.
+template <int NWP, bool PXL, bool OOL, bool REC>
+__device__ __forceinline__ void walk_op_coop(const uint4 P, bool mine, uint32_t jj, uint32_t sub, const uint32_t *opl,
+                                             uint32_t od, uint2 *runl, uint32_t rd, const uint2 *bql, gptr_u32 xl,
+                                             uint32_t xd, uint32_t qadj, bool maxdel_active, uint32_t maxdel, uint32_t a,
+                                             uint32_t n, uint32_t *hist, int32_t *dV, int32_t *dD, uint32_t pxw,
+                                             int64_t key0, uint32_t roff, bool rec, const EvRec &ev, EvOut &eo) {
+    const uint32_t fl = P.w >> 24, slen = P.w & 0xFFFFFFu;
+    const uint32_t w = mine ? opl[jj + od] : 0u, op = w & 15u, l = w >> 4;
+    const bool bases = mine && op_bases(op), dash = mine && op_dash(op);
+    const bool qop = bases || (mine && (op == S2C_OP_I || op == S2C_OP_S));
+    const uint32_t start = xscan4(qop ? l : 0u, sub);
+    const uint32_t take = bases ? (start < slen ? min(l, slen - start) : 0u) : (dash ? l : 0u);
+    const uint32_t kk = xscan4(take, sub);
+    const uint32_t dsum = sum4(dash ? l : 0u);
+    if (!mine) return;
+    const uint32_t ql = 16u * P.y + qadj;   // SEQ[0] in the LDS planes
+    const uint32_t e_tile = a + n;
+    uint2 r = make_uint2(0u, 0u);
+    if (take) {
+        const uint32_t gp = P.x + kk;
+        const uint32_t c0 = max(gp, a), c1 = min(gp + take, e_tile);   // the tile's part
+        if (bases) {
+            const uint32_t q = ql + start;
+            r = rec_enc(gp - (a & ~31u), take, q);
+            if (c1 > c0) {
+                atomicAdd(&dV[c0 - a], 1);
+                atomicSub(&dV[c1 - a], 1);
+                if (PXL && (fl & (S2C_PF_X | S2C_PF_XFEW)) == (S2C_PF_X | S2C_PF_XFEW)) {
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const uint32_t off = (pxw >> (16 * h)) & 0xFFFFu, p = gp + (off - start);   // (0xFFFF: none)
+                        if (off != 0xFFFFu && off - start < take && p >= c0 && p < c1) Hist<NWP>::add1(hist, SL_N, p - a, 1u);
+                    }
+                } else if (fl & S2C_PF_X) {
+                    x_fix<NWP, OOL>(bql, xl, xd, q + (c0 - gp), c1 - c0, c0 - a, false, hist);
+                }
+            }
+        } else if (c1 > c0 && !(maxdel_active && dsum > maxdel)) {
+            atomicAdd(&dD[c0 - a], 1);
+            atomicSub(&dD[c1 - a], 1);
+        }
+    }
+    if (REC && rec && op == S2C_OP_I) {   // an insertion event (:73-75) keyed in the tile, motif <= 16 bases
+        const uint32_t ti = start < slen ? min(l, slen - start) : 0u;
+        const int64_t gk = key0 + (int64_t)kk;
+        if (ti && ti <= S2C_SHORT_MOTIF && gk >= (int64_t)roff && gk >= (int64_t)a && gk < (int64_t)e_tile) {
+            if (eo.n == 2) {   // (a lane's third held event: the planes now)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                ev_flush(bql, xl, xd, eo, ev);
+            }
+            const uint32_t tq = (uint32_t)(gk - (int64_t)a) | ti << 11 | ((fl & S2C_PF_X) ? 1u << 16 : 0u);
+            if (eo.n == 0) { eo.q0 = ql + start; eo.t0 = tq; } else { eo.q1 = ql + start; eo.t1 = tq; }
+            eo.n++;
+        }
+    }
+    runl[jj + rd] = r;
+}
+
 template <int NWP, bool WQB>
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 3 : 2))) void k_tile(const TileArgs d, const uint32_t *items) {
     constexpr int HP = 17 * NWP;
@@ -1397,11 +1484,46 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
         TPROF_MARK(11);    // (the one-token pieces; MARK(9) below: the op walks)
         if constexpr (WQ) {
             if (nwq) wave_lds_sync();   // (the queue)
-            for (uint32_t k = lane; k < nwq; k += 64) {
+            // 16 queued pieces per pass, 4 lanes each: a piece of ≤ 4 op words (no shard range,
+            // no '-' in SEQ) one op word per lane (walk_op_coop); any other by its group's first lane
+            constexpr bool COOP = NWP >= 16;   // (k_tile<8, true>: the serial walks only; the cooperative one spills there)
+            const uint32_t sub = lane & 3u;
+            bool serial = !COOP;   // (uniform) some queued piece takes the serial walk
+            for (uint32_t kb = 0; kb < (COOP ? nwq : 0u); kb += 16) {
+                const uint32_t k = kb + (lane >> 2);
+                const bool have = k < nwq;
+                const uint32_t i = have ? (uint32_t)C.wq[k] : 0u;
+                const uint4 P = have ? pcr[i] : make_uint4(0u, 0u, 0u, 0u);
+                const uint32_t oend = have ? (i + 1 < NPc ? pcr[i + 1].z : O1) : 0u;
+                const uint32_t fl = P.w >> 24;
+                const bool ins = (fl & S2C_PF_INS) != 0u;
+                const uint32_t j0 = P.z + (ins ? 3u : 0u);
+                const bool coop = have && !(fl & (S2C_PF_RANGE | S2C_PF_DASH)) && oend - j0 <= 4u;
+                const uint32_t pxw = have && PXL ? pxl[i] : 0xFFFFFFFFu;
+                serial = serial || __ballot(have && !coop) != 0ull;
+                if (__ballot(coop)) {
+                    const bool rec = REC && evr.on && coop && ins;
+                    int64_t key0 = 0;
+                    uint32_t roff = 0;
+                    if (rec) {
+                        key0 = (int64_t)((uint64_t)opl[P.z + od] | ((uint64_t)opl[P.z + 1 + od] << 32));
+                        roff = opl[P.z + 2 + od];
+                    }
+                    if (coop && ins && sub < 3u) C.runl[P.z + sub - O0] = make_uint2(0u, 0u);   // (the key words' slots)
+                    walk_op_coop<NWP, PXL, WQ, REC>(P, coop && sub < oend - j0, j0 + sub, sub, opl, od, C.runl, 0u - O0, bql, xg,
+                                                    0u, qadj, d.maxdel_active != 0, (uint32_t)d.maxdel, a, n, hist, dV, dD,
+                                                    pxw, key0, roff, rec, evr, eo);
+                }
+            }
+            // the other queued pieces (rare): one lane each, the serial walk
+            for (uint32_t k = lane; k < (serial ? nwq : 0u); k += 64) {
                 const uint32_t i = C.wq[k];
-                const uint32_t oend = i + 1 < NPc ? pcr[i + 1].z : O1;
-                walk_chunk_piece<NWP, PXL, WQ, REC>(pcr[i], oend, opl, od, C.runl, 0u - O0, bql, xg, 0u, qadj, d.maxdel_active != 0,
-                                           (uint32_t)d.maxdel, a, n, hist, dV, dD, PXL ? pxl[i] : 0xFFFFFFFFu, evr, eo);
+                const uint4 P = pcr[i];
+                const uint32_t oend = i + 1 < NPc ? pcr[i + 1].z : O1, fl = P.w >> 24;
+                const bool coop = COOP && !(fl & (S2C_PF_RANGE | S2C_PF_DASH)) && oend - (P.z + ((fl & S2C_PF_INS) ? 3u : 0u)) <= 4u;
+                if (!coop)
+                    walk_chunk_piece<NWP, PXL, WQ, REC>(P, oend, opl, od, C.runl, 0u - O0, bql, xg, 0u, qadj, d.maxdel_active != 0,
+                                               (uint32_t)d.maxdel, a, n, hist, dV, dD, PXL ? pxl[i] : 0xFFFFFFFFu, evr, eo);
             }
         }
         wave_lds_sync();   // every run record written; the piece records and op words read
