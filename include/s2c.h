@@ -166,6 +166,13 @@ int s2c_layout(int64_t *out, int n);
    word are <= S2C_ITEM_RECS (its u16 histogram). */
 #define S2C_CHUNK_PIECES     128
 #define S2C_CHUNK_QBYTES    4096
+/* a layer's base-plane bytes in k_tile<nwp, wq> (nwp: the tile's 32-position words, wq: the
+   walk-queue instantiation, s2c_batch_info walk_queue as planned): 4,320 for the non-queue
+   instantiations of tiles of <= 512 positions (C3 -2.7 %, C4 -3.3 % against 4,096: fewer
+   layers, each one's DMA round trips and barriers saved; 4,608 measured no better), the base
+   for the others (k_tile<16, walk queue> has no LDS left under 53,536 bytes, the largest share
+   measured to keep 3 workgroups per CU).  The non-ACGT words of a layer <= half of it. */
+#define S2C_CHUNK_QBYTES_OF(nwp, wq) ((nwp) <= 16 && !(wq) ? 4320 : S2C_CHUNK_QBYTES)
 #define S2C_CHUNK_XBYTES    2048
 #define S2C_CHUNK_OBYTES    1024
 #define S2C_CHUNK_RECS       192

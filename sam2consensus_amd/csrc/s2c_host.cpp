@@ -1568,7 +1568,9 @@ static void mark_runs(s2c_batch *b) {
             need[lo] = 1;
         }
     }
-    b->info.walk_queue = walk_queue_of(b->info);
+    // (the layers were cut for the instantiation planned, I.walk_queue: a shard whose parent
+    // was planned for the non-queue one keeps it, whose chunk holds more plane bytes)
+    b->info.walk_queue = walk_queue_of(b->info) && b->info.walk_queue ? 1 : 0;
     static const bool no_tile_events = plan_env("S2C_NO_TILE_EVENTS") != nullptr;   // (A/B: k_reads hashes every event)
     b->info.tile_events = b->info.walk_queue && !no_tile_events ? 1 : 0;
     const bool rec = b->info.tile_events != 0;
@@ -1671,8 +1673,11 @@ static void tile_cuts(const std::vector<LayerSeg> &seg, uint64_t nl, std::vector
     for (size_t i = 0; i < seg.size(); i++) layer_cuts(seg[i], nl, &cuts[i * (nl + 1)]);
 }
 
+// a layer's plane bytes in k_tile<nwp, wq>'s chunk, nwp = 64 / G (s2c.h S2C_CHUNK_QBYTES_OF)
+static inline uint64_t chunk_qbytes(int64_t G, int64_t wq) { return S2C_CHUNK_QBYTES_OF(64 / std::max<int64_t>(G, 1), wq); }
+
 static bool layer_fits(const PieceBlocks &B, size_t NS, const std::vector<uint64_t> &cuts, int64_t S0, int64_t W0,
-                       int64_t W1, int64_t K, int64_t G, uint64_t l, uint64_t nl, std::vector<int64_t> &recs) {
+                       int64_t W1, int64_t K, int64_t G, int64_t wq, uint64_t l, uint64_t nl, std::vector<int64_t> &recs) {
     uint64_t np = 0, nh = 0, rc = 0;
     for (size_t i = 0; i < NS; i++) {
         const uint64_t lo = cuts[i * (nl + 1) + l], hi = cuts[i * (nl + 1) + l + 1];
@@ -1682,7 +1687,8 @@ static bool layer_fits(const PieceBlocks &B, size_t NS, const std::vector<uint64
         rc += (uint64_t)recs[i];
     }
     // (planes: 8 B per 2 half-words, + the funnel word, rounded to 16 B; non-ACGT: half)
-    if (np > S2C_CHUNK_PIECES || 4 * nh + 32 > S2C_CHUNK_QBYTES || 2 * nh + 32 > S2C_CHUNK_XBYTES ||
+    const uint64_t qb = chunk_qbytes(G, wq);
+    if (np > S2C_CHUNK_PIECES || 4 * nh + 32 > qb || 2 * nh + 32 > qb / 2 ||
         4 * rc + 32 > S2C_CHUNK_OBYTES || rc > S2C_CHUNK_RECS)
         return false;
     for (int64_t W = W0; W < W1; W++) {
@@ -1694,7 +1700,7 @@ static bool layer_fits(const PieceBlocks &B, size_t NS, const std::vector<uint64
 }
 
 // nl of tile [a, e) (0: a layer cannot fit, i.e. one piece alone exceeds the chunk)
-static int64_t plan_layers(const s2c_batch *b, const PieceBlocks &B, int64_t K, uint64_t a, uint64_t e, int64_t G) {
+static int64_t plan_layers(const s2c_batch *b, const PieceBlocks &B, int64_t K, uint64_t a, uint64_t e, int64_t G, int64_t wq) {
     const int64_t W0 = (int64_t)(a >> 5), W1 = (int64_t)((e + 31) >> 5), S0 = std::max<int64_t>(W0 - K, 0);
     std::vector<LayerSeg> seg;
     uint64_t tp = 0, th = 0, tr = 0, maxn = 0;
@@ -1712,7 +1718,7 @@ static int64_t plan_layers(const s2c_batch *b, const PieceBlocks &B, int64_t K, 
     // the fewest layers that fit (each layer costs its DMA round trips and barriers whatever
     // it holds: C3 −2.5 %, C4 −1.2 % against a start 10 % above the capacity bound): from the
     // capacity bound up in growing steps, then bisected back to the first fitting count
-    uint64_t nl = std::max<uint64_t>({1, tp / S2C_CHUNK_PIECES + 1, (4 * th) / S2C_CHUNK_QBYTES + 1,
+    uint64_t nl = std::max<uint64_t>({1, tp / S2C_CHUNK_PIECES + 1, (4 * th) / chunk_qbytes(G, wq) + 1,
                                       tr / S2C_CHUNK_RECS + 1});
     // (past maxn layers the rotation still spreads the segments' pieces: up to 4 per piece)
     const uint64_t nlmax = std::max<uint64_t>(maxn, 4 * tp);
@@ -1720,7 +1726,7 @@ static int64_t plan_layers(const s2c_batch *b, const PieceBlocks &B, int64_t K, 
     auto fits = [&](uint64_t n) {
         tile_cuts(seg, n, cuts);
         bool ok = true;
-        for (uint64_t l = 0; l < n && ok; l++) ok = layer_fits(B, seg.size(), cuts, S0, W0, W1, K, G, l, n, recs);
+        for (uint64_t l = 0; l < n && ok; l++) ok = layer_fits(B, seg.size(), cuts, S0, W0, W1, K, G, wq, l, n, recs);
         return ok;
     };
     uint64_t bad = nl - 1;   // (a count known not to fit, or the bound − 1)
@@ -1744,8 +1750,9 @@ static int64_t plan_layers(const s2c_batch *b, const PieceBlocks &B, int64_t K, 
 // arrays' own 16-byte phases.
 static bool main_window_fits(const s2c_batch *b, const uint32_t *tw, int64_t K, int64_t G) {
     const uint64_t np = tw[14] - tw[13], no = tw[16] - tw[15], nq = tw[18] - tw[17];
-    if (np > S2C_CHUNK_PIECES || no > S2C_CHUNK_RECS || 4 * no + 32 > S2C_CHUNK_OBYTES || 8 * nq + 32 > S2C_CHUNK_QBYTES ||
-        4 * nq + 32 > S2C_CHUNK_XBYTES)
+    const uint64_t qb = chunk_qbytes(G, b->info.walk_queue);   // (the instantiation that runs it)
+    if (np > S2C_CHUNK_PIECES || no > S2C_CHUNK_RECS || 4 * no + 32 > S2C_CHUNK_OBYTES || 8 * nq + 32 > qb ||
+        4 * nq + 32 > qb / 2)
         return false;
     const int64_t W0 = tw[0] >> 5, W1 = (tw[1] + 31) >> 5;
     for (int64_t W = W0; W < W1; W++)
@@ -3011,6 +3018,10 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
     b->tiles.assign((size_t)NT * S2C_TILE_WORDS, 0u);
     uint64_t boff = 0, loff = 0, coff = 0;
     int64_t runs_max = 0;
+    // the k_tile instantiation the layers are cut for (its chunk's plane bytes): a shard of this
+    // batch keeps the non-queue one when this is planned for it (mark_runs)
+    I.walk_queue = walk_queue_of(I);
+    const int64_t wq = I.walk_queue;
     // per tile (host threads): its window, the most candidate runs of a word, layers, items
     std::vector<int64_t> t_nl(NT, 0), t_nch(NT, 0), t_maxc(NT, 0), t_wruns(NT, 0);   // (0: an unplanned tile)
     std::atomic<bool> too_big{false};
@@ -3024,7 +3035,7 @@ static int build_batch(s2c_parser *p, s2c_batch **out) {
             for (int64_t W = w0; W < w1; W++)
                 maxc = std::max<int64_t>(maxc, (int64_t)b->rs[W + 1] - (int64_t)b->rs[std::max<int64_t>(W - K, 0)] + nlg);
             t_maxc[t] = maxc;
-            const int64_t nl = plan_layers(b, PB, K, (uint64_t)T.a, (uint64_t)T.b, G);
+            const int64_t nl = plan_layers(b, PB, K, (uint64_t)T.a, (uint64_t)T.b, G, wq);
             t_nl[t] = nl;
             if (nl <= 0) { too_big = true; continue; }
             t_nch[t] = plan_items(b, K, (uint64_t)T.a, (uint64_t)T.b, nl, item_layers());

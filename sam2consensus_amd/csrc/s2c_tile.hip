@@ -724,10 +724,10 @@ template <> struct ChunkExt<true> {
     alignas(16) uint32_t pxl[S2C_CHUNK_PIECES + 4];
     uint8_t wq[S2C_CHUNK_PIECES];
 };
-template <bool EXT>
+template <bool EXT, uint32_t QB>
 struct ChunkLds : ChunkExt<EXT> {
     uint16_t segR[CSEG + 1];   // (u16: record offsets < S2C_CHUNK_RECS + RPAD; the LDS of 3 workgroups per CU)
-    alignas(16) uint8_t pl[16 + S2C_CHUNK_QBYTES + 16];
+    alignas(16) uint8_t pl[16 + QB + 16];   // (QB = S2C_CHUNK_QBYTES_OF(NWP, WQB))
     alignas(16) uint4 pcb[S2C_CHUNK_PIECES];
     alignas(16) uint8_t ol[S2C_CHUNK_OBYTES + 16];
     alignas(16) uint2 runl[S2C_CHUNK_RECS + RPAD];
@@ -796,9 +796,9 @@ struct EpiLds {
     FastLds<ICOL> L;
     uint32_t cols[ICOL * NSYM];
 };
-template <uint32_t ICOL, bool EXT>
+template <uint32_t ICOL, bool EXT, uint32_t QB>
 union TileLds {
-    ChunkLds<EXT> c[WV];   // one chunk per wave
+    ChunkLds<EXT, QB> c[WV];   // one chunk per wave
     EpiLds<ICOL> e;
 };
 // the non-ACGT words in HBM, as a global-address-space pointer (a uniform base + 32-bit lane
@@ -1171,7 +1171,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     // WQB: the launch's batch has pieces walked op by op (s2c_dev n_walked); without them the
     // queue's code costs C3 / C4 4 % (profiles/r05/v9_*), so it is a separate instantiation
     constexpr bool PXL = NWP <= 32, WQ = WQB && NWP <= 32;   // (ChunkLds' EXT)
-    __shared__ __attribute__((aligned(16))) TileLds<ICOL, PXL || WQ> U;
+    __shared__ __attribute__((aligned(16))) TileLds<ICOL, PXL || WQ, S2C_CHUNK_QBYTES_OF(NWP, WQB)> U;
     // a finish tile's own short-motif insertion events (EvRec; the 2048-position instantiation
     // leaves them to k_reads: its LDS)
     constexpr bool REC = WQB && NWP <= 32;   // (the walk-queue instantiation's LDS has room for the list)

@@ -6,10 +6,11 @@ import re
 import sys
 
 
-# k_tile's workgroups per CU by LDS (160 KB, 256-byte allocation granules): 3 for tiles of
-# <= 512 positions (NWP 8 / 16), 2 above — a kernel 32 bytes over its share ran C2 40 % slower
-# in round 5 with no other sign (the occupancy remark does not round to granules)
-LDS_CAP = {"k_tileILi8E": 54528, "k_tileILi16E": 54528, "k_tileILi32E": 81920, "k_tileILi64E": 81920}
+# k_tile's workgroups per CU by LDS: 3 for tiles of <= 512 positions (NWP 8 / 16), 2 above.
+# The share is the largest measured to keep 3: 53,536 bytes ran at 3 per CU, 54,176 (round 6,
+# profiles/r06/d1_*, d2_*) and 54,560 (round 5) bytes ran C2 40-47 % slower with no other sign
+# (the occupancy remark does not count the CU's reserved LDS or its allocation granules)
+LDS_CAP = {"k_tileILi8E": 53536, "k_tileILi16E": 53536, "k_tileILi32E": 81920, "k_tileILi64E": 81920}
 
 
 def main(path):

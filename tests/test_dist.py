@@ -76,6 +76,22 @@ def test_split_is_balanced_and_contiguous():
         assert max(loads) < 1.3 * (sum(loads) / world)
 
 
+def test_shard_keeps_the_instantiation_its_layers_were_cut_for():
+    """Layers are cut for the k_tile instantiation planned for the whole batch (s2c.h
+    S2C_CHUNK_QBYTES_OF: the non-queue one holds more plane bytes per layer), and a shard inherits
+    its tiles' layer counts: a shard may drop the walk queue but never take it up when its parent
+    was planned without it."""
+    for name, over in (("c2", {"n_refs": 40}), ("c2", {"n_refs": 40, "ins_frac": 0.0, "del_frac": 0.004}),
+                       ("c4", {"ref_len": 2000, "depth": 3000.0})):
+        hb = configs.synth_batch(name, **over)
+        for world in (2, 4):
+            for r in range(world):
+                sub = shard.sub_batch(hb, r, world)
+                assert sub.info.walk_queue <= hb.info.walk_queue, (name, over, world, r)
+                assert (sub.tiles[:, 19] == hb.tiles[sub.t0:sub.t1, 19]).all()
+                sub.free()
+
+
 def test_exchange_volumes_count_the_duplicated_reads():
     """shard.exchange_volumes (bench.py's dup_frac): the pieces summed over the
     shards are at least the workload's and exceed it by the reads reaching across a cut."""
