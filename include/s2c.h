@@ -167,12 +167,13 @@ int s2c_layout(int64_t *out, int n);
 #define S2C_CHUNK_PIECES     128
 #define S2C_CHUNK_QBYTES    4096
 /* a layer's base-plane bytes in k_tile<nwp, wq> (nwp: the tile's 32-position words, wq: the
-   walk-queue instantiation, s2c_batch_info walk_queue as planned): 4,320 for the non-queue
-   instantiations of tiles of <= 512 positions (C3 -2.7 %, C4 -3.3 % against 4,096: fewer
-   layers, each one's DMA round trips and barriers saved; 4,608 measured no better), the base
-   for the others (k_tile<16, walk queue> has no LDS left under 53,536 bytes, the largest share
-   measured to keep 3 workgroups per CU).  The non-ACGT words of a layer <= half of it. */
-#define S2C_CHUNK_QBYTES_OF(nwp, wq) ((nwp) <= 16 && !(wq) ? 4320 : S2C_CHUNK_QBYTES)
+   walk-queue instantiation, s2c_batch_info walk_queue as planned): 4,352 for tiles of <= 512
+   positions (against 4,096: fewer layers, each one's DMA round trips and barriers saved; C3
+   -2.2 %, C4 -3.4 % at 4,320; 4,608 no better), the base for wider ones; every k_tile<16>
+   stays under 53,536 LDS bytes, the largest share measured to keep 3 workgroups per CU.  The
+   non-ACGT words of a layer <= half of it.  (wq: kept in the signature — the host cuts the
+   layers for the instantiation it plans, and a shard keeps that one.) */
+#define S2C_CHUNK_QBYTES_OF(nwp, wq) ((void)(wq), (nwp) <= 16 ? 4352 : S2C_CHUNK_QBYTES)
 #define S2C_CHUNK_XBYTES    2048
 #define S2C_CHUNK_OBYTES    1024
 #define S2C_CHUNK_RECS       192

@@ -700,7 +700,9 @@ __device__ __forceinline__ void tile_epilogue_fast(const D &d, uint32_t tile, co
 
 constexpr int GS = 8;                 // records per counting group
 constexpr int CSEG = S2C_CHUNK_SEGS;  // segments of a window (≤ 64 words + kwin ≤ 32)
-constexpr uint32_t RPAD = 64;         // zero records after a chunk's last (a group's reads past it: ≤ 7·G ≤ 56)
+// zero records after a chunk's last: a counting group reads up to 7·G past it (G = 64 / NWP
+// lanes per word), so 8·G (k_tile<16>: 32, 256 LDS bytes per wave left for its planes)
+constexpr uint32_t rpad_of(int NWP) { return 8u * (64u / (uint32_t)NWP); }
 constexpr uint32_t WV = WG / 64;      // waves per workgroup (each its own chunk)
 // raw histogram slots while counting ("-ACGNT" slots after the reconstruction)
 constexpr uint32_t SL_SDC = 0, SL_SD = 1, SL_X = 2, SL_Y = 3, SL_N = 4, SL_Z = 5;
@@ -724,7 +726,7 @@ template <> struct ChunkExt<true> {
     alignas(16) uint32_t pxl[S2C_CHUNK_PIECES + 4];
     uint8_t wq[S2C_CHUNK_PIECES];
 };
-template <bool EXT, uint32_t QB>
+template <bool EXT, uint32_t QB, uint32_t RPAD>
 struct ChunkLds : ChunkExt<EXT> {
     uint16_t segR[CSEG + 1];   // (u16: record offsets < S2C_CHUNK_RECS + RPAD; the LDS of 3 workgroups per CU)
     alignas(16) uint8_t pl[16 + QB + 16];   // (QB = S2C_CHUNK_QBYTES_OF(NWP, WQB))
@@ -796,9 +798,9 @@ struct EpiLds {
     FastLds<ICOL> L;
     uint32_t cols[ICOL * NSYM];
 };
-template <uint32_t ICOL, bool EXT, uint32_t QB>
+template <uint32_t ICOL, bool EXT, uint32_t QB, uint32_t RPAD>
 union TileLds {
-    ChunkLds<EXT, QB> c[WV];   // one chunk per wave
+    ChunkLds<EXT, QB, RPAD> c[WV];   // one chunk per wave
     EpiLds<ICOL> e;
 };
 // the non-ACGT words in HBM, as a global-address-space pointer (a uniform base + 32-bit lane
@@ -1171,7 +1173,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
     // WQB: the launch's batch has pieces walked op by op (s2c_dev n_walked); without them the
     // queue's code costs C3 / C4 4 % (profiles/r05/v9_*), so it is a separate instantiation
     constexpr bool PXL = NWP <= 32, WQ = WQB && NWP <= 32;   // (ChunkLds' EXT)
-    __shared__ __attribute__((aligned(16))) TileLds<ICOL, PXL || WQ, S2C_CHUNK_QBYTES_OF(NWP, WQB)> U;
+    __shared__ __attribute__((aligned(16))) TileLds<ICOL, PXL || WQ, S2C_CHUNK_QBYTES_OF(NWP, WQB), rpad_of(NWP)> U;
     // a finish tile's own short-motif insertion events (EvRec; the 2048-position instantiation
     // leaves them to k_reads: its LDS)
     constexpr bool REC = WQB && NWP <= 32;   // (the walk-queue instantiation's LDS has room for the list)
@@ -1431,7 +1433,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(NWP <= 16 ? 
         if (NPc == 0)
             for (uint32_t sg = lane; sg <= NS; sg += 64) C.segR[sg] = 0;
         if (__ballot(planes)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the planes, for those walks)
-        for (uint32_t i = lane; i < RPAD; i += 64) C.runl[NR + i] = make_uint2(0u, 0u);
+        for (uint32_t i = lane; i < rpad_of(NWP); i += 64) C.runl[NR + i] = make_uint2(0u, 0u);
         TPROF_MARK(10);    // (the records, segments and any planes wait of the walk)
         if (TABL(1))   // (ablated walk: zero records)
             for (uint32_t i = lane; i < NR; i += 64) C.runl[i] = make_uint2(0u, 0u);
