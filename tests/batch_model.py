@@ -262,7 +262,13 @@ def check_plan(hb):
     assert len(set(rl.tolist())) == len(rl)
 
 
-CHUNK_PIECES, CHUNK_QBYTES, CHUNK_XBYTES, CHUNK_OBYTES, CHUNK_RECS = 128, 4096, 2048, 1024, 192   # include/s2c.h (per wave)
+CHUNK_PIECES, CHUNK_QBYTES, CHUNK_OBYTES, CHUNK_RECS = 128, 4096, 1024, 192   # include/s2c.h (per wave)
+
+
+def chunk_qbytes(nwp, wq):
+    """include/s2c.h S2C_CHUNK_QBYTES_OF: a layer's plane bytes in k_tile<nwp, wq> (the
+    non-ACGT words: half of it)."""
+    return 4352 if nwp <= 16 else CHUNK_QBYTES
 LY_MAIN = 0xFFFFFFFF
 CHUNK_LANE_RECS, ITEM_RECS = 248, 60000
 
@@ -300,6 +306,7 @@ def check_layers(hb):
     while nwp * 32 < i.tile_max:
         nwp *= 2
     G = 64 // nwp   # counting lanes per word of one wave
+    qb = chunk_qbytes(nwp, i.walk_queue)   # (the instantiation that runs the layers)
     K = i.kwin
     lly, lpc = hb.lly.astype(np.int64), hb.lpc.astype(np.int64)
     T = hb.tiles.astype(np.int64)
@@ -311,7 +318,7 @@ def check_layers(hb):
             assert row[19] == 1
             np_, no, nq = row[14] - row[13], row[16] - row[15], row[18] - row[17]
             assert np_ <= CHUNK_PIECES and no <= CHUNK_RECS and _region(4 * no, 4 * (row[15] & 3)) <= CHUNK_OBYTES
-            assert _region(8 * nq, 8 * (row[17] & 1)) <= CHUNK_QBYTES and _region(4 * nq, 4 * (row[17] & 3)) <= CHUNK_XBYTES
+            assert _region(8 * nq, 8 * (row[17] & 1)) <= qb and _region(4 * nq, 4 * (row[17] & 3)) <= qb // 2
             rs = hb.rs.astype(np.int64)
             for W in range(W0, W1):
                 assert rs[W + 1] - rs[max(W - K, 0)] <= CHUNK_LANE_RECS * G
@@ -339,7 +346,7 @@ def check_layers(hb):
                 qa, nq = h0 >> 1, ((h1 + 1) >> 1) + 1 - (h0 >> 1)
                 assert p1 - p0 <= CHUNK_PIECES and o1 - o0 == recs.sum() <= CHUNK_RECS
                 assert _region(4 * (o1 - o0), 4 * (o0 & 3)) <= CHUNK_OBYTES
-                assert _region(8 * nq, 8 * (qa & 1)) <= CHUNK_QBYTES and _region(4 * nq, 4 * (qa & 3)) <= CHUNK_XBYTES
+                assert _region(8 * nq, 8 * (qa & 1)) <= qb and _region(4 * nq, 4 * (qa & 3)) <= qb // 2
                 for W in range(W0, W1):
                     a = max(W - K, S0) - S0
                     assert recs[a:W - S0 + 1].sum() <= CHUNK_LANE_RECS * G
