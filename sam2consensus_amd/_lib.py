@@ -123,12 +123,25 @@ EXPORTS = [
 ]
 
 
+def _hip_runtime():
+    """One HIP runtime per process: torch (the library paths' device allocator) brings its own
+    libamdhip64.so.7; mapping that file first (by path, RTLD_GLOBAL — without importing torch,
+    1.8 s on the box) makes libs2c.so's DT_NEEDED libamdhip64.so.7 bind to that same copy, and
+    a later `import torch` reuses it, instead of /opt/rocm's being mapped as a second runtime
+    (which then reports hipErrorNoDevice for our launches).  Without torch: the system's."""
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        spec = None
+    if spec is not None and spec.origin:
+        path = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+        if os.path.exists(path):
+            C.CDLL(path, mode=C.RTLD_GLOBAL)
+
+
 def _load():
-    # One HIP runtime per process: torch (the device allocator) brings its own
-    # libamdhip64.so.7; loading it first makes libs2c.so's DT_NEEDED libamdhip64.so.7 bind
-    # to that same copy instead of mapping /opt/rocm's as a second runtime (which then
-    # reports hipErrorNoDevice for our launches).
-    import torch  # noqa: F401
+    _hip_runtime()
     if not os.path.exists(LIB_PATH):
         raise ImportError("libs2c.so not built (%s): run `make` or __graft_entry__.build()" % LIB_PATH)
     lib = C.CDLL(LIB_PATH)

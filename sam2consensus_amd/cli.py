@@ -147,42 +147,29 @@ def _log_failed_parse(log, parser):
         log(line)
 
 
-def _warm_device(device, reserve=0, timing=None):
-    """Start the HIP runtime and the device's context on a side thread (the first device
-    call costs tenths of a second) so it overlaps the host parse; join() before the upload.
-    ``reserve`` > 0 (a large input): also allocate the upload's pinned staging ring and a
-    device block of ``reserve`` bytes on its copy stream, released at once into torch's
-    caching allocator, whose next allocation there (the batch's one upload buffer) is then
-    carved from it instead of a fresh hipMalloc (86-90 ms for C5's 1.06 GB on the box).
-    A failure here is left to the upload to report."""
+def _warm_session(sess, reserve, timing):
+    """Bring up the HIP runtime and the device on a side thread (the first device call costs
+    tenths of a second) so it overlaps the host parse, and reserve the batch's device buffer
+    and pinned staging (``reserve`` bytes: a large input's estimate) there too; join() before
+    the upload.  A failure is raised on the main thread by ``_join_session``."""
     import threading
-
-    t = timing if timing is not None else {}
 
     def run():
         try:
-            from . import _lib
-            from .engine import _dev
-            import torch
-            t0 = time.perf_counter()
-            d = _dev(device)
-            torch.empty(1, device=d)
-            _lib.plan_for_device(d)   # (the plan's grid shaping: this device's CUs, once known)
-            t1 = time.perf_counter()
-            t["warm_context"] = t1 - t0
-            if reserve > 0:
-                from .engine import default_uploader
-                up = default_uploader(d).prime()
-                t2 = time.perf_counter()
-                free, _ = torch.cuda.mem_get_info(d)
-                with torch.cuda.stream(up.copy_stream):
-                    torch.empty(min(int(reserve), free // 2), dtype=torch.uint8, device=d)
-                t["warm_pinned"], t["warm_reserve"] = t2 - t1, time.perf_counter() - t2
-        except Exception:  # noqa: BLE001 - reported by DeviceBatch on the main thread
-            pass
+            sess.reserve(reserve)
+        except Exception as e:  # noqa: BLE001 - re-raised by _join_session on the main thread
+            sess.error = e
+        timing.update(sess.timing)
+    sess.error = None
     th = threading.Thread(target=run, daemon=True)
     th.start()
     return th
+
+
+def _join_session(sess, th):
+    th.join()
+    if sess.error is not None:
+        raise sess.error
 
 
 def upload_estimate(filename):
@@ -198,30 +185,55 @@ def upload_estimate(filename):
     return int(size * (2.4 if filename.endswith(".gz") else 0.6))
 
 
+def consensus_batch_hip(sess, hb, thresholds, prefix, min_depth=1, fill=b"-", nchar=0, timings=None):
+    """consensus_batch through hiprun.Session (no PyTorch): the one-process CLI's device side."""
+    from .records import build_records, render
+
+    t = timings if timings is not None else {}
+    t0 = time.perf_counter()
+    stats, offs, out = sess.run(hb, thresholds, min_depth, fill, t)
+    t["device"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    fastas = build_records(hb, thresholds, prefix, stats, offs, out)
+    pre = prefix.encode("latin-1") if isinstance(prefix, str) else prefix
+    files = {}
+    for name, recs in fastas.items():
+        files[name.encode("latin-1") + b"__" + pre + b".fasta"] = render(recs, nchar)
+    t["format"] = time.perf_counter() - t0
+    return files
+
+
 def consensus_files(filename, thresholds, prefix, min_depth=1, fill=b"-", nchar=0, maxdel_active=True,
                     device=None, log=None):
     """Run the whole pipeline on one SAM/SAM.gz file; returns a RunResult whose
-    ``files`` maps ``REF__PREFIX.fasta`` → content bytes (nothing written)."""
+    ``files`` maps ``REF__PREFIX.fasta`` → content bytes (nothing written).  The device side
+    runs through the HIP runtime directly (hiprun.py): this path never imports PyTorch."""
     from .batch import Parser
+    from .hiprun import Session, device_index
 
     t = {}
     t0 = time.perf_counter()
-    warm = _warm_device(device, upload_estimate(filename), t)   # (the HIP context comes up while the host parses)
-    p = Parser(maxdel_active, 150)
+    sess = Session(device_index(device))
+    warm = _warm_session(sess, upload_estimate(filename), t)   # (the device comes up while the host parses)
     try:
-        p.feed_file(filename)
-        hb = p.finish()
-    except REF_ERRORS:
+        p = Parser(maxdel_active, 150)
+        try:
+            p.feed_file(filename)
+            hb = p.finish()
+        except REF_ERRORS:
+            if log:
+                _log_failed_parse(log, p)
+            raise
+        finally:
+            p.close()
+        t["parse"] = time.perf_counter() - t0
+        _join_session(sess, warm)
         if log:
-            _log_failed_parse(log, p)
-        raise
+            _log_summary(log, hb.info)
+        files = consensus_batch_hip(sess, hb, thresholds, prefix, min_depth, fill, nchar, t)
     finally:
-        p.close()
-    t["parse"] = time.perf_counter() - t0
-    warm.join()
-    if log:
-        _log_summary(log, hb.info)
-    files = consensus_batch(hb, thresholds, prefix, min_depth, fill, nchar, device, t)
+        warm.join()
+        sess.close()
     # the batch's host arrays (GBs for a large input: ~60 ms of munmap on the box) released
     # beside the caller's file writes
     return RunResult(files, t, hb.info, hb.free_async())

@@ -15,6 +15,7 @@ import torch
 
 from . import _lib as L
 from ._lib import lib
+from .devargs import ARRAYS, fill_dev
 
 
 def _dev(device):
@@ -187,8 +188,7 @@ class DeviceBatch:
     default for batches of 64 MB or more) the arrays go through its pinned staging ring and
     copy stream (asynchronous); otherwise each array is copied synchronously."""
 
-    ARRAYS = ("pc", "ops", "bq", "bx", "rs", "tiles", "items", "dense", "deep", "lp", "wtile", "rlist", "ps",
-              "lly", "lpc", "lops", "lbq", "lbx", "px", "dwin", "lpx", "dpc")
+    ARRAYS = ARRAYS   # (devargs: s2c_dev's pointer fields, in upload order)
 
     def __init__(self, hb, device=None, uploader=None, dense_layers=False):
         self.device = _dev(device) if uploader is None else uploader.device
@@ -258,11 +258,16 @@ class Workspace:
         self.out_stride = self.fill_w * i.padded_len + i.n_cols
         cap = int(sz.out_per_fill) * self.fill_w + int(sz.out_fixed)
         self.out = u8(cap)
-        d = L.Dev()
-        for name in DeviceBatch.ARRAYS:
-            setattr(d, name, _ptr(getattr(db, name)))
-        d.n_pieces, d.n_ops, d.n_qwords, d.n_tiles = i.n_pieces, i.n_ops, i.n_qwords, i.n_tiles
-        d.n_items, d.n_dense, d.n_deep = i.n_items, i.n_dense, i.n_deep
+        # the maxdel rule (:210) runs on the device: the parser's setting unless overridden
+        if maxdel_active is None:
+            maxdel_active = getattr(db.hb, "maxdel_active", True)
+        if maxdel is None:
+            maxdel = getattr(db.hb, "maxdel", 150)
+        bufs = {n: getattr(self, n).data_ptr() for n in ("runs", "ibkt", "ilong", "ilong_n", "counts", "ins_cols",
+                                                           "ins_chr", "tile_stats", "blk_len", "out")}
+        bufs.update(thresholds=self.thr.data_ptr(), fill=self.fill.data_ptr())
+        d = fill_dev(i, {name: getattr(db, name).data_ptr() for name in DeviceBatch.ARRAYS}, bufs, self.T, min_depth,
+                     fill, maxdel_active, maxdel, cap)
         if tile_range is not None:
             t0, t1 = tile_range
             hb = db.hb
@@ -276,28 +281,6 @@ class Workspace:
             d.n_items = int(len(keep(hb.items, 0)))
             d.n_dense = int(len(keep(hb.dense, 0)))
             d.n_deep = int(((hb.deep >= t0) & (hb.deep < t1)).sum())
-        d.padded_len, d.chunk, d.kwin, d.tile_max = i.padded_len, i.chunk, i.kwin, i.tile_max
-        d.dense_lds = i.dense_lds
-        d.n_rlist = i.n_rlist
-        d.n_layers, d.n_lpieces, d.n_lops, d.n_lqwords = i.n_layers, i.n_lpieces, i.n_lops, i.n_lqwords
-        d.layers_dense, d.layers_built = i.layers_dense, i.layers_built
-        d.word_lo, d.word_hi = i.word_lo, i.word_hi
-        d.walk_queue, d.tile_events, d.n_rlist_run = i.walk_queue, i.tile_events, i.n_rlist_run
-        # the maxdel rule (:210) runs on the device: the parser's setting unless overridden
-        if maxdel_active is None:
-            maxdel_active = getattr(db.hb, "maxdel_active", True)
-        if maxdel is None:
-            maxdel = getattr(db.hb, "maxdel", 150)
-        d.maxdel_active, d.maxdel = 1 if maxdel_active else 0, int(maxdel)
-        d.thresholds, d.n_thr = _ptr(self.thr), self.T
-        d.min_depth = int(max(min(min_depth, 2**31 - 1), -2**31))
-        d.fill_len, d.fill_nondash = len(fill), sum(1 for c in fill if c != ord("-"))
-        d.fill = _ptr(self.fill)
-        d.runs, d.ibkt, d.ilong, d.ilong_n = _ptr(self.runs), _ptr(self.ibkt), _ptr(self.ilong), _ptr(self.ilong_n)
-        d.counts = _ptr(self.counts)
-        d.ins_cols, d.ins_chr, d.n_cols = _ptr(self.ins_cols), _ptr(self.ins_chr), i.n_cols
-        d.tile_stats, d.blk_len = _ptr(self.tile_stats), _ptr(self.blk_len)
-        d.out, d.out_cap = _ptr(self.out), cap
         self.dev = d
 
     def stream_handle(self):

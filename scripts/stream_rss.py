@@ -28,10 +28,6 @@ def child(mode, path, name, batch_mb):
     thr = [float(x) for x in a.thresholds.split(",")]
     prefix = os.path.basename(path).split(".")[0].encode()
     common = (thr, prefix, a.min_depth, a.fill.encode(), a.n, not isinstance(a.maxdel, str))
-    if os.environ.get("E2E_NO_RESERVE"):   # (A/B: the CLI's warm-up thread without the upload reservation)
-        import sam2consensus_amd.cli as cli
-        warm = cli._warm_device
-        cli._warm_device = lambda device, reserve=0, timing=None: warm(device, 0, timing)
     t0 = time.perf_counter()
     if mode == "whole":
         r = consensus_files(path, *common)
@@ -77,8 +73,7 @@ def main():
         # environment settings (keys "stream:A=1,B=2", ...)
         runs = [("whole", {}), ("stream", {})]
         if os.environ.get("STREAM_WHOLE_ONLY"):   # (the whole-file CLI only, twice: box-to-box spread)
-            runs = [("whole", {}), ("whole:E2E_NO_RESERVE=1", {"E2E_NO_RESERVE": "1"}), ("whole:again", {}),
-                    ("whole:E2E_NO_RESERVE=1,again", {"E2E_NO_RESERVE": "1"})]
+            runs = [("whole", {}), ("whole:again", {})]
         for v in filter(None, os.environ.get("STREAM_VARIANTS", "").split(";")):
             runs.append(("stream:" + v, dict(kv.split("=", 1) for kv in v.split(","))))
         # WHOLE_VARIANTS="A=1;A=2": whole-file runs with those settings, the set twice in turn

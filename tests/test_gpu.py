@@ -196,6 +196,47 @@ def test_cli_end_to_end_c1(tmp_path):
     assert got == g["content"]
 
 
+def test_cli_process_runs_without_torch(tmp_path):
+    """The CLI process (sam2consensus.py, one GPU, whole file) never imports PyTorch — its
+    device side is hiprun.py on the HIP runtime libs2c.so is bound to — and writes the
+    reference's files: C1 against the golden content, a 5 %-scale C5 with -f N -n 60 -m 3
+    against the C restatement (the lengths != 1 fill takes the dense tiles' layered path)."""
+    import subprocess
+    import sys
+    from sam2consensus_amd import configs
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    run = ("import runpy, sys\n"
+           "sys.argv = [%r] + sys.argv[1:]\n"
+           "try:\n    runpy.run_path(%r, run_name='__main__')\n"
+           "except SystemExit as e:\n    assert not e.code, e.code\n"
+           "print('TORCH', 'torch' in sys.modules)\n") % (os.path.join(root, "sam2consensus.py"),
+                                                         os.path.join(root, "sam2consensus.py"))
+    g = CONFIGS["c1"]
+    sam = str(tmp_path / "c1.sam")
+    configs.synth_write("c1", sam)
+    out = tmp_path / "out"
+    r = subprocess.run([sys.executable, "-c", run, "-i", sam, "-o", str(out)] + g["args"], capture_output=True,
+                       text=True, timeout=240, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "TORCH False" in r.stdout, r.stdout[-500:]
+    got = {fn: open(os.path.join(out, fn), "rb").read().decode("latin-1") for fn in os.listdir(out)}
+    assert got == g["content"]
+    sam5 = str(tmp_path / "c5.sam")
+    configs.synth_write("c5", sam5, scale=0.05)
+    args = ["-c", "0.25,0.75", "-f", "N", "-n", "60", "-m", "3", "-p", "c5"]
+    out5, ref5 = tmp_path / "out5", tmp_path / "ref5"
+    r = subprocess.run([sys.executable, "-c", run, "-i", sam5, "-o", str(out5)] + args, capture_output=True,
+                       text=True, timeout=240, cwd=root)
+    assert r.returncode == 0 and "TORCH False" in r.stdout, r.stderr[-2000:]
+    subprocess.run(["make", "-s", "-C", os.path.join(root, "oracle")], check=True)
+    o = subprocess.run([os.path.join(root, "oracle", "build", "s2c_oracle_mc"), "16", "-i", sam5, "-o", str(ref5)] + args,
+                       capture_output=True, text=True, timeout=300)
+    assert "status: ok" in o.stdout, o.stdout[-500:]
+    assert sorted(os.listdir(out5)) == sorted(os.listdir(ref5)) and os.listdir(ref5)
+    for fn in os.listdir(ref5):
+        assert open(os.path.join(out5, fn), "rb").read() == open(os.path.join(ref5, fn), "rb").read(), fn
+
+
 def _free_port():
     import socket
     s = socket.socket()

@@ -765,6 +765,20 @@ def test_graft_build_entry():
     m.build()
 
 
+def test_cli_path_imports_no_torch_and_one_hip_runtime():
+    """The one-process CLI's modules import no PyTorch (`import torch` is 1.8 s on the box);
+    libs2c.so is bound to the HIP runtime torch bundles, so a process that imports torch after
+    it still maps one libamdhip64 (two runtimes fail our launches with hipErrorNoDevice)."""
+    import subprocess
+    import sys
+    code = ("import sys\nimport sam2consensus_amd.cli, sam2consensus_amd.hiprun, sam2consensus_amd.records\n"
+            "print('torch' in sys.modules)\nimport torch\n"
+            "print(len(set(l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l)))\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=ROOT, timeout=300)
+    assert r.returncode == 0, r.stderr[-1000:]
+    assert r.stdout.split() == ["False", "1"], r.stdout
+
+
 def test_cli_upload_reservation_estimate(tmp_path):
     """The whole-file CLI's warm-up reservation (cli.upload_estimate): nothing below 64 MB of
     input or for a missing file (the parser raises the reference's error), 0.6 × a plain file,
