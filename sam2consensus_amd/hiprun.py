@@ -56,10 +56,10 @@ class Hip:
 
     def set_device(self, dev):
         n = C.c_int(0)
-        self.check(self.h.hipGetDeviceCount(C.byref(n)), "hipGetDeviceCount")
-        if n.value <= dev:
-            raise RuntimeError("sam2consensus_amd needs a ROCm GPU (device %d of %d visible); no CPU fallback"
-                               % (dev, n.value))
+        rc = self.h.hipGetDeviceCount(C.byref(n))
+        if rc != 0 or n.value <= dev:
+            why = self.h.hipGetErrorString(rc).decode() if rc else "device %d of %d visible" % (dev, n.value)
+            raise RuntimeError("sam2consensus_amd needs a ROCm GPU (%s); no CPU fallback" % why)
         self.check(self.h.hipSetDevice(dev), "hipSetDevice")
 
     def cus(self, dev):

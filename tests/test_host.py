@@ -779,6 +779,20 @@ def test_cli_path_imports_no_torch_and_one_hip_runtime():
     assert r.stdout.split() == ["False", "1"], r.stdout
 
 
+def test_cli_without_a_gpu_fails_loudly(tmp_path):
+    """No CPU fallback: on a host without a GPU (this tier) the CLI raises from the HIP runtime
+    and writes no FASTA file."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    from sam2consensus_amd.cli import main
+    p = tmp_path / "a.sam"
+    p.write_text("@SQ\tSN:r\tLN:40\nq\t0\tr\t1\t60\t10M\t*\t0\t0\tACGTACGTAC\t*\n")
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        main(["-i", str(p), "-o", str(tmp_path / "out")])
+    assert not any(f.endswith(".fasta") for f in os.listdir(tmp_path / "out"))
+
+
 def test_cli_upload_reservation_estimate(tmp_path):
     """The whole-file CLI's warm-up reservation (cli.upload_estimate): nothing below 64 MB of
     input or for a missing file (the parser raises the reference's error), 0.6 × a plain file,
