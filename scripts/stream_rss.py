@@ -28,6 +28,9 @@ def child(mode, path, name, batch_mb):
     thr = [float(x) for x in a.thresholds.split(",")]
     prefix = os.path.basename(path).split(".")[0].encode()
     common = (thr, prefix, a.min_depth, a.fill.encode(), a.n, not isinstance(a.maxdel, str))
+    if os.environ.get("E2E_NO_RESERVE"):   # (A/B: the CLI's warm-up thread without the upload reservation)
+        import sam2consensus_amd.cli as cli
+        cli.upload_estimate = lambda filename: 0
     t0 = time.perf_counter()
     if mode == "whole":
         r = consensus_files(path, *common)
